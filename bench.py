@@ -1,0 +1,286 @@
+"""bench.py — matched publishes/s of the MI355X topic-matching engine on BASELINE config C.
+
+    python bench.py [--gpus N --steps K --warmup W] [--config C --scale 1.0 --batch 1000000]
+
+One step = one batch of `--batch` synthetic publishes matched against the 10M-key
+config-C filter set (BASELINE.json configs[2]: the config the metric is quoted on).
+Inputs are resident in HBM when the timed region starts; a step is the full device
+pipeline (tokenise -> word lookup -> trie walk -> output compaction) through the C-ABI
+(tm_match_device) on the current torch stream.
+
+Multi-GPU (launched by torch.distributed.run): the trie is replicated, every rank owns
+its own `--batch` publishes (weak scaling, no data-path collective); value = all ranks'
+publishes / max-over-ranks time.
+
+Rank 0 at N=1 also times the CPU baseline: the C++ restatement of the reference's
+emqx_trie_search over an Erlang-term-ordered key set (oracle/, "kind": "port") on a
+bounded sample of the same topics, and checks the GPU results of that sample bit-exactly.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "matched publishes/sec at 10M filters (1/2/4/8 GPU) + p99 batch latency"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(stats5, topic_bytes, n):
+    """Bytes one batch must move at minimum under the frozen layout:
+    topic bytes + u32 offsets in, one 32 B slot per word-table probe and per edge-table
+    probe, 4 B key read from the terminal-list arena + 4 B key written per match, and
+    12 B of per-topic results (offset, count, status)."""
+    visits, eprobes, wprobes, keys, levels = stats5
+    return topic_bytes + 4 * (n + 1) + 32 * wprobes + 32 * eprobes + 8 * keys + 12 * n
+
+
+def cpu_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="C")
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--batch", type=int, default=1_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work (s)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no CPU baseline)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    from emqx_amd import _native as N
+    from emqx_amd import workloads
+
+    # ---------------------------------------------------------------- build
+    t0 = time.time()
+    w = workloads.generate(args.config, scale=args.scale, n_topics=args.batch * world)
+    t_gen = time.time() - t0
+    t0 = time.time()
+    eng = N.Engine(local, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    t_build = time.time() - t0
+    st = eng.stats()
+    log(f"[rank {rank}] generated {w.n_keys} keys in {t_gen:.1f}s, engine build {t_build:.1f}s, "
+        f"nodes {st['n_nodes']}, words {st['n_words']}, index {st['device_bytes'] / 2**30:.2f} GiB")
+
+    lo, hi = rank * args.batch, (rank + 1) * args.batch
+    tb, to = w.topic_slice(lo, hi)
+    n = hi - lo
+    topic_bytes = int(to[-1])
+    dev = torch.device("cuda", local)
+    d_bytes = torch.from_numpy(tb).to(dev)
+    d_off = torch.from_numpy(to.view(np.int32)).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def step():
+        return eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, topic_bytes, sp)
+
+    # size the output arena from the first run (overflow -> grow -> rerun)
+    r = step()
+    torch.cuda.synchronize()
+    total = _read_u64(r.d_total)
+    if total > r.keys_cap:
+        eng.reserve_matches(int(total * 1.1) + 1024)
+        r = step()
+        torch.cuda.synchronize()
+        total = _read_u64(r.d_total)
+    assert total <= r.keys_cap
+    for _ in range(max(0, args.warmup - 1)):
+        step()
+    torch.cuda.synchronize()
+
+    # walk statistics for the algorithmic-byte count (one untimed, counted run)
+    eng.debug_stats(True, read=False)
+    step()
+    torch.cuda.synchronize()
+    stats5 = eng.debug_stats(False)
+    alg_bytes = algorithmic_bytes(stats5, topic_bytes, n)
+    eng.debug_stats(False, read=False)
+
+    # ---------------------------------------------------------------- timed region
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        step()
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        dist.barrier()
+    lat_ms = np.array([a.elapsed_time(b) for a, b in evs])
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_pubs = n * args.steps * world
+    value = total_pubs / elapsed
+
+    # dominant kernel (k_match_fast) duration: HIP events on its launch stream
+    kms = []
+    for _ in range(min(args.steps, 10)):
+        eng.timing(True)
+        step()
+        torch.cuda.synchronize()
+        kms.append(eng.timing(False))
+    kernel_ms = float(np.mean(kms))
+    slow_topics = eng.stats()["n_slow_topics"]
+
+    # ---------------------------------------------------------------- CPU baseline + parity sample
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile:
+        cpu, parity = cpu_baseline(args, w, eng, tb, to, n)
+
+    if rank == 0:
+        achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "publishes/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded generator, emqx_amd/workloads.py config C)",
+            "config": {
+                "workload": f"{args.config}: {w.n_keys} route keys, 10-level topics, '#'-heavy fan-out"
+                if args.config == "C" else f"{args.config} (scale {args.scale}): {w.n_keys} route keys",
+                "route_keys": w.n_keys,
+                "publishes_per_step_per_gpu": n,
+                "matches_per_step_per_gpu": int(total),
+                "parallelism": f"replicated trie, dp{world}",
+            },
+            "p50_batch_ms": round(float(np.percentile(lat_ms, 50)), 4),
+            "p99_batch_ms": round(float(np.percentile(lat_ms, 99)), 4),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "kernel": "k_match_fast",
+                "kernel_ms": round(kernel_ms, 4),
+                "algorithmic_bytes_per_launch": int(alg_bytes),
+                "walk": dict(zip(["node_visits", "edge_probes", "word_probes", "keys", "levels"],
+                                 [int(x) for x in stats5])),
+            },
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "spill_topics": int(slow_topics),
+            "build_s": round(t_build, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _read_u64(ptr):
+    """Read one u64 from device memory (the batch's requested-keys counter)."""
+    import ctypes as C
+
+    import torch
+    h = torch.empty(1, dtype=torch.int64)
+    lib = C.CDLL("libamdhip64.so")
+    lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    rc = lib.hipMemcpy(C.c_void_p(h.data_ptr()), C.c_void_p(ptr), 8, 2)  # hipMemcpyDeviceToHost
+    assert rc == 0, rc
+    return int(h.item())
+
+
+def cpu_baseline(args, w, eng, tb, to, n):
+    """Time oracle/'s emqx_trie_search restatement on a bounded sample of the same
+    batch, and check the engine's results for that sample bit-exactly."""
+    import oracle
+    from emqx_amd import _native as N
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    t0 = time.time()
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    t_build = time.time() - t0
+    # calibrate: rate on a small slice, then size the sample for ~cpu_seconds
+    cal = 2000
+    t0 = time.perf_counter()
+    ix.count(tb, to[:cal + 1], threads=threads)
+    rate = cal / max(time.perf_counter() - t0, 1e-6)
+    m = int(min(n, max(cal, rate * args.cpu_seconds)))
+    t0 = time.perf_counter()
+    ix.count(tb, to[:m + 1], threads=threads)
+    dt = time.perf_counter() - t0
+    # single-thread reference point
+    m1 = min(m, 4000)
+    t0 = time.perf_counter()
+    ix.count(tb, to[:m1 + 1], threads=1)
+    dt1 = time.perf_counter() - t0
+    # parity on a sample of the batch (host path through the same C-ABI)
+    ps = min(m, 20000)
+    eo, eids, est = ix.match(tb, to[:ps + 1], threads=threads)
+    buf = tb
+    off, cnt, keys, st = eng.match_packed(buf, to[:ps + 1])
+    ids = eng.key_ids(keys)
+    bad = 0
+    for i in range(ps):
+        if not np.array_equal(np.sort(ids[off[i]:off[i] + cnt[i]]), eids[eo[i]:eo[i + 1]]):
+            bad += 1
+    cpu = {
+        "value": round(m / dt, 1),
+        "unit": "publishes/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{m} publishes of the same batch vs the same {w.n_keys} keys; C++ restatement of "
+                  f"emqx_trie_search over an Erlang-term-ordered key set (oracle/trie_search.cpp), "
+                  f"{threads} threads on {cpu_info()}; 1 thread: {round(m1 / dt1, 1)} publishes/s; "
+                  f"index build {t_build:.1f}s untimed",
+    }
+    parity = {"sampled_topics": ps, "mismatches": bad, "oracle": "oracle/trie_search.cpp (emqx_trie_search)",
+              "matches_in_sample": int(eo[-1])}
+    if bad:
+        log(f"PARITY FAILURE: {bad}/{ps} topics differ")
+    return cpu, parity
+
+
+if __name__ == "__main__":
+    main()

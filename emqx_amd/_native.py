@@ -1,0 +1,288 @@
+"""ctypes binding of the C-ABI in include/emqx_tm.h (libemqx_tm.so, built in-tree).
+
+The product path is the HIP library and nothing else: if the library is missing,
+or the process has no gfx950 device, engine creation raises.  There is no CPU
+fallback (the CPU restatement of the reference lives in oracle/ and is test
+infrastructure only).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libemqx_tm.so")
+
+TM_OK = 0
+TM_EINVAL = -1
+TM_ENOMEM = -2
+TM_EDEVICE = -3
+TM_ESTATE = -4
+TM_ENOTFOUND = -5
+
+TM_TOPIC_OK = 0
+TM_BADARG = 1
+
+TM_OP_ADD = 1
+TM_OP_DEL = 2
+TM_KEY_WORDS = 1
+
+TM_MATCH_ALL = 0
+TM_MATCH_UNIQUE = 1
+TM_MATCH_FIRST = 2
+
+TM_CFG_FORCE_SLOW = 1
+
+# every symbol include/emqx_tm.h declares (tests check the .so exports them all)
+EXPORTS = (
+    "tm_abi_version", "tm_create", "tm_destroy", "tm_last_error", "tm_apply", "tm_apply_packed",
+    "tm_commit_epoch", "tm_match_batch", "tm_match_device", "tm_device_sync",
+    "tm_reserve_matches", "tm_key_info", "tm_key_ids", "tm_stats", "tm_debug_stats", "tm_debug_timing",
+)
+
+
+class tm_config(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32), ("flags", C.c_uint32),
+        ("reserve_keys", C.c_uint32), ("reserve_nodes", C.c_uint32),
+        ("reserve_topics", C.c_uint32), ("reserve_matches", C.c_uint32),
+        ("reserved", C.c_uint32 * 4),
+    ]
+
+
+class tm_op(C.Structure):
+    _fields_ = [
+        ("op", C.c_uint32), ("flags", C.c_uint32),
+        ("filter", C.c_void_p), ("filter_len", C.c_uint32), ("_pad", C.c_uint32),
+        ("id", C.c_uint64),
+    ]
+
+
+class tm_result(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint32), ("_pad", C.c_uint32), ("total", C.c_uint64),
+        ("off", C.POINTER(C.c_uint32)), ("cnt", C.POINTER(C.c_uint32)),
+        ("keys", C.POINTER(C.c_uint32)), ("status", C.POINTER(C.c_int32)),
+    ]
+
+
+class tm_dev_result(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint32), ("_pad", C.c_uint32),
+        ("d_off", C.c_void_p), ("d_cnt", C.c_void_p), ("d_keys", C.c_void_p),
+        ("d_status", C.c_void_p), ("d_total", C.c_void_p), ("keys_cap", C.c_uint64),
+    ]
+
+
+class tm_stats_t(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "epoch", "n_keys", "n_nodes", "n_words", "edge_slots", "word_slots", "list_words",
+        "device_bytes", "n_full_rebuilds", "n_delta_commits", "n_slow_topics")]
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libemqx_tm.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the HIP extension is the only matching path; there is no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    lib.tm_abi_version.restype = C.c_uint32
+    lib.tm_create.argtypes = [P(tm_config), P(C.c_void_p)]
+    lib.tm_destroy.argtypes = [C.c_void_p]
+    lib.tm_destroy.restype = None
+    lib.tm_last_error.argtypes = [C.c_void_p]
+    lib.tm_last_error.restype = C.c_char_p
+    lib.tm_apply.argtypes = [C.c_void_p, P(tm_op), C.c_size_t]
+    lib.tm_apply_packed.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_size_t]
+    lib.tm_commit_epoch.argtypes = [C.c_void_p, P(C.c_uint64)]
+    lib.tm_match_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, P(tm_result)]
+    lib.tm_match_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64,
+                                    C.c_void_p, P(tm_dev_result)]
+    lib.tm_device_sync.argtypes = [C.c_void_p]
+    lib.tm_reserve_matches.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32]
+    lib.tm_key_info.argtypes = [C.c_void_p, C.c_uint32, P(C.c_uint64), P(C.c_uint32), C.c_void_p,
+                                C.c_uint32, P(C.c_uint32)]
+    lib.tm_key_ids.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+    lib.tm_stats.argtypes = [C.c_void_p, P(tm_stats_t)]
+    lib.tm_debug_timing.argtypes = [C.c_void_p, C.c_int, P(C.c_float)]
+    lib.tm_debug_stats.argtypes = [C.c_void_p, C.c_int, P(C.c_uint64)]
+    for name in EXPORTS:
+        if name not in ("tm_destroy", "tm_last_error", "tm_abi_version"):
+            getattr(lib, name).restype = C.c_int
+    _lib = lib
+    return lib
+
+
+class TMError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__(f"tm error {rc}: {msg}")
+        self.rc = rc
+
+
+def pack_topics(topics) -> tuple[np.ndarray, np.ndarray]:
+    """Topics (bytes/str) -> (uint8 bytes, uint32 offsets[n+1])."""
+    bs = [t.encode() if isinstance(t, str) else bytes(t) for t in topics]
+    off = np.zeros(len(bs) + 1, dtype=np.uint32)
+    if bs:
+        off[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64).astype(np.uint32)
+    buf = np.frombuffer(b"".join(bs) + b"\0" * 16, dtype=np.uint8)
+    return buf, off
+
+
+class Engine:
+    """One engine = one GPU.  Thin owner of a tm_engine*."""
+
+    def __init__(self, device: int = 0, *, force_slow: bool = False, reserve_keys: int = 0,
+                 reserve_nodes: int = 0, reserve_matches: int = 0):
+        self.lib = load()
+        cfg = tm_config()
+        cfg.device = device
+        cfg.flags = TM_CFG_FORCE_SLOW if force_slow else 0
+        cfg.reserve_keys = reserve_keys
+        cfg.reserve_nodes = reserve_nodes
+        cfg.reserve_matches = reserve_matches
+        h = C.c_void_p()
+        rc = self.lib.tm_create(C.byref(cfg), C.byref(h))
+        if rc != TM_OK:
+            raise TMError(rc, "tm_create failed (no gfx950 HIP device visible?)")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.tm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int):
+        if rc != TM_OK:
+            raise TMError(rc, self.lib.tm_last_error(self.h).decode(errors="replace"))
+
+    # ---- writes
+    def apply(self, ops):
+        """ops: iterable of (op, filter_bytes, id[, flags])."""
+        ops = list(ops)
+        if not ops:
+            return
+        arr = (tm_op * len(ops))()
+        keep = []
+        for i, o in enumerate(ops):
+            op, f, ident = o[0], o[1], o[2]
+            flags = o[3] if len(o) > 3 else 0
+            fb = f.encode() if isinstance(f, str) else bytes(f)
+            cb = C.create_string_buffer(fb, len(fb) + 1)
+            keep.append(cb)
+            arr[i].op = op
+            arr[i].flags = flags
+            arr[i].filter = C.cast(cb, C.c_void_p)
+            arr[i].filter_len = len(fb)
+            arr[i].id = ident
+        self._check(self.lib.tm_apply(self.h, arr, len(ops)))
+
+    def apply_packed(self, op: int, buf: np.ndarray, off: np.ndarray, ids: np.ndarray, flags=None):
+        """Bulk ops: filter i = buf[off[i]:off[i+1]] (off uint64, n+1 entries), id ids[i]."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        n = len(ids)
+        assert len(off) == n + 1
+        fl = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint32)
+        self._check(self.lib.tm_apply_packed(self.h, op, buf.ctypes.data, off.ctypes.data, ids.ctypes.data,
+                                             None if fl is None else fl.ctypes.data, n))
+
+    def commit(self) -> int:
+        ep = C.c_uint64()
+        self._check(self.lib.tm_commit_epoch(self.h, C.byref(ep)))
+        return ep.value
+
+    # ---- reads
+    def match_packed(self, buf: np.ndarray, off: np.ndarray, mode: int = TM_MATCH_ALL):
+        """Match a packed batch; returns (off, cnt, keys, status) numpy copies."""
+        n = len(off) - 1
+        res = tm_result()
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        self._check(self.lib.tm_match_batch(self.h, buf.ctypes.data, off.ctypes.data, n, mode, C.byref(res)))
+        if n == 0:
+            e = np.zeros(0, dtype=np.uint32)
+            return e, e, e, np.zeros(0, dtype=np.int32)
+        o = np.ctypeslib.as_array(res.off, shape=(n,)).copy()
+        c = np.ctypeslib.as_array(res.cnt, shape=(n,)).copy()
+        st = np.ctypeslib.as_array(res.status, shape=(n,)).copy()
+        k = (np.ctypeslib.as_array(res.keys, shape=(res.total,)).copy() if res.total
+             else np.zeros(0, dtype=np.uint32))
+        return o, c, k, st
+
+    def match(self, topics, mode: int = TM_MATCH_ALL):
+        """List of topics -> list of key-handle lists (None for badarg topics)."""
+        buf, off = pack_topics(topics)
+        o, c, k, st = self.match_packed(buf, off, mode)
+        out = []
+        for i in range(len(topics)):
+            if st[i] == TM_BADARG:
+                out.append(None)
+            else:
+                out.append(k[o[i]:o[i] + c[i]].tolist())
+        return out
+
+    def key_info(self, key: int):
+        ident = C.c_uint64()
+        flags = C.c_uint32()
+        ln = C.c_uint32()
+        self._check(self.lib.tm_key_info(self.h, key, C.byref(ident), C.byref(flags), None, 0, C.byref(ln)))
+        buf = C.create_string_buffer(max(ln.value, 1))
+        self._check(self.lib.tm_key_info(self.h, key, C.byref(ident), C.byref(flags), buf, ln.value,
+                                         C.byref(ln)))
+        return ident.value, buf.raw[:ln.value], flags.value
+
+    def key_ids(self, keys: np.ndarray) -> np.ndarray:
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        out = np.zeros(len(keys), dtype=np.uint64)
+        if len(keys):
+            self._check(self.lib.tm_key_ids(self.h, keys.ctypes.data, len(keys), out.ctypes.data))
+        return out
+
+    def timing(self, enable: bool):
+        """Arm (True) / read (False -> ms of k_match_fast in the last match) kernel timing."""
+        ms = C.c_float()
+        self._check(self.lib.tm_debug_timing(self.h, 1 if enable else 0, None if enable else C.byref(ms)))
+        return None if enable else ms.value
+
+    def stats(self) -> dict:
+        s = tm_stats_t()
+        self._check(self.lib.tm_stats(self.h, C.byref(s)))
+        return {n: getattr(s, n) for n, _ in tm_stats_t._fields_}
+
+    def debug_stats(self, enable: bool, read: bool = True):
+        out = (C.c_uint64 * 5)()
+        self._check(self.lib.tm_debug_stats(self.h, 1 if enable else 0, out if read else None))
+        return list(out) if read else None
+
+    # ---- device-resident path (bench)
+    def match_device(self, d_bytes: int, d_off: int, n: int, total_bytes: int, stream: int = 0):
+        r = tm_dev_result()
+        self._check(self.lib.tm_match_device(self.h, C.c_void_p(d_bytes), C.c_void_p(d_off), n, total_bytes,
+                                             C.c_void_p(stream) if stream else None, C.byref(r)))
+        return r
+
+    def device_sync(self):
+        self._check(self.lib.tm_device_sync(self.h))
+
+    def reserve_matches(self, keys_cap: int, topics: int = 0):
+        self._check(self.lib.tm_reserve_matches(self.h, keys_cap, topics))

@@ -1,0 +1,56 @@
+// device_api.h — private interface between the host engine (engine.cpp) and
+// the gfx950 kernels (match_kernels.hip).  Not part of the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "layout.h"
+
+namespace tmx {
+
+// Everything one match launch needs.  Device pointers only.
+struct MatchArgs {
+    // topic batch: topic i is bytes[off[i] .. off[i+1])
+    const uint8_t *bytes;
+    const uint32_t *off;
+    uint32_t n;
+    uint32_t force_slow;  // 1: every topic takes the spill kernel (test aid)
+    // frozen index
+    const WordSlot *wtab;
+    uint64_t wmask;
+    const uint8_t *warena;
+    const EdgeSlot *etab;
+    uint64_t emask;
+    const RootRec *root;
+    const uint32_t *arena;
+    // results
+    uint32_t *out_off;
+    uint32_t *out_cnt;
+    int32_t *status;
+    uint32_t *keys;
+    uint64_t keys_cap;
+    unsigned long long *cursor;  // keys requested so far (may exceed keys_cap)
+    // spill path
+    uint32_t *slow_list;
+    uint32_t *slow_count;
+    uint32_t *scratch_w;  // (total bytes + 2n + 2) u32: word ids, at off[t]-off[0] + 2t
+    uint64_t *scratch_s;  // (total bytes + 2n + 2) u64: DFS stack, same indexing
+    // optional walk statistics (nullptr = off): [0] node visits, [1] edge-slot
+    // probes, [2] word-slot probes, [3] keys emitted, [4] levels
+    unsigned long long *stats;
+    // optional: events recorded around k_match_fast on the launch stream
+    hipEvent_t ev_fast0, ev_fast1;
+};
+
+// Enqueue the whole match pipeline for one batch on `stream`:
+// reset counters, fast wave-BFS kernel, spill kernel for topics the fast
+// kernel handed off.  Asynchronous.
+hipError_t launch_match(const MatchArgs &a, hipStream_t stream);
+
+// Delta-epoch patches: dst[idx[i]] = src[i].
+hipError_t launch_scatter_edges(EdgeSlot *dst, const uint64_t *idx, const EdgeSlot *src,
+                                uint64_t n, hipStream_t stream);
+hipError_t launch_scatter_words(WordSlot *dst, const uint64_t *idx, const WordSlot *src,
+                                uint64_t n, hipStream_t stream);
+
+}  // namespace tmx

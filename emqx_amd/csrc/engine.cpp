@@ -1,0 +1,1108 @@
+// engine.cpp — host side of the MI355X topic-matching engine and the C-ABI
+// declared in include/emqx_tm.h.
+//
+// What the reference does on this side of the path, and what replaces it:
+//   * emqx_topic_index:insert/4 / delete/3 (apps/emqx/src/emqx_topic_index.erl:53-62) write one
+//     {Words | Binary, {ID}} key into an ETS ordered_set (key shape from
+//     emqx_trie_search:make_key/2, apps/emqx/src/emqx_trie_search.erl:115-128).
+//     Here tm_apply stages the op and tm_commit_epoch folds a whole batch of ops into
+//     the frozen trie (one delta epoch), like emqx_router_syncer batches route ops
+//     (apps/emqx/src/emqx_router_syncer.erl:244-280,381-401).
+//   * emqx_topic_index:matches/3 / emqx_router:match_routes/1 run the ETS seek walk per
+//     topic (apps/emqx/src/emqx_trie_search.erl:192-389).  Here tm_match_batch ships a
+//     whole batch of topics to the GPU kernels in match_kernels.hip.
+//
+// Host state is the source of truth; the device copy is a derived cache rebuilt
+// from it (SURVEY.md §5 checkpoint/resume).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/emqx_tm.h"
+#include "device_api.h"
+#include "layout.h"
+
+using namespace tmx;
+
+namespace {
+
+// key kinds (where the key hangs in the trie)
+enum : uint8_t {
+    K_FREE = 0,
+    K_EXACT_BIN = 1,    // {Binary, {ID}}: filter without wildcards, binary form
+    K_EXACT_WORDS = 2,  // {Words, {ID}}: same filter given as a word list
+    K_WILD = 3,         // wildcard filter without a final '#': ends at the node
+    K_HASH = 4,         // "P/#": lives in P's hash list
+    K_DEAD = 5,         // '#' before the last level: can never match
+};
+inline bool is_term_kind(uint8_t k) { return k == K_EXACT_BIN || k == K_EXACT_WORDS || k == K_WILD; }
+
+struct KeyRec {
+    uint32_t node;  // terminal node (NONE for K_DEAD)
+    uint8_t kind;
+    uint8_t _p[3];
+    uint64_t id;
+};
+
+struct Delta {
+    uint32_t node;
+    uint32_t key;
+    uint8_t hash;  // 1: hash list, 0: term list
+    uint8_t add;   // 1 add, 0 delete
+};
+
+struct StagedOp {
+    uint32_t op, flags;
+    uint64_t id;
+    uint64_t off;  // filter bytes in tm_engine::stage_bytes
+    uint32_t len;
+};
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes ? bytes : 64;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 4096);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+inline uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+struct tm_engine {
+    tm_config cfg{};
+    std::string err;
+    uint64_t epoch = 0;
+
+    // ---- words (interner + device word table mirror)
+    std::vector<WordSlot> wtab;
+    uint64_t wmask = 0;
+    std::vector<uint8_t> warena;
+    std::vector<uint32_t> word_off, word_len;  // by word id
+    size_t warena_dev = 0;                      // bytes of warena already on device
+
+    // ---- edges / nodes
+    std::vector<EdgeSlot> etab;
+    uint64_t emask = 0;
+    uint64_t n_edges = 0;
+    std::vector<uint32_t> node_parent, node_word, node_slot;
+    RootRec root{0, 0, 0, 0};
+
+    // ---- terminal-list arena
+    std::vector<uint32_t> arena;
+    uint64_t arena_garbage = 0;
+    size_t arena_dev = 0;  // words already on device
+
+    // ---- keys
+    std::vector<KeyRec> keys;
+    std::vector<uint32_t> free_keys, free_pending;
+    uint64_t n_live = 0;
+    std::vector<uint32_t> kset;  // open addressing over key handles
+    uint64_t kmask = 0, kset_used = 0;
+    std::map<std::pair<std::string, uint64_t>, uint32_t> dead_keys;
+    std::vector<std::string> dead_filter;  // by key handle (only K_DEAD entries non-empty)
+
+    // ---- staged ops and epoch deltas
+    std::vector<StagedOp> staged;
+    std::vector<uint8_t> stage_bytes;
+    std::vector<std::pair<uint32_t, uint32_t>> lv_scratch;  // classify(): (start, len) per level
+    std::vector<Delta> deltas;
+    std::vector<uint64_t> dirty_eslots, dirty_wslots;
+    bool root_dirty = true;
+    bool need_full = true;  // full device upload at next commit
+
+    // ---- device copy
+    DevBuf d_wtab, d_warena, d_etab, d_root, d_arena;
+    DevBuf d_scatter_idx, d_scatter_src;
+    // batch buffers
+    DevBuf d_bytes, d_off, d_outoff, d_outcnt, d_status, d_keys, d_cursor, d_slow_list,
+        d_slow_count, d_scr_w, d_scr_s, d_stats;
+    uint64_t keys_cap = 0;
+    PinBuf h_bytes, h_off, h_outoff, h_outcnt, h_status, h_keys, h_cursor;
+    std::vector<uint32_t> pp_off, pp_cnt, pp_keys;  // post-processed results
+    hipStream_t stream = nullptr;
+    uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0;
+    bool stats_on = false;
+    hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // around k_match_fast (tm_debug_timing)
+    bool timing_on = false;
+
+    // =====================================================================
+    // words
+    uint32_t word_lookup(const uint8_t *p, uint32_t len) const {
+        uint64_t h = FNV_OFF;
+        for (uint32_t i = 0; i < len; i++) h = fnv_step(h, p[i]);
+        uint64_t s = word_slot_hash(h, len) & wmask;
+        for (;;) {
+            const WordSlot &w = wtab[s];
+            if (w.wid == NONE) return NONE;
+            if (w.hash == h && w.len == len && memcmp(&warena[w.arena_off], p, len) == 0) return w.wid;
+            s = (s + 1) & wmask;
+        }
+    }
+    void word_rehash(uint64_t cap) {
+        std::vector<WordSlot> old;
+        old.swap(wtab);
+        wtab.assign(cap, WordSlot{0, NONE, 0, 0, {0}});
+        wmask = cap - 1;
+        for (const WordSlot &w : old)
+            if (w.wid != NONE) {
+                uint64_t s = word_slot_hash(w.hash, w.len) & wmask;
+                while (wtab[s].wid != NONE) s = (s + 1) & wmask;
+                wtab[s] = w;
+            }
+        need_full = true;
+    }
+    uint32_t word_intern(const uint8_t *p, uint32_t len) {
+        uint32_t wid = word_lookup(p, len);
+        if (wid != NONE) return wid;
+        if ((word_off.size() + 1) * 2 > wtab.size()) word_rehash(wtab.size() * 2);
+        uint64_t h = FNV_OFF;
+        for (uint32_t i = 0; i < len; i++) h = fnv_step(h, p[i]);
+        WordSlot w{};
+        w.hash = h;
+        w.wid = (uint32_t)word_off.size();
+        w.len = len;
+        w.arena_off = (uint32_t)warena.size();
+        memset(w.inl, 0, sizeof(w.inl));
+        memcpy(w.inl, p, std::min<uint32_t>(len, WORD_INLINE));
+        warena.insert(warena.end(), p, p + len);
+        word_off.push_back(w.arena_off);
+        word_len.push_back(len);
+        uint64_t s = word_slot_hash(h, len) & wmask;
+        while (wtab[s].wid != NONE) s = (s + 1) & wmask;
+        wtab[s] = w;
+        dirty_wslots.push_back(s);
+        return w.wid;
+    }
+
+    // =====================================================================
+    // edges
+    uint64_t edge_find(uint32_t parent, uint32_t word) const {
+        uint64_t s = edge_hash(parent, word) & emask;
+        for (;;) {
+            const EdgeSlot &e = etab[s];
+            if (e.parent == NONE) return ~0ull;
+            if (e.parent == parent && e.word == word) return s;
+            s = (s + 1) & emask;
+        }
+    }
+    void edge_rehash(uint64_t cap) {
+        std::vector<EdgeSlot> old;
+        old.swap(etab);
+        EdgeSlot empty{};
+        empty.parent = NONE;
+        etab.assign(cap, empty);
+        emask = cap - 1;
+        for (const EdgeSlot &e : old)
+            if (e.parent != NONE) {
+                uint64_t s = edge_hash(e.parent, e.word) & emask;
+                while (etab[s].parent != NONE) s = (s + 1) & emask;
+                etab[s] = e;
+                node_slot[e.child] = (uint32_t)s;
+            }
+        need_full = true;
+    }
+    void node_set_flag(uint32_t node, uint32_t f) {
+        if (node == ROOT) {
+            if ((root.flags & f) != f) {
+                root.flags |= f;
+                root_dirty = true;
+            }
+            return;
+        }
+        EdgeSlot &e = etab[node_slot[node]];
+        if ((e.flags & f) != f) {
+            e.flags |= f;
+            dirty_eslots.push_back(node_slot[node]);
+        }
+    }
+    uint32_t edge_child(uint32_t parent, uint32_t word) {
+        uint64_t s = edge_find(parent, word);
+        if (s != ~0ull) return etab[s].child;
+        if ((n_edges + 1) * 2 > etab.size()) {
+            edge_rehash(etab.size() * 2);
+        }
+        uint32_t child = (uint32_t)node_parent.size();
+        node_parent.push_back(parent);
+        node_word.push_back(word);
+        node_slot.push_back(NONE);
+        s = edge_hash(parent, word) & emask;
+        while (etab[s].parent != NONE) s = (s + 1) & emask;
+        EdgeSlot e{};
+        e.parent = parent;
+        e.word = word;
+        e.child = child;
+        etab[s] = e;
+        node_slot[child] = (uint32_t)s;
+        n_edges++;
+        dirty_eslots.push_back(s);
+        node_set_flag(parent, word == W_PLUS ? F_PLUS : F_LIT);
+        return child;
+    }
+
+    // =====================================================================
+    // key set (linear probing over handles, backward-shift delete)
+    static uint64_t key_hash(uint32_t node, uint8_t kind, uint64_t id) {
+        return mix64(mix64(((uint64_t)node << 8) | kind) ^ id);
+    }
+    void kset_rehash(uint64_t cap) {
+        std::vector<uint32_t> old;
+        old.swap(kset);
+        kset.assign(cap, NONE);
+        kmask = cap - 1;
+        for (uint32_t h : old)
+            if (h != NONE) {
+                const KeyRec &k = keys[h];
+                uint64_t s = key_hash(k.node, k.kind, k.id) & kmask;
+                while (kset[s] != NONE) s = (s + 1) & kmask;
+                kset[s] = h;
+            }
+    }
+    uint32_t kset_find(uint32_t node, uint8_t kind, uint64_t id, uint64_t *slot_out) const {
+        uint64_t s = key_hash(node, kind, id) & kmask;
+        for (;;) {
+            uint32_t h = kset[s];
+            if (h == NONE) {
+                if (slot_out) *slot_out = s;
+                return NONE;
+            }
+            const KeyRec &k = keys[h];
+            if (k.node == node && k.kind == kind && k.id == id) {
+                if (slot_out) *slot_out = s;
+                return h;
+            }
+            s = (s + 1) & kmask;
+        }
+    }
+    void kset_erase_slot(uint64_t i) {
+        // backward-shift deletion for linear probing
+        uint64_t j = i;
+        for (;;) {
+            j = (j + 1) & kmask;
+            uint32_t h = kset[j];
+            if (h == NONE) break;
+            const KeyRec &k = keys[h];
+            uint64_t home = key_hash(k.node, k.kind, k.id) & kmask;
+            // can the entry at j move to i?
+            bool move = (i <= j) ? (home <= i || home > j) : (home <= i && home > j);
+            if (move) {
+                kset[i] = h;
+                i = j;
+            }
+        }
+        kset[i] = NONE;
+        kset_used--;
+    }
+    uint32_t alloc_key() {
+        if (!free_keys.empty()) {
+            uint32_t h = free_keys.back();
+            free_keys.pop_back();
+            return h;
+        }
+        keys.push_back(KeyRec{NONE, K_FREE, {0, 0, 0}, 0});
+        dead_filter.emplace_back();
+        return (uint32_t)(keys.size() - 1);
+    }
+
+    // =====================================================================
+    // filter parsing: emqx_trie_search:filter/1 + make_key/2 (emqx_trie_search.erl:115-140,358-366)
+    // Returns kind and the terminal node (creating the path when `create`).
+    bool classify(const uint8_t *f, uint32_t flen, uint32_t flags, bool create, uint8_t *kind_out,
+                  uint32_t *node_out) {
+        // split on '/': tokens (emqx_topic.erl:276-278)
+        std::vector<std::pair<uint32_t, uint32_t>> &lv = lv_scratch;  // (start, len)
+        lv.clear();
+        uint32_t st = 0;
+        for (uint32_t i = 0; i <= flen; i++) {
+            if (i == flen || f[i] == '/') {
+                lv.push_back({st, i - st});
+                st = i + 1;
+            }
+        }
+        bool wild = false;
+        int hash_pos = -1;
+        for (size_t i = 0; i < lv.size(); i++) {
+            const uint8_t *p = f + lv[i].first;
+            if (lv[i].second == 1 && (*p == '+' || *p == '#')) wild = true;
+            if (lv[i].second == 1 && *p == '#' && hash_pos < 0) hash_pos = (int)i;
+        }
+        if (hash_pos >= 0 && hash_pos != (int)lv.size() - 1) {
+            *kind_out = K_DEAD;
+            *node_out = NONE;
+            return true;
+        }
+        uint8_t kind = !wild ? ((flags & TM_KEY_WORDS) ? K_EXACT_WORDS : K_EXACT_BIN)
+                             : (hash_pos >= 0 ? K_HASH : K_WILD);
+        size_t nwalk = (kind == K_HASH) ? lv.size() - 1 : lv.size();
+        uint32_t node = ROOT;
+        for (size_t i = 0; i < nwalk; i++) {
+            const uint8_t *p = f + lv[i].first;
+            uint32_t len = lv[i].second;
+            uint32_t w;
+            if (len == 1 && *p == '+') {
+                w = W_PLUS;
+            } else if (create) {
+                w = word_intern(p, len);
+            } else {
+                w = word_lookup(p, len);
+                if (w == NONE) return false;
+            }
+            if (create) {
+                node = edge_child(node, w);
+            } else {
+                uint64_t s = edge_find(node, w);
+                if (s == ~0ull) return false;
+                node = etab[s].child;
+            }
+        }
+        *kind_out = kind;
+        *node_out = node;
+        return true;
+    }
+
+    void apply_one(const StagedOp &op) {
+        uint8_t kind;
+        uint32_t node;
+        const uint8_t *fp = stage_bytes.data() + op.off;
+        if (op.op == TM_OP_ADD) {
+            classify(fp, op.len, op.flags, true, &kind, &node);
+            if (kind == K_DEAD) {
+                auto key = std::make_pair(std::string((const char *)fp, op.len), op.id);
+                if (dead_keys.count(key)) return;
+                uint32_t h = alloc_key();
+                keys[h] = KeyRec{NONE, K_DEAD, {0, 0, 0}, op.id};
+                dead_filter[h] = key.first;
+                dead_keys[key] = h;
+                n_live++;
+                return;
+            }
+            if ((kset_used + 1) * 2 > kset.size()) kset_rehash(kset.size() * 2);
+            uint64_t slot;
+            if (kset_find(node, kind, op.id, &slot) != NONE) return;  // set semantics
+            uint32_t h = alloc_key();
+            keys[h] = KeyRec{node, kind, {0, 0, 0}, op.id};
+            kset[slot] = h;
+            kset_used++;
+            n_live++;
+            deltas.push_back(Delta{node, h, (uint8_t)(kind == K_HASH), 1});
+        } else if (op.op == TM_OP_DEL) {
+            if (!classify(fp, op.len, op.flags, false, &kind, &node)) return;  // idempotent
+            if (kind == K_DEAD) {
+                auto it = dead_keys.find(std::make_pair(std::string((const char *)fp, op.len), op.id));
+                if (it == dead_keys.end()) return;
+                uint32_t h = it->second;
+                keys[h] = KeyRec{NONE, K_FREE, {0, 0, 0}, 0};
+                dead_filter[h].clear();
+                dead_keys.erase(it);
+                free_pending.push_back(h);
+                n_live--;
+                return;
+            }
+            uint64_t slot;
+            uint32_t h = kset_find(node, kind, op.id, &slot);
+            if (h == NONE) return;
+            kset_erase_slot(slot);
+            deltas.push_back(Delta{node, h, (uint8_t)(kind == K_HASH), 0});
+            keys[h].kind = K_FREE;
+            free_pending.push_back(h);
+            n_live--;
+        }
+    }
+
+    // list location of a node
+    void node_list(uint32_t node, uint32_t **off, uint32_t **tc, uint32_t **hc) {
+        if (node == ROOT) {
+            *off = &root.list_off;
+            *tc = &root.term_cnt;
+            *hc = &root.hash_cnt;
+        } else {
+            EdgeSlot &e = etab[node_slot[node]];
+            *off = &e.list_off;
+            *tc = &e.term_cnt;
+            *hc = &e.hash_cnt;
+        }
+    }
+    void mark_node_dirty(uint32_t node) {
+        if (node == ROOT) root_dirty = true;
+        else dirty_eslots.push_back(node_slot[node]);
+    }
+
+    // Rebuild the whole arena from the key table (counting sort by node).
+    void rebuild_arena() {
+        size_t nn = node_parent.size();
+        std::vector<uint32_t> tcnt(nn, 0), hcnt(nn, 0);
+        for (size_t h = 0; h < keys.size(); h++) {
+            const KeyRec &k = keys[h];
+            if (k.kind == K_FREE || k.kind == K_DEAD) continue;
+            if (k.kind == K_HASH) hcnt[k.node]++;
+            else tcnt[k.node]++;
+        }
+        std::vector<uint32_t> pos(nn);
+        uint64_t total = 0;
+        for (size_t v = 0; v < nn; v++) {
+            pos[v] = (uint32_t)total;
+            total += tcnt[v] + hcnt[v];
+        }
+        arena.assign(total, 0);
+        std::vector<uint32_t> tfill(pos), hfill(nn);
+        for (size_t v = 0; v < nn; v++) hfill[v] = pos[v] + tcnt[v];
+        for (size_t h = 0; h < keys.size(); h++) {
+            const KeyRec &k = keys[h];
+            if (k.kind == K_FREE || k.kind == K_DEAD) continue;
+            if (k.kind == K_HASH) arena[hfill[k.node]++] = (uint32_t)h;
+            else arena[tfill[k.node]++] = (uint32_t)h;
+        }
+        for (size_t v = 0; v < nn; v++) {
+            uint32_t *o, *t, *hh;
+            node_list((uint32_t)v, &o, &t, &hh);
+            *o = (tcnt[v] + hcnt[v]) ? pos[v] : 0;
+            *t = tcnt[v];
+            *hh = hcnt[v];
+        }
+        arena_garbage = 0;
+        need_full = true;
+    }
+
+    // Fold this epoch's deltas into the arena by appending new lists for dirty nodes.
+    void apply_deltas() {
+        std::stable_sort(deltas.begin(), deltas.end(),
+                         [](const Delta &a, const Delta &b) { return a.node < b.node; });
+        std::vector<uint32_t> terms, hashes;
+        size_t i = 0;
+        while (i < deltas.size()) {
+            size_t j = i;
+            uint32_t node = deltas[i].node;
+            while (j < deltas.size() && deltas[j].node == node) j++;
+            uint32_t *o, *t, *hh;
+            node_list(node, &o, &t, &hh);
+            terms.assign(arena.begin() + *o, arena.begin() + *o + *t);
+            hashes.assign(arena.begin() + *o + *t, arena.begin() + *o + *t + *hh);
+            for (size_t k = i; k < j; k++) {
+                std::vector<uint32_t> &L = deltas[k].hash ? hashes : terms;
+                if (deltas[k].add) {
+                    L.push_back(deltas[k].key);
+                } else {
+                    auto it = std::find(L.begin(), L.end(), deltas[k].key);
+                    if (it != L.end()) L.erase(it);
+                }
+            }
+            arena_garbage += *t + *hh;
+            uint32_t off = (uint32_t)arena.size();
+            arena.insert(arena.end(), terms.begin(), terms.end());
+            arena.insert(arena.end(), hashes.begin(), hashes.end());
+            node_list(node, &o, &t, &hh);  // arena insert does not move slots, but be explicit
+            *o = (terms.size() + hashes.size()) ? off : 0;
+            *t = (uint32_t)terms.size();
+            *hh = (uint32_t)hashes.size();
+            mark_node_dirty(node);
+            i = j;
+        }
+    }
+
+    hipError_t upload_full() {
+        hipError_t e;
+        if ((e = d_wtab.ensure(wtab.size() * sizeof(WordSlot)))) return e;
+        if ((e = hipMemcpyAsync(d_wtab.p, wtab.data(), wtab.size() * sizeof(WordSlot),
+                                hipMemcpyHostToDevice, stream)))
+            return e;
+        if ((e = d_warena.ensure(std::max<size_t>(warena.size() * 3 / 2, 4096)))) return e;
+        if (!warena.empty() &&
+            (e = hipMemcpyAsync(d_warena.p, warena.data(), warena.size(), hipMemcpyHostToDevice, stream)))
+            return e;
+        warena_dev = warena.size();
+        if ((e = d_etab.ensure(etab.size() * sizeof(EdgeSlot)))) return e;
+        if ((e = hipMemcpyAsync(d_etab.p, etab.data(), etab.size() * sizeof(EdgeSlot),
+                                hipMemcpyHostToDevice, stream)))
+            return e;
+        if ((e = d_arena.ensure(std::max<size_t>(arena.size() * sizeof(uint32_t) * 3 / 2, 4096)))) return e;
+        if (!arena.empty() && (e = hipMemcpyAsync(d_arena.p, arena.data(), arena.size() * sizeof(uint32_t),
+                                                  hipMemcpyHostToDevice, stream)))
+            return e;
+        arena_dev = arena.size();
+        if ((e = d_root.ensure(sizeof(RootRec)))) return e;
+        if ((e = hipMemcpyAsync(d_root.p, &root, sizeof(RootRec), hipMemcpyHostToDevice, stream))) return e;
+        return hipStreamSynchronize(stream);
+    }
+
+    hipError_t upload_delta() {
+        hipError_t e;
+        // grow-or-append arenas
+        if (warena.size() > d_warena.cap || arena.size() * sizeof(uint32_t) > d_arena.cap) return upload_full();
+        if (warena.size() > warena_dev) {
+            if ((e = hipMemcpyAsync(d_warena.as<uint8_t>() + warena_dev, warena.data() + warena_dev,
+                                    warena.size() - warena_dev, hipMemcpyHostToDevice, stream)))
+                return e;
+            warena_dev = warena.size();
+        }
+        if (arena.size() > arena_dev) {
+            if ((e = hipMemcpyAsync(d_arena.as<uint32_t>() + arena_dev, arena.data() + arena_dev,
+                                    (arena.size() - arena_dev) * sizeof(uint32_t), hipMemcpyHostToDevice, stream)))
+                return e;
+            arena_dev = arena.size();
+        }
+        // scatter dirty slots
+        auto scatter = [&](std::vector<uint64_t> &dirty, auto &tab, auto *dtab, bool edges) -> hipError_t {
+            if (dirty.empty()) return hipSuccess;
+            std::sort(dirty.begin(), dirty.end());
+            dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+            size_t n = dirty.size();
+            using Slot = typename std::remove_reference<decltype(tab[0])>::type;
+            std::vector<Slot> src(n);
+            for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
+            hipError_t e2;
+            if ((e2 = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e2;
+            if ((e2 = d_scatter_src.ensure(n * sizeof(Slot)))) return e2;
+            if ((e2 = hipMemcpyAsync(d_scatter_idx.p, dirty.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                     stream)))
+                return e2;
+            if ((e2 = hipMemcpyAsync(d_scatter_src.p, src.data(), n * sizeof(Slot), hipMemcpyHostToDevice, stream)))
+                return e2;
+            if (edges)
+                e2 = launch_scatter_edges((EdgeSlot *)dtab, d_scatter_idx.as<uint64_t>(),
+                                          d_scatter_src.as<EdgeSlot>(), n, stream);
+            else
+                e2 = launch_scatter_words((WordSlot *)dtab, d_scatter_idx.as<uint64_t>(),
+                                          d_scatter_src.as<WordSlot>(), n, stream);
+            if (e2) return e2;
+            return hipStreamSynchronize(stream);  // src vectors die at scope exit
+        };
+        if ((e = scatter(dirty_wslots, wtab, d_wtab.p, false))) return e;
+        if ((e = scatter(dirty_eslots, etab, d_etab.p, true))) return e;
+        if (root_dirty) {
+            if ((e = hipMemcpyAsync(d_root.p, &root, sizeof(RootRec), hipMemcpyHostToDevice, stream))) return e;
+        }
+        return hipStreamSynchronize(stream);
+    }
+
+    int commit() {
+        for (const StagedOp &op : staged) apply_one(op);
+        staged.clear();
+        stage_bytes.clear();
+        bool full = need_full || deltas.size() > std::max<uint64_t>(n_live / 8, 1u << 16);
+        if (full) {
+            rebuild_arena();
+        } else if (!deltas.empty()) {
+            apply_deltas();
+            if (arena_garbage > std::max<uint64_t>(arena.size() / 2, 1u << 20)) rebuild_arena();
+        }
+        deltas.clear();
+        hipError_t e = need_full ? upload_full() : upload_delta();
+        if (e != hipSuccess) {
+            err = std::string("device upload failed: ") + hipGetErrorString(e);
+            return TM_EDEVICE;
+        }
+        if (need_full) n_full_rebuilds++;
+        else n_delta_commits++;
+        need_full = false;
+        root_dirty = false;
+        dirty_eslots.clear();
+        dirty_wslots.clear();
+        for (uint32_t h : free_pending) free_keys.push_back(h);
+        free_pending.clear();
+        epoch++;
+        return TM_OK;
+    }
+
+    // =====================================================================
+    // key -> filter bytes (emqx_topic_index:get_topic/1 = emqx_topic:join(Words))
+    std::string key_filter(uint32_t h) const {
+        const KeyRec &k = keys[h];
+        if (k.kind == K_DEAD) return dead_filter[h];
+        std::vector<uint32_t> path;
+        for (uint32_t v = k.node; v != ROOT; v = node_parent[v]) path.push_back(node_word[v]);
+        std::string s;
+        for (size_t i = path.size(); i-- > 0;) {
+            uint32_t w = path[i];
+            if (w == W_PLUS) s += '+';
+            else s.append((const char *)warena.data() + word_off[w], word_len[w]);
+            if (i) s += '/';
+        }
+        if (k.kind == K_HASH) s += path.empty() ? "#" : "/#";
+        return s;
+    }
+
+    // ETS term order of two keys (emqx_trie_search.erl:109-111 key shapes; Erlang term
+    // order: lists < binaries; atoms '#' < '+' < binaries; binaries bytewise; then {ID}).
+    // Used to reproduce return_first (the first key the ordered walk meets) and unique
+    // (last write wins in walk order) on top of an unordered match set.
+    void key_words(uint32_t h, std::vector<uint32_t> &out) const {
+        out.clear();
+        const KeyRec &k = keys[h];
+        for (uint32_t v = k.node; v != ROOT; v = node_parent[v]) out.push_back(node_word[v]);
+        std::reverse(out.begin(), out.end());
+        if (k.kind == K_HASH) out.push_back(NONE - 2);  // '#'
+    }
+    int cmp_word(uint32_t a, uint32_t b) const {
+        const uint32_t HASHW = NONE - 2;
+        auto cls = [&](uint32_t w) { return w == HASHW ? 0 : (w == W_PLUS ? 1 : 2); };
+        int ca = cls(a), cb = cls(b);
+        if (ca != cb) return ca < cb ? -1 : 1;
+        if (ca != 2 || a == b) return 0;
+        uint32_t la = word_len[a], lb = word_len[b];
+        int c = memcmp(&warena[word_off[a]], &warena[word_off[b]], std::min(la, lb));
+        if (c) return c < 0 ? -1 : 1;
+        return la < lb ? -1 : (la > lb ? 1 : 0);
+    }
+    int cmp_keys(uint32_t a, uint32_t b) const {
+        const KeyRec &ka = keys[a], &kb = keys[b];
+        bool ba = ka.kind == K_EXACT_BIN, bb = kb.kind == K_EXACT_BIN;
+        if (ba != bb) return ba ? 1 : -1;  // lists sort before binaries
+        int c;
+        if (ba) {
+            std::string fa = key_filter(a), fb = key_filter(b);
+            c = fa.compare(fb);  // bytewise (std::string compares as unsigned char)
+            c = c < 0 ? -1 : (c > 0 ? 1 : 0);
+        } else {
+            std::vector<uint32_t> wa, wb;
+            key_words(a, wa);
+            key_words(b, wb);
+            c = 0;
+            size_t n = std::min(wa.size(), wb.size());
+            for (size_t i = 0; i < n && !c; i++) c = cmp_word(wa[i], wb[i]);
+            if (!c && wa.size() != wb.size()) c = wa.size() < wb.size() ? -1 : 1;
+        }
+        if (c) return c;
+        return ka.id < kb.id ? -1 : (ka.id > kb.id ? 1 : 0);
+    }
+};
+
+// ============================================================================
+// C-ABI
+// ============================================================================
+
+#define TM_TRY_HIP(E, CODE, MSG)                                                     \
+    do {                                                                              \
+        hipError_t _e = (E);                                                          \
+        if (_e != hipSuccess) {                                                       \
+            eng->err = std::string(MSG) + ": " + hipGetErrorString(_e);              \
+            return CODE;                                                              \
+        }                                                                             \
+    } while (0)
+
+extern "C" {
+
+uint32_t tm_abi_version(void) { return TM_ABI_VERSION; }
+
+int tm_create(const tm_config *cfg, tm_engine **out) {
+    if (!out) return TM_EINVAL;
+    *out = nullptr;
+    tm_engine *eng = new (std::nothrow) tm_engine();
+    if (!eng) return TM_ENOMEM;
+    if (cfg) eng->cfg = *cfg;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= eng->cfg.device || eng->cfg.device < 0) {
+        delete eng;
+        return TM_EDEVICE;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, eng->cfg.device) != hipSuccess ||
+        std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        delete eng;
+        return TM_EDEVICE;  // kernels are built for gfx950 only
+    }
+    if (hipSetDevice(eng->cfg.device) != hipSuccess ||
+        hipStreamCreateWithFlags(&eng->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete eng;
+        return TM_EDEVICE;
+    }
+    uint64_t rk = eng->cfg.reserve_keys ? eng->cfg.reserve_keys : 1024;
+    uint64_t rn = eng->cfg.reserve_nodes ? eng->cfg.reserve_nodes : rk * 4;
+    eng->word_rehash(next_pow2(std::max<uint64_t>(rn / 2, 1024)));
+    eng->node_parent.reserve(rn);
+    eng->node_word.reserve(rn);
+    eng->node_slot.reserve(rn);
+    eng->node_parent.push_back(NONE);  // root
+    eng->node_word.push_back(NONE);
+    eng->node_slot.push_back(NONE);
+    eng->edge_rehash(next_pow2(std::max<uint64_t>(rn * 2, 1024)));
+    eng->kset_rehash(next_pow2(std::max<uint64_t>(rk * 2, 1024)));
+    eng->keys.reserve(rk);
+    eng->need_full = true;
+    int rc = eng->commit();  // empty epoch 1: device tables exist from the start
+    if (rc != TM_OK) {
+        tm_destroy(eng);
+        return rc;
+    }
+    *out = eng;
+    return TM_OK;
+}
+
+void tm_destroy(tm_engine *eng) {
+    if (!eng) return;
+    (void)hipSetDevice(eng->cfg.device);
+    if (eng->stream) (void)hipStreamSynchronize(eng->stream);
+    for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_etab, &eng->d_root, &eng->d_arena, &eng->d_scatter_idx,
+                      &eng->d_scatter_src, &eng->d_bytes, &eng->d_off, &eng->d_outoff, &eng->d_outcnt,
+                      &eng->d_status, &eng->d_keys, &eng->d_cursor, &eng->d_slow_list, &eng->d_slow_count,
+                      &eng->d_scr_w, &eng->d_scr_s, &eng->d_stats})
+        b->release();
+    for (PinBuf *b : {&eng->h_bytes, &eng->h_off, &eng->h_outoff, &eng->h_outcnt, &eng->h_status, &eng->h_keys,
+                      &eng->h_cursor})
+        b->release();
+    if (eng->ev_fast0) (void)hipEventDestroy(eng->ev_fast0);
+    if (eng->ev_fast1) (void)hipEventDestroy(eng->ev_fast1);
+    if (eng->stream) (void)hipStreamDestroy(eng->stream);
+    delete eng;
+}
+
+const char *tm_last_error(const tm_engine *eng) { return eng ? eng->err.c_str() : "null engine"; }
+
+int tm_apply(tm_engine *eng, const tm_op *ops, size_t n) {
+    if (!eng || (n && !ops)) return TM_EINVAL;
+    for (size_t i = 0; i < n; i++) {
+        const tm_op &o = ops[i];
+        if ((o.op != TM_OP_ADD && o.op != TM_OP_DEL) || o.filter_len > 65535u || (o.filter_len && !o.filter)) {
+            eng->err = "tm_apply: bad op";
+            return TM_EINVAL;
+        }
+    }
+    eng->staged.reserve(eng->staged.size() + n);
+    for (size_t i = 0; i < n; i++) {
+        const tm_op &o = ops[i];
+        eng->staged.push_back(StagedOp{o.op, o.flags, o.id, eng->stage_bytes.size(), o.filter_len});
+        eng->stage_bytes.insert(eng->stage_bytes.end(), o.filter, o.filter + o.filter_len);
+    }
+    return TM_OK;
+}
+
+int tm_apply_packed(tm_engine *eng, uint32_t op, const uint8_t *bytes, const uint64_t *off, const uint64_t *ids,
+                    const uint32_t *flags, size_t n) {
+    if (!eng || (n && (!off || !ids || (!bytes && off[n] > off[0])))) return TM_EINVAL;
+    if (op != TM_OP_ADD && op != TM_OP_DEL) return TM_EINVAL;
+    for (size_t i = 0; i < n; i++)
+        if (off[i + 1] < off[i] || off[i + 1] - off[i] > 65535u) {
+            eng->err = "tm_apply_packed: bad filter offsets";
+            return TM_EINVAL;
+        }
+    eng->staged.reserve(eng->staged.size() + n);
+    uint64_t base = eng->stage_bytes.size();
+    if (n) eng->stage_bytes.insert(eng->stage_bytes.end(), bytes + off[0], bytes + off[n]);
+    for (size_t i = 0; i < n; i++)
+        eng->staged.push_back(StagedOp{op, flags ? flags[i] : 0u, ids[i], base + (off[i] - off[0]),
+                                       (uint32_t)(off[i + 1] - off[i])});
+    return TM_OK;
+}
+
+int tm_commit_epoch(tm_engine *eng, uint64_t *epoch_out) {
+    if (!eng) return TM_EINVAL;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    int rc = eng->commit();
+    if (epoch_out) *epoch_out = eng->epoch;
+    return rc;
+}
+
+// Size the batch buffers for n topics / `bytes` topic bytes.
+static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
+    TM_TRY_HIP(eng->d_outoff.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_outcnt.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_status.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_slow_list.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_slow_count.ensure(64), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_cursor.ensure(64), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_stats.ensure(64), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_scr_w.ensure((bytes + 2ull * n + 2) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_scr_s.ensure((bytes + 2ull * n + 2) * 8), TM_ENOMEM, "alloc");
+    if (eng->keys_cap == 0) {
+        uint64_t want = eng->cfg.reserve_matches ? eng->cfg.reserve_matches : std::max<uint64_t>(n * 8ull, 1 << 16);
+        TM_TRY_HIP(eng->d_keys.ensure(want * 4), TM_ENOMEM, "alloc");
+        eng->keys_cap = want;
+    }
+    return TM_OK;
+}
+
+static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                                hipStream_t s) {
+    MatchArgs a{};
+    a.bytes = d_bytes;
+    a.off = d_off;
+    a.n = n;
+    a.force_slow = (eng->cfg.flags & TM_CFG_FORCE_SLOW) ? 1u : 0u;
+    a.wtab = eng->d_wtab.as<WordSlot>();
+    a.wmask = eng->wmask;
+    a.warena = eng->d_warena.as<uint8_t>();
+    a.etab = eng->d_etab.as<EdgeSlot>();
+    a.emask = eng->emask;
+    a.root = eng->d_root.as<RootRec>();
+    a.arena = eng->d_arena.as<uint32_t>();
+    a.out_off = eng->d_outoff.as<uint32_t>();
+    a.out_cnt = eng->d_outcnt.as<uint32_t>();
+    a.status = eng->d_status.as<int32_t>();
+    a.keys = eng->d_keys.as<uint32_t>();
+    a.keys_cap = eng->keys_cap;
+    a.cursor = eng->d_cursor.as<unsigned long long>();
+    a.slow_list = eng->d_slow_list.as<uint32_t>();
+    a.slow_count = eng->d_slow_count.as<uint32_t>();
+    a.scratch_w = eng->d_scr_w.as<uint32_t>();
+    a.scratch_s = eng->d_scr_s.as<uint64_t>();
+    a.stats = eng->stats_on ? eng->d_stats.as<unsigned long long>() : nullptr;
+    a.ev_fast0 = eng->timing_on ? eng->ev_fast0 : nullptr;
+    a.ev_fast1 = eng->timing_on ? eng->ev_fast1 : nullptr;
+    return launch_match(a, s);
+}
+
+int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
+                   tm_result *out) {
+    if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
+    if (mode > TM_MATCH_FIRST) return TM_EINVAL;
+    if (!eng->staged.empty()) {
+        eng->err = "tm_match_batch: staged ops not committed";
+        return TM_ESTATE;
+    }
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    memset(out, 0, sizeof(*out));
+    out->n = n;
+    if (n == 0) return TM_OK;
+    // rebase offsets to 0
+    uint32_t base = off[0];
+    uint64_t nbytes = (uint64_t)off[n] - base;
+    int rc = ensure_batch(eng, n, nbytes);
+    if (rc) return rc;
+    TM_TRY_HIP(eng->h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->h_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->d_bytes.ensure(nbytes + 16), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+    if (nbytes) memcpy(eng->h_bytes.p, bytes + base, nbytes);
+    uint32_t *ho = eng->h_off.as<uint32_t>();
+    for (uint32_t i = 0; i <= n; i++) ho[i] = off[i] - base;
+    hipStream_t s = eng->stream;
+    TM_TRY_HIP(hipMemcpyAsync(eng->d_bytes.p, eng->h_bytes.p, nbytes + 1, hipMemcpyHostToDevice, s), TM_EDEVICE,
+               "H2D");
+    TM_TRY_HIP(hipMemcpyAsync(eng->d_off.p, ho, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
+    TM_TRY_HIP(eng->h_cursor.ensure(64), TM_ENOMEM, "pinned alloc");
+    for (int attempt = 0; attempt < 2; attempt++) {
+        TM_TRY_HIP(enqueue_match(eng, eng->d_bytes.as<uint8_t>(), eng->d_off.as<uint32_t>(), n, s), TM_EDEVICE,
+                   "kernel launch");
+        TM_TRY_HIP(hipMemcpyAsync(eng->h_cursor.p, eng->d_cursor.p, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipMemcpyAsync((uint8_t *)eng->h_cursor.p + 8, eng->d_slow_count.p, 4, hipMemcpyDeviceToHost, s),
+                   TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "match kernels");
+        uint64_t total = *eng->h_cursor.as<uint64_t>();
+        eng->n_slow_last = *(uint32_t *)((uint8_t *)eng->h_cursor.p + 8);
+        if (total <= eng->keys_cap) break;
+        // output arena too small: grow to the demand and run again (once suffices:
+        // the cursor counts every key the batch asked for)
+        uint64_t want = total + total / 8 + 1024;
+        TM_TRY_HIP(eng->d_keys.ensure(want * 4), TM_ENOMEM, "alloc keys");
+        eng->keys_cap = want;
+    }
+    uint64_t total = *eng->h_cursor.as<uint64_t>();
+    TM_TRY_HIP(eng->h_outoff.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->h_outcnt.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->h_status.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->h_keys.ensure(total * 4 + 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(hipMemcpyAsync(eng->h_outoff.p, eng->d_outoff.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+               "D2H");
+    TM_TRY_HIP(hipMemcpyAsync(eng->h_outcnt.p, eng->d_outcnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+               "D2H");
+    TM_TRY_HIP(hipMemcpyAsync(eng->h_status.p, eng->d_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+               "D2H");
+    if (total)
+        TM_TRY_HIP(hipMemcpyAsync(eng->h_keys.p, eng->d_keys.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                   "D2H");
+    TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "D2H");
+    out->total = total;
+    out->off = eng->h_outoff.as<uint32_t>();
+    out->cnt = eng->h_outcnt.as<uint32_t>();
+    out->keys = eng->h_keys.as<uint32_t>();
+    out->status = eng->h_status.as<int32_t>();
+    if (mode == TM_MATCH_ALL) return TM_OK;
+
+    // UNIQUE / FIRST: reduce each topic's set under ETS term order.
+    eng->pp_off.resize(n);
+    eng->pp_cnt.resize(n);
+    eng->pp_keys.clear();
+    std::vector<uint32_t> tmp;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t *ks = out->keys + out->off[i];
+        uint32_t c = out->cnt[i];
+        eng->pp_off[i] = (uint32_t)eng->pp_keys.size();
+        if (c == 0) {
+            eng->pp_cnt[i] = 0;
+            continue;
+        }
+        tmp.assign(ks, ks + c);
+        std::sort(tmp.begin(), tmp.end(), [&](uint32_t a, uint32_t b) { return eng->cmp_keys(a, b) < 0; });
+        if (mode == TM_MATCH_FIRST) {
+            eng->pp_keys.push_back(tmp[0]);
+            eng->pp_cnt[i] = 1;
+        } else {
+            // maps:put in ascending walk order: the last (greatest) key per id wins,
+            // maps:values/1 returns them ordered by id (small maps are sorted).
+            std::vector<std::pair<uint64_t, uint32_t>> best;
+            for (uint32_t k : tmp) {
+                uint64_t id = eng->keys[k].id;
+                auto it = std::find_if(best.begin(), best.end(), [&](auto &p) { return p.first == id; });
+                if (it == best.end()) best.push_back({id, k});
+                else it->second = k;
+            }
+            std::sort(best.begin(), best.end());
+            for (auto &p : best) eng->pp_keys.push_back(p.second);
+            eng->pp_cnt[i] = (uint32_t)best.size();
+        }
+    }
+    out->off = eng->pp_off.data();
+    out->cnt = eng->pp_cnt.data();
+    out->keys = eng->pp_keys.data();
+    out->total = eng->pp_keys.size();
+    return TM_OK;
+}
+
+int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap) {
+    if (!eng) return TM_EINVAL;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    if (keys_cap > eng->keys_cap) {
+        TM_TRY_HIP(eng->d_keys.ensure(keys_cap * 4), TM_ENOMEM, "alloc keys");
+        eng->keys_cap = keys_cap;
+    }
+    (void)topics_cap;
+    return TM_OK;
+}
+
+int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                    uint64_t total_bytes, void *stream, tm_dev_result *out) {
+    if (!eng || !out || !d_off || (n && !d_bytes)) return TM_EINVAL;
+    if (!eng->staged.empty()) {
+        eng->err = "tm_match_device: staged ops not committed";
+        return TM_ESTATE;
+    }
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    // total_bytes = d_off[n] - d_off[0] sizes the spill kernel's scratch
+    int rc = ensure_batch(eng, n, total_bytes);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s), TM_EDEVICE, "kernel launch");
+    out->n = n;
+    out->d_off = eng->d_outoff.as<uint32_t>();
+    out->d_cnt = eng->d_outcnt.as<uint32_t>();
+    out->d_keys = eng->d_keys.as<uint32_t>();
+    out->d_status = eng->d_status.as<int32_t>();
+    out->d_total = eng->d_cursor.as<uint64_t>();
+    out->keys_cap = eng->keys_cap;
+    return TM_OK;
+}
+
+int tm_device_sync(tm_engine *eng) {
+    if (!eng) return TM_EINVAL;
+    TM_TRY_HIP(hipStreamSynchronize(eng->stream), TM_EDEVICE, "sync");
+    return TM_OK;
+}
+
+int tm_key_info(const tm_engine *eng, uint32_t key, uint64_t *id, uint32_t *flags, uint8_t *buf, uint32_t cap,
+                uint32_t *len) {
+    if (!eng) return TM_EINVAL;
+    if (key >= eng->keys.size() || eng->keys[key].kind == K_FREE) return TM_ENOTFOUND;
+    const KeyRec &k = eng->keys[key];
+    if (id) *id = k.id;
+    if (flags) *flags = (k.kind == K_EXACT_WORDS) ? TM_KEY_WORDS : 0u;
+    std::string f = eng->key_filter(key);
+    if (len) *len = (uint32_t)f.size();
+    if (buf && cap) memcpy(buf, f.data(), std::min<size_t>(cap, f.size()));
+    return TM_OK;
+}
+
+int tm_key_ids(const tm_engine *eng, const uint32_t *keys, size_t n, uint64_t *ids_out) {
+    if (!eng || (n && (!keys || !ids_out))) return TM_EINVAL;
+    for (size_t i = 0; i < n; i++) {
+        uint32_t k = keys[i];
+        if (k >= eng->keys.size() || eng->keys[k].kind == K_FREE) return TM_ENOTFOUND;
+        ids_out[i] = eng->keys[k].id;
+    }
+    return TM_OK;
+}
+
+int tm_stats(const tm_engine *eng, tm_stats_t *out) {
+    if (!eng || !out) return TM_EINVAL;
+    memset(out, 0, sizeof(*out));
+    out->epoch = eng->epoch;
+    out->n_keys = eng->n_live;
+    out->n_nodes = eng->node_parent.size();
+    out->n_words = eng->word_off.size();
+    out->edge_slots = eng->etab.size();
+    out->word_slots = eng->wtab.size();
+    out->list_words = eng->arena.size();
+    out->device_bytes = eng->d_wtab.cap + eng->d_warena.cap + eng->d_etab.cap + eng->d_arena.cap + eng->d_root.cap;
+    out->n_full_rebuilds = eng->n_full_rebuilds;
+    out->n_delta_commits = eng->n_delta_commits;
+    out->n_slow_topics = eng->n_slow_last;
+    return TM_OK;
+}
+
+// ---- diagnostics (not part of the reference surface): walk counters -------
+// Enable per-batch walk statistics (node visits, edge probes, word probes, keys,
+// levels), accumulated on the device across batches until read.
+int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out5) {
+    if (!eng) return TM_EINVAL;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    TM_TRY_HIP(eng->d_stats.ensure(64), TM_ENOMEM, "alloc");
+    if (out5) {
+        TM_TRY_HIP(hipStreamSynchronize(eng->stream), TM_EDEVICE, "sync");
+        TM_TRY_HIP(hipMemcpy(out5, eng->d_stats.p, 40, hipMemcpyDeviceToHost), TM_EDEVICE, "D2H");
+    }
+    TM_TRY_HIP(hipMemset(eng->d_stats.p, 0, 64), TM_EDEVICE, "memset");
+    eng->stats_on = enable != 0;
+    return TM_OK;
+}
+
+// Time the dominant kernel (k_match_fast) of the NEXT match call with HIP events
+// recorded on the stream it is launched on.  tm_debug_timing(eng, 1, NULL) arms;
+// after the match and a sync, tm_debug_timing(eng, 0, &ms) returns its duration.
+int tm_debug_timing(tm_engine *eng, int enable, float *ms_out) {
+    if (!eng) return TM_EINVAL;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    if (!eng->ev_fast0) {
+        TM_TRY_HIP(hipEventCreate(&eng->ev_fast0), TM_EDEVICE, "event");
+        TM_TRY_HIP(hipEventCreate(&eng->ev_fast1), TM_EDEVICE, "event");
+    }
+    if (ms_out) {
+        TM_TRY_HIP(hipEventSynchronize(eng->ev_fast1), TM_EDEVICE, "event sync");
+        TM_TRY_HIP(hipEventElapsedTime(ms_out, eng->ev_fast0, eng->ev_fast1), TM_EDEVICE, "elapsed");
+    }
+    eng->timing_on = enable != 0;
+    return TM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,160 @@
+"""Host mirror of `emqx_topic_index` (apps/emqx/src/emqx_topic_index.erl:21-32) over the
+MI355X engine.
+
+Same names, argument meaning and error behaviour as the reference module, so the
+reference's suite (apps/emqx/test/emqx_topic_index_SUITE.erl) reads the same:
+
+    tab = TopicIndex.new()
+    tab.insert(b"sensor/+/#", "t_insert_2", b"")      # insert/4
+    tab.matches(b"sensor/1", [])                      # matches/3 -> [Key]
+    tab.match(b"sensor")                              # match/2 -> Key | False
+    get_id(key), get_topic(key), tab.get_record(key)
+
+A key is the reference's `{Filter, {ID}}`: `(words_tuple | bytes, (ID,))`.  Writes are
+visible to the next read (ETS semantics for one caller): they are staged in the
+engine and committed as one delta epoch before the next match.  `matches_batch`
+is the batched entry point the GPU exists for.
+
+IDs may be any hashable Erlang-like term (int, str-as-atom, tuple, bytes); the
+engine sees a dense u64 per distinct ID and the mirror maps back.
+"""
+from __future__ import annotations
+
+from . import _native as N
+from .topic import HASH, PLUS, filter_words, join, term_key, wildcard
+
+
+class BadArg(ValueError):
+    """error(badarg): a topic level is exactly '+' or '#' (emqx_trie_search.erl:374-375)."""
+
+
+def make_key(topic_or_words, ident):
+    """emqx_trie_search:make_key/2 (emqx_trie_search.erl:115-128)."""
+    if isinstance(topic_or_words, (list, tuple)):
+        return (tuple(topic_or_words), (ident,))
+    ws = filter_words(topic_or_words)
+    if wildcard(ws):
+        return (tuple(ws), (ident,))
+    return (bytes(topic_or_words) if not isinstance(topic_or_words, str) else topic_or_words.encode(), (ident,))
+
+
+def get_id(key):
+    """emqx_topic_index:get_id/1."""
+    return key[1][0]
+
+
+def get_topic(key):
+    """emqx_topic_index:get_topic/1: join the words of a list key, or the binary."""
+    f = key[0]
+    return join(list(f)) if isinstance(f, tuple) else f
+
+
+def _key_order(key):
+    f, (ident,) = key
+    fk = term_key(list(f)) if isinstance(f, tuple) else term_key(f)
+    return (fk, term_key(ident))
+
+
+class TopicIndex:
+    def __init__(self, device: int = 0, engine: N.Engine | None = None, **engine_kw):
+        self.eng = engine or N.Engine(device, **engine_kw)
+        self._ids: dict = {}        # term -> u64
+        self._terms: list = []      # u64 -> term
+        self._records: dict = {}    # key -> record
+        self._dirty = False
+
+    @classmethod
+    def new(cls, device: int = 0, **kw) -> "TopicIndex":
+        return cls(device, **kw)
+
+    # ---- id mapping
+    def _id(self, term) -> int:
+        u = self._ids.get(term)
+        if u is None:
+            u = len(self._terms)
+            self._ids[term] = u
+            self._terms.append(term)
+        return u
+
+    @staticmethod
+    def _filter_bytes(filt):
+        """(bytes, flags) handed to the engine for a binary or word-list filter."""
+        if isinstance(filt, (list, tuple)):
+            ws = list(filt)
+            for w in ws:
+                if isinstance(w, (bytes, bytearray)) and b"/" in w:
+                    raise ValueError("word contains '/'")
+            return join(ws), N.TM_KEY_WORDS
+        return (filt.encode() if isinstance(filt, str) else bytes(filt)), 0
+
+    # ---- writes: insert/4, delete/3
+    def insert(self, filt, ident, record=b"", tab=None) -> bool:
+        fb, flags = self._filter_bytes(filt)
+        self.eng.apply([(N.TM_OP_ADD, fb, self._id(ident), flags)])
+        self._records[make_key(filt, ident)] = record
+        self._dirty = True
+        return True
+
+    def delete(self, filt, ident, tab=None) -> bool:
+        fb, flags = self._filter_bytes(filt)
+        if ident in self._ids:
+            self.eng.apply([(N.TM_OP_DEL, fb, self._ids[ident], flags)])
+            self._records.pop(make_key(filt, ident), None)
+            self._dirty = True
+        return True
+
+    def commit(self):
+        if self._dirty:
+            self.eng.commit()
+            self._dirty = False
+
+    # ---- reads
+    def _key_of(self, handle: int):
+        u, fb, flags = self.eng.key_info(handle)
+        ident = self._terms[u]
+        if flags & N.TM_KEY_WORDS or wildcard(filter_words(fb)):
+            return (tuple(filter_words(fb)), (ident,))
+        return (fb, (ident,))
+
+    def matches_batch(self, topics, opts=()) -> list:
+        """Batched matches/3: one list of keys per topic; BadArg instances for
+        topics with a '+'/'#' level."""
+        self.commit()
+        handles = self.eng.match(topics, N.TM_MATCH_ALL)
+        out = []
+        for hs in handles:
+            if hs is None:
+                out.append(BadArg("badarg"))
+                continue
+            keys = [self._key_of(h) for h in hs]
+            out.append(self._reduce(keys, opts))
+        return out
+
+    @staticmethod
+    def _reduce(keys, opts):
+        opts = list(opts)
+        if "return_first" in opts:
+            return [min(keys, key=_key_order)] if keys else []
+        if "unique" in opts:
+            best = {}
+            for k in sorted(keys, key=_key_order):  # ascending walk order: last write wins
+                best[get_id(k)] = k
+            return [best[i] for i in sorted(best, key=term_key)]
+        return keys
+
+    def matches(self, topic, tab=None, opts=()):
+        r = self.matches_batch([topic], opts)[0]
+        if isinstance(r, BadArg):
+            raise r
+        return r
+
+    def match(self, topic, tab=None):
+        """match/2: the first key in ETS term order, or False."""
+        r = self.matches(topic, None, ["return_first"])
+        return r[0] if r else False
+
+    def get_record(self, key, tab=None):
+        return self._records.get(key)
+
+    def stats(self):
+        return self.eng.stats()

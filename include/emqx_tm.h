@@ -1,0 +1,194 @@
+/*
+ * emqx_tm.h — C-ABI of the MI355X batched topic-matching engine.
+ *
+ * This is the drop-in boundary for EMQX's routing hot path: the lookup that
+ * emqx_router:match_routes/1 -> emqx_topic_index:matches/3 -> emqx_trie_search
+ * performs for every PUBLISH.  Everything above this header (an Erlang NIF, the
+ * Python mirror in emqx_amd/, bench.py) calls only these symbols; everything
+ * below it (host trie builder, delta epochs, HIP kernels for gfx950) is private.
+ *
+ * Reference interfaces replaced (paths relative to the ivangsm/emqx tree):
+ *   tm_create / tm_destroy      emqx_topic_index:new/0,1          apps/emqx/src/emqx_topic_index.erl:40-48
+ *   tm_apply (TM_OP_ADD)        emqx_topic_index:insert/4         apps/emqx/src/emqx_topic_index.erl:53-56
+ *                               emqx_router:do_add_route/2 (v2)   apps/emqx/src/emqx_router.erl:194-196,483-490
+ *   tm_apply (TM_OP_DEL)        emqx_topic_index:delete/3         apps/emqx/src/emqx_topic_index.erl:60-62
+ *                               emqx_router:do_delete_route/2     apps/emqx/src/emqx_router.erl:238-240,497-509
+ *   tm_apply batch + commit     emqx_router:do_batch/1 (syncer)   apps/emqx/src/emqx_router.erl:255-257,
+ *                                                                 apps/emqx/src/emqx_router_syncer.erl:381-401
+ *   tm_match_batch (ALL)        emqx_topic_index:matches/3 ([])   apps/emqx/src/emqx_topic_index.erl:76-78
+ *                               emqx_router:match_routes/1 (v2)   apps/emqx/src/emqx_router.erl:205-212,511-516
+ *   tm_match_batch (UNIQUE)     emqx_topic_index:matches/3 ([unique])  apps/emqx/src/emqx_trie_search.erl:350-352
+ *   tm_match_batch (FIRST)      emqx_topic_index:match/2 (return_first) apps/emqx/src/emqx_trie_search.erl:171-178
+ *   tm_key_info                 emqx_topic_index:get_id/1, get_topic/1 apps/emqx/src/emqx_topic_index.erl:87-94
+ *   tm_stats                    emqx_router:stats/1 (n_routes)    apps/emqx/src/emqx_router.erl:632-635
+ *
+ * Conventions
+ *   - No exceptions cross this ABI.  Every call returns an int status (TM_OK = 0,
+ *     negative on error); tm_last_error() gives a message for the last failure.
+ *   - A "key" is the reference's index key {Filter, {ID}} (emqx_trie_search.erl:110):
+ *     one (filter, id) pair.  Inserting the same pair twice is one key; deleting a
+ *     missing key is not an error (emqx_topic_index.erl:58-62).  The engine names
+ *     each live key by a stable u32 "key handle"; matches are reported as handles.
+ *   - Topics whose levels include a level exactly equal to "+" or "#" get the
+ *     per-topic status TM_BADARG, mirroring error(badarg) in
+ *     emqx_trie_search:word/2 (emqx_trie_search.erl:374-375).
+ *   - Ops are staged by tm_apply and become visible atomically at tm_commit_epoch
+ *     (one delta epoch).  Within one epoch the LAST op per key wins, the rule of
+ *     emqx_router_syncer:merge_route_op/2.  A match batch always sees exactly one
+ *     committed epoch (stronger than ETS' per-key atomicity).
+ *   - One engine drives one GPU (tm_config.device) and owns one HIP stream; calls
+ *     on one engine must be serialised by the caller (the NIF holds a lock).
+ */
+#ifndef EMQX_TM_H
+#define EMQX_TM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TM_ABI_VERSION 1u
+
+/* status codes */
+#define TM_OK          0
+#define TM_EINVAL     (-1)   /* bad argument */
+#define TM_ENOMEM     (-2)   /* host or device allocation failed */
+#define TM_EDEVICE    (-3)   /* HIP runtime error / no gfx950 device */
+#define TM_ESTATE     (-4)   /* call not valid in this state */
+#define TM_ENOTFOUND  (-5)   /* key handle not live */
+
+/* per-topic status in tm_result.status */
+#define TM_TOPIC_OK      0
+#define TM_BADARG        1   /* a level is exactly "+" or "#" */
+
+/* op kinds for tm_op.op */
+#define TM_OP_ADD 1u
+#define TM_OP_DEL 2u
+
+/* tm_op.flags */
+#define TM_KEY_WORDS 1u  /* key was given as a word list (emqx_trie_search:make_key/2 list
+                            clause, :127-128).  For a filter WITHOUT wildcards this is a
+                            different key from the binary form (:121-125); for a wildcard
+                            filter both forms are the same key. */
+
+/* match modes for tm_match_batch */
+#define TM_MATCH_ALL    0u  /* every matching key (matches/3 with [])            */
+#define TM_MATCH_UNIQUE 1u  /* one key per id (matches/3 with [unique])          */
+#define TM_MATCH_FIRST  2u  /* the first key in ETS term order (match/2)         */
+
+/* tm_config.flags */
+#define TM_CFG_FORCE_SLOW 1u  /* route every topic through the spill (slow) kernel: test aid */
+
+typedef struct tm_engine tm_engine;
+
+typedef struct tm_config {
+    int32_t  device;        /* HIP device ordinal                                  */
+    uint32_t flags;         /* TM_CFG_*                                            */
+    uint32_t reserve_keys;  /* capacity hints (0 = default); tables grow as needed */
+    uint32_t reserve_nodes;
+    uint32_t reserve_topics;      /* largest batch expected                    */
+    uint32_t reserve_matches;     /* expected matches per batch (output arena) */
+    uint32_t reserved[4];
+} tm_config;
+
+typedef struct tm_op {
+    uint32_t       op;          /* TM_OP_ADD | TM_OP_DEL          */
+    uint32_t       flags;       /* TM_KEY_*                       */
+    const uint8_t *filter;      /* filter bytes (not NUL-terminated) */
+    uint32_t       filter_len;  /* <= 65535 (MQTT max topic length) */
+    uint32_t       _pad;
+    uint64_t       id;          /* caller's record id / route dest id */
+} tm_op;
+
+/* Result of one match batch.  Engine-owned host memory, valid until the next
+ * tm_match_batch / tm_commit_epoch / tm_destroy on the same engine.
+ * Topic i's matches are keys[off[i] .. off[i]+cnt[i]), in unspecified order
+ * (the reference returns them in reverse ETS term order; callers must not rely
+ * on order).  In TM_MATCH_FIRST mode cnt[i] is 0 or 1. */
+typedef struct tm_result {
+    uint32_t        n;
+    uint32_t        _pad;
+    uint64_t        total;     /* sum of cnt[]                      */
+    const uint32_t *off;       /* n entries                         */
+    const uint32_t *cnt;       /* n entries                         */
+    const uint32_t *keys;      /* key handles                       */
+    const int32_t  *status;    /* n entries: TM_TOPIC_OK / TM_BADARG */
+} tm_result;
+
+/* Device-resident result (tm_match_device): device pointers, engine-owned. */
+typedef struct tm_dev_result {
+    uint32_t  n;
+    uint32_t  _pad;
+    uint32_t *d_off;      /* n entries: start of topic i's keys in d_keys   */
+    uint32_t *d_cnt;      /* n entries                                      */
+    uint32_t *d_keys;     /* capacity tm_dev_result.keys_cap                */
+    int32_t  *d_status;   /* n entries                                      */
+    uint64_t *d_total;    /* 1 entry: keys requested by the batch (device)  */
+    uint64_t  keys_cap;
+} tm_dev_result;
+
+typedef struct tm_stats_t {
+    uint64_t epoch;
+    uint64_t n_keys;        /* live keys (emqx_router:stats(n_routes))      */
+    uint64_t n_nodes;       /* trie nodes incl. root                        */
+    uint64_t n_words;       /* interned level words                         */
+    uint64_t edge_slots;    /* device edge-table capacity (slots)           */
+    uint64_t word_slots;    /* device word-table capacity (slots)           */
+    uint64_t list_words;    /* u32 words in the terminal-list arena (live+garbage) */
+    uint64_t device_bytes;  /* HBM held by the frozen index                 */
+    uint64_t n_full_rebuilds;
+    uint64_t n_delta_commits;
+    uint64_t n_slow_topics; /* topics routed to the spill kernel in the last batch */
+} tm_stats_t;
+
+/* lifecycle --------------------------------------------------------------- */
+uint32_t    tm_abi_version(void);
+int         tm_create(const tm_config *cfg, tm_engine **out);
+void        tm_destroy(tm_engine *eng);
+const char *tm_last_error(const tm_engine *eng);
+
+/* writes ------------------------------------------------------------------ */
+int tm_apply(tm_engine *eng, const tm_op *ops, size_t n);
+/* Bulk form of tm_apply for one op kind: filter i is bytes[off[i] .. off[i+1])
+ * (off has n+1 entries), id ids[i], flags flags[i] (flags may be NULL). */
+int tm_apply_packed(tm_engine *eng, uint32_t op, const uint8_t *bytes, const uint64_t *off,
+                    const uint64_t *ids, const uint32_t *flags, size_t n);
+int tm_commit_epoch(tm_engine *eng, uint64_t *epoch_out);
+
+/* reads ------------------------------------------------------------------- */
+/* Host buffers in, host result out (H2D + kernels + D2H inside).
+ * Topic i is bytes[off[i] .. off[i+1]); `off` has n+1 entries. */
+int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off,
+                   uint32_t n, uint32_t mode, tm_result *out);
+/* Device buffers in, device result out, asynchronous on the engine's stream
+ * (or on `stream` if non-NULL: a hipStream_t).  `d_off` has n+1 entries and
+ * total_bytes = d_off[n] - d_off[0] (it sizes the spill kernel's scratch).
+ * Call tm_device_sync() before reading; if *d_total > keys_cap the batch
+ * overflowed and must be re-run after tm_reserve_matches().
+ * Batch limits: total topic bytes < 4 GiB, total matches < 4 Gi keys. */
+int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off,
+                    uint32_t n, uint64_t total_bytes, void *stream, tm_dev_result *out);
+int tm_device_sync(tm_engine *eng);
+int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap);
+
+/* key introspection (get_id/1, get_topic/1) */
+int tm_key_info(const tm_engine *eng, uint32_t key, uint64_t *id, uint32_t *flags,
+                uint8_t *filter_buf, uint32_t buf_cap, uint32_t *filter_len);
+/* Bulk get_id/1: ids_out[i] = id of key handle keys[i] (TM_ENOTFOUND if any is not live). */
+int tm_key_ids(const tm_engine *eng, const uint32_t *keys, size_t n, uint64_t *ids_out);
+int tm_stats(const tm_engine *eng, tm_stats_t *out);
+
+/* diagnostics: enable/disable device walk counters; when out5 != NULL, first
+ * read the counters accumulated since the last call: {node visits, edge-slot
+ * probes, word-slot probes, keys emitted, topic levels}. */
+int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out5);
+/* diagnostics: time the dominant kernel of the next match with HIP events on its
+ * launch stream; enable=1 arms, then (after the match) enable=0 + ms_out reads. */
+int tm_debug_timing(tm_engine *eng, int enable, float *ms_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EMQX_TM_H */

@@ -1,0 +1,212 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU restatement of the
+reference (oracle/) and the reference's own known-answer cases.  Bit-exact sorted
+matched-id sets; integer work, no tolerance."""
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+import oracle
+from emqx_amd import _native as N
+from emqx_amd import workloads
+from oracle import emqx_topic as et
+from tests.kat import run_index_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", params=[False, True], ids=["fast", "spill"])
+def mode(request):
+    return request.param
+
+
+def _engine(force_slow=False, **kw):
+    return N.Engine(0, force_slow=force_slow, **kw)
+
+
+def _engine_sets(eng, t_bytes, t_off, mode=N.TM_MATCH_ALL):
+    off, cnt, keys, st = eng.match_packed(t_bytes, t_off, mode)
+    ids = eng.key_ids(keys)
+    return off, cnt, ids, st
+
+
+def _assert_same(eng_res, orc_res, what=""):
+    off, cnt, ids, st = eng_res
+    eo, eids, est = orc_res
+    assert np.array_equal(st, est), what
+    assert np.array_equal(cnt.astype(np.int64), np.diff(eo).astype(np.int64)), what
+    bad = []
+    for i in range(len(cnt)):
+        got = np.sort(ids[off[i]:off[i] + cnt[i]])
+        if not np.array_equal(got, eids[eo[i]:eo[i + 1]]):
+            bad.append(i)
+            if len(bad) > 5:
+                break
+    assert not bad, f"{what}: topics {bad} differ"
+
+
+def _load(eng, w):
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+
+
+# ------------------------------------------------------------------ reference KATs
+def test_index_kats_gpu(golden, mode):
+    from emqx_amd.topic_index import TopicIndex
+    errs = []
+    for case in golden("kat_index.json"):
+        run_index_case(case, lambda: TopicIndex(0, force_slow=mode), lambda c, m: c or errs.append(m))
+    assert not errs, "\n".join(errs)
+
+
+def test_router_kats_gpu(golden):
+    from emqx_amd.router import Router
+    for case in golden("kat_router.json"):
+        r = Router(0, node="node")
+        for step in case["steps"]:
+            kind = step[0]
+            dest = (lambda d: tuple(d) if isinstance(d, list) else d)
+            if kind == "add":
+                r.add_route(step[1], dest(step[2]))
+            elif kind == "del":
+                r.delete_route(step[1], dest(step[2]))
+            elif kind == "match":
+                got = sorted(((f.decode(), d) for f, d in r.match_routes(step[1])), key=repr)
+                exp = sorted(((f, dest(d)) for f, d in step[2]), key=repr)
+                assert got == exp, (case["name"], step)
+            elif kind == "topics":
+                assert sorted(t.decode() for t in r.topics()) == sorted(step[1])
+
+
+def test_config_a_golden_sample_gpu(golden, mode):
+    g = golden("config_a_sample.json")
+    eng = _engine(mode)
+    eng.apply([(N.TM_OP_ADD, f, i) for f, i in zip(g["filters"], g["ids"])])
+    eng.commit()
+    res = eng.match(g["topics"])
+    for i, exp in enumerate(g["expected"]):
+        assert sorted(eng.key_ids(np.array(res[i], dtype=np.uint32)).tolist()) == exp, g["topics"][i]
+
+
+# ------------------------------------------------------------- seeded configs
+@pytest.mark.parametrize("name,scale,nt", [("A", 1.0, 100_000), ("B", 0.2, 50_000), ("C", 0.02, 50_000),
+                                           ("E", 0.1, 50_000)])
+def test_config_parity(name, scale, nt, mode):
+    w = workloads.generate(name, scale=scale, n_topics=nt)
+    eng = _engine(mode)
+    _load(eng, w)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    _assert_same(_engine_sets(eng, w.t_bytes, w.t_off), ix.match(w.t_bytes, w.t_off, threads=8), name)
+    if not mode:
+        assert eng.stats()["n_slow_topics"] == 0 or name == "C"
+
+
+def test_modes_unique_first_vs_oracle():
+    w = workloads.generate("E", scale=0.02, n_topics=4000)
+    eng = _engine()
+    _load(eng, w)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    _assert_same(_engine_sets(eng, w.t_bytes, w.t_off, N.TM_MATCH_UNIQUE),
+                 ix.match(w.t_bytes, w.t_off, mode=oracle.MODE_UNIQUE), "unique")
+    _assert_same(_engine_sets(eng, w.t_bytes, w.t_off, N.TM_MATCH_FIRST),
+                 ix.match(w.t_bytes, w.t_off, mode=oracle.MODE_FIRST), "first")
+
+
+# ------------------------------------------------------------- edge cases
+EDGE_FILTERS = [b"#", b"+", b"+/+", b"/#", b"/+", b"//", b"", b"a", b"a/#", b"a/+", b"a//b", b"a/+/+", b"+/#",
+                b"$SYS/#", b"$SYS/+", b"$SYS/brokers/+/clients/#", b"+/brokers/#", b"a/#/b", b"a/b#", b"a/b+",
+                b"sport/", b"sport/+", b"$share", b"$queue/x", b"\xc3\xa9t\xc3\xa9/+", b"x" * 300 + b"/#",
+                b"/".join([b"+"] * 26) + b"/#", b"/".join([b"+"] * 40), b"/".join(b"L%d" % i for i in range(30))]
+EDGE_TOPICS = [b"", b"/", b"//", b"a", b"a/", b"a/b", b"a//b", b"a/b/c", b"$SYS", b"$SYS/brokers/n1/clients/c",
+               b"$", b"$x/y", b"sport/", b"sport", b"a/b#", b"a/b+", b"\xc3\xa9t\xc3\xa9/x", b"x" * 300 + b"/y",
+               b"/".join(b"L%d" % i for i in range(30)), b"/".join([b"q"] * 40), b"/".join([b"q"] * 26),
+               b"/" * 200, b"+", b"#", b"a/+/b", b"a/b/#", b"b" * 65535, b"/".join([b"z"] * 3000)]
+
+
+def test_edge_cases_vs_python_semantics(mode):
+    eng = _engine(mode)
+    eng.apply([(N.TM_OP_ADD, f, i) for i, f in enumerate(EDGE_FILTERS)])
+    eng.commit()
+    res = eng.match(EDGE_TOPICS)
+    for t, r in zip(EDGE_TOPICS, res):
+        levels = t.split(b"/")
+        if b"+" in levels or b"#" in levels:
+            assert r is None, t  # badarg
+            continue
+        exp = sorted(i for i, f in enumerate(EDGE_FILTERS) if et.match(t, f))
+        got = sorted(eng.key_ids(np.array(r, dtype=np.uint32)).tolist())
+        assert got == exp, (t[:60], got, exp)
+
+
+def test_empty_index_and_empty_batch():
+    eng = _engine()
+    assert eng.match([]) == []
+    assert eng.match([b"a/b", b"", b"$SYS/x"]) == [[], [], []]
+    eng.commit()  # empty epoch
+    assert eng.match([b"a"]) == [[]]
+
+
+def test_output_arena_overflow_rerun():
+    w = workloads.generate("C", scale=0.005, n_topics=3000)
+    eng = _engine(reserve_matches=16)
+    _load(eng, w)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    _assert_same(_engine_sets(eng, w.t_bytes, w.t_off), ix.match(w.t_bytes, w.t_off), "overflow")
+
+
+# ------------------------------------------------------------- delta epochs (config E)
+def test_churn_epochs_vs_oracle():
+    rng = np.random.default_rng(0xE11A0005)
+    w = workloads.generate("E", scale=0.02, n_topics=5000)
+    filters = w.filters()
+    ids = w.f_id.tolist()
+    eng = _engine()
+    live = set(range(len(ids)))
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    next_id = max(ids) + 1
+    extra = {}
+    for epoch in range(4):
+        dels = rng.choice(sorted(live), size=max(1, len(live) // 100), replace=False)
+        ops = [(N.TM_OP_DEL, filters[k] if k < len(filters) else extra[k][0], ids[k] if k < len(ids) else extra[k][1])
+               for k in dels]
+        for k in dels:
+            live.discard(int(k))
+        adds = []
+        for _ in range(max(1, len(live) // 100)):
+            src = int(rng.integers(len(filters)))
+            f = filters[src] if rng.random() < 0.5 else b"$share-like/" + filters[src]
+            extra[next_id] = (f, next_id)
+            adds.append((N.TM_OP_ADD, f, next_id))
+            live.add(next_id)
+            next_id += 1
+        # re-adding and re-deleting inside one epoch: last op wins
+        ops += adds + [(N.TM_OP_DEL, adds[0][1], adds[0][2]), (N.TM_OP_ADD, adds[0][1], adds[0][2])]
+        eng.apply(ops)
+        eng.commit()
+        lf = [filters[k] if k < len(filters) else extra[k][0] for k in sorted(live)]
+        li = [ids[k] if k < len(ids) else extra[k][1] for k in sorted(live)]
+        ix = oracle.OrderedIndex.from_filters(lf, li)
+        _assert_same(_engine_sets(eng, w.t_bytes, w.t_off), ix.match(w.t_bytes, w.t_off), f"epoch {epoch}")
+    s = eng.stats()
+    assert s["n_delta_commits"] >= 4 and s["n_keys"] == len(live)
+
+
+# ------------------------------------------------------------- property
+_lvl = st.sampled_from([b"a", b"b", b"c", b"", b"foo", b"$x", b"0F"])
+_topic = st.lists(_lvl, min_size=1, max_size=7).map(lambda l: b"/".join(l))
+_flvl = st.sampled_from([b"a", b"b", b"", b"+", b"+", b"#", b"$x", b"foo"])
+_filter = st.lists(_flvl, min_size=1, max_size=7).map(lambda l: b"/".join(l))
+
+
+@settings(max_examples=25, deadline=None, suppress_health_check=list(HealthCheck))
+@given(filters=st.lists(_filter, min_size=1, max_size=40), topics=st.lists(_topic, min_size=1, max_size=40),
+       slow=st.booleans())
+def test_property_engine_vs_match2(filters, topics, slow):
+    eng = _engine(slow)
+    eng.apply([(N.TM_OP_ADD, f, i) for i, f in enumerate(filters)])
+    eng.commit()
+    for t, r in zip(topics, eng.match(topics)):
+        exp = sorted({i for i, f in enumerate(filters) if et.match(t, f)})
+        assert sorted(eng.key_ids(np.array(r, dtype=np.uint32)).tolist()) == exp, (t, filters)
+    eng.close()

@@ -1,0 +1,179 @@
+"""CPU: pin the oracle (the CPU restatement of the reference) to the reference's own
+known-answer cases, and cross-check its two algorithms (brute-force emqx_topic:match/2
+vs the emqx_trie_search restatement) against each other.  No GPU involved."""
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+import oracle
+from oracle import emqx_topic as et
+from tests.kat import OracleIndex, run_index_case
+
+
+def _atom(x):
+    if isinstance(x, dict):
+        return x["atom"]
+    return x.encode() if isinstance(x, str) else x
+
+
+# ---------------------------------------------------------------------- emqx_topic
+def test_topic_match_kats(golden):
+    g = golden("kat_topic.json")
+    assert len(g["match"]) >= 50
+    for name, filt, exp in g["match"]:
+        assert et.match(name.encode(), filt.encode()) is exp, (name, filt)
+
+
+def test_topic_match_tokens_kats(golden):
+    # emqx_topic_SUITE:t_match_tokens — raw tokens (<<>>) against words ('')
+    for name, filt, exp in golden("kat_topic.json")["match_tokens"]:
+        assert et.match(et.tokens(name.encode()), et.words(filt.encode())) is exp, (name, filt)
+
+
+def test_topic_misc_kats(golden):
+    g = golden("kat_topic.json")
+    for t, exp in g["wildcard"]:
+        assert et.wildcard(t.encode()) is exp
+    for kind, t, exp in g["validate"]:
+        if exp is True:
+            assert et.validate(t.encode(), kind) is True, t
+        else:
+            with pytest.raises(et.TopicError) as ei:
+                et.validate(t.encode(), kind)
+            assert ei.value.reason == exp, (t, ei.value.reason)
+    for t, n in g["levels"]:
+        assert et.levels(t.encode()) == n
+    for t, toks in g["tokens"]:
+        assert et.tokens(t.encode()) == [x.encode() for x in toks]
+    for t, ws in g["words"]:
+        assert et.words(t.encode()) == [_atom(w) for w in ws]
+    for ws, exp in g["join"]:
+        if isinstance(ws, str) and ws.startswith("@words:"):
+            ws = et.words(ws[len("@words:"):].encode())
+        else:
+            ws = [_atom(w) for w in ws]
+        if isinstance(exp, dict):
+            with pytest.raises(et.TopicError):
+                et.join(ws)
+        else:
+            assert et.join(ws) == exp.encode()
+    for a, b, exp in g["intersection"]:
+        r = et.intersection(a.encode(), b.encode())
+        assert r == (exp.encode() if exp else False), (a, b, r)
+        assert et.intersection(b.encode(), a.encode()) == r  # commutative
+    for parent, w, exp in g["prepend"]:
+        p = _atom(parent) if isinstance(parent, dict) else (parent.encode() if parent is not None else None)
+        assert et.prepend(p, w.encode()) == exp.encode()
+    for t, exp in g["parse"]:
+        if isinstance(exp, dict) and "error" in exp:
+            with pytest.raises(et.TopicError):
+                et.parse(t.encode())
+        elif isinstance(exp, dict):
+            assert et.parse(t.encode())[0] == et.Share(*(x.encode() for x in exp["share"]))
+        else:
+            assert et.parse(t.encode())[0] == exp.encode()
+
+
+def test_product_parse_agrees_with_oracle(golden):
+    from emqx_amd import topic as pt
+    for t, exp in golden("kat_topic.json")["parse"]:
+        tb = t.encode()
+        try:
+            o = et.parse(tb)[0]
+        except et.TopicError:
+            with pytest.raises(ValueError):
+                pt.parse(tb)
+            continue
+        p = pt.parse(tb)[0]
+        if isinstance(o, et.Share):
+            assert (p.group, p.topic) == (o.group, o.topic)
+        else:
+            assert p == o
+
+
+# ---------------------------------------------------------------------- index KATs
+def test_index_kats_on_trie_search_restatement(golden):
+    cases = golden("kat_index.json")
+    assert len(cases) >= 20
+    errs = []
+    for case in cases:
+        run_index_case(case, OracleIndex, lambda c, m: c or errs.append(m))
+    assert not errs, "\n".join(errs)
+
+
+# ---------------------------------------------------------------------- config A
+def test_config_a_golden_sample(golden):
+    g = golden("config_a_sample.json")
+    ix = oracle.OrderedIndex.from_filters(g["filters"], g["ids"])
+    bs = [t.encode() for t in g["topics"]]
+    off = np.zeros(len(bs) + 1, dtype=np.uint32)
+    off[1:] = np.cumsum([len(b) for b in bs])
+    buf = np.frombuffer(b"".join(bs) + b"\0", dtype=np.uint8)
+    for algo in (oracle.ALGO_TRIE, oracle.ALGO_BRUTE):
+        o, ids, _ = ix.match(buf, off, algo=algo)
+        for i, exp in enumerate(g["expected"]):
+            assert ids[o[i]:o[i + 1]].tolist() == exp, (algo, g["topics"][i])
+
+
+def test_trie_restatement_equals_brute_force_config_a():
+    from emqx_amd import workloads
+    w = workloads.generate("A", n_topics=5000)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    o1, i1, s1 = ix.match(w.t_bytes, w.t_off, algo=oracle.ALGO_TRIE)
+    o2, i2, s2 = ix.match(w.t_bytes, w.t_off, algo=oracle.ALGO_BRUTE, threads=4)
+    assert np.array_equal(o1, o2) and np.array_equal(i1, i2)
+    assert o1[-1] > 0
+
+
+def test_trie_restatement_equals_brute_force_config_e_sys_share():
+    from emqx_amd import workloads
+    w = workloads.generate("E", scale=0.01, n_topics=3000)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    o1, i1, _ = ix.match(w.t_bytes, w.t_off, algo=oracle.ALGO_TRIE)
+    o2, i2, _ = ix.match(w.t_bytes, w.t_off, algo=oracle.ALGO_BRUTE, threads=4)
+    assert np.array_equal(o1, o2) and np.array_equal(i1, i2)
+    topics = w.topics()
+    assert any(t.startswith(b"$SYS/") and o1[i + 1] > o1[i] for i, t in enumerate(topics))
+
+
+# ------------------------------------------- property (bidirectional t_prop_matches)
+# Generator shape of emqx_topic_index_SUITE:topic_t/topic_filter_pattern_t (:381-419):
+# per-level entropy [1,2,3,4], fixed words foo/bar/baz/xyzzy, level:'+':'#' = 5:2:1.
+def _level(entropy):
+    width = int(1 + np.log2(entropy) / 4) if entropy > 1 else 1
+    return st.one_of(st.integers(1, max(1, entropy)).map(lambda i: f"{i:0{width}X}".encode()),
+                     st.sampled_from([b"foo", b"bar", b"baz", b"xyzzy", b"", b"$x"]))
+
+
+topic_st = st.lists(st.sampled_from([1, 2, 3, 4]), min_size=1, max_size=6).flatmap(
+    lambda ews: st.tuples(*[_level(4 * e) for e in ews]).map(list))
+pat_st = st.lists(st.sampled_from(["level"] * 5 + ["+"] * 2 + ["#"]), max_size=7)
+
+
+def _mk_filter(pat, topic):
+    out = []
+    for p, lvl in zip(pat, topic):
+        if p == "#":
+            out.append(b"#")
+            return b"/".join(out)
+        out.append(b"+" if p == "+" else lvl)
+    return b"/".join(out)
+
+
+@settings(max_examples=60, deadline=None)
+@given(topics=st.lists(topic_st, min_size=1, max_size=24), pats=st.lists(pat_st, min_size=1, max_size=24),
+       sys_first=st.booleans())
+def test_property_trie_restatement_vs_python_match(topics, pats, sys_first):
+    topics = [b"/".join(t) for t in topics]
+    if sys_first:
+        topics[0] = b"$SYS/" + topics[0]
+    filters = [_mk_filter(p, t.split(b"/")) for p, t in zip(pats, topics)] + [b"#", b"+/#", b"$SYS/#"]
+    ix = oracle.OrderedIndex.from_filters(filters)
+    off = np.zeros(len(topics) + 1, dtype=np.uint32)
+    off[1:] = np.cumsum([len(t) for t in topics])
+    buf = np.frombuffer(b"".join(topics) + b"\0", dtype=np.uint8)
+    o, ids, _ = ix.match(buf, off)
+    for i, t in enumerate(topics):
+        exp = [k for k, f in enumerate(filters) if et.match(t, f)]
+        assert ids[o[i]:o[i + 1]].tolist() == exp, (t, filters)
