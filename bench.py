@@ -42,7 +42,7 @@ def algorithmic_bytes(stats5, topic_bytes, n):
     topic bytes + u32 offsets in, one 32 B slot per word-table probe and per edge-table
     probe, 4 B key read from the terminal-list arena + 4 B key written per match, and
     12 B of per-topic results (offset, count, status)."""
-    visits, eprobes, wprobes, keys, levels = stats5
+    visits, eprobes, wprobes, keys, levels = stats5[:5]
     return topic_bytes + 4 * (n + 1) + 32 * wprobes + 32 * eprobes + 8 * keys + 12 * n
 
 
@@ -206,8 +206,7 @@ def main():
                 "kernel": "k_match_fast",
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_bytes_per_launch": int(alg_bytes),
-                "walk": dict(zip(["node_visits", "edge_probes", "word_probes", "keys", "levels"],
-                                 [int(x) for x in stats5])),
+                "walk": dict(zip(N.Engine.STAT_NAMES, [int(x) for x in stats5])),
             },
             "cpu_baseline": cpu,
             "parity": parity,

@@ -48,7 +48,7 @@ class tm_config(C.Structure):
         ("device", C.c_int32), ("flags", C.c_uint32),
         ("reserve_keys", C.c_uint32), ("reserve_nodes", C.c_uint32),
         ("reserve_topics", C.c_uint32), ("reserve_matches", C.c_uint32),
-        ("reserved", C.c_uint32 * 4),
+        ("seg_chunks", C.c_uint32), ("reserved", C.c_uint32 * 3),
     ]
 
 
@@ -144,7 +144,7 @@ class Engine:
     """One engine = one GPU.  Thin owner of a tm_engine*."""
 
     def __init__(self, device: int = 0, *, force_slow: bool = False, reserve_keys: int = 0,
-                 reserve_nodes: int = 0, reserve_matches: int = 0):
+                 reserve_nodes: int = 0, reserve_matches: int = 0, seg_chunks: int = 0):
         self.lib = load()
         cfg = tm_config()
         cfg.device = device
@@ -152,6 +152,7 @@ class Engine:
         cfg.reserve_keys = reserve_keys
         cfg.reserve_nodes = reserve_nodes
         cfg.reserve_matches = reserve_matches
+        cfg.seg_chunks = seg_chunks
         h = C.c_void_p()
         rc = self.lib.tm_create(C.byref(cfg), C.byref(h))
         if rc != TM_OK:
@@ -269,8 +270,11 @@ class Engine:
         self._check(self.lib.tm_stats(self.h, C.byref(s)))
         return {n: getattr(s, n) for n, _ in tm_stats_t._fields_}
 
+    STAT_NAMES = ("node_visits", "edge_probes", "word_probes", "keys", "levels", "spilled_topics",
+                  "segments", "chunk_flushes", "frontier_chunks")
+
     def debug_stats(self, enable: bool, read: bool = True):
-        out = (C.c_uint64 * 5)()
+        out = (C.c_uint64 * 9)()
         self._check(self.lib.tm_debug_stats(self.h, 1 if enable else 0, out if read else None))
         return list(out) if read else None
 

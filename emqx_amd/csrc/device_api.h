@@ -8,6 +8,9 @@
 
 namespace tmx {
 
+constexpr int SEG_CHUNK = 256;  // key segments per global chunk (16 B each)
+constexpr int FR_CHUNK = 256;   // frontier entries per global overflow chunk (8 B each)
+
 // Everything one match launch needs.  Device pointers only.
 struct MatchArgs {
     // topic batch: topic i is bytes[off[i] .. off[i+1])
@@ -35,8 +38,18 @@ struct MatchArgs {
     uint32_t *slow_count;
     uint32_t *scratch_w;  // (total bytes + 2n + 2) u32: word ids, at off[t]-off[0] + 2t
     uint64_t *scratch_s;  // (total bytes + 2n + 2) u64: DFS stack, same indexing
+    // segment chunk pool (wave LDS overflow): seg_chunks chunks of SEG_CHUNK uint4
+    uint4 *seg_pool;
+    uint64_t seg_chunks;
+    unsigned long long *seg_cursor;  // chunks requested (may exceed seg_chunks)
+    // frontier overflow pool: fr_chunks chunks of FR_CHUNK uint2 {node, meta}
+    uint2 *fr_pool;
+    uint64_t fr_chunks;
+    unsigned long long *fr_cursor;
     // optional walk statistics (nullptr = off): [0] node visits, [1] edge-slot
-    // probes, [2] word-slot probes, [3] keys emitted, [4] levels
+    // probes, [2] word-slot probes, [3] keys emitted, [4] topic levels,
+    // [5] topics spilled, [6] key segments, [7] segment-chunk flushes,
+    // [8] frontier overflow chunks
     unsigned long long *stats;
     // optional: events recorded around k_match_fast on the launch stream
     hipEvent_t ev_fast0, ev_fast1;

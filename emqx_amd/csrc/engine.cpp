@@ -160,12 +160,12 @@ struct tm_engine {
     DevBuf d_scatter_idx, d_scatter_src;
     // batch buffers
     DevBuf d_bytes, d_off, d_outoff, d_outcnt, d_status, d_keys, d_cursor, d_slow_list,
-        d_slow_count, d_scr_w, d_scr_s, d_stats;
-    uint64_t keys_cap = 0;
+        d_slow_count, d_scr_w, d_scr_s, d_stats, d_seg_pool, d_seg_cursor, d_fr_pool, d_fr_cursor;
+    uint64_t keys_cap = 0, seg_chunks = 0, fr_chunks = 0;
     PinBuf h_bytes, h_off, h_outoff, h_outcnt, h_status, h_keys, h_cursor;
     std::vector<uint32_t> pp_off, pp_cnt, pp_keys;  // post-processed results
     hipStream_t stream = nullptr;
-    uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0;
+    uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0, seg_demand_last = 0;
     bool stats_on = false;
     hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // around k_match_fast (tm_debug_timing)
     bool timing_on = false;
@@ -778,7 +778,8 @@ void tm_destroy(tm_engine *eng) {
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_etab, &eng->d_root, &eng->d_arena, &eng->d_scatter_idx,
                       &eng->d_scatter_src, &eng->d_bytes, &eng->d_off, &eng->d_outoff, &eng->d_outcnt,
                       &eng->d_status, &eng->d_keys, &eng->d_cursor, &eng->d_slow_list, &eng->d_slow_count,
-                      &eng->d_scr_w, &eng->d_scr_s, &eng->d_stats})
+                      &eng->d_scr_w, &eng->d_scr_s, &eng->d_stats, &eng->d_seg_pool, &eng->d_seg_cursor,
+                      &eng->d_fr_pool, &eng->d_fr_cursor})
         b->release();
     for (PinBuf *b : {&eng->h_bytes, &eng->h_off, &eng->h_outoff, &eng->h_outcnt, &eng->h_status, &eng->h_keys,
                       &eng->h_cursor})
@@ -843,9 +844,27 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
     TM_TRY_HIP(eng->d_slow_list.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_slow_count.ensure(64), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_cursor.ensure(64), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_stats.ensure(64), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_stats.ensure(128), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_scr_w.ensure((bytes + 2ull * n + 2) * 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_scr_s.ensure((bytes + 2ull * n + 2) * 8), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_seg_cursor.ensure(64), TM_ENOMEM, "alloc");
+    {
+        // chunk pool for waves whose staged key segments overflow LDS
+        uint64_t want = eng->cfg.seg_chunks ? eng->cfg.seg_chunks : std::max<uint64_t>(1024, ((uint64_t)n + 63) / 64 * 2);
+        if (want > eng->seg_chunks) {
+            TM_TRY_HIP(eng->d_seg_pool.ensure(want * SEG_CHUNK * sizeof(uint4)), TM_ENOMEM, "alloc seg pool");
+            eng->seg_chunks = want;
+        }
+    }
+    TM_TRY_HIP(eng->d_fr_cursor.ensure(64), TM_ENOMEM, "alloc");
+    {
+        // frontier overflow pool (waves whose per-depth frontier exceeds LDS)
+        uint64_t want = eng->cfg.seg_chunks ? eng->cfg.seg_chunks : std::max<uint64_t>(1024, ((uint64_t)n + 63) / 64 * 4);
+        if (want > eng->fr_chunks) {
+            TM_TRY_HIP(eng->d_fr_pool.ensure(want * FR_CHUNK * sizeof(uint2)), TM_ENOMEM, "alloc frontier pool");
+            eng->fr_chunks = want;
+        }
+    }
     if (eng->keys_cap == 0) {
         uint64_t want = eng->cfg.reserve_matches ? eng->cfg.reserve_matches : std::max<uint64_t>(n * 8ull, 1 << 16);
         TM_TRY_HIP(eng->d_keys.ensure(want * 4), TM_ENOMEM, "alloc");
@@ -878,6 +897,12 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.slow_count = eng->d_slow_count.as<uint32_t>();
     a.scratch_w = eng->d_scr_w.as<uint32_t>();
     a.scratch_s = eng->d_scr_s.as<uint64_t>();
+    a.seg_pool = eng->d_seg_pool.as<uint4>();
+    a.seg_chunks = eng->seg_chunks;
+    a.seg_cursor = eng->d_seg_cursor.as<unsigned long long>();
+    a.fr_pool = eng->d_fr_pool.as<uint2>();
+    a.fr_chunks = eng->fr_chunks;
+    a.fr_cursor = eng->d_fr_cursor.as<unsigned long long>();
     a.stats = eng->stats_on ? eng->d_stats.as<unsigned long long>() : nullptr;
     a.ev_fast0 = eng->timing_on ? eng->ev_fast0 : nullptr;
     a.ev_fast1 = eng->timing_on ? eng->ev_fast1 : nullptr;
@@ -919,9 +944,12 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
         TM_TRY_HIP(hipMemcpyAsync(eng->h_cursor.p, eng->d_cursor.p, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
         TM_TRY_HIP(hipMemcpyAsync((uint8_t *)eng->h_cursor.p + 8, eng->d_slow_count.p, 4, hipMemcpyDeviceToHost, s),
                    TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipMemcpyAsync((uint8_t *)eng->h_cursor.p + 16, eng->d_seg_cursor.p, 8, hipMemcpyDeviceToHost, s),
+                   TM_EDEVICE, "D2H");
         TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "match kernels");
         uint64_t total = *eng->h_cursor.as<uint64_t>();
         eng->n_slow_last = *(uint32_t *)((uint8_t *)eng->h_cursor.p + 8);
+        eng->seg_demand_last = *(uint64_t *)((uint8_t *)eng->h_cursor.p + 16);
         if (total <= eng->keys_cap) break;
         // output arena too small: grow to the demand and run again (once suffices:
         // the cursor counts every key the batch asked for)
@@ -944,6 +972,12 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
         TM_TRY_HIP(hipMemcpyAsync(eng->h_keys.p, eng->d_keys.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                    "D2H");
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "D2H");
+    if (eng->seg_demand_last > eng->seg_chunks && !eng->cfg.seg_chunks) {
+        // those waves' topics took the spill kernel (still exact); size up for next time
+        uint64_t want = eng->seg_demand_last + eng->seg_demand_last / 4 + 64;
+        TM_TRY_HIP(eng->d_seg_pool.ensure(want * SEG_CHUNK * sizeof(uint4)), TM_ENOMEM, "alloc seg pool");
+        eng->seg_chunks = want;
+    }
     out->total = total;
     out->off = eng->h_outoff.as<uint32_t>();
     out->cnt = eng->h_outcnt.as<uint32_t>();
@@ -1073,16 +1107,17 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
 
 // ---- diagnostics (not part of the reference surface): walk counters -------
 // Enable per-batch walk statistics (node visits, edge probes, word probes, keys,
-// levels), accumulated on the device across batches until read.
-int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out5) {
+// levels, spilled topics, segments, chunk flushes), accumulated on the device
+// across batches until read.
+int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out9) {
     if (!eng) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
-    TM_TRY_HIP(eng->d_stats.ensure(64), TM_ENOMEM, "alloc");
-    if (out5) {
-        TM_TRY_HIP(hipStreamSynchronize(eng->stream), TM_EDEVICE, "sync");
-        TM_TRY_HIP(hipMemcpy(out5, eng->d_stats.p, 40, hipMemcpyDeviceToHost), TM_EDEVICE, "D2H");
+    TM_TRY_HIP(eng->d_stats.ensure(128), TM_ENOMEM, "alloc");
+    if (out9) {
+        TM_TRY_HIP(hipDeviceSynchronize(), TM_EDEVICE, "sync");
+        TM_TRY_HIP(hipMemcpy(out9, eng->d_stats.p, 72, hipMemcpyDeviceToHost), TM_EDEVICE, "D2H");
     }
-    TM_TRY_HIP(hipMemset(eng->d_stats.p, 0, 64), TM_EDEVICE, "memset");
+    TM_TRY_HIP(hipMemset(eng->d_stats.p, 0, 128), TM_EDEVICE, "memset");
     eng->stats_on = enable != 0;
     return TM_OK;
 }

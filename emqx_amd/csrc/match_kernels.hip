@@ -19,10 +19,11 @@
 //                 compacted with wave prefix scans.  At the end the wave reserves its
 //                 output with ONE atomic and expands the segments with a
 //                 load-balanced copy (every lane busy, contiguous stores).
-//   k_match_slow  spill path for topics the fast kernel cannot hold in LDS (more
-//                 than LCAP levels, frontier or segment overflow): one lane per
-//                 topic, depth-first with the stack in global scratch (depth
-//                 bounded by the level count), count pass + fill pass.
+//                 Levels are tokenised lazily, one per depth, so there is no level
+//                 cap; segments overflow LDS into a global chunk pool.
+//   k_match_slow  spill path for topics whose wave frontier overflows LDS (FCAP
+//                 entries): one lane per topic, depth-first with the stack in global
+//                 scratch (depth bounded by the level count), count pass + fill pass.
 // No MFMA: this is a latency/gather-bound walk.
 #include <hip/hip_runtime.h>
 
@@ -31,9 +32,11 @@
 namespace tmx {
 
 constexpr int WAVE = 64;
-constexpr int LCAP = 16;   // levels per topic held in LDS by the fast kernel
-constexpr int FCAP = 256;  // frontier entries per wave per depth
-constexpr int SCAP = 384;  // key segments per wave
+constexpr int FCAP = 256;      // frontier entries per wave per depth held in LDS
+constexpr int FCH = FR_CHUNK;  // frontier entries per global overflow chunk
+constexpr int MAXF = 64;       // overflow chunks per wave per depth
+constexpr int SCAP = SEG_CHUNK;  // key segments staged in LDS = one global chunk
+constexpr int MAXCHUNK = 64;   // global segment chunks one wave may flush
 
 // ---------------------------------------------------------------------------
 // wave helpers
@@ -142,21 +145,60 @@ __device__ __forceinline__ uint32_t tokenize(const MatchArgs &a, uint32_t t, boo
 
 // ---------------------------------------------------------------------------
 // fast kernel: one wavefront (= one 64-thread workgroup) per 64 topics
+//
+// LDS per wave (~10 KiB): the two frontier buffers (FCAP entries each, extended by
+// global overflow chunks), a segment staging buffer that is flushed to a global
+// chunk pool when full, and per-topic cursors.  Levels are tokenised lazily (one
+// level per depth, lane = topic) so there is no level cap; a topic only spills to
+// k_match_slow when a pool is exhausted.
 struct WaveLds {
-    uint32_t wid[WAVE][LCAP];
     uint32_t fr_node[2][FCAP];
-    uint8_t fr_lane[2][FCAP];
-    uint8_t fr_flag[2][FCAP];
-    uint32_t seg_src[SCAP];
-    uint32_t seg_cnt[SCAP];
-    uint32_t seg_rel[SCAP];
+    uint8_t fr_meta[2][FCAP];     // topic lane | node flags << 6
+    uint32_t fch[2][MAXF];        // global overflow chunks of each frontier buffer
+    uint4 seg[SCAP];  // {src, cnt, rel, topic lane}
     uint32_t seg_scan[SCAP + 1];
-    uint8_t seg_lane[SCAP];
-    uint32_t cnt[WAVE];
+    uint32_t chunk[MAXCHUNK];
+    uint32_t cur[WAVE];    // byte offset where the topic's next level starts
+    uint32_t wid[WAVE];    // word id of the level being expanded
     uint32_t nlev[WAVE];
-    uint32_t tbase[WAVE];
-    uint32_t lflags[WAVE];  // bit0: spill to slow kernel
+    uint32_t cnt[WAVE];    // keys matched so far (allocates each segment's rel)
+    uint32_t tbase[WAVE];  // output base of the topic
+    uint32_t lflags[WAVE]; // bit0: spill to k_match_slow
+    uint32_t alive[2][WAVE];  // frontier entries per topic at this / the next depth
 };
+
+// Expand L.seg[0..ns) into the output (all lanes busy: element e of the flattened
+// segment list is found by binary search over the segment prefix sums).
+__device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, uint32_t ns) {
+    const uint32_t lane = lane_id();
+    uint32_t run = 0;
+    for (uint32_t sb = 0; sb < ns; sb += WAVE) {
+        const uint32_t j = sb + lane;
+        uint32_t c = 0;
+        if (j < ns) {
+            const uint4 g = L.seg[j];
+            if (!(L.lflags[g.w] & 1u)) c = g.y;
+        }
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan(c, &tot);
+        if (j < ns) L.seg_scan[j] = run + ex;
+        run += tot;
+    }
+    if (lane == 0) L.seg_scan[ns] = run;
+    __syncthreads();
+    for (uint32_t e = lane; e < run; e += WAVE) {
+        uint32_t lo = 0, hi = ns;  // seg_scan[lo] <= e < seg_scan[hi]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (L.seg_scan[mid] <= e) lo = mid;
+            else hi = mid;
+        }
+        const uint4 g = L.seg[lo];
+        const uint32_t k = e - L.seg_scan[lo];
+        a.keys[L.tbase[g.w] + g.z + k] = a.arena[g.x + k];
+    }
+    __syncthreads();
+}
 
 template <bool STATS>
 __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
@@ -164,135 +206,194 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     const uint32_t lane = lane_id();
     const uint32_t t = blockIdx.x * WAVE + lane;
     const bool active = t < a.n;
-    uint32_t st_visit = 0, st_probe = 0, st_wprobe = 0, st_keys = 0, st_lev = 0;
+    uint32_t st_visit = 0, st_probe = 0, st_wprobe = 0, st_seg = 0, st_flush = 0, st_frch = 0;
 
-    // ---- 1. tokenise (lane = topic)
+    // ---- 1. pre-scan (lane = topic): levels, badarg, '$'
     bool badarg = false, dollar = false;
-    uint32_t nl = 0;
+    uint32_t nl = 0, b = 0;
     if (active) {
-        nl = tokenize(a, t, &badarg, &dollar, &st_wprobe, [&](uint32_t i, uint32_t w) {
-            if (i < LCAP) L.wid[lane][i] = w;
-        });
+        b = a.off[t];
+        const uint32_t e = a.off[t + 1];
+        dollar = (e > b) && a.bytes[b] == '$';
+        uint32_t st = b;
+        for (uint32_t i = b;; ++i) {
+            const bool end = i == e;
+            const uint8_t c = end ? (uint8_t)'/' : a.bytes[i];
+            if (c == '/') {
+                if (i - st == 1 && (a.bytes[st] == '+' || a.bytes[st] == '#')) badarg = true;
+                nl++;
+                st = i + 1;
+                if (end) break;
+            }
+        }
     }
-    st_lev = nl;
-    bool spill = active && !badarg && (nl > LCAP || a.force_slow);
-    const bool walk = active && !badarg && !spill;
+    const bool spill0 = active && !badarg && a.force_slow;
+    const bool walk = active && !badarg && !spill0;
+    L.cur[lane] = b;
     L.nlev[lane] = nl;
     L.cnt[lane] = 0;
-    L.lflags[lane] = spill ? 1u : 0u;
+    L.lflags[lane] = spill0 ? 1u : 0u;
+    L.alive[0][lane] = 0;
+    L.alive[1][lane] = 0;
 
     // ---- 2. root: emit "#" keys (not for '$' topics), seed the frontier
-    RootRec R = *a.root;
-    uint32_t nseg = 0;  // wave-uniform
+    const RootRec R = *a.root;
+    uint32_t nseg = 0, nchunk = 0;  // wave-uniform
+    uint32_t nfr;
     {
         const bool em = walk && !dollar && R.hash_cnt;
         uint32_t tot;
-        uint32_t pos = nseg + wave_excl_scan(em ? 1u : 0u, &tot);
+        const uint32_t pos = wave_excl_scan(em ? 1u : 0u, &tot);
         if (em) {
-            if (pos < SCAP) {
-                L.seg_src[pos] = R.list_off + R.term_cnt;
-                L.seg_cnt[pos] = R.hash_cnt;
-                L.seg_rel[pos] = 0;
-                L.seg_lane[pos] = (uint8_t)lane;
-                L.cnt[lane] = R.hash_cnt;
-                st_keys += R.hash_cnt;
-            } else {
-                L.lflags[lane] |= 1u;
-            }
+            L.seg[pos] = make_uint4(R.list_off + R.term_cnt, R.hash_cnt, 0u, lane);
+            L.cnt[lane] = R.hash_cnt;
         }
-        nseg = min(nseg + tot, (uint32_t)SCAP);
+        nseg = tot;
+        st_seg += em;
         const uint32_t rf = dollar ? (R.flags & F_LIT) : (R.flags & F_KIDS);
         const bool push = walk && rf;
-        uint32_t p2 = wave_excl_scan(push ? 1u : 0u, &tot);
+        const uint32_t p2 = wave_excl_scan(push ? 1u : 0u, &tot);
         if (push) {
             L.fr_node[0][p2] = ROOT;
-            L.fr_lane[0][p2] = (uint8_t)lane;
-            L.fr_flag[0][p2] = (uint8_t)rf;
+            L.fr_meta[0][p2] = (uint8_t)(lane | (rf << 6));
+            L.alive[0][lane] = 1;
             st_visit++;
         }
-        __syncthreads();
-        // frontier size
-        uint32_t nfr = tot;
-
-        // ---- 3. level-synchronous walk
-        for (uint32_t d = 0; nfr > 0; ++d) {
-            const uint32_t cur = d & 1, nxt = cur ^ 1;
-            uint32_t nnext = 0;
-            for (uint32_t base = 0; base < nfr; base += WAVE) {
-                const uint32_t i = base + lane;
-                const bool has = i < nfr;
-                uint32_t node = 0, tl = 0, fl = 0;
-                if (has) {
-                    node = L.fr_node[cur][i];
-                    tl = L.fr_lane[cur][i];
-                    fl = L.fr_flag[cur][i];
-                }
-                const uint32_t tnl = has ? L.nlev[tl] : 0;
-                const uint32_t w = has ? L.wid[tl][d] : NONE;
-                Rec r1{}, r2{};
-                bool f1 = false, f2 = false;
-                // both probes issued before either result is needed
-                if (has && (fl & F_LIT) && w != NONE) f1 = edge_probe(a, node, w, &r1, &st_probe) != ~0ull;
-                if (has && (fl & F_PLUS)) f2 = edge_probe(a, node, W_PLUS, &r2, &st_probe) != ~0ull;
-                const bool last = (d + 1 == tnl);
-                // segments this lane emits (hash list of each found child; term list at the last level)
-                const bool s1h = f1 && r1.hash_cnt, s1t = f1 && last && r1.term_cnt;
-                const bool s2h = f2 && r2.hash_cnt, s2t = f2 && last && r2.term_cnt;
-                const uint32_t ns = (uint32_t)s1h + s1t + s2h + s2t;
-                uint32_t tot_s;
-                uint32_t ps = nseg + wave_excl_scan(ns, &tot_s);
-                if (ns) {
-                    if (ps + ns <= SCAP) {
-                        auto put = [&](uint32_t src, uint32_t c) {
-                            L.seg_src[ps] = src;
-                            L.seg_cnt[ps] = c;
-                            L.seg_rel[ps] = atomicAdd(&L.cnt[tl], c);
-                            L.seg_lane[ps] = (uint8_t)tl;
-                            ps++;
-                            st_keys += c;
-                        };
-                        if (s1t) put(r1.list_off, r1.term_cnt);
-                        if (s1h) put(r1.list_off + r1.term_cnt, r1.hash_cnt);
-                        if (s2t) put(r2.list_off, r2.term_cnt);
-                        if (s2h) put(r2.list_off + r2.term_cnt, r2.hash_cnt);
-                    } else {
-                        atomicOr(&L.lflags[tl], 1u);
-                    }
-                }
-                nseg = min(nseg + tot_s, (uint32_t)SCAP);
-                // next frontier
-                const bool p1 = f1 && !last && (r1.flags & F_KIDS);
-                const bool p2b = f2 && !last && (r2.flags & F_KIDS);
-                uint32_t tot_p;
-                uint32_t pp = nnext + wave_excl_scan((uint32_t)p1 + p2b, &tot_p);
-                if (p1 || p2b) {
-                    if (pp + (uint32_t)p1 + p2b <= FCAP) {
-                        if (p1) {
-                            L.fr_node[nxt][pp] = r1.child;
-                            L.fr_lane[nxt][pp] = (uint8_t)tl;
-                            L.fr_flag[nxt][pp] = (uint8_t)(r1.flags & F_KIDS);
-                            pp++;
-                        }
-                        if (p2b) {
-                            L.fr_node[nxt][pp] = r2.child;
-                            L.fr_lane[nxt][pp] = (uint8_t)tl;
-                            L.fr_flag[nxt][pp] = (uint8_t)(r2.flags & F_KIDS);
-                        }
-                    } else {
-                        atomicOr(&L.lflags[tl], 1u);
-                    }
-                }
-                nnext = min(nnext + tot_p, (uint32_t)FCAP);
-                st_visit += (uint32_t)f1 + f2;
-            }
-            __syncthreads();
-            nfr = nnext;
-        }
+        nfr = tot;
     }
     __syncthreads();
 
-    // ---- 4. reserve output with one atomic, write per-topic (off, cnt, status)
-    spill = active && (L.lflags[lane] & 1u) && !badarg;
+    // frontier = LDS entries [0, FCAP) + global overflow chunks beyond
+    uint32_t nfch[2] = {0, 0};  // overflow chunks held by each buffer (wave-uniform)
+    auto fr_read = [&](uint32_t lvl, uint32_t i, uint32_t &node, uint32_t &meta) {
+        if (i < (uint32_t)FCAP) {
+            node = L.fr_node[lvl][i];
+            meta = L.fr_meta[lvl][i];
+        } else {
+            const uint32_t k = i - FCAP;
+            const uint2 v = a.fr_pool[(uint64_t)L.fch[lvl][k / FCH] * FCH + k % FCH];
+            node = v.x;
+            meta = v.y;
+        }
+    };
+    auto fr_write = [&](uint32_t lvl, uint32_t i, uint32_t node, uint32_t meta) {
+        if (i < (uint32_t)FCAP) {
+            L.fr_node[lvl][i] = node;
+            L.fr_meta[lvl][i] = (uint8_t)meta;
+        } else {
+            const uint32_t k = i - FCAP;
+            a.fr_pool[(uint64_t)L.fch[lvl][k / FCH] * FCH + k % FCH] = make_uint2(node, meta);
+        }
+    };
+
+    // ---- 3. level-synchronous walk
+    for (uint32_t d = 0; nfr > 0; ++d) {
+        const uint32_t cur = d & 1, nxt = cur ^ 1;
+        nfch[nxt] = 0;
+        // 3a. tokenise level d of every topic that still has frontier entries
+        if (walk && L.alive[cur][lane]) {
+            uint32_t i = L.cur[lane];
+            const uint32_t st = i, e = a.off[t + 1];
+            uint64_t h = FNV_OFF;
+            while (i < e && a.bytes[i] != '/') h = fnv_step(h, a.bytes[i++]);
+            L.wid[lane] = word_lookup(a, a.bytes + st, i - st, h, &st_wprobe);
+            L.cur[lane] = i + 1;
+        }
+        L.alive[nxt][lane] = 0;
+        __syncthreads();
+        // 3b. expand the frontier, 64 entries per round
+        uint32_t nnext = 0;
+        for (uint32_t base = 0; base < nfr; base += WAVE) {
+            const uint32_t i = base + lane;
+            const bool has = i < nfr;
+            uint32_t node = 0, tl = 0, fl = 0;
+            if (has) {
+                uint32_t meta;
+                fr_read(cur, i, node, meta);
+                tl = meta & 63u;
+                fl = meta >> 6;
+            }
+            const uint32_t w = has ? L.wid[tl] : NONE;
+            const bool last = has && (d + 1 == L.nlev[tl]);
+            Rec r1{}, r2{};
+            bool f1 = false, f2 = false;
+            if (has && (fl & F_LIT) && w != NONE) f1 = edge_probe(a, node, w, &r1, &st_probe) != ~0ull;
+            if (has && (fl & F_PLUS)) f2 = edge_probe(a, node, W_PLUS, &r2, &st_probe) != ~0ull;
+            // segments: each found child's '#' list; its exact list at the topic's last level
+            const bool s1h = f1 && r1.hash_cnt, s1t = f1 && last && r1.term_cnt;
+            const bool s2h = f2 && r2.hash_cnt, s2t = f2 && last && r2.term_cnt;
+            const uint32_t ns = (uint32_t)s1h + s1t + s2h + s2t;
+            uint32_t tot_s;
+            uint32_t ps = wave_excl_scan(ns, &tot_s);
+            if (tot_s && nseg + tot_s > (uint32_t)SCAP) {
+                // flush the staged segments to one global chunk
+                __syncthreads();
+                uint32_t c = 0;
+                if (lane == 0) c = (uint32_t)atomicAdd(a.seg_cursor, 1ull);
+                c = __shfl(c, 0, WAVE);
+                if (c < a.seg_chunks && nchunk < (uint32_t)MAXCHUNK) {
+                    uint4 *dst = a.seg_pool + (uint64_t)c * SCAP;
+                    for (uint32_t j = lane; j < (uint32_t)SCAP; j += WAVE)
+                        dst[j] = j < nseg ? L.seg[j] : make_uint4(0u, 0u, 0u, 0u);
+                    if (lane == 0) L.chunk[nchunk] = c;
+                    nchunk++;
+                    st_flush++;
+                } else {
+                    // pool exhausted: those topics take the spill kernel instead
+                    for (uint32_t j = lane; j < nseg; j += WAVE) atomicOr(&L.lflags[L.seg[j].w], 1u);
+                }
+                nseg = 0;
+                __syncthreads();
+            }
+            ps += nseg;
+            if (ns) {
+                auto put = [&](uint32_t src, uint32_t c) {
+                    L.seg[ps++] = make_uint4(src, c, atomicAdd(&L.cnt[tl], c), tl);
+                };
+                if (s1t) put(r1.list_off, r1.term_cnt);
+                if (s1h) put(r1.list_off + r1.term_cnt, r1.hash_cnt);
+                if (s2t) put(r2.list_off, r2.term_cnt);
+                if (s2h) put(r2.list_off + r2.term_cnt, r2.hash_cnt);
+            }
+            nseg += tot_s;
+            st_seg += ns;
+            // next frontier: children that can still expand
+            const bool p1 = f1 && !last && (r1.flags & F_KIDS);
+            const bool p2b = f2 && !last && (r2.flags & F_KIDS);
+            uint32_t tot_p;
+            uint32_t pp = nnext + wave_excl_scan((uint32_t)p1 + p2b, &tot_p);
+            // capacity of the next buffer: LDS + overflow chunks (grown on demand)
+            uint32_t cap = FCAP + nfch[nxt] * FCH;
+            if (nnext + tot_p > cap && nfch[nxt] < (uint32_t)MAXF) {
+                const uint32_t want = min((nnext + tot_p - FCAP + FCH - 1) / FCH, (uint32_t)MAXF) - nfch[nxt];
+                unsigned long long c0 = 0;
+                if (lane == 0) c0 = atomicAdd(a.fr_cursor, (unsigned long long)want);
+                c0 = __shfl(c0, 0, WAVE);
+                const uint32_t got = c0 >= a.fr_chunks ? 0u : (uint32_t)min((unsigned long long)want, a.fr_chunks - c0);
+                if (lane < got) L.fch[nxt][nfch[nxt] + lane] = (uint32_t)(c0 + lane);
+                nfch[nxt] += got;
+                cap = FCAP + nfch[nxt] * FCH;
+                __syncthreads();
+                st_frch += got;
+            }
+            if (p1 || p2b) {
+                if (pp + (uint32_t)p1 + p2b <= cap) {
+                    if (p1) fr_write(nxt, pp++, r1.child, tl | ((r1.flags & F_KIDS) << 6));
+                    if (p2b) fr_write(nxt, pp, r2.child, tl | ((r2.flags & F_KIDS) << 6));
+                    atomicAdd(&L.alive[nxt][tl], (uint32_t)p1 + p2b);
+                } else {
+                    atomicOr(&L.lflags[tl], 1u);  // frontier overflow: topic spills
+                }
+            }
+            nnext = min(nnext + tot_p, cap);
+            st_visit += (uint32_t)f1 + f2;
+        }
+        __syncthreads();
+        nfr = nnext;
+    }
+
+    // ---- 4. reserve this wave's output with one atomic; per-topic results
+    const bool spill = active && !badarg && (L.lflags[lane] & 1u);
     const uint32_t my = (walk && !spill) ? L.cnt[lane] : 0u;
     uint32_t total;
     const uint32_t excl = wave_excl_scan(my, &total);
@@ -316,43 +417,30 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     }
     __syncthreads();
 
-    // ---- 5. load-balanced expansion of the key segments
+    // ---- 5. load-balanced expansion: staged segments, then flushed chunks
     if (!overflow && total) {
-        uint32_t run = 0;
-        for (uint32_t sb = 0; sb < nseg; sb += WAVE) {
-            const uint32_t j = sb + lane;
-            uint32_t c = 0;
-            if (j < nseg && !(L.lflags[L.seg_lane[j]] & 1u)) c = L.seg_cnt[j];
-            uint32_t tot;
-            const uint32_t ex = wave_excl_scan(c, &tot);
-            if (j < nseg) L.seg_scan[j] = run + ex;
-            run += tot;
-        }
-        if (lane == 0) L.seg_scan[nseg] = run;
-        __syncthreads();
-        for (uint32_t e = lane; e < run; e += WAVE) {
-            // last segment j with seg_scan[j] <= e
-            uint32_t lo = 0, hi = nseg;  // invariant: seg_scan[lo] <= e < seg_scan[hi]
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (L.seg_scan[mid] <= e) lo = mid;
-                else hi = mid;
-            }
-            const uint32_t k = e - L.seg_scan[lo];
-            a.keys[L.tbase[L.seg_lane[lo]] + L.seg_rel[lo] + k] = a.arena[L.seg_src[lo] + k];
+        expand_segments(a, L, nseg);
+        for (uint32_t c = 0; c < nchunk; ++c) {
+            const uint4 *src = a.seg_pool + (uint64_t)L.chunk[c] * SCAP;
+            for (uint32_t j = lane; j < (uint32_t)SCAP; j += WAVE) L.seg[j] = src[j];
+            __syncthreads();
+            expand_segments(a, L, SCAP);
         }
     }
 
     if constexpr (STATS) {
-        uint64_t v0 = wave_sum64(st_visit), v1 = wave_sum64(st_probe), v2 = wave_sum64(st_wprobe),
-                 v3 = wave_sum64(walk && !spill ? st_keys : 0), v4 = wave_sum64(st_lev);
-        (void)v3;
+        const uint64_t v0 = wave_sum64(st_visit), v1 = wave_sum64(st_probe), v2 = wave_sum64(st_wprobe),
+                       v4 = wave_sum64(nl), v5 = wave_sum64(spill ? 1u : 0u), v6 = wave_sum64(st_seg);
         if (lane == 0) {
             atomicAdd(&a.stats[0], (unsigned long long)v0);
             atomicAdd(&a.stats[1], (unsigned long long)v1);
             atomicAdd(&a.stats[2], (unsigned long long)v2);
             atomicAdd(&a.stats[3], (unsigned long long)total);
             atomicAdd(&a.stats[4], (unsigned long long)v4);
+            atomicAdd(&a.stats[5], (unsigned long long)v5);
+            atomicAdd(&a.stats[6], (unsigned long long)v6);
+            atomicAdd(&a.stats[7], (unsigned long long)st_flush);
+            atomicAdd(&a.stats[8], (unsigned long long)st_frch);
         }
     }
 }
@@ -437,11 +525,12 @@ __global__ __launch_bounds__(WAVE) void k_match_slow(MatchArgs a) {
         if (pos + c <= a.keys_cap) dfs_walk<true>(a, R, wid, stk, nl, dollar, a.keys + pos, &st_probe, &st_visit);
     }
     if constexpr (STATS) {
+        // levels were already counted by the fast kernel's pre-scan
         atomicAdd(&a.stats[0], (unsigned long long)st_visit);
         atomicAdd(&a.stats[1], (unsigned long long)st_probe);
         atomicAdd(&a.stats[2], (unsigned long long)st_wprobe);
         atomicAdd(&a.stats[3], (unsigned long long)st_keys);
-        atomicAdd(&a.stats[4], (unsigned long long)st_lev);
+        (void)st_lev;
     }
 }
 
@@ -469,6 +558,8 @@ hipError_t launch_match(const MatchArgs &a, hipStream_t s) {
     hipError_t e;
     if ((e = hipMemsetAsync(a.cursor, 0, sizeof(unsigned long long), s))) return e;
     if ((e = hipMemsetAsync(a.slow_count, 0, sizeof(uint32_t), s))) return e;
+    if ((e = hipMemsetAsync(a.seg_cursor, 0, sizeof(unsigned long long), s))) return e;
+    if ((e = hipMemsetAsync(a.fr_cursor, 0, sizeof(unsigned long long), s))) return e;
     if (a.n == 0) return hipSuccess;
     const unsigned grid = (a.n + WAVE - 1) / WAVE;
     if (a.ev_fast0 && (e = hipEventRecord(a.ev_fast0, s))) return e;

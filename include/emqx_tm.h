@@ -90,7 +90,10 @@ typedef struct tm_config {
     uint32_t reserve_nodes;
     uint32_t reserve_topics;      /* largest batch expected                    */
     uint32_t reserve_matches;     /* expected matches per batch (output arena) */
-    uint32_t reserved[4];
+    uint32_t seg_chunks;          /* 0 = auto; else fixed size of the key-segment and
+                                     frontier-overflow chunk pools (test aid: exhaustion
+                                     routes topics to the spill kernel, results stay exact) */
+    uint32_t reserved[3];
 } tm_config;
 
 typedef struct tm_op {
@@ -180,10 +183,11 @@ int tm_key_info(const tm_engine *eng, uint32_t key, uint64_t *id, uint32_t *flag
 int tm_key_ids(const tm_engine *eng, const uint32_t *keys, size_t n, uint64_t *ids_out);
 int tm_stats(const tm_engine *eng, tm_stats_t *out);
 
-/* diagnostics: enable/disable device walk counters; when out5 != NULL, first
+/* diagnostics: enable/disable device walk counters; when out9 != NULL, first
  * read the counters accumulated since the last call: {node visits, edge-slot
- * probes, word-slot probes, keys emitted, topic levels}. */
-int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out5);
+ * probes, word-slot probes, keys emitted, topic levels, topics spilled to the
+ * slow kernel, key segments, segment-chunk flushes, frontier overflow chunks}. */
+int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out9);
 /* diagnostics: time the dominant kernel of the next match with HIP events on its
  * launch stream; enable=1 arms, then (after the match) enable=0 + ms_out reads. */
 int tm_debug_timing(tm_engine *eng, int enable, float *ms_out);

@@ -113,22 +113,22 @@ def run_index_case(case, make_index, check):
         kind, topic = q[0], q[1].encode()
         if kind == "badarg":
             try:
-                ix.matches(topic, [])
+                ix.matches(topic, opts=[])
             except Exception as e:  # BadArg / BadArgError
                 check("badarg" in type(e).__name__.lower() or "badarg" in str(e).lower(), f"{case['name']}: {e!r}")
                 continue
             check(False, f"{case['name']}: {topic!r} should be badarg")
         elif kind == "matches_topics":
-            got = sorted(key_topic(k).decode() for k in ix.matches(topic, []))
+            got = sorted(key_topic(k).decode() for k in ix.matches(topic, opts=[]))
             check(got == sorted(q[2]), f"{case['name']} {topic!r}: {got} != {q[2]}")
         elif kind == "matches_ids":
             opts, exp = q[2], q[3]
-            got = [k[1][0] for k in ix.matches(topic, opts)]
+            got = [k[1][0] for k in ix.matches(topic, opts=opts)]
             if "unique" not in opts:
                 got, exp = sorted(got, key=repr), sorted(exp, key=repr)
             check(got == exp, f"{case['name']} {topic!r} {opts}: {got} != {exp}")
         elif kind == "count":
-            got = len(ix.matches(topic, []))
+            got = len(ix.matches(topic, opts=[]))
             check(got == q[2], f"{case['name']} {topic!r}: count {got} != {q[2]}")
         elif kind in ("match_id", "match_topic"):
             k = ix.match(topic)

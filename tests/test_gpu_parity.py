@@ -154,6 +154,25 @@ def test_output_arena_overflow_rerun():
     _assert_same(_engine_sets(eng, w.t_bytes, w.t_off), ix.match(w.t_bytes, w.t_off), "overflow")
 
 
+def test_segment_chunks_and_pool_exhaustion():
+    # config C topics emit many key segments: waves flush LDS into the chunk pool; with a
+    # one-chunk pool the overflowing topics must take the spill kernel, still exact
+    w = workloads.generate("C", scale=0.01, n_topics=20000)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    exp = ix.match(w.t_bytes, w.t_off, threads=8)
+    for chunks in (0, 1):
+        eng = _engine(seg_chunks=chunks)
+        _load(eng, w)
+        eng.debug_stats(True, read=False)
+        res = _engine_sets(eng, w.t_bytes, w.t_off)
+        st = dict(zip(N.Engine.STAT_NAMES, eng.debug_stats(False)))
+        _assert_same(res, exp, f"seg_chunks={chunks}")
+        assert st["chunk_flushes"] > 0 and st["frontier_chunks"] > 0, st
+        if chunks == 1:
+            assert st["spilled_topics"] > 0
+        eng.close()
+
+
 # ------------------------------------------------------------- delta epochs (config E)
 def test_churn_epochs_vs_oracle():
     rng = np.random.default_rng(0xE11A0005)
