@@ -263,7 +263,8 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     }
     __syncthreads();
 
-    // frontier = LDS entries [0, FCAP) + global overflow chunks beyond
+    // frontier = LDS entries [0, FCAP) + global overflow chunks beyond; a buffer keeps
+    // its chunks from level to level (it is rewritten every other depth)
     uint32_t nfch[2] = {0, 0};  // overflow chunks held by each buffer (wave-uniform)
     auto fr_read = [&](uint32_t lvl, uint32_t i, uint32_t &node, uint32_t &meta) {
         if (i < (uint32_t)FCAP) {
@@ -289,7 +290,6 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     // ---- 3. level-synchronous walk
     for (uint32_t d = 0; nfr > 0; ++d) {
         const uint32_t cur = d & 1, nxt = cur ^ 1;
-        nfch[nxt] = 0;
         // 3a. tokenise level d of every topic that still has frontier entries
         if (walk && L.alive[cur][lane]) {
             uint32_t i = L.cur[lane];

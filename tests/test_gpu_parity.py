@@ -154,22 +154,44 @@ def test_output_arena_overflow_rerun():
     _assert_same(_engine_sets(eng, w.t_bytes, w.t_off), ix.match(w.t_bytes, w.t_off), "overflow")
 
 
-def test_segment_chunks_and_pool_exhaustion():
-    # config C topics emit many key segments: waves flush LDS into the chunk pool; with a
-    # one-chunk pool the overflowing topics must take the spill kernel, still exact
-    w = workloads.generate("C", scale=0.01, n_topics=20000)
-    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
-    exp = ix.match(w.t_bytes, w.t_off, threads=8)
+def _pool_workload(n_topics=2048, levels=10):
+    """Half the topics match one '#' key at each of their prefixes and at every copy of
+    a prefix with one level replaced by '+': dozens of key segments and a frontier
+    about as wide as the depth per topic, so waves overflow their LDS segment and
+    frontier buffers into the global chunk pools."""
+    rng = np.random.default_rng(7)
+    topics = [b"/".join(b"w%d" % rng.integers(0, 50) for _ in range(levels)) for _ in range(n_topics)]
+    filters = set()
+    for t in topics[: n_topics // 2]:
+        ws = t.split(b"/")
+        for d in range(1, levels):
+            filters.add(b"/".join(ws[:d]) + b"/#")
+            for j in range(d):  # '+' at every single position: frontier ~ depth wide
+                pw = list(ws[:d])
+                pw[j] = b"+"
+                filters.add(b"/".join(pw) + b"/#")
+    filters = sorted(filters)
+    return filters, topics
+
+
+def test_segment_and_frontier_chunks_and_pool_exhaustion():
+    filters, topics = _pool_workload()
+    ix = oracle.OrderedIndex.from_filters(filters)
+    buf, off = N.pack_topics(topics)
+    exp = ix.match(buf, off, threads=8)
     for chunks in (0, 1):
         eng = _engine(seg_chunks=chunks)
-        _load(eng, w)
+        eng.apply([(N.TM_OP_ADD, f, i) for i, f in enumerate(filters)])
+        eng.commit()
         eng.debug_stats(True, read=False)
-        res = _engine_sets(eng, w.t_bytes, w.t_off)
+        res = _engine_sets(eng, buf, off)
         st = dict(zip(N.Engine.STAT_NAMES, eng.debug_stats(False)))
         _assert_same(res, exp, f"seg_chunks={chunks}")
         assert st["chunk_flushes"] > 0 and st["frontier_chunks"] > 0, st
         if chunks == 1:
-            assert st["spilled_topics"] > 0
+            assert st["spilled_topics"] > 0, st
+        else:
+            assert st["spilled_topics"] == 0, st
         eng.close()
 
 
