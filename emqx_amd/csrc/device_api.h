@@ -8,7 +8,7 @@
 
 namespace tmx {
 
-constexpr int SEG_CHUNK = 256;  // key segments per global chunk (16 B each)
+constexpr int SEG_CHUNK = 128;  // key segments per global chunk (16 B each)
 constexpr int FR_CHUNK = 256;   // frontier entries per global overflow chunk (8 B each)
 
 // Everything one match launch needs.  Device pointers only.

@@ -751,7 +751,7 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     }
     uint64_t rk = eng->cfg.reserve_keys ? eng->cfg.reserve_keys : 1024;
     uint64_t rn = eng->cfg.reserve_nodes ? eng->cfg.reserve_nodes : rk * 4;
-    eng->word_rehash(next_pow2(std::max<uint64_t>(rn / 2, 1024)));
+    eng->word_rehash(1024);  // grows with the vocabulary (load <= 1/2), not with nodes
     eng->node_parent.reserve(rn);
     eng->node_word.reserve(rn);
     eng->node_slot.reserve(rn);

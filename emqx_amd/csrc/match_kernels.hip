@@ -35,8 +35,9 @@ constexpr int WAVE = 64;
 constexpr int FCAP = 256;      // frontier entries per wave per depth held in LDS
 constexpr int FCH = FR_CHUNK;  // frontier entries per global overflow chunk
 constexpr int MAXF = 64;       // overflow chunks per wave per depth
-constexpr int SCAP = SEG_CHUNK;  // key segments staged in LDS = one global chunk
+constexpr int SCAP = SEG_CHUNK;  // key segments staged in LDS = one global chunk (128)
 constexpr int MAXCHUNK = 64;   // global segment chunks one wave may flush
+constexpr int TBCAP = 3072;    // topic bytes of one wave staged in LDS (else read from HBM)
 
 // ---------------------------------------------------------------------------
 // wave helpers
@@ -112,6 +113,53 @@ __device__ __forceinline__ uint64_t edge_probe(const MatchArgs &a, uint32_t pare
     }
 }
 
+// Probe (parent, word) and (parent, '+') together: both first loads are in flight
+// before either result is consumed (the two are independent chains).
+__device__ __forceinline__ void edge_probe2(const MatchArgs &a, uint32_t parent, bool want1, uint32_t word,
+                                            bool want2, Rec *r1, bool *f1, Rec *r2, bool *f2, uint32_t *probes) {
+    uint64_t s1 = edge_hash(parent, word) & a.emask;
+    uint64_t s2 = edge_hash(parent, W_PLUS) & a.emask;
+    bool p1 = want1, p2 = want2;
+    *f1 = false;
+    *f2 = false;
+    while (p1 || p2) {
+        uint4 x1 = make_uint4(NONE, 0, 0, 0), y1 = x1, x2 = x1, y2 = x1;
+        if (p1) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(a.etab + s1);
+            x1 = q[0];
+            y1 = q[1];
+        }
+        if (p2) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(a.etab + s2);
+            x2 = q[0];
+            y2 = q[1];
+        }
+        *probes += (uint32_t)p1 + (uint32_t)p2;
+        if (p1) {
+            if (x1.x == NONE) {
+                p1 = false;
+            } else if (x1.x == parent && x1.y == word) {
+                *r1 = Rec{x1.z, x1.w, y1.x, y1.y, y1.z};
+                *f1 = true;
+                p1 = false;
+            } else {
+                s1 = (s1 + 1) & a.emask;
+            }
+        }
+        if (p2) {
+            if (x2.x == NONE) {
+                p2 = false;
+            } else if (x2.x == parent && x2.y == W_PLUS) {
+                *r2 = Rec{x2.z, x2.w, y2.x, y2.y, y2.z};
+                *f2 = true;
+                p2 = false;
+            } else {
+                s2 = (s2 + 1) & a.emask;
+            }
+        }
+    }
+}
+
 // Tokenise topic t: calls f(level_index, word_id) per level; returns levels,
 // sets *badarg when a level is exactly "+" or "#", *dollar when the first level
 // starts with '$'.
@@ -152,6 +200,7 @@ __device__ __forceinline__ uint32_t tokenize(const MatchArgs &a, uint32_t t, boo
 // level per depth, lane = topic) so there is no level cap; a topic only spills to
 // k_match_slow when a pool is exhausted.
 struct WaveLds {
+    uint8_t tb[TBCAP];            // the wave's topic bytes (16-B aligned window)
     uint32_t fr_node[2][FCAP];
     uint8_t fr_meta[2][FCAP];     // topic lane | node flags << 6
     uint32_t fch[2][MAXF];        // global overflow chunks of each frontier buffer
@@ -208,19 +257,36 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     const bool active = t < a.n;
     uint32_t st_visit = 0, st_probe = 0, st_wprobe = 0, st_seg = 0, st_flush = 0, st_frch = 0;
 
+    // ---- 0. stage the wave's topic bytes in LDS with 16-B coalesced loads
+    const uint32_t t0 = blockIdx.x * WAVE;
+    const uint32_t wb0 = a.off[t0], wb1 = a.off[min(t0 + WAVE, a.n)];
+    const uint32_t tbase = wb0 & ~15u;
+    const bool staged = ((reinterpret_cast<uintptr_t>(a.bytes) & 15u) == 0) && (wb1 - tbase <= (uint32_t)TBCAP);
+    if (staged) {
+        for (uint32_t j = lane * 16; tbase + j < wb1; j += WAVE * 16) {
+            if (tbase + j + 16 <= wb1) {
+                *reinterpret_cast<uint4 *>(&L.tb[j]) = *reinterpret_cast<const uint4 *>(a.bytes + tbase + j);
+            } else {
+                for (uint32_t k = 0; tbase + j + k < wb1; k++) L.tb[j + k] = a.bytes[tbase + j + k];
+            }
+        }
+        __syncthreads();
+    }
+    auto byte_at = [&](uint32_t i) -> uint8_t { return staged ? L.tb[i - tbase] : a.bytes[i]; };
+
     // ---- 1. pre-scan (lane = topic): levels, badarg, '$'
     bool badarg = false, dollar = false;
-    uint32_t nl = 0, b = 0;
+    uint32_t nl = 0, b = 0, e = 0;
     if (active) {
         b = a.off[t];
-        const uint32_t e = a.off[t + 1];
-        dollar = (e > b) && a.bytes[b] == '$';
+        e = a.off[t + 1];
+        dollar = (e > b) && byte_at(b) == '$';
         uint32_t st = b;
         for (uint32_t i = b;; ++i) {
             const bool end = i == e;
-            const uint8_t c = end ? (uint8_t)'/' : a.bytes[i];
+            const uint8_t c = end ? (uint8_t)'/' : byte_at(i);
             if (c == '/') {
-                if (i - st == 1 && (a.bytes[st] == '+' || a.bytes[st] == '#')) badarg = true;
+                if (i - st == 1 && (byte_at(st) == '+' || byte_at(st) == '#')) badarg = true;
                 nl++;
                 st = i + 1;
                 if (end) break;
@@ -293,10 +359,15 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
         // 3a. tokenise level d of every topic that still has frontier entries
         if (walk && L.alive[cur][lane]) {
             uint32_t i = L.cur[lane];
-            const uint32_t st = i, e = a.off[t + 1];
+            const uint32_t st = i;
             uint64_t h = FNV_OFF;
-            while (i < e && a.bytes[i] != '/') h = fnv_step(h, a.bytes[i++]);
-            L.wid[lane] = word_lookup(a, a.bytes + st, i - st, h, &st_wprobe);
+            uint8_t c;
+            while (i < e && (c = byte_at(i)) != '/') {
+                h = fnv_step(h, c);
+                i++;
+            }
+            L.wid[lane] = staged ? word_lookup(a, &L.tb[st - tbase], i - st, h, &st_wprobe)
+                                 : word_lookup(a, a.bytes + st, i - st, h, &st_wprobe);
             L.cur[lane] = i + 1;
         }
         L.alive[nxt][lane] = 0;
@@ -316,9 +387,9 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
             const uint32_t w = has ? L.wid[tl] : NONE;
             const bool last = has && (d + 1 == L.nlev[tl]);
             Rec r1{}, r2{};
-            bool f1 = false, f2 = false;
-            if (has && (fl & F_LIT) && w != NONE) f1 = edge_probe(a, node, w, &r1, &st_probe) != ~0ull;
-            if (has && (fl & F_PLUS)) f2 = edge_probe(a, node, W_PLUS, &r2, &st_probe) != ~0ull;
+            bool f1, f2;
+            edge_probe2(a, node, has && (fl & F_LIT) && w != NONE, w, has && (fl & F_PLUS), &r1, &f1, &r2, &f2,
+                        &st_probe);
             // segments: each found child's '#' list; its exact list at the topic's last level
             const bool s1h = f1 && r1.hash_cnt, s1t = f1 && last && r1.term_cnt;
             const bool s2h = f2 && r2.hash_cnt, s2t = f2 && last && r2.term_cnt;
