@@ -22,8 +22,10 @@ struct MatchArgs {
     const WordSlot *wtab;
     uint64_t wmask;
     const uint8_t *warena;
+    const uint32_t *word_off;  // arena offset of each word (long-word verification)
     const EdgeSlot *etab;
     uint64_t emask;
+    const NodeRec *nodes;      // terminal lists of nodes with >= 2 keys
     const RootRec *root;
     const uint32_t *arena;
     // results
@@ -60,10 +62,7 @@ struct MatchArgs {
 // kernel handed off.  Asynchronous.
 hipError_t launch_match(const MatchArgs &a, hipStream_t stream);
 
-// Delta-epoch patches: dst[idx[i]] = src[i].
-hipError_t launch_scatter_edges(EdgeSlot *dst, const uint64_t *idx, const EdgeSlot *src,
-                                uint64_t n, hipStream_t stream);
-hipError_t launch_scatter_words(WordSlot *dst, const uint64_t *idx, const WordSlot *src,
-                                uint64_t n, hipStream_t stream);
+// Delta-epoch patches of 16-byte records: dst[idx[i]] = src[i].
+hipError_t launch_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n, hipStream_t stream);
 
 }  // namespace tmx

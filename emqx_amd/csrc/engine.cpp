@@ -130,6 +130,7 @@ struct tm_engine {
     uint64_t emask = 0;
     uint64_t n_edges = 0;
     std::vector<uint32_t> node_parent, node_word, node_slot;
+    std::vector<NodeRec> node_rec;  // terminal list of every node (device copy: d_nodes)
     RootRec root{0, 0, 0, 0};
 
     // ---- terminal-list arena
@@ -151,12 +152,13 @@ struct tm_engine {
     std::vector<uint8_t> stage_bytes;
     std::vector<std::pair<uint32_t, uint32_t>> lv_scratch;  // classify(): (start, len) per level
     std::vector<Delta> deltas;
-    std::vector<uint64_t> dirty_eslots, dirty_wslots;
+    std::vector<uint64_t> dirty_eslots, dirty_wslots, dirty_nodes;
     bool root_dirty = true;
     bool need_full = true;  // full device upload at next commit
 
     // ---- device copy
-    DevBuf d_wtab, d_warena, d_etab, d_root, d_arena;
+    DevBuf d_wtab, d_warena, d_word_off, d_etab, d_nodes, d_root, d_arena;
+    size_t word_off_dev = 0, nodes_dev = 0;  // entries already on device
     DevBuf d_scatter_idx, d_scatter_src;
     // batch buffers
     DevBuf d_bytes, d_off, d_outoff, d_outcnt, d_status, d_keys, d_cursor, d_slow_list,
@@ -171,26 +173,39 @@ struct tm_engine {
     bool timing_on = false;
 
     // =====================================================================
-    // words
-    uint32_t word_lookup(const uint8_t *p, uint32_t len) const {
+    // words: a word of <= 8 bytes is its own key (zero-padded LE bytes); longer
+    // words are keyed by FNV-1a 64 and verified against the arena
+    static uint64_t word_key(const uint8_t *p, uint32_t len) {
+        if (len <= 8) {
+            uint64_t k = 0;
+            for (uint32_t i = 0; i < len; i++) k |= (uint64_t)p[i] << (8 * i);
+            return k;
+        }
         uint64_t h = FNV_OFF;
         for (uint32_t i = 0; i < len; i++) h = fnv_step(h, p[i]);
-        uint64_t s = word_slot_hash(h, len) & wmask;
+        return h;
+    }
+    static uint32_t word_tag(uint32_t len) { return len > 8 ? (len | W_LONG) : len; }
+    uint32_t word_lookup(const uint8_t *p, uint32_t len) const {
+        const uint64_t key = word_key(p, len);
+        const uint32_t tag = word_tag(len);
+        uint64_t s = word_slot_hash(key, tag) & wmask;
         for (;;) {
             const WordSlot &w = wtab[s];
             if (w.wid == NONE) return NONE;
-            if (w.hash == h && w.len == len && memcmp(&warena[w.arena_off], p, len) == 0) return w.wid;
+            if (w.key == key && w.len == tag && (len <= 8 || memcmp(&warena[word_off[w.wid]], p, len) == 0))
+                return w.wid;
             s = (s + 1) & wmask;
         }
     }
     void word_rehash(uint64_t cap) {
         std::vector<WordSlot> old;
         old.swap(wtab);
-        wtab.assign(cap, WordSlot{0, NONE, 0, 0, {0}});
+        wtab.assign(cap, WordSlot{0, 0, NONE});
         wmask = cap - 1;
         for (const WordSlot &w : old)
             if (w.wid != NONE) {
-                uint64_t s = word_slot_hash(w.hash, w.len) & wmask;
+                uint64_t s = word_slot_hash(w.key, w.len) & wmask;
                 while (wtab[s].wid != NONE) s = (s + 1) & wmask;
                 wtab[s] = w;
             }
@@ -200,19 +215,11 @@ struct tm_engine {
         uint32_t wid = word_lookup(p, len);
         if (wid != NONE) return wid;
         if ((word_off.size() + 1) * 2 > wtab.size()) word_rehash(wtab.size() * 2);
-        uint64_t h = FNV_OFF;
-        for (uint32_t i = 0; i < len; i++) h = fnv_step(h, p[i]);
-        WordSlot w{};
-        w.hash = h;
-        w.wid = (uint32_t)word_off.size();
-        w.len = len;
-        w.arena_off = (uint32_t)warena.size();
-        memset(w.inl, 0, sizeof(w.inl));
-        memcpy(w.inl, p, std::min<uint32_t>(len, WORD_INLINE));
-        warena.insert(warena.end(), p, p + len);
-        word_off.push_back(w.arena_off);
+        WordSlot w{word_key(p, len), word_tag(len), (uint32_t)word_off.size()};
+        word_off.push_back((uint32_t)warena.size());
         word_len.push_back(len);
-        uint64_t s = word_slot_hash(h, len) & wmask;
+        warena.insert(warena.end(), p, p + len);
+        uint64_t s = word_slot_hash(w.key, w.len) & wmask;
         while (wtab[s].wid != NONE) s = (s + 1) & wmask;
         wtab[s] = w;
         dirty_wslots.push_back(s);
@@ -248,15 +255,15 @@ struct tm_engine {
     }
     void node_set_flag(uint32_t node, uint32_t f) {
         if (node == ROOT) {
-            if ((root.flags & f) != f) {
-                root.flags |= f;
+            if ((root.info & f) != f) {
+                root.info |= f;
                 root_dirty = true;
             }
             return;
         }
         EdgeSlot &e = etab[node_slot[node]];
-        if ((e.flags & f) != f) {
-            e.flags |= f;
+        if ((e.info & f) != f) {
+            e.info |= f;
             dirty_eslots.push_back(node_slot[node]);
         }
     }
@@ -270,6 +277,7 @@ struct tm_engine {
         node_parent.push_back(parent);
         node_word.push_back(word);
         node_slot.push_back(NONE);
+        node_rec.push_back(NodeRec{0, 0, 0, 0});
         s = edge_hash(parent, word) & emask;
         while (etab[s].parent != NONE) s = (s + 1) & emask;
         EdgeSlot e{};
@@ -280,7 +288,7 @@ struct tm_engine {
         node_slot[child] = (uint32_t)s;
         n_edges++;
         dirty_eslots.push_back(s);
-        node_set_flag(parent, word == W_PLUS ? F_PLUS : F_LIT);
+        node_set_flag(parent, word == W_PLUS ? I_PLUS : I_LIT);
         return child;
     }
 
@@ -453,22 +461,28 @@ struct tm_engine {
         }
     }
 
-    // list location of a node
-    void node_list(uint32_t node, uint32_t **off, uint32_t **tc, uint32_t **hc) {
+    // Recompute a node's emission bits from its list (and keep its I_PLUS/I_LIT):
+    // a single key goes inline into the slot, two or more use the node record.
+    void refresh_info(uint32_t node) {
+        const NodeRec &r = node_rec[node];
         if (node == ROOT) {
-            *off = &root.list_off;
-            *tc = &root.term_cnt;
-            *hc = &root.hash_cnt;
-        } else {
-            EdgeSlot &e = etab[node_slot[node]];
-            *off = &e.list_off;
-            *tc = &e.term_cnt;
-            *hc = &e.hash_cnt;
+            root.list_off = r.list_off;
+            root.term_cnt = r.term_cnt;
+            root.hash_cnt = r.hash_cnt;
+            root_dirty = true;
+            return;
         }
-    }
-    void mark_node_dirty(uint32_t node) {
-        if (node == ROOT) root_dirty = true;
-        else dirty_eslots.push_back(node_slot[node]);
+        EdgeSlot &e = etab[node_slot[node]];
+        uint32_t info = e.info & I_KIDS;
+        const uint32_t n = r.term_cnt + r.hash_cnt;
+        if (n == 1 && arena[r.list_off] < INLINE_KEY_LIMIT)
+            info |= (M_INLINE << I_MODE_SHIFT) | (r.hash_cnt ? I_INL_HASH : 0u) | arena[r.list_off];
+        else if (n)
+            info |= M_REC << I_MODE_SHIFT;
+        if (info != e.info) {
+            e.info = info;
+            dirty_eslots.push_back(node_slot[node]);
+        }
     }
 
     // Rebuild the whole arena from the key table (counting sort by node).
@@ -497,11 +511,8 @@ struct tm_engine {
             else arena[tfill[k.node]++] = (uint32_t)h;
         }
         for (size_t v = 0; v < nn; v++) {
-            uint32_t *o, *t, *hh;
-            node_list((uint32_t)v, &o, &t, &hh);
-            *o = (tcnt[v] + hcnt[v]) ? pos[v] : 0;
-            *t = tcnt[v];
-            *hh = hcnt[v];
+            node_rec[v] = NodeRec{(tcnt[v] + hcnt[v]) ? pos[v] : 0u, tcnt[v], hcnt[v], 0u};
+            refresh_info((uint32_t)v);
         }
         arena_garbage = 0;
         need_full = true;
@@ -517,101 +528,99 @@ struct tm_engine {
             size_t j = i;
             uint32_t node = deltas[i].node;
             while (j < deltas.size() && deltas[j].node == node) j++;
-            uint32_t *o, *t, *hh;
-            node_list(node, &o, &t, &hh);
-            terms.assign(arena.begin() + *o, arena.begin() + *o + *t);
-            hashes.assign(arena.begin() + *o + *t, arena.begin() + *o + *t + *hh);
+            NodeRec &r = node_rec[node];
+            terms.assign(arena.begin() + r.list_off, arena.begin() + r.list_off + r.term_cnt);
+            hashes.assign(arena.begin() + r.list_off + r.term_cnt,
+                          arena.begin() + r.list_off + r.term_cnt + r.hash_cnt);
             for (size_t k = i; k < j; k++) {
-                std::vector<uint32_t> &L = deltas[k].hash ? hashes : terms;
+                std::vector<uint32_t> &Lst = deltas[k].hash ? hashes : terms;
                 if (deltas[k].add) {
-                    L.push_back(deltas[k].key);
+                    Lst.push_back(deltas[k].key);
                 } else {
-                    auto it = std::find(L.begin(), L.end(), deltas[k].key);
-                    if (it != L.end()) L.erase(it);
+                    auto it = std::find(Lst.begin(), Lst.end(), deltas[k].key);
+                    if (it != Lst.end()) Lst.erase(it);
                 }
             }
-            arena_garbage += *t + *hh;
+            arena_garbage += r.term_cnt + r.hash_cnt;
             uint32_t off = (uint32_t)arena.size();
             arena.insert(arena.end(), terms.begin(), terms.end());
             arena.insert(arena.end(), hashes.begin(), hashes.end());
-            node_list(node, &o, &t, &hh);  // arena insert does not move slots, but be explicit
-            *o = (terms.size() + hashes.size()) ? off : 0;
-            *t = (uint32_t)terms.size();
-            *hh = (uint32_t)hashes.size();
-            mark_node_dirty(node);
+            r = NodeRec{(terms.size() + hashes.size()) ? off : 0u, (uint32_t)terms.size(), (uint32_t)hashes.size(), 0u};
+            dirty_nodes.push_back(node);
+            refresh_info(node);
             i = j;
         }
     }
 
+    template <class T>
+    hipError_t put(DevBuf &d, const std::vector<T> &h, size_t headroom_num = 3, size_t headroom_den = 2) {
+        hipError_t e;
+        size_t bytes = h.size() * sizeof(T);
+        if ((e = d.ensure(std::max<size_t>(bytes * headroom_num / headroom_den, 4096)))) return e;
+        if (bytes && (e = hipMemcpyAsync(d.p, h.data(), bytes, hipMemcpyHostToDevice, stream))) return e;
+        return hipSuccess;
+    }
+    template <class T>
+    hipError_t put_tail(DevBuf &d, const std::vector<T> &h, size_t &dev_n) {
+        if (h.size() <= dev_n) return hipSuccess;
+        hipError_t e = hipMemcpyAsync(d.as<T>() + dev_n, h.data() + dev_n, (h.size() - dev_n) * sizeof(T),
+                                      hipMemcpyHostToDevice, stream);
+        if (e == hipSuccess) dev_n = h.size();
+        return e;
+    }
+
     hipError_t upload_full() {
         hipError_t e;
-        if ((e = d_wtab.ensure(wtab.size() * sizeof(WordSlot)))) return e;
-        if ((e = hipMemcpyAsync(d_wtab.p, wtab.data(), wtab.size() * sizeof(WordSlot),
-                                hipMemcpyHostToDevice, stream)))
-            return e;
-        if ((e = d_warena.ensure(std::max<size_t>(warena.size() * 3 / 2, 4096)))) return e;
-        if (!warena.empty() &&
-            (e = hipMemcpyAsync(d_warena.p, warena.data(), warena.size(), hipMemcpyHostToDevice, stream)))
-            return e;
+        if ((e = put(d_wtab, wtab, 1, 1))) return e;
+        if ((e = put(d_warena, warena))) return e;
         warena_dev = warena.size();
-        if ((e = d_etab.ensure(etab.size() * sizeof(EdgeSlot)))) return e;
-        if ((e = hipMemcpyAsync(d_etab.p, etab.data(), etab.size() * sizeof(EdgeSlot),
-                                hipMemcpyHostToDevice, stream)))
-            return e;
-        if ((e = d_arena.ensure(std::max<size_t>(arena.size() * sizeof(uint32_t) * 3 / 2, 4096)))) return e;
-        if (!arena.empty() && (e = hipMemcpyAsync(d_arena.p, arena.data(), arena.size() * sizeof(uint32_t),
-                                                  hipMemcpyHostToDevice, stream)))
-            return e;
+        if ((e = put(d_word_off, word_off))) return e;
+        word_off_dev = word_off.size();
+        if ((e = put(d_etab, etab, 1, 1))) return e;
+        if ((e = put(d_nodes, node_rec))) return e;
+        nodes_dev = node_rec.size();
+        if ((e = put(d_arena, arena))) return e;
         arena_dev = arena.size();
         if ((e = d_root.ensure(sizeof(RootRec)))) return e;
         if ((e = hipMemcpyAsync(d_root.p, &root, sizeof(RootRec), hipMemcpyHostToDevice, stream))) return e;
         return hipStreamSynchronize(stream);
     }
 
+    // dst[idx[i]] = src[i] for 16-byte records (edge slots, word slots, node records)
+    template <class Rec16>
+    hipError_t scatter16(std::vector<uint64_t> &dirty, const std::vector<Rec16> &tab, void *dtab) {
+        static_assert(sizeof(Rec16) == 16, "16-byte records");
+        if (dirty.empty()) return hipSuccess;
+        std::sort(dirty.begin(), dirty.end());
+        dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+        size_t n = dirty.size();
+        std::vector<Rec16> src(n);
+        for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
+        hipError_t e;
+        if ((e = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e;
+        if ((e = d_scatter_src.ensure(n * 16))) return e;
+        if ((e = hipMemcpyAsync(d_scatter_idx.p, dirty.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, stream)))
+            return e;
+        if ((e = hipMemcpyAsync(d_scatter_src.p, src.data(), n * 16, hipMemcpyHostToDevice, stream))) return e;
+        if ((e = launch_scatter16((uint4 *)dtab, d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint4>(), n,
+                                  stream)))
+            return e;
+        return hipStreamSynchronize(stream);  // src dies at scope exit
+    }
+
     hipError_t upload_delta() {
         hipError_t e;
-        // grow-or-append arenas
-        if (warena.size() > d_warena.cap || arena.size() * sizeof(uint32_t) > d_arena.cap) return upload_full();
-        if (warena.size() > warena_dev) {
-            if ((e = hipMemcpyAsync(d_warena.as<uint8_t>() + warena_dev, warena.data() + warena_dev,
-                                    warena.size() - warena_dev, hipMemcpyHostToDevice, stream)))
-                return e;
-            warena_dev = warena.size();
-        }
-        if (arena.size() > arena_dev) {
-            if ((e = hipMemcpyAsync(d_arena.as<uint32_t>() + arena_dev, arena.data() + arena_dev,
-                                    (arena.size() - arena_dev) * sizeof(uint32_t), hipMemcpyHostToDevice, stream)))
-                return e;
-            arena_dev = arena.size();
-        }
-        // scatter dirty slots
-        auto scatter = [&](std::vector<uint64_t> &dirty, auto &tab, auto *dtab, bool edges) -> hipError_t {
-            if (dirty.empty()) return hipSuccess;
-            std::sort(dirty.begin(), dirty.end());
-            dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
-            size_t n = dirty.size();
-            using Slot = typename std::remove_reference<decltype(tab[0])>::type;
-            std::vector<Slot> src(n);
-            for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
-            hipError_t e2;
-            if ((e2 = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e2;
-            if ((e2 = d_scatter_src.ensure(n * sizeof(Slot)))) return e2;
-            if ((e2 = hipMemcpyAsync(d_scatter_idx.p, dirty.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice,
-                                     stream)))
-                return e2;
-            if ((e2 = hipMemcpyAsync(d_scatter_src.p, src.data(), n * sizeof(Slot), hipMemcpyHostToDevice, stream)))
-                return e2;
-            if (edges)
-                e2 = launch_scatter_edges((EdgeSlot *)dtab, d_scatter_idx.as<uint64_t>(),
-                                          d_scatter_src.as<EdgeSlot>(), n, stream);
-            else
-                e2 = launch_scatter_words((WordSlot *)dtab, d_scatter_idx.as<uint64_t>(),
-                                          d_scatter_src.as<WordSlot>(), n, stream);
-            if (e2) return e2;
-            return hipStreamSynchronize(stream);  // src vectors die at scope exit
-        };
-        if ((e = scatter(dirty_wslots, wtab, d_wtab.p, false))) return e;
-        if ((e = scatter(dirty_eslots, etab, d_etab.p, true))) return e;
+        // arrays that only grow: append the tail, or re-upload everything when full
+        if (warena.size() > d_warena.cap || arena.size() * sizeof(uint32_t) > d_arena.cap ||
+            word_off.size() * sizeof(uint32_t) > d_word_off.cap || node_rec.size() * sizeof(NodeRec) > d_nodes.cap)
+            return upload_full();
+        if ((e = put_tail(d_warena, warena, warena_dev))) return e;
+        if ((e = put_tail(d_word_off, word_off, word_off_dev))) return e;
+        if ((e = put_tail(d_arena, arena, arena_dev))) return e;
+        if ((e = put_tail(d_nodes, node_rec, nodes_dev))) return e;
+        if ((e = scatter16(dirty_wslots, wtab, d_wtab.p))) return e;
+        if ((e = scatter16(dirty_eslots, etab, d_etab.p))) return e;
+        if ((e = scatter16(dirty_nodes, node_rec, d_nodes.p))) return e;
         if (root_dirty) {
             if ((e = hipMemcpyAsync(d_root.p, &root, sizeof(RootRec), hipMemcpyHostToDevice, stream))) return e;
         }
@@ -641,6 +650,7 @@ struct tm_engine {
         root_dirty = false;
         dirty_eslots.clear();
         dirty_wslots.clear();
+        dirty_nodes.clear();
         for (uint32_t h : free_pending) free_keys.push_back(h);
         free_pending.clear();
         epoch++;
@@ -758,6 +768,8 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     eng->node_parent.push_back(NONE);  // root
     eng->node_word.push_back(NONE);
     eng->node_slot.push_back(NONE);
+    eng->node_rec.reserve(rn);
+    eng->node_rec.push_back(NodeRec{0, 0, 0, 0});
     eng->edge_rehash(next_pow2(std::max<uint64_t>(rn * 2, 1024)));
     eng->kset_rehash(next_pow2(std::max<uint64_t>(rk * 2, 1024)));
     eng->keys.reserve(rk);
@@ -775,7 +787,8 @@ void tm_destroy(tm_engine *eng) {
     if (!eng) return;
     (void)hipSetDevice(eng->cfg.device);
     if (eng->stream) (void)hipStreamSynchronize(eng->stream);
-    for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_etab, &eng->d_root, &eng->d_arena, &eng->d_scatter_idx,
+    for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_nodes, &eng->d_root,
+                      &eng->d_arena, &eng->d_scatter_idx,
                       &eng->d_scatter_src, &eng->d_bytes, &eng->d_off, &eng->d_outoff, &eng->d_outcnt,
                       &eng->d_status, &eng->d_keys, &eng->d_cursor, &eng->d_slow_list, &eng->d_slow_count,
                       &eng->d_scr_w, &eng->d_scr_s, &eng->d_stats, &eng->d_seg_pool, &eng->d_seg_cursor,
@@ -883,7 +896,9 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.wtab = eng->d_wtab.as<WordSlot>();
     a.wmask = eng->wmask;
     a.warena = eng->d_warena.as<uint8_t>();
+    a.word_off = eng->d_word_off.as<uint32_t>();
     a.etab = eng->d_etab.as<EdgeSlot>();
+    a.nodes = eng->d_nodes.as<NodeRec>();
     a.emask = eng->emask;
     a.root = eng->d_root.as<RootRec>();
     a.arena = eng->d_arena.as<uint32_t>();
@@ -1098,7 +1113,8 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
     out->edge_slots = eng->etab.size();
     out->word_slots = eng->wtab.size();
     out->list_words = eng->arena.size();
-    out->device_bytes = eng->d_wtab.cap + eng->d_warena.cap + eng->d_etab.cap + eng->d_arena.cap + eng->d_root.cap;
+    out->device_bytes = eng->d_wtab.cap + eng->d_warena.cap + eng->d_word_off.cap + eng->d_etab.cap +
+                        eng->d_nodes.cap + eng->d_arena.cap + eng->d_root.cap;
     out->n_full_rebuilds = eng->n_full_rebuilds;
     out->n_delta_commits = eng->n_delta_commits;
     out->n_slow_topics = eng->n_slow_last;

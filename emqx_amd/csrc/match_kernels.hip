@@ -11,19 +11,19 @@
 //   * a topic with a level exactly "+" or "#" is badarg (emqx_trie_search.erl:374-375).
 //
 // Kernels
-//   k_match_fast  one WAVEFRONT per 64 topics.  Lane = topic for tokenising; then a
-//                 level-synchronous walk whose frontier (all 64 topics' live trie
-//                 nodes at this depth) is staged in LDS and processed 64 entries at a
-//                 time, so '+' fan-out of one topic spreads over the whole wave.
-//                 Child probes, emitted key segments and next-frontier pushes are
-//                 compacted with wave prefix scans.  At the end the wave reserves its
-//                 output with ONE atomic and expands the segments with a
-//                 load-balanced copy (every lane busy, contiguous stores).
-//                 Levels are tokenised lazily, one per depth, so there is no level
-//                 cap; segments overflow LDS into a global chunk pool.
-//   k_match_slow  spill path for topics whose wave frontier overflows LDS (FCAP
-//                 entries): one lane per topic, depth-first with the stack in global
-//                 scratch (depth bounded by the level count), count pass + fill pass.
+//   k_match_fast  one WAVEFRONT per 64 topics.  The wave's topic bytes are staged in
+//                 LDS with 16-B loads; lane = topic for the pre-scan and for the
+//                 per-depth tokenise + word lookup.  The walk is level-synchronous:
+//                 the frontier (all 64 topics' live trie nodes at this depth) sits in
+//                 LDS and is expanded 64 entries per round, so one topic's '+'
+//                 fan-out spreads over the whole wave; each lane issues its literal
+//                 and '+' probes together.  Emitted key segments and next-frontier
+//                 pushes are compacted with wave prefix scans; both overflow LDS into
+//                 global chunk pools.  At the end the wave reserves its output with
+//                 ONE atomic and expands the segments with a load-balanced copy.
+//   k_match_slow  spill path for topics whose wave ran out of pool chunks: one lane
+//                 per topic, depth-first with the stack in global scratch (depth
+//                 bounded by the level count), count pass + fill pass.
 // No MFMA: this is a latency/gather-bound walk.
 #include <hip/hip_runtime.h>
 
@@ -32,12 +32,13 @@
 namespace tmx {
 
 constexpr int WAVE = 64;
-constexpr int FCAP = 256;      // frontier entries per wave per depth held in LDS
-constexpr int FCH = FR_CHUNK;  // frontier entries per global overflow chunk
-constexpr int MAXF = 64;       // overflow chunks per wave per depth
-constexpr int SCAP = SEG_CHUNK;  // key segments staged in LDS = one global chunk (128)
-constexpr int MAXCHUNK = 64;   // global segment chunks one wave may flush
-constexpr int TBCAP = 3072;    // topic bytes of one wave staged in LDS (else read from HBM)
+constexpr int FCAP = 256;        // frontier entries per wave per depth held in LDS
+constexpr int FCH = FR_CHUNK;    // frontier entries per global overflow chunk
+constexpr int MAXF = 64;         // overflow chunks per frontier buffer per wave
+constexpr int SCAP = SEG_CHUNK;  // key segments staged in LDS = one global chunk
+constexpr int MAXCHUNK = 64;     // global segment chunks one wave may flush
+constexpr int TBCAP = 3072;      // topic bytes of one wave staged in LDS (else read from HBM)
+constexpr uint32_t SEG_INLINE = 1u << 8;  // segment.w flag: .x is the key itself
 
 // ---------------------------------------------------------------------------
 // wave helpers
@@ -63,58 +64,67 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 }
 
 // ---------------------------------------------------------------------------
-// word table: bytes -> word id (byte-verified; never trusts the hash alone)
-__device__ __forceinline__ uint32_t word_lookup(const MatchArgs &a, const uint8_t *p, uint32_t len, uint64_t h,
-                                                uint32_t *probes) {
-    uint64_t s = word_slot_hash(h, len) & a.wmask;
+// word table: (key, tag) -> word id.  key = the word's bytes (<= 8) or its FNV-1a
+// hash (longer, then verified byte-for-byte against the arena: never trust a hash).
+template <class ByteAt>
+__device__ __forceinline__ uint32_t word_lookup(const MatchArgs &a, uint64_t key, uint32_t len, uint32_t st,
+                                                ByteAt &&byte_at, uint32_t *probes) {
+    const uint32_t tag = len > 8 ? (len | W_LONG) : len;
+    uint64_t s = word_slot_hash(key, tag) & a.wmask;
     for (;;) {
-        const uint4 *q = reinterpret_cast<const uint4 *>(a.wtab + s);
-        uint4 x = q[0];
-        uint4 y = q[1];
+        const uint4 x = *reinterpret_cast<const uint4 *>(a.wtab + s);
         (*probes)++;
-        uint64_t sh = (uint64_t)x.x | ((uint64_t)x.y << 32);
-        uint32_t wid = x.z;
-        if (wid == NONE) return NONE;
-        if (sh == h && x.w == len) {
-            // y = {arena_off, inl[0..3], inl[4..7], inl[8..11]}
+        if (x.w == NONE) return NONE;
+        if (x.z == tag && x.x == (uint32_t)key && x.y == (uint32_t)(key >> 32)) {
+            if (len <= 8) return x.w;
+            const uint8_t *w = a.warena + a.word_off[x.w];
             bool eq = true;
-            uint32_t inl[3] = {y.y, y.z, y.w};
-            uint32_t ni = len < WORD_INLINE ? len : WORD_INLINE;
-            for (uint32_t i = 0; i < ni && eq; i++) eq = p[i] == (uint8_t)(inl[i >> 2] >> ((i & 3) * 8));
-            for (uint32_t i = WORD_INLINE; i < len && eq; i++) eq = p[i] == a.warena[y.x + i];
-            if (eq) return wid;
+            for (uint32_t i = 0; i < len && eq; i++) eq = byte_at(st + i) == w[i];
+            if (eq) return x.w;
         }
         s = (s + 1) & a.wmask;
     }
 }
 
-// edge table: (parent, word) -> 32-byte slot; returns slot index or ~0
+// Tokenise one level starting at byte *i (== e for an empty last level):
+// returns the word key and advances *i to the '/' or the end.
+template <class ByteAt>
+__device__ __forceinline__ uint64_t level_key(uint32_t *i, uint32_t e, ByteAt &&byte_at) {
+    uint64_t w8 = 0, h = FNV_OFF;
+    uint32_t k = *i, n = 0;
+    uint8_t c;
+    while (k < e && (c = byte_at(k)) != '/') {
+        if (n < 8) w8 |= (uint64_t)c << (8 * n);
+        h = fnv_step(h, c);
+        k++;
+        n++;
+    }
+    *i = k;
+    return n <= 8 ? w8 : h;
+}
+
+// edge table: (parent, word) -> 16-byte slot
 struct Rec {
-    uint32_t child, flags, list_off, term_cnt, hash_cnt;
+    uint32_t child, info;
 };
 __device__ __forceinline__ uint64_t edge_probe(const MatchArgs &a, uint32_t parent, uint32_t word, Rec *r,
                                                uint32_t *probes) {
     uint64_t s = edge_hash(parent, word) & a.emask;
     for (;;) {
-        const uint4 *q = reinterpret_cast<const uint4 *>(a.etab + s);
-        uint4 x = q[0];
-        uint4 y = q[1];
+        const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + s);
         (*probes)++;
         if (x.x == NONE) return ~0ull;
         if (x.x == parent && x.y == word) {
             r->child = x.z;
-            r->flags = x.w;
-            r->list_off = y.x;
-            r->term_cnt = y.y;
-            r->hash_cnt = y.z;
+            r->info = x.w;
             return s;
         }
         s = (s + 1) & a.emask;
     }
 }
 
-// Probe (parent, word) and (parent, '+') together: both first loads are in flight
-// before either result is consumed (the two are independent chains).
+// Probe (parent, word) and (parent, '+') together: both loads are in flight before
+// either result is consumed (the two chains are independent).
 __device__ __forceinline__ void edge_probe2(const MatchArgs &a, uint32_t parent, bool want1, uint32_t word,
                                             bool want2, Rec *r1, bool *f1, Rec *r2, bool *f2, uint32_t *probes) {
     uint64_t s1 = edge_hash(parent, word) & a.emask;
@@ -123,23 +133,15 @@ __device__ __forceinline__ void edge_probe2(const MatchArgs &a, uint32_t parent,
     *f1 = false;
     *f2 = false;
     while (p1 || p2) {
-        uint4 x1 = make_uint4(NONE, 0, 0, 0), y1 = x1, x2 = x1, y2 = x1;
-        if (p1) {
-            const uint4 *q = reinterpret_cast<const uint4 *>(a.etab + s1);
-            x1 = q[0];
-            y1 = q[1];
-        }
-        if (p2) {
-            const uint4 *q = reinterpret_cast<const uint4 *>(a.etab + s2);
-            x2 = q[0];
-            y2 = q[1];
-        }
+        uint4 x1 = make_uint4(NONE, 0, 0, 0), x2 = x1;
+        if (p1) x1 = *reinterpret_cast<const uint4 *>(a.etab + s1);
+        if (p2) x2 = *reinterpret_cast<const uint4 *>(a.etab + s2);
         *probes += (uint32_t)p1 + (uint32_t)p2;
         if (p1) {
             if (x1.x == NONE) {
                 p1 = false;
             } else if (x1.x == parent && x1.y == word) {
-                *r1 = Rec{x1.z, x1.w, y1.x, y1.y, y1.z};
+                *r1 = Rec{x1.z, x1.w};
                 *f1 = true;
                 p1 = false;
             } else {
@@ -150,7 +152,7 @@ __device__ __forceinline__ void edge_probe2(const MatchArgs &a, uint32_t parent,
             if (x2.x == NONE) {
                 p2 = false;
             } else if (x2.x == parent && x2.y == W_PLUS) {
-                *r2 = Rec{x2.z, x2.w, y2.x, y2.y, y2.z};
+                *r2 = Rec{x2.z, x2.w};
                 *f2 = true;
                 p2 = false;
             } else {
@@ -160,51 +162,20 @@ __device__ __forceinline__ void edge_probe2(const MatchArgs &a, uint32_t parent,
     }
 }
 
-// Tokenise topic t: calls f(level_index, word_id) per level; returns levels,
-// sets *badarg when a level is exactly "+" or "#", *dollar when the first level
-// starts with '$'.
-template <class F>
-__device__ __forceinline__ uint32_t tokenize(const MatchArgs &a, uint32_t t, bool *badarg, bool *dollar,
-                                             uint32_t *wprobes, F &&f) {
-    const uint32_t b = a.off[t], e = a.off[t + 1];
-    *dollar = (e > b) && a.bytes[b] == '$';
-    *badarg = false;
-    uint32_t nl = 0, st = b;
-    uint64_t h = FNV_OFF;
-    for (uint32_t i = b;; ++i) {
-        const bool end = (i == e);
-        const uint8_t c = end ? (uint8_t)'/' : a.bytes[i];
-        if (c == '/') {
-            const uint32_t len = i - st;
-            uint32_t wid = NONE;
-            if (len == 1 && (a.bytes[st] == '+' || a.bytes[st] == '#')) *badarg = true;
-            else wid = word_lookup(a, a.bytes + st, len, h, wprobes);
-            f(nl, wid);
-            nl++;
-            h = FNV_OFF;
-            st = i + 1;
-            if (end) break;
-        } else {
-            h = fnv_step(h, c);
-        }
-    }
-    return nl;
-}
-
 // ---------------------------------------------------------------------------
 // fast kernel: one wavefront (= one 64-thread workgroup) per 64 topics
 //
-// LDS per wave (~10 KiB): the two frontier buffers (FCAP entries each, extended by
-// global overflow chunks), a segment staging buffer that is flushed to a global
-// chunk pool when full, and per-topic cursors.  Levels are tokenised lazily (one
-// level per depth, lane = topic) so there is no level cap; a topic only spills to
-// k_match_slow when a pool is exhausted.
+// LDS per wave (~10.5 KiB): the topic bytes, the two frontier buffers (FCAP
+// entries each, extended by global overflow chunks), a segment staging buffer that
+// is flushed to a global chunk pool when full, and per-topic cursors.  Levels are
+// tokenised lazily (one level per depth) so there is no level cap; a topic only
+// spills to k_match_slow when a pool is exhausted.
 struct WaveLds {
     uint8_t tb[TBCAP];            // the wave's topic bytes (16-B aligned window)
     uint32_t fr_node[2][FCAP];
-    uint8_t fr_meta[2][FCAP];     // topic lane | node flags << 6
+    uint8_t fr_meta[2][FCAP];     // topic lane | node I_KIDS bits >> 24
     uint32_t fch[2][MAXF];        // global overflow chunks of each frontier buffer
-    uint4 seg[SCAP];  // {src, cnt, rel, topic lane}
+    uint4 seg[SCAP];              // {src or key, cnt, rel, topic lane | SEG_INLINE}
     uint32_t seg_scan[SCAP + 1];
     uint32_t chunk[MAXCHUNK];
     uint32_t cur[WAVE];    // byte offset where the topic's next level starts
@@ -226,7 +197,7 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
         uint32_t c = 0;
         if (j < ns) {
             const uint4 g = L.seg[j];
-            if (!(L.lflags[g.w] & 1u)) c = g.y;
+            if (!(L.lflags[g.w & 0xFFu] & 1u)) c = g.y;
         }
         uint32_t tot;
         const uint32_t ex = wave_excl_scan(c, &tot);
@@ -244,7 +215,8 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
         }
         const uint4 g = L.seg[lo];
         const uint32_t k = e - L.seg_scan[lo];
-        a.keys[L.tbase[g.w] + g.z + k] = a.arena[g.x + k];
+        const uint32_t key = (g.w & SEG_INLINE) ? g.x : a.arena[g.x + k];
+        a.keys[L.tbase[g.w & 0xFFu] + g.z + k] = key;
     }
     __syncthreads();
 }
@@ -316,12 +288,12 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
         }
         nseg = tot;
         st_seg += em;
-        const uint32_t rf = dollar ? (R.flags & F_LIT) : (R.flags & F_KIDS);
+        const uint32_t rf = dollar ? (R.info & I_LIT) : (R.info & I_KIDS);
         const bool push = walk && rf;
         const uint32_t p2 = wave_excl_scan(push ? 1u : 0u, &tot);
         if (push) {
             L.fr_node[0][p2] = ROOT;
-            L.fr_meta[0][p2] = (uint8_t)(lane | (rf << 6));
+            L.fr_meta[0][p2] = (uint8_t)(lane | (rf >> 24));
             L.alive[0][lane] = 1;
             st_visit++;
         }
@@ -360,14 +332,8 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
         if (walk && L.alive[cur][lane]) {
             uint32_t i = L.cur[lane];
             const uint32_t st = i;
-            uint64_t h = FNV_OFF;
-            uint8_t c;
-            while (i < e && (c = byte_at(i)) != '/') {
-                h = fnv_step(h, c);
-                i++;
-            }
-            L.wid[lane] = staged ? word_lookup(a, &L.tb[st - tbase], i - st, h, &st_wprobe)
-                                 : word_lookup(a, a.bytes + st, i - st, h, &st_wprobe);
+            const uint64_t key = level_key(&i, e, byte_at);
+            L.wid[lane] = word_lookup(a, key, i - st, st, byte_at, &st_wprobe);
             L.cur[lane] = i + 1;
         }
         L.alive[nxt][lane] = 0;
@@ -382,18 +348,25 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                 uint32_t meta;
                 fr_read(cur, i, node, meta);
                 tl = meta & 63u;
-                fl = meta >> 6;
+                fl = (meta & 0xC0u) << 24;  // back to I_PLUS | I_LIT
             }
             const uint32_t w = has ? L.wid[tl] : NONE;
             const bool last = has && (d + 1 == L.nlev[tl]);
             Rec r1{}, r2{};
             bool f1, f2;
-            edge_probe2(a, node, has && (fl & F_LIT) && w != NONE, w, has && (fl & F_PLUS), &r1, &f1, &r2, &f2,
+            edge_probe2(a, node, has && (fl & I_LIT) && w != NONE, w, has && (fl & I_PLUS), &r1, &f1, &r2, &f2,
                         &st_probe);
-            // segments: each found child's '#' list; its exact list at the topic's last level
-            const bool s1h = f1 && r1.hash_cnt, s1t = f1 && last && r1.term_cnt;
-            const bool s2h = f2 && r2.hash_cnt, s2t = f2 && last && r2.term_cnt;
-            const uint32_t ns = (uint32_t)s1h + s1t + s2h + s2t;
+            // what each found child emits: its '#' keys always, its exact keys at the
+            // topic's last level; one key inline in the slot, more via the node record
+            const uint32_t m1 = f1 ? info_mode(r1.info) : M_NONE, m2 = f2 ? info_mode(r2.info) : M_NONE;
+            NodeRec n1{0, 0, 0, 0}, n2{0, 0, 0, 0};
+            if (m1 == M_REC) n1 = a.nodes[r1.child];
+            if (m2 == M_REC) n2 = a.nodes[r2.child];
+            const bool i1 = m1 == M_INLINE && ((r1.info & I_INL_HASH) || last);
+            const bool i2 = m2 == M_INLINE && ((r2.info & I_INL_HASH) || last);
+            const bool s1h = n1.hash_cnt, s1t = last && n1.term_cnt;
+            const bool s2h = n2.hash_cnt, s2t = last && n2.term_cnt;
+            const uint32_t ns = (uint32_t)i1 + s1h + s1t + i2 + s2h + s2t;
             uint32_t tot_s;
             uint32_t ps = wave_excl_scan(ns, &tot_s);
             if (tot_s && nseg + tot_s > (uint32_t)SCAP) {
@@ -411,26 +384,28 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                     st_flush++;
                 } else {
                     // pool exhausted: those topics take the spill kernel instead
-                    for (uint32_t j = lane; j < nseg; j += WAVE) atomicOr(&L.lflags[L.seg[j].w], 1u);
+                    for (uint32_t j = lane; j < nseg; j += WAVE) atomicOr(&L.lflags[L.seg[j].w & 0xFFu], 1u);
                 }
                 nseg = 0;
                 __syncthreads();
             }
             ps += nseg;
             if (ns) {
-                auto put = [&](uint32_t src, uint32_t c) {
-                    L.seg[ps++] = make_uint4(src, c, atomicAdd(&L.cnt[tl], c), tl);
+                auto put = [&](uint32_t src, uint32_t c, uint32_t fl2) {
+                    L.seg[ps++] = make_uint4(src, c, atomicAdd(&L.cnt[tl], c), tl | fl2);
                 };
-                if (s1t) put(r1.list_off, r1.term_cnt);
-                if (s1h) put(r1.list_off + r1.term_cnt, r1.hash_cnt);
-                if (s2t) put(r2.list_off, r2.term_cnt);
-                if (s2h) put(r2.list_off + r2.term_cnt, r2.hash_cnt);
+                if (i1) put(r1.info & I_KEY_MASK, 1u, SEG_INLINE);
+                if (s1t) put(n1.list_off, n1.term_cnt, 0u);
+                if (s1h) put(n1.list_off + n1.term_cnt, n1.hash_cnt, 0u);
+                if (i2) put(r2.info & I_KEY_MASK, 1u, SEG_INLINE);
+                if (s2t) put(n2.list_off, n2.term_cnt, 0u);
+                if (s2h) put(n2.list_off + n2.term_cnt, n2.hash_cnt, 0u);
             }
             nseg += tot_s;
             st_seg += ns;
             // next frontier: children that can still expand
-            const bool p1 = f1 && !last && (r1.flags & F_KIDS);
-            const bool p2b = f2 && !last && (r2.flags & F_KIDS);
+            const bool p1 = f1 && !last && (r1.info & I_KIDS);
+            const bool p2b = f2 && !last && (r2.info & I_KIDS);
             uint32_t tot_p;
             uint32_t pp = nnext + wave_excl_scan((uint32_t)p1 + p2b, &tot_p);
             // capacity of the next buffer: LDS + overflow chunks (grown on demand)
@@ -449,8 +424,8 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
             }
             if (p1 || p2b) {
                 if (pp + (uint32_t)p1 + p2b <= cap) {
-                    if (p1) fr_write(nxt, pp++, r1.child, tl | ((r1.flags & F_KIDS) << 6));
-                    if (p2b) fr_write(nxt, pp, r2.child, tl | ((r2.flags & F_KIDS) << 6));
+                    if (p1) fr_write(nxt, pp++, r1.child, tl | ((r1.info & I_KIDS) >> 24));
+                    if (p2b) fr_write(nxt, pp, r2.child, tl | ((r2.info & I_KIDS) >> 24));
                     atomicAdd(&L.alive[nxt][tl], (uint32_t)p1 + p2b);
                 } else {
                     atomicOr(&L.lflags[tl], 1u);  // frontier overflow: topic spills
@@ -530,22 +505,27 @@ __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_
         const uint64_t ent = stk[--sp];
         const uint64_t slot = ent >> 24;
         const uint32_t d = (uint32_t)(ent & 0xFFFFFF);
-        const bool is_root = slot == ROOT_MARK;
-        uint32_t node, flags, lo, tc, hc;
-        if (is_root) {
+        uint32_t node, info, lo = 0, tc = 0, hc = 0;
+        if (slot == ROOT_MARK) {
             node = ROOT;
-            flags = dollar ? (R.flags & F_LIT) : R.flags;
+            info = dollar ? (R.info & I_LIT) : R.info;
             lo = R.list_off;
-            tc = R.term_cnt;
             hc = dollar ? 0 : R.hash_cnt;
         } else {
-            const uint4 *q = reinterpret_cast<const uint4 *>(a.etab + slot);
-            uint4 x = q[0], y = q[1];
+            const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + slot);
             node = x.z;
-            flags = x.w;
-            lo = y.x;
-            tc = y.y;
-            hc = y.z;
+            info = x.w;
+            const uint32_t m = info_mode(info);
+            if (m == M_REC) {
+                const NodeRec nr = a.nodes[node];
+                lo = nr.list_off;
+                tc = nr.term_cnt;
+                hc = nr.hash_cnt;
+            } else if (m == M_INLINE && ((info & I_INL_HASH) || d == nl)) {
+                // the node's only key, inline in the slot
+                if (WRITE) out[count] = info & I_KEY_MASK;
+                count++;
+            }
         }
         (*visits)++;
         // "P/#" keys match at P and below
@@ -559,12 +539,12 @@ __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_
             continue;
         }
         Rec r;
-        if (flags & F_PLUS) {
+        if (info & I_PLUS) {
             uint64_t s = edge_probe(a, node, W_PLUS, &r, probes);
             if (s != ~0ull) stk[sp++] = (s << 24) | (d + 1);
         }
         const uint32_t w = wid[d];
-        if ((flags & F_LIT) && w != NONE) {
+        if ((info & I_LIT) && w != NONE) {
             uint64_t s = edge_probe(a, node, w, &r, probes);
             if (s != ~0ull) stk[sp++] = (s << 24) | (d + 1);
         }
@@ -577,15 +557,22 @@ __global__ __launch_bounds__(WAVE) void k_match_slow(MatchArgs a) {
     const uint32_t nslow = *a.slow_count;
     const RootRec R = *a.root;
     uint32_t st_visit = 0, st_probe = 0, st_wprobe = 0;
-    uint64_t st_keys = 0, st_lev = 0;
+    uint64_t st_keys = 0;
+    auto byte_at = [&](uint32_t i) -> uint8_t { return a.bytes[i]; };
     for (uint32_t idx = blockIdx.x * WAVE + lane_id(); idx < nslow; idx += gridDim.x * WAVE) {
         const uint32_t t = a.slow_list[idx];
         const uint64_t sbase = (uint64_t)(a.off[t] - a.off[0]) + 2ull * t;  // len+2 entries per topic
         uint32_t *wid = a.scratch_w + sbase;
         uint64_t *stk = a.scratch_s + sbase;
-        bool badarg, dollar;
-        const uint32_t nl = tokenize(a, t, &badarg, &dollar, &st_wprobe, [&](uint32_t i, uint32_t w) { wid[i] = w; });
-        st_lev += nl;
+        const uint32_t b = a.off[t], e = a.off[t + 1];
+        const bool dollar = (e > b) && a.bytes[b] == '$';
+        uint32_t nl = 0;
+        for (uint32_t i = b;; ++i) {  // tokenise every level (the topic is not badarg)
+            const uint32_t st = i;
+            const uint64_t key = level_key(&i, e, byte_at);
+            wid[nl++] = word_lookup(a, key, i - st, st, byte_at, &st_wprobe);
+            if (i >= e) break;
+        }
         uint32_t dummy_v = 0, dummy_p = 0;
         const uint32_t c = dfs_walk<false>(a, R, wid, stk, nl, dollar, nullptr, &dummy_p, &dummy_v);
         const unsigned long long pos = atomicAdd(a.cursor, (unsigned long long)c);
@@ -601,27 +588,18 @@ __global__ __launch_bounds__(WAVE) void k_match_slow(MatchArgs a) {
         atomicAdd(&a.stats[1], (unsigned long long)st_probe);
         atomicAdd(&a.stats[2], (unsigned long long)st_wprobe);
         atomicAdd(&a.stats[3], (unsigned long long)st_keys);
-        (void)st_lev;
     }
 }
 
 // ---------------------------------------------------------------------------
-template <class Slot>
-__global__ void k_scatter(Slot *dst, const uint64_t *idx, const Slot *src, uint64_t n) {
+__global__ void k_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) dst[idx[i]] = src[i];
 }
 
-hipError_t launch_scatter_edges(EdgeSlot *dst, const uint64_t *idx, const EdgeSlot *src, uint64_t n,
-                                hipStream_t s) {
+hipError_t launch_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n, hipStream_t s) {
     if (!n) return hipSuccess;
-    k_scatter<EdgeSlot><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
-    return hipGetLastError();
-}
-hipError_t launch_scatter_words(WordSlot *dst, const uint64_t *idx, const WordSlot *src, uint64_t n,
-                                hipStream_t s) {
-    if (!n) return hipSuccess;
-    k_scatter<WordSlot><<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
+    k_scatter16<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
     return hipGetLastError();
 }
 

@@ -116,11 +116,14 @@ def test_modes_unique_first_vs_oracle():
 EDGE_FILTERS = [b"#", b"+", b"+/+", b"/#", b"/+", b"//", b"", b"a", b"a/#", b"a/+", b"a//b", b"a/+/+", b"+/#",
                 b"$SYS/#", b"$SYS/+", b"$SYS/brokers/+/clients/#", b"+/brokers/#", b"a/#/b", b"a/b#", b"a/b+",
                 b"sport/", b"sport/+", b"$share", b"$queue/x", b"\xc3\xa9t\xc3\xa9/+", b"x" * 300 + b"/#",
-                b"/".join([b"+"] * 26) + b"/#", b"/".join([b"+"] * 40), b"/".join(b"L%d" % i for i in range(30))]
+                b"/".join([b"+"] * 26) + b"/#", b"/".join([b"+"] * 40), b"/".join(b"L%d" % i for i in range(30)),
+                b"abcdefgh/+", b"abcdefghi/#", b"abcdefgh", b"abcdefghi", b"abcdefghij/x", b"\x00a/+", b"a\x00"]
 EDGE_TOPICS = [b"", b"/", b"//", b"a", b"a/", b"a/b", b"a//b", b"a/b/c", b"$SYS", b"$SYS/brokers/n1/clients/c",
                b"$", b"$x/y", b"sport/", b"sport", b"a/b#", b"a/b+", b"\xc3\xa9t\xc3\xa9/x", b"x" * 300 + b"/y",
                b"/".join(b"L%d" % i for i in range(30)), b"/".join([b"q"] * 40), b"/".join([b"q"] * 26),
-               b"/" * 200, b"+", b"#", b"a/+/b", b"a/b/#", b"b" * 65535, b"/".join([b"z"] * 3000)]
+               b"/" * 200, b"+", b"#", b"a/+/b", b"a/b/#", b"b" * 65535, b"/".join([b"z"] * 3000),
+               b"abcdefgh", b"abcdefgh/1", b"abcdefghi", b"abcdefghi/2", b"abcdefghij/x", b"abcdefghiJ/x",
+               b"\x00a/q", b"a\x00", b"a", b"abcdefg"]
 
 
 def test_edge_cases_vs_python_semantics(mode):
