@@ -113,7 +113,7 @@ def main():
 
     # size the output arena from the first run (overflow -> grow -> rerun)
     r = step()
-    torch.cuda.synchronize()
+    eng.device_sync()  # also sizes the engine's chunk pools to this batch's demand
     total = _read_u64(r.d_total)
     if total > r.keys_cap:
         eng.reserve_matches(int(total * 1.1) + 1024)
@@ -123,6 +123,7 @@ def main():
     assert total <= r.keys_cap
     for _ in range(max(0, args.warmup - 1)):
         step()
+    eng.device_sync()
     torch.cuda.synchronize()
 
     # walk statistics for the algorithmic-byte count (one untimed, counted run)
@@ -163,6 +164,7 @@ def main():
         torch.cuda.synchronize()
         kms.append(eng.timing(False))
     kernel_ms = float(np.mean(kms))
+    eng.device_sync()
     slow_topics = eng.stats()["n_slow_topics"]
 
     # ---------------------------------------------------------------- CPU baseline + parity sample

@@ -167,7 +167,8 @@ struct tm_engine {
     PinBuf h_bytes, h_off, h_outoff, h_outcnt, h_status, h_keys, h_cursor;
     std::vector<uint32_t> pp_off, pp_cnt, pp_keys;  // post-processed results
     hipStream_t stream = nullptr;
-    uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0, seg_demand_last = 0;
+    uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0, seg_demand_last = 0, fr_demand_last = 0;
+    hipStream_t last_stream = nullptr;  // stream of the last tm_match_device call
     bool stats_on = false;
     hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // around k_match_fast (tm_debug_timing)
     bool timing_on = false;
@@ -863,7 +864,7 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
     TM_TRY_HIP(eng->d_seg_cursor.ensure(64), TM_ENOMEM, "alloc");
     {
         // chunk pool for waves whose staged key segments overflow LDS
-        uint64_t want = eng->cfg.seg_chunks ? eng->cfg.seg_chunks : std::max<uint64_t>(1024, ((uint64_t)n + 63) / 64 * 2);
+        uint64_t want = eng->cfg.seg_chunks ? eng->cfg.seg_chunks : std::max<uint64_t>(1024, ((uint64_t)n + 63) / 64 * 8);
         if (want > eng->seg_chunks) {
             TM_TRY_HIP(eng->d_seg_pool.ensure(want * SEG_CHUNK * sizeof(uint4)), TM_ENOMEM, "alloc seg pool");
             eng->seg_chunks = want;
@@ -882,6 +883,23 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
         uint64_t want = eng->cfg.reserve_matches ? eng->cfg.reserve_matches : std::max<uint64_t>(n * 8ull, 1 << 16);
         TM_TRY_HIP(eng->d_keys.ensure(want * 4), TM_ENOMEM, "alloc");
         eng->keys_cap = want;
+    }
+    return TM_OK;
+}
+
+// After a batch: pools that ran short sent some topics to the spill kernel (results
+// stay exact); size them to the observed demand for the next batch.
+static int grow_pools(tm_engine *eng) {
+    if (eng->cfg.seg_chunks) return TM_OK;  // fixed by the caller (test aid)
+    if (eng->seg_demand_last > eng->seg_chunks) {
+        uint64_t want = eng->seg_demand_last + eng->seg_demand_last / 4 + 64;
+        TM_TRY_HIP(eng->d_seg_pool.ensure(want * SEG_CHUNK * sizeof(uint4)), TM_ENOMEM, "alloc seg pool");
+        eng->seg_chunks = want;
+    }
+    if (eng->fr_demand_last > eng->fr_chunks) {
+        uint64_t want = eng->fr_demand_last + eng->fr_demand_last / 4 + 64;
+        TM_TRY_HIP(eng->d_fr_pool.ensure(want * FR_CHUNK * sizeof(uint2)), TM_ENOMEM, "alloc frontier pool");
+        eng->fr_chunks = want;
     }
     return TM_OK;
 }
@@ -961,10 +979,13 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
                    TM_EDEVICE, "D2H");
         TM_TRY_HIP(hipMemcpyAsync((uint8_t *)eng->h_cursor.p + 16, eng->d_seg_cursor.p, 8, hipMemcpyDeviceToHost, s),
                    TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipMemcpyAsync((uint8_t *)eng->h_cursor.p + 24, eng->d_fr_cursor.p, 8, hipMemcpyDeviceToHost, s),
+                   TM_EDEVICE, "D2H");
         TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "match kernels");
         uint64_t total = *eng->h_cursor.as<uint64_t>();
         eng->n_slow_last = *(uint32_t *)((uint8_t *)eng->h_cursor.p + 8);
         eng->seg_demand_last = *(uint64_t *)((uint8_t *)eng->h_cursor.p + 16);
+        eng->fr_demand_last = *(uint64_t *)((uint8_t *)eng->h_cursor.p + 24);
         if (total <= eng->keys_cap) break;
         // output arena too small: grow to the demand and run again (once suffices:
         // the cursor counts every key the batch asked for)
@@ -987,12 +1008,7 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
         TM_TRY_HIP(hipMemcpyAsync(eng->h_keys.p, eng->d_keys.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                    "D2H");
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "D2H");
-    if (eng->seg_demand_last > eng->seg_chunks && !eng->cfg.seg_chunks) {
-        // those waves' topics took the spill kernel (still exact); size up for next time
-        uint64_t want = eng->seg_demand_last + eng->seg_demand_last / 4 + 64;
-        TM_TRY_HIP(eng->d_seg_pool.ensure(want * SEG_CHUNK * sizeof(uint4)), TM_ENOMEM, "alloc seg pool");
-        eng->seg_chunks = want;
-    }
+    if ((rc = grow_pools(eng))) return rc;
     out->total = total;
     out->off = eng->h_outoff.as<uint32_t>();
     out->cnt = eng->h_outcnt.as<uint32_t>();
@@ -1063,6 +1079,7 @@ int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_of
     int rc = ensure_batch(eng, n, total_bytes);
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    eng->last_stream = s;
     TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s), TM_EDEVICE, "kernel launch");
     out->n = n;
     out->d_off = eng->d_outoff.as<uint32_t>();
@@ -1076,7 +1093,22 @@ int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_of
 
 int tm_device_sync(tm_engine *eng) {
     if (!eng) return TM_EINVAL;
-    TM_TRY_HIP(hipStreamSynchronize(eng->stream), TM_EDEVICE, "sync");
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    hipStream_t s = eng->last_stream ? eng->last_stream : eng->stream;
+    TM_TRY_HIP(eng->h_cursor.ensure(64), TM_ENOMEM, "pinned alloc");
+    uint8_t *h = (uint8_t *)eng->h_cursor.p;
+    if (eng->d_cursor.p) {
+        TM_TRY_HIP(hipMemcpyAsync(h + 8, eng->d_slow_count.p, 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(h + 16, eng->d_seg_cursor.p, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(h + 24, eng->d_fr_cursor.p, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+    }
+    TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "sync");
+    if (eng->d_cursor.p) {
+        eng->n_slow_last = *(uint32_t *)(h + 8);
+        eng->seg_demand_last = *(uint64_t *)(h + 16);
+        eng->fr_demand_last = *(uint64_t *)(h + 24);
+        return grow_pools(eng);
+    }
     return TM_OK;
 }
 

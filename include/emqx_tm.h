@@ -173,6 +173,8 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off,
  * Batch limits: total topic bytes < 4 GiB, total matches < 4 Gi keys. */
 int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off,
                     uint32_t n, uint64_t total_bytes, void *stream, tm_dev_result *out);
+/* Wait for the last tm_match_device batch; refresh tm_stats().n_slow_topics and size
+ * the internal chunk pools to that batch's demand for the next one. */
 int tm_device_sync(tm_engine *eng);
 int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap);
 
