@@ -37,13 +37,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def algorithmic_bytes(stats5, topic_bytes, n):
-    """Bytes one batch must move at minimum under the frozen layout:
-    topic bytes + u32 offsets in, one 32 B slot per word-table probe and per edge-table
-    probe, 4 B key read from the terminal-list arena + 4 B key written per match, and
-    12 B of per-topic results (offset, count, status)."""
-    visits, eprobes, wprobes, keys, levels = stats5[:5]
-    return topic_bytes + 4 * (n + 1) + 32 * wprobes + 32 * eprobes + 8 * keys + 12 * n
+def algorithmic_bytes(st, topic_bytes, n):
+    """Bytes one batch must move at minimum under the frozen layout, from
+    the kernel's own walk counters `st` (Engine.STAT_NAMES):
+      topic bytes + u32 offsets in,
+      16 B per word-table probe, 16 B per edge-table probe, 16 B per node record read,
+      4 B per key read from the terminal-list arena (keys not inlined in an edge slot),
+      4 B per key written, 12 B per topic of results (offset, count, status)."""
+    arena_keys = st["keys"] - st["inline_keys"]
+    return (topic_bytes + 4 * (n + 1) + 16 * st["word_probes"] + 16 * st["edge_probes"]
+            + 16 * st["node_records"] + 4 * arena_keys + 4 * st["keys"] + 12 * n)
 
 
 def cpu_info():
@@ -105,7 +108,7 @@ def main():
     dev = torch.device("cuda", local)
     d_bytes = torch.from_numpy(tb).to(dev)
     d_off = torch.from_numpy(to.view(np.int32)).to(dev)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # kernels and timing events share this stream
     sp = stream.cuda_stream
 
     def step():
@@ -130,8 +133,8 @@ def main():
     eng.debug_stats(True, read=False)
     step()
     torch.cuda.synchronize()
-    stats5 = eng.debug_stats(False)
-    alg_bytes = algorithmic_bytes(stats5, topic_bytes, n)
+    walk = dict(zip(N.Engine.STAT_NAMES, [int(x) for x in eng.debug_stats(False)]))
+    alg_bytes = algorithmic_bytes(walk, topic_bytes, n)
     eng.debug_stats(False, read=False)
 
     # ---------------------------------------------------------------- timed region
@@ -208,7 +211,7 @@ def main():
                 "kernel": "k_match_fast",
                 "kernel_ms": round(kernel_ms, 4),
                 "algorithmic_bytes_per_launch": int(alg_bytes),
-                "walk": dict(zip(N.Engine.STAT_NAMES, [int(x) for x in stats5])),
+                "walk": walk,
             },
             "cpu_baseline": cpu,
             "parity": parity,

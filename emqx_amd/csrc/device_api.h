@@ -51,7 +51,8 @@ struct MatchArgs {
     // optional walk statistics (nullptr = off): [0] node visits, [1] edge-slot
     // probes, [2] word-slot probes, [3] keys emitted, [4] topic levels,
     // [5] topics spilled, [6] key segments, [7] segment-chunk flushes,
-    // [8] frontier overflow chunks
+    // [8] frontier overflow chunks, [9] node-record reads, [10] keys emitted inline
+    // (fast kernel only for [5]-[10])
     unsigned long long *stats;
     // optional: events recorded around k_match_fast on the launch stream
     hipEvent_t ev_fast0, ev_fast1;

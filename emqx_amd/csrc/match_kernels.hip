@@ -227,7 +227,8 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     const uint32_t lane = lane_id();
     const uint32_t t = blockIdx.x * WAVE + lane;
     const bool active = t < a.n;
-    uint32_t st_visit = 0, st_probe = 0, st_wprobe = 0, st_seg = 0, st_flush = 0, st_frch = 0;
+    uint32_t st_visit = 0, st_probe = 0, st_wprobe = 0, st_seg = 0, st_flush = 0, st_frch = 0, st_rec = 0,
+             st_inl = 0;
 
     // ---- 0. stage the wave's topic bytes in LDS with 16-B coalesced loads
     const uint32_t t0 = blockIdx.x * WAVE;
@@ -362,11 +363,13 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
             NodeRec n1{0, 0, 0, 0}, n2{0, 0, 0, 0};
             if (m1 == M_REC) n1 = a.nodes[r1.child];
             if (m2 == M_REC) n2 = a.nodes[r2.child];
+            st_rec += (uint32_t)(m1 == M_REC) + (uint32_t)(m2 == M_REC);
             const bool i1 = m1 == M_INLINE && ((r1.info & I_INL_HASH) || last);
             const bool i2 = m2 == M_INLINE && ((r2.info & I_INL_HASH) || last);
             const bool s1h = n1.hash_cnt, s1t = last && n1.term_cnt;
             const bool s2h = n2.hash_cnt, s2t = last && n2.term_cnt;
             const uint32_t ns = (uint32_t)i1 + s1h + s1t + i2 + s2h + s2t;
+            st_inl += (uint32_t)i1 + (uint32_t)i2;
             uint32_t tot_s;
             uint32_t ps = wave_excl_scan(ns, &tot_s);
             if (tot_s && nseg + tot_s > (uint32_t)SCAP) {
@@ -476,7 +479,8 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
 
     if constexpr (STATS) {
         const uint64_t v0 = wave_sum64(st_visit), v1 = wave_sum64(st_probe), v2 = wave_sum64(st_wprobe),
-                       v4 = wave_sum64(nl), v5 = wave_sum64(spill ? 1u : 0u), v6 = wave_sum64(st_seg);
+                       v4 = wave_sum64(nl), v5 = wave_sum64(spill ? 1u : 0u), v6 = wave_sum64(st_seg),
+                       v9 = wave_sum64(st_rec), v10 = wave_sum64(st_inl);
         if (lane == 0) {
             atomicAdd(&a.stats[0], (unsigned long long)v0);
             atomicAdd(&a.stats[1], (unsigned long long)v1);
@@ -487,6 +491,8 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
             atomicAdd(&a.stats[6], (unsigned long long)v6);
             atomicAdd(&a.stats[7], (unsigned long long)st_flush);
             atomicAdd(&a.stats[8], (unsigned long long)st_frch);
+            atomicAdd(&a.stats[9], (unsigned long long)v9);
+            atomicAdd(&a.stats[10], (unsigned long long)v10);
         }
     }
 }
