@@ -463,7 +463,9 @@ struct tm_engine {
     }
 
     // Recompute a node's emission bits from its list (and keep its I_PLUS/I_LIT):
-    // a single key goes inline into the slot, two or more use the node record.
+    // a single key goes inline into the slot; otherwise the counts go inline and the
+    // list offset stays in the node record (M_CNT), or, for huge lists, everything
+    // stays in the node record (M_REC).
     void refresh_info(uint32_t node) {
         const NodeRec &r = node_rec[node];
         if (node == ROOT) {
@@ -478,6 +480,8 @@ struct tm_engine {
         const uint32_t n = r.term_cnt + r.hash_cnt;
         if (n == 1 && arena[r.list_off] < INLINE_KEY_LIMIT)
             info |= (M_INLINE << I_MODE_SHIFT) | (r.hash_cnt ? I_INL_HASH : 0u) | arena[r.list_off];
+        else if (n && r.term_cnt <= CNT_MAX && r.hash_cnt <= CNT_MAX)
+            info |= (M_CNT << I_MODE_SHIFT) | (r.term_cnt << CNT_BITS) | r.hash_cnt;
         else if (n)
             info |= M_REC << I_MODE_SHIFT;
         if (info != e.info) {

@@ -37,13 +37,21 @@ constexpr uint32_t ROOT = 0u;              // root node id
 constexpr uint32_t I_PLUS = 1u << 31;       // child has a '+' child
 constexpr uint32_t I_LIT = 1u << 30;        // child has at least one literal child
 constexpr uint32_t I_KIDS = I_PLUS | I_LIT;
-constexpr uint32_t I_MODE_SHIFT = 28;       // emission mode (2 bits)
-constexpr uint32_t M_NONE = 0, M_INLINE = 1, M_REC = 2;
+constexpr uint32_t I_MODE_SHIFT = 28;       // emission mode (2 bits):
+constexpr uint32_t M_NONE = 0;    //   no keys end here
+constexpr uint32_t M_INLINE = 1;  //   exactly one key, its handle inline (bits 0-26)
+constexpr uint32_t M_CNT = 2;     //   list counts inline (term 14 b | hash 14 b); the list
+                                  //   offset is read from the node record only when the
+                                  //   keys are copied out (off the walk's critical path)
+constexpr uint32_t M_REC = 3;     //   counts too large: read the node record during the walk
 constexpr uint32_t I_INL_HASH = 1u << 27;   // M_INLINE: the key is a '#' key (else exact)
 constexpr uint32_t I_KEY_MASK = (1u << 27) - 1;  // M_INLINE: the key handle
 constexpr uint32_t INLINE_KEY_LIMIT = 1u << 27;  // handles >= this never go inline
+constexpr uint32_t CNT_BITS = 14, CNT_MAX = (1u << CNT_BITS) - 1;
 
 TM_HD uint32_t info_mode(uint32_t info) { return (info >> I_MODE_SHIFT) & 3u; }
+TM_HD uint32_t info_term_cnt(uint32_t info) { return (info >> CNT_BITS) & CNT_MAX; }
+TM_HD uint32_t info_hash_cnt(uint32_t info) { return info & CNT_MAX; }
 
 struct alignas(16) EdgeSlot {
     uint32_t parent;  // NONE = empty
@@ -53,7 +61,7 @@ struct alignas(16) EdgeSlot {
 };
 static_assert(sizeof(EdgeSlot) == 16, "edge slot is 16 B");
 
-// Terminal list of a node with >= 2 keys (M_REC), indexed by node id.
+// Terminal list of a node (read for M_CNT / M_REC nodes), indexed by node id.
 struct alignas(16) NodeRec {
     uint32_t list_off;
     uint32_t term_cnt;  // keys whose filter ends exactly at the node

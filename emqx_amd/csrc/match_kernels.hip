@@ -38,7 +38,11 @@ constexpr int MAXF = 64;         // overflow chunks per frontier buffer per wave
 constexpr int SCAP = SEG_CHUNK;  // key segments staged in LDS = one global chunk
 constexpr int MAXCHUNK = 64;     // global segment chunks one wave may flush
 constexpr int TBCAP = 3072;      // topic bytes of one wave staged in LDS (else read from HBM)
-constexpr uint32_t SEG_INLINE = 1u << 8;  // segment.w flag: .x is the key itself
+constexpr uint32_t SEG_INLINE = 1u << 8;    // segment.w flag: .x is the key itself
+constexpr uint32_t SEG_NODE = 1u << 9;      // segment.w flag: .x is a node id (list offset
+                                            // from its record at copy-out time)
+constexpr uint32_t SEG_HASHPART = 1u << 10; // with SEG_NODE: the node's '#' part
+constexpr int RPL = 2;                      // frontier entries per lane per round
 
 // ---------------------------------------------------------------------------
 // wave helpers
@@ -196,7 +200,13 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
         const uint32_t j = sb + lane;
         uint32_t c = 0;
         if (j < ns) {
-            const uint4 g = L.seg[j];
+            uint4 g = L.seg[j];
+            if (g.w & SEG_NODE) {  // M_CNT list: its offset comes from the node record now
+                const NodeRec nr = a.nodes[g.x];
+                g.x = nr.list_off + ((g.w & SEG_HASHPART) ? nr.term_cnt : 0u);
+                g.w &= ~(SEG_NODE | SEG_HASHPART);
+                L.seg[j] = g;
+            }
             if (!(L.lflags[g.w & 0xFFu] & 1u)) c = g.y;
         }
         uint32_t tot;
@@ -339,37 +349,93 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
         }
         L.alive[nxt][lane] = 0;
         __syncthreads();
-        // 3b. expand the frontier, 64 entries per round
+        // 3b. expand the frontier, WAVE * RPL entries per round (RPL per lane, so each
+        //     lane has up to 2 * RPL independent probes in flight)
         uint32_t nnext = 0;
-        for (uint32_t base = 0; base < nfr; base += WAVE) {
-            const uint32_t i = base + lane;
-            const bool has = i < nfr;
-            uint32_t node = 0, tl = 0, fl = 0;
-            if (has) {
-                uint32_t meta;
-                fr_read(cur, i, node, meta);
-                tl = meta & 63u;
-                fl = (meta & 0xC0u) << 24;  // back to I_PLUS | I_LIT
+        for (uint32_t base = 0; base < nfr; base += WAVE * RPL) {
+            uint32_t tl[RPL];
+            bool last[RPL], f1[RPL], f2[RPL];
+            Rec r1[RPL], r2[RPL];
+            {
+                uint32_t node[RPL], fl[RPL], w[RPL];
+                bool has[RPL];
+#pragma unroll
+                for (int k = 0; k < RPL; k++) {
+                    const uint32_t i = base + k * WAVE + lane;
+                    has[k] = i < nfr;
+                    node[k] = 0;
+                    tl[k] = 0;
+                    fl[k] = 0;
+                    if (has[k]) {
+                        uint32_t meta;
+                        fr_read(cur, i, node[k], meta);
+                        tl[k] = meta & 63u;
+                        fl[k] = (meta & 0xC0u) << 24;  // back to I_PLUS | I_LIT
+                    }
+                    w[k] = has[k] ? L.wid[tl[k]] : NONE;
+                    last[k] = has[k] && (d + 1 == L.nlev[tl[k]]);
+                }
+                // all 2*RPL probe chains advance together
+                uint64_t s1[RPL], s2[RPL];
+                bool p1[RPL], p2[RPL];
+#pragma unroll
+                for (int k = 0; k < RPL; k++) {
+                    p1[k] = has[k] && (fl[k] & I_LIT) && w[k] != NONE;
+                    p2[k] = has[k] && (fl[k] & I_PLUS);
+                    s1[k] = edge_hash(node[k], w[k]) & a.emask;
+                    s2[k] = edge_hash(node[k], W_PLUS) & a.emask;
+                    f1[k] = f2[k] = false;
+                }
+                for (;;) {
+                    bool any = false;
+#pragma unroll
+                    for (int k = 0; k < RPL; k++) any = any || p1[k] || p2[k];
+                    if (!any) break;
+                    uint4 x1[RPL], x2[RPL];
+#pragma unroll
+                    for (int k = 0; k < RPL; k++) {
+                        x1[k] = p1[k] ? *reinterpret_cast<const uint4 *>(a.etab + s1[k]) : make_uint4(NONE, 0, 0, 0);
+                        x2[k] = p2[k] ? *reinterpret_cast<const uint4 *>(a.etab + s2[k]) : make_uint4(NONE, 0, 0, 0);
+                        st_probe += (uint32_t)p1[k] + (uint32_t)p2[k];
+                    }
+#pragma unroll
+                    for (int k = 0; k < RPL; k++) {
+                        if (p1[k]) {
+                            if (x1[k].x == NONE) p1[k] = false;
+                            else if (x1[k].x == node[k] && x1[k].y == w[k]) {
+                                r1[k] = Rec{x1[k].z, x1[k].w};
+                                f1[k] = true;
+                                p1[k] = false;
+                            } else s1[k] = (s1[k] + 1) & a.emask;
+                        }
+                        if (p2[k]) {
+                            if (x2[k].x == NONE) p2[k] = false;
+                            else if (x2[k].x == node[k] && x2[k].y == W_PLUS) {
+                                r2[k] = Rec{x2[k].z, x2[k].w};
+                                f2[k] = true;
+                                p2[k] = false;
+                            } else s2[k] = (s2[k] + 1) & a.emask;
+                        }
+                    }
+                }
             }
-            const uint32_t w = has ? L.wid[tl] : NONE;
-            const bool last = has && (d + 1 == L.nlev[tl]);
-            Rec r1{}, r2{};
-            bool f1, f2;
-            edge_probe2(a, node, has && (fl & I_LIT) && w != NONE, w, has && (fl & I_PLUS), &r1, &f1, &r2, &f2,
-                        &st_probe);
             // what each found child emits: its '#' keys always, its exact keys at the
-            // topic's last level; one key inline in the slot, more via the node record
-            const uint32_t m1 = f1 ? info_mode(r1.info) : M_NONE, m2 = f2 ? info_mode(r2.info) : M_NONE;
-            NodeRec n1{0, 0, 0, 0}, n2{0, 0, 0, 0};
-            if (m1 == M_REC) n1 = a.nodes[r1.child];
-            if (m2 == M_REC) n2 = a.nodes[r2.child];
-            st_rec += (uint32_t)(m1 == M_REC) + (uint32_t)(m2 == M_REC);
-            const bool i1 = m1 == M_INLINE && ((r1.info & I_INL_HASH) || last);
-            const bool i2 = m2 == M_INLINE && ((r2.info & I_INL_HASH) || last);
-            const bool s1h = n1.hash_cnt, s1t = last && n1.term_cnt;
-            const bool s2h = n2.hash_cnt, s2t = last && n2.term_cnt;
-            const uint32_t ns = (uint32_t)i1 + s1h + s1t + i2 + s2h + s2t;
-            st_inl += (uint32_t)i1 + (uint32_t)i2;
+            // topic's last level.  One key: inline.  Counts inline (M_CNT): a node
+            // segment resolved at copy-out.  Huge lists (M_REC): read the record now.
+            uint32_t ns = 0;
+#pragma unroll
+            for (int k = 0; k < RPL; k++) {
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    const bool f = c ? f2[k] : f1[k];
+                    const uint32_t info = c ? r2[k].info : r1[k].info;
+                    if (!f) continue;
+                    const uint32_t m = info_mode(info);
+                    if (m == M_INLINE) ns += ((info & I_INL_HASH) || last[k]);
+                    else if (m == M_CNT) ns += (info_hash_cnt(info) != 0) + (last[k] && info_term_cnt(info) != 0);
+                    else if (m == M_REC) ns += 2;  // upper bound; unused slots get cnt 0
+                }
+            }
             uint32_t tot_s;
             uint32_t ps = wave_excl_scan(ns, &tot_s);
             if (tot_s && nseg + tot_s > (uint32_t)SCAP) {
@@ -394,23 +460,45 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
             }
             ps += nseg;
             if (ns) {
-                auto put = [&](uint32_t src, uint32_t c, uint32_t fl2) {
-                    L.seg[ps++] = make_uint4(src, c, atomicAdd(&L.cnt[tl], c), tl | fl2);
-                };
-                if (i1) put(r1.info & I_KEY_MASK, 1u, SEG_INLINE);
-                if (s1t) put(n1.list_off, n1.term_cnt, 0u);
-                if (s1h) put(n1.list_off + n1.term_cnt, n1.hash_cnt, 0u);
-                if (i2) put(r2.info & I_KEY_MASK, 1u, SEG_INLINE);
-                if (s2t) put(n2.list_off, n2.term_cnt, 0u);
-                if (s2h) put(n2.list_off + n2.term_cnt, n2.hash_cnt, 0u);
+#pragma unroll
+                for (int k = 0; k < RPL; k++) {
+                    auto put = [&](uint32_t src, uint32_t cnt, uint32_t fl2) {
+                        L.seg[ps++] = make_uint4(src, cnt, cnt ? atomicAdd(&L.cnt[tl[k]], cnt) : 0u, tl[k] | fl2);
+                    };
+#pragma unroll
+                    for (int c = 0; c < 2; c++) {
+                        const bool f = c ? f2[k] : f1[k];
+                        const Rec r = c ? r2[k] : r1[k];
+                        if (!f) continue;
+                        const uint32_t m = info_mode(r.info);
+                        if (m == M_INLINE) {
+                            if ((r.info & I_INL_HASH) || last[k]) {
+                                put(r.info & I_KEY_MASK, 1u, SEG_INLINE);
+                                st_inl++;
+                            }
+                        } else if (m == M_CNT) {
+                            const uint32_t tc = info_term_cnt(r.info), hc = info_hash_cnt(r.info);
+                            if (last[k] && tc) put(r.child, tc, SEG_NODE);
+                            if (hc) put(r.child, hc, SEG_NODE | SEG_HASHPART);
+                        } else if (m == M_REC) {
+                            const NodeRec nr = a.nodes[r.child];
+                            st_rec++;
+                            put(nr.list_off, last[k] ? nr.term_cnt : 0u, 0u);
+                            put(nr.list_off + nr.term_cnt, nr.hash_cnt, 0u);
+                        }
+                    }
+                }
             }
             nseg += tot_s;
             st_seg += ns;
             // next frontier: children that can still expand
-            const bool p1 = f1 && !last && (r1.info & I_KIDS);
-            const bool p2b = f2 && !last && (r2.info & I_KIDS);
+            uint32_t np = 0;
+#pragma unroll
+            for (int k = 0; k < RPL; k++)
+                np += (uint32_t)(f1[k] && !last[k] && (r1[k].info & I_KIDS)) +
+                      (uint32_t)(f2[k] && !last[k] && (r2[k].info & I_KIDS));
             uint32_t tot_p;
-            uint32_t pp = nnext + wave_excl_scan((uint32_t)p1 + p2b, &tot_p);
+            uint32_t pp = nnext + wave_excl_scan(np, &tot_p);
             // capacity of the next buffer: LDS + overflow chunks (grown on demand)
             uint32_t cap = FCAP + nfch[nxt] * FCH;
             if (nnext + tot_p > cap && nfch[nxt] < (uint32_t)MAXF) {
@@ -425,17 +513,25 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                 __syncthreads();
                 st_frch += got;
             }
-            if (p1 || p2b) {
-                if (pp + (uint32_t)p1 + p2b <= cap) {
-                    if (p1) fr_write(nxt, pp++, r1.child, tl | ((r1.info & I_KIDS) >> 24));
-                    if (p2b) fr_write(nxt, pp, r2.child, tl | ((r2.info & I_KIDS) >> 24));
-                    atomicAdd(&L.alive[nxt][tl], (uint32_t)p1 + p2b);
+            if (np) {
+                if (pp + np <= cap) {
+#pragma unroll
+                    for (int k = 0; k < RPL; k++) {
+                        const bool q1 = f1[k] && !last[k] && (r1[k].info & I_KIDS);
+                        const bool q2 = f2[k] && !last[k] && (r2[k].info & I_KIDS);
+                        if (q1) fr_write(nxt, pp++, r1[k].child, tl[k] | ((r1[k].info & I_KIDS) >> 24));
+                        if (q2) fr_write(nxt, pp++, r2[k].child, tl[k] | ((r2[k].info & I_KIDS) >> 24));
+                        if (q1 || q2) atomicAdd(&L.alive[nxt][tl[k]], (uint32_t)q1 + (uint32_t)q2);
+                    }
                 } else {
-                    atomicOr(&L.lflags[tl], 1u);  // frontier overflow: topic spills
+#pragma unroll
+                    for (int k = 0; k < RPL; k++)  // frontier overflow: those topics spill
+                        if ((f1[k] || f2[k]) && !last[k]) atomicOr(&L.lflags[tl[k]], 1u);
                 }
             }
             nnext = min(nnext + tot_p, cap);
-            st_visit += (uint32_t)f1 + f2;
+#pragma unroll
+            for (int k = 0; k < RPL; k++) st_visit += (uint32_t)f1[k] + (uint32_t)f2[k];
         }
         __syncthreads();
         nfr = nnext;
@@ -522,7 +618,7 @@ __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_
             node = x.z;
             info = x.w;
             const uint32_t m = info_mode(info);
-            if (m == M_REC) {
+            if (m == M_REC || m == M_CNT) {
                 const NodeRec nr = a.nodes[node];
                 lo = nr.list_off;
                 tc = nr.term_cnt;
