@@ -438,7 +438,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
             }
             uint32_t tot_s;
             uint32_t ps = wave_excl_scan(ns, &tot_s);
-            if (tot_s && nseg + tot_s > (uint32_t)SCAP) {
+            if (tot_s && nseg && nseg + tot_s > (uint32_t)SCAP) {
                 // flush the staged segments to one global chunk
                 __syncthreads();
                 uint32_t c = 0;
@@ -458,12 +458,37 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                 nseg = 0;
                 __syncthreads();
             }
-            ps += nseg;
+            // a round that emits more than the staging buffer holds writes its segments
+            // straight into freshly reserved global chunks (wave-uniform decision)
+            const bool direct = tot_s > (uint32_t)SCAP;
+            uint32_t dc0 = 0;
+            bool dok = true;
+            if (direct) {
+                const uint32_t ndc = (tot_s + SCAP - 1) / SCAP;
+                unsigned long long c0 = 0;
+                if (lane == 0) c0 = atomicAdd(a.seg_cursor, (unsigned long long)ndc);
+                c0 = __shfl(c0, 0, WAVE);
+                dok = c0 + ndc <= a.seg_chunks && nchunk + ndc <= (uint32_t)MAXCHUNK;
+                dc0 = (uint32_t)c0;
+                if (dok) {
+                    if (lane < ndc) L.chunk[nchunk + lane] = dc0 + lane;
+                    for (uint32_t j = tot_s + lane; j < ndc * SCAP; j += WAVE)  // pad the last chunk
+                        a.seg_pool[(uint64_t)dc0 * SCAP + j] = make_uint4(0u, 0u, 0u, 0u);
+                    nchunk += ndc;
+                    st_flush += ndc;
+                }
+            } else {
+                ps += nseg;
+            }
             if (ns) {
 #pragma unroll
                 for (int k = 0; k < RPL; k++) {
                     auto put = [&](uint32_t src, uint32_t cnt, uint32_t fl2) {
-                        L.seg[ps++] = make_uint4(src, cnt, cnt ? atomicAdd(&L.cnt[tl[k]], cnt) : 0u, tl[k] | fl2);
+                        const uint4 g = make_uint4(src, cnt, cnt ? atomicAdd(&L.cnt[tl[k]], cnt) : 0u, tl[k] | fl2);
+                        if (!direct) L.seg[ps] = g;
+                        else if (dok) a.seg_pool[(uint64_t)dc0 * SCAP + ps] = g;
+                        else atomicOr(&L.lflags[tl[k]], 1u);  // pool exhausted: topic spills
+                        ps++;
                     };
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
@@ -489,7 +514,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                     }
                 }
             }
-            nseg += tot_s;
+            nseg = direct ? 0u : nseg + tot_s;
             st_seg += ns;
             // next frontier: children that can still expand
             uint32_t np = 0;
