@@ -25,7 +25,7 @@ struct MatchArgs {
     const uint32_t *word_off;  // arena offset of each word (long-word verification)
     const EdgeSlot *etab;
     uint64_t emask;
-    const NodeRec *nodes;      // terminal lists of nodes with >= 2 keys
+    const uint32_t *slot_list; // node (= slot) -> first key of its list in the arena
     const RootRec *root;
     const uint32_t *arena;
     // results
@@ -63,7 +63,8 @@ struct MatchArgs {
 // kernel handed off.  Asynchronous.
 hipError_t launch_match(const MatchArgs &a, hipStream_t stream);
 
-// Delta-epoch patches of 16-byte records: dst[idx[i]] = src[i].
+// Delta-epoch patches: dst[idx[i]] = src[i] (16-byte records / u32 entries).
 hipError_t launch_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n, hipStream_t stream);
+hipError_t launch_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *src, uint64_t n, hipStream_t stream);
 
 }  // namespace tmx

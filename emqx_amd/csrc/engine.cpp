@@ -130,7 +130,9 @@ struct tm_engine {
     uint64_t emask = 0;
     uint64_t n_edges = 0;
     std::vector<uint32_t> node_parent, node_word, node_slot;
-    std::vector<NodeRec> node_rec;  // terminal list of every node (device copy: d_nodes)
+    std::vector<NodeList> node_list;  // terminal list of every node (host numbering)
+    std::vector<uint32_t> slot_node;  // slot -> host node (NONE for empty slots)
+    std::vector<uint32_t> slot_list;  // slot -> first key of the node's list (device copy)
     RootRec root{0, 0, 0, 0};
 
     // ---- terminal-list arena
@@ -152,13 +154,13 @@ struct tm_engine {
     std::vector<uint8_t> stage_bytes;
     std::vector<std::pair<uint32_t, uint32_t>> lv_scratch;  // classify(): (start, len) per level
     std::vector<Delta> deltas;
-    std::vector<uint64_t> dirty_eslots, dirty_wslots, dirty_nodes;
+    std::vector<uint64_t> dirty_eslots, dirty_wslots, dirty_lists;
     bool root_dirty = true;
     bool need_full = true;  // full device upload at next commit
 
     // ---- device copy
-    DevBuf d_wtab, d_warena, d_word_off, d_etab, d_nodes, d_root, d_arena;
-    size_t word_off_dev = 0, nodes_dev = 0;  // entries already on device
+    DevBuf d_wtab, d_warena, d_word_off, d_etab, d_slot_list, d_root, d_arena;
+    size_t word_off_dev = 0;  // entries already on device
     DevBuf d_scatter_idx, d_scatter_src;
     // batch buffers
     DevBuf d_bytes, d_off, d_outoff, d_outcnt, d_status, d_keys, d_cursor, d_slow_list,
@@ -228,68 +230,79 @@ struct tm_engine {
     }
 
     // =====================================================================
-    // edges
-    uint64_t edge_find(uint32_t parent, uint32_t word) const {
-        uint64_t s = edge_hash(parent, word) & emask;
+    // edges.  Host nodes are numbered in creation order (a parent before its
+    // children); on the device a node is the index of its edge slot.
+    uint32_t dev_id(uint32_t node) const { return node == ROOT ? ROOT_ID : node_slot[node]; }
+    uint64_t edge_find(uint32_t parent_dev, uint32_t word) const {
+        uint64_t s = edge_hash(parent_dev, word) & emask;
         for (;;) {
             const EdgeSlot &e = etab[s];
             if (e.parent == NONE) return ~0ull;
-            if (e.parent == parent && e.word == word) return s;
+            if (e.parent == parent_dev && e.word == word) return s;
             s = (s + 1) & emask;
         }
     }
+    uint64_t edge_place(uint32_t parent_dev, uint32_t word) const {
+        uint64_t s = edge_hash(parent_dev, word) & emask;
+        while (etab[s].parent != NONE) s = (s + 1) & emask;
+        return s;
+    }
+    // Re-place every node: slot positions hash the parent's slot, so nodes go in in
+    // creation order (parents first).  Node ids on the device change: full upload.
     void edge_rehash(uint64_t cap) {
         std::vector<EdgeSlot> old;
         old.swap(etab);
-        EdgeSlot empty{};
-        empty.parent = NONE;
+        EdgeSlot empty{NONE, 0, 0, 0};
         etab.assign(cap, empty);
         emask = cap - 1;
-        for (const EdgeSlot &e : old)
-            if (e.parent != NONE) {
-                uint64_t s = edge_hash(e.parent, e.word) & emask;
-                while (etab[s].parent != NONE) s = (s + 1) & emask;
-                etab[s] = e;
-                node_slot[e.child] = (uint32_t)s;
-            }
+        std::vector<uint32_t> old_list;
+        old_list.swap(slot_list);
+        slot_list.assign(cap, 0);
+        slot_node.assign(cap, NONE);
+        for (size_t v = 1; v < node_parent.size(); v++) {
+            const uint32_t os = node_slot[v];
+            const uint32_t pd = dev_id(node_parent[v]);
+            const uint64_t ns = edge_place(pd, node_word[v]);
+            etab[ns] = EdgeSlot{pd, node_word[v], old[os].bloom, old[os].info};
+            slot_list[ns] = old_list[os];
+            slot_node[ns] = (uint32_t)v;
+            node_slot[v] = (uint32_t)ns;
+        }
         need_full = true;
     }
-    void node_set_flag(uint32_t node, uint32_t f) {
+    void node_set_flag(uint32_t node, uint32_t f, uint32_t bloom) {
         if (node == ROOT) {
-            if ((root.info & f) != f) {
+            if ((root.info & f) != f || (root.bloom & bloom) != bloom) {
                 root.info |= f;
+                root.bloom |= bloom;
                 root_dirty = true;
             }
             return;
         }
         EdgeSlot &e = etab[node_slot[node]];
-        if ((e.info & f) != f) {
+        if ((e.info & f) != f || (e.bloom & bloom) != bloom) {
             e.info |= f;
+            e.bloom |= bloom;
             dirty_eslots.push_back(node_slot[node]);
         }
     }
     uint32_t edge_child(uint32_t parent, uint32_t word) {
-        uint64_t s = edge_find(parent, word);
-        if (s != ~0ull) return etab[s].child;
-        if ((n_edges + 1) * 2 > etab.size()) {
-            edge_rehash(etab.size() * 2);
-        }
-        uint32_t child = (uint32_t)node_parent.size();
+        uint64_t s = edge_find(dev_id(parent), word);
+        if (s != ~0ull) return slot_node[s];
+        if ((n_edges + 1) * 2 > etab.size()) edge_rehash(etab.size() * 2);
+        const uint32_t child = (uint32_t)node_parent.size();
         node_parent.push_back(parent);
         node_word.push_back(word);
         node_slot.push_back(NONE);
-        node_rec.push_back(NodeRec{0, 0, 0, 0});
-        s = edge_hash(parent, word) & emask;
-        while (etab[s].parent != NONE) s = (s + 1) & emask;
-        EdgeSlot e{};
-        e.parent = parent;
-        e.word = word;
-        e.child = child;
-        etab[s] = e;
+        node_list.push_back(NodeList{0, 0, 0});
+        const uint32_t pd = dev_id(parent);
+        s = edge_place(pd, word);
+        etab[s] = EdgeSlot{pd, word, 0, 0};
+        slot_node[s] = child;
         node_slot[child] = (uint32_t)s;
         n_edges++;
         dirty_eslots.push_back(s);
-        node_set_flag(parent, word == W_PLUS ? I_PLUS : I_LIT);
+        node_set_flag(parent, word == W_PLUS ? I_PLUS : I_LIT, word == W_PLUS ? 0u : bloom_bit(word));
         return child;
     }
 
@@ -403,9 +416,9 @@ struct tm_engine {
             if (create) {
                 node = edge_child(node, w);
             } else {
-                uint64_t s = edge_find(node, w);
+                uint64_t s = edge_find(dev_id(node), w);
                 if (s == ~0ull) return false;
-                node = etab[s].child;
+                node = slot_node[s];
             }
         }
         *kind_out = kind;
@@ -464,18 +477,18 @@ struct tm_engine {
 
     // Recompute a node's emission bits from its list (and keep its I_PLUS/I_LIT):
     // a single key goes inline into the slot; otherwise the counts go inline and the
-    // list offset stays in the node record (M_CNT), or, for huge lists, everything
-    // stays in the node record (M_REC).
+    // list offset stays in slot_list (M_CNT), or, for huge lists, the walk reads the
+    // counts from the list header (M_REC).
     void refresh_info(uint32_t node) {
-        const NodeRec &r = node_rec[node];
+        const NodeList &r = node_list[node];
         if (node == ROOT) {
             root.list_off = r.list_off;
-            root.term_cnt = r.term_cnt;
             root.hash_cnt = r.hash_cnt;
             root_dirty = true;
             return;
         }
-        EdgeSlot &e = etab[node_slot[node]];
+        const uint32_t sl = node_slot[node];
+        EdgeSlot &e = etab[sl];
         uint32_t info = e.info & I_KIDS;
         const uint32_t n = r.term_cnt + r.hash_cnt;
         if (n == 1 && arena[r.list_off] < INLINE_KEY_LIMIT)
@@ -486,12 +499,28 @@ struct tm_engine {
             info |= M_REC << I_MODE_SHIFT;
         if (info != e.info) {
             e.info = info;
-            dirty_eslots.push_back(node_slot[node]);
+            if (!need_full) dirty_eslots.push_back(sl);
         }
+        if (slot_list[sl] != r.list_off) {
+            slot_list[sl] = r.list_off;
+            if (!need_full) dirty_lists.push_back(sl);
+        }
+    }
+
+    // Append one list ([term_cnt, hash_cnt] header, term keys, hash keys) to the arena.
+    NodeList append_list(const uint32_t *terms, uint32_t tc, const uint32_t *hashes, uint32_t hc) {
+        if (tc + hc == 0) return NodeList{0, 0, 0};
+        arena.push_back(tc);
+        arena.push_back(hc);
+        const uint32_t off = (uint32_t)arena.size();
+        arena.insert(arena.end(), terms, terms + tc);
+        arena.insert(arena.end(), hashes, hashes + hc);
+        return NodeList{off, tc, hc};
     }
 
     // Rebuild the whole arena from the key table (counting sort by node).
     void rebuild_arena() {
+        need_full = true;  // everything is re-uploaded: no dirty tracking
         size_t nn = node_parent.size();
         std::vector<uint32_t> tcnt(nn, 0), hcnt(nn, 0);
         for (size_t h = 0; h < keys.size(); h++) {
@@ -503,12 +532,19 @@ struct tm_engine {
         std::vector<uint32_t> pos(nn);
         uint64_t total = 0;
         for (size_t v = 0; v < nn; v++) {
-            pos[v] = (uint32_t)total;
-            total += tcnt[v] + hcnt[v];
+            const uint32_t n = tcnt[v] + hcnt[v];
+            pos[v] = n ? (uint32_t)(total + 2) : 0u;
+            total += n ? n + 2 : 0;
         }
         arena.assign(total, 0);
         std::vector<uint32_t> tfill(pos), hfill(nn);
-        for (size_t v = 0; v < nn; v++) hfill[v] = pos[v] + tcnt[v];
+        for (size_t v = 0; v < nn; v++) {
+            hfill[v] = pos[v] + tcnt[v];
+            if (pos[v]) {
+                arena[pos[v] - 2] = tcnt[v];
+                arena[pos[v] - 1] = hcnt[v];
+            }
+        }
         for (size_t h = 0; h < keys.size(); h++) {
             const KeyRec &k = keys[h];
             if (k.kind == K_FREE || k.kind == K_DEAD) continue;
@@ -516,7 +552,7 @@ struct tm_engine {
             else arena[tfill[k.node]++] = (uint32_t)h;
         }
         for (size_t v = 0; v < nn; v++) {
-            node_rec[v] = NodeRec{(tcnt[v] + hcnt[v]) ? pos[v] : 0u, tcnt[v], hcnt[v], 0u};
+            node_list[v] = NodeList{pos[v], tcnt[v], hcnt[v]};
             refresh_info((uint32_t)v);
         }
         arena_garbage = 0;
@@ -533,7 +569,7 @@ struct tm_engine {
             size_t j = i;
             uint32_t node = deltas[i].node;
             while (j < deltas.size() && deltas[j].node == node) j++;
-            NodeRec &r = node_rec[node];
+            const NodeList r = node_list[node];
             terms.assign(arena.begin() + r.list_off, arena.begin() + r.list_off + r.term_cnt);
             hashes.assign(arena.begin() + r.list_off + r.term_cnt,
                           arena.begin() + r.list_off + r.term_cnt + r.hash_cnt);
@@ -546,12 +582,8 @@ struct tm_engine {
                     if (it != Lst.end()) Lst.erase(it);
                 }
             }
-            arena_garbage += r.term_cnt + r.hash_cnt;
-            uint32_t off = (uint32_t)arena.size();
-            arena.insert(arena.end(), terms.begin(), terms.end());
-            arena.insert(arena.end(), hashes.begin(), hashes.end());
-            r = NodeRec{(terms.size() + hashes.size()) ? off : 0u, (uint32_t)terms.size(), (uint32_t)hashes.size(), 0u};
-            dirty_nodes.push_back(node);
+            arena_garbage += r.term_cnt + r.hash_cnt + (r.term_cnt + r.hash_cnt ? 2 : 0);
+            node_list[node] = append_list(terms.data(), (uint32_t)terms.size(), hashes.data(), (uint32_t)hashes.size());
             refresh_info(node);
             i = j;
         }
@@ -582,8 +614,7 @@ struct tm_engine {
         if ((e = put(d_word_off, word_off))) return e;
         word_off_dev = word_off.size();
         if ((e = put(d_etab, etab, 1, 1))) return e;
-        if ((e = put(d_nodes, node_rec))) return e;
-        nodes_dev = node_rec.size();
+        if ((e = put(d_slot_list, slot_list, 1, 1))) return e;
         if ((e = put(d_arena, arena))) return e;
         arena_dev = arena.size();
         if ((e = d_root.ensure(sizeof(RootRec)))) return e;
@@ -613,19 +644,38 @@ struct tm_engine {
         return hipStreamSynchronize(stream);  // src dies at scope exit
     }
 
+    // dst[idx[i]] = src[i] for u32 entries (slot_list)
+    hipError_t scatter4(std::vector<uint64_t> &dirty, const std::vector<uint32_t> &tab, void *dtab) {
+        if (dirty.empty()) return hipSuccess;
+        std::sort(dirty.begin(), dirty.end());
+        dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+        size_t n = dirty.size();
+        std::vector<uint32_t> src(n);
+        for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
+        hipError_t e;
+        if ((e = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e;
+        if ((e = d_scatter_src.ensure(n * 4))) return e;
+        if ((e = hipMemcpyAsync(d_scatter_idx.p, dirty.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, stream)))
+            return e;
+        if ((e = hipMemcpyAsync(d_scatter_src.p, src.data(), n * 4, hipMemcpyHostToDevice, stream))) return e;
+        if ((e = launch_scatter4((uint32_t *)dtab, d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint32_t>(), n,
+                                 stream)))
+            return e;
+        return hipStreamSynchronize(stream);
+    }
+
     hipError_t upload_delta() {
         hipError_t e;
         // arrays that only grow: append the tail, or re-upload everything when full
         if (warena.size() > d_warena.cap || arena.size() * sizeof(uint32_t) > d_arena.cap ||
-            word_off.size() * sizeof(uint32_t) > d_word_off.cap || node_rec.size() * sizeof(NodeRec) > d_nodes.cap)
+            word_off.size() * sizeof(uint32_t) > d_word_off.cap)
             return upload_full();
         if ((e = put_tail(d_warena, warena, warena_dev))) return e;
         if ((e = put_tail(d_word_off, word_off, word_off_dev))) return e;
         if ((e = put_tail(d_arena, arena, arena_dev))) return e;
-        if ((e = put_tail(d_nodes, node_rec, nodes_dev))) return e;
         if ((e = scatter16(dirty_wslots, wtab, d_wtab.p))) return e;
         if ((e = scatter16(dirty_eslots, etab, d_etab.p))) return e;
-        if ((e = scatter16(dirty_nodes, node_rec, d_nodes.p))) return e;
+        if ((e = scatter4(dirty_lists, slot_list, d_slot_list.p))) return e;
         if (root_dirty) {
             if ((e = hipMemcpyAsync(d_root.p, &root, sizeof(RootRec), hipMemcpyHostToDevice, stream))) return e;
         }
@@ -655,7 +705,7 @@ struct tm_engine {
         root_dirty = false;
         dirty_eslots.clear();
         dirty_wslots.clear();
-        dirty_nodes.clear();
+        dirty_lists.clear();
         for (uint32_t h : free_pending) free_keys.push_back(h);
         free_pending.clear();
         epoch++;
@@ -773,8 +823,8 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     eng->node_parent.push_back(NONE);  // root
     eng->node_word.push_back(NONE);
     eng->node_slot.push_back(NONE);
-    eng->node_rec.reserve(rn);
-    eng->node_rec.push_back(NodeRec{0, 0, 0, 0});
+    eng->node_list.reserve(rn);
+    eng->node_list.push_back(NodeList{0, 0, 0});
     eng->edge_rehash(next_pow2(std::max<uint64_t>(rn * 2, 1024)));
     eng->kset_rehash(next_pow2(std::max<uint64_t>(rk * 2, 1024)));
     eng->keys.reserve(rk);
@@ -792,7 +842,7 @@ void tm_destroy(tm_engine *eng) {
     if (!eng) return;
     (void)hipSetDevice(eng->cfg.device);
     if (eng->stream) (void)hipStreamSynchronize(eng->stream);
-    for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_nodes, &eng->d_root,
+    for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
                       &eng->d_arena, &eng->d_scatter_idx,
                       &eng->d_scatter_src, &eng->d_bytes, &eng->d_off, &eng->d_outoff, &eng->d_outcnt,
                       &eng->d_status, &eng->d_keys, &eng->d_cursor, &eng->d_slow_list, &eng->d_slow_count,
@@ -920,7 +970,7 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.warena = eng->d_warena.as<uint8_t>();
     a.word_off = eng->d_word_off.as<uint32_t>();
     a.etab = eng->d_etab.as<EdgeSlot>();
-    a.nodes = eng->d_nodes.as<NodeRec>();
+    a.slot_list = eng->d_slot_list.as<uint32_t>();
     a.emask = eng->emask;
     a.root = eng->d_root.as<RootRec>();
     a.arena = eng->d_arena.as<uint32_t>();
@@ -1150,7 +1200,7 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
     out->word_slots = eng->wtab.size();
     out->list_words = eng->arena.size();
     out->device_bytes = eng->d_wtab.cap + eng->d_warena.cap + eng->d_word_off.cap + eng->d_etab.cap +
-                        eng->d_nodes.cap + eng->d_arena.cap + eng->d_root.cap;
+                        eng->d_slot_list.cap + eng->d_arena.cap + eng->d_root.cap;
     out->n_full_rebuilds = eng->n_full_rebuilds;
     out->n_delta_commits = eng->n_delta_commits;
     out->n_slow_topics = eng->n_slow_last;

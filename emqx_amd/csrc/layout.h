@@ -7,13 +7,17 @@
 // open-addressed hash table keyed by (parent node, level-word id):
 //
 //   word table  : level-word bytes  -> word id    (tokeniser, one probe per topic level)
-//   edge table  : (parent, word id) -> child      (walk, one probe per frontier node/level)
-//   node records: child -> terminal list          (only nodes with >= 2 keys)
-//   list arena  : u32 key handles; a node's exact-terminal keys followed by its
-//                 '#'-child keys ("filter/#" hangs off the node of "filter").
+//   edge table  : (parent, word id) -> slot       (walk, one probe per frontier node/level)
+//   slot lists  : slot -> offset of the node's terminal list in the arena
+//   list arena  : u32 key handles; per list a 2-word header [term_cnt, hash_cnt], then
+//                 the exact-terminal keys, then the '#'-child keys ("filter/#" hangs
+//                 off the node of "filter").
 //
-// A 16-byte edge slot carries the child's expansion flags and, when the child has
-// exactly one key, that key inline: most probes are one 16-B read with nothing
+// A node IS the index of the edge slot that leads to it (the root is ROOT_ID), so a
+// slot needs no child field.  Its 16 bytes carry the key (parent, word), a 32-bit
+// bloom of the node's literal child words (a lookup the bloom rules out is never
+// issued: it would only miss), and the node's expansion flags plus, when the node
+// has one key, that key inline: most probes are one 16-B read with nothing
 // dependent behind them.  '+' edges are ordinary edges with word id W_PLUS.  '#'
 // never becomes a node.  A filter whose '#' is not the last level can never match
 // (emqx_topic.erl:99-101 only accepts a final '#'; emqx_trie_search.erl:282-290
@@ -31,7 +35,8 @@ namespace tmx {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;     // empty slot / missing node / unknown word
 constexpr uint32_t W_PLUS = 0xFFFFFFFEu;   // '+' edge label
-constexpr uint32_t ROOT = 0u;              // root node id
+constexpr uint32_t ROOT = 0u;              // root node id (host numbering)
+constexpr uint32_t ROOT_ID = 0xFFFFFFFDu;  // the root as a parent in device edge keys
 
 // EdgeSlot.info: what the CHILD node the slot leads to does
 constexpr uint32_t I_PLUS = 1u << 31;       // child has a '+' child
@@ -54,27 +59,29 @@ TM_HD uint32_t info_term_cnt(uint32_t info) { return (info >> CNT_BITS) & CNT_MA
 TM_HD uint32_t info_hash_cnt(uint32_t info) { return info & CNT_MAX; }
 
 struct alignas(16) EdgeSlot {
-    uint32_t parent;  // NONE = empty
+    uint32_t parent;  // the parent's slot index (ROOT_ID for the root); NONE = empty
     uint32_t word;    // literal word id or W_PLUS
-    uint32_t child;   // child node id
-    uint32_t info;    // I_* of the child
+    uint32_t bloom;   // bloom_bit() of every literal child word of this node
+    uint32_t info;    // I_* of this node
 };
 static_assert(sizeof(EdgeSlot) == 16, "edge slot is 16 B");
 
-// Terminal list of a node (read for M_CNT / M_REC nodes), indexed by node id.
-struct alignas(16) NodeRec {
-    uint32_t list_off;
-    uint32_t term_cnt;  // keys whose filter ends exactly at the node
-    uint32_t hash_cnt;  // keys of "node-path/#" (follow the term keys)
-    uint32_t _pad;
-};
+// One bit of a node's 32-bit child-word bloom (k = 1).
+TM_HD uint32_t bloom_bit(uint32_t word) { return 1u << ((word * 0x9E3779B1u) >> 27); }
 
 // Root record (the root has no incoming edge; no filter ends at it).
 struct alignas(16) RootRec {
     uint32_t info;      // I_PLUS | I_LIT
-    uint32_t list_off;
-    uint32_t term_cnt;  // always 0
+    uint32_t bloom;     // literal child words of the root
+    uint32_t list_off;  // first key of the "#" list
     uint32_t hash_cnt;  // keys of "#"
+};
+
+// Host-side terminal list of a node (host node numbering).
+struct NodeList {
+    uint32_t list_off;  // first key (the 2-word header sits just before it)
+    uint32_t term_cnt;  // keys whose filter ends exactly at the node
+    uint32_t hash_cnt;  // keys of "node-path/#" (follow the term keys)
 };
 
 // 16-byte word slot.  Words of up to 8 bytes are their own key (the bytes, zero

@@ -39,9 +39,11 @@ constexpr int SCAP = SEG_CHUNK;  // key segments staged in LDS = one global chun
 constexpr int MAXCHUNK = 64;     // global segment chunks one wave may flush
 constexpr int TBCAP = 3072;      // topic bytes of one wave staged in LDS (else read from HBM)
 constexpr uint32_t SEG_INLINE = 1u << 8;    // segment.w flag: .x is the key itself
-constexpr uint32_t SEG_NODE = 1u << 9;      // segment.w flag: .x is a node id (list offset
-                                            // from its record at copy-out time)
-constexpr uint32_t SEG_HASHPART = 1u << 10; // with SEG_NODE: the node's '#' part
+constexpr uint32_t SEG_NODE = 1u << 9;      // segment.w flag: .x is a node (slot); its list
+                                            // offset is read from slot_list at copy-out
+constexpr uint32_t SEG_SKIP_SHIFT = 11;     // with SEG_NODE: keys to skip (term_cnt for the
+                                            // '#' part) in .w bits 11-31
+constexpr uint32_t DO_PLUS = 0x80u, DO_LIT = 0x40u;  // frontier meta: probes this entry needs
 constexpr int RPL = 2;                      // frontier entries per lane per round
 
 // ---------------------------------------------------------------------------
@@ -107,63 +109,31 @@ __device__ __forceinline__ uint64_t level_key(uint32_t *i, uint32_t e, ByteAt &&
     return n <= 8 ? w8 : h;
 }
 
-// edge table: (parent, word) -> 16-byte slot
+// edge table: (parent, word) -> 16-byte slot; the child node IS the slot index
 struct Rec {
-    uint32_t child, info;
+    uint32_t child, bloom, info;
 };
-__device__ __forceinline__ uint64_t edge_probe(const MatchArgs &a, uint32_t parent, uint32_t word, Rec *r,
-                                               uint32_t *probes) {
+__device__ __forceinline__ bool edge_probe(const MatchArgs &a, uint32_t parent, uint32_t word, Rec *r,
+                                           uint32_t *probes) {
     uint64_t s = edge_hash(parent, word) & a.emask;
     for (;;) {
         const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + s);
         (*probes)++;
-        if (x.x == NONE) return ~0ull;
+        if (x.x == NONE) return false;
         if (x.x == parent && x.y == word) {
-            r->child = x.z;
-            r->info = x.w;
-            return s;
+            *r = Rec{(uint32_t)s, x.z, x.w};
+            return true;
         }
         s = (s + 1) & a.emask;
     }
 }
 
-// Probe (parent, word) and (parent, '+') together: both loads are in flight before
-// either result is consumed (the two chains are independent).
-__device__ __forceinline__ void edge_probe2(const MatchArgs &a, uint32_t parent, bool want1, uint32_t word,
-                                            bool want2, Rec *r1, bool *f1, Rec *r2, bool *f2, uint32_t *probes) {
-    uint64_t s1 = edge_hash(parent, word) & a.emask;
-    uint64_t s2 = edge_hash(parent, W_PLUS) & a.emask;
-    bool p1 = want1, p2 = want2;
-    *f1 = false;
-    *f2 = false;
-    while (p1 || p2) {
-        uint4 x1 = make_uint4(NONE, 0, 0, 0), x2 = x1;
-        if (p1) x1 = *reinterpret_cast<const uint4 *>(a.etab + s1);
-        if (p2) x2 = *reinterpret_cast<const uint4 *>(a.etab + s2);
-        *probes += (uint32_t)p1 + (uint32_t)p2;
-        if (p1) {
-            if (x1.x == NONE) {
-                p1 = false;
-            } else if (x1.x == parent && x1.y == word) {
-                *r1 = Rec{x1.z, x1.w};
-                *f1 = true;
-                p1 = false;
-            } else {
-                s1 = (s1 + 1) & a.emask;
-            }
-        }
-        if (p2) {
-            if (x2.x == NONE) {
-                p2 = false;
-            } else if (x2.x == parent && x2.y == W_PLUS) {
-                *r2 = Rec{x2.z, x2.w};
-                *f2 = true;
-                p2 = false;
-            } else {
-                s2 = (s2 + 1) & a.emask;
-            }
-        }
-    }
+// Which probes a node at depth d needs for the topic's level-d word w: the '+' child
+// if it has one; the literal child only if the child-word bloom admits w.
+__device__ __forceinline__ uint32_t probes_needed(uint32_t info, uint32_t bloom, uint32_t w) {
+    uint32_t m = (info & I_PLUS) ? DO_PLUS : 0u;
+    if ((info & I_LIT) && w != NONE && (bloom & bloom_bit(w))) m |= DO_LIT;
+    return m;
 }
 
 // ---------------------------------------------------------------------------
@@ -177,13 +147,13 @@ __device__ __forceinline__ void edge_probe2(const MatchArgs &a, uint32_t parent,
 struct WaveLds {
     uint8_t tb[TBCAP];            // the wave's topic bytes (16-B aligned window)
     uint32_t fr_node[2][FCAP];
-    uint8_t fr_meta[2][FCAP];     // topic lane | node I_KIDS bits >> 24
+    uint8_t fr_meta[2][FCAP];     // topic lane | DO_PLUS / DO_LIT
     uint32_t fch[2][MAXF];        // global overflow chunks of each frontier buffer
     uint4 seg[SCAP];              // {src or key, cnt, rel, topic lane | SEG_INLINE}
     uint32_t seg_scan[SCAP + 1];
     uint32_t chunk[MAXCHUNK];
     uint32_t cur[WAVE];    // byte offset where the topic's next level starts
-    uint32_t wid[WAVE];    // word id of the level being expanded
+    uint32_t wid[2][WAVE]; // word id of level d (wid[d&1]) and of level d+1 (tokenised ahead)
     uint32_t nlev[WAVE];
     uint32_t cnt[WAVE];    // keys matched so far (allocates each segment's rel)
     uint32_t tbase[WAVE];  // output base of the topic
@@ -201,10 +171,9 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
         uint32_t c = 0;
         if (j < ns) {
             uint4 g = L.seg[j];
-            if (g.w & SEG_NODE) {  // M_CNT list: its offset comes from the node record now
-                const NodeRec nr = a.nodes[g.x];
-                g.x = nr.list_off + ((g.w & SEG_HASHPART) ? nr.term_cnt : 0u);
-                g.w &= ~(SEG_NODE | SEG_HASHPART);
+            if (g.w & SEG_NODE) {  // M_CNT list: its offset is read now, off the walk
+                g.x = a.slot_list[g.x] + (g.w >> SEG_SKIP_SHIFT);
+                g.w &= 0xFFu | SEG_INLINE;
                 L.seg[j] = g;
             }
             if (!(L.lflags[g.w & 0xFFu] & 1u)) c = g.y;
@@ -285,8 +254,18 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     L.alive[0][lane] = 0;
     L.alive[1][lane] = 0;
 
+    // tokenise one level of this lane's topic (the cursor walks left to right)
+    auto tokenize_next = [&](uint32_t slot) {
+        uint32_t i = L.cur[lane];
+        const uint32_t st = i;
+        const uint64_t key = level_key(&i, e, byte_at);
+        L.wid[slot][lane] = word_lookup(a, key, i - st, st, byte_at, &st_wprobe);
+        L.cur[lane] = i + 1;
+    };
+
     // ---- 2. root: emit "#" keys (not for '$' topics), seed the frontier
     const RootRec R = *a.root;
+    if (walk) tokenize_next(0);  // level 0
     uint32_t nseg = 0, nchunk = 0;  // wave-uniform
     uint32_t nfr;
     {
@@ -294,17 +273,17 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
         uint32_t tot;
         const uint32_t pos = wave_excl_scan(em ? 1u : 0u, &tot);
         if (em) {
-            L.seg[pos] = make_uint4(R.list_off + R.term_cnt, R.hash_cnt, 0u, lane);
+            L.seg[pos] = make_uint4(R.list_off, R.hash_cnt, 0u, lane);
             L.cnt[lane] = R.hash_cnt;
         }
         nseg = tot;
         st_seg += em;
-        const uint32_t rf = dollar ? (R.info & I_LIT) : (R.info & I_KIDS);
-        const bool push = walk && rf;
-        const uint32_t p2 = wave_excl_scan(push ? 1u : 0u, &tot);
-        if (push) {
-            L.fr_node[0][p2] = ROOT;
-            L.fr_meta[0][p2] = (uint8_t)(lane | (rf >> 24));
+        const uint32_t rinfo = dollar ? (R.info & I_LIT) : R.info;  // '$' topics: no root '+'
+        const uint32_t m = walk ? probes_needed(rinfo, R.bloom, L.wid[0][lane]) : 0u;
+        const uint32_t p2 = wave_excl_scan(m ? 1u : 0u, &tot);
+        if (m) {
+            L.fr_node[0][p2] = ROOT_ID;
+            L.fr_meta[0][p2] = (uint8_t)(lane | m);
             L.alive[0][lane] = 1;
             st_visit++;
         }
@@ -339,14 +318,9 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     // ---- 3. level-synchronous walk
     for (uint32_t d = 0; nfr > 0; ++d) {
         const uint32_t cur = d & 1, nxt = cur ^ 1;
-        // 3a. tokenise level d of every topic that still has frontier entries
-        if (walk && L.alive[cur][lane]) {
-            uint32_t i = L.cur[lane];
-            const uint32_t st = i;
-            const uint64_t key = level_key(&i, e, byte_at);
-            L.wid[lane] = word_lookup(a, key, i - st, st, byte_at, &st_wprobe);
-            L.cur[lane] = i + 1;
-        }
+        // 3a. tokenise level d+1 ahead for topics that are still alive and go deeper:
+        //     the children pushed at this depth are filtered with it (bloom)
+        if (walk && L.alive[cur][lane] && d + 1 < nl) tokenize_next(nxt);
         L.alive[nxt][lane] = 0;
         __syncthreads();
         // 3b. expand the frontier, WAVE * RPL entries per round (RPL per lane, so each
@@ -357,35 +331,26 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
             bool last[RPL], f1[RPL], f2[RPL];
             Rec r1[RPL], r2[RPL];
             {
-                uint32_t node[RPL], fl[RPL], w[RPL];
-                bool has[RPL];
+                uint32_t node[RPL], w[RPL];
+                bool p1[RPL], p2[RPL];
+                uint64_t s1[RPL], s2[RPL];
 #pragma unroll
                 for (int k = 0; k < RPL; k++) {
                     const uint32_t i = base + k * WAVE + lane;
-                    has[k] = i < nfr;
+                    const bool has = i < nfr;
+                    uint32_t meta = 0;
                     node[k] = 0;
-                    tl[k] = 0;
-                    fl[k] = 0;
-                    if (has[k]) {
-                        uint32_t meta;
-                        fr_read(cur, i, node[k], meta);
-                        tl[k] = meta & 63u;
-                        fl[k] = (meta & 0xC0u) << 24;  // back to I_PLUS | I_LIT
-                    }
-                    w[k] = has[k] ? L.wid[tl[k]] : NONE;
-                    last[k] = has[k] && (d + 1 == L.nlev[tl[k]]);
-                }
-                // all 2*RPL probe chains advance together
-                uint64_t s1[RPL], s2[RPL];
-                bool p1[RPL], p2[RPL];
-#pragma unroll
-                for (int k = 0; k < RPL; k++) {
-                    p1[k] = has[k] && (fl[k] & I_LIT) && w[k] != NONE;
-                    p2[k] = has[k] && (fl[k] & I_PLUS);
+                    if (has) fr_read(cur, i, node[k], meta);
+                    tl[k] = meta & 63u;
+                    w[k] = has ? L.wid[cur][tl[k]] : NONE;
+                    last[k] = has && (d + 1 == L.nlev[tl[k]]);
+                    p1[k] = has && (meta & DO_LIT);
+                    p2[k] = has && (meta & DO_PLUS);
                     s1[k] = edge_hash(node[k], w[k]) & a.emask;
                     s2[k] = edge_hash(node[k], W_PLUS) & a.emask;
                     f1[k] = f2[k] = false;
                 }
+                // all 2*RPL probe chains advance together
                 for (;;) {
                     bool any = false;
 #pragma unroll
@@ -403,7 +368,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                         if (p1[k]) {
                             if (x1[k].x == NONE) p1[k] = false;
                             else if (x1[k].x == node[k] && x1[k].y == w[k]) {
-                                r1[k] = Rec{x1[k].z, x1[k].w};
+                                r1[k] = Rec{(uint32_t)s1[k], x1[k].z, x1[k].w};
                                 f1[k] = true;
                                 p1[k] = false;
                             } else s1[k] = (s1[k] + 1) & a.emask;
@@ -411,7 +376,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                         if (p2[k]) {
                             if (x2[k].x == NONE) p2[k] = false;
                             else if (x2[k].x == node[k] && x2[k].y == W_PLUS) {
-                                r2[k] = Rec{x2[k].z, x2[k].w};
+                                r2[k] = Rec{(uint32_t)s2[k], x2[k].z, x2[k].w};
                                 f2[k] = true;
                                 p2[k] = false;
                             } else s2[k] = (s2[k] + 1) & a.emask;
@@ -421,7 +386,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
             }
             // what each found child emits: its '#' keys always, its exact keys at the
             // topic's last level.  One key: inline.  Counts inline (M_CNT): a node
-            // segment resolved at copy-out.  Huge lists (M_REC): read the record now.
+            // segment resolved at copy-out.  Huge lists (M_REC): read the header now.
             uint32_t ns = 0;
 #pragma unroll
             for (int k = 0; k < RPL; k++) {
@@ -433,7 +398,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                     const uint32_t m = info_mode(info);
                     if (m == M_INLINE) ns += ((info & I_INL_HASH) || last[k]);
                     else if (m == M_CNT) ns += (info_hash_cnt(info) != 0) + (last[k] && info_term_cnt(info) != 0);
-                    else if (m == M_REC) ns += 2;  // upper bound; unused slots get cnt 0
+                    else if (m == M_REC) ns += 2;  // upper bound; an unused one gets cnt 0
                 }
             }
             uint32_t tot_s;
@@ -504,24 +469,29 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                         } else if (m == M_CNT) {
                             const uint32_t tc = info_term_cnt(r.info), hc = info_hash_cnt(r.info);
                             if (last[k] && tc) put(r.child, tc, SEG_NODE);
-                            if (hc) put(r.child, hc, SEG_NODE | SEG_HASHPART);
+                            if (hc) put(r.child, hc, SEG_NODE | (tc << SEG_SKIP_SHIFT));
                         } else if (m == M_REC) {
-                            const NodeRec nr = a.nodes[r.child];
+                            const uint32_t lo = a.slot_list[r.child];
+                            const uint32_t tc = a.arena[lo - 2], hc = a.arena[lo - 1];
                             st_rec++;
-                            put(nr.list_off, last[k] ? nr.term_cnt : 0u, 0u);
-                            put(nr.list_off + nr.term_cnt, nr.hash_cnt, 0u);
+                            put(lo, last[k] ? tc : 0u, 0u);
+                            put(lo + tc, hc, 0u);
                         }
                     }
                 }
             }
             nseg = direct ? 0u : nseg + tot_s;
             st_seg += ns;
-            // next frontier: children that can still expand
+            // next frontier: children that still need a probe for level d+1
+            uint32_t q1[RPL], q2[RPL];
             uint32_t np = 0;
 #pragma unroll
-            for (int k = 0; k < RPL; k++)
-                np += (uint32_t)(f1[k] && !last[k] && (r1[k].info & I_KIDS)) +
-                      (uint32_t)(f2[k] && !last[k] && (r2[k].info & I_KIDS));
+            for (int k = 0; k < RPL; k++) {
+                const uint32_t wn = last[k] ? NONE : L.wid[nxt][tl[k]];
+                q1[k] = (f1[k] && !last[k]) ? probes_needed(r1[k].info, r1[k].bloom, wn) : 0u;
+                q2[k] = (f2[k] && !last[k]) ? probes_needed(r2[k].info, r2[k].bloom, wn) : 0u;
+                np += (uint32_t)(q1[k] != 0) + (uint32_t)(q2[k] != 0);
+            }
             uint32_t tot_p;
             uint32_t pp = nnext + wave_excl_scan(np, &tot_p);
             // capacity of the next buffer: LDS + overflow chunks (grown on demand)
@@ -542,16 +512,14 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                 if (pp + np <= cap) {
 #pragma unroll
                     for (int k = 0; k < RPL; k++) {
-                        const bool q1 = f1[k] && !last[k] && (r1[k].info & I_KIDS);
-                        const bool q2 = f2[k] && !last[k] && (r2[k].info & I_KIDS);
-                        if (q1) fr_write(nxt, pp++, r1[k].child, tl[k] | ((r1[k].info & I_KIDS) >> 24));
-                        if (q2) fr_write(nxt, pp++, r2[k].child, tl[k] | ((r2[k].info & I_KIDS) >> 24));
-                        if (q1 || q2) atomicAdd(&L.alive[nxt][tl[k]], (uint32_t)q1 + (uint32_t)q2);
+                        if (q1[k]) fr_write(nxt, pp++, r1[k].child, tl[k] | q1[k]);
+                        if (q2[k]) fr_write(nxt, pp++, r2[k].child, tl[k] | q2[k]);
+                        if (q1[k] || q2[k]) atomicAdd(&L.alive[nxt][tl[k]], (uint32_t)(q1[k] != 0) + (q2[k] != 0));
                     }
                 } else {
 #pragma unroll
                     for (int k = 0; k < RPL; k++)  // frontier overflow: those topics spill
-                        if ((f1[k] || f2[k]) && !last[k]) atomicOr(&L.lflags[tl[k]], 1u);
+                        if (q1[k] || q2[k]) atomicOr(&L.lflags[tl[k]], 1u);
                 }
             }
             nnext = min(nnext + tot_p, cap);
@@ -632,22 +600,23 @@ __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_
         const uint64_t ent = stk[--sp];
         const uint64_t slot = ent >> 24;
         const uint32_t d = (uint32_t)(ent & 0xFFFFFF);
-        uint32_t node, info, lo = 0, tc = 0, hc = 0;
+        uint32_t node, info, bloom, lo = 0, tc = 0, hc = 0;
         if (slot == ROOT_MARK) {
-            node = ROOT;
+            node = ROOT_ID;
             info = dollar ? (R.info & I_LIT) : R.info;
+            bloom = R.bloom;
             lo = R.list_off;
             hc = dollar ? 0 : R.hash_cnt;
         } else {
             const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + slot);
-            node = x.z;
+            node = (uint32_t)slot;
+            bloom = x.z;
             info = x.w;
             const uint32_t m = info_mode(info);
             if (m == M_REC || m == M_CNT) {
-                const NodeRec nr = a.nodes[node];
-                lo = nr.list_off;
-                tc = nr.term_cnt;
-                hc = nr.hash_cnt;
+                lo = a.slot_list[node];
+                tc = a.arena[lo - 2];
+                hc = a.arena[lo - 1];
             } else if (m == M_INLINE && ((info & I_INL_HASH) || d == nl)) {
                 // the node's only key, inline in the slot
                 if (WRITE) out[count] = info & I_KEY_MASK;
@@ -665,16 +634,10 @@ __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_
             count += tc;
             continue;
         }
+        const uint32_t need = probes_needed(info, bloom, wid[d]);
         Rec r;
-        if (info & I_PLUS) {
-            uint64_t s = edge_probe(a, node, W_PLUS, &r, probes);
-            if (s != ~0ull) stk[sp++] = (s << 24) | (d + 1);
-        }
-        const uint32_t w = wid[d];
-        if ((info & I_LIT) && w != NONE) {
-            uint64_t s = edge_probe(a, node, w, &r, probes);
-            if (s != ~0ull) stk[sp++] = (s << 24) | (d + 1);
-        }
+        if ((need & DO_PLUS) && edge_probe(a, node, W_PLUS, &r, probes)) stk[sp++] = ((uint64_t)r.child << 24) | (d + 1);
+        if ((need & DO_LIT) && edge_probe(a, node, wid[d], &r, probes)) stk[sp++] = ((uint64_t)r.child << 24) | (d + 1);
     }
     return count;
 }
@@ -724,9 +687,20 @@ __global__ void k_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, u
     if (i < n) dst[idx[i]] = src[i];
 }
 
+__global__ void k_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *src, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[idx[i]] = src[i];
+}
+
 hipError_t launch_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n, hipStream_t s) {
     if (!n) return hipSuccess;
     k_scatter16<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *src, uint64_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    k_scatter4<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
     return hipGetLastError();
 }
 
