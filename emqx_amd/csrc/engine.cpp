@@ -105,6 +105,10 @@ struct PinBuf {
     template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
+// Edge table load <= 1/EDGE_LOAD_INV.  A wave waits for the longest of its ~256
+// concurrent probe chains, so short chains (low load) matter more than table size.
+constexpr uint64_t EDGE_LOAD_INV = 4;
+
 inline uint64_t next_pow2(uint64_t x) {
     uint64_t p = 1;
     while (p < x) p <<= 1;
@@ -289,7 +293,7 @@ struct tm_engine {
     uint32_t edge_child(uint32_t parent, uint32_t word) {
         uint64_t s = edge_find(dev_id(parent), word);
         if (s != ~0ull) return slot_node[s];
-        if ((n_edges + 1) * 2 > etab.size()) edge_rehash(etab.size() * 2);
+        if ((n_edges + 1) * EDGE_LOAD_INV > etab.size()) edge_rehash(etab.size() * 2);
         const uint32_t child = (uint32_t)node_parent.size();
         node_parent.push_back(parent);
         node_word.push_back(word);
@@ -825,7 +829,7 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     eng->node_slot.push_back(NONE);
     eng->node_list.reserve(rn);
     eng->node_list.push_back(NodeList{0, 0, 0});
-    eng->edge_rehash(next_pow2(std::max<uint64_t>(rn * 2, 1024)));
+    eng->edge_rehash(next_pow2(std::max<uint64_t>(rn * EDGE_LOAD_INV, 1024)));
     eng->kset_rehash(next_pow2(std::max<uint64_t>(rk * 2, 1024)));
     eng->keys.reserve(rk);
     eng->need_full = true;
