@@ -45,6 +45,7 @@ constexpr uint32_t SEG_SKIP_SHIFT = 11;     // with SEG_NODE: keys to skip (term
                                             // '#' part) in .w bits 11-31
 constexpr uint32_t DO_PLUS = 0x80u, DO_LIT = 0x40u;  // frontier meta: probes this entry needs
 constexpr int RPL = 2;                      // frontier entries per lane per round
+constexpr int CP_UNROLL = 8;                // arena loads in flight per lane at copy-out
 
 // ---------------------------------------------------------------------------
 // wave helpers
@@ -185,17 +186,38 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
     }
     if (lane == 0) L.seg_scan[ns] = run;
     __syncthreads();
-    for (uint32_t e = lane; e < run; e += WAVE) {
-        uint32_t lo = 0, hi = ns;  // seg_scan[lo] <= e < seg_scan[hi]
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (L.seg_scan[mid] <= e) lo = mid;
+    if (run == 0) return;
+    // Element e of the flattened list lives in the last segment j with seg_scan[j] <= e.
+    // One binary search per lane, then the lane's segment cursor only moves forward
+    // (its next element is 64 further on); CP_UNROLL independent arena loads are in
+    // flight per lane before any store.
+    uint32_t j = 0;
+    {
+        uint32_t hi = ns;  // seg_scan[j] <= e < seg_scan[hi]
+        const uint32_t e = min(lane, run - 1);
+        while (hi - j > 1) {
+            const uint32_t mid = (j + hi) >> 1;
+            if (L.seg_scan[mid] <= e) j = mid;
             else hi = mid;
         }
-        const uint4 g = L.seg[lo];
-        const uint32_t k = e - L.seg_scan[lo];
-        const uint32_t key = (g.w & SEG_INLINE) ? g.x : a.arena[g.x + k];
-        a.keys[L.tbase[g.w & 0xFFu] + g.z + k] = key;
+    }
+    for (uint32_t e0 = lane; e0 < run; e0 += WAVE * CP_UNROLL) {
+        uint32_t key[CP_UNROLL], dst[CP_UNROLL];
+#pragma unroll
+        for (int u = 0; u < CP_UNROLL; u++) {
+            const uint32_t e = e0 + u * WAVE;
+            dst[u] = NONE;
+            if (e < run) {
+                while (L.seg_scan[j + 1] <= e) j++;
+                const uint4 g = L.seg[j];
+                const uint32_t k = e - L.seg_scan[j];
+                dst[u] = L.tbase[g.w & 0xFFu] + g.z + k;
+                key[u] = (g.w & SEG_INLINE) ? g.x : a.arena[g.x + k];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < CP_UNROLL; u++)
+            if (dst[u] != NONE) a.keys[dst[u]] = key[u];
     }
     __syncthreads();
 }
