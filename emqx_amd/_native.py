@@ -271,10 +271,11 @@ class Engine:
         return {n: getattr(s, n) for n, _ in tm_stats_t._fields_}
 
     STAT_NAMES = ("node_visits", "edge_probes", "word_probes", "keys", "levels", "spilled_topics",
-                  "segments", "chunk_flushes", "frontier_chunks", "node_records", "inline_keys")
+                  "segments", "chunk_flushes", "frontier_chunks", "node_records", "inline_keys",
+                  "cyc_prescan", "cyc_walk", "cyc_copyout")
 
     def debug_stats(self, enable: bool, read: bool = True):
-        out = (C.c_uint64 * 11)()
+        out = (C.c_uint64 * 14)()
         self._check(self.lib.tm_debug_stats(self.h, 1 if enable else 0, out if read else None))
         return list(out) if read else None
 

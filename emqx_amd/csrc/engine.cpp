@@ -1215,13 +1215,13 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
 // Enable per-batch walk statistics (node visits, edge probes, word probes, keys,
 // levels, spilled topics, segments, chunk flushes), accumulated on the device
 // across batches until read.
-int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out11) {
+int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out14) {
     if (!eng) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     TM_TRY_HIP(eng->d_stats.ensure(128), TM_ENOMEM, "alloc");
-    if (out11) {
+    if (out14) {
         TM_TRY_HIP(hipDeviceSynchronize(), TM_EDEVICE, "sync");
-        TM_TRY_HIP(hipMemcpy(out11, eng->d_stats.p, 88, hipMemcpyDeviceToHost), TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipMemcpy(out14, eng->d_stats.p, 112, hipMemcpyDeviceToHost), TM_EDEVICE, "D2H");
     }
     TM_TRY_HIP(hipMemset(eng->d_stats.p, 0, 128), TM_EDEVICE, "memset");
     eng->stats_on = enable != 0;

@@ -230,6 +230,9 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     const bool active = t < a.n;
     uint32_t st_visit = 0, st_probe = 0, st_wprobe = 0, st_seg = 0, st_flush = 0, st_frch = 0, st_rec = 0,
              st_inl = 0;
+    // STATS build only: phase stamps (shares of wave time, not absolute kernel time)
+    uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
+    if constexpr (STATS) ts0 = __builtin_amdgcn_s_memtime();
 
     // ---- 0. stage the wave's topic bytes in LDS with 16-B coalesced loads
     const uint32_t t0 = blockIdx.x * WAVE;
@@ -337,6 +340,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
         }
     };
 
+    if constexpr (STATS) ts1 = __builtin_amdgcn_s_memtime();
     // ---- 3. level-synchronous walk
     for (uint32_t d = 0; nfr > 0; ++d) {
         const uint32_t cur = d & 1, nxt = cur ^ 1;
@@ -552,6 +556,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
         nfr = nnext;
     }
 
+    if constexpr (STATS) ts2 = __builtin_amdgcn_s_memtime();
     // ---- 4. reserve this wave's output with one atomic; per-topic results
     const bool spill = active && !badarg && (L.lflags[lane] & 1u);
     const uint32_t my = (walk && !spill) ? L.cnt[lane] : 0u;
@@ -589,6 +594,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     }
 
     if constexpr (STATS) {
+        ts3 = __builtin_amdgcn_s_memtime();
         const uint64_t v0 = wave_sum64(st_visit), v1 = wave_sum64(st_probe), v2 = wave_sum64(st_wprobe),
                        v4 = wave_sum64(nl), v5 = wave_sum64(spill ? 1u : 0u), v6 = wave_sum64(st_seg),
                        v9 = wave_sum64(st_rec), v10 = wave_sum64(st_inl);
@@ -604,6 +610,9 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
             atomicAdd(&a.stats[8], (unsigned long long)st_frch);
             atomicAdd(&a.stats[9], (unsigned long long)v9);
             atomicAdd(&a.stats[10], (unsigned long long)v10);
+            atomicAdd(&a.stats[11], (unsigned long long)(ts1 - ts0));  // stage + pre-scan + root
+            atomicAdd(&a.stats[12], (unsigned long long)(ts2 - ts1));  // walk
+            atomicAdd(&a.stats[13], (unsigned long long)(ts3 - ts2));  // reserve + copy-out
         }
     }
 }

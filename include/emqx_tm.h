@@ -185,12 +185,13 @@ int tm_key_info(const tm_engine *eng, uint32_t key, uint64_t *id, uint32_t *flag
 int tm_key_ids(const tm_engine *eng, const uint32_t *keys, size_t n, uint64_t *ids_out);
 int tm_stats(const tm_engine *eng, tm_stats_t *out);
 
-/* diagnostics: enable/disable device walk counters; when out11 != NULL, first
+/* diagnostics: enable/disable device walk counters; when out14 != NULL, first
  * read the counters accumulated since the last call: {node visits, edge-slot
  * probes, word-slot probes, keys emitted, topic levels, topics spilled to the
  * slow kernel, key segments, segment-chunk flushes, frontier overflow chunks,
- * node-record reads, keys emitted inline from edge slots}. */
-int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out11);
+ * list-header reads, keys emitted inline from edge slots, and the summed wave
+ * cycles of the fast kernel's phases: stage+pre-scan, walk, copy-out}. */
+int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out14);
 /* diagnostics: time the dominant kernel of the next match with HIP events on its
  * launch stream; enable=1 arms, then (after the match) enable=0 + ms_out reads. */
 int tm_debug_timing(tm_engine *eng, int enable, float *ms_out);
