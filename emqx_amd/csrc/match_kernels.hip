@@ -45,7 +45,8 @@ constexpr uint32_t SEG_SKIP_SHIFT = 11;     // with SEG_NODE: keys to skip (term
                                             // '#' part) in .w bits 11-31
 constexpr uint32_t DO_PLUS = 0x80u, DO_LIT = 0x40u;  // frontier meta: probes this entry needs
 constexpr int RPL = 2;                      // frontier entries per lane per round
-constexpr int CP_UNROLL = 8;                // arena loads in flight per lane at copy-out
+constexpr int CP_UNROLL = 8;                // arena loads in flight per lane, long lists
+constexpr int CP_SHORT = 8;                 // lists up to this long are copied by one lane
 
 // ---------------------------------------------------------------------------
 // wave helpers
@@ -162,62 +163,62 @@ struct WaveLds {
     uint32_t alive[2][WAVE];  // frontier entries per topic at this / the next depth
 };
 
-// Expand L.seg[0..ns) into the output (all lanes busy: element e of the flattened
-// segment list is found by binary search over the segment prefix sums).
+// Expand L.seg[0..ns) into the output.  Short segments (<= CP_SHORT keys, most of them
+// single inline keys) are copied by the lane that holds them; long ones (hot '#'
+// filters with thousands of subscribers) are queued and copied by the whole wave, 64
+// consecutive keys per instruction, CP_UNROLL instructions in flight.
 __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, uint32_t ns) {
     const uint32_t lane = lane_id();
-    uint32_t run = 0;
+    uint32_t nlong = 0;  // wave-uniform; long segment indices are queued in L.seg_scan
     for (uint32_t sb = 0; sb < ns; sb += WAVE) {
         const uint32_t j = sb + lane;
-        uint32_t c = 0;
+        uint4 g = make_uint4(0u, 0u, 0u, 0u);
         if (j < ns) {
-            uint4 g = L.seg[j];
+            g = L.seg[j];
             if (g.w & SEG_NODE) {  // M_CNT list: its offset is read now, off the walk
                 g.x = a.slot_list[g.x] + (g.w >> SEG_SKIP_SHIFT);
                 g.w &= 0xFFu | SEG_INLINE;
                 L.seg[j] = g;
             }
-            if (!(L.lflags[g.w & 0xFFu] & 1u)) c = g.y;
+            if (L.lflags[g.w & 0xFFu] & 1u) g.y = 0;  // spilled topic: the slow kernel owns it
         }
-        uint32_t tot;
-        const uint32_t ex = wave_excl_scan(c, &tot);
-        if (j < ns) L.seg_scan[j] = run + ex;
-        run += tot;
-    }
-    if (lane == 0) L.seg_scan[ns] = run;
-    __syncthreads();
-    if (run == 0) return;
-    // Element e of the flattened list lives in the last segment j with seg_scan[j] <= e.
-    // One binary search per lane, then the lane's segment cursor only moves forward
-    // (its next element is 64 further on); CP_UNROLL independent arena loads are in
-    // flight per lane before any store.
-    uint32_t j = 0;
-    {
-        uint32_t hi = ns;  // seg_scan[j] <= e < seg_scan[hi]
-        const uint32_t e = min(lane, run - 1);
-        while (hi - j > 1) {
-            const uint32_t mid = (j + hi) >> 1;
-            if (L.seg_scan[mid] <= e) j = mid;
-            else hi = mid;
-        }
-    }
-    for (uint32_t e0 = lane; e0 < run; e0 += WAVE * CP_UNROLL) {
-        uint32_t key[CP_UNROLL], dst[CP_UNROLL];
+        const bool is_long = g.y > (uint32_t)CP_SHORT;
+        if (!is_long && g.y) {
+            const uint32_t dst = L.tbase[g.w & 0xFFu] + g.z;
+            if (g.w & SEG_INLINE) {
+                a.keys[dst] = g.x;
+            } else {
+                uint32_t key[CP_SHORT];
 #pragma unroll
-        for (int u = 0; u < CP_UNROLL; u++) {
-            const uint32_t e = e0 + u * WAVE;
-            dst[u] = NONE;
-            if (e < run) {
-                while (L.seg_scan[j + 1] <= e) j++;
-                const uint4 g = L.seg[j];
-                const uint32_t k = e - L.seg_scan[j];
-                dst[u] = L.tbase[g.w & 0xFFu] + g.z + k;
-                key[u] = (g.w & SEG_INLINE) ? g.x : a.arena[g.x + k];
+                for (int k = 0; k < CP_SHORT; k++)
+                    if ((uint32_t)k < g.y) key[k] = a.arena[g.x + k];
+#pragma unroll
+                for (int k = 0; k < CP_SHORT; k++)
+                    if ((uint32_t)k < g.y) a.keys[dst + k] = key[k];
             }
         }
+        uint32_t tot;
+        const uint32_t q = nlong + wave_excl_scan(is_long ? 1u : 0u, &tot);
+        if (is_long) L.seg_scan[q] = j;
+        nlong += tot;
+    }
+    __syncthreads();
+    for (uint32_t q = 0; q < nlong; q++) {
+        const uint4 g = L.seg[L.seg_scan[q]];
+        const uint32_t dst = L.tbase[g.w & 0xFFu] + g.z;
+        for (uint32_t k0 = lane; k0 < g.y; k0 += WAVE * CP_UNROLL) {
+            uint32_t key[CP_UNROLL];
 #pragma unroll
-        for (int u = 0; u < CP_UNROLL; u++)
-            if (dst[u] != NONE) a.keys[dst[u]] = key[u];
+            for (int u = 0; u < CP_UNROLL; u++) {
+                const uint32_t k = k0 + u * WAVE;
+                if (k < g.y) key[u] = a.arena[g.x + k];
+            }
+#pragma unroll
+            for (int u = 0; u < CP_UNROLL; u++) {
+                const uint32_t k = k0 + u * WAVE;
+                if (k < g.y) a.keys[dst + k] = key[u];
+            }
+        }
     }
     __syncthreads();
 }
