@@ -34,6 +34,10 @@ def per_kernel(path, kernel=KERNEL):
 
 def main(src, dst):
     out = {"source": src}
+    sha = os.path.join(src, "src.sha")
+    if os.path.exists(sha):
+        import hashlib
+        out["kernel_src_sha"] = hashlib.sha256(open(sha, "rb").read()).hexdigest()
     stats_csv = os.path.join(src, "trace", "trace_kernel_stats.csv")
     rows = list(csv.DictReader(open(stats_csv)))
     out["kernel_stats"] = [{k: r[k] for k in ("Name", "Calls", "AverageNs", "Percentage", "MinNs", "MaxNs")}
