@@ -4,6 +4,9 @@ The product path is the HIP library and nothing else: if the library is missing,
 or the process has no gfx950 device, engine creation raises.  There is no CPU
 fallback (the CPU restatement of the reference lives in oracle/ and is test
 infrastructure only).
+
+A process that also uses torch on the GPU must import torch BEFORE this library is loaded:
+torch bundles its own libamdhip64.so.7 and the first HIP runtime loaded serves the process.
 """
 from __future__ import annotations
 
@@ -13,7 +16,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libemqx_tm.so")
+# EMQX_TM_LIB: path of an alternative build of the same library (kernel-parameter sweeps
+# by tools/variants.py); unset = the in-tree product build.
+LIB_PATH = os.environ.get("EMQX_TM_LIB") or os.path.join(HERE, "libemqx_tm.so")
 
 TM_OK = 0
 TM_EINVAL = -1
@@ -40,6 +45,7 @@ EXPORTS = (
     "tm_abi_version", "tm_create", "tm_destroy", "tm_last_error", "tm_apply", "tm_apply_packed",
     "tm_commit_epoch", "tm_match_batch", "tm_match_device", "tm_device_sync",
     "tm_reserve_matches", "tm_key_info", "tm_key_ids", "tm_stats", "tm_debug_stats", "tm_debug_timing",
+    "tm_result_ids_device", "tm_merge_shards_device", "tm_merge_shards",
 )
 
 
@@ -48,7 +54,7 @@ class tm_config(C.Structure):
         ("device", C.c_int32), ("flags", C.c_uint32),
         ("reserve_keys", C.c_uint32), ("reserve_nodes", C.c_uint32),
         ("reserve_topics", C.c_uint32), ("reserve_matches", C.c_uint32),
-        ("seg_chunks", C.c_uint32), ("reserved", C.c_uint32 * 3),
+        ("seg_chunks", C.c_uint32), ("edge_load_inv", C.c_uint32), ("reserved", C.c_uint32 * 2),
     ]
 
 
@@ -117,11 +123,34 @@ def load() -> C.CDLL:
     lib.tm_stats.argtypes = [C.c_void_p, P(tm_stats_t)]
     lib.tm_debug_timing.argtypes = [C.c_void_p, C.c_int, P(C.c_float)]
     lib.tm_debug_stats.argtypes = [C.c_void_p, C.c_int, P(C.c_uint64)]
+    lib.tm_result_ids_device.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    lib.tm_merge_shards_device.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64,
+                                           C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+    lib.tm_merge_shards.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                    C.c_void_p, C.c_uint64]
     for name in EXPORTS:
         if name not in ("tm_destroy", "tm_last_error", "tm_abi_version"):
             getattr(lib, name).restype = C.c_int
     _lib = lib
     return lib
+
+
+def merge_shards(counts: np.ndarray, ids: np.ndarray):
+    """Host form of the shard merge (tm_merge_shards): counts [G, n] u32, ids [G, stride]
+    u64 (shard r's topic-major ids) -> (off[n+1] u32, merged ids u64)."""
+    lib = load()
+    counts = np.ascontiguousarray(counts, dtype=np.uint32)
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    G, n = counts.shape
+    stride = ids.shape[1] if ids.ndim == 2 else 0
+    total = int(counts.sum(dtype=np.uint64))
+    off = np.zeros(n + 1, dtype=np.uint32)
+    out = np.zeros(max(total, 1), dtype=np.uint64)
+    rc = lib.tm_merge_shards(G, n, counts.ctypes.data, ids.ctypes.data, stride, off.ctypes.data, out.ctypes.data,
+                             total)
+    if rc != TM_OK:
+        raise TMError(rc, "tm_merge_shards failed")
+    return off, out[:total]
 
 
 class TMError(RuntimeError):
@@ -144,7 +173,7 @@ class Engine:
     """One engine = one GPU.  Thin owner of a tm_engine*."""
 
     def __init__(self, device: int = 0, *, force_slow: bool = False, reserve_keys: int = 0,
-                 reserve_nodes: int = 0, reserve_matches: int = 0, seg_chunks: int = 0):
+                 reserve_nodes: int = 0, reserve_matches: int = 0, seg_chunks: int = 0, edge_load_inv: int = 0):
         self.lib = load()
         cfg = tm_config()
         cfg.device = device
@@ -153,6 +182,7 @@ class Engine:
         cfg.reserve_nodes = reserve_nodes
         cfg.reserve_matches = reserve_matches
         cfg.seg_chunks = seg_chunks
+        cfg.edge_load_inv = edge_load_inv or int(os.environ.get("EMQX_TM_EDGE_LOAD_INV", "0"))
         h = C.c_void_p()
         rc = self.lib.tm_create(C.byref(cfg), C.byref(h))
         if rc != TM_OK:
@@ -285,6 +315,17 @@ class Engine:
         self._check(self.lib.tm_match_device(self.h, C.c_void_p(d_bytes), C.c_void_p(d_off), n, total_bytes,
                                              C.c_void_p(stream) if stream else None, C.byref(r)))
         return r
+
+    def result_ids_device(self, d_ids: int, ids_cap: int, d_off: int, stream: int = 0):
+        """Route ids of the last batch, topic-major, into device buffers (d_off: n+1 u32)."""
+        self._check(self.lib.tm_result_ids_device(self.h, C.c_void_p(d_ids), ids_cap, C.c_void_p(d_off),
+                                                  C.c_void_p(stream) if stream else None))
+
+    def merge_shards_device(self, G: int, n: int, d_counts: int, d_ids: int, stride: int, d_out_off: int,
+                            d_out_ids: int, out_cap: int, stream: int = 0):
+        self._check(self.lib.tm_merge_shards_device(self.h, G, n, C.c_void_p(d_counts), C.c_void_p(d_ids), stride,
+                                                    C.c_void_p(d_out_off), C.c_void_p(d_out_ids), out_cap,
+                                                    C.c_void_p(stream) if stream else None))
 
     def device_sync(self):
         self._check(self.lib.tm_device_sync(self.h))

@@ -9,6 +9,7 @@
 namespace tmx {
 
 constexpr int SEG_CHUNK = 128;  // key segments per global chunk (16 B each)
+constexpr int SEG_MAXCHUNK = 128;  // segment chunks one wave may flush (its list lives in HBM)
 constexpr int FR_CHUNK = 256;   // frontier entries per global overflow chunk (8 B each)
 
 // Everything one match launch needs.  Device pointers only.
@@ -44,6 +45,7 @@ struct MatchArgs {
     uint4 *seg_pool;
     uint64_t seg_chunks;
     unsigned long long *seg_cursor;  // chunks requested (may exceed seg_chunks)
+    uint32_t *wave_chunks;           // SEG_MAXCHUNK chunk indices per wave (grid * SEG_MAXCHUNK)
     // frontier overflow pool: fr_chunks chunks of FR_CHUNK uint2 {node, meta}
     uint2 *fr_pool;
     uint64_t fr_chunks;
@@ -66,5 +68,23 @@ hipError_t launch_match(const MatchArgs &a, hipStream_t stream);
 // Delta-epoch patches: dst[idx[i]] = src[i] (16-byte records / u32 entries).
 hipError_t launch_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n, hipStream_t stream);
 hipError_t launch_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *src, uint64_t n, hipStream_t stream);
+
+// result_kernels.hip --------------------------------------------------------
+// Exclusive scan of n u32 values (in[i * in_stride]) into out[0..n]; out[n] = total.
+// scratch: scan_scratch_words(n) u32.
+uint64_t scan_scratch_words(uint32_t n);
+hipError_t launch_excl_scan(const uint32_t *in, uint64_t in_stride, uint32_t n, uint32_t *out, uint32_t *scratch,
+                            hipStream_t stream);
+// ids[dst_off[t] + k] = key_id[keys[src_off[t] + k]] for k < cnt[t] (topics whose range
+// would pass `cap` are skipped).
+hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
+                             const uint64_t *key_id, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
+                             uint64_t cap, hipStream_t stream);
+// Concatenate G shards' topic-major results per topic.  roff: G*(n+1) u32, tot: n u32,
+// scratch: scan_scratch_words(n) u32 (work areas); off: n+1 u32 out; out: merged ids.
+hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,
+                               uint32_t *roff, uint32_t *tot, uint32_t *scratch, uint32_t *off, uint64_t *out,
+                               uint64_t cap, hipStream_t stream);
+hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, hipStream_t stream);
 
 }  // namespace tmx

@@ -107,7 +107,9 @@ struct PinBuf {
 
 // Edge table load <= 1/EDGE_LOAD_INV.  A wave waits for the longest of its ~256
 // concurrent probe chains, so short chains (low load) matter more than table size.
-constexpr uint64_t EDGE_LOAD_INV = 4;
+constexpr uint64_t EDGE_LOAD_INV = 8;
+// Word table load <= 1/WORD_LOAD_INV (small: it sizes with the vocabulary, not the nodes).
+constexpr uint64_t WORD_LOAD_INV = 4;
 
 inline uint64_t next_pow2(uint64_t x) {
     uint64_t p = 1;
@@ -166,18 +168,24 @@ struct tm_engine {
     DevBuf d_wtab, d_warena, d_word_off, d_etab, d_slot_list, d_root, d_arena;
     size_t word_off_dev = 0;  // entries already on device
     DevBuf d_scatter_idx, d_scatter_src;
+    DevBuf d_key_id;                  // key handle -> caller id (u64), for device-side id results
+    std::vector<uint64_t> dirty_kid;  // handles (re)assigned since the last upload
+    DevBuf d_res_scan, d_mrg_roff, d_mrg_tot;  // scratch of tm_result_ids_device / tm_merge_shards_device
     // batch buffers
     DevBuf d_bytes, d_off, d_outoff, d_outcnt, d_status, d_keys, d_cursor, d_slow_list,
-        d_slow_count, d_scr_w, d_scr_s, d_stats, d_seg_pool, d_seg_cursor, d_fr_pool, d_fr_cursor;
+        d_slow_count, d_scr_w, d_scr_s, d_stats, d_seg_pool, d_seg_cursor, d_fr_pool, d_fr_cursor, d_wave_chunks;
     uint64_t keys_cap = 0, seg_chunks = 0, fr_chunks = 0;
     PinBuf h_bytes, h_off, h_outoff, h_outcnt, h_status, h_keys, h_cursor;
     std::vector<uint32_t> pp_off, pp_cnt, pp_keys;  // post-processed results
     hipStream_t stream = nullptr;
     uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0, seg_demand_last = 0, fr_demand_last = 0;
     hipStream_t last_stream = nullptr;  // stream of the last tm_match_device call
+    uint32_t last_n = 0;                // topics of the last match batch
     bool stats_on = false;
     hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // around k_match_fast (tm_debug_timing)
     bool timing_on = false;
+
+    uint64_t edge_load_inv() const { return cfg.edge_load_inv ? cfg.edge_load_inv : EDGE_LOAD_INV; }
 
     // =====================================================================
     // words: a word of <= 8 bytes is its own key (zero-padded LE bytes); longer
@@ -221,7 +229,7 @@ struct tm_engine {
     uint32_t word_intern(const uint8_t *p, uint32_t len) {
         uint32_t wid = word_lookup(p, len);
         if (wid != NONE) return wid;
-        if ((word_off.size() + 1) * 2 > wtab.size()) word_rehash(wtab.size() * 2);
+        if ((word_off.size() + 1) * WORD_LOAD_INV > wtab.size()) word_rehash(wtab.size() * 2);
         WordSlot w{word_key(p, len), word_tag(len), (uint32_t)word_off.size()};
         word_off.push_back((uint32_t)warena.size());
         word_len.push_back(len);
@@ -293,7 +301,7 @@ struct tm_engine {
     uint32_t edge_child(uint32_t parent, uint32_t word) {
         uint64_t s = edge_find(dev_id(parent), word);
         if (s != ~0ull) return slot_node[s];
-        if ((n_edges + 1) * EDGE_LOAD_INV > etab.size()) edge_rehash(etab.size() * 2);
+        if ((n_edges + 1) * edge_load_inv() > etab.size()) edge_rehash(etab.size() * 2);
         const uint32_t child = (uint32_t)node_parent.size();
         node_parent.push_back(parent);
         node_word.push_back(word);
@@ -451,6 +459,7 @@ struct tm_engine {
             if (kset_find(node, kind, op.id, &slot) != NONE) return;  // set semantics
             uint32_t h = alloc_key();
             keys[h] = KeyRec{node, kind, {0, 0, 0}, op.id};
+            dirty_kid.push_back(h);
             kset[slot] = h;
             kset_used++;
             n_live++;
@@ -623,6 +632,39 @@ struct tm_engine {
         arena_dev = arena.size();
         if ((e = d_root.ensure(sizeof(RootRec)))) return e;
         if ((e = hipMemcpyAsync(d_root.p, &root, sizeof(RootRec), hipMemcpyHostToDevice, stream))) return e;
+        if ((e = upload_key_ids_full())) return e;
+        return hipStreamSynchronize(stream);
+    }
+
+    hipError_t upload_key_ids_full() {
+        std::vector<uint64_t> ids(keys.size());
+        for (size_t h = 0; h < keys.size(); h++) ids[h] = keys[h].id;
+        dirty_kid.clear();
+        hipError_t e = put(d_key_id, ids);
+        if (e) return e;
+        return hipStreamSynchronize(stream);  // `ids` dies at scope exit
+    }
+
+    hipError_t upload_key_ids_delta() {
+        if (dirty_kid.empty()) return hipSuccess;
+        if (keys.size() * sizeof(uint64_t) > d_key_id.cap) return upload_key_ids_full();
+        std::sort(dirty_kid.begin(), dirty_kid.end());
+        dirty_kid.erase(std::unique(dirty_kid.begin(), dirty_kid.end()), dirty_kid.end());
+        const size_t n = dirty_kid.size();
+        std::vector<uint64_t> idx(n), src(n);
+        for (size_t i = 0; i < n; i++) {
+            idx[i] = dirty_kid[i];
+            src[i] = keys[dirty_kid[i]].id;
+        }
+        dirty_kid.clear();
+        hipError_t e;
+        if ((e = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e;
+        if ((e = d_scatter_src.ensure(n * sizeof(uint64_t)))) return e;
+        if ((e = hipMemcpyAsync(d_scatter_idx.p, idx.data(), n * 8, hipMemcpyHostToDevice, stream))) return e;
+        if ((e = hipMemcpyAsync(d_scatter_src.p, src.data(), n * 8, hipMemcpyHostToDevice, stream))) return e;
+        if ((e = launch_scatter8(d_key_id.as<uint64_t>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint64_t>(),
+                                 n, stream)))
+            return e;
         return hipStreamSynchronize(stream);
     }
 
@@ -680,6 +722,7 @@ struct tm_engine {
         if ((e = scatter16(dirty_wslots, wtab, d_wtab.p))) return e;
         if ((e = scatter16(dirty_eslots, etab, d_etab.p))) return e;
         if ((e = scatter4(dirty_lists, slot_list, d_slot_list.p))) return e;
+        if ((e = upload_key_ids_delta())) return e;
         if (root_dirty) {
             if ((e = hipMemcpyAsync(d_root.p, &root, sizeof(RootRec), hipMemcpyHostToDevice, stream))) return e;
         }
@@ -820,7 +863,7 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     }
     uint64_t rk = eng->cfg.reserve_keys ? eng->cfg.reserve_keys : 1024;
     uint64_t rn = eng->cfg.reserve_nodes ? eng->cfg.reserve_nodes : rk * 4;
-    eng->word_rehash(1024);  // grows with the vocabulary (load <= 1/2), not with nodes
+    eng->word_rehash(1024);  // grows with the vocabulary (load <= 1/4), not with nodes
     eng->node_parent.reserve(rn);
     eng->node_word.reserve(rn);
     eng->node_slot.reserve(rn);
@@ -829,7 +872,7 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     eng->node_slot.push_back(NONE);
     eng->node_list.reserve(rn);
     eng->node_list.push_back(NodeList{0, 0, 0});
-    eng->edge_rehash(next_pow2(std::max<uint64_t>(rn * EDGE_LOAD_INV, 1024)));
+    eng->edge_rehash(next_pow2(std::max<uint64_t>(rn * eng->edge_load_inv(), 1024)));
     eng->kset_rehash(next_pow2(std::max<uint64_t>(rk * 2, 1024)));
     eng->keys.reserve(rk);
     eng->need_full = true;
@@ -846,12 +889,14 @@ void tm_destroy(tm_engine *eng) {
     if (!eng) return;
     (void)hipSetDevice(eng->cfg.device);
     if (eng->stream) (void)hipStreamSynchronize(eng->stream);
+    for (DevBuf *b : {&eng->d_key_id, &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot})
+        b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
                       &eng->d_arena, &eng->d_scatter_idx,
                       &eng->d_scatter_src, &eng->d_bytes, &eng->d_off, &eng->d_outoff, &eng->d_outcnt,
                       &eng->d_status, &eng->d_keys, &eng->d_cursor, &eng->d_slow_list, &eng->d_slow_count,
                       &eng->d_scr_w, &eng->d_scr_s, &eng->d_stats, &eng->d_seg_pool, &eng->d_seg_cursor,
-                      &eng->d_fr_pool, &eng->d_fr_cursor})
+                      &eng->d_fr_pool, &eng->d_fr_cursor, &eng->d_wave_chunks})
         b->release();
     for (PinBuf *b : {&eng->h_bytes, &eng->h_off, &eng->h_outoff, &eng->h_outcnt, &eng->h_status, &eng->h_keys,
                       &eng->h_cursor})
@@ -920,6 +965,7 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
     TM_TRY_HIP(eng->d_scr_w.ensure((bytes + 2ull * n + 2) * 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_scr_s.ensure((bytes + 2ull * n + 2) * 8), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_seg_cursor.ensure(64), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_wave_chunks.ensure(((uint64_t)n + 63) / 64 * SEG_MAXCHUNK * 4 + 4), TM_ENOMEM, "alloc");
     {
         // chunk pool for waves whose staged key segments overflow LDS
         uint64_t want = eng->cfg.seg_chunks ? eng->cfg.seg_chunks : std::max<uint64_t>(1024, ((uint64_t)n + 63) / 64 * 8);
@@ -991,6 +1037,7 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.seg_pool = eng->d_seg_pool.as<uint4>();
     a.seg_chunks = eng->seg_chunks;
     a.seg_cursor = eng->d_seg_cursor.as<unsigned long long>();
+    a.wave_chunks = eng->d_wave_chunks.as<uint32_t>();
     a.fr_pool = eng->d_fr_pool.as<uint2>();
     a.fr_chunks = eng->fr_chunks;
     a.fr_cursor = eng->d_fr_cursor.as<unsigned long long>();
@@ -1030,6 +1077,7 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
     TM_TRY_HIP(hipMemcpyAsync(eng->d_off.p, ho, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
     TM_TRY_HIP(eng->h_cursor.ensure(64), TM_ENOMEM, "pinned alloc");
     for (int attempt = 0; attempt < 2; attempt++) {
+        eng->last_n = n;
         TM_TRY_HIP(enqueue_match(eng, eng->d_bytes.as<uint8_t>(), eng->d_off.as<uint32_t>(), n, s), TM_EDEVICE,
                    "kernel launch");
         TM_TRY_HIP(hipMemcpyAsync(eng->h_cursor.p, eng->d_cursor.p, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
@@ -1138,6 +1186,7 @@ int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_of
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
     eng->last_stream = s;
+    eng->last_n = n;
     TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s), TM_EDEVICE, "kernel launch");
     out->n = n;
     out->d_off = eng->d_outoff.as<uint32_t>();
@@ -1167,6 +1216,63 @@ int tm_device_sync(tm_engine *eng) {
         eng->fr_demand_last = *(uint64_t *)(h + 24);
         return grow_pools(eng);
     }
+    return TM_OK;
+}
+
+int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out, void *stream) {
+    if (!eng || !d_off_out || (ids_cap && !d_ids)) return TM_EINVAL;
+    if (!eng->d_cursor.p) {
+        eng->err = "tm_result_ids_device: no tm_match_device batch yet";
+        return TM_ESTATE;
+    }
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    hipStream_t s = stream ? (hipStream_t)stream : (eng->last_stream ? eng->last_stream : eng->stream);
+    const uint32_t n = eng->last_n;
+    TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(launch_excl_scan(eng->d_outcnt.as<uint32_t>(), 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s),
+               TM_EDEVICE, "scan");
+    TM_TRY_HIP(launch_result_ids(eng->d_outcnt.as<uint32_t>(), eng->d_outoff.as<uint32_t>(), eng->d_keys.as<uint32_t>(),
+                                 eng->d_key_id.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, s),
+               TM_EDEVICE, "result ids");
+    return TM_OK;
+}
+
+int tm_merge_shards_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_t *d_counts, const uint64_t *d_ids,
+                           uint64_t stride, uint32_t *d_off_out, uint64_t *d_ids_out, uint64_t out_cap, void *stream) {
+    if (!eng || G == 0 || !d_off_out || (n && (!d_counts || !d_ids)) || (out_cap && !d_ids_out)) return TM_EINVAL;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_mrg_roff.ensure((uint64_t)G * (n + 1) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_mrg_tot.ensure((uint64_t)n * 4 + 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(launch_merge_shards(G, n, d_counts, d_ids, stride, eng->d_mrg_roff.as<uint32_t>(),
+                                   eng->d_mrg_tot.as<uint32_t>(), eng->d_res_scan.as<uint32_t>(), d_off_out, d_ids_out,
+                                   out_cap, s),
+               TM_EDEVICE, "merge");
+    return TM_OK;
+}
+
+int tm_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,
+                    uint32_t *off_out, uint64_t *ids_out, uint64_t out_cap) {
+    if (G == 0 || !off_out || (n && (!counts || !ids))) return TM_EINVAL;
+    std::vector<uint64_t> roff(G, 0);  // running source offset of each shard
+    uint64_t total = 0;
+    for (uint32_t t = 0; t < n; t++)
+        for (uint32_t r = 0; r < G; r++) total += counts[(uint64_t)r * n + t];
+    if (total > 0xFFFFFFFFull) return TM_EINVAL;
+    if (total > out_cap || (total && !ids_out)) return TM_ENOMEM;
+    uint64_t dst = 0;
+    for (uint32_t t = 0; t < n; t++) {
+        off_out[t] = (uint32_t)dst;
+        for (uint32_t r = 0; r < G; r++) {
+            const uint32_t c = counts[(uint64_t)r * n + t];
+            if (roff[r] + c > stride) return TM_EINVAL;
+            memcpy(ids_out + dst, ids + (uint64_t)r * stride + roff[r], (size_t)c * sizeof(uint64_t));
+            roff[r] += c;
+            dst += c;
+        }
+    }
+    off_out[n] = (uint32_t)dst;
     return TM_OK;
 }
 

@@ -34,18 +34,33 @@ namespace tmx {
 constexpr int WAVE = 64;
 constexpr int FCAP = 256;        // frontier entries per wave per depth held in LDS
 constexpr int FCH = FR_CHUNK;    // frontier entries per global overflow chunk
-constexpr int MAXF = 64;         // overflow chunks per frontier buffer per wave
-constexpr int SCAP = SEG_CHUNK;  // key segments staged in LDS = one global chunk
-constexpr int MAXCHUNK = 64;     // global segment chunks one wave may flush
-constexpr int TBCAP = 3072;      // topic bytes of one wave staged in LDS (else read from HBM)
+constexpr int MAXF = 32;         // overflow chunks per frontier buffer per wave
+#ifndef TM_SCAP
+#define TM_SCAP 128
+#endif
+#ifndef TM_TBCAP
+#define TM_TBCAP 3072
+#endif
+#ifndef TM_MIN_WAVES
+#define TM_MIN_WAVES 1
+#endif
+constexpr int SCAP = TM_SCAP;    // key segments staged in LDS (<= one global chunk)
+constexpr int MAXCHUNK = SEG_MAXCHUNK;  // global segment chunks one wave may flush (list in HBM)
+constexpr int TBCAP = TM_TBCAP;  // topic bytes of one wave staged in LDS (else read from HBM)
 constexpr uint32_t SEG_INLINE = 1u << 8;    // segment.w flag: .x is the key itself
 constexpr uint32_t SEG_NODE = 1u << 9;      // segment.w flag: .x is a node (slot); its list
                                             // offset is read from slot_list at copy-out
 constexpr uint32_t SEG_SKIP_SHIFT = 11;     // with SEG_NODE: keys to skip (term_cnt for the
                                             // '#' part) in .w bits 11-31
 constexpr uint32_t DO_PLUS = 0x80u, DO_LIT = 0x40u;  // frontier meta: probes this entry needs
-constexpr int RPL = 2;                      // frontier entries per lane per round
-constexpr int CP_UNROLL = 8;                // arena loads in flight per lane, long lists
+#ifndef TM_RPL
+#define TM_RPL 2
+#endif
+#ifndef TM_CP_UNROLL
+#define TM_CP_UNROLL 8
+#endif
+constexpr int RPL = TM_RPL;                 // frontier entries per lane per round
+constexpr int CP_UNROLL = TM_CP_UNROLL;     // arena loads in flight per lane, long lists
 constexpr int CP_SHORT = 8;                 // lists up to this long are copied by one lane
 
 // ---------------------------------------------------------------------------
@@ -153,14 +168,12 @@ struct WaveLds {
     uint32_t fch[2][MAXF];        // global overflow chunks of each frontier buffer
     uint4 seg[SCAP];              // {src or key, cnt, rel, topic lane | SEG_INLINE}
     uint32_t seg_scan[SCAP + 1];
-    uint32_t chunk[MAXCHUNK];
-    uint32_t cur[WAVE];    // byte offset where the topic's next level starts
     uint32_t wid[2][WAVE]; // word id of level d (wid[d&1]) and of level d+1 (tokenised ahead)
     uint32_t nlev[WAVE];
     uint32_t cnt[WAVE];    // keys matched so far (allocates each segment's rel)
     uint32_t tbase[WAVE];  // output base of the topic
-    uint32_t lflags[WAVE]; // bit0: spill to k_match_slow
-    uint32_t alive[2][WAVE];  // frontier entries per topic at this / the next depth
+    unsigned long long spill;     // bit per topic lane: spill to k_match_slow
+    unsigned long long alive[2];  // bit per topic lane: has frontier entries at this / the next depth
 };
 
 // Expand L.seg[0..ns) into the output.  Short segments (<= CP_SHORT keys, most of them
@@ -180,7 +193,7 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
                 g.w &= 0xFFu | SEG_INLINE;
                 L.seg[j] = g;
             }
-            if (L.lflags[g.w & 0xFFu] & 1u) g.y = 0;  // spilled topic: the slow kernel owns it
+            if ((L.spill >> (g.w & 0x3Fu)) & 1ull) g.y = 0;  // spilled topic: the slow kernel owns it
         }
         const bool is_long = g.y > (uint32_t)CP_SHORT;
         if (!is_long && g.y) {
@@ -224,8 +237,9 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
+__global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) {
     __shared__ WaveLds L;
+    uint32_t *const wchunks = a.wave_chunks + (uint64_t)blockIdx.x * MAXCHUNK;  // this wave's flushed chunks
     const uint32_t lane = lane_id();
     const uint32_t t = blockIdx.x * WAVE + lane;
     const bool active = t < a.n;
@@ -273,20 +287,25 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     }
     const bool spill0 = active && !badarg && a.force_slow;
     const bool walk = active && !badarg && !spill0;
-    L.cur[lane] = b;
+    uint32_t cur_b = b;  // byte offset where this lane's topic's next level starts
     L.nlev[lane] = nl;
     L.cnt[lane] = 0;
-    L.lflags[lane] = spill0 ? 1u : 0u;
-    L.alive[0][lane] = 0;
-    L.alive[1][lane] = 0;
+    {
+        const unsigned long long sp0 = __ballot(spill0);
+        if (lane == 0) {
+            L.spill = sp0;
+            L.alive[0] = 0;
+            L.alive[1] = 0;
+        }
+    }
 
     // tokenise one level of this lane's topic (the cursor walks left to right)
     auto tokenize_next = [&](uint32_t slot) {
-        uint32_t i = L.cur[lane];
+        uint32_t i = cur_b;
         const uint32_t st = i;
         const uint64_t key = level_key(&i, e, byte_at);
         L.wid[slot][lane] = word_lookup(a, key, i - st, st, byte_at, &st_wprobe);
-        L.cur[lane] = i + 1;
+        cur_b = i + 1;
     };
 
     // ---- 2. root: emit "#" keys (not for '$' topics), seed the frontier
@@ -306,11 +325,12 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
         st_seg += em;
         const uint32_t rinfo = dollar ? (R.info & I_LIT) : R.info;  // '$' topics: no root '+'
         const uint32_t m = walk ? probes_needed(rinfo, R.bloom, L.wid[0][lane]) : 0u;
+        const unsigned long long al0 = __ballot(m != 0);
+        if (lane == 0) L.alive[0] = al0;
         const uint32_t p2 = wave_excl_scan(m ? 1u : 0u, &tot);
         if (m) {
             L.fr_node[0][p2] = ROOT_ID;
             L.fr_meta[0][p2] = (uint8_t)(lane | m);
-            L.alive[0][lane] = 1;
             st_visit++;
         }
         nfr = tot;
@@ -347,8 +367,8 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
         const uint32_t cur = d & 1, nxt = cur ^ 1;
         // 3a. tokenise level d+1 ahead for topics that are still alive and go deeper:
         //     the children pushed at this depth are filtered with it (bloom)
-        if (walk && L.alive[cur][lane] && d + 1 < nl) tokenize_next(nxt);
-        L.alive[nxt][lane] = 0;
+        if (walk && ((L.alive[cur] >> lane) & 1ull) && d + 1 < nl) tokenize_next(nxt);
+        if (lane == 0) L.alive[nxt] = 0;
         __syncthreads();
         // 3b. expand the frontier, WAVE * RPL entries per round (RPL per lane, so each
         //     lane has up to 2 * RPL independent probes in flight)
@@ -440,12 +460,12 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                     uint4 *dst = a.seg_pool + (uint64_t)c * SCAP;
                     for (uint32_t j = lane; j < (uint32_t)SCAP; j += WAVE)
                         dst[j] = j < nseg ? L.seg[j] : make_uint4(0u, 0u, 0u, 0u);
-                    if (lane == 0) L.chunk[nchunk] = c;
+                    if (lane == 0) wchunks[nchunk] = c;
                     nchunk++;
                     st_flush++;
                 } else {
                     // pool exhausted: those topics take the spill kernel instead
-                    for (uint32_t j = lane; j < nseg; j += WAVE) atomicOr(&L.lflags[L.seg[j].w & 0xFFu], 1u);
+                    for (uint32_t j = lane; j < nseg; j += WAVE) atomicOr(&L.spill, 1ull << (L.seg[j].w & 0x3Fu));
                 }
                 nseg = 0;
                 __syncthreads();
@@ -463,7 +483,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                 dok = c0 + ndc <= a.seg_chunks && nchunk + ndc <= (uint32_t)MAXCHUNK;
                 dc0 = (uint32_t)c0;
                 if (dok) {
-                    if (lane < ndc) L.chunk[nchunk + lane] = dc0 + lane;
+                    for (uint32_t j = lane; j < ndc; j += WAVE) wchunks[nchunk + j] = dc0 + j;
                     for (uint32_t j = tot_s + lane; j < ndc * SCAP; j += WAVE)  // pad the last chunk
                         a.seg_pool[(uint64_t)dc0 * SCAP + j] = make_uint4(0u, 0u, 0u, 0u);
                     nchunk += ndc;
@@ -479,7 +499,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                         const uint4 g = make_uint4(src, cnt, cnt ? atomicAdd(&L.cnt[tl[k]], cnt) : 0u, tl[k] | fl2);
                         if (!direct) L.seg[ps] = g;
                         else if (dok) a.seg_pool[(uint64_t)dc0 * SCAP + ps] = g;
-                        else atomicOr(&L.lflags[tl[k]], 1u);  // pool exhausted: topic spills
+                        else atomicOr(&L.spill, 1ull << tl[k]);  // pool exhausted: topic spills
                         ps++;
                     };
 #pragma unroll
@@ -541,12 +561,12 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
                     for (int k = 0; k < RPL; k++) {
                         if (q1[k]) fr_write(nxt, pp++, r1[k].child, tl[k] | q1[k]);
                         if (q2[k]) fr_write(nxt, pp++, r2[k].child, tl[k] | q2[k]);
-                        if (q1[k] || q2[k]) atomicAdd(&L.alive[nxt][tl[k]], (uint32_t)(q1[k] != 0) + (q2[k] != 0));
+                        if (q1[k] || q2[k]) atomicOr(&L.alive[nxt], 1ull << tl[k]);
                     }
                 } else {
 #pragma unroll
                     for (int k = 0; k < RPL; k++)  // frontier overflow: those topics spill
-                        if (q1[k] || q2[k]) atomicOr(&L.lflags[tl[k]], 1u);
+                        if (q1[k] || q2[k]) atomicOr(&L.spill, 1ull << tl[k]);
                 }
             }
             nnext = min(nnext + tot_p, cap);
@@ -559,7 +579,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
 
     if constexpr (STATS) ts2 = __builtin_amdgcn_s_memtime();
     // ---- 4. reserve this wave's output with one atomic; per-topic results
-    const bool spill = active && !badarg && (L.lflags[lane] & 1u);
+    const bool spill = active && !badarg && ((L.spill >> lane) & 1ull);
     const uint32_t my = (walk && !spill) ? L.cnt[lane] : 0u;
     uint32_t total;
     const uint32_t excl = wave_excl_scan(my, &total);
@@ -587,7 +607,7 @@ __global__ __launch_bounds__(WAVE) void k_match_fast(MatchArgs a) {
     if (!overflow && total) {
         expand_segments(a, L, nseg);
         for (uint32_t c = 0; c < nchunk; ++c) {
-            const uint4 *src = a.seg_pool + (uint64_t)L.chunk[c] * SCAP;
+            const uint4 *src = a.seg_pool + (uint64_t)wchunks[c] * SCAP;
             for (uint32_t j = lane; j < (uint32_t)SCAP; j += WAVE) L.seg[j] = src[j];
             __syncthreads();
             expand_segments(a, L, SCAP);

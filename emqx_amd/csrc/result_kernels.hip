@@ -1,0 +1,198 @@
+// result_kernels.hip — gfx950 kernels that reshape match results after k_match_fast:
+//
+//   * key handles -> route ids, compacted topic-major (tm_result_ids_device).  The walk
+//     writes each wave's keys wherever its one atomic reserved them; a consumer that
+//     ships results off the GPU (the sharded mode's all-gather, a NIF copying to the
+//     caller's heap like match_to_route/1, apps/emqx/src/emqx_router.erl:648-649) wants
+//     them as ids in topic order.
+//   * merge of per-shard results (tm_merge_shards_device): every rank of the filter-
+//     sharded mode matched the same topics against a disjoint key shard;
+//     after the all-gather, topic t's result is the concatenation of its slices from
+//     rank 0..G-1 (shards are disjoint, so no dedupe).
+//
+// All of it is byte movement: coalesced where the layout allows, HBM-bound.
+#include <hip/hip_runtime.h>
+
+#include "device_api.h"
+
+namespace tmx {
+
+constexpr int SCAN_T = 256;           // threads per scan block
+constexpr int SCAN_V = 8;             // values per thread
+constexpr int SCAN_B = SCAN_T * SCAN_V;  // values per scan block
+
+// ---------------------------------------------------------------------------
+// exclusive scan of u32 values into out[0..n] (out[n] = total), three passes.
+// Values are counts whose total stays below 2^32 (a batch's key count).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *sh, uint32_t *total) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+    for (uint32_t w = 0; w < SCAN_T / 64; w++) {
+        if (w < wid) base += sh[w];
+        tot += sh[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_local(const uint32_t *in, uint64_t in_stride, uint32_t n,
+                                                      uint32_t *out, uint32_t *block_sums) {
+    __shared__ uint32_t sh[SCAN_T / 64];
+    const uint64_t b0 = (uint64_t)blockIdx.x * SCAN_B + (uint64_t)threadIdx.x * SCAN_V;
+    uint32_t v[SCAN_V], s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_V; k++) {
+        v[k] = (b0 + k < n) ? in[(b0 + k) * in_stride] : 0u;
+        s += v[k];
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan(s, sh, &tot);
+#pragma unroll
+    for (int k = 0; k < SCAN_V; k++) {
+        if (b0 + k < n) out[b0 + k] = run;
+        run += v[k];
+    }
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
+}
+
+// one block: exclusive scan of the block sums in place; sums[nb] = total
+__global__ __launch_bounds__(SCAN_T) void k_scan_sums(uint32_t *sums, uint32_t nb) {
+    __shared__ uint32_t sh[SCAN_T / 64];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += SCAN_T) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < nb ? sums[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan(v, sh, &tot);
+        if (i < nb) sums[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) sums[nb] = carry;
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_add(uint32_t *out, uint32_t n, const uint32_t *sums, uint32_t nb) {
+    const uint64_t b0 = (uint64_t)blockIdx.x * SCAN_B + (uint64_t)threadIdx.x * SCAN_V;
+    const uint32_t add = sums[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < SCAN_V; k++)
+        if (b0 + k < n) out[b0 + k] += add;
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = sums[nb];
+}
+
+uint64_t scan_scratch_words(uint32_t n) { return (uint64_t)(n + SCAN_B - 1) / SCAN_B + 1; }
+
+hipError_t launch_excl_scan(const uint32_t *in, uint64_t in_stride, uint32_t n, uint32_t *out, uint32_t *scratch,
+                            hipStream_t s) {
+    const uint32_t nb = (uint32_t)((n + SCAN_B - 1) / SCAN_B);
+    if (nb == 0) return hipMemsetAsync(out, 0, sizeof(uint32_t), s);
+    k_scan_local<<<nb, SCAN_T, 0, s>>>(in, in_stride, n, out, scratch);
+    k_scan_sums<<<1, SCAN_T, 0, s>>>(scratch, nb);
+    k_scan_add<<<nb, SCAN_T, 0, s>>>(out, n, scratch, nb);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// key handles -> ids, topic-major.  One wave per 64 topics: lists of up to 8 keys are
+// copied by the topic's own lane; longer ones (hot '#' lists) by the whole wave, 64
+// consecutive keys per instruction.
+__global__ __launch_bounds__(64) void k_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
+                                                   const uint64_t *key_id, const uint32_t *dst_off, uint32_t n,
+                                                   uint64_t *ids, uint64_t cap) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t t = blockIdx.x * 64 + lane;
+    uint32_t c = 0, so = 0, dofs = 0;
+    if (t < n) {
+        c = cnt[t];
+        so = src_off[t];
+        dofs = dst_off[t];
+        if ((uint64_t)dofs + c > cap) c = 0;  // caller's buffer too small: it re-sizes from d_off[n]
+    }
+    const bool is_long = c > 8;
+    if (!is_long) {
+        for (uint32_t k = 0; k < c; k++) ids[(uint64_t)dofs + k] = key_id[keys[(uint64_t)so + k]];
+    }
+    uint64_t longs = __ballot(is_long);
+    while (longs) {
+        const int l = __builtin_ctzll(longs);
+        longs &= longs - 1;
+        const uint32_t lc = __shfl(c, l, 64), ls = __shfl(so, l, 64), ld = __shfl(dofs, l, 64);
+        for (uint32_t k = lane; k < lc; k += 64) ids[(uint64_t)ld + k] = key_id[keys[(uint64_t)ls + k]];
+    }
+}
+
+hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
+                             const uint64_t *key_id, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
+                             uint64_t cap, hipStream_t s) {
+    if (!n) return hipSuccess;
+    k_result_ids<<<(n + 63) / 64, 64, 0, s>>>(cnt, src_off, keys, key_id, dst_off, n, ids, cap);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// shard merge.  counts: G rows of n; ids: G rows of `stride` (rank r's compacted,
+// topic-major ids); roff: G rows of n+1 (per-rank exclusive scans of counts);
+// off: merged exclusive scan (n+1).
+__global__ void k_colsum(const uint32_t *counts, uint32_t G, uint32_t n, uint32_t *tot) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    uint32_t s = 0;
+    for (uint32_t r = 0; r < G; r++) s += counts[(uint64_t)r * n + t];
+    tot[t] = s;
+}
+
+__global__ __launch_bounds__(64) void k_merge(const uint32_t *counts, const uint64_t *ids, uint64_t stride,
+                                              const uint32_t *roff, const uint32_t *off, uint32_t G, uint32_t n,
+                                              uint64_t *out, uint64_t cap) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t t0 = blockIdx.x * 64;
+    for (uint32_t i = 0; i < 64 && t0 + i < n; i++) {
+        const uint32_t t = t0 + i;
+        uint64_t dst = off[t];
+        if (off[t + 1] > cap) return;  // caller's buffer too small (wave-uniform; it re-sizes from off[n])
+        for (uint32_t r = 0; r < G; r++) {
+            const uint32_t c = counts[(uint64_t)r * n + t];
+            const uint64_t src = (uint64_t)r * stride + roff[(uint64_t)r * (n + 1) + t];
+            for (uint32_t k = lane; k < c; k += 64) out[dst + k] = ids[src + k];
+            dst += c;
+        }
+    }
+}
+
+hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,
+                               uint32_t *roff, uint32_t *tot, uint32_t *scratch, uint32_t *off, uint64_t *out,
+                               uint64_t cap, hipStream_t s) {
+    hipError_t e;
+    for (uint32_t r = 0; r < G; r++)
+        if ((e = launch_excl_scan(counts + (uint64_t)r * n, 1, n, roff + (uint64_t)r * (n + 1), scratch, s))) return e;
+    if (n) {
+        k_colsum<<<(n + 255) / 256, 256, 0, s>>>(counts, G, n, tot);
+        if ((e = hipGetLastError())) return e;
+    }
+    if ((e = launch_excl_scan(tot, 1, n, off, scratch, s))) return e;
+    if (!n) return hipSuccess;
+    k_merge<<<(n + 63) / 64, 64, 0, s>>>(counts, ids, stride, roff, off, G, n, out, cap);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+__global__ void k_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[idx[i]] = src[i];
+}
+
+hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    k_scatter8<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
+    return hipGetLastError();
+}
+
+}  // namespace tmx

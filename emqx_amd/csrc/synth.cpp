@@ -101,6 +101,8 @@ typedef struct synth_params {
     uint32_t hot_depth_min, hot_depth_max;
     double p_topic_hot;     // topic drawn under a random hot filter's prefix
     double hash_w[16];      // if any > 0: '#' cut depth d drawn with weight hash_w[d]
+    uint32_t shard_count;   // > 1: emit only the route keys of shard `shard_index`
+    uint32_t shard_index;   //      (shard_of(id) = splitmix64 finaliser(id) % shard_count)
 } synth_params;
 
 typedef struct synth_out {
@@ -147,6 +149,13 @@ static std::string joinv(const std::vector<std::string> &lv, size_t n) {
     return s;
 }
 
+// The filter-sharded mode's key placement (emqx_amd/shard.py shard_of).
+static uint64_t shard_mix(uint64_t x) {
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
 int synth_generate(const synth_params *pp, synth_out **out) {
     if (!pp || !out || pp->max_levels < pp->min_levels || pp->min_levels == 0) return -1;
     const synth_params &p = *pp;
@@ -159,12 +168,14 @@ int synth_generate(const synth_params *pp, synth_out **out) {
     std::vector<uint8_t> fb;
     std::vector<uint64_t> foff{0}, fid;
     std::vector<uint64_t> src_seed;  // rng seed of each filter's source topic
-    fb.reserve(p.n_filters * 48);
-    foff.reserve(p.n_filters + 1);
-    fid.reserve(p.n_filters);
+    const uint64_t kept = p.n_filters / (p.shard_count > 1 ? p.shard_count : 1) + 1024;
+    fb.reserve(kept * 48);
+    foff.reserve(kept + 1);
+    fid.reserve(kept);
     src_seed.reserve(p.n_filters);
     std::vector<std::string> lv;
     uint64_t next_id = 0;
+    auto keep = [&](uint64_t id) { return p.shard_count <= 1 || shard_mix(id) % p.shard_count == p.shard_index; };
     for (uint64_t i = 0; i < p.n_filters; i++) {
         uint64_t sseed = r.next();
         src_seed.push_back(sseed);
@@ -204,10 +215,11 @@ int synth_generate(const synth_params *pp, synth_out **out) {
         if (hash) f += n ? "/#" : "#";
         uint32_t copies = 1;
         if ((hash || plus) && p.p_multi > 0 && r.uni() < p.p_multi) copies += 1 + r.below(p.multi_max ? p.multi_max : 1);
-        for (uint32_t c = 0; c < copies; c++) {
+        for (uint32_t c = 0; c < copies; c++, next_id++) {
+            if (!keep(next_id)) continue;
             fb.insert(fb.end(), f.begin(), f.end());
             foff.push_back(fb.size());
-            fid.push_back(next_id++);
+            fid.push_back(next_id);
         }
     }
     // hot '#' filters: a short prefix subscribed by many clients (ids)
@@ -224,10 +236,11 @@ int synth_generate(const synth_params *pp, synth_out **out) {
         std::string f = joinv(lv, d) + (d ? "/#" : "#");
         double lo = std::log((double)std::max(1u, p.hot_ids_min)), hi = std::log((double)std::max(p.hot_ids_min, p.hot_ids_max));
         uint32_t copies = (uint32_t)std::exp(lo + (hi - lo) * r.uni());
-        for (uint32_t c = 0; c < copies; c++) {
+        for (uint32_t c = 0; c < copies; c++, next_id++) {
+            if (!keep(next_id)) continue;
             fb.insert(fb.end(), f.begin(), f.end());
             foff.push_back(fb.size());
-            fid.push_back(next_id++);
+            fid.push_back(next_id);
         }
     }
 

@@ -33,6 +33,7 @@ class synth_params(C.Structure):
         ("hot_ids_min", C.c_uint32), ("hot_ids_max", C.c_uint32),
         ("hot_depth_min", C.c_uint32), ("hot_depth_max", C.c_uint32),
         ("p_topic_hot", C.c_double), ("hash_w", C.c_double * 16),
+        ("shard_count", C.c_uint32), ("shard_index", C.c_uint32),
     ]
 
 

@@ -93,7 +93,10 @@ typedef struct tm_config {
     uint32_t seg_chunks;          /* 0 = auto; else fixed size of the key-segment and
                                      frontier-overflow chunk pools (test aid: exhaustion
                                      routes topics to the spill kernel, results stay exact) */
-    uint32_t reserved[3];
+    uint32_t edge_load_inv;       /* edge-table load <= 1/edge_load_inv (0 = default 8): a wave
+                                     waits for its longest probe chain, so lower load shortens
+                                     the walk at the price of HBM (16 B per slot) */
+    uint32_t reserved[2];
 } tm_config;
 
 typedef struct tm_op {
@@ -177,6 +180,27 @@ int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_of
  * the internal chunk pools to that batch's demand for the next one. */
 int tm_device_sync(tm_engine *eng);
 int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap);
+
+/* Route ids of the last match batch (all keys, TM_MATCH_ALL), compacted topic-major on
+ * the device: topic i's ids are d_ids[d_off[i] .. d_off[i+1]); d_off has n+1 entries and
+ * d_off[n] = *d_total.  This is get_id/1 (emqx_topic_index.erl:87-89) applied on the GPU to
+ * every key, in the topic order a caller expects (emqx_router.erl:648-649 maps each key
+ * to a #route{}).  Asynchronous on `stream` (NULL: the batch's stream).  Topics whose ids
+ * would pass ids_cap are left unwritten: size d_ids from *d_total. */
+int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off, void *stream);
+
+/* Filter-sharded mode: G shards matched the same n topics against disjoint
+ * key sets; shard r's compacted result (tm_result_ids_device) is counts[r*n .. r*n+n) and
+ * ids[r*stride ..).  Writes the merged result: topic i's ids are the concatenation of its
+ * slices from shard 0..G-1 at out_ids[out_off[i] .. out_off[i+1]) (shards are disjoint, so
+ * nothing is deduplicated; the reference's own result is one unordered list per topic).
+ * Device form: asynchronous on `stream`; topics past out_cap are left unwritten.
+ * Host form: no device needed; TM_ENOMEM if out_cap is too small. */
+int tm_merge_shards_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_t *d_counts, const uint64_t *d_ids,
+                           uint64_t stride, uint32_t *d_out_off, uint64_t *d_out_ids, uint64_t out_cap,
+                           void *stream);
+int tm_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,
+                    uint32_t *out_off, uint64_t *out_ids, uint64_t out_cap);
 
 /* key introspection (get_id/1, get_topic/1) */
 int tm_key_info(const tm_engine *eng, uint32_t key, uint64_t *id, uint32_t *flags,

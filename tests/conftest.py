@@ -3,6 +3,12 @@ import sys
 
 import pytest
 
+# torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's): whichever is loaded
+# first serves the whole process.  Load torch's before libemqx_tm.so so that GPU tests
+# that mix torch device tensors with the engine run on one HIP runtime (bench.py and
+# __graft_entry__ already import in that order or do not use torch at all).
+import torch  # noqa: E402,F401
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -1,0 +1,216 @@
+"""Filter-sharded mode (SURVEY.md §8(e) mode 2).
+
+CPU (not gpu): world_size-2 gloo runs of emqx_amd.shard.ShardedIndex exercise the real
+placement, the real exchange (all-gather of counts, padded all-gather of ids) and the
+real host merge (tm_merge_shards in libemqx_tm.so).  The per-shard matcher there is a
+TEST DOUBLE: the oracle's restated index over the rank's keys (there is no GPU on this
+host).  The merged result is checked bit-exactly against the oracle over ALL keys.
+
+GPU: G shard engines on cuda:0 in one process, device compaction + device merge
+(tm_result_ids_device, tm_merge_shards_device); the all-gather is replaced by stacking
+the shards' buffers (what RCCL's all-gather produces), since one box has one GPU.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle
+from emqx_amd import _native as N
+from emqx_amd import shard as S
+from emqx_amd import workloads
+
+
+class OracleShard:
+    """Test double for EngineShard: the restated index over this rank's keys."""
+
+    def __init__(self):
+        self.keys = {}  # (filter bytes, id) -> flags
+        self.ix = None
+
+    def apply_packed(self, op, buf, off, ids, flags=None):
+        b = bytes(np.asarray(buf, dtype=np.uint8))
+        for i in range(len(ids)):
+            k = (b[int(off[i]):int(off[i + 1])], int(ids[i]))
+            if op == N.TM_OP_ADD:
+                self.keys[k] = 0 if flags is None else int(flags[i])
+            else:
+                self.keys.pop(k, None)
+
+    def commit(self):
+        ks = sorted(self.keys)
+        self.ix = oracle.OrderedIndex.from_filters([k[0] for k in ks], [k[1] for k in ks],
+                                                   [self.keys[k] for k in ks])
+
+    def match_ids(self, t_bytes, t_off):
+        off, ids, st = self.ix.match(t_bytes, t_off)
+        return np.diff(off).astype(np.uint32), ids, st
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        w = workloads.generate("A", scale=0.5, n_topics=3000)
+        six = S.ShardedIndex(OracleShard(), rank, world)
+        six.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+        six.commit()
+        off, ids, st = six.match(w.t_bytes, w.t_off)
+        # epoch 2: delete every 7th key, add a root '#' and a '+/...' key (placement by id)
+        dm = np.arange(w.n_keys) % 7 == 0
+        b, o, i, _ = S.select_keys(w.f_bytes, w.f_off, w.f_id, dm)
+        six.apply_packed(N.TM_OP_DEL, b, o, i)
+        xb, xo = N.pack_topics([b"#", b"+/+/+/+"])
+        six.apply_packed(N.TM_OP_ADD, xb, xo.astype(np.uint64), np.array([10**9, 10**9 + 1], np.uint64))
+        six.commit()
+        off2, ids2, st2 = six.match(w.t_bytes, w.t_off)
+        q.put((rank, off.tolist(), ids.tolist(), st.tolist(), off2.tolist(), ids2.tolist(), None))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, None, None, None, None, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _reference(w):
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    off, ids, st = ix.match(w.t_bytes, w.t_off)
+    dm = np.arange(w.n_keys) % 7 != 0
+    b, o, i, _ = S.select_keys(w.f_bytes, w.f_off, w.f_id, dm)
+    fl = [bytes(b[int(o[k]):int(o[k + 1])]) for k in range(len(i))] + [b"#", b"+/+/+/+"]
+    ix2 = oracle.OrderedIndex.from_filters(fl, list(i) + [10**9, 10**9 + 1])
+    off2, ids2, _ = ix2.match(w.t_bytes, w.t_off)
+    return off, ids, st, off2, ids2
+
+
+def _same_sets(off, ids, eoff, eids):
+    off, ids, eoff, eids = map(np.asarray, (off, ids, eoff, eids))
+    assert len(off) == len(eoff)
+    assert np.array_equal(np.diff(off.astype(np.int64)), np.diff(eoff.astype(np.int64)))
+    for t in range(len(off) - 1):
+        got = np.sort(ids[off[t]:off[t + 1]].astype(np.uint64))
+        assert np.array_equal(got, eids[eoff[t]:eoff[t + 1]]), t
+
+
+def test_shard_placement_matches_generator():
+    full = workloads.generate("A", scale=0.3, n_topics=10)
+    for r in range(3):
+        part = workloads.generate("A", scale=0.3, n_topics=10, shard_count=3, shard_index=r)
+        assert np.array_equal(part.f_id, full.f_id[S.shard_of(full.f_id, 3) == r])
+
+
+def test_select_keys_roundtrip():
+    w = workloads.generate("A", scale=0.1, n_topics=10)
+    mask = np.arange(w.n_keys) % 3 == 1
+    b, o, i, _ = S.select_keys(w.f_bytes, w.f_off, w.f_id, mask)
+    fl = w.filters()
+    got = [bytes(b[int(o[k]):int(o[k + 1])]) for k in range(len(i))]
+    assert got == [fl[k] for k in np.nonzero(mask)[0]]
+    assert np.array_equal(i, w.f_id[mask])
+
+
+def test_host_merge_concatenates_per_topic():
+    rng = np.random.default_rng(5)
+    G, n = 3, 50
+    counts = rng.integers(0, 6, size=(G, n)).astype(np.uint32)
+    stride = int(counts.sum(1).max()) + 3
+    ids = np.zeros((G, stride), np.uint64)
+    per = [[None] * n for _ in range(G)]
+    for r in range(G):
+        pos = 0
+        for t in range(n):
+            v = rng.integers(0, 2**63, size=counts[r, t], dtype=np.uint64)
+            ids[r, pos:pos + len(v)] = v
+            per[r][t] = v
+            pos += len(v)
+    off, merged = N.merge_shards(counts, ids)
+    for t in range(n):
+        exp = np.concatenate([per[r][t] for r in range(G)])
+        assert np.array_equal(merged[off[t]:off[t + 1]], exp)
+    assert off[-1] == counts.sum()
+
+
+def test_sharded_gloo_world2_matches_unsharded_oracle():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for r in res:
+        assert r[6] is None, r[6]
+    w = workloads.generate("A", scale=0.5, n_topics=3000)
+    eoff, eids, est, eoff2, eids2 = _reference(w)
+    for rank, off, ids, st, off2, ids2, _ in res:
+        _same_sets(off, ids, eoff, eids)
+        assert np.array_equal(np.asarray(st), est)
+        _same_sets(off2, ids2, eoff2, eids2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G", [1, 2, 3])
+def test_sharded_device_merge_gpu(G):
+    import torch
+    w = workloads.generate("B", scale=0.05, n_topics=20000)
+    n = w.n_topics
+    dev = torch.device("cuda", 0)
+    d_bytes = torch.from_numpy(w.t_bytes).to(dev)
+    d_off = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
+    engs, offs, idss, tots = [], [], [], []
+    for r in range(G):
+        eng = N.Engine(0)
+        six = S.ShardedIndex(S.EngineShard(eng), r, G)
+        six.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+        six.commit()
+        res = eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, int(w.t_off[-1]), 0)
+        eng.device_sync()
+        total = S._read_u64(res.d_total)
+        if total > res.keys_cap:
+            eng.reserve_matches(total + 1024)
+            res = eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, int(w.t_off[-1]), 0)
+            eng.device_sync()
+        lo = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        ids = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
+        eng.result_ids_device(ids.data_ptr(), max(total, 1), lo.data_ptr(), 0)
+        torch.cuda.synchronize()
+        assert int(lo[-1].item()) == total
+        engs.append(eng)
+        offs.append(lo)
+        idss.append(ids)
+        tots.append(total)
+    stride = max(max(tots), 1)
+    C = torch.stack([(o[1:] - o[:-1]) for o in offs]).contiguous()
+    Ids = torch.zeros((G, stride), dtype=torch.int64, device=dev)
+    for r in range(G):
+        Ids[r, :tots[r]] = idss[r][:tots[r]]
+    out_total = sum(tots)
+    out_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    out_ids = torch.empty(max(out_total, 1), dtype=torch.int64, device=dev)
+    engs[0].merge_shards_device(G, n, C.data_ptr(), Ids.data_ptr(), stride, out_off.data_ptr(), out_ids.data_ptr(),
+                                out_total, 0)
+    torch.cuda.synchronize()
+    off = out_off.cpu().numpy().view(np.uint32)
+    ids = out_ids[:out_total].cpu().numpy().view(np.uint64)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    eoff, eids, _ = ix.match(w.t_bytes, w.t_off)
+    _same_sets(off, ids, eoff, eids)
+    # the host merge of the same buffers agrees with the device merge
+    hoff, hids = N.merge_shards(C.cpu().numpy().view(np.uint32), Ids.cpu().numpy().view(np.uint64))
+    assert np.array_equal(hoff, off) and np.array_equal(hids, ids)
+    for e in engs:
+        e.close()

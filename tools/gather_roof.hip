@@ -1,0 +1,71 @@
+// tools/gather_roof.hip — the random-gather ceiling of one MI355X, for the walk's roofline.
+//
+// k_match_fast's probes are independent random 16-B loads into a table of GiBs (the edge
+// table).  Their ceiling is not the streaming HBM bandwidth but the rate at which the
+// memory system serves random 16-B requests that miss the caches.  This measures it with
+// no dependence between loads: every lane keeps U loads in flight, tables of 256 MiB to
+// 4 GiB (the config-C edge table is 4 GiB), 16 waves per CU.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 tools/gather_roof.hip -o tools/gather_roof
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+__device__ __forceinline__ unsigned long long mix(unsigned long long x) {
+    x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27; x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_gather(const uint4 *tab, unsigned long long mask16, unsigned iters,
+                                                unsigned seed, unsigned *out) {
+    const unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned acc = 0;
+    for (unsigned it = 0; it < iters; it++) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = tab[mix((g * iters + it) * U + u + seed) & mask16];
+#pragma unroll
+        for (int u = 0; u < U; u++) acc += v[u].x ^ v[u].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int U>
+static void run(const uint4 *tab, unsigned long long bytes, unsigned *out) {
+    const unsigned blocks = 256 * 4, threads = 256;  // 16 waves per CU
+    const unsigned iters = 64 / U * 4;
+    const unsigned long long loads = (unsigned long long)blocks * threads * iters * U;
+    k_gather<U><<<blocks, threads>>>(tab, bytes / 16 - 1, iters, 1, out);
+    hipDeviceSynchronize();
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0);
+    k_gather<U><<<blocks, threads>>>(tab, bytes / 16 - 1, iters, 7, out);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("{\"table_MiB\": %llu, \"inflight_per_lane\": %d, \"loads\": %llu, \"ms\": %.4f, \"G_loads_per_s\": %.2f, "
+           "\"GBps_at_64B\": %.0f}\n",
+           bytes >> 20, U, loads, ms, loads / (ms * 1e6), loads * 64.0 / (ms * 1e6));
+}
+
+int main() {
+    const unsigned long long maxb = 4ull << 30;
+    uint4 *tab;
+    unsigned *out;
+    if (hipMalloc(&tab, maxb) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
+    hipMemset(tab, 1, maxb);
+    for (unsigned long long b : {256ull << 20, 1ull << 30, 4ull << 30}) {
+        run<1>(tab, b, out);
+        run<4>(tab, b, out);
+        run<8>(tab, b, out);
+        run<16>(tab, b, out);
+    }
+    hipFree(tab);
+    hipFree(out);
+    return 0;
+}

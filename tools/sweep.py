@@ -1,0 +1,157 @@
+"""Kernel-parameter sweep on one GPU (development tool, not the product or the bench).
+
+    python tools/sweep.py build                      # here: compile the variants (hipcc, gfx950)
+    python tools/sweep.py run [--config C] [...]     # on the GPU box: time every variant
+
+Each variant is the same engine.cpp + kernels compiled with different -D knobs into
+emqx_amd/variants/libemqx_tm_<name>.so (git-ignored, travels to the box like the product
+.so), optionally with a different edge-table load (tm_config.edge_load_inv).  The workload
+is generated once; every variant builds its own index, runs warm-up + timed batches through
+tm_match_device and reports the k_match_fast time (HIP events on its stream), the batch
+time and the walk counters.  Results are checked against the product build's key counts.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+VDIR = os.path.join(ROOT, "emqx_amd", "variants")
+CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
+
+# name -> (extra hipcc flags, edge_load_inv)
+# "head": the committed match_kernels.hip (git HEAD) with the working tree's engine, as the
+# same-process reference point.
+VARIANTS = {
+    "head": ([], 0),
+    "diet": ([], 0),
+    "diet_load8": ([], 8),
+    "diet_load16": ([], 16),
+    "w20": (["-DTM_SCAP=64", "-DTM_TBCAP=2560", "-DTM_MIN_WAVES=5"], 0),
+    "w20_load16": (["-DTM_SCAP=64", "-DTM_TBCAP=2560", "-DTM_MIN_WAVES=5"], 16),
+    "w24": (["-DTM_SCAP=64", "-DTM_TBCAP=2048", "-DTM_MIN_WAVES=6"], 0),
+    "w20b": (["-DTM_SCAP=48", "-DTM_TBCAP=3072", "-DTM_MIN_WAVES=5"], 0),
+}
+
+
+def build(names):
+    os.makedirs(VDIR, exist_ok=True)
+    procs = []
+    for name in names:
+        flags, _ = VARIANTS[name]
+        out = os.path.join(VDIR, f"libemqx_tm_{name}.so")
+        kern = os.path.join(CSRC, "match_kernels.hip")
+        if name == "head":
+            kern = os.path.join(CSRC, "_head_match_kernels.hip")
+            with open(kern, "w") as f:
+                f.write(subprocess.check_output(["git", "-C", ROOT, "show", "HEAD:emqx_amd/csrc/match_kernels.hip"],
+                                                text=True))
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-Wno-unused-function", *flags, os.path.join(CSRC, "engine.cpp"),
+               kern, os.path.join(CSRC, "result_kernels.hip"), "-o", out]
+        procs.append((name, subprocess.Popen(cmd)))
+        if len(procs) >= 4:
+            n, p = procs.pop(0)
+            assert p.wait() == 0, n
+    for n, p in procs:
+        assert p.wait() == 0, n
+
+
+def run(args):
+    import numpy as np
+    import torch
+
+    from emqx_amd import workloads
+    w = workloads.generate(args.config, scale=args.scale, n_topics=args.batch)
+    tb, to = w.topic_slice(0, args.batch)
+    n = args.batch
+    dev = torch.device("cuda", 0)
+    d_bytes = torch.from_numpy(tb).to(dev)
+    d_off = torch.from_numpy(to.view(np.int32)).to(dev)
+    stream = torch.cuda.Stream(dev)
+    import importlib
+    results = []
+    for name in args.variants:
+        lib = os.path.join(VDIR, f"libemqx_tm_{name}.so")
+        os.environ["EMQX_TM_LIB"] = lib
+        from emqx_amd import _native
+        importlib.reload(_native)
+        N = _native
+        t0 = time.time()
+        eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4, edge_load_inv=VARIANTS[name][1])
+        eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+        eng.commit()
+        tbuild = time.time() - t0
+        sp = stream.cuda_stream
+
+        def step():
+            return eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, int(to[-1]), sp)
+
+        r = step()
+        eng.device_sync()
+        total = _read_u64(r.d_total)
+        if total > r.keys_cap:
+            eng.reserve_matches(int(total * 1.1) + 1024)
+        for _ in range(3):
+            step()
+        eng.device_sync()
+        torch.cuda.synchronize()
+        eng.debug_stats(True, read=False)
+        step()
+        torch.cuda.synchronize()
+        walk = dict(zip(N.Engine.STAT_NAMES, [int(x) for x in eng.debug_stats(False)]))
+        eng.debug_stats(False, read=False)
+        kms = []
+        for _ in range(args.steps):
+            eng.timing(True)
+            step()
+            torch.cuda.synchronize()
+            kms.append(eng.timing(False))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        bms = (time.perf_counter() - t0) / args.steps * 1e3
+        st = eng.stats()
+        rec = {"variant": name, "kernel_ms": round(float(np.mean(kms)), 4), "kernel_ms_min": round(float(min(kms)), 4),
+               "batch_ms": round(bms, 4), "keys": walk["keys"], "edge_probes": walk["edge_probes"],
+               "word_probes": walk["word_probes"], "edge_slots": st["edge_slots"], "build_s": round(tbuild, 1),
+               "cyc": [walk["cyc_prescan"], walk["cyc_walk"], walk["cyc_copyout"]]}
+        print(json.dumps(rec), flush=True)
+        results.append(rec)
+        eng.close()
+        del eng
+    keys = {r["keys"] for r in results}
+    print(json.dumps({"consistent_key_counts": len(keys) == 1}), flush=True)
+
+
+def _read_u64(ptr):
+    import torch
+    h = torch.empty(1, dtype=torch.int64)
+    lib = C.CDLL("libamdhip64.so")
+    lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert lib.hipMemcpy(C.c_void_p(h.data_ptr()), C.c_void_p(ptr), 8, 2) == 0
+    return int(h.item())
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=("build", "run"))
+    ap.add_argument("--variants", nargs="*", default=list(VARIANTS))
+    ap.add_argument("--config", default="C")
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--batch", type=int, default=1_000_000)
+    ap.add_argument("--steps", type=int, default=10)
+    a = ap.parse_args()
+    if a.cmd == "build":
+        build(a.variants)
+    else:
+        import torch  # noqa: F401  (torch's HIP runtime first: see emqx_amd/_native.py)
+        run(a)
