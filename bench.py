@@ -129,9 +129,14 @@ def main():
     ap.add_argument("--mode", choices=("replicated", "sharded"), default="replicated",
                     help="replicated trie, publishes data-parallel (default); or filters hash-sharded over "
                          "ranks with an RCCL all-gather merge (config D; DESIGN.md §6)")
+    ap.add_argument("--churn", type=int, default=0, metavar="EPOCHS",
+                    help="config-E style run: EPOCHS delta epochs of 1%% adds + 1%% deletes, each committed "
+                         "between match batches (commit and match timed separately)")
     args = ap.parse_args()
     if args.mode == "sharded":
         return run_sharded(args)
+    if args.churn:
+        return run_churn(args)
 
     import torch
     import torch.distributed as dist
@@ -228,6 +233,36 @@ def main():
     eng.device_sync()
     slow_topics = eng.stats()["n_slow_topics"]
 
+    # ---------------------------------------------------------------- latency vs batch size
+    # (not the metric: the batching window's trade-off); rank 0 only
+    lat_sweep = []
+    host_path = None
+    if rank == 0 and not args.profile:
+        for bs in (1024, 16384, 131072):
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(30)]
+            tbb = int(to[bs])
+            for k in range(35):
+                if k >= 5:
+                    ev[k - 5][0].record(stream)
+                eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), bs, tbb, sp)
+                if k >= 5:
+                    ev[k - 5][1].record(stream)
+            torch.cuda.synchronize()
+            ms = np.array([a.elapsed_time(b) for a, b in ev])
+            lat_sweep.append({"batch": bs, "p50_ms": round(float(np.percentile(ms, 50)), 4),
+                              "p99_ms": round(float(np.percentile(ms, 99)), 4),
+                              "publishes_per_s": round(bs / (float(np.mean(ms)) * 1e-3), 1)})
+        # host buffers in, host results out (H2D + kernels + D2H of every key): PCIe-inclusive
+        eng.match_packed(tb, to)
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            eng.match_packed(tb, to)
+        dt = (time.perf_counter() - t0) / reps
+        host_path = {"api": "tm_match_batch", "batch": n, "ms_per_batch": round(dt * 1e3, 3),
+                     "publishes_per_s": round(n / dt, 1),
+                     "note": "host topic bytes in, host key lists out; bounded by PCIe D2H of the keys"}
+
     # ---------------------------------------------------------------- CPU baseline + parity sample
     cpu = None
     parity = None
@@ -278,6 +313,8 @@ def main():
                 "walk": walk,
             },
             "gather": gather_roof(walk, kernel_ms),
+            "latency_vs_batch": lat_sweep,
+            "host_path": host_path,
             "cpu_baseline": cpu,
             "parity": parity,
             "spill_topics": int(slow_topics),
@@ -357,6 +394,117 @@ def run_sharded(args):
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _new_filter(f, n):
+    """A new, VALID filter near f (emqx_topic:validate/1 rejects a '#' that is not the last
+    level, emqx_topic.erl:206-207): one more level, inserted before a trailing '#'."""
+    if f == b"#":
+        return b"n%d/#" % n
+    if f.endswith(b"/#"):
+        return f[:-2] + b"/n%d/#" % n
+    return f + b"/n%d" % n
+
+
+def run_churn(args):
+    """Live subscribe/unsubscribe churn (BASELINE configs[4]): every epoch deletes 1% of the
+    live route keys and adds 1% new ones (half are new dests on existing filters, like a
+    $share group joining: emqx_shared_sub.erl:450; half new filter strings), commits them as
+    one delta epoch (tm_commit_epoch: host trie update + stream-ordered device patch), then
+    matches a batch.  Rank 0, one GPU.  The last epoch is checked against the oracle on a
+    sample of the batch."""
+    import torch
+
+    from emqx_amd import _native as N
+    from emqx_amd import shard as S
+    from emqx_amd import workloads
+    cfg = args.config if args.config != "C" else "E"
+    w = workloads.generate(cfg, scale=args.scale, n_topics=args.batch)
+    dev = torch.device("cuda", 0)
+    eng = N.Engine(0, reserve_keys=w.n_keys * 2, reserve_nodes=w.n_keys * 8)
+    t0 = time.time()
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    t_build = time.time() - t0
+    n = w.n_topics
+    d_bytes = torch.from_numpy(w.t_bytes).to(dev)
+    d_off = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
+    stream = torch.cuda.Stream(dev)
+    sp = stream.cuda_stream
+    rng = np.random.default_rng(0xE11A0005)
+    # live key set as packed arrays: (filter bytes list, ids)
+    fl = w.filters()
+    live_f = list(fl)
+    live_id = w.f_id.astype(np.uint64).copy()
+    next_id = int(live_id.max()) + 1
+    commit_ms, match_ms, nops = [], [], []
+
+    def pack(fs, ids):
+        off = np.zeros(len(fs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(f) for f in fs])
+        return np.frombuffer(b"".join(fs) + b"\0" * 16, dtype=np.uint8), off, np.asarray(ids, dtype=np.uint64)
+
+    r = eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, int(w.t_off[-1]), sp)
+    eng.device_sync()
+    tot = _read_u64(r.d_total)
+    eng.reserve_matches(int(tot * 1.5) + 1024)
+    for ep in range(args.warmup + args.churn):
+        k = max(1, len(live_id) // 100)
+        dsel = rng.choice(len(live_id), size=k, replace=False)
+        keep = np.ones(len(live_id), dtype=bool)
+        keep[dsel] = False
+        del_f = [live_f[i] for i in dsel]
+        del_id = live_id[dsel]
+        src = rng.integers(0, len(fl), size=k)
+        add_f = [fl[j] if (i & 1) else _new_filter(fl[j], next_id + i) for i, j in enumerate(src)]
+        add_id = np.arange(next_id, next_id + k, dtype=np.uint64)
+        next_id += k
+        db, do, di = pack(del_f, del_id)
+        ab, ao, ai = pack(add_f, add_id)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.apply_packed(N.TM_OP_DEL, db, do, di)
+        eng.apply_packed(N.TM_OP_ADD, ab, ao, ai)
+        eng.commit()
+        t1 = time.perf_counter()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        r = eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, int(w.t_off[-1]), sp)
+        e1.record(stream)
+        eng.device_sync()
+        torch.cuda.synchronize()
+        if _read_u64(r.d_total) > r.keys_cap:
+            raise RuntimeError("output arena overflow during churn bench")
+        live_f = [f for f, kk in zip(live_f, keep) if kk] + add_f
+        live_id = np.concatenate([live_id[keep], add_id])
+        if ep >= args.warmup:
+            commit_ms.append((t1 - t0) * 1e3)
+            match_ms.append(e0.elapsed_time(e1))
+            nops.append(2 * k)
+    # parity of the last epoch on a sample
+    import oracle
+    ps = min(n, 20000)
+    lb, lo, li = pack(live_f, live_id)
+    ix = oracle.OrderedIndex(lb, lo, li)
+    eo, eids, _ = ix.match(w.t_bytes, w.t_off[:ps + 1], threads=16)
+    off, cnt, keys, _ = eng.match_packed(w.t_bytes, w.t_off[:ps + 1])
+    ids = eng.key_ids(keys)
+    bad = sum(not np.array_equal(np.sort(ids[off[i]:off[i] + cnt[i]]), eids[eo[i]:eo[i + 1]]) for i in range(ps))
+    st = eng.stats()
+    print(json.dumps({
+        "metric": "delta-epoch churn: route ops/s committed + matched publishes/s between epochs",
+        "config": {"workload": f"{cfg} (scale {args.scale}): {w.n_keys} initial route keys, 1% adds + 1% deletes "
+                               f"per epoch", "publishes_per_batch": n},
+        "epochs": args.churn, "ops_per_epoch": int(np.mean(nops)),
+        "commit_ms_p50": round(float(np.percentile(commit_ms, 50)), 3),
+        "commit_ms_p99": round(float(np.percentile(commit_ms, 99)), 3),
+        "route_ops_per_s": round(float(np.sum(nops) / (np.sum(commit_ms) * 1e-3)), 1),
+        "match_ms_p50": round(float(np.percentile(match_ms, 50)), 4),
+        "publishes_per_s_incl_commit": round(n * len(match_ms) / ((np.sum(match_ms) + np.sum(commit_ms)) * 1e-3), 1),
+        "full_rebuilds": st["n_full_rebuilds"], "delta_commits": st["n_delta_commits"],
+        "build_s": round(t_build, 2),
+        "parity": {"sampled_topics": ps, "mismatches": int(bad), "oracle": "oracle/trie_search.cpp"},
+    }), flush=True)
 
 
 def _read_u64(ptr):

@@ -163,6 +163,7 @@ struct tm_engine {
     std::vector<uint64_t> dirty_eslots, dirty_wslots, dirty_lists;
     bool root_dirty = true;
     bool need_full = true;  // full device upload at next commit
+    bool words_full = false;  // word table rehashed: re-upload it whole at next commit
 
     // ---- device copy
     DevBuf d_wtab, d_warena, d_word_off, d_etab, d_slot_list, d_root, d_arena;
@@ -224,7 +225,7 @@ struct tm_engine {
                 while (wtab[s].wid != NONE) s = (s + 1) & wmask;
                 wtab[s] = w;
             }
-        need_full = true;
+        words_full = true;  // only the word table is re-uploaded (word ids do not change)
     }
     uint32_t word_intern(const uint8_t *p, uint32_t len) {
         uint32_t wid = word_lookup(p, len);
@@ -719,7 +720,12 @@ struct tm_engine {
         if ((e = put_tail(d_warena, warena, warena_dev))) return e;
         if ((e = put_tail(d_word_off, word_off, word_off_dev))) return e;
         if ((e = put_tail(d_arena, arena, arena_dev))) return e;
-        if ((e = scatter16(dirty_wslots, wtab, d_wtab.p))) return e;
+        if (words_full) {
+            if ((e = put(d_wtab, wtab, 1, 1))) return e;
+            dirty_wslots.clear();
+        } else if ((e = scatter16(dirty_wslots, wtab, d_wtab.p))) {
+            return e;
+        }
         if ((e = scatter16(dirty_eslots, etab, d_etab.p))) return e;
         if ((e = scatter4(dirty_lists, slot_list, d_slot_list.p))) return e;
         if ((e = upload_key_ids_delta())) return e;
@@ -749,6 +755,7 @@ struct tm_engine {
         if (need_full) n_full_rebuilds++;
         else n_delta_commits++;
         need_full = false;
+        words_full = false;
         root_dirty = false;
         dirty_eslots.clear();
         dirty_wslots.clear();

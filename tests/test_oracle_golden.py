@@ -137,6 +137,27 @@ def test_trie_restatement_equals_brute_force_config_e_sys_share():
     assert any(t.startswith(b"$SYS/") and o1[i + 1] > o1[i] for i, t in enumerate(topics))
 
 
+def test_reference_seek_quirk_with_invalid_filter():
+    """emqx_trie_search's seek (compare/3, emqx_trie_search.erl:340-347) and match/2 disagree
+    when an INVALID filter with '#' before its last level is in the table: for topic
+    "a/b", key "a/#/x" makes compare/3 return {1, <<"b">>} (an atom sorts below a binary),
+    and the seek to ["a", <<"b">>] jumps past the valid key "a/+/#".  The restatement keeps
+    that reference behaviour; match/2 (and the engine) match "a/+/#".  Every subscribe
+    path validates filters first (emqx_topic:validate/1 rejects the '#', emqx_topic.erl:
+    206-207), so a route table never holds such a key; the churn bench generates only
+    valid filters for that reason."""
+    filters = [b"a/+/#", b"a/#/x"]
+    ix = oracle.OrderedIndex.from_filters(filters)
+    buf = np.frombuffer(b"a/b\0", dtype=np.uint8)
+    off = np.array([0, 3], dtype=np.uint32)
+    assert ix.match(buf, off, algo=oracle.ALGO_TRIE)[1].tolist() == []
+    assert ix.match(buf, off, algo=oracle.ALGO_BRUTE)[1].tolist() == [0]
+    assert et.match(b"a/b", b"a/+/#") and not et.match(b"a/b", b"a/#/x")
+    # without the invalid key both algorithms agree
+    ix2 = oracle.OrderedIndex.from_filters(filters[:1])
+    assert ix2.match(buf, off, algo=oracle.ALGO_TRIE)[1].tolist() == [0]
+
+
 # ------------------------------------------- property (bidirectional t_prop_matches)
 # Generator shape of emqx_topic_index_SUITE:topic_t/topic_filter_pattern_t (:381-419):
 # per-level entropy [1,2,3,4], fixed words foo/bar/baz/xyzzy, level:'+':'#' = 5:2:1.

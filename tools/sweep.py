@@ -30,13 +30,10 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 # same-process reference point.
 VARIANTS = {
     "head": ([], 0),
-    "diet": ([], 0),
-    "diet_load8": ([], 8),
-    "diet_load16": ([], 16),
-    "w20": (["-DTM_SCAP=64", "-DTM_TBCAP=2560", "-DTM_MIN_WAVES=5"], 0),
-    "w20_load16": (["-DTM_SCAP=64", "-DTM_TBCAP=2560", "-DTM_MIN_WAVES=5"], 16),
-    "w24": (["-DTM_SCAP=64", "-DTM_TBCAP=2048", "-DTM_MIN_WAVES=6"], 0),
-    "w20b": (["-DTM_SCAP=48", "-DTM_TBCAP=3072", "-DTM_MIN_WAVES=5"], 0),
+    "nosplit": (["-DTM_SPLIT=0"], 0),
+    "split": (["-DTM_SPLIT=1"], 0),
+    "split_cp16": (["-DTM_SPLIT=1", "-DTM_CP_UNROLL=16"], 0),
+    "split_load16": (["-DTM_SPLIT=1"], 16),
 }
 
 
