@@ -260,6 +260,14 @@ class Engine:
              else np.zeros(0, dtype=np.uint32))
         return o, c, k, st
 
+    def match_packed_view(self, buf: np.ndarray, off: np.ndarray, mode: int = TM_MATCH_ALL) -> tm_result:
+        """tm_match_batch without copying: the engine-owned tm_result (valid until the next
+        call on this engine).  For timing the C-ABI host path."""
+        res = tm_result()
+        self._check(self.lib.tm_match_batch(self.h, buf.ctypes.data, off.ctypes.data, len(off) - 1, mode,
+                                            C.byref(res)))
+        return res
+
     def match(self, topics, mode: int = TM_MATCH_ALL):
         """List of topics -> list of key-handle lists (None for badarg topics)."""
         buf, off = pack_topics(topics)
