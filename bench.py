@@ -237,6 +237,7 @@ def main():
     # (not the metric: the batching window's trade-off); rank 0 only
     lat_sweep = []
     host_path = None
+    mode_rates = {}
     if rank == 0 and not args.profile:
         for bs in (1024, 16384, 131072):
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(30)]
@@ -252,6 +253,19 @@ def main():
             lat_sweep.append({"batch": bs, "p50_ms": round(float(np.percentile(ms, 50)), 4),
                               "p99_ms": round(float(np.percentile(ms, 99)), 4),
                               "publishes_per_s": round(bs / (float(np.mean(ms)) * 1e-3), 1)})
+        # the other reducers on the same batch: return_first (k_match_first) and counts only
+        for mname, mode in (("first", N.TM_MATCH_FIRST), ("count", N.TM_MATCH_COUNT)):
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+            for k in range(12):
+                if k >= 2:
+                    ev[k - 2][0].record(stream)
+                eng.match_device_mode(d_bytes.data_ptr(), d_off.data_ptr(), n, topic_bytes, mode, sp)
+                if k >= 2:
+                    ev[k - 2][1].record(stream)
+            torch.cuda.synchronize()
+            ms = np.array([a.elapsed_time(b) for a, b in ev])
+            mode_rates[mname] = {"ms_per_batch": round(float(np.mean(ms)), 4),
+                                 "publishes_per_s": round(n / (float(np.mean(ms)) * 1e-3), 1)}
         # host buffers in, host results out (H2D + kernels + D2H of every key): PCIe-inclusive
         to32 = np.ascontiguousarray(to, dtype=np.uint32)
         eng.match_packed_view(tb, to32)
@@ -316,6 +330,7 @@ def main():
             "gather": gather_roof(walk, kernel_ms),
             "latency_vs_batch": lat_sweep,
             "host_path": host_path,
+            "other_modes": mode_rates,
             "cpu_baseline": cpu,
             "parity": parity,
             "spill_topics": int(slow_topics),

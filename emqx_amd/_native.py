@@ -17,7 +17,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # EMQX_TM_LIB: path of an alternative build of the same library (kernel-parameter sweeps
-# by tools/variants.py); unset = the in-tree product build.
+# by tools/sweep.py); unset = the in-tree product build.
 LIB_PATH = os.environ.get("EMQX_TM_LIB") or os.path.join(HERE, "libemqx_tm.so")
 
 TM_OK = 0
@@ -37,6 +37,7 @@ TM_KEY_WORDS = 1
 TM_MATCH_ALL = 0
 TM_MATCH_UNIQUE = 1
 TM_MATCH_FIRST = 2
+TM_MATCH_COUNT = 3
 
 TM_CFG_FORCE_SLOW = 1
 
@@ -45,7 +46,7 @@ EXPORTS = (
     "tm_abi_version", "tm_create", "tm_destroy", "tm_last_error", "tm_apply", "tm_apply_packed",
     "tm_commit_epoch", "tm_match_batch", "tm_match_device", "tm_device_sync",
     "tm_reserve_matches", "tm_key_info", "tm_key_ids", "tm_stats", "tm_debug_stats", "tm_debug_timing",
-    "tm_result_ids_device", "tm_merge_shards_device", "tm_merge_shards",
+    "tm_result_ids_device", "tm_merge_shards_device", "tm_merge_shards", "tm_match_device_mode",
 )
 
 
@@ -116,6 +117,8 @@ def load() -> C.CDLL:
     lib.tm_match_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64,
                                     C.c_void_p, P(tm_dev_result)]
     lib.tm_device_sync.argtypes = [C.c_void_p]
+    lib.tm_match_device_mode.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
+                                         C.c_void_p, P(tm_dev_result)]
     lib.tm_reserve_matches.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32]
     lib.tm_key_info.argtypes = [C.c_void_p, C.c_uint32, P(C.c_uint64), P(C.c_uint32), C.c_void_p,
                                 C.c_uint32, P(C.c_uint32)]
@@ -334,6 +337,12 @@ class Engine:
         self._check(self.lib.tm_merge_shards_device(self.h, G, n, C.c_void_p(d_counts), C.c_void_p(d_ids), stride,
                                                     C.c_void_p(d_out_off), C.c_void_p(d_out_ids), out_cap,
                                                     C.c_void_p(stream) if stream else None))
+
+    def match_device_mode(self, d_bytes: int, d_off: int, n: int, total_bytes: int, mode: int, stream: int = 0):
+        r = tm_dev_result()
+        self._check(self.lib.tm_match_device_mode(self.h, C.c_void_p(d_bytes), C.c_void_p(d_off), n, total_bytes,
+                                                  mode, C.c_void_p(stream) if stream else None, C.byref(r)))
+        return r
 
     def device_sync(self):
         self._check(self.lib.tm_device_sync(self.h))

@@ -8,6 +8,7 @@
 
 namespace tmx {
 
+constexpr uint32_t MODE_ALL = 0, MODE_COUNT = 1, MODE_FIRST = 2;  // MatchArgs.mode
 constexpr int SEG_CHUNK = 128;  // key segments per global chunk (16 B each)
 constexpr int SEG_MAXCHUNK = 128;  // segment chunks one wave may flush (its list lives in HBM)
 constexpr int FR_CHUNK = 256;   // frontier entries per global overflow chunk (8 B each)
@@ -19,6 +20,7 @@ struct MatchArgs {
     const uint32_t *off;
     uint32_t n;
     uint32_t force_slow;  // 1: every topic takes the spill kernel (test aid)
+    uint32_t mode;        // MODE_ALL: every key; MODE_COUNT: counts only; MODE_FIRST: k_match_first
     // frozen index
     const WordSlot *wtab;
     uint64_t wmask;
@@ -29,6 +31,8 @@ struct MatchArgs {
     const uint32_t *slot_list; // node (= slot) -> first key of its list in the arena
     const RootRec *root;
     const uint32_t *arena;
+    const uint64_t *key_id;    // key handle -> caller id (MODE_FIRST: smallest id wins)
+    const uint32_t *key_bin;   // key handle -> 1 for {Binary, {ID}} keys (sort after word lists)
     // results
     uint32_t *out_off;
     uint32_t *out_cnt;

@@ -170,6 +170,7 @@ struct tm_engine {
     size_t word_off_dev = 0;  // entries already on device
     DevBuf d_scatter_idx, d_scatter_src;
     DevBuf d_key_id;                  // key handle -> caller id (u64), for device-side id results
+    DevBuf d_key_bin;                 // key handle -> 1 for {Binary, {ID}} keys (u32; FIRST order)
     std::vector<uint64_t> dirty_kid;  // handles (re)assigned since the last upload
     DevBuf d_res_scan, d_mrg_roff, d_mrg_tot;  // scratch of tm_result_ids_device / tm_merge_shards_device
     // batch buffers
@@ -521,14 +522,33 @@ struct tm_engine {
         }
     }
 
-    // Append one list ([term_cnt, hash_cnt] header, term keys, hash keys) to the arena.
+    // The list header (layout.h LIST_HDR words before the first key):
+    //   [min bin-term key, min word-term key, min '#' key, term_cnt, hash_cnt]
+    // where "min" = the key with the smallest id of that kind (NONE if none).  A node's keys
+    // all spell the same filter per kind, so these are the return_first candidates
+    // (k_match_first) without scanning the list.
+    void write_header(uint32_t pos, const uint32_t *terms, uint32_t tc, const uint32_t *hashes, uint32_t hc) {
+        uint32_t mb = NONE, mw = NONE, mh = NONE;
+        auto take = [&](uint32_t &m, uint32_t h) {
+            if (m == NONE || keys[h].id < keys[m].id) m = h;
+        };
+        for (uint32_t i = 0; i < tc; i++) take(keys[terms[i]].kind == K_EXACT_BIN ? mb : mw, terms[i]);
+        for (uint32_t i = 0; i < hc; i++) take(mh, hashes[i]);
+        arena[pos - 5] = mb;
+        arena[pos - 4] = mw;
+        arena[pos - 3] = mh;
+        arena[pos - 2] = tc;
+        arena[pos - 1] = hc;
+    }
+
+    // Append one list (header, term keys, hash keys) to the arena.
     NodeList append_list(const uint32_t *terms, uint32_t tc, const uint32_t *hashes, uint32_t hc) {
         if (tc + hc == 0) return NodeList{0, 0, 0};
-        arena.push_back(tc);
-        arena.push_back(hc);
+        arena.resize(arena.size() + LIST_HDR);
         const uint32_t off = (uint32_t)arena.size();
         arena.insert(arena.end(), terms, terms + tc);
         arena.insert(arena.end(), hashes, hashes + hc);
+        write_header(off, terms, tc, hashes, hc);
         return NodeList{off, tc, hc};
     }
 
@@ -547,18 +567,12 @@ struct tm_engine {
         uint64_t total = 0;
         for (size_t v = 0; v < nn; v++) {
             const uint32_t n = tcnt[v] + hcnt[v];
-            pos[v] = n ? (uint32_t)(total + 2) : 0u;
-            total += n ? n + 2 : 0;
+            pos[v] = n ? (uint32_t)(total + LIST_HDR) : 0u;
+            total += n ? n + LIST_HDR : 0;
         }
         arena.assign(total, 0);
         std::vector<uint32_t> tfill(pos), hfill(nn);
-        for (size_t v = 0; v < nn; v++) {
-            hfill[v] = pos[v] + tcnt[v];
-            if (pos[v]) {
-                arena[pos[v] - 2] = tcnt[v];
-                arena[pos[v] - 1] = hcnt[v];
-            }
-        }
+        for (size_t v = 0; v < nn; v++) hfill[v] = pos[v] + tcnt[v];
         for (size_t h = 0; h < keys.size(); h++) {
             const KeyRec &k = keys[h];
             if (k.kind == K_FREE || k.kind == K_DEAD) continue;
@@ -567,6 +581,7 @@ struct tm_engine {
         }
         for (size_t v = 0; v < nn; v++) {
             node_list[v] = NodeList{pos[v], tcnt[v], hcnt[v]};
+            if (pos[v]) write_header(pos[v], &arena[pos[v]], tcnt[v], &arena[pos[v] + tcnt[v]], hcnt[v]);
             refresh_info((uint32_t)v);
         }
         arena_garbage = 0;
@@ -596,7 +611,7 @@ struct tm_engine {
                     if (it != Lst.end()) Lst.erase(it);
                 }
             }
-            arena_garbage += r.term_cnt + r.hash_cnt + (r.term_cnt + r.hash_cnt ? 2 : 0);
+            arena_garbage += r.term_cnt + r.hash_cnt + (r.term_cnt + r.hash_cnt ? LIST_HDR : 0);
             node_list[node] = append_list(terms.data(), (uint32_t)terms.size(), hashes.data(), (uint32_t)hashes.size());
             refresh_info(node);
             i = j;
@@ -639,23 +654,31 @@ struct tm_engine {
 
     hipError_t upload_key_ids_full() {
         std::vector<uint64_t> ids(keys.size());
-        for (size_t h = 0; h < keys.size(); h++) ids[h] = keys[h].id;
+        std::vector<uint32_t> bin(keys.size());
+        for (size_t h = 0; h < keys.size(); h++) {
+            ids[h] = keys[h].id;
+            bin[h] = keys[h].kind == K_EXACT_BIN ? 1u : 0u;
+        }
         dirty_kid.clear();
         hipError_t e = put(d_key_id, ids);
         if (e) return e;
-        return hipStreamSynchronize(stream);  // `ids` dies at scope exit
+        if ((e = put(d_key_bin, bin))) return e;
+        return hipStreamSynchronize(stream);  // `ids`, `bin` die at scope exit
     }
 
     hipError_t upload_key_ids_delta() {
         if (dirty_kid.empty()) return hipSuccess;
-        if (keys.size() * sizeof(uint64_t) > d_key_id.cap) return upload_key_ids_full();
+        if (keys.size() * sizeof(uint64_t) > d_key_id.cap || keys.size() * sizeof(uint32_t) > d_key_bin.cap)
+            return upload_key_ids_full();
         std::sort(dirty_kid.begin(), dirty_kid.end());
         dirty_kid.erase(std::unique(dirty_kid.begin(), dirty_kid.end()), dirty_kid.end());
         const size_t n = dirty_kid.size();
         std::vector<uint64_t> idx(n), src(n);
+        std::vector<uint32_t> bin(n);
         for (size_t i = 0; i < n; i++) {
             idx[i] = dirty_kid[i];
             src[i] = keys[dirty_kid[i]].id;
+            bin[i] = keys[dirty_kid[i]].kind == K_EXACT_BIN ? 1u : 0u;
         }
         dirty_kid.clear();
         hipError_t e;
@@ -665,6 +688,11 @@ struct tm_engine {
         if ((e = hipMemcpyAsync(d_scatter_src.p, src.data(), n * 8, hipMemcpyHostToDevice, stream))) return e;
         if ((e = launch_scatter8(d_key_id.as<uint64_t>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint64_t>(),
                                  n, stream)))
+            return e;
+        if ((e = hipStreamSynchronize(stream))) return e;  // d_scatter_src is reused below
+        if ((e = hipMemcpyAsync(d_scatter_src.p, bin.data(), n * 4, hipMemcpyHostToDevice, stream))) return e;
+        if ((e = launch_scatter4(d_key_bin.as<uint32_t>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint32_t>(), n,
+                                 stream)))
             return e;
         return hipStreamSynchronize(stream);
     }
@@ -896,7 +924,7 @@ void tm_destroy(tm_engine *eng) {
     if (!eng) return;
     (void)hipSetDevice(eng->cfg.device);
     if (eng->stream) (void)hipStreamSynchronize(eng->stream);
-    for (DevBuf *b : {&eng->d_key_id, &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot})
+    for (DevBuf *b : {&eng->d_key_id, &eng->d_key_bin, &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
                       &eng->d_arena, &eng->d_scatter_idx,
@@ -1016,8 +1044,11 @@ static int grow_pools(tm_engine *eng) {
 }
 
 static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
-                                hipStream_t s) {
+                                hipStream_t s, uint32_t mode = MODE_ALL) {
     MatchArgs a{};
+    a.mode = mode;
+    a.key_id = eng->d_key_id.as<uint64_t>();
+    a.key_bin = eng->d_key_bin.as<uint32_t>();
     a.bytes = d_bytes;
     a.off = d_off;
     a.n = n;
@@ -1057,7 +1088,7 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
 int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
                    tm_result *out) {
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
-    if (mode > TM_MATCH_FIRST) return TM_EINVAL;
+    if (mode > TM_MATCH_COUNT) return TM_EINVAL;
     if (!eng->staged.empty()) {
         eng->err = "tm_match_batch: staged ops not committed";
         return TM_ESTATE;
@@ -1083,9 +1114,15 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
                "H2D");
     TM_TRY_HIP(hipMemcpyAsync(eng->d_off.p, ho, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
     TM_TRY_HIP(eng->h_cursor.ensure(64), TM_ENOMEM, "pinned alloc");
+    // FIRST runs k_match_first (<= 1 key per topic); COUNT skips the key copy-out
+    const uint32_t kmode = mode == TM_MATCH_FIRST ? MODE_FIRST : (mode == TM_MATCH_COUNT ? MODE_COUNT : MODE_ALL);
+    if (kmode == MODE_FIRST && eng->keys_cap < n) {
+        TM_TRY_HIP(eng->d_keys.ensure((uint64_t)n * 4), TM_ENOMEM, "alloc keys");
+        eng->keys_cap = n;
+    }
     for (int attempt = 0; attempt < 2; attempt++) {
         eng->last_n = n;
-        TM_TRY_HIP(enqueue_match(eng, eng->d_bytes.as<uint8_t>(), eng->d_off.as<uint32_t>(), n, s), TM_EDEVICE,
+        TM_TRY_HIP(enqueue_match(eng, eng->d_bytes.as<uint8_t>(), eng->d_off.as<uint32_t>(), n, s, kmode), TM_EDEVICE,
                    "kernel launch");
         TM_TRY_HIP(hipMemcpyAsync(eng->h_cursor.p, eng->d_cursor.p, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
         TM_TRY_HIP(hipMemcpyAsync((uint8_t *)eng->h_cursor.p + 8, eng->d_slow_count.p, 4, hipMemcpyDeviceToHost, s),
@@ -1099,14 +1136,14 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
         eng->n_slow_last = *(uint32_t *)((uint8_t *)eng->h_cursor.p + 8);
         eng->seg_demand_last = *(uint64_t *)((uint8_t *)eng->h_cursor.p + 16);
         eng->fr_demand_last = *(uint64_t *)((uint8_t *)eng->h_cursor.p + 24);
-        if (total <= eng->keys_cap) break;
+        if (kmode != MODE_ALL || total <= eng->keys_cap) break;
         // output arena too small: grow to the demand and run again (once suffices:
         // the cursor counts every key the batch asked for)
         uint64_t want = total + total / 8 + 1024;
         TM_TRY_HIP(eng->d_keys.ensure(want * 4), TM_ENOMEM, "alloc keys");
         eng->keys_cap = want;
     }
-    uint64_t total = *eng->h_cursor.as<uint64_t>();
+    uint64_t total = kmode == MODE_ALL ? *eng->h_cursor.as<uint64_t>() : (kmode == MODE_FIRST ? n : 0);
     TM_TRY_HIP(eng->h_outoff.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(eng->h_outcnt.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(eng->h_status.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
@@ -1128,8 +1165,27 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
     out->keys = eng->h_keys.as<uint32_t>();
     out->status = eng->h_status.as<int32_t>();
     if (mode == TM_MATCH_ALL) return TM_OK;
+    if (mode == TM_MATCH_COUNT) {  // counts only: no keys
+        eng->pp_off.assign(n, 0);
+        out->off = eng->pp_off.data();
+        out->keys = nullptr;
+        out->total = 0;
+        return TM_OK;
+    }
+    if (mode == TM_MATCH_FIRST) {  // k_match_first wrote topic i's key (if any) at keys[i]: compact
+        eng->pp_off.resize(n);
+        eng->pp_keys.clear();
+        for (uint32_t i = 0; i < n; i++) {
+            eng->pp_off[i] = (uint32_t)eng->pp_keys.size();
+            if (out->cnt[i]) eng->pp_keys.push_back(out->keys[i]);
+        }
+        out->off = eng->pp_off.data();
+        out->keys = eng->pp_keys.data();
+        out->total = eng->pp_keys.size();
+        return TM_OK;
+    }
 
-    // UNIQUE / FIRST: reduce each topic's set under ETS term order.
+    // UNIQUE: reduce each topic's set under ETS term order.
     eng->pp_off.resize(n);
     eng->pp_cnt.resize(n);
     eng->pp_keys.clear();
@@ -1182,6 +1238,12 @@ int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap) {
 
 int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                     uint64_t total_bytes, void *stream, tm_dev_result *out) {
+    return tm_match_device_mode(eng, d_bytes, d_off, n, total_bytes, TM_MATCH_ALL, stream, out);
+}
+
+int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                         uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out) {
+    if (mode != TM_MATCH_ALL && mode != TM_MATCH_FIRST && mode != TM_MATCH_COUNT) return TM_EINVAL;
     if (!eng || !out || !d_off || (n && !d_bytes)) return TM_EINVAL;
     if (!eng->staged.empty()) {
         eng->err = "tm_match_device: staged ops not committed";
@@ -1194,7 +1256,12 @@ int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_of
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
     eng->last_stream = s;
     eng->last_n = n;
-    TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s), TM_EDEVICE, "kernel launch");
+    const uint32_t kmode = mode == TM_MATCH_FIRST ? MODE_FIRST : (mode == TM_MATCH_COUNT ? MODE_COUNT : MODE_ALL);
+    if (kmode == MODE_FIRST && eng->keys_cap < n) {
+        TM_TRY_HIP(eng->d_keys.ensure((uint64_t)n * 4), TM_ENOMEM, "alloc keys");
+        eng->keys_cap = n;
+    }
+    TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s, kmode), TM_EDEVICE, "kernel launch");
     out->n = n;
     out->d_off = eng->d_outoff.as<uint32_t>();
     out->d_cnt = eng->d_outcnt.as<uint32_t>();

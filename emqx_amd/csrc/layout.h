@@ -9,9 +9,10 @@
 //   word table  : level-word bytes  -> word id    (tokeniser, one probe per topic level)
 //   edge table  : (parent, word id) -> slot       (walk, one probe per frontier node/level)
 //   slot lists  : slot -> offset of the node's terminal list in the arena
-//   list arena  : u32 key handles; per list a 2-word header [term_cnt, hash_cnt], then
-//                 the exact-terminal keys, then the '#'-child keys ("filter/#" hangs
-//                 off the node of "filter").
+//   list arena  : u32 key handles; per list a LIST_HDR-word header [min bin-term key,
+//                 min word-term key, min '#' key, term_cnt, hash_cnt], then the
+//                 exact-terminal keys, then the '#'-child keys ("filter/#" hangs off the
+//                 node of "filter").
 //
 // A node IS the index of the edge slot that leads to it (the root is ROOT_ID), so a
 // slot needs no child field.  Its 16 bytes carry the key (parent, word), a 32-bit
@@ -53,6 +54,10 @@ constexpr uint32_t I_INL_HASH = 1u << 27;   // M_INLINE: the key is a '#' key (e
 constexpr uint32_t I_KEY_MASK = (1u << 27) - 1;  // M_INLINE: the key handle
 constexpr uint32_t INLINE_KEY_LIMIT = 1u << 27;  // handles >= this never go inline
 constexpr uint32_t CNT_BITS = 14, CNT_MAX = (1u << CNT_BITS) - 1;
+// List header words before a list's first key (lo): lo-5 smallest-id {Binary,{ID}} term key,
+// lo-4 smallest-id word-list term key, lo-3 smallest-id '#' key (NONE if none), lo-2
+// term_cnt, lo-1 hash_cnt.
+constexpr uint32_t LIST_HDR = 5;
 
 TM_HD uint32_t info_mode(uint32_t info) { return (info >> I_MODE_SHIFT) & 3u; }
 TM_HD uint32_t info_term_cnt(uint32_t info) { return (info >> CNT_BITS) & CNT_MAX; }
@@ -79,7 +84,7 @@ struct alignas(16) RootRec {
 
 // Host-side terminal list of a node (host node numbering).
 struct NodeList {
-    uint32_t list_off;  // first key (the 2-word header sits just before it)
+    uint32_t list_off;  // first key (the LIST_HDR-word header sits just before it)
     uint32_t term_cnt;  // keys whose filter ends exactly at the node
     uint32_t hash_cnt;  // keys of "node-path/#" (follow the term keys)
 };

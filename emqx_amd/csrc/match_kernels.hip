@@ -604,7 +604,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     __syncthreads();
 
     // ---- 5. load-balanced expansion: staged segments, then flushed chunks
-    if (!overflow && total) {
+    if (!overflow && total && a.mode == MODE_ALL) {
         expand_segments(a, L, nseg);
         for (uint32_t c = 0; c < nchunk; ++c) {
             const uint4 *src = a.seg_pool + (uint64_t)wchunks[c] * SCAP;
@@ -722,7 +722,8 @@ __global__ __launch_bounds__(WAVE) void k_match_slow(MatchArgs a) {
         a.out_cnt[t] = c;
         a.status[t] = 0;
         st_keys += c;
-        if (pos + c <= a.keys_cap) dfs_walk<true>(a, R, wid, stk, nl, dollar, a.keys + pos, &st_probe, &st_visit);
+        if (a.mode == MODE_ALL && pos + c <= a.keys_cap)
+            dfs_walk<true>(a, R, wid, stk, nl, dollar, a.keys + pos, &st_probe, &st_visit);
     }
     if constexpr (STATS) {
         // levels were already counted by the fast kernel's pre-scan
@@ -733,6 +734,106 @@ __global__ __launch_bounds__(WAVE) void k_match_slow(MatchArgs a) {
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_match_first: emqx_topic_index:match/2 (return_first, emqx_trie_search.erl:171-178) —
+// the FIRST matching key in ETS term order, per topic; lane per topic.
+//
+// Every key that matches topic T spells T's words at its literal levels, so two matching
+// keys differ only in WHERE they have '+' / '#' / the end of the list.  In Erlang term
+// order '#' < '+' < any binary and a shorter list sorts first, so the smallest matching
+// word-list key is the first one a depth-first walk meets when it tries, at each node:
+// the keys ending here (d == levels), then the node's "P/#" keys, then the '+' subtree,
+// then the literal subtree.  Equal word lists are one filter: the smallest id wins
+// ({ID} tuples).  {Binary, {ID}} keys sort after every list (emqx_trie_search.erl:381-389
+// finds them last), so one is the answer only when no word-list key matches.
+__global__ __launch_bounds__(WAVE) void k_match_first(MatchArgs a) {
+    const RootRec R = *a.root;
+    uint32_t dummy = 0;
+    auto byte_at = [&](uint32_t i) -> uint8_t { return a.bytes[i]; };
+    for (uint32_t t = blockIdx.x * WAVE + lane_id(); t < a.n; t += gridDim.x * WAVE) {
+        const uint32_t b = a.off[t], e = a.off[t + 1];
+        // badarg pre-scan (a level exactly "+" or "#")
+        bool badarg = false;
+        for (uint32_t i = b, st = b;; ++i) {
+            const bool end = i == e;
+            if (end || a.bytes[i] == '/') {
+                if (i - st == 1 && (a.bytes[st] == '+' || a.bytes[st] == '#')) badarg = true;
+                st = i + 1;
+                if (end) break;
+            }
+        }
+        a.out_off[t] = t;
+        a.status[t] = badarg ? 1 : 0;
+        if (badarg) {
+            a.out_cnt[t] = 0;
+            continue;
+        }
+        const uint64_t sbase = (uint64_t)(a.off[t] - a.off[0]) + 2ull * t;
+        uint32_t *wid = a.scratch_w + sbase;
+        uint64_t *stk = a.scratch_s + sbase;
+        const bool dollar = (e > b) && a.bytes[b] == '$';
+        uint32_t nl = 0;
+        for (uint32_t i = b;; ++i) {
+            const uint32_t st = i;
+            const uint64_t key = level_key(&i, e, byte_at);
+            wid[nl++] = word_lookup(a, key, i - st, st, byte_at, &dummy);
+            if (i >= e) break;
+        }
+        uint32_t best = NONE, bbest = NONE;
+        uint32_t sp = 0;
+        stk[sp++] = ROOT_MARK << 24;
+        while (sp) {
+            const uint64_t ent = stk[--sp];
+            const uint64_t slot = ent >> 24;
+            const uint32_t d = (uint32_t)(ent & 0xFFFFFF);
+            // the node's return_first candidates: its smallest-id {Binary,{ID}} term key,
+            // word-list term key and '#' key (list header, or the inline key)
+            uint32_t node, info, bloom, tb = NONE, tw = NONE, th = NONE;
+            if (slot == ROOT_MARK) {
+                node = ROOT_ID;
+                info = dollar ? (R.info & I_LIT) : R.info;
+                bloom = R.bloom;
+                if (!dollar && R.hash_cnt) th = a.arena[R.list_off - 3];
+            } else {
+                const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + slot);
+                node = (uint32_t)slot;
+                bloom = x.z;
+                info = x.w;
+                const uint32_t m = info_mode(info);
+                if (m == M_REC || m == M_CNT) {
+                    const uint32_t lo = a.slot_list[node];
+                    tb = a.arena[lo - 5];
+                    tw = a.arena[lo - 4];
+                    th = a.arena[lo - 3];
+                } else if (m == M_INLINE) {
+                    const uint32_t k = info & I_KEY_MASK;
+                    if (info & I_INL_HASH) th = k;
+                    else if (a.key_bin[k]) tb = k;
+                    else tw = k;
+                }
+            }
+            if (d == nl) {  // P + end of list, then P + '#'; binaries only if no list matches
+                if (tb != NONE) bbest = tb;  // only the all-literal path holds binary keys
+                best = tw != NONE ? tw : th;
+                if (best != NONE) break;
+                continue;
+            }
+            if (th != NONE) {  // P + '#'
+                best = th;
+                break;
+            }
+            // children: the '+' subtree before the literal one (pushed last, popped first)
+            const uint32_t need = probes_needed(info, bloom, wid[d]);
+            Rec r;
+            if ((need & DO_LIT) && edge_probe(a, node, wid[d], &r, &dummy)) stk[sp++] = ((uint64_t)r.child << 24) | (d + 1);
+            if ((need & DO_PLUS) && edge_probe(a, node, W_PLUS, &r, &dummy)) stk[sp++] = ((uint64_t)r.child << 24) | (d + 1);
+        }
+        if (best == NONE) best = bbest;
+        a.out_cnt[t] = best != NONE ? 1u : 0u;
+        a.keys[t] = best;
+    }
+}
 // ---------------------------------------------------------------------------
 __global__ void k_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -764,6 +865,13 @@ hipError_t launch_match(const MatchArgs &a, hipStream_t s) {
     if ((e = hipMemsetAsync(a.fr_cursor, 0, sizeof(unsigned long long), s))) return e;
     if (a.n == 0) return hipSuccess;
     const unsigned grid = (a.n + WAVE - 1) / WAVE;
+    if (a.mode == MODE_FIRST) {  // <= 1 key per topic at keys[t]; cursor stays 0
+        if (a.ev_fast0 && (e = hipEventRecord(a.ev_fast0, s))) return e;
+        k_match_first<<<grid < 4096u ? grid : 4096u, WAVE, 0, s>>>(a);
+        if ((e = hipGetLastError())) return e;
+        if (a.ev_fast1 && (e = hipEventRecord(a.ev_fast1, s))) return e;
+        return hipSuccess;
+    }
     if (a.ev_fast0 && (e = hipEventRecord(a.ev_fast0, s))) return e;
     if (a.stats) k_match_fast<true><<<grid, WAVE, 0, s>>>(a);
     else k_match_fast<false><<<grid, WAVE, 0, s>>>(a);

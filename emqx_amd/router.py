@@ -121,10 +121,20 @@ class Router:
     def has_route(self, topic, dest) -> bool:
         return dest in self._routes.get(self._t(topic), ())
 
-    def has_any_route(self, topic) -> bool:
-        """emqx_persistent_session_ds_router:has_any_route/1 (exact or return_first)."""
+    def has_any_route_batch(self, topics) -> list:
+        """emqx_persistent_session_ds_router:has_any_route/1 for a batch (exact lookup or
+        emqx_topic_index:match/2 =/= false, emqx_persistent_session_ds_router.erl:115-125):
+        only the per-topic counts are needed, so the GPU skips the key copy-out
+        (TM_MATCH_COUNT)."""
         self.commit()
-        return bool(self.eng.match([topic], N.TM_MATCH_FIRST)[0])
+        buf, off = N.pack_topics([self._t(t) for t in topics])
+        _, cnt, _, st = self.eng.match_packed(buf, off, N.TM_MATCH_COUNT)
+        if (st == N.TM_BADARG).any():
+            raise ValueError("badarg")
+        return [bool(c) for c in cnt]
+
+    def has_any_route(self, topic) -> bool:
+        return self.has_any_route_batch([topic])[0]
 
     def topics(self) -> list:
         return list(self._routes.keys())

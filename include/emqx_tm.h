@@ -76,7 +76,10 @@ extern "C" {
 /* match modes for tm_match_batch */
 #define TM_MATCH_ALL    0u  /* every matching key (matches/3 with [])            */
 #define TM_MATCH_UNIQUE 1u  /* one key per id (matches/3 with [unique])          */
-#define TM_MATCH_FIRST  2u  /* the first key in ETS term order (match/2)         */
+#define TM_MATCH_FIRST  2u  /* the first key in ETS term order (match/2); on the GPU
+                               (k_match_first): topic i's key, if any, is keys[off[i]]  */
+#define TM_MATCH_COUNT  3u  /* counts only, no keys: has_any_route/1
+                               (emqx_persistent_session_ds_router.erl:115-125) is cnt > 0 */
 
 /* tm_config.flags */
 #define TM_CFG_FORCE_SLOW 1u  /* route every topic through the spill (slow) kernel: test aid */
@@ -179,6 +182,11 @@ int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_of
 /* Wait for the last tm_match_device batch; refresh tm_stats().n_slow_topics and size
  * the internal chunk pools to that batch's demand for the next one. */
 int tm_device_sync(tm_engine *eng);
+/* tm_match_device with a match mode: TM_MATCH_ALL (= tm_match_device), TM_MATCH_FIRST
+ * (one key per topic, d_total not used) or TM_MATCH_COUNT (d_cnt only).  TM_MATCH_UNIQUE
+ * is host-side (tm_match_batch). */
+int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                         uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out);
 int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap);
 
 /* Route ids of the last match batch (all keys, TM_MATCH_ALL), compacted topic-major on

@@ -115,6 +115,76 @@ def test_modes_unique_first_vs_oracle():
                  ix.match(w.t_bytes, w.t_off, mode=oracle.MODE_FIRST), "first")
 
 
+@pytest.mark.parametrize("name,scale,nt", [("A", 1.0, 20_000), ("B", 0.05, 20_000), ("C", 0.01, 20_000),
+                                           ("E", 0.05, 20_000)])
+def test_device_first_and_count_modes(name, scale, nt):
+    """TM_MATCH_FIRST runs k_match_first (return_first, emqx_trie_search.erl:171-178) and
+    TM_MATCH_COUNT skips the key copy-out (has_any_route/1 is cnt > 0)."""
+    w = workloads.generate(name, scale=scale, n_topics=nt)
+    eng = _engine()
+    _load(eng, w)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    _assert_same(_engine_sets(eng, w.t_bytes, w.t_off, N.TM_MATCH_FIRST),
+                 ix.match(w.t_bytes, w.t_off, mode=oracle.MODE_FIRST, threads=8), f"first {name}")
+    o_all, c_all, _, s_all = eng.match_packed(w.t_bytes, w.t_off)
+    _, c_cnt, k_cnt, s_cnt = eng.match_packed(w.t_bytes, w.t_off, N.TM_MATCH_COUNT)
+    assert np.array_equal(c_all, c_cnt) and np.array_equal(s_all, s_cnt) and len(k_cnt) == 0
+
+
+def test_device_first_mode_through_device_api():
+    import torch
+    w = workloads.generate("E", scale=0.05, n_topics=10_000)
+    eng = _engine()
+    _load(eng, w)
+    dev = torch.device("cuda", 0)
+    d_bytes = torch.from_numpy(w.t_bytes).to(dev)
+    d_off = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
+    r = eng.match_device_mode(d_bytes.data_ptr(), d_off.data_ptr(), w.n_topics, int(w.t_off[-1]), N.TM_MATCH_FIRST)
+    eng.device_sync()
+    import ctypes as C
+    n = w.n_topics
+    cnt_t = torch.empty(n, dtype=torch.int32, device=dev)
+    keys_t = torch.empty(n, dtype=torch.int32, device=dev)
+    lib = C.CDLL("libamdhip64.so")
+    lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert lib.hipMemcpy(C.c_void_p(cnt_t.data_ptr()), C.c_void_p(r.d_cnt), 4 * n, 3) == 0
+    assert lib.hipMemcpy(C.c_void_p(keys_t.data_ptr()), C.c_void_p(r.d_keys), 4 * n, 3) == 0
+    cnt = cnt_t.cpu().numpy().view(np.uint32)
+    keys = keys_t.cpu().numpy().view(np.uint32)
+    off, hcnt, hkeys, _ = eng.match_packed(w.t_bytes, w.t_off, N.TM_MATCH_FIRST)
+    assert np.array_equal(cnt, hcnt)
+    assert np.array_equal(keys[cnt == 1], hkeys)
+
+
+def test_first_mode_term_order_kats():
+    """Term order of matching keys (Erlang: lists < binaries; '#' < '+' < binary words; a
+    shorter list first; then {ID}): KATs for the device FIRST walk."""
+    eng = _engine()
+    ops = [(N.TM_OP_ADD, b"a/b", 1), (N.TM_OP_ADD, b"a/b", 2, N.TM_KEY_WORDS), (N.TM_OP_ADD, b"a/+", 5),
+           (N.TM_OP_ADD, b"a/#", 9), (N.TM_OP_ADD, b"a/#", 7), (N.TM_OP_ADD, b"+/b", 3), (N.TM_OP_ADD, b"#", 8),
+           (N.TM_OP_ADD, b"x/y", 4), (N.TM_OP_ADD, b"x/y", 6), (N.TM_OP_ADD, b"$s/+", 10), (N.TM_OP_ADD, b"$s/q", 11)]
+    eng.apply(ops)
+    eng.commit()
+    first = lambda t: [eng.key_info(k)[0] for k in eng.match([t], N.TM_MATCH_FIRST)[0]]  # noqa: E731
+    assert first(b"a/b") == [8]       # ['#'] is the smallest list
+    assert first(b"x/y") == [8]
+    assert first(b"$s/q") == [10]     # no root '#' for '$' topics; ['$s','+'] < <<"$s/q">>
+    eng.apply([(N.TM_OP_DEL, b"#", 8)])
+    eng.commit()
+    assert first(b"a/b") == [3]       # ['+', b] < ['a', ...]
+    assert first(b"x/y") == [4]       # only binaries: smallest id
+    eng.apply([(N.TM_OP_DEL, b"+/b", 3)])
+    eng.commit()
+    assert first(b"a/b") == [7]       # ['a','#'] (ids 7, 9) < ['a','+'] < ['a','b'] < <<"a/b">>
+    eng.apply([(N.TM_OP_DEL, b"a/#", 7), (N.TM_OP_DEL, b"a/#", 9)])
+    eng.commit()
+    assert first(b"a/b") == [5]
+    eng.apply([(N.TM_OP_DEL, b"a/+", 5)])
+    eng.commit()
+    assert first(b"a/b") == [2]       # the word-list key sorts before the binary one
+    assert first(b"q") == []
+
+
 # ------------------------------------------------------------- edge cases
 EDGE_FILTERS = [b"#", b"+", b"+/+", b"/#", b"/+", b"//", b"", b"a", b"a/#", b"a/+", b"a//b", b"a/+/+", b"+/#",
                 b"$SYS/#", b"$SYS/+", b"$SYS/brokers/+/clients/#", b"+/brokers/#", b"a/#/b", b"a/b#", b"a/b+",
