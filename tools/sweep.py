@@ -30,10 +30,9 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 # same-process reference point.
 VARIANTS = {
     "head": ([], 0),
-    "nosplit": (["-DTM_SPLIT=0"], 0),
-    "split": (["-DTM_SPLIT=1"], 0),
-    "split_cp16": (["-DTM_SPLIT=1", "-DTM_CP_UNROLL=16"], 0),
-    "split_load16": (["-DTM_SPLIT=1"], 16),
+    "cp4": (["-DTM_CP_UNROLL=4"], 0),
+    "cp16": (["-DTM_CP_UNROLL=16"], 0),
+    "rpl1": (["-DTM_RPL=1"], 0),
 }
 
 
