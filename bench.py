@@ -144,8 +144,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # EMQX_BENCH_BACKEND=gloo: rehearse the multi-rank path on fewer GPUs than ranks (ranks
+    # share devices, barrier/all-reduce over gloo); the default is RCCL, one rank per GPU
+    backend = os.environ.get("EMQX_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
 
     from emqx_amd import _native as N
@@ -216,7 +224,7 @@ def main():
         dist.barrier()
     lat_ms = np.array([a.elapsed_time(b) for a, b in evs])
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend != "gloo" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     total_pubs = n * args.steps * world
