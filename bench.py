@@ -60,7 +60,7 @@ def kernel_src_sha():
     return hashlib.sha256(lines.encode()).hexdigest()
 
 
-def profiled_traffic(workload_keys, batch):
+def profiled_traffic(workload_keys, batch, any_config=False):
     """HBM bytes per k_match_fast launch from the committed PMC profile of THIS kernel
     source (profiles/*.json written by tools/summarize_prof.py from tools/prof_pmc.sh),
     or None.  rocprofv3 cannot run inside the process it profiles, so the counters come
@@ -76,9 +76,14 @@ def profiled_traffic(workload_keys, batch):
         if d.get("kernel_src_sha") != sha:
             continue
         cfg = d.get("bench_line", {}).get("config", {})
-        if cfg.get("route_keys") != workload_keys or cfg.get("publishes_per_step_per_gpu") != batch:
+        if not any_config and (cfg.get("route_keys") != workload_keys
+                               or cfg.get("publishes_per_step_per_gpu") != batch):
             continue
-        best = (p, d["traffic"])
+        t = dict(d["traffic"])
+        pmc = d.get("pmc_per_launch", {})
+        if "TCC_HIT_sum" in pmc:
+            t["tcc_hit"], t["tcc_miss"] = pmc["TCC_HIT_sum"], pmc["TCC_MISS_sum"]
+        best = (p, t)
     return best
 
 
@@ -97,8 +102,24 @@ def gather_roof(walk, kernel_ms):
     rate = probes / (kernel_ms * 1e-3) / 1e9
     out = {"probes_per_launch": probes, "achieved_G_probes_per_s": round(rate, 2)}
     if ceil:
-        out.update({"ceiling_G_loads_per_s": ceil[1], "frac": round(rate / ceil[1], 3), "source": ceil[0],
-                    "note": "probes include L2 hits (upper trie levels), so frac can exceed 1"})
+        out.update({"ceiling_G_loads_per_s": ceil[1], "source": ceil[0]})
+        # request model: every L2 miss at the random-miss rate, every L2 hit at the
+        # L2-resident random rate (2 MiB table), the key writes at the stream rate; the
+        # L2 hit/miss request counts come from the PMC profile of this kernel source
+        rows = [json.loads(x) for x in open(os.path.join(ROOT, ceil[0])) if x.strip().startswith("{")]
+        hit_rate = max([r["G_loads_per_s"] for r in rows if r.get("table_MiB") == 2] or [0])
+        prof = profiled_traffic(None, None, any_config=True)
+        if hit_rate and prof:
+            pmc = prof[1]
+            hits, misses = pmc.get("tcc_hit"), pmc.get("tcc_miss")
+            if hits and misses:
+                model_ms = (misses / (ceil[1] * 1e9) + hits / (hit_rate * 1e9)
+                            + 4 * walk["keys"] / 6.29e12) * 1e3
+                out["request_model"] = {"l2_miss_requests": int(misses), "l2_hit_requests": int(hits),
+                                        "miss_rate_G_per_s": ceil[1], "hit_rate_G_per_s": hit_rate,
+                                        "key_write_GBps": 6290.0, "model_ms": round(model_ms, 4),
+                                        "frac": round(model_ms / kernel_ms, 3),
+                                        "source": os.path.relpath(prof[0], ROOT)}
     return out
 
 

@@ -3,8 +3,8 @@
 // k_match_fast's probes are independent random 16-B loads into a table of GiBs (the edge
 // table).  Their ceiling is not the streaming HBM bandwidth but the rate at which the
 // memory system serves random 16-B requests that miss the caches.  This measures it with
-// no dependence between loads: every lane keeps U loads in flight, tables of 256 MiB to
-// 4 GiB (the config-C edge table is 4 GiB), 16 waves per CU.
+// no dependence between loads: every lane keeps U loads in flight, tables of 2 MiB (L2-
+// resident) to 4 GiB (the config-C edge table is 8 GiB), 16 waves per CU.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 tools/gather_roof.hip -o tools/gather_roof
 #include <hip/hip_runtime.h>
@@ -59,7 +59,7 @@ int main() {
     unsigned *out;
     if (hipMalloc(&tab, maxb) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
     hipMemset(tab, 1, maxb);
-    for (unsigned long long b : {256ull << 20, 1ull << 30, 4ull << 30}) {
+    for (unsigned long long b : {2ull << 20, 16ull << 20, 64ull << 20, 256ull << 20, 1ull << 30, 4ull << 30}) {
         run<1>(tab, b, out);
         run<4>(tab, b, out);
         run<8>(tab, b, out);
