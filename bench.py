@@ -150,6 +150,8 @@ def main():
     ap.add_argument("--mode", choices=("replicated", "sharded"), default="replicated",
                     help="replicated trie, publishes data-parallel (default); or filters hash-sharded over "
                          "ranks with an RCCL all-gather merge (config D; DESIGN.md §6)")
+    ap.add_argument("--shard-of", type=int, default=0, metavar="G",
+                    help="sharded mode on one process: hold shard 0 of a G-way split (per-GPU share of G GPUs)")
     ap.add_argument("--churn", type=int, default=0, metavar="EPOCHS",
                     help="config-E style run: EPOCHS delta epochs of 1%% adds + 1%% deletes, each committed "
                          "between match batches (commit and match timed separately)")
@@ -390,11 +392,15 @@ def run_sharded(args):
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     t0 = time.time()
-    w = workloads.generate(args.config, scale=args.scale, n_topics=args.batch, shard_count=world, shard_index=rank)
+    # --shard-of G on one process: this rank holds shard 0 of a G-way split (the per-GPU
+    # share of a G-GPU run) and the exchange is the identity
+    nshards = args.shard_of if (args.shard_of and world == 1) else world
+    w = workloads.generate(args.config, scale=args.scale, n_topics=args.batch, shard_count=nshards,
+                           shard_index=rank)
     eng = N.Engine(local, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
     eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)  # already this shard's keys only
     eng.commit()
-    log(f"[rank {rank}] shard {rank}/{world}: {w.n_keys} keys, build {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] shard {rank}/{nshards}: {w.n_keys} keys, build {time.time() - t0:.1f}s")
     six = S.ShardedIndex(S.EngineShard(eng), rank, world)
     n = w.n_topics
     d_bytes = torch.from_numpy(w.t_bytes).to(dev)
@@ -431,7 +437,8 @@ def run_sharded(args):
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "u32",
             "data": f"synthetic (seeded generator, emqx_amd/workloads.py config {args.config}, scale {args.scale})",
-            "config": {"workload": f"{args.config} filter-sharded over {world} rank(s): {w.n_keys} keys on rank 0",
+            "config": {"workload": f"{args.config} filter-sharded {nshards} ways over {world} rank(s): "
+                                   f"{w.n_keys} keys on rank 0",
                        "publishes_per_step": n, "matches_per_step": matches,
                        "parallelism": f"filter hash-shard x{world}, RCCL all-gather merge"},
             "p50_batch_ms": round(float(np.percentile(lat, 50)), 4),

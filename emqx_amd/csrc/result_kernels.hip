@@ -160,8 +160,10 @@ __global__ __launch_bounds__(64) void k_merge(const uint32_t *counts, const uint
         if (off[t + 1] > cap) return;  // caller's buffer too small (wave-uniform; it re-sizes from off[n])
         for (uint32_t r = 0; r < G; r++) {
             const uint32_t c = counts[(uint64_t)r * n + t];
-            const uint64_t src = (uint64_t)r * stride + roff[(uint64_t)r * (n + 1) + t];
-            for (uint32_t k = lane; k < c; k += 64) out[dst + k] = ids[src + k];
+            const uint32_t so = roff[(uint64_t)r * (n + 1) + t];
+            const uint64_t src = (uint64_t)r * stride + so;
+            if ((uint64_t)so + c <= stride)  // a shard's slice never leaves its row
+                for (uint32_t k = lane; k < c; k += 64) out[dst + k] = ids[src + k];
             dst += c;
         }
     }

@@ -133,41 +133,49 @@ class ShardedIndex:
     # ---- device path (RCCL over xGMI)
     def match_device(self, eng: "N.Engine", d_bytes: int, d_off: int, n: int, total_bytes: int):
         """GPU path: local walk, ids compacted on device, RCCL all-gathers, device merge.
-        Everything runs on torch's current stream; returns device tensors (off[n+1] i32,
-        ids i64 holding u64 route ids)."""
+        The engine calls and the torch ops between them all run on ONE torch stream (the
+        engine's own stream is non-blocking, so torch's legacy default stream would not
+        order after it); the caller's current stream waits for it before this returns.
+        Returns device tensors (off[n+1] i32, ids i64 holding u64 route ids)."""
         import torch
         import torch.distributed as dist
-        s = torch.cuda.current_stream()
-        sp = s.cuda_stream
         dev = torch.device("cuda", torch.cuda.current_device())
-        r = eng.match_device(d_bytes, d_off, n, total_bytes, sp)
-        eng.device_sync()
-        total = _read_u64(r.d_total)
-        if total > r.keys_cap:
-            eng.reserve_matches(int(total * 1.1) + 1024)
+        caller = torch.cuda.current_stream()
+        if getattr(self, "_stream", None) is None:
+            self._stream = torch.cuda.Stream(dev)
+        s = self._stream
+        s.wait_stream(caller)  # the topic batch was written on the caller's stream
+        sp = s.cuda_stream
+        with torch.cuda.stream(s):
             r = eng.match_device(d_bytes, d_off, n, total_bytes, sp)
             eng.device_sync()
             total = _read_u64(r.d_total)
-        loc_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        maxT = torch.tensor([total], dtype=torch.int64, device=dev)
-        if self.world > 1:
-            dist.all_reduce(maxT, op=dist.ReduceOp.MAX, group=self.group)
-        stride = max(int(maxT.item()), 1)
-        mine = torch.zeros(stride, dtype=torch.int64, device=dev)
-        eng.result_ids_device(mine.data_ptr(), stride, loc_off.data_ptr(), sp)
-        cnt = (loc_off[1:] - loc_off[:-1]).contiguous()
-        if self.world > 1:
-            C = torch.empty(self.world * n, dtype=torch.int32, device=dev)
-            dist.all_gather_into_tensor(C, cnt, group=self.group)
-            Ids = torch.empty(self.world * stride, dtype=torch.int64, device=dev)
-            dist.all_gather_into_tensor(Ids, mine, group=self.group)
-        else:  # one shard: the exchange is the identity
-            C, Ids = cnt, mine
-        out_total = int(C.to(torch.int64).sum().item())
-        out_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        out_ids = torch.empty(max(out_total, 1), dtype=torch.int64, device=dev)
-        eng.merge_shards_device(self.world, n, C.data_ptr(), Ids.data_ptr(), stride, out_off.data_ptr(),
-                                out_ids.data_ptr(), out_total, sp)
+            if total > r.keys_cap:
+                eng.reserve_matches(int(total * 1.1) + 1024)
+                r = eng.match_device(d_bytes, d_off, n, total_bytes, sp)
+                eng.device_sync()
+                total = _read_u64(r.d_total)
+            loc_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            maxT = torch.tensor([total], dtype=torch.int64, device=dev)
+            if self.world > 1:
+                dist.all_reduce(maxT, op=dist.ReduceOp.MAX, group=self.group)
+            stride = max(int(maxT.item()), 1)
+            mine = torch.zeros(stride, dtype=torch.int64, device=dev)
+            eng.result_ids_device(mine.data_ptr(), stride, loc_off.data_ptr(), sp)
+            cnt = (loc_off[1:] - loc_off[:-1]).contiguous()
+            if self.world > 1:
+                C = torch.empty(self.world * n, dtype=torch.int32, device=dev)
+                dist.all_gather_into_tensor(C, cnt, group=self.group)
+                Ids = torch.empty(self.world * stride, dtype=torch.int64, device=dev)
+                dist.all_gather_into_tensor(Ids, mine, group=self.group)
+            else:  # one shard: the exchange is the identity
+                C, Ids = cnt, mine
+            out_total = int(C.to(torch.int64).sum().item())
+            out_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            out_ids = torch.empty(max(out_total, 1), dtype=torch.int64, device=dev)
+            eng.merge_shards_device(self.world, n, C.data_ptr(), Ids.data_ptr(), stride, out_off.data_ptr(),
+                                    out_ids.data_ptr(), out_total, sp)
+        caller.wait_stream(s)
         return out_off, out_ids[:out_total]
 
 
