@@ -56,6 +56,12 @@ constexpr uint32_t DO_PLUS = 0x80u, DO_LIT = 0x40u;  // frontier meta: probes th
 #ifndef TM_RPL
 #define TM_RPL 2
 #endif
+#ifndef TM_QCOPY
+#define TM_QCOPY 8  // lanes per group copying one medium list (0: the whole wave copies each long list)
+#endif
+#ifndef TM_QMED
+#define TM_QMED 2  // a "medium" list is at most TM_QMED group-iterations long
+#endif
 #ifndef TM_CP_UNROLL
 #define TM_CP_UNROLL 8
 #endif
@@ -183,6 +189,8 @@ struct WaveLds {
 __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, uint32_t ns) {
     const uint32_t lane = lane_id();
     uint32_t nlong = 0;  // wave-uniform; long segment indices are queued in L.seg_scan
+    uint32_t nmed = 0;   // TM_QCOPY: medium lists, queued from the front (huge ones from the back)
+    (void)nmed;
     for (uint32_t sb = 0; sb < ns; sb += WAVE) {
         const uint32_t j = sb + lane;
         uint4 g = make_uint4(0u, 0u, 0u, 0u);
@@ -210,13 +218,58 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
                     if ((uint32_t)k < g.y) a.keys[dst + k] = key[k];
             }
         }
+#if TM_QCOPY
+        // medium lists go to lane groups (several lists in flight), huge ones to the wave
+        const bool is_med = is_long && g.y <= (uint32_t)(TM_QCOPY * CP_UNROLL * TM_QMED);
+        uint32_t totm;
+        const uint32_t qm = nmed + wave_excl_scan(is_med ? 1u : 0u, &totm);
+        if (is_med) L.seg_scan[qm] = j;
+        nmed += totm;
+        const bool is_huge = is_long && !is_med;
+        uint32_t tot;
+        const uint32_t q = nlong + wave_excl_scan(is_huge ? 1u : 0u, &tot);
+        if (is_huge) L.seg_scan[SCAP - q] = j;
+        nlong += tot;
+#else
         uint32_t tot;
         const uint32_t q = nlong + wave_excl_scan(is_long ? 1u : 0u, &tot);
         if (is_long) L.seg_scan[q] = j;
         nlong += tot;
+#endif
     }
     __syncthreads();
-    for (uint32_t q = 0; q < nlong; q++) {
+#if TM_QCOPY
+    {
+        constexpr uint32_t GRP = TM_QCOPY, NG = WAVE / TM_QCOPY;
+        const uint32_t grp = lane / GRP, gl = lane % GRP;
+        for (uint32_t qb = 0; qb < nmed; qb += NG) {
+            const uint32_t qi = qb + grp;
+            if (qi < nmed) {
+                const uint4 g = L.seg[L.seg_scan[qi]];
+                const uint32_t dst = L.tbase[g.w & 0xFFu] + g.z;
+                for (uint32_t k0 = gl; k0 < g.y; k0 += GRP * CP_UNROLL) {
+                    uint32_t key[CP_UNROLL];
+#pragma unroll
+                    for (int u = 0; u < CP_UNROLL; u++) {
+                        const uint32_t k = k0 + u * GRP;
+                        if (k < g.y) key[u] = a.arena[g.x + k];
+                    }
+#pragma unroll
+                    for (int u = 0; u < CP_UNROLL; u++) {
+                        const uint32_t k = k0 + u * GRP;
+                        if (k < g.y) a.keys[dst + k] = key[u];
+                    }
+                }
+            }
+        }
+    }
+#endif
+    for (uint32_t qq = 0; qq < nlong; qq++) {
+#if TM_QCOPY
+        const uint32_t q = SCAP - qq;
+#else
+        const uint32_t q = qq;
+#endif
         const uint4 g = L.seg[L.seg_scan[q]];
         const uint32_t dst = L.tbase[g.w & 0xFFu] + g.z;
         for (uint32_t k0 = lane; k0 < g.y; k0 += WAVE * CP_UNROLL) {

@@ -172,7 +172,10 @@ int tm_commit_epoch(tm_engine *eng, uint64_t *epoch_out);
 int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off,
                    uint32_t n, uint32_t mode, tm_result *out);
 /* Device buffers in, device result out, asynchronous on the engine's stream
- * (or on `stream` if non-NULL: a hipStream_t).  `d_off` has n+1 entries and
+ * (or on `stream` if non-NULL: a hipStream_t).  The engine's own stream is
+ * non-blocking: work the caller queues on other streams (including the legacy
+ * default stream) is NOT ordered after it; pass your stream, or tm_device_sync()
+ * first.  `d_off` has n+1 entries and
  * total_bytes = d_off[n] - d_off[0] (it sizes the spill kernel's scratch).
  * Call tm_device_sync() before reading; if *d_total > keys_cap the batch
  * overflowed and must be re-run after tm_reserve_matches().

@@ -29,10 +29,12 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 # "head": the committed match_kernels.hip (git HEAD) with the working tree's engine, as the
 # same-process reference point.
 VARIANTS = {
-    "head": ([], 0),
-    "cp4": (["-DTM_CP_UNROLL=4"], 0),
-    "cp16": (["-DTM_CP_UNROLL=16"], 0),
-    "rpl1": (["-DTM_RPL=1"], 0),
+    "q8": (["-DTM_QCOPY=8"], 0),
+    "q8m4": (["-DTM_QCOPY=8", "-DTM_QMED=4"], 0),
+    "q8m8": (["-DTM_QCOPY=8", "-DTM_QMED=8"], 0),
+    "q4": (["-DTM_QCOPY=4"], 0),
+    "q4m4": (["-DTM_QCOPY=4", "-DTM_QMED=4"], 0),
+    "q8m1": (["-DTM_QCOPY=8", "-DTM_QMED=1"], 0),
 }
 
 
