@@ -29,12 +29,9 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 # "head": the committed match_kernels.hip (git HEAD) with the working tree's engine, as the
 # same-process reference point.
 VARIANTS = {
-    "q8": (["-DTM_QCOPY=8"], 0),
-    "q8m4": (["-DTM_QCOPY=8", "-DTM_QMED=4"], 0),
-    "q8m8": (["-DTM_QCOPY=8", "-DTM_QMED=8"], 0),
-    "q4": (["-DTM_QCOPY=4"], 0),
-    "q4m4": (["-DTM_QCOPY=4", "-DTM_QMED=4"], 0),
-    "q8m1": (["-DTM_QCOPY=8", "-DTM_QMED=1"], 0),
+    "head": ([], 0),
+    "tkovl": (["-DTM_TKOVL=1"], 0),
+    "notkovl": (["-DTM_TKOVL=0"], 0),
 }
 
 
