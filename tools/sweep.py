@@ -30,8 +30,8 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 # same-process reference point.
 VARIANTS = {
     "head": ([], 0),
-    "tkovl": (["-DTM_TKOVL=1"], 0),
-    "notkovl": (["-DTM_TKOVL=0"], 0),
+    "fast": (["-DTM_FAST=1"], 0),
+    "nofast": (["-DTM_FAST=0"], 0),
 }
 
 
