@@ -55,7 +55,8 @@ class tm_config(C.Structure):
         ("device", C.c_int32), ("flags", C.c_uint32),
         ("reserve_keys", C.c_uint32), ("reserve_nodes", C.c_uint32),
         ("reserve_topics", C.c_uint32), ("reserve_matches", C.c_uint32),
-        ("seg_chunks", C.c_uint32), ("edge_load_inv", C.c_uint32), ("reserved", C.c_uint32 * 2),
+        ("seg_chunks", C.c_uint32), ("edge_load_inv", C.c_uint32),
+        ("topics_per_wave", C.c_uint32), ("reserved", C.c_uint32 * 1),
     ]
 
 
@@ -176,7 +177,8 @@ class Engine:
     """One engine = one GPU.  Thin owner of a tm_engine*."""
 
     def __init__(self, device: int = 0, *, force_slow: bool = False, reserve_keys: int = 0,
-                 reserve_nodes: int = 0, reserve_matches: int = 0, seg_chunks: int = 0, edge_load_inv: int = 0):
+                 reserve_nodes: int = 0, reserve_matches: int = 0, seg_chunks: int = 0, edge_load_inv: int = 0,
+                 topics_per_wave: int = 0):
         self.lib = load()
         cfg = tm_config()
         cfg.device = device
@@ -185,6 +187,7 @@ class Engine:
         cfg.reserve_nodes = reserve_nodes
         cfg.reserve_matches = reserve_matches
         cfg.seg_chunks = seg_chunks
+        cfg.topics_per_wave = topics_per_wave
         cfg.edge_load_inv = edge_load_inv or int(os.environ.get("EMQX_TM_EDGE_LOAD_INV", "0"))
         h = C.c_void_p()
         rc = self.lib.tm_create(C.byref(cfg), C.byref(h))

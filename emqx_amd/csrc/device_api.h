@@ -21,6 +21,7 @@ struct MatchArgs {
     uint32_t n;
     uint32_t force_slow;  // 1: every topic takes the spill kernel (test aid)
     uint32_t mode;        // MODE_ALL: every key; MODE_COUNT: counts only; MODE_FIRST: k_match_first
+    uint32_t tpw;         // topics per wave of k_match_fast (pick_tpw)
     // frozen index
     const WordSlot *wtab;
     uint64_t wmask;
@@ -63,6 +64,17 @@ struct MatchArgs {
     // optional: events recorded around k_match_fast on the launch stream
     hipEvent_t ev_fast0, ev_fast1;
 };
+
+// Topics per wave of k_match_fast.  A wave's walk is a chain of dependent round trips
+// whose length grows with its frontier, so a small batch is spread thin (down to 4
+// topics per wave) to fill the chip with short waves; from 256 Ki topics on, 64 per wave.
+inline uint32_t pick_tpw(uint32_t n, uint32_t fixed = 0) {
+    if (fixed == 4 || fixed == 8 || fixed == 16 || fixed == 32 || fixed == 64) return fixed;
+    uint32_t t = 4;
+    while (t < 64 && (uint64_t)t * 2 * 4096 <= n) t *= 2;
+    return t;
+}
+inline uint64_t match_grid(uint32_t n, uint32_t tpw) { return ((uint64_t)n + tpw - 1) / tpw; }
 
 // Enqueue the whole match pipeline for one batch on `stream`:
 // reset counters, fast wave-BFS kernel, spill kernel for topics the fast

@@ -1000,7 +1000,8 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
     TM_TRY_HIP(eng->d_scr_w.ensure((bytes + 2ull * n + 2) * 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_scr_s.ensure((bytes + 2ull * n + 2) * 8), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_seg_cursor.ensure(64), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_wave_chunks.ensure(((uint64_t)n + 63) / 64 * SEG_MAXCHUNK * 4 + 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_wave_chunks.ensure(match_grid(n, pick_tpw(n, eng->cfg.topics_per_wave)) * SEG_MAXCHUNK * 4 + 4),
+               TM_ENOMEM, "alloc");
     {
         // chunk pool for waves whose staged key segments overflow LDS
         uint64_t want = eng->cfg.seg_chunks ? eng->cfg.seg_chunks : std::max<uint64_t>(1024, ((uint64_t)n + 63) / 64 * 8);
@@ -1047,6 +1048,7 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
                                 hipStream_t s, uint32_t mode = MODE_ALL) {
     MatchArgs a{};
     a.mode = mode;
+    a.tpw = pick_tpw(n, eng->cfg.topics_per_wave);
     a.key_id = eng->d_key_id.as<uint64_t>();
     a.key_bin = eng->d_key_bin.as<uint32_t>();
     a.bytes = d_bytes;

@@ -294,8 +294,8 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     __shared__ WaveLds L;
     uint32_t *const wchunks = a.wave_chunks + (uint64_t)blockIdx.x * MAXCHUNK;  // this wave's flushed chunks
     const uint32_t lane = lane_id();
-    const uint32_t t = blockIdx.x * WAVE + lane;
-    const bool active = t < a.n;
+    const uint32_t t = blockIdx.x * a.tpw + lane;
+    const bool active = lane < a.tpw && t < a.n;
     uint32_t st_visit = 0, st_probe = 0, st_wprobe = 0, st_seg = 0, st_flush = 0, st_frch = 0, st_rec = 0,
              st_inl = 0;
     // STATS build only: phase stamps (shares of wave time, not absolute kernel time)
@@ -303,8 +303,8 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     if constexpr (STATS) ts0 = __builtin_amdgcn_s_memtime();
 
     // ---- 0. stage the wave's topic bytes in LDS with 16-B coalesced loads
-    const uint32_t t0 = blockIdx.x * WAVE;
-    const uint32_t wb0 = a.off[t0], wb1 = a.off[min(t0 + WAVE, a.n)];
+    const uint32_t t0 = blockIdx.x * a.tpw;
+    const uint32_t wb0 = a.off[t0], wb1 = a.off[min(t0 + a.tpw, a.n)];
     const uint32_t tbase = wb0 & ~15u;
     const bool staged = ((reinterpret_cast<uintptr_t>(a.bytes) & 15u) == 0) && (wb1 - tbase <= (uint32_t)TBCAP);
     if (staged) {
@@ -917,7 +917,7 @@ hipError_t launch_match(const MatchArgs &a, hipStream_t s) {
     if ((e = hipMemsetAsync(a.seg_cursor, 0, sizeof(unsigned long long), s))) return e;
     if ((e = hipMemsetAsync(a.fr_cursor, 0, sizeof(unsigned long long), s))) return e;
     if (a.n == 0) return hipSuccess;
-    const unsigned grid = (a.n + WAVE - 1) / WAVE;
+    const unsigned grid = (unsigned)match_grid(a.n, a.tpw);
     if (a.mode == MODE_FIRST) {  // <= 1 key per topic at keys[t]; cursor stays 0
         if (a.ev_fast0 && (e = hipEventRecord(a.ev_fast0, s))) return e;
         k_match_first<<<grid < 4096u ? grid : 4096u, WAVE, 0, s>>>(a);

@@ -99,7 +99,8 @@ typedef struct tm_config {
     uint32_t edge_load_inv;       /* edge-table load <= 1/edge_load_inv (0 = default 8): a wave
                                      waits for its longest probe chain, so lower load shortens
                                      the walk at the price of HBM (16 B per slot) */
-    uint32_t reserved[2];
+    uint32_t topics_per_wave;     /* 0 = by batch size (4..64); else 4, 8, 16, 32 or 64 */
+    uint32_t reserved[1];
 } tm_config;
 
 typedef struct tm_op {

@@ -104,6 +104,18 @@ def test_config_parity(name, scale, nt, mode):
         assert eng.stats()["n_slow_topics"] == 0
 
 
+@pytest.mark.parametrize("tpw", [4, 16, 64])
+@pytest.mark.parametrize("name,scale,nt", [("A", 1.0, 50_000), ("C", 0.02, 50_000), ("E", 0.1, 50_000)])
+def test_config_parity_topics_per_wave(name, scale, nt, tpw):
+    """Every wave width (tm_config.topics_per_wave) gives the same sets; test-sized batches
+    otherwise run at the narrow width the batch size picks."""
+    w = workloads.generate(name, scale=scale, n_topics=nt)
+    eng = _engine(topics_per_wave=tpw)
+    _load(eng, w)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    _assert_same(_engine_sets(eng, w.t_bytes, w.t_off), ix.match(w.t_bytes, w.t_off, threads=8), f"{name} tpw={tpw}")
+
+
 def test_modes_unique_first_vs_oracle():
     w = workloads.generate("E", scale=0.02, n_topics=4000)
     eng = _engine()
@@ -256,7 +268,7 @@ def test_segment_and_frontier_chunks_and_pool_exhaustion():
     buf, off = N.pack_topics(topics)
     exp = ix.match(buf, off, threads=8)
     for chunks in (0, 1):
-        eng = _engine(seg_chunks=chunks)
+        eng = _engine(seg_chunks=chunks, topics_per_wave=64)  # wide waves: frontiers overflow LDS
         eng.apply([(N.TM_OP_ADD, f, i) for i, f in enumerate(filters)])
         eng.commit()
         eng.debug_stats(True, read=False)

@@ -25,13 +25,14 @@ sys.path.insert(0, ROOT)
 VDIR = os.path.join(ROOT, "emqx_amd", "variants")
 CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 
-# name -> (extra hipcc flags, edge_load_inv)
+# name -> (extra hipcc flags, edge_load_inv[, topics_per_wave])
 # "head": the committed match_kernels.hip (git HEAD) with the working tree's engine, as the
 # same-process reference point.
 VARIANTS = {
-    "head": ([], 0),
-    "fast": (["-DTM_FAST=1"], 0),
-    "nofast": (["-DTM_FAST=0"], 0),
+    "base": ([], 0),
+    "tpw32": ([], 0, 32),
+    "tpw16": ([], 0, 16),
+    "tpw64": ([], 0, 64),
 }
 
 
@@ -39,7 +40,7 @@ def build(names):
     os.makedirs(VDIR, exist_ok=True)
     procs = []
     for name in names:
-        flags, _ = VARIANTS[name]
+        flags = VARIANTS[name][0]
         out = os.path.join(VDIR, f"libemqx_tm_{name}.so")
         kern = os.path.join(CSRC, "match_kernels.hip")
         if name == "head":
@@ -79,7 +80,9 @@ def run(args):
         importlib.reload(_native)
         N = _native
         t0 = time.time()
-        eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4, edge_load_inv=VARIANTS[name][1])
+        v = VARIANTS[name]
+        eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4, edge_load_inv=v[1],
+                       topics_per_wave=v[2] if len(v) > 2 else 0)
         eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
         eng.commit()
         tbuild = time.time() - t0
