@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -1209,11 +1210,13 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
             // maps:put in ascending walk order: the last (greatest) key per id wins,
             // maps:values/1 returns them ordered by id (small maps are sorted).
             std::vector<std::pair<uint64_t, uint32_t>> best;
+            std::unordered_map<uint64_t, size_t> at;  // id -> index in best
+            at.reserve(tmp.size() * 2);
             for (uint32_t k : tmp) {
-                uint64_t id = eng->keys[k].id;
-                auto it = std::find_if(best.begin(), best.end(), [&](auto &p) { return p.first == id; });
-                if (it == best.end()) best.push_back({id, k});
-                else it->second = k;
+                const uint64_t id = eng->keys[k].id;
+                auto ins = at.emplace(id, best.size());
+                if (ins.second) best.push_back({id, k});
+                else best[ins.first->second].second = k;
             }
             std::sort(best.begin(), best.end());
             for (auto &p : best) eng->pp_keys.push_back(p.second);
