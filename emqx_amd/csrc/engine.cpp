@@ -109,6 +109,9 @@ struct PinBuf {
 // Edge table load <= 1/EDGE_LOAD_INV.  A wave waits for the longest of its ~256
 // concurrent probe chains, so short chains (low load) matter more than table size.
 constexpr uint64_t EDGE_LOAD_INV = 8;
+// Largest edge table: node ids are u32 slot indices and must stay below the sentinels
+// (NONE, W_PLUS, ROOT_ID); 2^31 slots = 32 GiB of HBM.
+constexpr uint64_t MAX_EDGE_SLOTS = 1ull << 31;
 // Word table load <= 1/WORD_LOAD_INV (small: it sizes with the vocabulary, not the nodes).
 constexpr uint64_t WORD_LOAD_INV = 4;
 
@@ -264,6 +267,7 @@ struct tm_engine {
     }
     // Re-place every node: slot positions hash the parent's slot, so nodes go in in
     // creation order (parents first).  Node ids on the device change: full upload.
+    bool edge_full = false;  // the edge table hit MAX_EDGE_SLOTS at load 1/2: commit fails
     void edge_rehash(uint64_t cap) {
         std::vector<EdgeSlot> old;
         old.swap(etab);
@@ -304,7 +308,15 @@ struct tm_engine {
     uint32_t edge_child(uint32_t parent, uint32_t word) {
         uint64_t s = edge_find(dev_id(parent), word);
         if (s != ~0ull) return slot_node[s];
-        if ((n_edges + 1) * edge_load_inv() > etab.size()) edge_rehash(etab.size() * 2);
+        if ((n_edges + 1) * edge_load_inv() > etab.size()) {
+            // a node is its slot index (u32, below the NONE/ROOT_ID sentinels): at the
+            // size cap the table fills up to half instead of growing
+            if (etab.size() < MAX_EDGE_SLOTS) edge_rehash(etab.size() * 2);
+            else if ((n_edges + 1) * 2 > etab.size()) {
+                edge_full = true;
+                return ROOT;  // dropped; commit() reports TM_ENOMEM
+            }
+        }
         const uint32_t child = (uint32_t)node_parent.size();
         node_parent.push_back(parent);
         node_word.push_back(word);
@@ -766,6 +778,11 @@ struct tm_engine {
 
     int commit() {
         for (const StagedOp &op : staged) apply_one(op);
+        if (edge_full) {
+            err = "edge table full: more trie nodes than MAX_EDGE_SLOTS / 2 (shard the filters over more GPUs); "
+                  "the engine is unusable and must be recreated";
+            return TM_ENOMEM;
+        }
         staged.clear();
         stage_bytes.clear();
         bool full = need_full || deltas.size() > std::max<uint64_t>(n_live / 8, 1u << 16);
@@ -908,7 +925,7 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     eng->node_slot.push_back(NONE);
     eng->node_list.reserve(rn);
     eng->node_list.push_back(NodeList{0, 0, 0});
-    eng->edge_rehash(next_pow2(std::max<uint64_t>(rn * eng->edge_load_inv(), 1024)));
+    eng->edge_rehash(std::min<uint64_t>(next_pow2(std::max<uint64_t>(rn * eng->edge_load_inv(), 1024)), MAX_EDGE_SLOTS));
     eng->kset_rehash(next_pow2(std::max<uint64_t>(rk * 2, 1024)));
     eng->keys.reserve(rk);
     eng->need_full = true;
@@ -1092,6 +1109,7 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
                    tm_result *out) {
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
     if (mode > TM_MATCH_COUNT) return TM_EINVAL;
+    if (eng->edge_full) return TM_ESTATE;
     if (!eng->staged.empty()) {
         eng->err = "tm_match_batch: staged ops not committed";
         return TM_ESTATE;
@@ -1249,6 +1267,7 @@ int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_of
 int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                          uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out) {
     if (mode != TM_MATCH_ALL && mode != TM_MATCH_FIRST && mode != TM_MATCH_COUNT) return TM_EINVAL;
+    if (!eng || eng->edge_full) return eng ? TM_ESTATE : TM_EINVAL;
     if (!eng || !out || !d_off || (n && !d_bytes)) return TM_EINVAL;
     if (!eng->staged.empty()) {
         eng->err = "tm_match_device: staged ops not committed";
