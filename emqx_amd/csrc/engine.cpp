@@ -793,6 +793,12 @@ struct tm_engine {
             if (arena_garbage > std::max<uint64_t>(arena.size() / 2, 1u << 20)) rebuild_arena();
         }
         deltas.clear();
+        if (arena.size() >= 0xFFFFFFF0ull) {  // list offsets are u32
+            edge_full = true;
+            err = "terminal-list arena beyond 4 Gi entries (shard the filters over more GPUs); "
+                  "the engine is unusable and must be recreated";
+            return TM_ENOMEM;
+        }
         hipError_t e = need_full ? upload_full() : upload_delta();
         if (e != hipSuccess) {
             err = std::string("device upload failed: ") + hipGetErrorString(e);
