@@ -87,7 +87,8 @@ class tm_dev_result(C.Structure):
 class tm_stats_t(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "epoch", "n_keys", "n_nodes", "n_words", "edge_slots", "word_slots", "list_words",
-        "device_bytes", "n_full_rebuilds", "n_delta_commits", "n_slow_topics")]
+        "device_bytes", "n_full_rebuilds", "n_delta_commits", "n_slow_topics",
+        "commit_apply_us", "commit_lists_us", "commit_upload_us")]
 
 
 _lib = None

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -185,6 +186,7 @@ struct tm_engine {
     std::vector<uint32_t> pp_off, pp_cnt, pp_keys;  // post-processed results
     hipStream_t stream = nullptr;
     uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0, seg_demand_last = 0, fr_demand_last = 0;
+    uint64_t commit_us[3] = {0, 0, 0};  // last commit: apply / lists / upload (tm_stats)
     hipStream_t last_stream = nullptr;  // stream of the last tm_match_device call
     uint32_t last_n = 0;                // topics of the last match batch
     bool stats_on = false;
@@ -776,7 +778,14 @@ struct tm_engine {
         return hipStreamSynchronize(stream);
     }
 
+    static uint64_t now_us() {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch())
+            .count();
+    }
+
     int commit() {
+        const uint64_t t0 = now_us();
         for (const StagedOp &op : staged) apply_one(op);
         if (edge_full) {
             err = "edge table full: more trie nodes than MAX_EDGE_SLOTS / 2 (shard the filters over more GPUs); "
@@ -785,6 +794,7 @@ struct tm_engine {
         }
         staged.clear();
         stage_bytes.clear();
+        const uint64_t t1 = now_us();
         bool full = need_full || deltas.size() > std::max<uint64_t>(n_live / 8, 1u << 16);
         if (full) {
             rebuild_arena();
@@ -799,11 +809,15 @@ struct tm_engine {
                   "the engine is unusable and must be recreated";
             return TM_ENOMEM;
         }
+        const uint64_t t2 = now_us();
         hipError_t e = need_full ? upload_full() : upload_delta();
         if (e != hipSuccess) {
             err = std::string("device upload failed: ") + hipGetErrorString(e);
             return TM_EDEVICE;
         }
+        commit_us[0] = t1 - t0;
+        commit_us[1] = t2 - t1;
+        commit_us[2] = now_us() - t2;
         if (need_full) n_full_rebuilds++;
         else n_delta_commits++;
         need_full = false;
@@ -1418,6 +1432,9 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
     out->n_full_rebuilds = eng->n_full_rebuilds;
     out->n_delta_commits = eng->n_delta_commits;
     out->n_slow_topics = eng->n_slow_last;
+    out->commit_apply_us = eng->commit_us[0];
+    out->commit_lists_us = eng->commit_us[1];
+    out->commit_upload_us = eng->commit_us[2];
     return TM_OK;
 }
 

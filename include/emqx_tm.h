@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define TM_ABI_VERSION 1u
+#define TM_ABI_VERSION 2u
 
 /* status codes */
 #define TM_OK          0
@@ -151,6 +151,11 @@ typedef struct tm_stats_t {
     uint64_t n_full_rebuilds;
     uint64_t n_delta_commits;
     uint64_t n_slow_topics; /* topics routed to the spill kernel in the last batch */
+    /* wall time of the last tm_commit_epoch by phase, microseconds (host clock):
+     * staged ops folded into the host trie / lists rebuilt or appended / device upload */
+    uint64_t commit_apply_us;
+    uint64_t commit_lists_us;
+    uint64_t commit_upload_us;
 } tm_stats_t;
 
 /* lifecycle --------------------------------------------------------------- */
