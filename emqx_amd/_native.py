@@ -38,6 +38,15 @@ TM_MATCH_ALL = 0
 TM_MATCH_UNIQUE = 1
 TM_MATCH_FIRST = 2
 TM_MATCH_COUNT = 3
+TM_MATCH_AGGRE = 4
+
+TM_ID_SHARED = 1 << 63
+
+
+def shared_id(group: int, member: int) -> int:
+    """TM_SHARED_ID(group, member): the route id of a $share dest {Group, Node}."""
+    return TM_ID_SHARED | (group << 32) | (member & 0xFFFFFFFF)
+
 
 TM_CFG_FORCE_SLOW = 1
 
@@ -88,7 +97,7 @@ class tm_stats_t(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "epoch", "n_keys", "n_nodes", "n_words", "edge_slots", "word_slots", "list_words",
         "device_bytes", "n_full_rebuilds", "n_delta_commits", "n_slow_topics",
-        "commit_apply_us", "commit_lists_us", "commit_upload_us")]
+        "commit_apply_us", "commit_lists_us", "commit_upload_us", "n_deep_keys")]
 
 
 _lib = None
@@ -263,7 +272,9 @@ class Engine:
         o = np.ctypeslib.as_array(res.off, shape=(n,)).copy()
         c = np.ctypeslib.as_array(res.cnt, shape=(n,)).copy()
         st = np.ctypeslib.as_array(res.status, shape=(n,)).copy()
-        k = (np.ctypeslib.as_array(res.keys, shape=(res.total,)).copy() if res.total
+        # UNIQUE / AGGRE lists sit at the full result's offsets: copy the whole span
+        span = int((o.astype(np.uint64) + c).max()) if res.total else 0
+        k = (np.ctypeslib.as_array(res.keys, shape=(span,)).copy() if span
              else np.zeros(0, dtype=np.uint32))
         return o, c, k, st
 

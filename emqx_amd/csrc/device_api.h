@@ -32,7 +32,6 @@ struct MatchArgs {
     const uint32_t *slot_list; // node (= slot) -> first key of its list in the arena
     const RootRec *root;
     const uint32_t *arena;
-    const uint64_t *key_id;    // key handle -> caller id (MODE_FIRST: smallest id wins)
     const uint32_t *key_bin;   // key handle -> 1 for {Binary, {ID}} keys (sort after word lists)
     // results
     uint32_t *out_off;
@@ -91,16 +90,24 @@ hipError_t launch_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *s
 uint64_t scan_scratch_words(uint32_t n);
 hipError_t launch_excl_scan(const uint32_t *in, uint64_t in_stride, uint32_t n, uint32_t *out, uint32_t *scratch,
                             hipStream_t stream);
-// ids[dst_off[t] + k] = key_id[keys[src_off[t] + k]] for k < cnt[t] (topics whose range
+// ids[dst_off[t] + k] = key_rec[2 * keys[src_off[t] + k]] (the id word of the key's
+// {id, order code} record) for k < cnt[t] (topics whose range
 // would pass `cap` are skipped).
 hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
-                             const uint64_t *key_id, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
+                             const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
                              uint64_t cap, hipStream_t stream);
 // Concatenate G shards' topic-major results per topic.  roff: G*(n+1) u32, tot: n u32,
 // scratch: scan_scratch_words(n) u32 (work areas); off: n+1 u32 out; out: merged ids.
 hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,
                                uint32_t *roff, uint32_t *tot, uint32_t *scratch, uint32_t *off, uint64_t *out,
                                uint64_t cap, hipStream_t stream);
+// Per-topic reducers over a TM_MATCH_ALL result (result_kernels.hip k_dedupe): topic t's
+// reduced keys go to ukeys[off[t] ..), their number to ucnt[t].  key_rec: 2 u64 per key
+// handle {id, order code}; key_node: u32 per handle (device slot of the key's node).
+constexpr uint32_t DD_UNIQUE = 0, DD_AGGRE = 1;
+hipError_t launch_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off, const uint32_t *keys,
+                         uint64_t keys_cap, const uint64_t *key_rec, const uint32_t *key_node, uint32_t n,
+                         uint32_t *ucnt, uint32_t *ukeys, hipStream_t stream);
 hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, hipStream_t stream);
 
 }  // namespace tmx

@@ -174,9 +174,14 @@ struct tm_engine {
     DevBuf d_wtab, d_warena, d_word_off, d_etab, d_slot_list, d_root, d_arena;
     size_t word_off_dev = 0;  // entries already on device
     DevBuf d_scatter_idx, d_scatter_src;
-    DevBuf d_key_id;                  // key handle -> caller id (u64), for device-side id results
+    DevBuf d_key_rec;                 // key handle -> {caller id, order code} (2 u64; key_ord)
+    DevBuf d_key_node;                // key handle -> device slot of its node (u32; AGGRE classes)
     DevBuf d_key_bin;                 // key handle -> 1 for {Binary, {ID}} keys (u32; FIRST order)
     std::vector<uint64_t> dirty_kid;  // handles (re)assigned since the last upload
+    uint64_t n_deep = 0;              // live word-list keys too deep for the 64-bit order code
+    DevBuf d_ukeys, d_ucnt;           // reduced results (UNIQUE / AGGRE) at the full result's offsets
+    uint64_t ukeys_cap = 0;
+    uint32_t last_mode = 0;           // TM_MATCH_* of the last batch
     DevBuf d_res_scan, d_mrg_roff, d_mrg_tot;  // scratch of tm_result_ids_device / tm_merge_shards_device
     // batch buffers
     DevBuf d_bytes, d_off, d_outoff, d_outcnt, d_status, d_keys, d_cursor, d_slow_list,
@@ -476,6 +481,7 @@ struct tm_engine {
             if (kset_find(node, kind, op.id, &slot) != NONE) return;  // set semantics
             uint32_t h = alloc_key();
             keys[h] = KeyRec{node, kind, {0, 0, 0}, op.id};
+            if (key_is_deep(h)) n_deep++;
             dirty_kid.push_back(h);
             kset[slot] = h;
             kset_used++;
@@ -499,6 +505,7 @@ struct tm_engine {
             if (h == NONE) return;
             kset_erase_slot(slot);
             deltas.push_back(Delta{node, h, (uint8_t)(kind == K_HASH), 0});
+            if (key_is_deep(h)) n_deep--;
             keys[h].kind = K_FREE;
             free_pending.push_back(h);
             n_live--;
@@ -667,47 +674,60 @@ struct tm_engine {
         return hipStreamSynchronize(stream);
     }
 
+    // key handle -> {id, order code}, device node slot, binary flag
+    void key_dev_rec(uint32_t h, uint64_t *rec, uint32_t *node, uint32_t *bin) const {
+        const KeyRec &k = keys[h];
+        rec[0] = k.id;
+        (void)key_ord(h, &rec[1]);
+        const bool live = k.kind != K_FREE && k.kind != K_DEAD;
+        *node = live ? dev_id(k.node) : NONE;
+        *bin = k.kind == K_EXACT_BIN ? 1u : 0u;
+    }
+
     hipError_t upload_key_ids_full() {
-        std::vector<uint64_t> ids(keys.size());
-        std::vector<uint32_t> bin(keys.size());
-        for (size_t h = 0; h < keys.size(); h++) {
-            ids[h] = keys[h].id;
-            bin[h] = keys[h].kind == K_EXACT_BIN ? 1u : 0u;
-        }
+        std::vector<uint64_t> rec(keys.size() * 2);
+        std::vector<uint32_t> node(keys.size()), bin(keys.size());
+        for (size_t h = 0; h < keys.size(); h++) key_dev_rec((uint32_t)h, &rec[2 * h], &node[h], &bin[h]);
         dirty_kid.clear();
-        hipError_t e = put(d_key_id, ids);
+        hipError_t e = put(d_key_rec, rec);
         if (e) return e;
+        if ((e = put(d_key_node, node))) return e;
         if ((e = put(d_key_bin, bin))) return e;
-        return hipStreamSynchronize(stream);  // `ids`, `bin` die at scope exit
+        return hipStreamSynchronize(stream);  // the staging vectors die at scope exit
     }
 
     hipError_t upload_key_ids_delta() {
         if (dirty_kid.empty()) return hipSuccess;
-        if (keys.size() * sizeof(uint64_t) > d_key_id.cap || keys.size() * sizeof(uint32_t) > d_key_bin.cap)
+        if (keys.size() * 16 > d_key_rec.cap || keys.size() * sizeof(uint32_t) > d_key_bin.cap ||
+            keys.size() * sizeof(uint32_t) > d_key_node.cap)
             return upload_key_ids_full();
         std::sort(dirty_kid.begin(), dirty_kid.end());
         dirty_kid.erase(std::unique(dirty_kid.begin(), dirty_kid.end()), dirty_kid.end());
         const size_t n = dirty_kid.size();
-        std::vector<uint64_t> idx(n), src(n);
-        std::vector<uint32_t> bin(n);
+        std::vector<uint64_t> idx(n), rec(2 * n);
+        std::vector<uint32_t> node(n), bin(n);
         for (size_t i = 0; i < n; i++) {
             idx[i] = dirty_kid[i];
-            src[i] = keys[dirty_kid[i]].id;
-            bin[i] = keys[dirty_kid[i]].kind == K_EXACT_BIN ? 1u : 0u;
+            key_dev_rec((uint32_t)dirty_kid[i], &rec[2 * i], &node[i], &bin[i]);
         }
         dirty_kid.clear();
         hipError_t e;
         if ((e = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e;
-        if ((e = d_scatter_src.ensure(n * sizeof(uint64_t)))) return e;
+        if ((e = d_scatter_src.ensure(n * 16))) return e;
         if ((e = hipMemcpyAsync(d_scatter_idx.p, idx.data(), n * 8, hipMemcpyHostToDevice, stream))) return e;
-        if ((e = hipMemcpyAsync(d_scatter_src.p, src.data(), n * 8, hipMemcpyHostToDevice, stream))) return e;
-        if ((e = launch_scatter8(d_key_id.as<uint64_t>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint64_t>(),
-                                 n, stream)))
+        if ((e = hipMemcpyAsync(d_scatter_src.p, rec.data(), n * 16, hipMemcpyHostToDevice, stream))) return e;
+        if ((e = launch_scatter16(d_key_rec.as<uint4>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint4>(), n,
+                                  stream)))
             return e;
         if ((e = hipStreamSynchronize(stream))) return e;  // d_scatter_src is reused below
         if ((e = hipMemcpyAsync(d_scatter_src.p, bin.data(), n * 4, hipMemcpyHostToDevice, stream))) return e;
         if ((e = launch_scatter4(d_key_bin.as<uint32_t>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint32_t>(), n,
                                  stream)))
+            return e;
+        if ((e = hipStreamSynchronize(stream))) return e;
+        if ((e = hipMemcpyAsync(d_scatter_src.p, node.data(), n * 4, hipMemcpyHostToDevice, stream))) return e;
+        if ((e = launch_scatter4(d_key_node.as<uint32_t>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint32_t>(),
+                                 n, stream)))
             return e;
         return hipStreamSynchronize(stream);
     }
@@ -850,6 +870,44 @@ struct tm_engine {
         return s;
     }
 
+    // Order code of a key among the keys that match ONE topic.  Such keys agree on every
+    // literal level (each equals the topic's word), so Erlang term order between them is
+    // decided by the shape alone: per level END < '#' < '+' < literal ('#' < '+' as atoms,
+    // atoms < binaries, a list that ends first sorts first), and every {Binary, {ID}} key
+    // sorts after every word list.  Code: bit 62 = binary key; levels 0..30 as 2-bit
+    // symbols from bit 61 down (END 0, '#' 1, '+' 2, literal 3); bit 63 flags a '#' key and
+    // is not part of the order.  Returns false when the shape needs more than 31 levels.
+    static constexpr uint64_t ORD_HASH = 1ull << 63, ORD_BIN = 1ull << 62;
+    bool key_ord(uint32_t h, uint64_t *ord) const {
+        const KeyRec &k = keys[h];
+        *ord = 0;
+        if (k.kind == K_EXACT_BIN) {
+            *ord = ORD_BIN;
+            return true;
+        }
+        if (k.kind != K_EXACT_WORDS && k.kind != K_WILD && k.kind != K_HASH) return true;
+        uint32_t n = 0;
+        for (uint32_t v = k.node; v != ROOT; v = node_parent[v]) n++;
+        uint64_t o = 0;
+        uint32_t i = n;
+        for (uint32_t v = k.node; v != ROOT; v = node_parent[v]) {
+            i--;
+            if (i < 31) o |= (uint64_t)(node_word[v] == W_PLUS ? 2u : 3u) << (60 - 2 * i);
+        }
+        bool deep = n > 31;
+        if (k.kind == K_HASH) {
+            if (n < 31) o |= 1ull << (60 - 2 * n);
+            o |= ORD_HASH;
+            deep = n > 30;
+        }
+        *ord = o;
+        return !deep;
+    }
+    bool key_is_deep(uint32_t h) const {
+        uint64_t o;
+        return !key_ord(h, &o);
+    }
+
     // ETS term order of two keys (emqx_trie_search.erl:109-111 key shapes; Erlang term
     // order: lists < binaries; atoms '#' < '+' < binaries; binaries bytewise; then {ID}).
     // Used to reproduce return_first (the first key the ordered walk meets) and unique
@@ -962,7 +1020,8 @@ void tm_destroy(tm_engine *eng) {
     if (!eng) return;
     (void)hipSetDevice(eng->cfg.device);
     if (eng->stream) (void)hipStreamSynchronize(eng->stream);
-    for (DevBuf *b : {&eng->d_key_id, &eng->d_key_bin, &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot})
+    for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_ukeys, &eng->d_ucnt,
+                      &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
                       &eng->d_arena, &eng->d_scatter_idx,
@@ -1087,7 +1146,6 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     MatchArgs a{};
     a.mode = mode;
     a.tpw = pick_tpw(n, eng->cfg.topics_per_wave);
-    a.key_id = eng->d_key_id.as<uint64_t>();
     a.key_bin = eng->d_key_bin.as<uint32_t>();
     a.bytes = d_bytes;
     a.off = d_off;
@@ -1125,10 +1183,28 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     return launch_match(a, s);
 }
 
+// UNIQUE / AGGRE on the GPU: k_dedupe reduces the full result of the batch just enqueued
+// into d_ukeys / d_ucnt (same offsets).
+static bool reduced_mode(uint32_t mode) { return mode == TM_MATCH_UNIQUE || mode == TM_MATCH_AGGRE; }
+
+static int enqueue_reduce(tm_engine *eng, uint32_t mode, uint32_t n, hipStream_t s) {
+    if (eng->ukeys_cap < eng->keys_cap) {
+        TM_TRY_HIP(eng->d_ukeys.ensure(eng->keys_cap * 4), TM_ENOMEM, "alloc reduced keys");
+        eng->ukeys_cap = eng->keys_cap;
+    }
+    TM_TRY_HIP(eng->d_ucnt.ensure((uint64_t)n * 4 + 4), TM_ENOMEM, "alloc reduced counts");
+    TM_TRY_HIP(launch_dedupe(mode == TM_MATCH_UNIQUE ? DD_UNIQUE : DD_AGGRE, eng->d_outcnt.as<uint32_t>(),
+                             eng->d_outoff.as<uint32_t>(), eng->d_keys.as<uint32_t>(), eng->keys_cap,
+                             eng->d_key_rec.as<uint64_t>(), eng->d_key_node.as<uint32_t>(), n,
+                             eng->d_ucnt.as<uint32_t>(), eng->d_ukeys.as<uint32_t>(), s),
+               TM_EDEVICE, "dedupe");
+    return TM_OK;
+}
+
 int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
                    tm_result *out) {
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
-    if (mode > TM_MATCH_COUNT) return TM_EINVAL;
+    if (mode > TM_MATCH_AGGRE) return TM_EINVAL;
     if (eng->edge_full) return TM_ESTATE;
     if (!eng->staged.empty()) {
         eng->err = "tm_match_batch: staged ops not committed";
@@ -1137,6 +1213,9 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     memset(out, 0, sizeof(*out));
     out->n = n;
+    // UNIQUE is reduced on the GPU unless a key is too deep for the device order code
+    const bool dev_reduce = reduced_mode(mode) && (mode == TM_MATCH_AGGRE || eng->n_deep == 0);
+    eng->last_mode = (reduced_mode(mode) && !dev_reduce) ? TM_MATCH_ALL : mode;  // what the device holds
     if (n == 0) return TM_OK;
     // rebase offsets to 0
     uint32_t base = off[0];
@@ -1185,19 +1264,22 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
         eng->keys_cap = want;
     }
     uint64_t total = kmode == MODE_ALL ? *eng->h_cursor.as<uint64_t>() : (kmode == MODE_FIRST ? n : 0);
+    if (dev_reduce && (rc = enqueue_reduce(eng, mode, n, s))) return rc;
     TM_TRY_HIP(eng->h_outoff.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(eng->h_outcnt.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(eng->h_status.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(eng->h_keys.ensure(total * 4 + 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(hipMemcpyAsync(eng->h_outoff.p, eng->d_outoff.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                "D2H");
-    TM_TRY_HIP(hipMemcpyAsync(eng->h_outcnt.p, eng->d_outcnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-               "D2H");
+    TM_TRY_HIP(hipMemcpyAsync(eng->h_outcnt.p, (dev_reduce ? eng->d_ucnt : eng->d_outcnt).p, (size_t)n * 4,
+                              hipMemcpyDeviceToHost, s),
+               TM_EDEVICE, "D2H");
     TM_TRY_HIP(hipMemcpyAsync(eng->h_status.p, eng->d_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                "D2H");
     if (total)
-        TM_TRY_HIP(hipMemcpyAsync(eng->h_keys.p, eng->d_keys.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-                   "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(eng->h_keys.p, (dev_reduce ? eng->d_ukeys : eng->d_keys).p, total * 4,
+                                  hipMemcpyDeviceToHost, s),
+                   TM_EDEVICE, "D2H");
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "D2H");
     if ((rc = grow_pools(eng))) return rc;
     out->total = total;
@@ -1206,6 +1288,12 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
     out->keys = eng->h_keys.as<uint32_t>();
     out->status = eng->h_status.as<int32_t>();
     if (mode == TM_MATCH_ALL) return TM_OK;
+    if (dev_reduce) {  // reduced lists sit at the full result's offsets, with gaps
+        uint64_t t = 0;
+        for (uint32_t i = 0; i < n; i++) t += out->cnt[i];
+        out->total = t;
+        return TM_OK;
+    }
     if (mode == TM_MATCH_COUNT) {  // counts only: no keys
         eng->pp_off.assign(n, 0);
         out->off = eng->pp_off.data();
@@ -1226,7 +1314,8 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
         return TM_OK;
     }
 
-    // UNIQUE: reduce each topic's set under ETS term order.
+    // UNIQUE with a key deeper than the device order code: reduce each topic's set under
+    // ETS term order here.
     eng->pp_off.resize(n);
     eng->pp_cnt.resize(n);
     eng->pp_keys.clear();
@@ -1286,8 +1375,12 @@ int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_of
 
 int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                          uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out) {
-    if (mode != TM_MATCH_ALL && mode != TM_MATCH_FIRST && mode != TM_MATCH_COUNT) return TM_EINVAL;
+    if (mode > TM_MATCH_AGGRE) return TM_EINVAL;
     if (!eng || eng->edge_full) return eng ? TM_ESTATE : TM_EINVAL;
+    if (mode == TM_MATCH_UNIQUE && eng->n_deep) {
+        eng->err = "tm_match_device_mode: UNIQUE with filters deeper than 31 levels is host-only (tm_match_batch)";
+        return TM_ESTATE;
+    }
     if (!eng || !out || !d_off || (n && !d_bytes)) return TM_EINVAL;
     if (!eng->staged.empty()) {
         eng->err = "tm_match_device: staged ops not committed";
@@ -1306,10 +1399,12 @@ int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t 
         eng->keys_cap = n;
     }
     TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s, kmode), TM_EDEVICE, "kernel launch");
+    eng->last_mode = mode;
+    if (reduced_mode(mode) && (rc = enqueue_reduce(eng, mode, n, s))) return rc;
     out->n = n;
     out->d_off = eng->d_outoff.as<uint32_t>();
-    out->d_cnt = eng->d_outcnt.as<uint32_t>();
-    out->d_keys = eng->d_keys.as<uint32_t>();
+    out->d_cnt = (reduced_mode(mode) ? eng->d_ucnt : eng->d_outcnt).as<uint32_t>();
+    out->d_keys = (reduced_mode(mode) ? eng->d_ukeys : eng->d_keys).as<uint32_t>();
     out->d_status = eng->d_status.as<int32_t>();
     out->d_total = eng->d_cursor.as<uint64_t>();
     out->keys_cap = eng->keys_cap;
@@ -1347,10 +1442,11 @@ int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint
     hipStream_t s = stream ? (hipStream_t)stream : (eng->last_stream ? eng->last_stream : eng->stream);
     const uint32_t n = eng->last_n;
     TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(launch_excl_scan(eng->d_outcnt.as<uint32_t>(), 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s),
-               TM_EDEVICE, "scan");
-    TM_TRY_HIP(launch_result_ids(eng->d_outcnt.as<uint32_t>(), eng->d_outoff.as<uint32_t>(), eng->d_keys.as<uint32_t>(),
-                                 eng->d_key_id.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, s),
+    const bool red = reduced_mode(eng->last_mode);
+    const uint32_t *cnt = (red ? eng->d_ucnt : eng->d_outcnt).as<uint32_t>();
+    TM_TRY_HIP(launch_excl_scan(cnt, 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s), TM_EDEVICE, "scan");
+    TM_TRY_HIP(launch_result_ids(cnt, eng->d_outoff.as<uint32_t>(), (red ? eng->d_ukeys : eng->d_keys).as<uint32_t>(),
+                                 eng->d_key_rec.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, s),
                TM_EDEVICE, "result ids");
     return TM_OK;
 }
@@ -1435,6 +1531,7 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
     out->commit_apply_us = eng->commit_us[0];
     out->commit_lists_us = eng->commit_us[1];
     out->commit_upload_us = eng->commit_us[2];
+    out->n_deep_keys = eng->n_deep;
     return TM_OK;
 }
 

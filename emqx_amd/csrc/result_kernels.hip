@@ -10,6 +10,9 @@
 //     after the all-gather, topic t's result is the concatenation of its slices from
 //     rank 0..G-1 (shards are disjoint, so no dedupe).
 //
+//   * per-topic reducers (k_dedupe): matches/3 with [unique] and emqx_broker:aggre/1 on
+//     the GPU, over the full result.
+//
 // All of it is byte movement: coalesced where the layout allows, HBM-bound.
 #include <hip/hip_runtime.h>
 
@@ -105,7 +108,7 @@ hipError_t launch_excl_scan(const uint32_t *in, uint64_t in_stride, uint32_t n, 
 // copied by the topic's own lane; longer ones (hot '#' lists) by the whole wave, 64
 // consecutive keys per instruction.
 __global__ __launch_bounds__(64) void k_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
-                                                   const uint64_t *key_id, const uint32_t *dst_off, uint32_t n,
+                                                   const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n,
                                                    uint64_t *ids, uint64_t cap) {
     const uint32_t lane = threadIdx.x;
     const uint32_t t = blockIdx.x * 64 + lane;
@@ -118,22 +121,22 @@ __global__ __launch_bounds__(64) void k_result_ids(const uint32_t *cnt, const ui
     }
     const bool is_long = c > 8;
     if (!is_long) {
-        for (uint32_t k = 0; k < c; k++) ids[(uint64_t)dofs + k] = key_id[keys[(uint64_t)so + k]];
+        for (uint32_t k = 0; k < c; k++) ids[(uint64_t)dofs + k] = key_rec[2ull * keys[(uint64_t)so + k]];
     }
     uint64_t longs = __ballot(is_long);
     while (longs) {
         const int l = __builtin_ctzll(longs);
         longs &= longs - 1;
         const uint32_t lc = __shfl(c, l, 64), ls = __shfl(so, l, 64), ld = __shfl(dofs, l, 64);
-        for (uint32_t k = lane; k < lc; k += 64) ids[(uint64_t)ld + k] = key_id[keys[(uint64_t)ls + k]];
+        for (uint32_t k = lane; k < lc; k += 64) ids[(uint64_t)ld + k] = key_rec[2ull * keys[(uint64_t)ls + k]];
     }
 }
 
 hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
-                             const uint64_t *key_id, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
+                             const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
                              uint64_t cap, hipStream_t s) {
     if (!n) return hipSuccess;
-    k_result_ids<<<(n + 63) / 64, 64, 0, s>>>(cnt, src_off, keys, key_id, dst_off, n, ids, cap);
+    k_result_ids<<<(n + 63) / 64, 64, 0, s>>>(cnt, src_off, keys, key_rec, dst_off, n, ids, cap);
     return hipGetLastError();
 }
 
@@ -182,6 +185,136 @@ hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, c
     if ((e = launch_excl_scan(tot, 1, n, off, scratch, s))) return e;
     if (!n) return hipSuccess;
     k_merge<<<(n + 63) / 64, 64, 0, s>>>(counts, ids, stride, roff, off, G, n, out, cap);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Per-topic reducers over a full (TM_MATCH_ALL) result, written to a second key array
+// at the same offsets (a reduced list is never longer than the full one):
+//
+//   DD_UNIQUE  matches/3 with [unique]: the walk visits keys in ascending ETS term order
+//              and match_add/2 does Acc#{ID => K} (emqx_trie_search.erl:349-351), so per
+//              id the GREATEST matching key survives.  key_rec[2h+1] is the key's order
+//              code (engine.cpp key_ord): among keys that match one topic it orders them
+//              exactly as Erlang term order does.
+//   DD_AGGRE   emqx_broker:aggre/1 (emqx_broker.erl:361-377): keys of shared dests
+//              (TM_ID_SHARED) collapse per {Filter, Group}; a filter is (node slot, '#'
+//              flag) among the keys of one topic; the largest handle represents the class.
+//
+// One wave per topic (grid-stride).  A per-wave LDS hash table {class, max value}; a list
+// longer than DD_PASS keys is done in ceil(c / DD_PASS) passes, pass p taking the classes
+// whose hash falls in p, so the table never runs past half full.  Insert = CAS on the
+// class word then a 64-bit LDS atomic max on the value; every lane's probe loop ends on
+// its own CAS result, so no lane waits on another.
+constexpr int DD_TAB = 1024;   // slots per wave (16 KiB of LDS)
+constexpr uint32_t DD_PASS = 512;
+constexpr uint64_t DD_EMPTY = ~0ull;
+constexpr uint64_t ORD_HASH_FLAG = 1ull << 63;  // key_rec ord bit 63: a '#' key (not part of the order)
+
+__device__ __forceinline__ bool dd_class(uint32_t mode, uint32_t h, const uint64_t *key_rec, const uint32_t *key_node,
+                                         uint64_t *cls, uint64_t *val) {
+    const uint64_t id = key_rec[2ull * h];
+    const uint64_t ord = key_rec[2ull * h + 1];
+    if (mode == DD_UNIQUE) {
+        *cls = id;
+        *val = ord & ~ORD_HASH_FLAG;
+        return true;
+    }
+    if (!(id >> 63)) return false;  // plain node dest: always kept
+    *cls = ((uint64_t)key_node[h] << 32) | (((id >> 32) & 0x7FFFFFFFull) << 1) | (ord >> 63);
+    *val = h;
+    return true;
+}
+
+__global__ __launch_bounds__(64) void k_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off,
+                                               const uint32_t *keys, uint64_t keys_cap, const uint64_t *key_rec,
+                                               const uint32_t *key_node, uint32_t n, uint32_t *ucnt,
+                                               uint32_t *ukeys) {
+    __shared__ unsigned long long t_cls[DD_TAB];
+    __shared__ unsigned long long t_val[DD_TAB];
+    __shared__ unsigned long long ff_val;  // the one class equal to DD_EMPTY (UNIQUE id ~0)
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t t = blockIdx.x; t < n; t += gridDim.x) {
+        uint32_t c = cnt[t];
+        const uint64_t o = off[t];
+        if (o + c > keys_cap) c = 0;  // overflowed batch: the caller re-runs it
+        if (c <= 1) {
+            if (lane == 0) {
+                if (c) ukeys[o] = keys[o];
+                ucnt[t] = c;
+            }
+            continue;
+        }
+        const uint32_t P = (c + DD_PASS - 1) / DD_PASS;
+        uint32_t S = 64;
+        while (S < 2 * c && S < (uint32_t)DD_TAB) S <<= 1;
+        const uint32_t smask = S - 1;
+        uint32_t base = 0;
+        for (uint32_t p = 0; p < P; p++) {
+            for (uint32_t j = lane; j < S; j += 64) {
+                t_cls[j] = DD_EMPTY;
+                t_val[j] = 0;
+            }
+            if (lane == 0) ff_val = 0;
+            __syncthreads();
+            for (uint32_t i = lane; i < c; i += 64) {
+                uint64_t cl, v;
+                if (!dd_class(mode, keys[o + i], key_rec, key_node, &cl, &v)) continue;
+                const uint64_t hm = mix64(cl);
+                if ((uint32_t)(hm >> 40) % P != p) continue;
+                if (cl == DD_EMPTY) {
+                    atomicMax(&ff_val, (unsigned long long)v);
+                    continue;
+                }
+                uint32_t s = (uint32_t)hm & smask;
+                for (;;) {
+                    const unsigned long long prev = atomicCAS(&t_cls[s], DD_EMPTY, (unsigned long long)cl);
+                    if (prev == DD_EMPTY || prev == cl) {
+                        atomicMax(&t_val[s], (unsigned long long)v);
+                        break;
+                    }
+                    s = (s + 1) & smask;
+                }
+            }
+            __syncthreads();
+            for (uint32_t i0 = 0; i0 < c; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                bool keep = false;
+                uint32_t h = 0;
+                if (i < c) {
+                    h = keys[o + i];
+                    uint64_t cl, v;
+                    if (!dd_class(mode, h, key_rec, key_node, &cl, &v)) {
+                        keep = p == 0;  // never deduplicated: emitted once, in the first pass
+                    } else {
+                        const uint64_t hm = mix64(cl);
+                        if ((uint32_t)(hm >> 40) % P == p) {
+                            if (cl == DD_EMPTY) {
+                                keep = ff_val == v;
+                            } else {
+                                uint32_t s = (uint32_t)hm & smask;
+                                while (t_cls[s] != cl) s = (s + 1) & smask;
+                                keep = t_val[s] == v;
+                            }
+                        }
+                    }
+                }
+                const uint64_t m = __ballot(keep);
+                if (keep) ukeys[o + base + __popcll(m & ((1ull << lane) - 1))] = h;
+                base += __popcll(m);
+            }
+            __syncthreads();
+        }
+        if (lane == 0) ucnt[t] = base;
+    }
+}
+
+hipError_t launch_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off, const uint32_t *keys,
+                         uint64_t keys_cap, const uint64_t *key_rec, const uint32_t *key_node, uint32_t n,
+                         uint32_t *ucnt, uint32_t *ukeys, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint32_t grid = n < 65536u ? n : 65536u;
+    k_dedupe<<<grid, 64, 0, s>>>(mode, cnt, off, keys, keys_cap, key_rec, key_node, n, ucnt, ukeys);
     return hipGetLastError();
 }
 

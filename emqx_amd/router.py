@@ -25,16 +25,25 @@ class Router:
         self.eng = engine or N.Engine(device, **kw)
         self.node = node
         self._dest_id: dict = {}
-        self._dests: list = []
+        self._dests: dict = {}  # route id -> dest
+        self._groups: dict = {}  # shared group -> [group index, members so far]
         self._routes: dict = {}  # filter bytes -> set(dest)   (lookup_routes / topics)
         self._dirty = False
 
     def _did(self, dest) -> int:
+        """Route id of a dest.  A shared dest {Group, Node} gets TM_SHARED_ID(group, member)
+        (include/emqx_tm.h), so the GPU can collapse {Filter, Group} for aggre/1; a node dest
+        gets a plain id."""
         u = self._dest_id.get(dest)
         if u is None:
-            u = len(self._dests)
+            if isinstance(dest, tuple):
+                g = self._groups.setdefault(dest[0], [len(self._groups), 0])
+                u = N.shared_id(g[0], g[1])
+                g[1] += 1
+            else:
+                u = len(self._dest_id)
             self._dest_id[dest] = u
-            self._dests.append(dest)
+            self._dests[u] = dest
         return u
 
     @staticmethod
@@ -109,6 +118,29 @@ class Router:
                 u, fb, _ = self.eng.key_info(h)
                 routes.append((fb, self._dests[u]))
             out.append(routes)
+        return out
+
+    def match_aggre_batch(self, topics) -> list:
+        """[aggre(match_routes(T)) per topic] with the {Filter, Group} collapse done on the GPU
+        (TM_MATCH_AGGRE).  emqx_broker:do_route/1 feeds match_routes/1 through aggre/1
+        (emqx_broker.erl:361-377) before dispatch; only the final usort ordering is done
+        here."""
+        self.commit()
+        res = self.eng.match(topics, N.TM_MATCH_AGGRE)
+        out = []
+        for hs in res:
+            if hs is None:
+                raise ValueError("badarg")
+            acc, dedup = [], False
+            for h in hs:
+                u, fb, _ = self.eng.key_info(h)
+                d = self._dests[u]
+                if isinstance(d, tuple):
+                    dedup = True
+                    acc.append((fb, d[0]))
+                else:
+                    acc.append((fb, d))
+            out.append(sorted(acc, key=repr) if dedup else acc)
         return out
 
     def match_routes(self, topic) -> list:

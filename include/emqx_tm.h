@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define TM_ABI_VERSION 2u
+#define TM_ABI_VERSION 3u
 
 /* status codes */
 #define TM_OK          0
@@ -80,6 +80,17 @@ extern "C" {
                                (k_match_first): topic i's key, if any, is keys[off[i]]  */
 #define TM_MATCH_COUNT  3u  /* counts only, no keys: has_any_route/1
                                (emqx_persistent_session_ds_router.erl:115-125) is cnt > 0 */
+#define TM_MATCH_AGGRE  4u  /* emqx_broker:aggre/1 (emqx_broker.erl:361-377): keys whose id is a
+                               shared-subscription dest (TM_ID_SHARED) collapse to one key per
+                               {Filter, Group}; every other key is kept */
+
+/* Route-id convention for TM_MATCH_AGGRE: a $share/$queue dest {Group, Node}
+ * (emqx_shared_sub.erl:444-456) gets an id with TM_ID_SHARED set and its group index in
+ * bits 32..62; the low 32 bits tell the nodes of one group apart.  Ids without the flag
+ * are plain node dests. */
+#define TM_ID_SHARED        (1ull << 63)
+#define TM_ID_GROUP(id)     (((id) >> 32) & 0x7FFFFFFFull)
+#define TM_SHARED_ID(group, member) (TM_ID_SHARED | ((uint64_t)(group) << 32) | (uint32_t)(member))
 
 /* tm_config.flags */
 #define TM_CFG_FORCE_SLOW 1u  /* route every topic through the spill (slow) kernel: test aid */
@@ -116,7 +127,8 @@ typedef struct tm_op {
  * tm_match_batch / tm_commit_epoch / tm_destroy on the same engine.
  * Topic i's matches are keys[off[i] .. off[i]+cnt[i]), in unspecified order
  * (the reference returns them in reverse ETS term order; callers must not rely
- * on order).  In TM_MATCH_FIRST mode cnt[i] is 0 or 1. */
+ * on order).  In TM_MATCH_FIRST mode cnt[i] is 0 or 1.  Lists need not be contiguous:
+ * TM_MATCH_UNIQUE / TM_MATCH_AGGRE reduce each list in place of the full one. */
 typedef struct tm_result {
     uint32_t        n;
     uint32_t        _pad;
@@ -156,6 +168,7 @@ typedef struct tm_stats_t {
     uint64_t commit_apply_us;
     uint64_t commit_lists_us;
     uint64_t commit_upload_us;
+    uint64_t n_deep_keys;   /* live word-list keys deeper than the device order code (31 levels) */
 } tm_stats_t;
 
 /* lifecycle --------------------------------------------------------------- */
@@ -192,8 +205,12 @@ int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_of
  * the internal chunk pools to that batch's demand for the next one. */
 int tm_device_sync(tm_engine *eng);
 /* tm_match_device with a match mode: TM_MATCH_ALL (= tm_match_device), TM_MATCH_FIRST
- * (one key per topic, d_total not used) or TM_MATCH_COUNT (d_cnt only).  TM_MATCH_UNIQUE
- * is host-side (tm_match_batch). */
+ * (one key per topic, d_total not used), TM_MATCH_COUNT (d_cnt only), TM_MATCH_UNIQUE or
+ * TM_MATCH_AGGRE (the full set is reduced on the GPU: topic i's keys are
+ * d_keys[d_off[i] .. d_off[i]+d_cnt[i]); *d_total still counts the UNREDUCED keys and
+ * decides overflow as for TM_MATCH_ALL).  TM_MATCH_UNIQUE returns TM_ESTATE while the index
+ * holds a filter of more than 31 levels (its term order does not fit the device's 64-bit
+ * order code); tm_match_batch then reduces on the host. */
 int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                          uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out);
 int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap);

@@ -31,8 +31,8 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert name in exported, name
         assert getattr(lib, name) is not None
-    assert lib.tm_abi_version() == 2
-    assert C.sizeof(N.tm_stats_t) == 14 * 8  # mirrors tm_stats_t in include/emqx_tm.h
+    assert lib.tm_abi_version() == 3
+    assert C.sizeof(N.tm_stats_t) == 15 * 8  # mirrors tm_stats_t in include/emqx_tm.h
 
 
 def test_kernels_are_gfx950_code_objects():
