@@ -284,8 +284,10 @@ def main():
             lat_sweep.append({"batch": bs, "p50_ms": round(float(np.percentile(ms, 50)), 4),
                               "p99_ms": round(float(np.percentile(ms, 99)), 4),
                               "publishes_per_s": round(bs / (float(np.mean(ms)) * 1e-3), 1)})
-        # the other reducers on the same batch: return_first (k_match_first) and counts only
-        for mname, mode in (("first", N.TM_MATCH_FIRST), ("count", N.TM_MATCH_COUNT)):
+        # the other reducers on the same batch: return_first (k_match_first), counts only, and
+        # the full walk + k_dedupe ([unique]; aggre/1)
+        for mname, mode in (("first", N.TM_MATCH_FIRST), ("count", N.TM_MATCH_COUNT), ("unique", N.TM_MATCH_UNIQUE),
+                            ("aggre", N.TM_MATCH_AGGRE)):
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
             for k in range(12):
                 if k >= 2:

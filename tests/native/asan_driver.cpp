@@ -7,6 +7,7 @@
 // adds/deletes (incl. invalid and $-filters, word-list keys, re-adds inside one epoch),
 // matches in every mode, key introspection, result shaping and the shard merge, and
 // checks the modes against each other: COUNT == |ALL|, FIRST in ALL, UNIQUE subset of ALL.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -129,6 +130,23 @@ int main() {
         for (uint32_t i = 0; i < n; i++) {
             CHECK(res.cnt[i] <= acnt[i]);
             CHECK(acnt[i] == 0 || res.cnt[i] >= 1);
+            // one key per id, and every id of the full set is there
+            std::vector<uint64_t> uid(res.cnt[i]), aid(acnt[i]);
+            CHECK(tm_key_ids(eng, res.keys + res.off[i], res.cnt[i], uid.data()) == TM_OK);
+            CHECK(tm_key_ids(eng, akeys.data() + aoff[i], acnt[i], aid.data()) == TM_OK);
+            std::sort(uid.begin(), uid.end());
+            std::sort(aid.begin(), aid.end());
+            aid.erase(std::unique(aid.begin(), aid.end()), aid.end());
+            CHECK(uid == aid);
+        }
+        CHECK(tm_match_batch(eng, (const uint8_t *)bytes.data(), off.data(), n, TM_MATCH_AGGRE, &res) == TM_OK);
+        for (uint32_t i = 0; i < n; i++) {
+            CHECK(res.cnt[i] <= acnt[i]);
+            for (uint32_t k = 0; k < res.cnt[i]; k++) {
+                bool found = false;
+                for (uint32_t j = 0; j < acnt[i]; j++) found |= akeys[aoff[i] + j] == res.keys[res.off[i] + k];
+                CHECK(found);
+            }
         }
         // introspection of every matched key
         for (uint32_t k : akeys) {
