@@ -135,6 +135,12 @@ def cpu_info():
     return model
 
 
+def host_rss_gib():
+    """Peak resident host memory of this rank (the engine's host master copy + workload)."""
+    import resource
+    return round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 2)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -368,6 +374,7 @@ def main():
             "parity": parity,
             "spill_topics": int(slow_topics),
             "build_s": round(t_build, 2),
+            "host_peak_rss_gib": host_rss_gib(),
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -557,6 +564,7 @@ def run_churn(args):
         "publishes_per_s_incl_commit": round(n * len(match_ms) / ((np.sum(match_ms) + np.sum(commit_ms)) * 1e-3), 1),
         "full_rebuilds": st["n_full_rebuilds"], "delta_commits": st["n_delta_commits"],
         "build_s": round(t_build, 2),
+        "host_peak_rss_gib": host_rss_gib(),
         "parity": {"sampled_topics": ps, "mismatches": int(bad), "oracle": "oracle/trie_search.cpp"},
     }), flush=True)
 
