@@ -498,7 +498,7 @@ def run_churn(args):
     live_f = list(fl)
     live_id = w.f_id.astype(np.uint64).copy()
     next_id = int(live_id.max()) + 1
-    commit_ms, match_ms, nops = [], [], []
+    commit_ms, match_ms, nops, phases = [], [], [], []
 
     def pack(fs, ids):
         off = np.zeros(len(fs) + 1, dtype=np.uint64)
@@ -539,6 +539,8 @@ def run_churn(args):
         live_f = [f for f, kk in zip(live_f, keep) if kk] + add_f
         live_id = np.concatenate([live_id[keep], add_id])
         if ep >= args.warmup:
+            cs = eng.stats()
+            phases.append((cs["commit_apply_us"], cs["commit_lists_us"], cs["commit_upload_us"]))
             commit_ms.append((t1 - t0) * 1e3)
             match_ms.append(e0.elapsed_time(e1))
             nops.append(2 * k)
@@ -559,6 +561,8 @@ def run_churn(args):
         "epochs": args.churn, "ops_per_epoch": int(np.mean(nops)),
         "commit_ms_p50": round(float(np.percentile(commit_ms, 50)), 3),
         "commit_ms_p99": round(float(np.percentile(commit_ms, 99)), 3),
+        "commit_phase_ms_p50": dict(zip(("apply", "lists", "upload"),
+                                        (round(float(x) / 1e3, 3) for x in np.percentile(np.array(phases), 50, axis=0)))),
         "route_ops_per_s": round(float(np.sum(nops) / (np.sum(commit_ms) * 1e-3)), 1),
         "match_ms_p50": round(float(np.percentile(match_ms, 50)), 4),
         "publishes_per_s_incl_commit": round(n * len(match_ms) / ((np.sum(match_ms) + np.sum(commit_ms)) * 1e-3), 1),
