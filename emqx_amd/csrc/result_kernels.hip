@@ -201,30 +201,60 @@ hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, c
 //              (TM_ID_SHARED) collapse per {Filter, Group}; a filter is (node slot, '#'
 //              flag) among the keys of one topic; the largest handle represents the class.
 //
-// One wave per topic (grid-stride).  A per-wave LDS hash table {class, max value}; a list
-// longer than DD_PASS keys is done in ceil(c / DD_PASS) passes, pass p taking the classes
-// whose hash falls in p, so the table never runs past half full.  Insert = CAS on the
-// class word then a 64-bit LDS atomic max on the value; every lane's probe loop ends on
-// its own CAS result, so no lane waits on another.
+// One wave per topic (grid-stride).  A per-wave LDS hash table {class, max value}.
+//   * Lists of up to DD_REG keys (nearly all of them) take ONE pass with every key held in
+//     registers: DD_U keys per lane, their handle loads and then their 16-B record
+//     gathers all issued before the first is used, so a topic costs two dependent
+//     round trips, not two per 64 keys.
+//   * Longer lists take ceil(c / DD_PASS) passes, pass p handling the classes whose hash
+//     falls in p, so the table never runs past half full.
+// Insert = CAS on the class word, then a 64-bit LDS atomic max on the value; every lane's
+// probe loop ends on its own CAS result, so no lane waits on another.
 constexpr int DD_TAB = 1024;   // slots per wave (16 KiB of LDS)
 constexpr uint32_t DD_PASS = 512;
+constexpr int DD_U = 8;        // keys per lane in the one-pass case
+constexpr uint32_t DD_REG = 64u * DD_U;
 constexpr uint64_t DD_EMPTY = ~0ull;
 constexpr uint64_t ORD_HASH_FLAG = 1ull << 63;  // key_rec ord bit 63: a '#' key (not part of the order)
 
-__device__ __forceinline__ bool dd_class(uint32_t mode, uint32_t h, const uint64_t *key_rec, const uint32_t *key_node,
-                                         uint64_t *cls, uint64_t *val) {
-    const uint64_t id = key_rec[2ull * h];
-    const uint64_t ord = key_rec[2ull * h + 1];
-    if (mode == DD_UNIQUE) {
-        *cls = id;
-        *val = ord & ~ORD_HASH_FLAG;
-        return true;
-    }
-    if (!(id >> 63)) return false;  // plain node dest: always kept
-    *cls = ((uint64_t)key_node[h] << 32) | (((id >> 32) & 0x7FFFFFFFull) << 1) | (ord >> 63);
-    *val = h;
-    return true;
+struct DdKey {
+    uint64_t cls, val;
+    bool dd;  // false: never deduplicated (AGGRE plain dest)
+};
+
+__device__ __forceinline__ DdKey dd_class(uint32_t mode, uint32_t h, const uint64_t *key_rec,
+                                          const uint32_t *key_node) {
+    const ulonglong2 r = *reinterpret_cast<const ulonglong2 *>(key_rec + 2ull * h);  // {id, ord}
+    if (mode == DD_UNIQUE) return DdKey{r.x, r.y & ~ORD_HASH_FLAG, true};
+    if (!(r.x >> 63)) return DdKey{0, 0, false};  // plain node dest: always kept
+    return DdKey{((uint64_t)key_node[h] << 32) | (((r.x >> 32) & 0x7FFFFFFFull) << 1) | (r.y >> 63), h, true};
 }
+
+struct DdTable {
+    unsigned long long *cls, *val, *ff;
+    uint32_t mask;
+    __device__ __forceinline__ void insert(const DdKey &k) const {
+        if (k.cls == DD_EMPTY) {
+            atomicMax(ff, (unsigned long long)k.val);
+            return;
+        }
+        uint32_t s = (uint32_t)mix64(k.cls) & mask;
+        for (;;) {
+            const unsigned long long prev = atomicCAS(&cls[s], DD_EMPTY, (unsigned long long)k.cls);
+            if (prev == DD_EMPTY || prev == k.cls) {
+                atomicMax(&val[s], (unsigned long long)k.val);
+                return;
+            }
+            s = (s + 1) & mask;
+        }
+    }
+    __device__ __forceinline__ bool winner(const DdKey &k) const {
+        if (k.cls == DD_EMPTY) return *ff == k.val;
+        uint32_t s = (uint32_t)mix64(k.cls) & mask;
+        while (cls[s] != k.cls) s = (s + 1) & mask;
+        return val[s] == k.val;
+    }
+};
 
 __global__ __launch_bounds__(64) void k_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off,
                                                const uint32_t *keys, uint64_t keys_cap, const uint64_t *key_rec,
@@ -245,65 +275,75 @@ __global__ __launch_bounds__(64) void k_dedupe(uint32_t mode, const uint32_t *cn
             }
             continue;
         }
-        const uint32_t P = (c + DD_PASS - 1) / DD_PASS;
         uint32_t S = 64;
         while (S < 2 * c && S < (uint32_t)DD_TAB) S <<= 1;
-        const uint32_t smask = S - 1;
+        const DdTable T{t_cls, t_val, &ff_val, S - 1};
+        for (uint32_t j = lane; j < S; j += 64) {
+            t_cls[j] = DD_EMPTY;
+            t_val[j] = 0;
+        }
+        if (lane == 0) ff_val = 0;
         uint32_t base = 0;
-        for (uint32_t p = 0; p < P; p++) {
-            for (uint32_t j = lane; j < S; j += 64) {
-                t_cls[j] = DD_EMPTY;
-                t_val[j] = 0;
+        if (c <= DD_REG) {
+            uint32_t hh[DD_U];
+            DdKey kk[DD_U];
+#pragma unroll
+            for (int u = 0; u < DD_U; u++) {
+                const uint32_t i = u * 64 + lane;
+                hh[u] = i < c ? keys[o + i] : 0u;
             }
-            if (lane == 0) ff_val = 0;
-            __syncthreads();
-            for (uint32_t i = lane; i < c; i += 64) {
-                uint64_t cl, v;
-                if (!dd_class(mode, keys[o + i], key_rec, key_node, &cl, &v)) continue;
-                const uint64_t hm = mix64(cl);
-                if ((uint32_t)(hm >> 40) % P != p) continue;
-                if (cl == DD_EMPTY) {
-                    atomicMax(&ff_val, (unsigned long long)v);
-                    continue;
-                }
-                uint32_t s = (uint32_t)hm & smask;
-                for (;;) {
-                    const unsigned long long prev = atomicCAS(&t_cls[s], DD_EMPTY, (unsigned long long)cl);
-                    if (prev == DD_EMPTY || prev == cl) {
-                        atomicMax(&t_val[s], (unsigned long long)v);
-                        break;
-                    }
-                    s = (s + 1) & smask;
-                }
+#pragma unroll
+            for (int u = 0; u < DD_U; u++) {
+                const uint32_t i = u * 64 + lane;
+                kk[u] = i < c ? dd_class(mode, hh[u], key_rec, key_node) : DdKey{0, 0, false};
             }
+            __syncthreads();  // table cleared
+#pragma unroll
+            for (int u = 0; u < DD_U; u++)
+                if (kk[u].dd) T.insert(kk[u]);
             __syncthreads();
-            for (uint32_t i0 = 0; i0 < c; i0 += 64) {
-                const uint32_t i = i0 + lane;
-                bool keep = false;
-                uint32_t h = 0;
-                if (i < c) {
-                    h = keys[o + i];
-                    uint64_t cl, v;
-                    if (!dd_class(mode, h, key_rec, key_node, &cl, &v)) {
-                        keep = p == 0;  // never deduplicated: emitted once, in the first pass
-                    } else {
-                        const uint64_t hm = mix64(cl);
-                        if ((uint32_t)(hm >> 40) % P == p) {
-                            if (cl == DD_EMPTY) {
-                                keep = ff_val == v;
-                            } else {
-                                uint32_t s = (uint32_t)hm & smask;
-                                while (t_cls[s] != cl) s = (s + 1) & smask;
-                                keep = t_val[s] == v;
-                            }
-                        }
-                    }
-                }
+#pragma unroll
+            for (int u = 0; u < DD_U; u++) {
+                if (u * 64u >= c) break;  // wave-uniform
+                const uint32_t i = u * 64 + lane;
+                const bool keep = i < c && (!kk[u].dd || T.winner(kk[u]));
                 const uint64_t m = __ballot(keep);
-                if (keep) ukeys[o + base + __popcll(m & ((1ull << lane) - 1))] = h;
+                if (keep) ukeys[o + base + __popcll(m & ((1ull << lane) - 1))] = hh[u];
                 base += __popcll(m);
             }
-            __syncthreads();
+            __syncthreads();  // the table is cleared again for the next topic
+        } else {
+            const uint32_t P = (c + DD_PASS - 1) / DD_PASS;
+            for (uint32_t p = 0; p < P; p++) {
+                if (p) {
+                    for (uint32_t j = lane; j < S; j += 64) {
+                        t_cls[j] = DD_EMPTY;
+                        t_val[j] = 0;
+                    }
+                    if (lane == 0) ff_val = 0;
+                }
+                __syncthreads();
+                for (uint32_t i = lane; i < c; i += 64) {
+                    const DdKey k = dd_class(mode, keys[o + i], key_rec, key_node);
+                    if (k.dd && (uint32_t)(mix64(k.cls) >> 40) % P == p) T.insert(k);
+                }
+                __syncthreads();
+                for (uint32_t i0 = 0; i0 < c; i0 += 64) {
+                    const uint32_t i = i0 + lane;
+                    bool keep = false;
+                    uint32_t h = 0;
+                    if (i < c) {
+                        h = keys[o + i];
+                        const DdKey k = dd_class(mode, h, key_rec, key_node);
+                        if (!k.dd) keep = p == 0;  // never deduplicated: emitted once, in the first pass
+                        else keep = (uint32_t)(mix64(k.cls) >> 40) % P == p && T.winner(k);
+                    }
+                    const uint64_t m = __ballot(keep);
+                    if (keep) ukeys[o + base + __popcll(m & ((1ull << lane) - 1))] = h;
+                    base += __popcll(m);
+                }
+                __syncthreads();
+            }
         }
         if (lane == 0) ucnt[t] = base;
     }
