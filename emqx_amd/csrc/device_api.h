@@ -101,13 +101,18 @@ hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const
 hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,
                                uint32_t *roff, uint32_t *tot, uint32_t *scratch, uint32_t *off, uint64_t *out,
                                uint64_t cap, hipStream_t stream);
-// Per-topic reducers over a TM_MATCH_ALL result (result_kernels.hip k_dedupe): topic t's
-// reduced keys go to ukeys[off[t] ..), their number to ucnt[t].  key_rec: 2 u64 per key
-// handle {id, order code}; key_node: u32 per handle (device slot of the key's node).
+// Per-topic reducers over a TM_MATCH_ALL result (result_kernels.hip k_dd_pass + k_dedupe),
+// in place: topic t's reduced keys overwrite keys[off[t] ..), their number goes to
+// ucnt[t].  key_rec: 2 u64 per key handle {id, order code}; key_node: u32 per handle
+// (device slot of the key's node); key_dd: u8 per handle, the KDD_* flags of the keys
+// that can collapse at all.  scratch: keys_cap u32; wl: n uint2; wl_n: one u32.
 constexpr uint32_t DD_UNIQUE = 0, DD_AGGRE = 1;
-hipError_t launch_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off, const uint32_t *keys,
-                         uint64_t keys_cap, const uint64_t *key_rec, const uint32_t *key_node, uint32_t n,
-                         uint32_t *ucnt, uint32_t *ukeys, hipStream_t stream);
+constexpr uint8_t KDD_MULTI = 1;   // UNIQUE: the key's id is carried by more than one live key
+constexpr uint8_t KDD_SHARED = 2;  // AGGRE: the key's dest is a shared-subscription member
+hipError_t launch_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off, uint32_t *keys, uint64_t keys_cap,
+                         const uint64_t *key_rec, const uint32_t *key_node, const uint8_t *key_dd, uint32_t n,
+                         uint32_t *ucnt, uint32_t *scratch, uint2 *wl, uint32_t *wl_n, hipStream_t stream);
+hipError_t launch_scatter1(uint8_t *dst, const uint64_t *idx, const uint8_t *src, uint64_t n, hipStream_t stream);
 hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, hipStream_t stream);
 
 }  // namespace tmx

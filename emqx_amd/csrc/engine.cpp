@@ -47,7 +47,7 @@ inline bool is_term_kind(uint8_t k) { return k == K_EXACT_BIN || k == K_EXACT_WO
 struct KeyRec {
     uint32_t node;  // terminal node (NONE for K_DEAD)
     uint8_t kind;
-    uint8_t _p[3];
+    uint8_t _p[3];  // _p[0]: KR_MULTI once another live key carries the same id
     uint64_t id;
 };
 
@@ -158,6 +158,61 @@ struct tm_engine {
     std::vector<uint32_t> kset;  // open addressing over key handles
     uint64_t kmask = 0, kset_used = 0;
     std::map<std::pair<std::string, uint64_t>, uint32_t> dead_keys;
+
+    // ---- live keys per id.  k_dedupe's UNIQUE table only needs the keys whose id some
+    // other live key also carries (KR_MULTI, set once and kept: a stale flag only costs
+    // a table insert).  Open addressing over ids; a slot with cnt == ID_EMPTY is free.
+    struct IdUse {
+        uint64_t id;
+        uint32_t cnt;
+        uint32_t solo;  // the one live key while cnt == 1 and it is not flagged yet
+    };
+    static constexpr uint32_t ID_EMPTY = 0xFFFFFFFFu;
+    static constexpr uint8_t KR_MULTI = 1;
+    std::vector<IdUse> idtab;
+    uint64_t idtab_used = 0;
+    void id_rehash() {  // drops ids with no live key
+        std::vector<IdUse> old;
+        old.swap(idtab);
+        uint64_t live = 0;
+        for (const IdUse &e : old) live += e.cnt != ID_EMPTY && e.cnt;
+        uint64_t sz = 1024;
+        while (sz < (live + 1) * 4) sz <<= 1;
+        idtab.assign(sz, IdUse{0, ID_EMPTY, NONE});
+        idtab_used = 0;
+        for (const IdUse &e : old)
+            if (e.cnt != ID_EMPTY && e.cnt) id_use(e.id) = e;
+    }
+    IdUse &id_use(uint64_t id) {
+        if ((idtab_used + 1) * 2 > idtab.size()) id_rehash();
+        const uint64_t m = idtab.size() - 1;
+        uint64_t i = mix64(id) & m;
+        while (idtab[i].cnt != ID_EMPTY && idtab[i].id != id) i = (i + 1) & m;
+        if (idtab[i].cnt == ID_EMPTY) {
+            idtab[i] = IdUse{id, 0, NONE};
+            idtab_used++;
+        }
+        return idtab[i];
+    }
+    void id_add(uint32_t h) {
+        IdUse &e = id_use(keys[h].id);
+        if (e.cnt == 0) {
+            e.solo = h;
+        } else {
+            if (e.solo != NONE) {  // the id's first key meets a second one: flag it too
+                keys[e.solo]._p[0] |= KR_MULTI;
+                dirty_kid.push_back(e.solo);
+                e.solo = NONE;
+            }
+            keys[h]._p[0] |= KR_MULTI;
+        }
+        e.cnt++;
+    }
+    void id_del(uint32_t h) {
+        IdUse &e = id_use(keys[h].id);
+        e.cnt--;
+        e.solo = NONE;  // a key left behind was flagged when the count reached 2
+    }
     std::vector<std::string> dead_filter;  // by key handle (only K_DEAD entries non-empty)
 
     // ---- staged ops and epoch deltas
@@ -177,9 +232,11 @@ struct tm_engine {
     DevBuf d_key_rec;                 // key handle -> {caller id, order code} (2 u64; key_ord)
     DevBuf d_key_node;                // key handle -> device slot of its node (u32; AGGRE classes)
     DevBuf d_key_bin;                 // key handle -> 1 for {Binary, {ID}} keys (u32; FIRST order)
+    DevBuf d_key_dd;                  // key handle -> KDD_* flags (u8; which keys k_dedupe must table)
     std::vector<uint64_t> dirty_kid;  // handles (re)assigned since the last upload
     uint64_t n_deep = 0;              // live word-list keys too deep for the 64-bit order code
-    DevBuf d_ukeys, d_ucnt;           // reduced results (UNIQUE / AGGRE) at the full result's offsets
+    DevBuf d_ukeys, d_ucnt;           // UNIQUE / AGGRE: reducer scratch at the result's offsets; reduced counts
+    DevBuf d_dd_wl, d_dd_wl_n;        // k_dd_pass -> k_dedupe worklist
     uint64_t ukeys_cap = 0;
     uint32_t last_mode = 0;           // TM_MATCH_* of the last batch
     DevBuf d_res_scan, d_mrg_roff, d_mrg_tot;  // scratch of tm_result_ids_device / tm_merge_shards_device
@@ -482,6 +539,7 @@ struct tm_engine {
             uint32_t h = alloc_key();
             keys[h] = KeyRec{node, kind, {0, 0, 0}, op.id};
             if (key_is_deep(h)) n_deep++;
+            id_add(h);
             dirty_kid.push_back(h);
             kset[slot] = h;
             kset_used++;
@@ -506,6 +564,7 @@ struct tm_engine {
             kset_erase_slot(slot);
             deltas.push_back(Delta{node, h, (uint8_t)(kind == K_HASH), 0});
             if (key_is_deep(h)) n_deep--;
+            id_del(h);
             keys[h].kind = K_FREE;
             free_pending.push_back(h);
             n_live--;
@@ -675,40 +734,44 @@ struct tm_engine {
     }
 
     // key handle -> {id, order code}, device node slot, binary flag
-    void key_dev_rec(uint32_t h, uint64_t *rec, uint32_t *node, uint32_t *bin) const {
+    void key_dev_rec(uint32_t h, uint64_t *rec, uint32_t *node, uint32_t *bin, uint8_t *dd) const {
         const KeyRec &k = keys[h];
         rec[0] = k.id;
         (void)key_ord(h, &rec[1]);
         const bool live = k.kind != K_FREE && k.kind != K_DEAD;
         *node = live ? dev_id(k.node) : NONE;
         *bin = k.kind == K_EXACT_BIN ? 1u : 0u;
+        *dd = (uint8_t)(((k._p[0] & KR_MULTI) ? KDD_MULTI : 0) | ((k.id & TM_ID_SHARED) ? KDD_SHARED : 0));
     }
 
     hipError_t upload_key_ids_full() {
         std::vector<uint64_t> rec(keys.size() * 2);
         std::vector<uint32_t> node(keys.size()), bin(keys.size());
-        for (size_t h = 0; h < keys.size(); h++) key_dev_rec((uint32_t)h, &rec[2 * h], &node[h], &bin[h]);
+        std::vector<uint8_t> dd(keys.size());
+        for (size_t h = 0; h < keys.size(); h++) key_dev_rec((uint32_t)h, &rec[2 * h], &node[h], &bin[h], &dd[h]);
         dirty_kid.clear();
         hipError_t e = put(d_key_rec, rec);
         if (e) return e;
         if ((e = put(d_key_node, node))) return e;
         if ((e = put(d_key_bin, bin))) return e;
+        if ((e = put(d_key_dd, dd))) return e;
         return hipStreamSynchronize(stream);  // the staging vectors die at scope exit
     }
 
     hipError_t upload_key_ids_delta() {
         if (dirty_kid.empty()) return hipSuccess;
         if (keys.size() * 16 > d_key_rec.cap || keys.size() * sizeof(uint32_t) > d_key_bin.cap ||
-            keys.size() * sizeof(uint32_t) > d_key_node.cap)
+            keys.size() * sizeof(uint32_t) > d_key_node.cap || keys.size() > d_key_dd.cap)
             return upload_key_ids_full();
         std::sort(dirty_kid.begin(), dirty_kid.end());
         dirty_kid.erase(std::unique(dirty_kid.begin(), dirty_kid.end()), dirty_kid.end());
         const size_t n = dirty_kid.size();
         std::vector<uint64_t> idx(n), rec(2 * n);
         std::vector<uint32_t> node(n), bin(n);
+        std::vector<uint8_t> dd(n);
         for (size_t i = 0; i < n; i++) {
             idx[i] = dirty_kid[i];
-            key_dev_rec((uint32_t)dirty_kid[i], &rec[2 * i], &node[i], &bin[i]);
+            key_dev_rec((uint32_t)dirty_kid[i], &rec[2 * i], &node[i], &bin[i], &dd[i]);
         }
         dirty_kid.clear();
         hipError_t e;
@@ -728,6 +791,11 @@ struct tm_engine {
         if ((e = hipMemcpyAsync(d_scatter_src.p, node.data(), n * 4, hipMemcpyHostToDevice, stream))) return e;
         if ((e = launch_scatter4(d_key_node.as<uint32_t>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint32_t>(),
                                  n, stream)))
+            return e;
+        if ((e = hipStreamSynchronize(stream))) return e;
+        if ((e = hipMemcpyAsync(d_scatter_src.p, dd.data(), n, hipMemcpyHostToDevice, stream))) return e;
+        if ((e = launch_scatter1(d_key_dd.as<uint8_t>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint8_t>(), n,
+                                 stream)))
             return e;
         return hipStreamSynchronize(stream);
     }
@@ -1020,7 +1088,8 @@ void tm_destroy(tm_engine *eng) {
     if (!eng) return;
     (void)hipSetDevice(eng->cfg.device);
     if (eng->stream) (void)hipStreamSynchronize(eng->stream);
-    for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_ukeys, &eng->d_ucnt,
+    for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_dd_wl,
+                      &eng->d_dd_wl_n, &eng->d_ukeys, &eng->d_ucnt,
                       &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
@@ -1184,7 +1253,7 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
 }
 
 // UNIQUE / AGGRE on the GPU: k_dedupe reduces the full result of the batch just enqueued
-// into d_ukeys / d_ucnt (same offsets).
+// in place in d_keys, the reduced counts in d_ucnt.
 static bool reduced_mode(uint32_t mode) { return mode == TM_MATCH_UNIQUE || mode == TM_MATCH_AGGRE; }
 
 static int enqueue_reduce(tm_engine *eng, uint32_t mode, uint32_t n, hipStream_t s) {
@@ -1193,10 +1262,13 @@ static int enqueue_reduce(tm_engine *eng, uint32_t mode, uint32_t n, hipStream_t
         eng->ukeys_cap = eng->keys_cap;
     }
     TM_TRY_HIP(eng->d_ucnt.ensure((uint64_t)n * 4 + 4), TM_ENOMEM, "alloc reduced counts");
+    TM_TRY_HIP(eng->d_dd_wl.ensure((uint64_t)n * 8), TM_ENOMEM, "alloc reducer worklist");
+    TM_TRY_HIP(eng->d_dd_wl_n.ensure(4), TM_ENOMEM, "alloc reducer worklist");
     TM_TRY_HIP(launch_dedupe(mode == TM_MATCH_UNIQUE ? DD_UNIQUE : DD_AGGRE, eng->d_outcnt.as<uint32_t>(),
                              eng->d_outoff.as<uint32_t>(), eng->d_keys.as<uint32_t>(), eng->keys_cap,
-                             eng->d_key_rec.as<uint64_t>(), eng->d_key_node.as<uint32_t>(), n,
-                             eng->d_ucnt.as<uint32_t>(), eng->d_ukeys.as<uint32_t>(), s),
+                             eng->d_key_rec.as<uint64_t>(), eng->d_key_node.as<uint32_t>(),
+                             eng->d_key_dd.as<uint8_t>(), n, eng->d_ucnt.as<uint32_t>(), eng->d_ukeys.as<uint32_t>(),
+                             eng->d_dd_wl.as<uint2>(), eng->d_dd_wl_n.as<uint32_t>(), s),
                TM_EDEVICE, "dedupe");
     return TM_OK;
 }
@@ -1277,7 +1349,7 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
     TM_TRY_HIP(hipMemcpyAsync(eng->h_status.p, eng->d_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                "D2H");
     if (total)
-        TM_TRY_HIP(hipMemcpyAsync(eng->h_keys.p, (dev_reduce ? eng->d_ukeys : eng->d_keys).p, total * 4,
+        TM_TRY_HIP(hipMemcpyAsync(eng->h_keys.p, eng->d_keys.p, total * 4,
                                   hipMemcpyDeviceToHost, s),
                    TM_EDEVICE, "D2H");
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "D2H");
@@ -1404,7 +1476,7 @@ int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t 
     out->n = n;
     out->d_off = eng->d_outoff.as<uint32_t>();
     out->d_cnt = (reduced_mode(mode) ? eng->d_ucnt : eng->d_outcnt).as<uint32_t>();
-    out->d_keys = (reduced_mode(mode) ? eng->d_ukeys : eng->d_keys).as<uint32_t>();
+    out->d_keys = eng->d_keys.as<uint32_t>();  // reduced modes compact in place
     out->d_status = eng->d_status.as<int32_t>();
     out->d_total = eng->d_cursor.as<uint64_t>();
     out->keys_cap = eng->keys_cap;
@@ -1445,7 +1517,7 @@ int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint
     const bool red = reduced_mode(eng->last_mode);
     const uint32_t *cnt = (red ? eng->d_ucnt : eng->d_outcnt).as<uint32_t>();
     TM_TRY_HIP(launch_excl_scan(cnt, 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s), TM_EDEVICE, "scan");
-    TM_TRY_HIP(launch_result_ids(cnt, eng->d_outoff.as<uint32_t>(), (red ? eng->d_ukeys : eng->d_keys).as<uint32_t>(),
+    TM_TRY_HIP(launch_result_ids(cnt, eng->d_outoff.as<uint32_t>(), eng->d_keys.as<uint32_t>(),
                                  eng->d_key_rec.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, s),
                TM_EDEVICE, "result ids");
     return TM_OK;

@@ -189,8 +189,9 @@ hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, c
 }
 
 // ---------------------------------------------------------------------------
-// Per-topic reducers over a full (TM_MATCH_ALL) result, written to a second key array
-// at the same offsets (a reduced list is never longer than the full one):
+// Per-topic reducers over a full (TM_MATCH_ALL) result, IN PLACE: topic t's reduced list
+// overwrites the head of its full list (a reduced list is never longer), its length goes
+// to ucnt[t]:
 //
 //   DD_UNIQUE  matches/3 with [unique]: the walk visits keys in ascending ETS term order
 //              and match_add/2 does Acc#{ID => K} (emqx_trie_search.erl:349-351), so per
@@ -201,33 +202,101 @@ hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, c
 //              (TM_ID_SHARED) collapse per {Filter, Group}; a filter is (node slot, '#'
 //              flag) among the keys of one topic; the largest handle represents the class.
 //
-// One wave per topic (grid-stride).  A per-wave LDS hash table {class, max value}.
-//   * Lists of up to DD_REG keys (nearly all of them) take ONE pass with every key held in
-//     registers: DD_U keys per lane, their handle loads and then their 16-B record
-//     gathers all issued before the first is used, so a topic costs two dependent
-//     round trips, not two per 64 keys.
-//   * Longer lists take ceil(c / DD_PASS) passes, pass p handling the classes whose hash
-//     falls in p, so the table never runs past half full.
-// Insert = CAS on the class word, then a 64-bit LDS atomic max on the value; every lane's
-// probe loop ends on its own CAS result, so no lane waits on another.
+// Only some keys can ever collapse, and the engine flags them per handle in key_dd:
+//   KDD_MULTI   (UNIQUE) the key's id is carried by more than one live key of the index —
+//               a key whose id is its own can meet no other key of that id;
+//   KDD_SHARED  (AGGRE) the key's dest is a shared-subscription member.
+// So the reduction is two launches:
+//   k_dd_pass   one wave per 64 topics, read-only over the keys: streams the 64 lists
+//               as one sequence (DDP_U keys per lane in flight) and gathers the handles'
+//               1-byte flags.  A topic with fewer than two flagged keys is final as it
+//               stands (ucnt = cnt); the others go to a worklist with their flagged-key
+//               count.
+//   k_dedupe    one wave per worklist topic: a per-wave LDS hash table {class, max value}
+//               over the flagged keys only (unflagged keys are kept as they are).
+//     * up to DD_REG keys (nearly all lists): ONE pass with every key held in registers,
+//       all loads issued before the first is used;
+//     * longer lists: ceil(flagged / DD_PASS) passes, pass p handling the classes whose
+//       hash falls in p, so the table never runs past half full; every pass re-reads the
+//       list, so it is first copied to a scratch array at the same offsets.
+//     Insert = CAS on the class word, then a 64-bit LDS atomic max on the value; every
+//     lane's probe loop ends on its own CAS result, so no lane waits on another.
 constexpr int DD_TAB = 1024;   // slots per wave (16 KiB of LDS)
 constexpr uint32_t DD_PASS = 512;
 constexpr int DD_U = 8;        // keys per lane in the one-pass case
 constexpr uint32_t DD_REG = 64u * DD_U;
 constexpr uint64_t DD_EMPTY = ~0ull;
 constexpr uint64_t ORD_HASH_FLAG = 1ull << 63;  // key_rec ord bit 63: a '#' key (not part of the order)
+constexpr int DDP_U = 8;       // keys per lane per round in k_dd_pass
+
+__device__ __forceinline__ uint8_t dd_bit(uint32_t mode) { return mode == DD_UNIQUE ? KDD_MULTI : KDD_SHARED; }
 
 struct DdKey {
     uint64_t cls, val;
-    bool dd;  // false: never deduplicated (AGGRE plain dest)
+    bool dd;  // false: never deduplicated (kept as is)
 };
 
+// class and value of a FLAGGED key
 __device__ __forceinline__ DdKey dd_class(uint32_t mode, uint32_t h, const uint64_t *key_rec,
                                           const uint32_t *key_node) {
     const ulonglong2 r = *reinterpret_cast<const ulonglong2 *>(key_rec + 2ull * h);  // {id, ord}
     if (mode == DD_UNIQUE) return DdKey{r.x, r.y & ~ORD_HASH_FLAG, true};
-    if (!(r.x >> 63)) return DdKey{0, 0, false};  // plain node dest: always kept
+    if (!(r.x >> 63)) return DdKey{0, 0, false};  // plain node dest (a stale flag): always kept
     return DdKey{((uint64_t)key_node[h] << 32) | (((r.x >> 32) & 0x7FFFFFFFull) << 1) | (r.y >> 63), h, true};
+}
+
+__global__ __launch_bounds__(64) void k_dd_pass(uint32_t mode, const uint32_t *cnt, const uint32_t *off,
+                                                const uint32_t *keys, uint64_t keys_cap, const uint8_t *key_dd,
+                                                uint32_t n, uint32_t *ucnt, uint2 *wl, uint32_t *wl_n) {
+    __shared__ uint32_t s_start[65];  // exclusive prefix of the 64 topics' counts
+    __shared__ uint32_t s_off[64];
+    __shared__ uint32_t s_nflag[64];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t t = blockIdx.x * 64 + lane;
+    uint32_t c = 0, o = 0;
+    if (t < n) {
+        c = cnt[t];
+        o = off[t];
+        if ((uint64_t)o + c > keys_cap) c = 0;  // overflowed batch: the caller re-runs it
+    }
+    uint32_t x = c;  // inclusive scan over the wave
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    s_start[lane + 1] = x;
+    if (lane == 0) s_start[0] = 0;
+    s_off[lane] = o;
+    s_nflag[lane] = 0;
+    const uint32_t total = __shfl(x, 63);
+    __syncthreads();
+    const uint8_t bit = dd_bit(mode);
+    // the 64 topics' lists as one sequence, 64 * DDP_U keys per round; a lane's key index
+    // only grows, so its topic cursor only moves forward
+    uint32_t ti = 0;
+    for (uint32_t base = 0; base < total; base += 64 * DDP_U) {
+        uint32_t hh[DDP_U], tt[DDP_U];
+#pragma unroll
+        for (int u = 0; u < DDP_U; u++) {
+            const uint32_t j = base + u * 64 + lane;
+            hh[u] = 0;
+            tt[u] = 64;
+            if (j < total) {
+                while (s_start[ti + 1] <= j) ti++;
+                hh[u] = keys[(uint64_t)s_off[ti] + (j - s_start[ti])];
+                tt[u] = ti;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < DDP_U; u++)
+            if (tt[u] < 64 && (key_dd[hh[u]] & bit)) atomicAdd(&s_nflag[tt[u]], 1u);
+    }
+    __syncthreads();
+    if (t < n) {
+        const uint32_t nf = s_nflag[lane];
+        if (nf >= 2) wl[atomicAdd(wl_n, 1u)] = make_uint2(t, nf);
+        else ucnt[t] = c;
+    }
 }
 
 struct DdTable {
@@ -257,26 +326,22 @@ struct DdTable {
 };
 
 __global__ __launch_bounds__(64) void k_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off,
-                                               const uint32_t *keys, uint64_t keys_cap, const uint64_t *key_rec,
-                                               const uint32_t *key_node, uint32_t n, uint32_t *ucnt,
-                                               uint32_t *ukeys) {
+                                               uint32_t *keys, const uint64_t *key_rec, const uint32_t *key_node,
+                                               const uint8_t *key_dd, const uint2 *wl, const uint32_t *wl_n,
+                                               uint32_t *ucnt, uint32_t *scratch) {
     __shared__ unsigned long long t_cls[DD_TAB];
     __shared__ unsigned long long t_val[DD_TAB];
     __shared__ unsigned long long ff_val;  // the one class equal to DD_EMPTY (UNIQUE id ~0)
     const uint32_t lane = threadIdx.x;
-    for (uint32_t t = blockIdx.x; t < n; t += gridDim.x) {
-        uint32_t c = cnt[t];
+    const uint8_t bit = dd_bit(mode);
+    const uint32_t nwl = *wl_n;
+    for (uint32_t w = blockIdx.x; w < nwl; w += gridDim.x) {
+        const uint2 job = wl[w];
+        const uint32_t t = job.x, nflag = job.y;
+        const uint32_t c = cnt[t];  // k_dd_pass listed only topics inside keys_cap
         const uint64_t o = off[t];
-        if (o + c > keys_cap) c = 0;  // overflowed batch: the caller re-runs it
-        if (c <= 1) {
-            if (lane == 0) {
-                if (c) ukeys[o] = keys[o];
-                ucnt[t] = c;
-            }
-            continue;
-        }
         uint32_t S = 64;
-        while (S < 2 * c && S < (uint32_t)DD_TAB) S <<= 1;
+        while (S < 2 * nflag && S < (uint32_t)DD_TAB) S <<= 1;
         const DdTable T{t_cls, t_val, &ff_val, S - 1};
         for (uint32_t j = lane; j < S; j += 64) {
             t_cls[j] = DD_EMPTY;
@@ -295,7 +360,8 @@ __global__ __launch_bounds__(64) void k_dedupe(uint32_t mode, const uint32_t *cn
 #pragma unroll
             for (int u = 0; u < DD_U; u++) {
                 const uint32_t i = u * 64 + lane;
-                kk[u] = i < c ? dd_class(mode, hh[u], key_rec, key_node) : DdKey{0, 0, false};
+                kk[u] = (i < c && (key_dd[hh[u]] & bit)) ? dd_class(mode, hh[u], key_rec, key_node)
+                                                         : DdKey{0, 0, false};
             }
             __syncthreads();  // table cleared
 #pragma unroll
@@ -308,12 +374,14 @@ __global__ __launch_bounds__(64) void k_dedupe(uint32_t mode, const uint32_t *cn
                 const uint32_t i = u * 64 + lane;
                 const bool keep = i < c && (!kk[u].dd || T.winner(kk[u]));
                 const uint64_t m = __ballot(keep);
-                if (keep) ukeys[o + base + __popcll(m & ((1ull << lane) - 1))] = hh[u];
+                if (keep) keys[o + base + __popcll(m & ((1ull << lane) - 1))] = hh[u];  // reads all done
                 base += __popcll(m);
             }
             __syncthreads();  // the table is cleared again for the next topic
         } else {
-            const uint32_t P = (c + DD_PASS - 1) / DD_PASS;
+            for (uint32_t i = lane; i < c; i += 64) scratch[o + i] = keys[o + i];
+            const uint32_t *src = scratch;  // the passes read the copy and compact into keys
+            const uint32_t P = (nflag + DD_PASS - 1) / DD_PASS;
             for (uint32_t p = 0; p < P; p++) {
                 if (p) {
                     for (uint32_t j = lane; j < S; j += 64) {
@@ -324,7 +392,9 @@ __global__ __launch_bounds__(64) void k_dedupe(uint32_t mode, const uint32_t *cn
                 }
                 __syncthreads();
                 for (uint32_t i = lane; i < c; i += 64) {
-                    const DdKey k = dd_class(mode, keys[o + i], key_rec, key_node);
+                    const uint32_t h = src[o + i];
+                    if (!(key_dd[h] & bit)) continue;
+                    const DdKey k = dd_class(mode, h, key_rec, key_node);
                     if (k.dd && (uint32_t)(mix64(k.cls) >> 40) % P == p) T.insert(k);
                 }
                 __syncthreads();
@@ -333,13 +403,13 @@ __global__ __launch_bounds__(64) void k_dedupe(uint32_t mode, const uint32_t *cn
                     bool keep = false;
                     uint32_t h = 0;
                     if (i < c) {
-                        h = keys[o + i];
-                        const DdKey k = dd_class(mode, h, key_rec, key_node);
+                        h = src[o + i];
+                        const DdKey k = (key_dd[h] & bit) ? dd_class(mode, h, key_rec, key_node) : DdKey{0, 0, false};
                         if (!k.dd) keep = p == 0;  // never deduplicated: emitted once, in the first pass
                         else keep = (uint32_t)(mix64(k.cls) >> 40) % P == p && T.winner(k);
                     }
                     const uint64_t m = __ballot(keep);
-                    if (keep) ukeys[o + base + __popcll(m & ((1ull << lane) - 1))] = h;
+                    if (keep) keys[o + base + __popcll(m & ((1ull << lane) - 1))] = h;
                     base += __popcll(m);
                 }
                 __syncthreads();
@@ -349,16 +419,31 @@ __global__ __launch_bounds__(64) void k_dedupe(uint32_t mode, const uint32_t *cn
     }
 }
 
-hipError_t launch_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off, const uint32_t *keys,
-                         uint64_t keys_cap, const uint64_t *key_rec, const uint32_t *key_node, uint32_t n,
-                         uint32_t *ucnt, uint32_t *ukeys, hipStream_t s) {
+hipError_t launch_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off, uint32_t *keys, uint64_t keys_cap,
+                         const uint64_t *key_rec, const uint32_t *key_node, const uint8_t *key_dd, uint32_t n,
+                         uint32_t *ucnt, uint32_t *scratch, uint2 *wl, uint32_t *wl_n, hipStream_t s) {
     if (!n) return hipSuccess;
-    const uint32_t grid = n < 65536u ? n : 65536u;
-    k_dedupe<<<grid, 64, 0, s>>>(mode, cnt, off, keys, keys_cap, key_rec, key_node, n, ucnt, ukeys);
+    hipError_t e = hipMemsetAsync(wl_n, 0, 4, s);
+    if (e) return e;
+    k_dd_pass<<<(n + 63) / 64, 64, 0, s>>>(mode, cnt, off, keys, keys_cap, key_dd, n, ucnt, wl, wl_n);
+    if ((e = hipGetLastError())) return e;
+    const uint32_t grid = n < 4096u ? n : 4096u;
+    k_dedupe<<<grid, 64, 0, s>>>(mode, cnt, off, keys, key_rec, key_node, key_dd, wl, wl_n, ucnt, scratch);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
+__global__ void k_scatter1(uint8_t *dst, const uint64_t *idx, const uint8_t *src, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[idx[i]] = src[i];
+}
+
+hipError_t launch_scatter1(uint8_t *dst, const uint64_t *idx, const uint8_t *src, uint64_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    k_scatter1<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
+    return hipGetLastError();
+}
+
 __global__ void k_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) dst[idx[i]] = src[i];

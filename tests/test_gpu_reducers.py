@@ -142,6 +142,44 @@ def test_unique_id_all_ones_and_zero():
     _unique_case(keys, t_bytes, t_off)
 
 
+def test_unique_churn_id_multiplicity():
+    """Only keys whose id another live key shares enter k_dedupe's table (KR_MULTI).  Ids
+    go 1 -> 2 -> 1 -> 2 keys over epochs, the first key of an id is flagged when a second
+    arrives, and a flagged key keeps its flag after the other one leaves; every epoch's
+    UNIQUE winners equal the oracle walk's over the live keys."""
+    rng = np.random.default_rng(11)
+    pool = [b"a/#", b"a/+", b"+/b", b"#", b"a/b", b"+/+", b"a/b/#", b"+/#", b"x/#", b"a/+/#"]
+    topics = [b"a/b", b"a", b"a/c", b"x/b", b"a/b/c", b"q/b"]
+    t_bytes, t_off = N.pack_topics(topics)
+    eng = N.Engine(0)
+    live = set()
+    for epoch in range(12):
+        ops = []
+        for _ in range(6):
+            k = (pool[int(rng.integers(0, len(pool)))], int(rng.integers(0, 4)), 0)
+            if k in live:
+                live.discard(k)
+                ops.append((N.TM_OP_DEL, k[0], k[1]))
+            else:
+                live.add(k)
+                ops.append((N.TM_OP_ADD, k[0], k[1]))
+        eng.apply(ops)
+        eng.commit()
+        keys = sorted(live)
+        if not keys:
+            continue
+        ix = oracle.OrderedIndex.from_filters([k[0] for k in keys], ids=[k[1] for k in keys],
+                                              word_form=[0] * len(keys))
+        walks, st = _walks(ix, t_bytes, t_off)
+        look = _engine_key_index(eng, keys)
+        off, cnt, hk, est = eng.match_packed(t_bytes, t_off, N.TM_MATCH_UNIQUE)
+        assert np.array_equal(est, st)
+        for t in range(len(topics)):
+            got = sorted(look(h) for h in hk[off[t]:off[t] + cnt[t]])
+            assert got == _unique_reference(walks[t], [k[1] for k in keys]), (epoch, topics[t])
+    eng.close()
+
+
 def test_unique_deep_filters_reduce_on_host():
     """Shapes deeper than the device order code (31 levels) are counted; tm_match_batch
     then reduces on the host and the device form refuses (TM_ESTATE)."""
