@@ -87,6 +87,37 @@ def profiled_traffic(workload_keys, batch, any_config=False):
     return best
 
 
+def batcher_load(eng, tb, to32, seconds):
+    """End to end through the batching aggregator (include/emqx_tm_batcher.h): P concurrent
+    publishers, each with one publish in flight (tools/loadgen.cpp), each publish answered
+    with its own route ids on the host.  Not the metric: the per-publish latency a broker
+    process would see, and the rate once the ids leave the GPU."""
+    import ctypes as C
+
+    from emqx_amd import _native as N
+    lg = C.CDLL(os.path.join(ROOT, "tools", "libtm_loadgen.so"))
+    lg.loadgen_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double,
+                               C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                               C.POINTER(C.c_double)]
+    runs = []
+    for pubs in (4096, 65536):
+        b = N.Batcher(eng, max_batch=65536, max_wait_us=200)
+        got, ids, errs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
+        rc = lg.loadgen_run(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, seconds, C.byref(got),
+                            C.byref(ids), C.byref(errs), C.byref(el))
+        st = b.stats()
+        b.close()
+        if rc != 0 or errs.value:
+            raise RuntimeError(f"batcher load failed: rc {rc}, {errs.value} failed publishes")
+        runs.append({"publishers": pubs, "publishes_per_s": round(got.value / el.value, 1),
+                     "ids_per_s": round(ids.value / el.value, 1),
+                     "mean_batch": round(st["publishes"] / max(st["batches"], 1), 1),
+                     "lat_p50_ms": round(st["lat_p50_us"] / 1e3, 3), "lat_p99_ms": round(st["lat_p99_us"] / 1e3, 3),
+                     "backend_frac": round(st["backend_us"] * 1e-6 / el.value, 3)})
+    return {"api": "tm_batcher_submit (max_batch 65536, max_wait 200 us)", "runs": runs,
+            "note": "closed loop: each publisher resubmits from its result callback; ids copied to host per batch"}
+
+
 def gather_roof(walk, kernel_ms):
     """The walk's second ceiling: independent random 16-B requests (edge + word probes).
     tools/gather_roof.hip measured what one MI355X serves with nothing dependent between
@@ -152,6 +183,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work (s)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--batcher-seconds", type=float, default=2.0,
+                    help="closed-loop load per publisher count through the batching aggregator (0: skip)")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no CPU baseline)")
     ap.add_argument("--mode", choices=("replicated", "sharded"), default="replicated",
                     help="replicated trie, publishes data-parallel (default); or filters hash-sharded over "
@@ -274,6 +307,7 @@ def main():
     # (not the metric: the batching window's trade-off); rank 0 only
     lat_sweep = []
     host_path = None
+    batcher = None
     mode_rates = {}
     if rank == 0 and not args.profile:
         for bs in (1024, 16384, 131072):
@@ -316,6 +350,7 @@ def main():
         host_path = {"api": "tm_match_batch", "batch": n, "ms_per_batch": round(dt * 1e3, 3),
                      "publishes_per_s": round(n / dt, 1),
                      "note": "host topic bytes in, host key lists out; bounded by PCIe D2H of the keys"}
+        batcher = batcher_load(eng, tb, to32, args.batcher_seconds) if args.batcher_seconds > 0 else None
 
     # ---------------------------------------------------------------- CPU baseline + parity sample
     cpu = None
@@ -369,6 +404,7 @@ def main():
             "gather": gather_roof(walk, kernel_ms),
             "latency_vs_batch": lat_sweep,
             "host_path": host_path,
+            "batcher": batcher,
             "other_modes": mode_rates,
             "cpu_baseline": cpu,
             "parity": parity,

@@ -57,6 +57,11 @@ EXPORTS = (
     "tm_reserve_matches", "tm_key_info", "tm_key_ids", "tm_stats", "tm_debug_stats", "tm_debug_timing",
     "tm_result_ids_device", "tm_merge_shards_device", "tm_merge_shards", "tm_match_device_mode",
 )
+# every symbol include/emqx_tm_batcher.h declares
+BATCHER_EXPORTS = (
+    "tm_batcher_create", "tm_batcher_create_fn", "tm_batcher_destroy", "tm_batcher_submit", "tm_batcher_match",
+    "tm_batcher_apply", "tm_batcher_commit", "tm_batcher_stats_get",
+)
 
 
 class tm_config(C.Structure):
@@ -99,6 +104,25 @@ class tm_stats_t(C.Structure):
         "device_bytes", "n_full_rebuilds", "n_delta_commits", "n_slow_topics",
         "commit_apply_us", "commit_lists_us", "commit_upload_us", "n_deep_keys")]
 
+
+class tm_batcher_config(C.Structure):
+    _fields_ = [("max_batch", C.c_uint32), ("max_wait_us", C.c_uint32), ("mode", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+class tm_batch_view(C.Structure):
+    _fields_ = [("off", C.c_void_p), ("cnt", C.c_void_p), ("ids", C.c_void_p), ("status", C.c_void_p)]
+
+
+class tm_batcher_stats(C.Structure):
+    _fields_ = [("batches", C.c_uint64), ("publishes", C.c_uint64), ("max_batch_seen", C.c_uint64),
+                ("backend_us", C.c_uint64), ("lat_p50_us", C.c_double), ("lat_p99_us", C.c_double),
+                ("lat_max_us", C.c_double)]
+
+
+tm_match_cb = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.POINTER(C.c_uint64), C.c_uint32)
+tm_batch_fn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32, C.c_uint32,
+                          C.POINTER(tm_batch_view))
 
 _lib = None
 
@@ -144,6 +168,19 @@ def load() -> C.CDLL:
                                     C.c_void_p, C.c_uint64]
     for name in EXPORTS:
         if name not in ("tm_destroy", "tm_last_error", "tm_abi_version"):
+            getattr(lib, name).restype = C.c_int
+    lib.tm_batcher_create.argtypes = [C.c_void_p, P(tm_batcher_config), P(C.c_void_p)]
+    lib.tm_batcher_create_fn.argtypes = [tm_batch_fn, C.c_void_p, P(tm_batcher_config), P(C.c_void_p)]
+    lib.tm_batcher_destroy.argtypes = [C.c_void_p]
+    lib.tm_batcher_destroy.restype = None
+    lib.tm_batcher_submit.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, tm_match_cb, C.c_void_p]
+    lib.tm_batcher_match.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, P(C.c_uint32),
+                                     P(C.c_int32)]
+    lib.tm_batcher_apply.argtypes = [C.c_void_p, P(tm_op), C.c_size_t]
+    lib.tm_batcher_commit.argtypes = [C.c_void_p, P(C.c_uint64)]
+    lib.tm_batcher_stats_get.argtypes = [C.c_void_p, P(tm_batcher_stats)]
+    for name in BATCHER_EXPORTS:
+        if name != "tm_batcher_destroy":
             getattr(lib, name).restype = C.c_int
     _lib = lib
     return lib
@@ -364,3 +401,106 @@ class Engine:
 
     def reserve_matches(self, keys_cap: int, topics: int = 0):
         self._check(self.lib.tm_reserve_matches(self.h, keys_cap, topics))
+
+
+class Batcher:
+    """The publish batching aggregator (include/emqx_tm_batcher.h): single publishes in,
+    one engine batch per window, each publisher's own id list back.
+
+    Over an Engine, or over `backend(topics: list[bytes], mode) -> (lists, statuses)` (a
+    Python batch matcher; the C-ABI's tm_batcher_create_fn)."""
+
+    def __init__(self, engine: "Engine | None" = None, *, backend=None, max_batch: int = 0, max_wait_us: int = 0,
+                 mode: int = TM_MATCH_ALL):
+        self.lib = load()
+        cfg = tm_batcher_config(max_batch, max_wait_us, mode, 0)
+        h = C.c_void_p()
+        self._keep = []
+        if engine is not None:
+            rc = self.lib.tm_batcher_create(engine.h, C.byref(cfg), C.byref(h))
+        else:
+            fn = tm_batch_fn(self._py_backend(backend))
+            self._keep.append(fn)
+            rc = self.lib.tm_batcher_create_fn(fn, None, C.byref(cfg), C.byref(h))
+        if rc != TM_OK:
+            raise TMError(rc, "tm_batcher_create failed")
+        self.h = h
+        self.engine = engine
+        self.mode = mode
+
+    def _py_backend(self, backend):
+        hold = []  # the last two batches' arrays: a view lives until the second-next call
+
+        def run(_be, bytes_p, off_p, n, mode, view):
+            try:
+                off = np.ctypeslib.as_array(off_p, shape=(n + 1,)).copy()
+                raw = C.string_at(bytes_p, int(off[n])) if n and off[n] else b""
+                topics = [raw[off[i]:off[i + 1]] for i in range(n)]
+                lists, status = backend(topics, mode)
+                cnt = np.array([len(x) for x in lists], dtype=np.uint32)
+                o = np.zeros(n + 1, dtype=np.uint32)
+                np.cumsum(cnt, out=o[1:])
+                ids = np.array([i for x in lists for i in x] or [0], dtype=np.uint64)
+                st = np.asarray(status, dtype=np.int32)
+                hold.append((o, cnt, ids, st))
+                del hold[:-2]
+                view.contents.off, view.contents.cnt = o.ctypes.data, cnt.ctypes.data
+                view.contents.ids = ids.ctypes.data if mode != TM_MATCH_COUNT else None
+                view.contents.status = st.ctypes.data
+                return TM_OK
+            except Exception:  # a failed backend fails its batch, as a device error would
+                return TM_EDEVICE
+        return run
+
+    def match(self, topic, cap: int = 1 << 16):
+        """Blocking: (status, [ids]) for one publish (waits for its window); in COUNT mode
+        (status, count)."""
+        tb = topic.encode() if isinstance(topic, str) else bytes(topic)
+        ids = np.zeros(max(cap, 1), dtype=np.uint64)
+        n = C.c_uint32()
+        st = C.c_int32()
+        rc = self.lib.tm_batcher_match(self.h, tb, len(tb), ids.ctypes.data, cap, C.byref(n), C.byref(st))
+        if rc < 0 and st.value >= 0:
+            raise TMError(rc, "tm_batcher_match failed")
+        if self.mode == TM_MATCH_COUNT and st.value >= 0:
+            return st.value, n.value
+        return st.value, ids[:min(n.value, cap)].tolist()
+
+    def apply(self, ops):
+        ops = list(ops)
+        arr = (tm_op * len(ops))()
+        keep = []
+        for i, o in enumerate(ops):
+            fb = o[1].encode() if isinstance(o[1], str) else bytes(o[1])
+            cb = C.create_string_buffer(fb, len(fb) + 1)
+            keep.append(cb)
+            arr[i].op, arr[i].flags = o[0], (o[3] if len(o) > 3 else 0)
+            arr[i].filter, arr[i].filter_len, arr[i].id = C.cast(cb, C.c_void_p), len(fb), o[2]
+        rc = self.lib.tm_batcher_apply(self.h, arr, len(ops))
+        if rc != TM_OK:
+            raise TMError(rc, "tm_batcher_apply failed")
+
+    def commit(self) -> int:
+        ep = C.c_uint64()
+        rc = self.lib.tm_batcher_commit(self.h, C.byref(ep))
+        if rc != TM_OK:
+            raise TMError(rc, "tm_batcher_commit failed")
+        return ep.value
+
+    def stats(self) -> dict:
+        st = tm_batcher_stats()
+        rc = self.lib.tm_batcher_stats_get(self.h, C.byref(st))
+        if rc != TM_OK:
+            raise TMError(rc, "tm_batcher_stats_get failed")
+        return {k: getattr(st, k) for k, _ in tm_batcher_stats._fields_}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.tm_batcher_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -21,12 +21,13 @@ def _newer(out, srcs):
 
 def build(force: bool = False, verbose: bool = True):
     tm = os.path.join(HERE, "libemqx_tm.so")
-    srcs = [os.path.join(CSRC, f) for f in ("engine.cpp", "match_kernels.hip", "result_kernels.hip", "layout.h",
-                                            "device_api.h")]
-    srcs.append(os.path.join(os.path.dirname(HERE), "include", "emqx_tm.h"))
+    srcs = [os.path.join(CSRC, f) for f in ("engine.cpp", "batcher.cpp", "match_kernels.hip",
+                                            "result_kernels.hip", "layout.h", "device_api.h")]
+    srcs += [os.path.join(os.path.dirname(HERE), "include", h) for h in ("emqx_tm.h", "emqx_tm_batcher.h")]
     if force or not _newer(tm, srcs):
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-               "-Wno-unused-function", os.path.join(CSRC, "engine.cpp"), os.path.join(CSRC, "match_kernels.hip"),
+               "-Wno-unused-function", os.path.join(CSRC, "engine.cpp"), os.path.join(CSRC, "batcher.cpp"),
+               os.path.join(CSRC, "match_kernels.hip"),
                os.path.join(CSRC, "result_kernels.hip"), "-o", tm]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
@@ -35,6 +36,15 @@ def build(force: bool = False, verbose: bool = True):
     ssrc = [os.path.join(CSRC, "synth.cpp")]
     if force or not _newer(syn, ssrc):
         cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", ssrc[0], "-o", syn]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+    # bench tooling (not product code): closed-loop publisher load for the batching aggregator
+    lg = os.path.join(os.path.dirname(HERE), "tools", "libtm_loadgen.so")
+    lsrc = [os.path.join(os.path.dirname(HERE), "tools", "loadgen.cpp"),
+            os.path.join(os.path.dirname(HERE), "include", "emqx_tm_batcher.h")]
+    if force or not _newer(lg, lsrc):
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", lsrc[0], "-o", lg, tm, "-Wl,-rpath,$ORIGIN/../emqx_amd"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)

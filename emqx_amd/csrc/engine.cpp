@@ -1108,6 +1108,9 @@ void tm_destroy(tm_engine *eng) {
     delete eng;
 }
 
+// library-internal (batcher.cpp), not part of the C-ABI
+__attribute__((visibility("hidden"))) int tmx_engine_device(const tm_engine *eng) { return eng->cfg.device; }
+
 const char *tm_last_error(const tm_engine *eng) { return eng ? eng->err.c_str() : "null engine"; }
 
 int tm_apply(tm_engine *eng, const tm_op *ops, size_t n) {

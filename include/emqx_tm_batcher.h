@@ -1,0 +1,99 @@
+/* emqx_tm_batcher.h — publish batching aggregator over the topic-matching engine.
+ *
+ * The reference matches one publish per call: every emqx_broker:do_publish/1
+ * (apps/emqx/src/emqx_broker.erl:285-290) runs emqx_router:match_routes/1
+ * (apps/emqx/src/emqx_router.erl:205-212) synchronously in the publishing process.  A GPU
+ * wants one call per WINDOW of publishes, so this aggregator sits between the many
+ * concurrent publishers and tm_match_*: publishers submit single topics, a worker thread
+ * cuts the queue into batches, runs one engine batch per window and hands each publisher
+ * its own id list (SURVEY.md §8 (b) "Who calls it", §8 (f) f3).
+ *
+ *   window   a batch is dispatched when max_batch publishes are queued, or when the
+ *            oldest queued publish has waited max_wait_us, or at tm_batcher_destroy
+ *            (which drains the queue).  While a batch runs on the GPU the next one keeps
+ *            filling, so under load batches grow by themselves.
+ *   result   per publish: TM_TOPIC_OK with the ids of its matched keys (route dests,
+ *            emqx_topic_index:get_id/1 of every key, emqx_topic_index.erl:87-89), or
+ *            TM_BADARG with no ids (a level exactly "+" or "#": emqx_trie_search.erl:374-375),
+ *            or a negative TM_E* status when the batch failed as a whole.  COUNT mode
+ *            gives the count and no ids.
+ *   writes   tm_batcher_apply / tm_batcher_commit serialise with the worker, so an epoch
+ *            swaps only between batches: every batch sees exactly one committed epoch.
+ *
+ * Erlang binding: a NIF calls tm_batcher_submit with a callback that
+ * enif_send()s the id list to the publishing pid, which waits in `receive`; the callback
+ * runs on the worker thread and must not block.
+ */
+#ifndef EMQX_TM_BATCHER_H
+#define EMQX_TM_BATCHER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "emqx_tm.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tm_batcher tm_batcher;
+
+typedef struct tm_batcher_config {
+    uint32_t max_batch;    /* publishes per engine batch (0 = 65536)              */
+    uint32_t max_wait_us;  /* window bound from the oldest queued publish (0 = 200) */
+    uint32_t mode;         /* TM_MATCH_ALL / UNIQUE / AGGRE / FIRST / COUNT        */
+    uint32_t reserved;
+} tm_batcher_config;
+
+/* One publish's result; `ids` is valid only during the call. */
+typedef void (*tm_match_cb)(void *ctx, int32_t status, const uint64_t *ids, uint32_t n);
+
+/* A batch matcher other than an engine (e.g. a filter-sharded index): match topics
+ * bytes[off[i] .. off[i+1]) for i < n and fill `out` with memory the backend owns until
+ * its next call.  Topic i's ids are ids[out->off[i] .. out->off[i] + out->cnt[i]).
+ * Calls are never concurrent. */
+typedef struct tm_batch_view {
+    const uint32_t *off;
+    const uint32_t *cnt;
+    const uint64_t *ids;     /* NULL in COUNT mode */
+    const int32_t  *status;
+} tm_batch_view;
+typedef int (*tm_batch_fn)(void *backend, const uint8_t *bytes, const uint32_t *off, uint32_t n,
+                           uint32_t mode, tm_batch_view *out);
+
+typedef struct tm_batcher_stats {
+    uint64_t batches;
+    uint64_t publishes;
+    uint64_t max_batch_seen;
+    uint64_t backend_us;        /* wall time inside the engine / backend, summed  */
+    /* submit -> callback latency over the last (up to) 65536 publishes, microseconds */
+    double   lat_p50_us, lat_p99_us, lat_max_us;
+} tm_batcher_stats;
+
+/* Over an engine: batches go through tm_match_device_mode on the engine's device and the
+ * ids come back topic-major (tm_result_ids_device); UNIQUE over filters deeper than the
+ * device order code goes through tm_match_batch.  The engine must outlive the batcher and
+ * receive its writes through tm_batcher_apply / tm_batcher_commit while the batcher runs. */
+int  tm_batcher_create(tm_engine *eng, const tm_batcher_config *cfg, tm_batcher **out);
+int  tm_batcher_create_fn(tm_batch_fn fn, void *backend, const tm_batcher_config *cfg, tm_batcher **out);
+/* Drains the queue (every submitted publish gets its callback), then stops the worker. */
+void tm_batcher_destroy(tm_batcher *b);
+
+/* Queue one publish (topic bytes are copied).  TM_ESTATE once destroy has begun. */
+int tm_batcher_submit(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_match_cb cb, void *ctx);
+/* Blocking form: waits for the publish's batch.  Copies up to `cap` ids, *n_out = the
+ * full count (> cap means truncated), *status = the publish's status. */
+int tm_batcher_match(tm_batcher *b, const uint8_t *topic, uint32_t len, uint64_t *ids, uint32_t cap,
+                     uint32_t *n_out, int32_t *status);
+
+/* Engine writes, serialised with the worker (engine batchers only: TM_ESTATE otherwise). */
+int tm_batcher_apply(tm_batcher *b, const tm_op *ops, size_t n);
+int tm_batcher_commit(tm_batcher *b, uint64_t *epoch_out);
+
+int tm_batcher_stats_get(tm_batcher *b, tm_batcher_stats *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EMQX_TM_BATCHER_H */

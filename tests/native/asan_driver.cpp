@@ -7,7 +7,11 @@
 // adds/deletes (incl. invalid and $-filters, word-list keys, re-adds inside one epoch),
 // matches in every mode, key introspection, result shaping and the shard merge, and
 // checks the modes against each other: COUNT == |ALL|, FIRST in ALL, UNIQUE subset of ALL.
+// Then the batching aggregator (include/emqx_tm_batcher.h): 8 publisher threads with
+// blocking publishes while the main thread commits epochs through the batcher.
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -17,6 +21,7 @@
 #include <vector>
 
 #include "../../include/emqx_tm.h"
+#include "../../include/emqx_tm_batcher.h"
 
 #define CHECK(c)                                                           \
     do {                                                                   \
@@ -176,6 +181,72 @@ int main() {
         std::vector<uint64_t> outids(64);
         CHECK(tm_merge_shards(G, n, counts, ids.data(), 16, outoff, outids.data(), outids.size()) == TM_OK);
         CHECK(tm_merge_shards(G, n, counts, ids.data(), 16, outoff, outids.data(), 1) == TM_ENOMEM);
+    }
+    // batching aggregator: publishers race a commit that only ADDS keys under id 1<<40, so
+    // every publish must return at least its ids from the epoch before (tm_match_batch) and
+    // nothing outside the epoch after
+    {
+        std::vector<std::string> topics;
+        for (int i = 0; i < 64; i++) topics.push_back(rand_topic(r));
+        std::vector<uint8_t> tb;
+        std::vector<uint32_t> to{0};
+        for (auto &t : topics) {
+            tb.insert(tb.end(), t.begin(), t.end());
+            to.push_back((uint32_t)tb.size());
+        }
+        auto ids_of = [&](std::vector<std::multiset<uint64_t>> &out) {
+            tm_result res;
+            CHECK(tm_match_batch(eng, tb.data(), to.data(), (uint32_t)topics.size(), TM_MATCH_ALL, &res) == TM_OK);
+            out.assign(topics.size(), {});
+            for (size_t i = 0; i < topics.size(); i++) {
+                std::vector<uint64_t> v(res.cnt[i] + 1);
+                CHECK(tm_key_ids(eng, res.keys + res.off[i], res.cnt[i], v.data()) == TM_OK);
+                out[i].insert(v.begin(), v.begin() + res.cnt[i]);
+            }
+        };
+        std::vector<std::multiset<uint64_t>> before, after;
+        ids_of(before);
+        tm_batcher_config bc{16, 300, TM_MATCH_ALL, 0};
+        tm_batcher *b = nullptr;
+        CHECK(tm_batcher_create(eng, &bc, &b) == TM_OK);
+        std::atomic<int> bad{0};
+        std::vector<std::thread> th;
+        for (int p = 0; p < 8; p++)
+            th.emplace_back([&, p] {
+                uint64_t ids[4096];
+                for (int it = 0; it < 200; it++) {
+                    const size_t i = (p * 131 + it * 7) % topics.size();
+                    uint32_t n = 0;
+                    int32_t st = 0;
+                    if (tm_batcher_match(b, (const uint8_t *)topics[i].data(), (uint32_t)topics[i].size(), ids, 4096,
+                                         &n, &st) != TM_OK || st != TM_TOPIC_OK || n > 4096) {
+                        bad++;
+                        continue;
+                    }
+                    std::multiset<uint64_t> got(ids, ids + n), old;
+                    for (uint64_t x : got)
+                        if (x < (1ull << 40)) old.insert(x);
+                    if (old != before[i]) bad++;
+                }
+            });
+        std::vector<tm_op> add;
+        const char *nf[] = {"#", "a/#", "+/+", "a/b"};
+        for (int k = 0; k < 4; k++) add.push_back(tm_op{TM_OP_ADD, 0, (const uint8_t *)nf[k], (uint32_t)strlen(nf[k]), 0,
+                                                         (1ull << 40) + k});
+        CHECK(tm_batcher_apply(b, add.data(), add.size()) == TM_OK);
+        uint64_t ep2 = 0;
+        CHECK(tm_batcher_commit(b, &ep2) == TM_OK);
+        for (auto &t : th) t.join();
+        CHECK(bad.load() == 0);
+        tm_batcher_stats bs;
+        CHECK(tm_batcher_stats_get(b, &bs) == TM_OK);
+        CHECK(bs.publishes == 8 * 200 && bs.max_batch_seen <= 16 && bs.batches < bs.publishes);
+        uint32_t n = 0;
+        int32_t st = 0;
+        CHECK(tm_batcher_match(b, (const uint8_t *)"a/+", 3, nullptr, 0, &n, &st) == TM_OK && st == TM_BADARG);
+        tm_batcher_destroy(b);
+        ids_of(after);
+        for (size_t i = 0; i < topics.size(); i++) CHECK(after[i].size() >= before[i].size());
     }
     // bad arguments
     CHECK(tm_apply(eng, nullptr, 1) == TM_EINVAL);

@@ -1,0 +1,230 @@
+"""The publish batching aggregator (include/emqx_tm_batcher.h, emqx_amd/csrc/batcher.cpp).
+
+It stands between many concurrent publishers — each of which runs
+emqx_router:match_routes/1 synchronously per publish in the reference
+(apps/emqx/src/emqx_broker.erl:285-290, apps/emqx/src/emqx_router.erl:205-212) — and one
+engine batch per window.
+
+CPU tests drive the real native batcher over a Python batch matcher (tm_batcher_create_fn)
+whose answers come from the oracle's emqx_topic:match/2: windowing, draining, per-publish
+hand-back, badarg and failed batches.  The GPU tests run it over a real engine and check
+every publish's ids bit-exactly against the oracle."""
+import ctypes as C
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import oracle.emqx_topic as T
+from emqx_amd import _native as N
+
+ROUTES = [(b"a/+", 1), (b"a/#", 2), (b"#", 3), (b"+/b", 4), (b"a/b", 5), (b"$SYS/#", 6), (b"x/y/z", 7),
+          (b"+/+", 8), (b"a/b", 9)]
+
+
+def _oracle_backend(routes, calls=None):
+    def backend(topics, mode):
+        if calls is not None:
+            calls.append(len(topics))
+        lists, status = [], []
+        for t in topics:
+            if any(l in (b"+", b"#") for l in t.split(b"/")):
+                lists.append([])
+                status.append(N.TM_BADARG)
+                continue
+            ids = sorted(i for f, i in routes if T.match(t, f))
+            lists.append(ids)
+            status.append(N.TM_TOPIC_OK)
+        return lists, status
+    return backend
+
+
+def _expect(topic, routes=ROUTES):
+    return sorted(i for f, i in routes if T.match(topic, f))
+
+
+def test_header_declares_batcher_surface():
+    import os
+    import re
+    src = open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "include", "emqx_tm_batcher.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    decl = set(re.findall(r"\b(tm_batcher_[a-z_0-9]+)\s*\(", src))
+    assert decl == set(N.BATCHER_EXPORTS)
+    import subprocess
+    out = subprocess.check_output(["nm", "-D", "--defined-only", N.LIB_PATH]).decode()
+    exported = set(re.findall(r" T (tm_batcher_\w+)", out))
+    assert decl <= exported
+
+
+def test_blocking_match_one_publish():
+    b = N.Batcher(backend=_oracle_backend(ROUTES), max_wait_us=100)
+    for t in (b"a/b", b"a", b"$SYS/x", b"q/r/s", b"x/y/z", b""):
+        st, ids = b.match(t)
+        assert st == N.TM_TOPIC_OK and sorted(ids) == _expect(t), t
+    st, ids = b.match(b"a/+")
+    assert st == N.TM_BADARG and ids == []
+    assert b.stats()["publishes"] == 7
+    b.close()
+
+
+def test_concurrent_publishers_share_windows():
+    calls = []
+    b = N.Batcher(backend=_oracle_backend(ROUTES, calls), max_batch=16, max_wait_us=20000)
+    rng = np.random.default_rng(5)
+    words = [b"a", b"b", b"x", b"y", b"z", b"$SYS", b""]
+    topics = [b"/".join(words[j] for j in rng.integers(0, len(words), rng.integers(1, 4))) for _ in range(400)]
+    bad = []
+
+    def worker(k):
+        for t in topics[k::32]:
+            st, ids = b.match(t)
+            if st != N.TM_TOPIC_OK or sorted(ids) != _expect(t):
+                bad.append(t)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(32)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    s = b.stats()
+    b.close()
+    assert not bad
+    assert s["publishes"] == len(topics) == sum(calls)
+    assert max(calls) <= 16 and s["max_batch_seen"] <= 16
+    assert s["batches"] < len(topics)  # publishers really were batched together
+    assert s["lat_p99_us"] >= s["lat_p50_us"] > 0
+
+
+def test_window_closes_on_time():
+    b = N.Batcher(backend=_oracle_backend(ROUTES), max_batch=1 << 20, max_wait_us=2000)
+    t0 = time.perf_counter()
+    st, ids = b.match(b"a/b")
+    dt = time.perf_counter() - t0
+    b.close()
+    assert st == N.TM_TOPIC_OK and sorted(ids) == _expect(b"a/b")
+    assert 0.0015 <= dt < 2.0  # waited for the window, not for max_batch publishes
+
+
+def test_destroy_drains_async_submissions():
+    got = {}
+    lock = threading.Lock()
+
+    @N.tm_match_cb
+    def cb(ctx, status, ids, n):
+        with lock:
+            got[ctx] = (status, sorted(ids[i] for i in range(n)))
+
+    b = N.Batcher(backend=_oracle_backend(ROUTES), max_batch=64, max_wait_us=1_000_000)
+    topics = [b"a/b", b"a/c", b"x/y/z", b"$SYS/q", b"b"] * 40
+    for k, t in enumerate(topics):
+        assert b.lib.tm_batcher_submit(b.h, t, len(t), cb, C.c_void_p(k + 1)) == N.TM_OK
+    b.close()  # windows of 1 s: only the drain at destroy delivers them
+    assert len(got) == len(topics)
+    for k, t in enumerate(topics):
+        assert got[k + 1] == (N.TM_TOPIC_OK, _expect(t)), t
+
+
+def test_failed_batch_reaches_every_publisher():
+    def broken(topics, mode):
+        raise RuntimeError("device lost")
+    b = N.Batcher(backend=broken, max_wait_us=100)
+    st, ids = b.match(b"a/b")
+    b.close()
+    assert st == N.TM_EDEVICE and ids == []
+
+
+def test_count_mode_and_write_calls_need_an_engine():
+    b = N.Batcher(backend=_oracle_backend(ROUTES), max_wait_us=100, mode=N.TM_MATCH_COUNT)
+    assert b.match(b"a/b") == (N.TM_TOPIC_OK, len(_expect(b"a/b")))
+    with pytest.raises(N.TMError):
+        b.commit()
+    with pytest.raises(N.TMError):
+        b.apply([(N.TM_OP_ADD, b"a", 1)])
+    b.close()
+    lib = N.load()
+    assert lib.tm_batcher_submit(None, b"a", 1, N.tm_match_cb(lambda *a: None), None) == N.TM_EINVAL
+    bad = N.tm_batcher_config(0, 0, 99, 0)
+    h = C.c_void_p()
+    fn = N.tm_batch_fn(lambda *a: 0)
+    assert lib.tm_batcher_create_fn(fn, None, C.byref(bad), C.byref(h)) == N.TM_EINVAL
+
+
+# ------------------------------------------------------------------ GPU: over a real engine
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [N.TM_MATCH_ALL, N.TM_MATCH_COUNT, N.TM_MATCH_FIRST])
+def test_gpu_batcher_over_engine_vs_oracle(mode):
+    from emqx_amd import workloads
+    import oracle
+    w = workloads.generate("A", scale=0.3, n_topics=3000)
+    eng = N.Engine(0)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    eoff, eids, est = ix.match(w.t_bytes, w.t_off)
+    topics = w.topics()
+    b = N.Batcher(eng, max_batch=512, max_wait_us=500, mode=mode)
+    bad = []
+
+    def worker(k):
+        for i in range(k, len(topics), 24):
+            st, ids = b.match(topics[i])
+            exp = eids[eoff[i]:eoff[i + 1]].tolist()
+            if st != est[i]:
+                bad.append(i)
+            elif mode == N.TM_MATCH_ALL and sorted(ids) != exp:
+                bad.append(i)
+            elif mode == N.TM_MATCH_COUNT and ids != len(exp):
+                bad.append(i)
+            elif mode == N.TM_MATCH_FIRST and (len(ids) != (1 if exp else 0) or (ids and ids[0] not in exp)):
+                bad.append(i)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(24)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    s = b.stats()
+    b.close()
+    eng.close()
+    assert not bad, bad[:8]
+    assert s["publishes"] == len(topics) and s["batches"] < len(topics)
+
+
+@pytest.mark.gpu
+def test_gpu_batcher_epochs_swap_between_batches():
+    """Writes through the batcher serialise with its worker: after commit returns, every
+    later publish sees the new epoch."""
+    eng = N.Engine(0)
+    b = N.Batcher(eng, max_batch=64, max_wait_us=200)
+    b.apply([(N.TM_OP_ADD, b"a/+", 1), (N.TM_OP_ADD, b"#", 2)])
+    b.commit()
+    assert sorted(b.match(b"a/b")[1]) == [1, 2]
+    b.apply([(N.TM_OP_DEL, b"#", 2), (N.TM_OP_ADD, b"a/b", 3), (N.TM_OP_ADD, b"a/b", N.shared_id(0, 9))])
+    b.commit()
+    assert sorted(b.match(b"a/b")[1]) == sorted([1, 3, N.shared_id(0, 9)])
+    assert b.match(b"$SYS/x") == (N.TM_TOPIC_OK, [])
+    assert b.match(b"a/#")[0] == N.TM_BADARG
+    b.close()
+    eng.close()
+
+
+def test_closed_loop_loadgen_over_python_backend():
+    """tools/loadgen.cpp (bench tooling): publishers resubmit from their callbacks until the
+    deadline, then the run drains; nothing fails and publishers share windows."""
+    import os
+    lib = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools", "libtm_loadgen.so"))
+    lib.loadgen_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double,
+                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                C.POINTER(C.c_double)]
+    tb, to = N.pack_topics([b"a/b", b"x/y/z", b"a", b"$SYS/a"])
+    b = N.Batcher(backend=_oracle_backend(ROUTES), max_batch=256, max_wait_us=500)
+    got, ids, errs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
+    rc = lib.loadgen_run(b.h, tb.ctypes.data, to.ctypes.data, 4, 64, 0.3, C.byref(got), C.byref(ids), C.byref(errs),
+                         C.byref(el))
+    s = b.stats()
+    b.close()
+    assert rc == 0 and errs.value == 0 and got.value >= 64
+    assert s["publishes"] == got.value and s["batches"] < got.value
+    per = [len(_expect(t)) for t in (b"a/b", b"x/y/z", b"a", b"$SYS/a")]
+    assert ids.value <= max(per) * got.value
