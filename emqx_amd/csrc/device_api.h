@@ -13,6 +13,9 @@ constexpr int SEG_CHUNK = 128;  // key segments per global chunk (16 B each)
 constexpr int SEG_MAXCHUNK = 128;  // segment chunks one wave may flush (its list lives in HBM)
 constexpr int FR_CHUNK = 256;   // frontier entries per global overflow chunk (8 B each)
 
+// Counter block of one launch (byte offsets); the engine alternates two of them.
+constexpr uint32_t CTL_BYTES = 32, CTL_CURSOR = 0, CTL_SLOW = 8, CTL_SEG = 16, CTL_FR = 24;
+
 // Everything one match launch needs.  Device pointers only.
 struct MatchArgs {
     // topic batch: topic i is bytes[off[i] .. off[i+1])
@@ -40,6 +43,9 @@ struct MatchArgs {
     uint32_t *keys;
     uint64_t keys_cap;
     unsigned long long *cursor;  // keys requested so far (may exceed keys_cap)
+    // the counters (cursor, slow_count, seg_cursor, fr_cursor) share one CTL_BYTES block;
+    // the launch zeroes the block the next launch will use (no memsets before a batch)
+    unsigned long long *ctl_next;
     // spill path
     uint32_t *slow_list;
     uint32_t *slow_count;

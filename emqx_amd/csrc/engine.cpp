@@ -241,8 +241,14 @@ struct tm_engine {
     uint32_t last_mode = 0;           // TM_MATCH_* of the last batch
     DevBuf d_res_scan, d_mrg_roff, d_mrg_tot;  // scratch of tm_result_ids_device / tm_merge_shards_device
     // batch buffers
-    DevBuf d_bytes, d_off, d_outoff, d_outcnt, d_status, d_keys, d_cursor, d_slow_list,
-        d_slow_count, d_scr_w, d_scr_s, d_stats, d_seg_pool, d_seg_cursor, d_fr_pool, d_fr_cursor, d_wave_chunks;
+    DevBuf d_bytes, d_off, d_outoff, d_outcnt, d_status, d_keys, d_slow_list, d_scr_w, d_scr_s, d_stats,
+        d_seg_pool, d_fr_pool, d_wave_chunks;
+    // A launch's counters live in one 32-B block {cursor u64, slow_count u32 (+pad),
+    // seg_cursor u64, fr_cursor u64}.  Two blocks alternate: each launch zeroes the block
+    // the NEXT launch will use, so no memset launches precede a batch.
+    DevBuf d_ctl;
+    uint8_t *p_ctl = nullptr;  // the last launch's block
+    uint32_t ctl_cur = 0;
     uint64_t keys_cap = 0, seg_chunks = 0, fr_chunks = 0;
     PinBuf h_bytes, h_off, h_outoff, h_outcnt, h_status, h_keys, h_cursor;
     std::vector<uint32_t> pp_off, pp_cnt, pp_keys;  // post-processed results
@@ -1095,9 +1101,9 @@ void tm_destroy(tm_engine *eng) {
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
                       &eng->d_arena, &eng->d_scatter_idx,
                       &eng->d_scatter_src, &eng->d_bytes, &eng->d_off, &eng->d_outoff, &eng->d_outcnt,
-                      &eng->d_status, &eng->d_keys, &eng->d_cursor, &eng->d_slow_list, &eng->d_slow_count,
-                      &eng->d_scr_w, &eng->d_scr_s, &eng->d_stats, &eng->d_seg_pool, &eng->d_seg_cursor,
-                      &eng->d_fr_pool, &eng->d_fr_cursor, &eng->d_wave_chunks})
+                      &eng->d_status, &eng->d_keys, &eng->d_ctl, &eng->d_slow_list,
+                      &eng->d_scr_w, &eng->d_scr_s, &eng->d_stats, &eng->d_seg_pool,
+                      &eng->d_fr_pool, &eng->d_wave_chunks})
         b->release();
     for (PinBuf *b : {&eng->h_bytes, &eng->h_off, &eng->h_outoff, &eng->h_outcnt, &eng->h_status, &eng->h_keys,
                       &eng->h_cursor})
@@ -1163,12 +1169,13 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
     TM_TRY_HIP(eng->d_outcnt.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_status.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_slow_list.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_slow_count.ensure(64), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_cursor.ensure(64), TM_ENOMEM, "alloc");
+    if (!eng->d_ctl.p) {
+        TM_TRY_HIP(eng->d_ctl.ensure(2 * CTL_BYTES), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(hipMemset(eng->d_ctl.p, 0, 2 * CTL_BYTES), TM_EDEVICE, "memset");  // both blocks start at 0
+    }
     TM_TRY_HIP(eng->d_stats.ensure(128), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_scr_w.ensure((bytes + 2ull * n + 2) * 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_scr_s.ensure((bytes + 2ull * n + 2) * 8), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_seg_cursor.ensure(64), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_wave_chunks.ensure(match_grid(n, pick_tpw(n, eng->cfg.topics_per_wave)) * SEG_MAXCHUNK * 4 + 4),
                TM_ENOMEM, "alloc");
     {
@@ -1179,7 +1186,6 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
             eng->seg_chunks = want;
         }
     }
-    TM_TRY_HIP(eng->d_fr_cursor.ensure(64), TM_ENOMEM, "alloc");
     {
         // frontier overflow pool (waves whose per-depth frontier exceeds LDS)
         uint64_t want = eng->cfg.seg_chunks ? eng->cfg.seg_chunks : std::max<uint64_t>(1024, ((uint64_t)n + 63) / 64 * 4);
@@ -1237,18 +1243,21 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.status = eng->d_status.as<int32_t>();
     a.keys = eng->d_keys.as<uint32_t>();
     a.keys_cap = eng->keys_cap;
-    a.cursor = eng->d_cursor.as<unsigned long long>();
+    eng->ctl_cur ^= 1u;
+    eng->p_ctl = eng->d_ctl.as<uint8_t>() + eng->ctl_cur * CTL_BYTES;
+    a.cursor = (unsigned long long *)(eng->p_ctl + CTL_CURSOR);
+    a.ctl_next = (unsigned long long *)(eng->d_ctl.as<uint8_t>() + (eng->ctl_cur ^ 1u) * CTL_BYTES);
     a.slow_list = eng->d_slow_list.as<uint32_t>();
-    a.slow_count = eng->d_slow_count.as<uint32_t>();
+    a.slow_count = (uint32_t *)(eng->p_ctl + CTL_SLOW);
     a.scratch_w = eng->d_scr_w.as<uint32_t>();
     a.scratch_s = eng->d_scr_s.as<uint64_t>();
     a.seg_pool = eng->d_seg_pool.as<uint4>();
     a.seg_chunks = eng->seg_chunks;
-    a.seg_cursor = eng->d_seg_cursor.as<unsigned long long>();
+    a.seg_cursor = (unsigned long long *)(eng->p_ctl + CTL_SEG);
     a.wave_chunks = eng->d_wave_chunks.as<uint32_t>();
     a.fr_pool = eng->d_fr_pool.as<uint2>();
     a.fr_chunks = eng->fr_chunks;
-    a.fr_cursor = eng->d_fr_cursor.as<unsigned long long>();
+    a.fr_cursor = (unsigned long long *)(eng->p_ctl + CTL_FR);
     a.stats = eng->stats_on ? eng->d_stats.as<unsigned long long>() : nullptr;
     a.ev_fast0 = eng->timing_on ? eng->ev_fast0 : nullptr;
     a.ev_fast1 = eng->timing_on ? eng->ev_fast1 : nullptr;
@@ -1319,13 +1328,9 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
         eng->last_n = n;
         TM_TRY_HIP(enqueue_match(eng, eng->d_bytes.as<uint8_t>(), eng->d_off.as<uint32_t>(), n, s, kmode), TM_EDEVICE,
                    "kernel launch");
-        TM_TRY_HIP(hipMemcpyAsync(eng->h_cursor.p, eng->d_cursor.p, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
-        TM_TRY_HIP(hipMemcpyAsync((uint8_t *)eng->h_cursor.p + 8, eng->d_slow_count.p, 4, hipMemcpyDeviceToHost, s),
-                   TM_EDEVICE, "D2H");
-        TM_TRY_HIP(hipMemcpyAsync((uint8_t *)eng->h_cursor.p + 16, eng->d_seg_cursor.p, 8, hipMemcpyDeviceToHost, s),
-                   TM_EDEVICE, "D2H");
-        TM_TRY_HIP(hipMemcpyAsync((uint8_t *)eng->h_cursor.p + 24, eng->d_fr_cursor.p, 8, hipMemcpyDeviceToHost, s),
-                   TM_EDEVICE, "D2H");
+        // the counter block has the host layout: cursor @0, slow_count @8, seg @16, fr @24
+        TM_TRY_HIP(hipMemcpyAsync(eng->h_cursor.p, eng->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                   "D2H");
         TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "match kernels");
         uint64_t total = *eng->h_cursor.as<uint64_t>();
         eng->n_slow_last = *(uint32_t *)((uint8_t *)eng->h_cursor.p + 8);
@@ -1481,7 +1486,7 @@ int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t 
     out->d_cnt = (reduced_mode(mode) ? eng->d_ucnt : eng->d_outcnt).as<uint32_t>();
     out->d_keys = eng->d_keys.as<uint32_t>();  // reduced modes compact in place
     out->d_status = eng->d_status.as<int32_t>();
-    out->d_total = eng->d_cursor.as<uint64_t>();
+    out->d_total = (uint64_t *)(eng->p_ctl + CTL_CURSOR);
     out->keys_cap = eng->keys_cap;
     return TM_OK;
 }
@@ -1492,13 +1497,10 @@ int tm_device_sync(tm_engine *eng) {
     hipStream_t s = eng->last_stream ? eng->last_stream : eng->stream;
     TM_TRY_HIP(eng->h_cursor.ensure(64), TM_ENOMEM, "pinned alloc");
     uint8_t *h = (uint8_t *)eng->h_cursor.p;
-    if (eng->d_cursor.p) {
-        TM_TRY_HIP(hipMemcpyAsync(h + 8, eng->d_slow_count.p, 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
-        TM_TRY_HIP(hipMemcpyAsync(h + 16, eng->d_seg_cursor.p, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
-        TM_TRY_HIP(hipMemcpyAsync(h + 24, eng->d_fr_cursor.p, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
-    }
+    if (eng->p_ctl)
+        TM_TRY_HIP(hipMemcpyAsync(h, eng->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "sync");
-    if (eng->d_cursor.p) {
+    if (eng->p_ctl) {
         eng->n_slow_last = *(uint32_t *)(h + 8);
         eng->seg_demand_last = *(uint64_t *)(h + 16);
         eng->fr_demand_last = *(uint64_t *)(h + 24);
@@ -1509,7 +1511,7 @@ int tm_device_sync(tm_engine *eng) {
 
 int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out, void *stream) {
     if (!eng || !d_off_out || (ids_cap && !d_ids)) return TM_EINVAL;
-    if (!eng->d_cursor.p) {
+    if (!eng->p_ctl) {
         eng->err = "tm_result_ids_device: no tm_match_device batch yet";
         return TM_ESTATE;
     }

@@ -301,6 +301,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     // STATS build only: phase stamps (shares of wave time, not absolute kernel time)
     uint64_t ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
     if constexpr (STATS) ts0 = __builtin_amdgcn_s_memtime();
+    if (blockIdx.x == 0 && threadIdx.x < CTL_BYTES / 8) a.ctl_next[threadIdx.x] = 0ull;  // next launch's counters
 
     // ---- 0. stage the wave's topic bytes in LDS with 16-B coalesced loads
     const uint32_t t0 = blockIdx.x * a.tpw;
@@ -802,6 +803,7 @@ __global__ __launch_bounds__(WAVE) void k_match_slow(MatchArgs a) {
 // finds them last), so one is the answer only when no word-list key matches.
 __global__ __launch_bounds__(WAVE) void k_match_first(MatchArgs a) {
     const RootRec R = *a.root;
+    if (blockIdx.x == 0 && threadIdx.x < CTL_BYTES / 8) a.ctl_next[threadIdx.x] = 0ull;  // next launch's counters
     uint32_t dummy = 0;
     auto byte_at = [&](uint32_t i) -> uint8_t { return a.bytes[i]; };
     for (uint32_t t = blockIdx.x * WAVE + lane_id(); t < a.n; t += gridDim.x * WAVE) {
@@ -912,11 +914,10 @@ hipError_t launch_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *s
 
 hipError_t launch_match(const MatchArgs &a, hipStream_t s) {
     hipError_t e;
-    if ((e = hipMemsetAsync(a.cursor, 0, sizeof(unsigned long long), s))) return e;
-    if ((e = hipMemsetAsync(a.slow_count, 0, sizeof(uint32_t), s))) return e;
-    if ((e = hipMemsetAsync(a.seg_cursor, 0, sizeof(unsigned long long), s))) return e;
-    if ((e = hipMemsetAsync(a.fr_cursor, 0, sizeof(unsigned long long), s))) return e;
-    if (a.n == 0) return hipSuccess;
+    // this launch's counters were zeroed by the previous launch (or at allocation); it
+    // zeroes the next launch's block itself — only an empty batch, which launches no
+    // kernel, does that with a memset
+    if (a.n == 0) return hipMemsetAsync(a.ctl_next, 0, CTL_BYTES, s);
     const unsigned grid = (unsigned)match_grid(a.n, a.tpw);
     if (a.mode == MODE_FIRST) {  // <= 1 key per topic at keys[t]; cursor stays 0
         if (a.ev_fast0 && (e = hipEventRecord(a.ev_fast0, s))) return e;
