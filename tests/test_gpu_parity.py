@@ -339,3 +339,54 @@ def test_property_engine_vs_match2(filters, topics, slow):
         exp = sorted({i for i, f in enumerate(filters) if et.match(t, f)})
         assert sorted(eng.key_ids(np.array(r, dtype=np.uint32)).tolist()) == exp, (t, filters)
     eng.close()
+
+
+def test_counter_blocks_across_empty_batches_and_modes():
+    """A launch's counters (output cursor, spill count, pool cursors) are zeroed by the
+    launch before it (two alternating blocks, no memsets): every sequence of empty
+    batches, FIRST / COUNT / ALL launches and spill-forcing launches must still start each
+    batch from zero — checked through the device total and the host results."""
+    import torch
+    w = workloads.generate("C", scale=0.005, n_topics=4000)
+    eng = _engine()
+    _load(eng, w)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    exp = ix.match(w.t_bytes, w.t_off)
+    want_total = int(exp[0][-1])
+    dev = torch.device("cuda", 0)
+    d_bytes = torch.from_numpy(w.t_bytes).to(dev)
+    d_off = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
+    tb = int(w.t_off[-1])
+
+    def dev_total(mode):
+        r = eng.match_device_mode(d_bytes.data_ptr(), d_off.data_ptr(), w.n_topics, tb, mode)
+        eng.device_sync()
+        t = torch.empty(1, dtype=torch.int64, device=dev)
+        import ctypes as C
+        lib = C.CDLL("libamdhip64.so")
+        lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        assert lib.hipMemcpy(C.c_void_p(t.data_ptr()), C.c_void_p(r.d_total), 8, 3) == 0
+        return int(t.cpu().item())
+
+    seq = [N.TM_MATCH_ALL, None, N.TM_MATCH_ALL, N.TM_MATCH_FIRST, N.TM_MATCH_ALL, N.TM_MATCH_COUNT, None, None,
+           N.TM_MATCH_ALL, N.TM_MATCH_UNIQUE, N.TM_MATCH_ALL, N.TM_MATCH_FIRST, N.TM_MATCH_FIRST, N.TM_MATCH_ALL]
+    for k, mode in enumerate(seq):
+        if mode is None:  # an empty batch launches no kernel
+            r = eng.match_device_mode(d_bytes.data_ptr(), d_off.data_ptr(), 0, 0, N.TM_MATCH_ALL)
+            eng.device_sync()
+            continue
+        tot = dev_total(mode)
+        if mode == N.TM_MATCH_FIRST:
+            assert tot == 0, (k, tot)  # k_match_first writes keys[t] directly, never the cursor
+        else:
+            assert tot == want_total, (k, mode, tot, want_total)
+    # the host path interleaved with the device path, then full parity
+    _assert_same(_engine_sets(eng, w.t_bytes, w.t_off), exp, "after device sequence")
+    assert eng.match([]) == []
+    _assert_same(_engine_sets(eng, w.t_bytes, w.t_off), exp, "after empty host batch")
+    # spilled topics count from zero in every batch too
+    slow = _engine(force_slow=True)
+    _load(slow, w)
+    for _ in range(3):
+        _assert_same(_engine_sets(slow, w.t_bytes, w.t_off), exp, "forced spill, repeated")
+        assert slow.stats()["n_slow_topics"] == w.n_topics
