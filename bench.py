@@ -175,8 +175,8 @@ def host_rss_gib():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)  # >= 100 timed batches
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--batch", type=int, default=1_000_000)
@@ -342,14 +342,18 @@ def main():
         # host buffers in, host results out (H2D + kernels + D2H of every key): PCIe-inclusive
         to32 = np.ascontiguousarray(to, dtype=np.uint32)
         eng.match_packed_view(tb, to32)
-        t0 = time.perf_counter()
-        reps = 5
-        for _ in range(reps):
+        hl = []
+        for _ in range(10):
+            t0 = time.perf_counter()
             eng.match_packed_view(tb, to32)
-        dt = (time.perf_counter() - t0) / reps
+            hl.append(time.perf_counter() - t0)
+        dt = float(np.mean(hl))
         host_path = {"api": "tm_match_batch", "batch": n, "ms_per_batch": round(dt * 1e3, 3),
+                     "p50_ms": round(float(np.percentile(hl, 50)) * 1e3, 3),
+                     "p99_ms": round(float(np.percentile(hl, 99)) * 1e3, 3),
                      "publishes_per_s": round(n / dt, 1),
-                     "note": "host topic bytes in, host key lists out; bounded by PCIe D2H of the keys"}
+                     "note": "H2D of the topics + kernels + D2H of every key + host result view; "
+                             "bounded by PCIe D2H of the keys"}
         batcher = batcher_load(eng, tb, to32, args.batcher_seconds) if args.batcher_seconds > 0 else None
 
     # ---------------------------------------------------------------- CPU baseline + parity sample
