@@ -23,6 +23,7 @@
 #include <map>
 #include <unordered_map>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/emqx_tm.h"
@@ -470,8 +471,12 @@ struct tm_engine {
     // =====================================================================
     // filter parsing: emqx_trie_search:filter/1 + make_key/2 (emqx_trie_search.erl:115-140,358-366)
     // Returns kind and the terminal node (creating the path when `create`).
+    // Returns kind and the terminal node (creating the path when `create`); *depth_out =
+    // the node's level count.  The walk may start below the root at a node known to lie
+    // on the filter's path (hint_node at level hint_depth: resolve_prefix()).
     bool classify(const uint8_t *f, uint32_t flen, uint32_t flags, bool create, uint8_t *kind_out,
-                  uint32_t *node_out) {
+                  uint32_t *node_out, uint32_t *depth_out = nullptr, uint32_t hint_node = ROOT,
+                  uint32_t hint_depth = 0) {
         // split on '/': tokens (emqx_topic.erl:276-278)
         std::vector<std::pair<uint32_t, uint32_t>> &lv = lv_scratch;  // (start, len)
         lv.clear();
@@ -497,8 +502,9 @@ struct tm_engine {
         uint8_t kind = !wild ? ((flags & TM_KEY_WORDS) ? K_EXACT_WORDS : K_EXACT_BIN)
                              : (hash_pos >= 0 ? K_HASH : K_WILD);
         size_t nwalk = (kind == K_HASH) ? lv.size() - 1 : lv.size();
-        uint32_t node = ROOT;
-        for (size_t i = 0; i < nwalk; i++) {
+        if (depth_out) *depth_out = (uint32_t)nwalk;
+        uint32_t node = hint_depth <= nwalk ? hint_node : ROOT;
+        for (size_t i = hint_depth <= nwalk ? hint_depth : 0; i < nwalk; i++) {
             const uint8_t *p = f + lv[i].first;
             uint32_t len = lv[i].second;
             uint32_t w;
@@ -523,12 +529,43 @@ struct tm_engine {
         return true;
     }
 
-    void apply_one(const StagedOp &op) {
+    // Deepest existing node on a filter's path, read-only (safe to run in parallel
+    // before an epoch's ops are applied: nodes are never removed while ops apply).
+    void resolve_prefix(const uint8_t *f, uint32_t flen, std::vector<std::pair<uint32_t, uint32_t>> &lv,
+                        uint32_t *node_out, uint32_t *depth_out) const {
+        lv.clear();
+        uint32_t st = 0;
+        for (uint32_t i = 0; i <= flen; i++)
+            if (i == flen || f[i] == '/') {
+                lv.push_back({st, i - st});
+                st = i + 1;
+            }
+        uint32_t node = ROOT, d = 0;
+        for (; d < lv.size(); d++) {
+            const uint8_t *p = f + lv[d].first;
+            const uint32_t len = lv[d].second;
+            if (len == 1 && *p == '#') break;
+            const uint32_t w = (len == 1 && *p == '+') ? W_PLUS : word_lookup(p, len);
+            if (w == NONE) break;
+            const uint64_t s = edge_find(dev_id(node), w);
+            if (s == ~0ull) break;
+            node = slot_node[s];
+        }
+        *node_out = node;
+        *depth_out = d;
+    }
+    // the shape test of key_ord() from the level count alone (no parent-chain walk)
+    static bool deep_shape(uint8_t kind, uint32_t depth) {
+        if (kind == K_HASH) return depth > 30;
+        return (kind == K_EXACT_WORDS || kind == K_WILD) && depth > 31;
+    }
+
+    void apply_one(const StagedOp &op, uint32_t hint_node = ROOT, uint32_t hint_depth = 0) {
         uint8_t kind;
-        uint32_t node;
+        uint32_t node, depth = 0;
         const uint8_t *fp = stage_bytes.data() + op.off;
         if (op.op == TM_OP_ADD) {
-            classify(fp, op.len, op.flags, true, &kind, &node);
+            classify(fp, op.len, op.flags, true, &kind, &node, &depth, hint_node, hint_depth);
             if (kind == K_DEAD) {
                 auto key = std::make_pair(std::string((const char *)fp, op.len), op.id);
                 if (dead_keys.count(key)) return;
@@ -544,7 +581,7 @@ struct tm_engine {
             if (kset_find(node, kind, op.id, &slot) != NONE) return;  // set semantics
             uint32_t h = alloc_key();
             keys[h] = KeyRec{node, kind, {0, 0, 0}, op.id};
-            if (key_is_deep(h)) n_deep++;
+            if (deep_shape(kind, depth)) n_deep++;
             id_add(h);
             dirty_kid.push_back(h);
             kset[slot] = h;
@@ -552,7 +589,8 @@ struct tm_engine {
             n_live++;
             deltas.push_back(Delta{node, h, (uint8_t)(kind == K_HASH), 1});
         } else if (op.op == TM_OP_DEL) {
-            if (!classify(fp, op.len, op.flags, false, &kind, &node)) return;  // idempotent
+            if (!classify(fp, op.len, op.flags, false, &kind, &node, &depth, hint_node, hint_depth))
+                return;  // idempotent
             if (kind == K_DEAD) {
                 auto it = dead_keys.find(std::make_pair(std::string((const char *)fp, op.len), op.id));
                 if (it == dead_keys.end()) return;
@@ -569,12 +607,37 @@ struct tm_engine {
             if (h == NONE) return;
             kset_erase_slot(slot);
             deltas.push_back(Delta{node, h, (uint8_t)(kind == K_HASH), 0});
-            if (key_is_deep(h)) n_deep--;
+            if (deep_shape(kind, depth)) n_deep--;
             id_del(h);
             keys[h].kind = K_FREE;
             free_pending.push_back(h);
             n_live--;
         }
+    }
+
+    // An epoch's ops in order.  Their filter paths are first resolved against the trie as
+    // it stands, in parallel (read-only, memory-latency bound: one dependent hash probe
+    // per level); the ops then apply in order, each walk starting at its resolved prefix.
+    // A prefix stays valid while ops apply (nodes are only ever added), and an op whose
+    // path appears only during this epoch resumes from where resolution stopped.
+    void apply_staged() {
+        const size_t n = staged.size();
+        const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        const unsigned nt = (n_edges == 0 || n < 4096) ? 1u : (unsigned)std::min<size_t>(hw, n / 2048);
+        if (nt <= 1) {
+            for (const StagedOp &op : staged) apply_one(op);
+            return;
+        }
+        std::vector<uint32_t> hnode(n), hdepth(n);
+        std::vector<std::thread> th;
+        for (unsigned k = 0; k < nt; k++)
+            th.emplace_back([&, k] {
+                std::vector<std::pair<uint32_t, uint32_t>> lv;
+                for (size_t i = k; i < n; i += nt)
+                    resolve_prefix(stage_bytes.data() + staged[i].off, staged[i].len, lv, &hnode[i], &hdepth[i]);
+            });
+        for (auto &t : th) t.join();
+        for (size_t i = 0; i < n; i++) apply_one(staged[i], hnode[i], hdepth[i]);
     }
 
     // Recompute a node's emission bits from its list (and keep its I_PLUS/I_LIT):
@@ -880,7 +943,7 @@ struct tm_engine {
 
     int commit() {
         const uint64_t t0 = now_us();
-        for (const StagedOp &op : staged) apply_one(op);
+        apply_staged();
         if (edge_full) {
             err = "edge table full: more trie nodes than MAX_EDGE_SLOTS / 2 (shard the filters over more GPUs); "
                   "the engine is unusable and must be recreated";
@@ -976,10 +1039,6 @@ struct tm_engine {
         }
         *ord = o;
         return !deep;
-    }
-    bool key_is_deep(uint32_t h) const {
-        uint64_t o;
-        return !key_ord(h, &o);
     }
 
     // ETS term order of two keys (emqx_trie_search.erl:109-111 key shapes; Erlang term

@@ -321,6 +321,74 @@ def test_churn_epochs_vs_oracle():
     assert s["n_delta_commits"] >= 4 and s["n_keys"] == len(live)
 
 
+def test_large_epochs_resolve_prefixes_in_parallel():
+    """Epochs of >= 4096 ops on a populated trie take the parallel prefix resolution
+    (engine.cpp apply_staged): paths resolved against the trie as it stood, then applied in
+    order.  Covers ops whose path appears only during the epoch (add, then delete or re-add
+    of the same key), deletes of keys that never existed, filters with '#' before the end
+    (kept on the host), word-list keys, and filters deeper than the device order code
+    (n_deep_keys), each epoch bit-exact vs the oracle."""
+    rng = np.random.default_rng(0xE11A0006)
+    w = workloads.generate("E", scale=0.05, n_topics=6000)
+    filters = w.filters()
+    base = [(f, int(i), 0) for f, i in zip(filters, w.f_id.tolist())]
+    eng = _engine()
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    live = set(base)
+    next_id = int(w.f_id.max()) + 1
+    deep = b"/".join([b"d"] * 34)
+    for epoch in range(3):
+        ops, dead = [], []
+        order = sorted(live)
+        for j in rng.choice(len(order), size=2500, replace=False):
+            k = order[int(j)]
+            ops.append((N.TM_OP_DEL, k[0], k[1], N.TM_KEY_WORDS if k[2] else 0))
+            live.discard(k)
+        for _ in range(2500):
+            src = filters[int(rng.integers(len(filters)))]
+            r = rng.random()
+            if r < 0.3:
+                f = src + b"/new%d" % int(rng.integers(50))      # a new level under an old path
+            elif r < 0.4:
+                f = b"fresh%d/" % int(rng.integers(30)) + src     # a new path from the root
+            elif r < 0.45:
+                f = deep + (b"/+" if rng.random() < 0.5 else b"/#")  # deeper than the order code
+            elif r < 0.5:
+                f = src + b"/#"
+            else:
+                f = src
+            wf = 1 if (r > 0.9 and b"+" not in f and b"#" not in f) else 0
+            k = (f, next_id, wf)
+            next_id += 1
+            ops.append((N.TM_OP_ADD, f, k[1], N.TM_KEY_WORDS if wf else 0))
+            live.add(k)
+        # same-epoch sequences: add then delete, delete then re-add, deletes of nothing
+        for t in range(200):
+            f = b"tmp%d/x/%d" % (epoch, t)
+            ops += [(N.TM_OP_ADD, f, 7), (N.TM_OP_DEL, f, 7)]
+            g = order[t]
+            if g in live:
+                ops += [(N.TM_OP_DEL, g[0], g[1], N.TM_KEY_WORDS if g[2] else 0),
+                        (N.TM_OP_ADD, g[0], g[1], N.TM_KEY_WORDS if g[2] else 0)]
+            ops.append((N.TM_OP_DEL, b"never/there/%d" % t, 1))
+        for t in range(20):  # '#' before the last level: stored, never matched
+            dead.append((b"z%d/#/y" % t, 5))
+            ops.append((N.TM_OP_ADD, b"z%d/#/y" % t, 5))
+        eng.apply(ops)
+        eng.commit()
+        keys = sorted(live)
+        ix = oracle.OrderedIndex.from_filters([k[0] for k in keys], ids=[k[1] for k in keys],
+                                              word_form=[k[2] for k in keys])
+        _assert_same(_engine_sets(eng, w.t_bytes, w.t_off), ix.match(w.t_bytes, w.t_off), f"epoch {epoch}")
+        deep_live = sum(1 for k in keys if k[0].startswith(deep))
+        st_ = eng.stats()
+        assert st_["n_deep_keys"] == deep_live, (st_["n_deep_keys"], deep_live)
+        assert st_["n_keys"] == len(live) + 20
+        eng.apply([(N.TM_OP_DEL, f, i) for f, i in dead])  # the dead keys go again
+        eng.commit()
+
+
 # ------------------------------------------------------------- property
 _lvl = st.sampled_from([b"a", b"b", b"c", b"", b"foo", b"$x", b"0F"])
 _topic = st.lists(_lvl, min_size=1, max_size=7).map(lambda l: b"/".join(l))
