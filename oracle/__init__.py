@@ -57,6 +57,7 @@ def load():
 
 
 ALGO_TRIE, ALGO_BRUTE = 0, 1
+ALGO_FILTER = 2  # matches_filter/3: the queries are topic filters (emqx_trie_search.erl:186-189)
 MODE_ALL, MODE_UNIQUE, MODE_FIRST = 0, 1, 2
 
 

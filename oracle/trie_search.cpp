@@ -122,6 +122,33 @@ CmpRes compare(const uint32_t *F, uint32_t FL, const uint32_t *W, uint32_t WL) {
     }
 }
 
+// compare/3 for a filter search (matches_filter/3, emqx_trie_search.erl:186-189): the
+// topic-search clauses plus the two "Filter search" clauses (:291-300) -- a query '#' as
+// the last word matches any remaining key words, a query '+' matches any one key word and
+// passes the deeper result through unchanged (a `lower` there stays `lower`, so it is
+// not a backtrack point).  Clause order as in the reference.
+CmpRes compare_filter(const uint32_t *F, uint32_t FL, const uint32_t *W, uint32_t WL) {
+    int last_plus = -1;
+    for (uint32_t pos = 0;; pos++) {
+        const bool fin = pos == FL, win = pos == WL;
+        if (fin && win) return {MATCH_FULL, 0, 0};                          // compare([], [], _)
+        if (fin) return {MATCH_PREFIX, 0, 0};                               // compare([], _Words, _)
+        if (FL - pos == 1 && F[pos] == R_HASH) return {MATCH_FULL, 0, 0};   // compare(['#'], ...)
+        if (!win && WL - pos == 1 && W[pos] == R_HASH) return {MATCH_FULL, 0, 0};  // compare(_, ['#'], _)
+        if (!win && W[pos] == R_PLUS) continue;                             // compare([_|TF], ['+'|TW], Pos)
+        if (F[pos] == R_PLUS && !win) {                                     // compare(['+'|TF], [HW|TW], Pos)
+            last_plus = (int)pos;
+            continue;
+        }
+        if (!win && F[pos] == W[pos]) continue;                             // compare([HW|TF], [HW|TW], Pos)
+        if (win || F[pos] > W[pos]) {                                       // lower (:325-340)
+            if (last_plus >= 0) return {SEEK, (uint32_t)last_plus, W[last_plus]};
+            return {LOWER, 0, 0};
+        }
+        return {SEEK, pos, W[pos]};                                         // {Pos, HW} (:341-348)
+    }
+}
+
 // ETS-like positions: [0, NL) list keys, [NL, NL+NB) binary keys, NL+NB = '$end_of_table'
 struct Searcher {
     const Index &ix;
@@ -205,6 +232,34 @@ struct Searcher {
         }
     }
 };
+
+// matches_filter/3 (emqx_trie_search.erl:186-189,192-228 with topic_filter set): the
+// same search_new/search_up loop over the list keys only -- a binary key compares
+// `lower` and the filter search never runs match_topics/4.  Appends input key indices in
+// walk order (the reference's accumulator holds them reversed).
+void search_filter(const Index &ix, const uint8_t *q, uint32_t qlen, const uint32_t *W, uint32_t WL, int mode,
+                   std::vector<uint32_t> &out, std::vector<uint32_t> &prefix, const Searcher &S) {
+    const size_t NL = ix.lk.size();
+    // base_init/1 (:160-163): a first word <<"$", _/bytes>> starts at [W0]
+    size_t cur = (qlen && q[0] == '$') ? S.next_base_list(W, 1) : S.next_base_list(nullptr, 0);
+    while (cur < NL) {
+        const ListKey &k = ix.lk[cur];
+        CmpRes r = compare_filter(&ix.wr[k.woff], k.wlen, W, WL);
+        if (r.k == MATCH_FULL) {
+            out.push_back(k.src);
+            if (mode == 2) return;
+            cur++;
+        } else if (r.k == MATCH_PREFIX) {
+            cur++;
+        } else if (r.k == LOWER) {
+            return;
+        } else {
+            prefix.assign(&ix.wr[k.woff], &ix.wr[k.woff] + r.pos);
+            prefix.push_back(r.word);
+            cur = S.next_base_list(prefix.data(), (uint32_t)prefix.size());
+        }
+    }
+}
 
 // emqx_topic:match/2 on token lists (emqx_topic.erl:78-102); tokens are bytes, '+'/'#'
 // levels are wildcards in the filter only.
@@ -317,7 +372,8 @@ static void to_words(const Index &ix, const uint8_t *t, uint32_t n, std::vector<
     }
 }
 
-// Match a batch with the trie-search restatement (algo 0) or brute force (algo 1),
+// Match a batch with the trie-search restatement (algo 0), brute force (algo 1) or the
+// filter search of matches_filter/3 (algo 2: queries are topic filters),
 // mode 0 = [], 1 = [unique], 2 = return_first; nthreads workers.  Returns a results
 // handle (per-topic ids sorted ascending) or, when `counts_only`, only fills
 // cnt_out and returns nullptr.
@@ -336,7 +392,7 @@ void *ots_match(void *h, const uint8_t *bytes, const uint32_t *off, uint64_t n, 
     auto worker = [&]() {
         Searcher S(ix);
         std::vector<std::string> tok;
-        std::vector<uint32_t> W, out;
+        std::vector<uint32_t> W, out, prefix;
         uint64_t local = 0;
         for (;;) {
             uint64_t b = next.fetch_add(256);
@@ -350,6 +406,20 @@ void *ots_match(void *h, const uint8_t *bytes, const uint32_t *off, uint64_t n, 
                 if (algo == 0) {
                     to_words(ix, t, tl, tok, W, &bad);
                     if (!bad) S.search(t, tl, W.data(), (uint32_t)W.size(), mode, out);
+                } else if (algo == 2) {
+                    // matches_filter/3: filter_words/1 (:356-366) -- '+'/'#' levels become
+                    // the atoms, no badarg
+                    split(t, tl, tok);
+                    W.resize(tok.size());
+                    for (size_t j = 0; j < tok.size(); j++)
+                        W[j] = tok[j] == "#" ? R_HASH : tok[j] == "+" ? R_PLUS : topic_rank(ix, tok[j]);
+                    // a '#' before the last level: the reference's walk does not terminate
+                    // (a '+' key backtracks to seek word '#', which sorts below the key), so
+                    // such a query is refused with the badarg status instead
+                    bad = false;
+                    for (size_t j = 0; j + 1 < W.size(); j++)
+                        if (W[j] == R_HASH) bad = true;
+                    if (!bad) search_filter(ix, t, tl, W.data(), (uint32_t)W.size(), mode, out, prefix, S);
                 } else {
                     split(t, tl, tok);
                     bad = false;
