@@ -56,6 +56,7 @@ EXPORTS = (
     "tm_commit_epoch", "tm_match_batch", "tm_match_device", "tm_device_sync",
     "tm_reserve_matches", "tm_key_info", "tm_key_ids", "tm_stats", "tm_debug_stats", "tm_debug_timing",
     "tm_result_ids_device", "tm_merge_shards_device", "tm_merge_shards", "tm_match_device_mode",
+    "tm_match_filter_batch",
 )
 # every symbol include/emqx_tm_batcher.h declares
 BATCHER_EXPORTS = (
@@ -149,6 +150,7 @@ def load() -> C.CDLL:
                                     C.c_size_t]
     lib.tm_commit_epoch.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.tm_match_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, P(tm_result)]
+    lib.tm_match_filter_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, P(tm_result)]
     lib.tm_match_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64,
                                     C.c_void_p, P(tm_dev_result)]
     lib.tm_device_sync.argtypes = [C.c_void_p]
@@ -314,6 +316,31 @@ class Engine:
         k = (np.ctypeslib.as_array(res.keys, shape=(span,)).copy() if span
              else np.zeros(0, dtype=np.uint32))
         return o, c, k, st
+
+    def match_filter_packed(self, buf: np.ndarray, off: np.ndarray, mode: int = TM_MATCH_ALL):
+        """tm_match_filter_batch (matches_filter/3) on packed topic filters; returns
+        (off, cnt, keys, status) numpy copies, keys per query in walk order."""
+        n = len(off) - 1
+        res = tm_result()
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        self._check(self.lib.tm_match_filter_batch(self.h, buf.ctypes.data, off.ctypes.data, n, mode, C.byref(res)))
+        if n == 0:
+            e = np.zeros(0, dtype=np.uint32)
+            return e, e, e, np.zeros(0, dtype=np.int32)
+        o = np.ctypeslib.as_array(res.off, shape=(n,)).copy()
+        c = np.ctypeslib.as_array(res.cnt, shape=(n,)).copy()
+        st = np.ctypeslib.as_array(res.status, shape=(n,)).copy()
+        k = (np.ctypeslib.as_array(res.keys, shape=(int(res.total),)).copy() if res.total
+             else np.zeros(0, dtype=np.uint32))
+        return o, c, k, st
+
+    def match_filter(self, filters, mode: int = TM_MATCH_ALL):
+        """List of topic filters -> list of key-handle lists in walk order (None for a
+        query the engine refuses: '#' before the last level)."""
+        buf, off = pack_topics(filters)
+        o, c, k, st = self.match_filter_packed(buf, off, mode)
+        return [None if st[i] == TM_BADARG else k[o[i]:o[i] + c[i]].tolist() for i in range(len(filters))]
 
     def match_packed_view(self, buf: np.ndarray, off: np.ndarray, mode: int = TM_MATCH_ALL) -> tm_result:
         """tm_match_batch without copying: the engine-owned tm_result (valid until the next

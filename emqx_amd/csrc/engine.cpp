@@ -1084,6 +1084,131 @@ struct tm_engine {
         if (c) return c;
         return ka.id < kb.id ? -1 : (ka.id > kb.id ? 1 : 0);
     }
+
+    // =====================================================================
+    // matches_filter/3 index (filter_kernels.hip): every word-list key ({Words, {ID}}:
+    // exact word-form, wildcard, 'P/#' and dead keys -- the keys a filter search can
+    // meet; {Binary, {ID}} keys compare `lower` and end it) as order codes, sorted in
+    // ETS term order.  Built on first use after a commit; the match path never pays it.
+    struct FilterIndex {
+        uint64_t epoch = UINT64_MAX;     // epoch the device copy was built for
+        std::vector<std::string> dict;   // sorted distinct literal words of the keys
+        uint32_t K = 0;
+        DevBuf d_kw, d_koff, d_kh;
+        DevBuf d_qw, d_qoff, d_qdollar, d_qstatus, d_cnt, d_off, d_out, d_scan;
+        std::vector<uint32_t> qw, qoff, h_off, h_cnt, h_keys, u_keys;
+        std::vector<uint8_t> qdollar;
+        std::vector<int32_t> qstatus;
+    } fx;
+
+    static void split_words(const uint8_t *p, size_t n, std::vector<std::pair<size_t, size_t>> &out) {
+        out.clear();
+        size_t st = 0;
+        for (size_t i = 0; i <= n; i++)
+            if (i == n || p[i] == '/') {
+                out.emplace_back(st, i - st);
+                st = i + 1;
+            }
+    }
+    // order code of a literal word: 2k+3 for the k-th dictionary word, 2k+2 for a word
+    // that is not in the dictionary and sorts just below its k-th entry
+    uint32_t fx_code(const char *p, size_t n) const {
+        const std::string w(p, n);
+        size_t k = std::lower_bound(fx.dict.begin(), fx.dict.end(), w) - fx.dict.begin();
+        return (uint32_t)(k < fx.dict.size() && fx.dict[k] == w ? 2 * k + 3 : 2 * k + 2);
+    }
+    static uint32_t fx_level(const char *p, size_t n) {  // '#' 0, '+' 1, else not a wildcard
+        if (n == 1 && p[0] == '#') return 0;
+        if (n == 1 && p[0] == '+') return 1;
+        return NONE;
+    }
+
+    int build_filter_index() {
+        const uint32_t HASHW = NONE - 2;
+        std::vector<uint32_t> lk;  // word-list key handles
+        std::vector<uint8_t> used(word_off.size(), 0);
+        std::vector<std::string> words;
+        std::vector<std::pair<size_t, size_t>> lv;
+        for (uint32_t h = 0; h < keys.size(); h++) {
+            const KeyRec &k = keys[h];
+            if (k.kind == K_EXACT_WORDS || k.kind == K_WILD || k.kind == K_HASH) {
+                lk.push_back(h);
+                for (uint32_t v = k.node; v != ROOT; v = node_parent[v])
+                    if (node_word[v] != W_PLUS) used[node_word[v]] = 1;
+            } else if (k.kind == K_DEAD) {
+                lk.push_back(h);
+                const std::string &f = dead_filter[h];
+                split_words((const uint8_t *)f.data(), f.size(), lv);
+                for (auto &x : lv)
+                    if (fx_level(f.data() + x.first, x.second) == NONE) words.emplace_back(f, x.first, x.second);
+            }
+        }
+        for (uint32_t w = 0; w < used.size(); w++)
+            if (used[w]) words.emplace_back((const char *)warena.data() + word_off[w], word_len[w]);
+        std::sort(words.begin(), words.end());
+        words.erase(std::unique(words.begin(), words.end()), words.end());
+        fx.dict.swap(words);
+        std::vector<uint32_t> wcode(word_off.size(), NONE);
+        for (uint32_t w = 0; w < used.size(); w++)
+            if (used[w]) wcode[w] = fx_code((const char *)warena.data() + word_off[w], word_len[w]);
+        // codes of every key, unsorted
+        std::vector<uint64_t> off(lk.size() + 1, 0);
+        std::vector<uint32_t> code, path;
+        for (size_t i = 0; i < lk.size(); i++) {
+            const uint32_t h = lk[i];
+            if (keys[h].kind == K_DEAD) {
+                const std::string &f = dead_filter[h];
+                split_words((const uint8_t *)f.data(), f.size(), lv);
+                for (auto &x : lv) {
+                    uint32_t c = fx_level(f.data() + x.first, x.second);
+                    code.push_back(c != NONE ? c : fx_code(f.data() + x.first, x.second));
+                }
+            } else {
+                key_words(h, path);
+                for (uint32_t w : path) code.push_back(w == HASHW ? 0u : w == W_PLUS ? 1u : wcode[w]);
+            }
+            off[i + 1] = code.size();
+        }
+        if (code.size() >= 0xFFFFFFFFull) {
+            err = "matches_filter index: more than 4 Gi key words";
+            return TM_ENOMEM;
+        }
+        // ETS term order: words (codes) lexicographically, a prefix first; then the id
+        std::vector<uint32_t> perm(lk.size());
+        for (uint32_t i = 0; i < perm.size(); i++) perm[i] = i;
+        std::sort(perm.begin(), perm.end(), [&](uint32_t a, uint32_t b) {
+            const uint32_t *pa = &code[off[a]], *pb = &code[off[b]];
+            const uint64_t na = off[a + 1] - off[a], nb = off[b + 1] - off[b];
+            for (uint64_t i = 0; i < std::min(na, nb); i++)
+                if (pa[i] != pb[i]) return pa[i] < pb[i];
+            if (na != nb) return na < nb;
+            return keys[lk[a]].id < keys[lk[b]].id;
+        });
+        std::vector<uint32_t> kw, koff(lk.size() + 1, 0), kh(lk.size());
+        kw.reserve(code.size());
+        for (size_t j = 0; j < perm.size(); j++) {
+            const uint32_t i = perm[j];
+            kw.insert(kw.end(), code.begin() + off[i], code.begin() + off[i + 1]);
+            koff[j + 1] = (uint32_t)kw.size();
+            kh[j] = lk[i];
+        }
+        fx.K = (uint32_t)lk.size();
+        hipError_t e;
+        if ((e = fx.d_kw.ensure(std::max<size_t>(kw.size(), 1) * 4)) != hipSuccess ||
+            (e = fx.d_koff.ensure(koff.size() * 4)) != hipSuccess ||
+            (e = fx.d_kh.ensure(std::max<size_t>(kh.size(), 1) * 4)) != hipSuccess) {
+            err = std::string("matches_filter index alloc: ") + hipGetErrorString(e);
+            return TM_ENOMEM;
+        }
+        if ((!kw.empty() && (e = hipMemcpy(fx.d_kw.p, kw.data(), kw.size() * 4, hipMemcpyHostToDevice))) ||
+            (e = hipMemcpy(fx.d_koff.p, koff.data(), koff.size() * 4, hipMemcpyHostToDevice)) ||
+            (!kh.empty() && (e = hipMemcpy(fx.d_kh.p, kh.data(), kh.size() * 4, hipMemcpyHostToDevice)))) {
+            err = std::string("matches_filter index upload: ") + hipGetErrorString(e);
+            return TM_EDEVICE;
+        }
+        fx.epoch = epoch;
+        return TM_OK;
+    }
 };
 
 // ============================================================================
@@ -1155,7 +1280,9 @@ void tm_destroy(tm_engine *eng) {
     if (eng->stream) (void)hipStreamSynchronize(eng->stream);
     for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_dd_wl,
                       &eng->d_dd_wl_n, &eng->d_ukeys, &eng->d_ucnt,
-                      &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot})
+                      &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
+                      &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
+                      &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
                       &eng->d_arena, &eng->d_scatter_idx,
@@ -1645,6 +1772,123 @@ int tm_key_ids(const tm_engine *eng, const uint32_t *keys, size_t n, uint64_t *i
         uint32_t k = keys[i];
         if (k >= eng->keys.size() || eng->keys[k].kind == K_FREE) return TM_ENOTFOUND;
         ids_out[i] = eng->keys[k].id;
+    }
+    return TM_OK;
+}
+
+int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
+                          tm_result *out) {
+    if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
+    if (mode != TM_MATCH_ALL && mode != TM_MATCH_UNIQUE && mode != TM_MATCH_FIRST) return TM_EINVAL;
+    if (!eng->staged.empty()) {
+        eng->err = "tm_match_filter_batch: staged ops not committed";
+        return TM_ESTATE;
+    }
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    memset(out, 0, sizeof(*out));
+    out->n = n;
+    if (n == 0) return TM_OK;
+    auto &fx = eng->fx;
+    int rc;
+    if (fx.epoch != eng->epoch && (rc = eng->build_filter_index())) return rc;
+    // filter_words/1 (emqx_trie_search.erl:356-366) as order codes; base_init/1 flag
+    fx.qw.clear();
+    fx.qoff.assign(1, 0);
+    fx.qdollar.assign(n, 0);
+    fx.qstatus.assign(n, TM_TOPIC_OK);
+    std::vector<std::pair<size_t, size_t>> lv;
+    for (uint32_t i = 0; i < n; i++) {
+        const char *t = (const char *)bytes + off[i];
+        const size_t tl = off[i + 1] - off[i];
+        tm_engine::split_words((const uint8_t *)t, tl, lv);
+        for (size_t j = 0; j < lv.size(); j++) {
+            uint32_t c = tm_engine::fx_level(t + lv[j].first, lv[j].second);
+            if (c == 0 && j + 1 < lv.size()) fx.qstatus[i] = TM_BADARG;  // '#' before the last level
+            fx.qw.push_back(c != NONE ? c : eng->fx_code(t + lv[j].first, lv[j].second));
+        }
+        if (fx.qw.size() >= 0xFFFFFFFFull) return TM_EINVAL;
+        fx.qoff.push_back((uint32_t)fx.qw.size());
+        fx.qdollar[i] = tl && t[0] == '$';
+    }
+    hipStream_t s = eng->stream;
+    const size_t nq = fx.qw.size();
+    TM_TRY_HIP(fx.d_qw.ensure(std::max<size_t>(nq, 1) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(fx.d_qoff.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(fx.d_qdollar.ensure(n), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(fx.d_qstatus.ensure((size_t)n * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(fx.d_cnt.ensure((size_t)n * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(fx.d_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(fx.d_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
+    if (nq) TM_TRY_HIP(hipMemcpyAsync(fx.d_qw.p, fx.qw.data(), nq * 4, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
+    TM_TRY_HIP(hipMemcpyAsync(fx.d_qoff.p, fx.qoff.data(), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s), TM_EDEVICE,
+               "H2D");
+    TM_TRY_HIP(hipMemcpyAsync(fx.d_qdollar.p, fx.qdollar.data(), n, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
+    TM_TRY_HIP(hipMemcpyAsync(fx.d_qstatus.p, fx.qstatus.data(), (size_t)n * 4, hipMemcpyHostToDevice, s), TM_EDEVICE,
+               "H2D");
+    FilterArgs a{};
+    a.kw = fx.d_kw.as<uint32_t>();
+    a.koff = fx.d_koff.as<uint32_t>();
+    a.kh = fx.d_kh.as<uint32_t>();
+    a.K = fx.K;
+    a.n = n;
+    a.qw = fx.d_qw.as<uint32_t>();
+    a.qoff = fx.d_qoff.as<uint32_t>();
+    a.qdollar = fx.d_qdollar.as<uint8_t>();
+    a.qstatus = fx.d_qstatus.as<int32_t>();
+    a.first = mode == TM_MATCH_FIRST;
+    a.cnt = fx.d_cnt.as<uint32_t>();
+    a.out_off = fx.d_off.as<uint32_t>();
+    TM_TRY_HIP(launch_filter_walk(a, 0, s), TM_EDEVICE, "k_filter_walk count");
+    TM_TRY_HIP(launch_excl_scan(a.cnt, 1, n, fx.d_off.as<uint32_t>(), fx.d_scan.as<uint32_t>(), s), TM_EDEVICE,
+               "scan");
+    fx.h_off.resize((size_t)n + 1);
+    fx.h_cnt.resize(n);
+    TM_TRY_HIP(hipMemcpyAsync(fx.h_off.data(), fx.d_off.p, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+               "D2H");
+    TM_TRY_HIP(hipMemcpyAsync(fx.h_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+    TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk count");
+    const uint64_t total = fx.h_off[n];
+    fx.h_keys.resize(total);
+    if (total) {
+        TM_TRY_HIP(fx.d_out.ensure(total * 4), TM_ENOMEM, "alloc");
+        a.out = fx.d_out.as<uint32_t>();
+        TM_TRY_HIP(launch_filter_walk(a, 1, s), TM_EDEVICE, "k_filter_walk emit");
+        TM_TRY_HIP(hipMemcpyAsync(fx.h_keys.data(), fx.d_out.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                   "D2H");
+        TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk emit");
+    }
+    out->total = total;
+    out->off = fx.h_off.data();
+    out->cnt = fx.h_cnt.data();
+    out->keys = fx.h_keys.data();
+    out->status = fx.qstatus.data();
+    if (mode == TM_MATCH_UNIQUE) {
+        // match_add/2 into a map (:350-352): the last key per id in walk order wins;
+        // maps:values/1 lists them by id
+        fx.u_keys.clear();
+        std::vector<std::pair<uint64_t, uint32_t>> best;
+        std::unordered_map<uint64_t, size_t> at;
+        for (uint32_t i = 0; i < n; i++) {
+            best.clear();
+            at.clear();
+            for (uint32_t k = fx.h_off[i]; k < fx.h_off[i] + fx.h_cnt[i]; k++) {
+                const uint32_t h = fx.h_keys[k];
+                const uint64_t id = eng->keys[h].id;
+                auto it = at.find(id);
+                if (it == at.end()) {
+                    at.emplace(id, best.size());
+                    best.emplace_back(id, h);
+                } else {
+                    best[it->second].second = h;
+                }
+            }
+            std::sort(best.begin(), best.end());
+            fx.h_off[i] = (uint32_t)fx.u_keys.size();
+            fx.h_cnt[i] = (uint32_t)best.size();
+            for (auto &b : best) fx.u_keys.push_back(b.second);
+        }
+        out->total = fx.u_keys.size();
+        out->keys = fx.u_keys.data();
     }
     return TM_OK;
 }

@@ -148,6 +148,29 @@ class TopicIndex:
             raise r
         return r
 
+    def matches_filter_batch(self, filters, opts=()) -> list:
+        """Batched matches_filter/3 (emqx_topic_index.erl:82-84): one list of keys per topic
+        filter, in the reference's list order (its accumulator: the walk's keys reversed,
+        i.e. descending term order).  BadArg for a filter with '#' before its last level
+        (the reference's walk never returns on one)."""
+        self.commit()
+        out = []
+        for hs in self.eng.match_filter(filters, N.TM_MATCH_ALL):
+            if hs is None:
+                out.append(BadArg("'#' before the last level"))
+                continue
+            keys = [self._key_of(h) for h in hs]
+            if not opts:
+                keys.sort(key=_key_order, reverse=True)
+            out.append(self._reduce(keys, opts))
+        return out
+
+    def matches_filter(self, topic_filter, tab=None, opts=()):
+        r = self.matches_filter_batch([topic_filter], opts)[0]
+        if isinstance(r, BadArg):
+            raise r
+        return r
+
     def match(self, topic, tab=None):
         """match/2: the first key in ETS term order, or False."""
         r = self.matches(topic, None, ["return_first"])

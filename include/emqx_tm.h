@@ -19,6 +19,8 @@
  *                               emqx_router:match_routes/1 (v2)   apps/emqx/src/emqx_router.erl:205-212,511-516
  *   tm_match_batch (UNIQUE)     emqx_topic_index:matches/3 ([unique])  apps/emqx/src/emqx_trie_search.erl:350-352
  *   tm_match_batch (FIRST)      emqx_topic_index:match/2 (return_first) apps/emqx/src/emqx_trie_search.erl:171-178
+ *   tm_match_filter_batch       emqx_topic_index:matches_filter/3 apps/emqx/src/emqx_topic_index.erl:82-84,
+ *                               emqx_trie_search:matches_filter/3 apps/emqx/src/emqx_trie_search.erl:186-189
  *   tm_key_info                 emqx_topic_index:get_id/1, get_topic/1 apps/emqx/src/emqx_topic_index.erl:87-94
  *   tm_stats                    emqx_router:stats/1 (n_routes)    apps/emqx/src/emqx_router.erl:632-635
  *
@@ -49,7 +51,7 @@
 extern "C" {
 #endif
 
-#define TM_ABI_VERSION 3u
+#define TM_ABI_VERSION 4u
 
 /* status codes */
 #define TM_OK          0
@@ -235,6 +237,19 @@ int tm_merge_shards_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_
                            void *stream);
 int tm_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,
                     uint32_t *out_off, uint64_t *out_ids, uint64_t out_cap);
+
+/* matches_filter/3: query i is a topic FILTER, bytes[off[i] .. off[i+1]).  Returns the keys
+ * the reference's seek walk (emqx_trie_search.erl:192-258 with the filter-search clauses of
+ * compare/3, :291-300) meets, as key handles in walk order (the reference's accumulator holds
+ * the same keys reversed).  Only word-list keys can match ({Binary, {ID}} keys end the walk).
+ * mode: TM_MATCH_ALL, TM_MATCH_UNIQUE (last key per id in walk order, listed by id) or
+ * TM_MATCH_FIRST (the first key met).  A query with '#' before its last level gets per-query
+ * status TM_BADARG: the reference's walk does not terminate on it.  The walk runs on the GPU
+ * (filter_kernels.hip) over a term-ordered copy of the word-list keys that the first call
+ * after each commit builds.  Result memory as for tm_match_batch, valid until the next
+ * tm_match_filter_batch / tm_commit_epoch / tm_destroy. */
+int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
+                          tm_result *out);
 
 /* key introspection (get_id/1, get_topic/1) */
 int tm_key_info(const tm_engine *eng, uint32_t key, uint64_t *id, uint32_t *flags,

@@ -50,7 +50,7 @@ def build(names):
                                                 text=True))
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wno-unused-function", *flags, os.path.join(CSRC, "engine.cpp"),
-               kern, os.path.join(CSRC, "result_kernels.hip"), "-o", out]
+               kern, os.path.join(CSRC, "result_kernels.hip"), os.path.join(CSRC, "filter_kernels.hip"), "-o", out]
         procs.append((name, subprocess.Popen(cmd)))
         if len(procs) >= 4:
             n, p = procs.pop(0)
