@@ -194,7 +194,12 @@ def main():
     ap.add_argument("--churn", type=int, default=0, metavar="EPOCHS",
                     help="config-E style run: EPOCHS delta epochs of 1%% adds + 1%% deletes, each committed "
                          "between match batches (commit and match timed separately)")
+    ap.add_argument("--filter-search", type=int, default=0, metavar="Q",
+                    help="matches_filter/3 run: Q topic-filter queries (the config's own filters, "
+                         "generalised) walked on the GPU (tm_match_filter_batch), oracle beside it")
     args = ap.parse_args()
+    if args.filter_search:
+        return run_filter(args)
     if args.mode == "sharded":
         return run_sharded(args)
     if args.churn:
@@ -624,6 +629,87 @@ def _read_u64(ptr):
     rc = lib.hipMemcpy(C.c_void_p(h.data_ptr()), C.c_void_p(ptr), 8, 2)  # hipMemcpyDeviceToHost
     assert rc == 0, rc
     return int(h.item())
+
+
+def filter_queries(w, q, seed=0xF11):
+    """Q topic filters from the workload's own filters: a third as stored, a third with one
+    level turned '+', a third cut to a deep prefix (at most 2 levels off) + '#' (valid
+    filters: '#' only last; shallow '#' queries would return most of the index)."""
+    rng = np.random.default_rng(seed)
+    nf = len(w.f_id)
+    pick = rng.integers(0, nf, q)
+    kind = rng.integers(0, 3, q)
+    out = []
+    for j, k in zip(pick, kind):
+        ws = bytes(w.f_bytes[w.f_off[j]:w.f_off[j + 1]]).split(b"/")
+        if ws[-1] == b"#":
+            ws = ws[:-1] or [b"a"]
+        if k == 1:
+            ws[int(rng.integers(0, len(ws)))] = b"+"
+        elif k == 2:
+            ws = ws[:int(rng.integers(max(1, len(ws) - 2), len(ws) + 1))] + [b"#"]
+        out.append(b"/".join(ws))
+    off = np.zeros(q + 1, dtype=np.uint32)
+    off[1:] = np.cumsum([len(x) for x in out])
+    return np.frombuffer(b"".join(out) + b"\0", dtype=np.uint8), off
+
+
+def run_filter(args):
+    """matches_filter/3: the seek walk over the term-ordered word-list keys,
+    one lane per query (filter_kernels.hip).  Times tm_match_filter_batch end to end (H2D
+    of the queries, count walk, scan, emit walk, D2H) after the per-epoch index build, and
+    the oracle's restatement (oracle/trie_search.cpp ALGO_FILTER) on the same queries."""
+    import oracle
+    from emqx_amd import _native as N
+    from emqx_amd import workloads
+    w = workloads.generate(args.config, scale=args.scale, n_topics=1000)
+    eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    qb, qo = filter_queries(w, args.filter_search)
+    q = len(qo) - 1
+    t0 = time.perf_counter()
+    eng.match_filter_packed(qb, qo[:2])  # first call after the commit builds the index
+    t_index = time.perf_counter() - t0
+    qo = np.ascontiguousarray(qo, dtype=np.uint32)
+    for _ in range(args.warmup):
+        eng.match_filter_view(qb, qo)
+    ts = []
+    for _ in range(max(1, min(args.steps, 20))):
+        t0 = time.perf_counter()
+        eng.match_filter_view(qb, qo)  # the C-ABI call: host result view, no Python copies
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.mean(ts))
+    o, c, k, st = eng.match_filter_packed(qb, qo)
+    total = int(c.sum())
+    # oracle on the same queries: timing (16 threads) and walk-order parity on a sample
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    t0 = time.perf_counter()
+    ix.count(qb, qo, algo=oracle.ALGO_FILTER, threads=threads)
+    dt_cpu = time.perf_counter() - t0
+    ps = min(q, 20000)
+    eo, eids, est, src = ix.match(qb, qo[:ps + 1], algo=oracle.ALGO_FILTER, with_src=True)
+    eng_ids = eng.key_ids(k[:int(o[ps - 1] + c[ps - 1])]) if ps else np.zeros(0, np.uint64)
+    bad = 0
+    for i in range(ps):
+        got = eng_ids[o[i]:o[i] + c[i]]
+        exp = w.f_id[src[eo[i]:eo[i + 1]]]
+        if not np.array_equal(got, exp):
+            bad += 1
+    print(json.dumps({
+        "metric": "matches_filter/3 topic-filter queries/s (host API, walk-order exact)",
+        "value": round(q / dt, 1), "unit": "queries/s", "n_gpus": 1,
+        "config": {"workload": f"{args.config}: {w.n_keys} route keys", "queries": q,
+                   "query_mix": "stored filters / one level '+' / deep prefix + '#', a third each"},
+        "ms_per_batch": round(dt * 1e3, 3), "keys_returned": total,
+        "index_build_ms": round(t_index * 1e3, 1),
+        "cpu_baseline": {"value": round(q / dt_cpu, 1), "unit": "queries/s", "cores": threads, "kind": "port",
+                         "sample": f"all {q} queries, oracle/trie_search.cpp ALGO_FILTER on {cpu_info()}"},
+        "parity": {"sampled_queries": ps, "mismatches": bad, "compared": "key ids in walk order"},
+    }), flush=True)
+    if bad:
+        log(f"PARITY FAILURE: {bad}/{ps} queries differ")
 
 
 def cpu_baseline(args, w, eng, tb, to, n):

@@ -335,6 +335,14 @@ class Engine:
              else np.zeros(0, dtype=np.uint32))
         return o, c, k, st
 
+    def match_filter_view(self, buf: np.ndarray, off: np.ndarray, mode: int = TM_MATCH_ALL) -> tm_result:
+        """tm_match_filter_batch without copying (engine-owned result, valid until the next
+        call).  For timing the C-ABI host path."""
+        res = tm_result()
+        self._check(self.lib.tm_match_filter_batch(self.h, buf.ctypes.data, off.ctypes.data, len(off) - 1, mode,
+                                                   C.byref(res)))
+        return res
+
     def match_filter(self, filters, mode: int = TM_MATCH_ALL):
         """List of topic filters -> list of key-handle lists in walk order (None for a
         query the engine refuses: '#' before the last level)."""

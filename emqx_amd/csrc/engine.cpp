@@ -1096,7 +1096,9 @@ struct tm_engine {
         uint32_t K = 0;
         DevBuf d_kw, d_koff, d_kh;
         DevBuf d_qw, d_qoff, d_qdollar, d_qstatus, d_cnt, d_off, d_out, d_scan;
-        std::vector<uint32_t> qw, qoff, h_off, h_cnt, h_keys, u_keys;
+        std::vector<uint32_t> qw, qoff, h_off, h_cnt, u_keys;
+        std::vector<uint32_t> wcode;     // interned word id -> order code (NONE: not cached yet)
+        PinBuf h_keys;                   // walk output (pinned: it can be GBs)
         std::vector<uint8_t> qdollar;
         std::vector<int32_t> qstatus;
     } fx;
@@ -1206,6 +1208,8 @@ struct tm_engine {
             err = std::string("matches_filter index upload: ") + hipGetErrorString(e);
             return TM_EDEVICE;
         }
+        fx.wcode.swap(wcode);
+        fx.wcode.resize(word_off.size(), NONE);
         fx.epoch = epoch;
         return TM_OK;
     }
@@ -1292,7 +1296,7 @@ void tm_destroy(tm_engine *eng) {
                       &eng->d_fr_pool, &eng->d_wave_chunks})
         b->release();
     for (PinBuf *b : {&eng->h_bytes, &eng->h_off, &eng->h_outoff, &eng->h_outcnt, &eng->h_status, &eng->h_keys,
-                      &eng->h_cursor})
+                      &eng->h_cursor, &eng->fx.h_keys})
         b->release();
     if (eng->ev_fast0) (void)hipEventDestroy(eng->ev_fast0);
     if (eng->ev_fast1) (void)hipEventDestroy(eng->ev_fast1);
@@ -1804,7 +1808,17 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
         for (size_t j = 0; j < lv.size(); j++) {
             uint32_t c = tm_engine::fx_level(t + lv[j].first, lv[j].second);
             if (c == 0 && j + 1 < lv.size()) fx.qstatus[i] = TM_BADARG;  // '#' before the last level
-            fx.qw.push_back(c != NONE ? c : eng->fx_code(t + lv[j].first, lv[j].second));
+            if (c == NONE) {  // a literal: through the interner's hash table when it knows the word
+                const uint8_t *wp = (const uint8_t *)t + lv[j].first;
+                const uint32_t wl = (uint32_t)lv[j].second, wid = eng->word_lookup(wp, wl);
+                if (wid == NONE || wid >= fx.wcode.size()) {
+                    c = eng->fx_code((const char *)wp, wl);
+                } else {
+                    if (fx.wcode[wid] == NONE) fx.wcode[wid] = eng->fx_code((const char *)wp, wl);
+                    c = fx.wcode[wid];
+                }
+            }
+            fx.qw.push_back(c);
         }
         if (fx.qw.size() >= 0xFFFFFFFFull) return TM_EINVAL;
         fx.qoff.push_back((uint32_t)fx.qw.size());
@@ -1848,19 +1862,18 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
     TM_TRY_HIP(hipMemcpyAsync(fx.h_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk count");
     const uint64_t total = fx.h_off[n];
-    fx.h_keys.resize(total);
+    TM_TRY_HIP(fx.h_keys.ensure(std::max<uint64_t>(total, 1) * 4), TM_ENOMEM, "pinned alloc");
     if (total) {
         TM_TRY_HIP(fx.d_out.ensure(total * 4), TM_ENOMEM, "alloc");
         a.out = fx.d_out.as<uint32_t>();
         TM_TRY_HIP(launch_filter_walk(a, 1, s), TM_EDEVICE, "k_filter_walk emit");
-        TM_TRY_HIP(hipMemcpyAsync(fx.h_keys.data(), fx.d_out.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-                   "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(fx.h_keys.p, fx.d_out.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
         TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk emit");
     }
     out->total = total;
     out->off = fx.h_off.data();
     out->cnt = fx.h_cnt.data();
-    out->keys = fx.h_keys.data();
+    out->keys = fx.h_keys.as<uint32_t>();
     out->status = fx.qstatus.data();
     if (mode == TM_MATCH_UNIQUE) {
         // match_add/2 into a map (:350-352): the last key per id in walk order wins;
@@ -1872,7 +1885,7 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
             best.clear();
             at.clear();
             for (uint32_t k = fx.h_off[i]; k < fx.h_off[i] + fx.h_cnt[i]; k++) {
-                const uint32_t h = fx.h_keys[k];
+                const uint32_t h = fx.h_keys.as<uint32_t>()[k];
                 const uint64_t id = eng->keys[h].id;
                 auto it = at.find(id);
                 if (it == at.end()) {

@@ -9,10 +9,10 @@
 // dictionary word 2k+3, a query word outside the dictionary 2*lower_bound+2), keys sorted by
 // (words, id).  `next({Prefix, {}})` is a lower bound; `next(Key)` is the following index.
 //
-// One lane per query: a walk is a chain of dependent probes whose length depends on the
-// query, and queries are few (the reference has no caller on the publish path).  Every
-// step either stops or moves to a strictly greater index (a seek target is greater than the
-// key it came from for queries with '#' only last; the host refuses the others), so a lane
+// One wave per query: the lanes compare 64 consecutive keys per step (the walk only jumps at
+// a seek) and search 64 probes wide.  Every step either stops or moves to a strictly greater
+// index (a seek target is greater than the key it came from for queries with '#' only last;
+// the host refuses the others, and wave_seek searches from the next key on), so a wave
 // makes at most K steps.
 #include "device_api.h"
 
@@ -38,28 +38,36 @@ __device__ inline int cmp_key_seek(const FilterArgs &a, uint32_t j, const uint32
     return L == np + 1 ? 0 : 1;
 }
 
-// next({pre ++ [w], {}}) among keys [lo, K): the first key >= the probe.  Galloping from lo
-// (seeks mostly land near the key they start from), then a binary search.
-__device__ uint32_t seek_from(const FilterArgs &a, uint32_t lo, const uint32_t *pre, uint32_t np, uint32_t w) {
-    const uint32_t K = a.K;
-    if (lo >= K || cmp_key_seek(a, lo, pre, np, w) >= 0) return lo;
-    uint32_t below = lo, hi = K;
-    for (uint64_t step = 1;; step <<= 1) {
-        const uint64_t p = (uint64_t)below + step;
-        if (p >= K) break;
-        if (cmp_key_seek(a, (uint32_t)p, pre, np, w) >= 0) {
-            hi = (uint32_t)p;
-            break;
-        }
-        below = (uint32_t)p;
-    }
-    uint32_t l = below + 1, h = hi;
+// next({pre ++ [w], {}}) among keys [lo, K): the first key >= the probe, found by the whole
+// wave.  Gallop: lane L probes lo + 2^L - 1 (lane 32 lies past any K < 2^32), which
+// brackets the answer; then 64-ary narrowing, each round probing 64 evenly spaced keys
+// (a range of K keys takes about log64(K) rounds).  Wave-uniform result.
+__device__ uint32_t wave_seek(const FilterArgs &a, uint32_t lo, const uint32_t *pre, uint32_t np, uint32_t w,
+                              uint32_t lane) {
+    const uint64_t K = a.K;
+    if (lo >= K) return (uint32_t)K;
+    const uint64_t p = lane < 33 ? (uint64_t)lo + ((1ull << lane) - 1) : ~0ull;
+    const bool ge = p >= K || cmp_key_seek(a, (uint32_t)p, pre, np, w) >= 0;
+    const uint32_t g = (uint32_t)__ffsll((long long)__ballot(ge)) - 1;  // lane 32 is always ge
+    if (g == 0) return lo;
+    // invariant: every key below l is < the probe; key h is >= it (or h == K)
+    uint64_t l = (uint64_t)lo + (1ull << (g - 1)), h = std::min<uint64_t>((uint64_t)lo + (1ull << g) - 1, K);
     while (l < h) {
-        const uint32_t m = l + (h - l) / 2;
-        if (cmp_key_seek(a, m, pre, np, w) < 0) l = m + 1;
-        else h = m;
+        const uint64_t step = (h - l + 63) / 64;
+        const uint64_t x = l + lane * step;
+        const bool xge = x >= h || cmp_key_seek(a, (uint32_t)x, pre, np, w) >= 0;
+        const uint64_t m = __ballot(xge);
+        if (!m) {
+            l = l + 63 * step + 1;
+            continue;
+        }
+        const uint32_t f = (uint32_t)__ffsll((long long)m) - 1;
+        if (f == 0) return (uint32_t)l;
+        const uint64_t hf = std::min<uint64_t>(l + f * step, h);
+        l = l + (f - 1) * step + 1;
+        h = hf;
     }
-    return l;
+    return (uint32_t)l;
 }
 
 // compare/3 with the filter-search clauses, iteratively: clause order as in the reference;
@@ -103,43 +111,64 @@ __device__ inline int cmp_filter(const uint32_t *F, uint32_t FL, const uint32_t 
     }
 }
 
-// pass 0: cnt[q] = keys the walk of query q matches; pass 1: write their handles at out_off[q]
+// One wave per query.  The walk moves to the next key after match_full / match_prefix, so
+// the 64 lanes compare keys idx .. idx+63 at once: up to the first key that compares
+// `lower` or seeks, the sequential walk visits exactly those keys in order.  FULL keys
+// before that point are emitted in order (ballot + prefix popcount); then the wave stops
+// (lower / end of table), seeks (wave_seek), or moves on by 64.
+// pass 0: cnt[q] = keys the walk matches; pass 1: write their handles at out_off[q].
 __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= a.n) return;
+    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (q >= a.n) return;  // wave-uniform
     const uint32_t qb = a.qoff[q], WL = a.qoff[q + 1] - qb;
     const uint32_t *W = a.qw + qb;
-    uint32_t c = 0;
+    const uint32_t K = a.K;
+    uint32_t c = 0;  // wave-uniform
     if (WL && a.qstatus[q] == 0) {
         // base_init/1 (:160-163): a first word <<"$", _/bytes>> starts at next({[W0], {}})
-        uint32_t idx = a.qdollar[q] ? seek_from(a, 0, nullptr, 0, W[0]) : 0;
+        uint32_t idx = a.qdollar[q] ? wave_seek(a, 0, nullptr, 0, W[0], lane) : 0;
         uint32_t *out = pass ? a.out + a.out_off[q] : nullptr;
-        while (idx < a.K) {
-            const uint32_t b = a.koff[idx];
+        const uint64_t below = (1ull << lane) - 1;
+        while (idx < K) {
+            const uint32_t j = idx + lane;
+            int r = R_LOWER;  // past the end of the table: the walk stops there
             uint32_t spos = 0, sword = 0;
-            const int r = cmp_filter(a.kw + b, a.koff[idx + 1] - b, W, WL, spos, sword);
-            if (r == R_FULL) {                   // match_add/2, then next(Cursor)
-                if (pass) out[c] = a.kh[idx];
-                c++;
-                if (a.first) break;              // return_first
-                idx++;
-            } else if (r == R_PREFIX) {
-                idx++;
-            } else if (r == R_LOWER) {
-                break;
-            } else {                             // seek/3: next({first spos words ++ [sword], {}})
-                idx = seek_from(a, idx + 1, a.kw + b, spos, sword);
+            if (j < K && j >= idx) {
+                const uint32_t b = a.koff[j];
+                r = cmp_filter(a.kw + b, a.koff[j + 1] - b, W, WL, spos, sword);
             }
+            const uint64_t stop = __ballot(r == R_LOWER || r == R_SEEK);
+            const uint32_t fs = stop ? (uint32_t)__ffsll((long long)stop) - 1 : 64;
+            const bool full = lane < fs && r == R_FULL;
+            const uint64_t fm = __ballot(full);
+            if (a.first && fm) {                 // return_first: the first key met
+                if (pass && lane == (uint32_t)__ffsll((long long)fm) - 1) out[0] = a.kh[j];
+                c = 1;
+                break;
+            }
+            if (pass && full) out[c + __popcll(fm & below)] = a.kh[j];  // match_add/2, walk order
+            c += __popcll(fm);
+            if (fs == 64) {                      // 64 x next(Cursor)
+                idx += 64;
+                continue;
+            }
+            const int rs = __shfl(r, fs);
+            const uint32_t ks = idx + fs;
+            if (rs == R_LOWER || ks >= K) break;  // lower, or '$end_of_table'
+            // seek/3: next({first spos words of key ks ++ [sword], {}})
+            const uint32_t sp = __shfl(spos, fs), sw = __shfl(sword, fs);
+            idx = wave_seek(a, ks + 1, a.kw + a.koff[ks], sp, sw, lane);
         }
     }
-    if (!pass) a.cnt[q] = c;
+    if (!pass && lane == 0) a.cnt[q] = c;
 }
 
 }  // namespace
 
 hipError_t launch_filter_walk(const FilterArgs &a, int pass, hipStream_t stream) {
     if (!a.n) return hipSuccess;
-    const uint32_t blocks = (a.n + 255) / 256;
+    const uint32_t blocks = (a.n + 3) / 4;  // 4 waves of 64 per block, one query per wave
     hipLaunchKernelGGL(k_filter_walk, dim3(blocks), dim3(256), 0, stream, a, pass);
     return hipGetLastError();
 }
