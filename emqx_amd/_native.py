@@ -56,7 +56,7 @@ EXPORTS = (
     "tm_commit_epoch", "tm_match_batch", "tm_match_device", "tm_device_sync",
     "tm_reserve_matches", "tm_key_info", "tm_key_ids", "tm_stats", "tm_debug_stats", "tm_debug_timing",
     "tm_result_ids_device", "tm_merge_shards_device", "tm_merge_shards", "tm_match_device_mode",
-    "tm_match_filter_batch",
+    "tm_match_filter_batch", "tm_intersect_batch",
 )
 # every symbol include/emqx_tm_batcher.h declares
 BATCHER_EXPORTS = (
@@ -89,6 +89,14 @@ class tm_result(C.Structure):
         ("off", C.POINTER(C.c_uint32)), ("cnt", C.POINTER(C.c_uint32)),
         ("keys", C.POINTER(C.c_uint32)), ("status", C.POINTER(C.c_int32)),
     ]
+
+
+class tm_intersect_result(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("_pad", C.c_uint32), ("off", C.POINTER(C.c_uint64)),
+                ("len", C.POINTER(C.c_int32)), ("bytes", C.POINTER(C.c_uint8))]
+
+
+TM_INTERSECT_FALSE, TM_INTERSECT_BADHASH = -1, -2
 
 
 class tm_dev_result(C.Structure):
@@ -150,6 +158,8 @@ def load() -> C.CDLL:
                                     C.c_size_t]
     lib.tm_commit_epoch.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.tm_match_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, P(tm_result)]
+    lib.tm_intersect_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                       P(tm_intersect_result)]
     lib.tm_match_filter_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, P(tm_result)]
     lib.tm_match_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64,
                                     C.c_void_p, P(tm_dev_result)]
@@ -204,6 +214,10 @@ def merge_shards(counts: np.ndarray, ids: np.ndarray):
     if rc != TM_OK:
         raise TMError(rc, "tm_merge_shards failed")
     return off, out[:total]
+
+
+class TopicInvalidHash(ValueError):
+    """error('topic_invalid_#') from emqx_topic:join/1 (emqx_topic.erl:319-320)."""
 
 
 class TMError(RuntimeError):
@@ -342,6 +356,32 @@ class Engine:
         self._check(self.lib.tm_match_filter_batch(self.h, buf.ctypes.data, off.ctypes.data, len(off) - 1, mode,
                                                    C.byref(res)))
         return res
+
+    def intersect(self, pairs):
+        """emqx_topic:intersection/2 on the GPU for each (a, b) pair (tm_intersect_batch):
+        bytes, False, or TopicInvalidHash where join/1 raises error('topic_invalid_#')."""
+        a_buf, a_off = pack_topics([p[0] for p in pairs])
+        b_buf, b_off = pack_topics([p[1] for p in pairs])
+        res = tm_intersect_result()
+        n = len(pairs)
+        self._check(self.lib.tm_intersect_batch(self.h, a_buf.ctypes.data, a_off.ctypes.data, b_buf.ctypes.data,
+                                                b_off.ctypes.data, n, C.byref(res)))
+        if n == 0:
+            return []
+        off = np.ctypeslib.as_array(res.off, shape=(n,))
+        ln = np.ctypeslib.as_array(res.len, shape=(n,))
+        cap = int(off[-1]) + max(int(ln[-1]), 0)
+        raw = bytes(np.ctypeslib.as_array(res.bytes, shape=(max(cap, 1),))) if cap else b""
+        out = []
+        for i in range(n):
+            L = int(ln[i])
+            if L == TM_INTERSECT_FALSE:
+                out.append(False)
+            elif L == TM_INTERSECT_BADHASH:
+                out.append(TopicInvalidHash())
+            else:
+                out.append(raw[int(off[i]):int(off[i]) + L])
+        return out
 
     def match_filter(self, filters, mode: int = TM_MATCH_ALL):
         """List of topic filters -> list of key-handle lists in walk order (None for a

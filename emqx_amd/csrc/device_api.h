@@ -136,6 +136,10 @@ struct FilterArgs {
     uint32_t *out;           // pass 1 out: key handles, per query in walk order
 };
 hipError_t launch_filter_walk(const FilterArgs &a, int pass, hipStream_t stream);
+// emqx_topic:intersection/2 per pair; out_len[i] = bytes, or one of:
+constexpr int32_t INTERSECT_FALSE = -1, INTERSECT_BADHASH = -2;
+hipError_t launch_intersect(const uint8_t *a, const uint32_t *a_off, const uint8_t *b, const uint32_t *b_off,
+                            uint32_t n, uint8_t *out, int32_t *out_len, hipStream_t stream);
 
 hipError_t launch_scatter1(uint8_t *dst, const uint64_t *idx, const uint8_t *src, uint64_t n, hipStream_t stream);
 hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, hipStream_t stream);

@@ -1102,6 +1102,11 @@ struct tm_engine {
         std::vector<uint8_t> qdollar;
         std::vector<int32_t> qstatus;
     } fx;
+    // intersection/2 batches (filter_kernels.hip k_intersect)
+    DevBuf d_ia, d_iaoff, d_ib, d_iboff, d_iout, d_ilen;
+    std::vector<uint64_t> ix_off;
+    std::vector<int32_t> ix_len;
+    std::vector<uint8_t> ix_bytes;
 
     static void split_words(const uint8_t *p, size_t n, std::vector<std::pair<size_t, size_t>> &out) {
         out.clear();
@@ -1286,7 +1291,8 @@ void tm_destroy(tm_engine *eng) {
                       &eng->d_dd_wl_n, &eng->d_ukeys, &eng->d_ucnt,
                       &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
-                      &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan})
+                      &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan, &eng->d_ia, &eng->d_iaoff,
+                      &eng->d_ib, &eng->d_iboff, &eng->d_iout, &eng->d_ilen})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
                       &eng->d_arena, &eng->d_scatter_idx,
@@ -1903,6 +1909,49 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
         out->total = fx.u_keys.size();
         out->keys = fx.u_keys.data();
     }
+    return TM_OK;
+}
+
+int tm_intersect_batch(tm_engine *eng, const uint8_t *a, const uint32_t *a_off, const uint8_t *b,
+                       const uint32_t *b_off, uint32_t n, tm_intersect_result *out) {
+    if (!eng || !out || (n && (!a_off || !b_off || (!a && a_off[n] > a_off[0]) || (!b && b_off[n] > b_off[0]))))
+        return TM_EINVAL;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    memset(out, 0, sizeof(*out));
+    out->n = n;
+    if (n == 0) return TM_OK;
+    const uint64_t na = (uint64_t)a_off[n] - a_off[0], nb = (uint64_t)b_off[n] - b_off[0];
+    const uint64_t cap = na + nb + n;
+    if (cap >= 0xFFFFFFFFull) return TM_EINVAL;  // out offsets are u32 on the device
+    hipStream_t s = eng->stream;
+    TM_TRY_HIP(eng->d_ia.ensure(na + 1), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_ib.ensure(nb + 1), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_iaoff.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_iboff.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_iout.ensure(cap + 1), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_ilen.ensure((size_t)n * 4), TM_ENOMEM, "alloc");
+    // offsets rebased to 0 (the kernel indexes the copies)
+    std::vector<uint32_t> ao(a_off, a_off + n + 1), bo(b_off, b_off + n + 1);
+    for (auto &v : ao) v -= a_off[0];
+    for (auto &v : bo) v -= b_off[0];
+    if (na) TM_TRY_HIP(hipMemcpyAsync(eng->d_ia.p, a + a_off[0], na, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
+    if (nb) TM_TRY_HIP(hipMemcpyAsync(eng->d_ib.p, b + b_off[0], nb, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
+    TM_TRY_HIP(hipMemcpyAsync(eng->d_iaoff.p, ao.data(), ao.size() * 4, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
+    TM_TRY_HIP(hipMemcpyAsync(eng->d_iboff.p, bo.data(), bo.size() * 4, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
+    TM_TRY_HIP(launch_intersect(eng->d_ia.as<uint8_t>(), eng->d_iaoff.as<uint32_t>(), eng->d_ib.as<uint8_t>(),
+                                eng->d_iboff.as<uint32_t>(), n, eng->d_iout.as<uint8_t>(), eng->d_ilen.as<int32_t>(), s),
+               TM_EDEVICE, "k_intersect");
+    eng->ix_len.resize(n);
+    eng->ix_bytes.resize(cap + 1);
+    TM_TRY_HIP(hipMemcpyAsync(eng->ix_len.data(), eng->d_ilen.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+               "D2H");
+    TM_TRY_HIP(hipMemcpyAsync(eng->ix_bytes.data(), eng->d_iout.p, cap, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+    TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_intersect");
+    eng->ix_off.resize(n);
+    for (uint32_t i = 0; i < n; i++) eng->ix_off[i] = (uint64_t)ao[i] + bo[i] + i;
+    out->off = eng->ix_off.data();
+    out->len = eng->ix_len.data();
+    out->bytes = eng->ix_bytes.data();
     return TM_OK;
 }
 

@@ -173,4 +173,119 @@ hipError_t launch_filter_walk(const FilterArgs &a, int pass, hipStream_t stream)
     return hipGetLastError();
 }
 
+
+// ============================================================================
+// emqx_topic:intersection/2 (apps/emqx/src/emqx_topic.erl:111-151), batched: pair i is
+// (a_i, b_i); one lane per pair walks both word lists level by level with the clauses of
+// intersect/2 in source order and writes join/1 of the result (:311-322) at
+// out[(a_off[i]-a_off[0]) + (b_off[i]-b_off[0]) + i] -- a result level is a level of a or
+// of b at the same position, so len(a) + len(b) + 1 bytes always suffice.
+// out_len[i]: bytes, INTERSECT_FALSE, or INTERSECT_BADHASH when join/1 would raise
+// error('topic_invalid_#') (a '#' before the last level; only for invalid inputs).
+namespace {
+
+struct Lvl {  // the remaining levels of one topic: the current level is [p, q), the topic ends at e
+    const uint8_t *p, *q, *e;
+    bool done;
+};
+__device__ inline void lvl_set(Lvl &l, const uint8_t *p) {
+    l.p = p;
+    l.done = p > l.e;
+    const uint8_t *q = p;
+    if (!l.done)
+        while (q < l.e && *q != '/') q++;
+    l.q = q;
+}
+__device__ inline void lvl_next(Lvl &l) { lvl_set(l, l.q + 1); }
+__device__ inline bool lvl_single(const Lvl &l) { return !l.done && l.q == l.e; }
+__device__ inline bool lvl_is(const Lvl &l, uint8_t c) { return !l.done && l.q - l.p == 1 && *l.p == c; }
+__device__ inline bool lvl_wild(const Lvl &l) { return lvl_is(l, '+') || lvl_is(l, '#'); }
+__device__ inline bool lvl_eq(const Lvl &x, const Lvl &y) {
+    if (x.q - x.p != y.q - y.p) return false;
+    for (const uint8_t *i = x.p, *j = y.p; i < x.q; i++, j++)
+        if (*i != *j) return false;
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_intersect(const uint8_t *a, const uint32_t *a_off, const uint8_t *b,
+                                                   const uint32_t *b_off, uint32_t n, uint8_t *out, int32_t *out_len) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Lvl x, y;
+    x.e = a + a_off[i + 1];
+    y.e = b + b_off[i + 1];
+    lvl_set(x, a + a_off[i]);
+    lvl_set(y, b + b_off[i]);
+    uint8_t *o0 = out + (uint64_t)(a_off[i] - a_off[0]) + (b_off[i] - b_off[0]) + i, *o = o0;
+    bool first = true;
+    auto put = [&](const uint8_t *p, const uint8_t *q) {  // append one level (or a run of levels)
+        if (!first) *o++ = '/';
+        first = false;
+        for (; p < q; p++) *o++ = *p;
+    };
+    // intersect_start/2: a '$' first word never meets a wildcard first word
+    if ((x.q > x.p && *x.p == '$' && lvl_wild(y)) || (y.q > y.p && *y.p == '$' && lvl_wild(x))) {
+        out_len[i] = INTERSECT_FALSE;
+        return;
+    }
+    int32_t res = 0;
+    for (;;) {
+        if (lvl_single(y) && lvl_is(y, '#')) {          // intersect(Words1, ['#']) -> Words1
+            if (!x.done) put(x.p, x.e);
+            break;
+        }
+        if (lvl_single(x) && lvl_is(x, '#')) {          // intersect(['#'], Words2) -> Words2
+            if (!y.done) put(y.p, y.e);
+            break;
+        }
+        if (lvl_single(x) && lvl_single(y) && lvl_is(y, '+')) {  // intersect([W1], ['+']) -> [W1]
+            put(x.p, x.q);
+            break;
+        }
+        if (lvl_single(x) && lvl_is(x, '+') && lvl_single(y)) {  // intersect(['+'], [W2]) -> [W2]
+            put(y.p, y.q);
+            break;
+        }
+        if (x.done || y.done) {                          // intersect([], []) -> []; else false
+            if (!(x.done && y.done)) res = INTERSECT_FALSE;
+            break;
+        }
+        const bool wx = lvl_wild(x), wy = lvl_wild(y);
+        if (wx && wy) {                                  // wildcard_intersection/2
+            if (lvl_eq(x, y)) put(x.p, x.q);
+            else {
+                const uint8_t plus = '+';
+                put(&plus, &plus + 1);
+            }
+        } else if (lvl_eq(x, y)) {
+            put(x.p, x.q);
+        } else if (wx) {
+            put(y.p, y.q);
+        } else if (wy) {
+            put(x.p, x.q);
+        } else {
+            res = INTERSECT_FALSE;
+            break;
+        }
+        lvl_next(x);
+        lvl_next(y);
+    }
+    if (res == 0) {
+        res = (int32_t)(o - o0);
+        // join/1 raises error('topic_invalid_#') on a '#' level before the last one
+        for (const uint8_t *p = o0; p < o; p++)
+            if (*p == '#' && (p == o0 || p[-1] == '/') && p + 1 < o && p[1] == '/') res = INTERSECT_BADHASH;
+    }
+    out_len[i] = res;
+}
+
+}  // namespace
+
+hipError_t launch_intersect(const uint8_t *a, const uint32_t *a_off, const uint8_t *b, const uint32_t *b_off,
+                            uint32_t n, uint8_t *out, int32_t *out_len, hipStream_t stream) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_intersect, dim3((n + 255) / 256), dim3(256), 0, stream, a, a_off, b, b_off, n, out, out_len);
+    return hipGetLastError();
+}
+
 }  // namespace tmx

@@ -21,6 +21,7 @@
  *   tm_match_batch (FIRST)      emqx_topic_index:match/2 (return_first) apps/emqx/src/emqx_trie_search.erl:171-178
  *   tm_match_filter_batch       emqx_topic_index:matches_filter/3 apps/emqx/src/emqx_topic_index.erl:82-84,
  *                               emqx_trie_search:matches_filter/3 apps/emqx/src/emqx_trie_search.erl:186-189
+ *   tm_intersect_batch          emqx_topic:intersection/2         apps/emqx/src/emqx_topic.erl:111-151
  *   tm_key_info                 emqx_topic_index:get_id/1, get_topic/1 apps/emqx/src/emqx_topic_index.erl:87-94
  *   tm_stats                    emqx_router:stats/1 (n_routes)    apps/emqx/src/emqx_router.erl:632-635
  *
@@ -250,6 +251,25 @@ int tm_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64
  * tm_match_filter_batch / tm_commit_epoch / tm_destroy. */
 int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
                           tm_result *out);
+
+/* emqx_topic:intersection/2 (apps/emqx/src/emqx_topic.erl:111-151), batched: pair i is
+ * (a[a_off[i] .. a_off[i+1]), b[b_off[i] .. b_off[i+1])).  Pair i's result (join/1 of the
+ * intersected words) is bytes[off[i] .. off[i]+len[i]) when len[i] >= 0; len[i] is
+ * TM_INTERSECT_FALSE for `false`, TM_INTERSECT_BADHASH where join/1 raises
+ * error('topic_invalid_#') (a '#' level before the last, only for invalid inputs).  No
+ * index involved (engine = the GPU and stream to run on; kernel k_intersect).  Result memory
+ * engine-owned until the next tm_intersect_batch / tm_destroy. */
+#define TM_INTERSECT_FALSE   (-1)
+#define TM_INTERSECT_BADHASH (-2)
+typedef struct tm_intersect_result {
+    uint32_t        n;
+    uint32_t        _pad;
+    const uint64_t *off;    /* n entries */
+    const int32_t  *len;    /* n entries */
+    const uint8_t  *bytes;
+} tm_intersect_result;
+int tm_intersect_batch(tm_engine *eng, const uint8_t *a, const uint32_t *a_off, const uint8_t *b,
+                       const uint32_t *b_off, uint32_t n, tm_intersect_result *out);
 
 /* key introspection (get_id/1, get_topic/1) */
 int tm_key_info(const tm_engine *eng, uint32_t key, uint64_t *id, uint32_t *flags,

@@ -1,4 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_s.log 2>&1 && tail -3 gpurun_out/pytest_gpu_s.log && \
-timeout -k 10 400 python -u bench.py > gpurun_out/bench_s.json 2> gpurun_out/bench_s.err && cat gpurun_out/bench_s.json | head -c 600
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_u.log 2>&1
+rc=$?; tail -n 3 gpurun_out/pytest_gpu_u.log; grep -E "FAILED|Error" gpurun_out/pytest_gpu_u.log | head -20; exit $rc
