@@ -153,6 +153,43 @@ int main() {
                 CHECK(found);
             }
         }
+        // matches_filter/3 on filters made from the topics (last level -> '#', and a few
+        // refused ones with '#' before the last level); modes checked against ALL
+        {
+            std::string fb;
+            std::vector<uint32_t> fo{0};
+            for (uint32_t i = 0; i < n; i++) {
+                std::string t = bytes.substr(off[i], off[i + 1] - off[i]);
+                if (i % 3 == 1) t = t.substr(0, t.rfind('/') == std::string::npos ? 0 : t.rfind('/') + 1) + "#";
+                if (i % 97 == 5) t = "#/" + t;
+                fb += t;
+                fo.push_back((uint32_t)fb.size());
+            }
+            tm_result fa, fr;
+            CHECK(tm_match_filter_batch(eng, (const uint8_t *)fb.data(), fo.data(), n, TM_MATCH_ALL, &fa) == TM_OK);
+            std::vector<uint32_t> fcnt(fa.cnt, fa.cnt + n), foff(fa.off, fa.off + n), fkeys(fa.keys, fa.keys + fa.total);
+            for (uint32_t i = 0; i < n; i++) CHECK((fa.status[i] == TM_BADARG) == (i % 97 == 5) && foff[i] + fcnt[i] <= fa.total);
+            CHECK(tm_match_filter_batch(eng, (const uint8_t *)fb.data(), fo.data(), n, TM_MATCH_FIRST, &fr) == TM_OK);
+            for (uint32_t i = 0; i < n; i++)
+                CHECK(fr.cnt[i] == (fcnt[i] ? 1u : 0u) && (!fr.cnt[i] || fr.keys[fr.off[i]] == fkeys[foff[i]]));
+            CHECK(tm_match_filter_batch(eng, (const uint8_t *)fb.data(), fo.data(), n, TM_MATCH_UNIQUE, &fr) == TM_OK);
+            for (uint32_t i = 0; i < n; i++) {
+                std::vector<uint64_t> uid(fr.cnt[i]), aid(fcnt[i]);
+                CHECK(tm_key_ids(eng, fr.keys + fr.off[i], fr.cnt[i], uid.data()) == TM_OK);
+                CHECK(tm_key_ids(eng, fkeys.data() + foff[i], fcnt[i], aid.data()) == TM_OK);
+                std::sort(aid.begin(), aid.end());
+                aid.erase(std::unique(aid.begin(), aid.end()), aid.end());
+                CHECK(uid == aid);  // listed by id
+            }
+            // intersection/2 of neighbouring filters
+            tm_intersect_result ir;
+            CHECK(tm_intersect_batch(eng, (const uint8_t *)fb.data(), fo.data(), (const uint8_t *)fb.data(),
+                                     fo.data() + 1, n - 1, &ir) == TM_OK);
+            for (uint32_t i = 0; i + 1 < n; i++) {
+                CHECK(ir.len[i] >= TM_INTERSECT_BADHASH);
+                CHECK(ir.len[i] < 0 || (uint64_t)ir.len[i] <= (uint64_t)(fo[i + 1] - fo[i]) + (fo[i + 2] - fo[i + 1]));
+            }
+        }
         // introspection of every matched key
         for (uint32_t k : akeys) {
             uint64_t id = 0;
