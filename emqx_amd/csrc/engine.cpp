@@ -1867,7 +1867,14 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
                "D2H");
     TM_TRY_HIP(hipMemcpyAsync(fx.h_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk count");
-    const uint64_t total = fx.h_off[n];
+    // the device scan is u32: a batch whose walks return 4 Gi keys or more is refused
+    // before the emit pass could write past its offsets
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) total += fx.h_cnt[i];
+    if (total >= 0xFFFFFFFFull) {
+        eng->err = "tm_match_filter_batch: the batch returns 4 Gi keys or more; split it";
+        return TM_ENOMEM;
+    }
     TM_TRY_HIP(fx.h_keys.ensure(std::max<uint64_t>(total, 1) * 4), TM_ENOMEM, "pinned alloc");
     if (total) {
         TM_TRY_HIP(fx.d_out.ensure(total * 4), TM_ENOMEM, "alloc");
