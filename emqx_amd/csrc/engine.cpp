@@ -28,6 +28,7 @@
 
 #include "../../include/emqx_tm.h"
 #include "device_api.h"
+#include "filter_api.h"
 #include "layout.h"
 
 using namespace tmx;

@@ -1,0 +1,35 @@
+// filter_api.h — private interface between the host engine (engine.cpp) and the
+// matches_filter/3 and intersection/2 kernels (filter_kernels.hip).  Not part of the C-ABI.
+// Kept apart from device_api.h so the match kernels' sources (and the hash that ties their
+// PMC profiles to them, bench.py kernel_src_sha) do not change with these.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tmx {
+
+// filter_kernels.hip ---------------------------------------------------------
+// matches_filter/3 over the term-ordered word-list keys (engine.cpp FilterIndex).
+struct FilterArgs {
+    const uint32_t *kw;    // order codes of every key's words, keys back to back
+    const uint32_t *koff;  // K+1: key j's words are kw[koff[j] .. koff[j+1])
+    const uint32_t *kh;    // K: key handle of sorted key j
+    uint32_t K;
+    uint32_t n;            // queries
+    const uint32_t *qw;    // order codes of the query words
+    const uint32_t *qoff;  // n+1
+    const uint8_t *qdollar;  // 1: the first query word starts with '$' (base_init/1)
+    const int32_t *qstatus;  // 0: walk; else skipped (count 0)
+    uint32_t first;          // return_first: stop at the first hit
+    uint32_t *cnt;           // pass 0 out: n
+    const uint32_t *out_off; // pass 1 in: n (exclusive scan of cnt)
+    uint32_t *out;           // pass 1 out: key handles, per query in walk order
+};
+hipError_t launch_filter_walk(const FilterArgs &a, int pass, hipStream_t stream);
+// emqx_topic:intersection/2 per pair; out_len[i] = bytes, or one of:
+constexpr int32_t INTERSECT_FALSE = -1, INTERSECT_BADHASH = -2;
+hipError_t launch_intersect(const uint8_t *a, const uint32_t *a_off, const uint8_t *b, const uint32_t *b_off,
+                            uint32_t n, uint8_t *out, int32_t *out_len, hipStream_t stream);
+
+
+}  // namespace tmx

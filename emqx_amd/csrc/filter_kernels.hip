@@ -14,7 +14,9 @@
 // index (a seek target is greater than the key it came from for queries with '#' only last;
 // the host refuses the others, and wave_seek searches from the next key on), so a wave
 // makes at most K steps.
-#include "device_api.h"
+#include <algorithm>
+
+#include "filter_api.h"
 
 namespace tmx {
 
