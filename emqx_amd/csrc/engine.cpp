@@ -1177,7 +1177,7 @@ struct tm_engine {
             }
             off[i + 1] = code.size();
         }
-        if (code.size() >= 0xFFFFFFFFull) {
+        if (code.size() + 8 >= 0xFFFFFFFFull) {
             err = "matches_filter index: more than 4 Gi key words";
             return TM_ENOMEM;
         }
@@ -1193,13 +1193,14 @@ struct tm_engine {
             return keys[lk[a]].id < keys[lk[b]].id;
         });
         std::vector<uint32_t> kw, koff(lk.size() + 1, 0), kh(lk.size());
-        kw.reserve(code.size());
+        kw.reserve(code.size() + 8);
         for (size_t j = 0; j < perm.size(); j++) {
             const uint32_t i = perm[j];
             kw.insert(kw.end(), code.begin() + off[i], code.begin() + off[i + 1]);
             koff[j + 1] = (uint32_t)kw.size();
             kh[j] = lk[i];
         }
+        kw.insert(kw.end(), 8, 0u);  // k_filter_walk preloads 8 words of a key unconditionally
         fx.K = (uint32_t)lk.size();
         hipError_t e;
         if ((e = fx.d_kw.ensure(std::max<size_t>(kw.size(), 1) * 4)) != hipSuccess ||
@@ -1832,6 +1833,7 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
         fx.qdollar[i] = tl && t[0] == '$';
     }
     hipStream_t s = eng->stream;
+    fx.qw.insert(fx.qw.end(), 8, 0u);  // k_filter_walk preloads 8 words of a query unconditionally
     const size_t nq = fx.qw.size();
     TM_TRY_HIP(fx.d_qw.ensure(std::max<size_t>(nq, 1) * 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(fx.d_qoff.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "alloc");

@@ -72,46 +72,60 @@ __device__ uint32_t wave_seek(const FilterArgs &a, uint32_t lo, const uint32_t *
     return (uint32_t)l;
 }
 
-// compare/3 with the filter-search clauses, iteratively: clause order as in the reference;
-// a filter '+' facing a query word is the last backtrack point, a query '+' passes the
-// deeper result through unchanged.
-__device__ inline int cmp_filter(const uint32_t *F, uint32_t FL, const uint32_t *W, uint32_t WL, uint32_t &spos,
-                                 uint32_t &sword) {
-    int last_plus = -1;
-    for (uint32_t pos = 0;; pos++) {
-        const bool fin = pos == FL, win = pos == WL;
-        if (fin) return win ? R_FULL : R_PREFIX;                      // compare([], [], _) / ([], _, _)
-        const uint32_t f = F[pos];
-        if (FL - pos == 1 && f == C_HASH) return R_FULL;               // compare(['#'], _, _)
-        if (win) {                                                     // compare([_|_], [], _): lower
-            if (last_plus >= 0) {
-                spos = (uint32_t)last_plus;
-                sword = W[last_plus];
-                return R_SEEK;
-            }
-            return R_LOWER;
-        }
-        const uint32_t w = W[pos];
-        if (WL - pos == 1 && w == C_HASH) return R_FULL;               // compare(_, ['#'], _)
-        if (w == C_PLUS) continue;                                     // compare([_|TF], ['+'|TW], Pos)
-        if (f == C_PLUS) {                                             // compare(['+'|TF], [HW|TW], Pos)
-            last_plus = (int)pos;
-            continue;
-        }
-        if (f == w) continue;                                          // compare([HW|TF], [HW|TW], Pos)
-        if (f > w) {                                                   // HF > HW: lower
-            if (last_plus >= 0) {
-                spos = (uint32_t)last_plus;
-                sword = W[last_plus];
-                return R_SEEK;
-            }
-            return R_LOWER;
-        }
-        spos = pos;                                                    // {Pos, HW}
-        sword = w;
-        return R_SEEK;
+// One position of compare/3 with the filter-search clauses, in the reference's clause
+// order; falls through to the next position.  A filter '+' facing a query word is the last
+// backtrack point (lp, with its query word lpw); a query '+' passes the deeper result
+// through unchanged.  F_ / W_ are evaluated only once the position exists.
+#define CMP_STEP(POS, F_, W_)                                                                  \
+    {                                                                                          \
+        const uint32_t pos_ = (POS);                                                           \
+        if (pos_ == FL) return pos_ == WL ? R_FULL : R_PREFIX; /* ([], [], _) / ([], _, _) */  \
+        const uint32_t f_ = (F_);                                                              \
+        if (FL - pos_ == 1 && f_ == C_HASH) return R_FULL; /* (['#'], _, _) */                 \
+        if (pos_ == WL) { /* ([_|_], [], _): lower */                                         \
+            if (lp >= 0) {                                                                     \
+                spos = (uint32_t)lp;                                                           \
+                sword = lpw;                                                                   \
+                return R_SEEK;                                                                 \
+            }                                                                                  \
+            return R_LOWER;                                                                    \
+        }                                                                                      \
+        const uint32_t w_ = (W_);                                                              \
+        if (WL - pos_ == 1 && w_ == C_HASH) return R_FULL; /* (_, ['#'], _) */                 \
+        if (w_ != C_PLUS) { /* ([_|TF], ['+'|TW], Pos) continues */                            \
+            if (f_ == C_PLUS) { /* (['+'|TF], [HW|TW], Pos) */                                 \
+                lp = (int)pos_;                                                                \
+                lpw = w_;                                                                      \
+            } else if (f_ != w_) { /* ([HW|TF], [HW|TW], Pos) continues */                     \
+                if (f_ > w_) { /* HF > HW: lower */                                            \
+                    if (lp >= 0) {                                                             \
+                        spos = (uint32_t)lp;                                                   \
+                        sword = lpw;                                                           \
+                        return R_SEEK;                                                         \
+                    }                                                                          \
+                    return R_LOWER;                                                            \
+                }                                                                              \
+                spos = pos_; /* {Pos, HW} */                                                   \
+                sword = w_;                                                                    \
+                return R_SEEK;                                                                 \
+            }                                                                                  \
+        }                                                                                      \
     }
+
+// compare/3 for a filter search.  The first 8 words of the key (fr) and of the query (wr)
+// come preloaded in registers and the first 8 positions are unrolled (static indices keep
+// them in registers), so a compare is not a chain of dependent loads.
+__device__ __attribute__((always_inline)) inline int cmp_filter(const uint32_t (&fr)[8], const uint32_t *F,
+                                                                uint32_t FL, const uint32_t (&wr)[8],
+                                                                const uint32_t *W, uint32_t WL, uint32_t &spos,
+                                                                uint32_t &sword) {
+    int lp = -1;
+    uint32_t lpw = 0;
+#pragma unroll
+    for (uint32_t p = 0; p < 8; p++) CMP_STEP(p, fr[p], wr[p])
+    for (uint32_t p = 8;; p++) CMP_STEP(p, F[p], W[p])
 }
+#undef CMP_STEP
 
 // One wave per query.  The walk moves to the next key after match_full / match_prefix, so
 // the 64 lanes compare keys idx .. idx+63 at once: up to the first key that compares
@@ -132,13 +146,19 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
         uint32_t idx = a.qdollar[q] ? wave_seek(a, 0, nullptr, 0, W[0], lane) : 0;
         uint32_t *out = pass ? a.out + a.out_off[q] : nullptr;
         const uint64_t below = (1ull << lane) - 1;
+        uint32_t wr[8];  // the query's first 8 words (qw is padded by 8 words on the device)
+#pragma unroll
+        for (int i = 0; i < 8; i++) wr[i] = W[i];
         while (idx < K) {
             const uint32_t j = idx + lane;
             int r = R_LOWER;  // past the end of the table: the walk stops there
             uint32_t spos = 0, sword = 0;
             if (j < K && j >= idx) {
                 const uint32_t b = a.koff[j];
-                r = cmp_filter(a.kw + b, a.koff[j + 1] - b, W, WL, spos, sword);
+                uint32_t fr[8];  // independent loads (kw is padded by 8 words on the device)
+#pragma unroll
+                for (int i = 0; i < 8; i++) fr[i] = a.kw[b + i];
+                r = cmp_filter(fr, a.kw + b, a.koff[j + 1] - b, wr, W, WL, spos, sword);
             }
             const uint64_t stop = __ballot(r == R_LOWER || r == R_SEEK);
             const uint32_t fs = stop ? (uint32_t)__ffsll((long long)stop) - 1 : 64;
