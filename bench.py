@@ -366,6 +366,8 @@ def main():
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile:
         cpu, parity = cpu_baseline(args, w, eng, tb, to, n)
+    # the rest of the index API on the same engine, off the headline metric
+    filt = filter_leg(args, w, eng, 20000) if rank == 0 and not args.profile else None
 
     if rank == 0:
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
@@ -415,6 +417,7 @@ def main():
             "host_path": host_path,
             "batcher": batcher,
             "other_modes": mode_rates,
+            "matches_filter": filt,
             "cpu_baseline": cpu,
             "parity": parity,
             "spill_topics": int(slow_topics),
@@ -631,6 +634,18 @@ def _read_u64(ptr):
     return int(h.item())
 
 
+_ORACLE_IX = {}
+
+
+def oracle_index(w):
+    """The oracle's ordered key set for workload w, built once per run (checker / CPU
+    baseline only)."""
+    import oracle
+    if id(w) not in _ORACLE_IX:
+        _ORACLE_IX[id(w)] = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    return _ORACLE_IX[id(w)]
+
+
 def filter_queries(w, q, seed=0xF11):
     """Q topic filters from the workload's own filters: a third as stored, a third with one
     level turned '+', a third cut to a deep prefix (at most 2 levels off) + '#' (valid
@@ -654,24 +669,18 @@ def filter_queries(w, q, seed=0xF11):
     return np.frombuffer(b"".join(out) + b"\0", dtype=np.uint8), off
 
 
-def run_filter(args):
-    """matches_filter/3: the seek walk over the term-ordered word-list keys,
-    one lane per query (filter_kernels.hip).  Times tm_match_filter_batch end to end (H2D
-    of the queries, count walk, scan, emit walk, D2H) after the per-epoch index build, and
-    the oracle's restatement (oracle/trie_search.cpp ALGO_FILTER) on the same queries."""
+def filter_leg(args, w, eng, q):
+    """matches_filter/3 on the loaded engine: q topic-filter queries made from
+    the workload's filters, walked on the GPU (filter_kernels.hip) through
+    tm_match_filter_batch end to end (H2D of the queries, count walk, scan, emit walk, D2H)
+    after the per-epoch index build; the oracle's restatement (oracle/trie_search.cpp
+    ALGO_FILTER) timed on the same queries; walk order compared on a sample."""
     import oracle
-    from emqx_amd import _native as N
-    from emqx_amd import workloads
-    w = workloads.generate(args.config, scale=args.scale, n_topics=1000)
-    eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
-    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
-    eng.commit()
-    qb, qo = filter_queries(w, args.filter_search)
-    q = len(qo) - 1
-    t0 = time.perf_counter()
-    eng.match_filter_packed(qb, qo[:2])  # first call after the commit builds the index
-    t_index = time.perf_counter() - t0
+    qb, qo = filter_queries(w, q)
     qo = np.ascontiguousarray(qo, dtype=np.uint32)
+    t0 = time.perf_counter()
+    eng.match_filter_view(qb, qo[:2])  # first call after the commit builds the index
+    t_index = time.perf_counter() - t0
     for _ in range(args.warmup):
         eng.match_filter_view(qb, qo)
     ts = []
@@ -682,9 +691,8 @@ def run_filter(args):
     dt = float(np.mean(ts))
     o, c, k, st = eng.match_filter_packed(qb, qo)
     total = int(c.sum())
-    # oracle on the same queries: timing (16 threads) and walk-order parity on a sample
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    ix = oracle_index(w)
     t0 = time.perf_counter()
     ix.count(qb, qo, algo=oracle.ALGO_FILTER, threads=threads)
     dt_cpu = time.perf_counter() - t0
@@ -693,23 +701,38 @@ def run_filter(args):
     eng_ids = eng.key_ids(k[:int(o[ps - 1] + c[ps - 1])]) if ps else np.zeros(0, np.uint64)
     bad = 0
     for i in range(ps):
-        got = eng_ids[o[i]:o[i] + c[i]]
-        exp = w.f_id[src[eo[i]:eo[i + 1]]]
-        if not np.array_equal(got, exp):
+        if not np.array_equal(eng_ids[o[i]:o[i] + c[i]], w.f_id[src[eo[i]:eo[i + 1]]]):
             bad += 1
-    print(json.dumps({
-        "metric": "matches_filter/3 topic-filter queries/s (host API, walk-order exact)",
-        "value": round(q / dt, 1), "unit": "queries/s", "n_gpus": 1,
-        "config": {"workload": f"{args.config}: {w.n_keys} route keys", "queries": q,
-                   "query_mix": "stored filters / one level '+' / deep prefix + '#', a third each"},
-        "ms_per_batch": round(dt * 1e3, 3), "keys_returned": total,
+    if bad:
+        log(f"PARITY FAILURE (matches_filter): {bad}/{ps} queries differ")
+    return {
+        "api": "tm_match_filter_batch (matches_filter/3)", "queries": q,
+        "query_mix": "stored filters / one level '+' / deep prefix + '#', a third each",
+        "queries_per_s": round(q / dt, 1), "ms_per_batch": round(dt * 1e3, 3), "keys_returned": total,
         "index_build_ms": round(t_index * 1e3, 1),
         "cpu_baseline": {"value": round(q / dt_cpu, 1), "unit": "queries/s", "cores": threads, "kind": "port",
-                         "sample": f"all {q} queries, oracle/trie_search.cpp ALGO_FILTER on {cpu_info()}"},
+                         "sample": f"all {q} queries, oracle/trie_search.cpp ALGO_FILTER, counts only"},
         "parity": {"sampled_queries": ps, "mismatches": bad, "compared": "key ids in walk order"},
+    }
+
+
+def run_filter(args):
+    """--filter-search Q: the matches_filter/3 leg alone, as its own JSON line."""
+    from emqx_amd import _native as N
+    from emqx_amd import workloads
+    w = workloads.generate(args.config, scale=args.scale, n_topics=1000)
+    eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    r = filter_leg(args, w, eng, args.filter_search)
+    print(json.dumps({
+        "metric": "matches_filter/3 topic-filter queries/s (host API, walk-order exact)",
+        "value": r["queries_per_s"], "unit": "queries/s", "n_gpus": 1,
+        "config": {"workload": f"{args.config}: {w.n_keys} route keys", "queries": r["queries"],
+                   "query_mix": r["query_mix"]},
+        "ms_per_batch": r["ms_per_batch"], "keys_returned": r["keys_returned"],
+        "index_build_ms": r["index_build_ms"], "cpu_baseline": r["cpu_baseline"], "parity": r["parity"],
     }), flush=True)
-    if bad:
-        log(f"PARITY FAILURE: {bad}/{ps} queries differ")
 
 
 def cpu_baseline(args, w, eng, tb, to, n):
@@ -719,7 +742,7 @@ def cpu_baseline(args, w, eng, tb, to, n):
     from emqx_amd import _native as N
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
     t0 = time.time()
-    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    ix = oracle_index(w)
     t_build = time.time() - t0
     # calibrate: rate on a small slice, then size the sample for ~cpu_seconds
     cal = 2000
