@@ -368,6 +368,7 @@ def main():
         cpu, parity = cpu_baseline(args, w, eng, tb, to, n)
     # the rest of the index API on the same engine, off the headline metric
     filt = filter_leg(args, w, eng, 20000) if rank == 0 and not args.profile else None
+    inter = intersect_leg(w, tb, to) if rank == 0 and not args.profile else None
 
     if rank == 0:
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
@@ -418,6 +419,7 @@ def main():
             "batcher": batcher,
             "other_modes": mode_rates,
             "matches_filter": filt,
+            "intersection": inter,
             "cpu_baseline": cpu,
             "parity": parity,
             "spill_topics": int(slow_topics),
@@ -714,6 +716,64 @@ def filter_leg(args, w, eng, q):
                          "sample": f"all {q} queries, oracle/trie_search.cpp ALGO_FILTER, counts only"},
         "parity": {"sampled_queries": ps, "mismatches": bad, "compared": "key ids in walk order"},
     }
+
+
+def intersect_leg(w, tb, to, n_pairs=1_000_000, cpu_pairs=50_000):
+    """emqx_topic:intersection/2 batched on the GPU (tm_intersect_batch,
+    k_intersect): n_pairs (filter, generalised filter or topic) pairs from the workload, end to end
+    through the C-ABI; the oracle's Python restatement on cpu_pairs of them, results
+    compared."""
+    from oracle import emqx_topic as et
+    from emqx_amd import _native as N
+    rng = np.random.default_rng(0x1A7)
+    nf, nt = len(w.f_id), len(to) - 1
+    fi = rng.integers(0, nf, n_pairs)
+    ti = rng.integers(0, nt, n_pairs)
+    use_f = rng.random(n_pairs) < 0.5
+    fbytes = [bytes(w.f_bytes[w.f_off[j]:w.f_off[j + 1]]) for j in fi]
+    cut = rng.integers(0, 1 << 30, n_pairs)
+
+    def variant(f, r):  # the same filter generalised: one level '+', or a prefix + '#'
+        ws = f.split(b"/")
+        if r & 1:
+            ws[(r >> 1) % len(ws)] = b"+"
+        else:
+            ws = ws[:(r >> 1) % len(ws)] + [b"#"]
+        return b"/".join(ws)
+
+    # half the pairs: a filter and a variant of it (mostly intersecting); half: a filter
+    # and a topic of the batch
+    other = [variant(f, int(r)) if u else bytes(tb[to[k]:to[k + 1]])
+             for f, r, k, u in zip(fbytes, cut, ti, use_f)]
+    pairs = list(zip(fbytes, other))
+    eng = N.Engine(0)
+    eng.intersect(pairs[:1000])
+    a_buf, a_off = N.pack_topics([p[0] for p in pairs])
+    b_buf, b_off = N.pack_topics([p[1] for p in pairs])
+    res = N.tm_intersect_result()
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        eng._check(eng.lib.tm_intersect_batch(eng.h, a_buf.ctypes.data, a_off.ctypes.data, b_buf.ctypes.data,
+                                              b_off.ctypes.data, n_pairs, N.C.byref(res)))
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.mean(ts))
+    got = eng.intersect(pairs[:cpu_pairs])
+    t0 = time.perf_counter()
+    exp = []
+    for a, b in pairs[:cpu_pairs]:
+        try:
+            exp.append(et.intersection(a, b))
+        except et.TopicError:
+            exp.append("badhash")
+    dt_cpu = time.perf_counter() - t0
+    bad = sum(1 for g, e in zip(got, exp) if (("badhash" if isinstance(g, N.TopicInvalidHash) else g) != e))
+    eng.close()
+    return {"api": "tm_intersect_batch (intersection/2)", "pairs": n_pairs, "pairs_per_s": round(n_pairs / dt, 1),
+            "ms_per_batch": round(dt * 1e3, 3), "non_false": int(sum(1 for g in got if g is not False)),
+            "cpu_baseline": {"value": round(cpu_pairs / dt_cpu, 1), "unit": "pairs/s", "cores": 1, "kind": "port",
+                             "sample": f"{cpu_pairs} pairs, oracle/emqx_topic.py (Python)"},
+            "parity": {"sampled_pairs": cpu_pairs, "mismatches": bad}}
 
 
 def run_filter(args):
