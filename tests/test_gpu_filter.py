@@ -179,3 +179,33 @@ def test_topic_index_matches_filter_order():
         assert got == exp, q
     with pytest.raises(ValueError):
         tab.matches_filter(b"#/a")
+
+
+def test_filter_walk_config_e_scaled():
+    """Config E (scaled): $SYS topics, root '#', '+/...' and $share duplicates (same filter,
+    several dests); queries include '$SYS/...' ones (base_init starts at [W0])."""
+    w = workloads.generate("E", scale=0.2, n_topics=2000)
+    filters = w.filters()
+    ids = [int(x) for x in w.f_id]
+    rng = random.Random(0xE5)
+    queries = []
+    for f in rng.sample(filters, 1500):
+        ws = f.split(b"/")
+        r = rng.random()
+        if r < 0.3:
+            ws[rng.randrange(len(ws))] = b"+"
+        elif r < 0.6:
+            if ws[-1] == b"#":
+                ws = ws[:-1] or [b"x"]
+            ws = ws[:rng.randint(1, len(ws))] + [b"#"]
+        queries.append(b"/".join(ws))
+    queries += [t for t in w.topics()[:500] if t.startswith(b"$SYS")][:100]
+    queries += [b"$SYS/#", b"$SYS/+/+/#", b"#", b"+/#"]
+    eng = N.Engine(0)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    got = _engine_walks(eng, queries)
+    exp, st = _oracle_walks(filters, ids, [0] * len(filters), queries)
+    assert not st.any()
+    bad = [q for q, g, e in zip(queries, got, exp) if g != e]
+    assert not bad, bad[:5]
