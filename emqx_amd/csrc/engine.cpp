@@ -1177,8 +1177,8 @@ struct tm_engine {
             }
             off[i + 1] = code.size();
         }
-        if (code.size() + 8 >= 0xFFFFFFFFull) {
-            err = "matches_filter index: more than 4 Gi key words";
+        if (code.size() + 8 >= 0xFFFFFFFFull || lk.size() >= 0xFFFFFF00ull) {
+            err = "matches_filter index: more than 4 Gi key words or keys";
             return TM_ENOMEM;
         }
         // ETS term order: words (codes) lexicographically, a prefix first; then the id
