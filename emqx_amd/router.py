@@ -17,7 +17,7 @@ from __future__ import annotations
 from collections import OrderedDict
 
 from . import _native as N
-from .topic import filter_words, wildcard
+from .topic import Share, parse
 
 
 class Router:
@@ -89,6 +89,24 @@ class Router:
                 raise ValueError(action)
         self.commit()
         return {}
+
+    def subscribe(self, topic_filter, node=None):
+        """The route a subscription adds (emqx_topic:parse/1, emqx_topic.erl:324-365):
+        `$share/G/F` and `$queue/F` become route (F, {G, Node}) (emqx_shared_sub.erl:450,
+        group <<"$queue">> for $queue), anything else (F, Node) (emqx_broker.erl:719)."""
+        f, dest = self._sub_route(topic_filter, node)
+        return self.do_add_route(f, dest)
+
+    def unsubscribe(self, topic_filter, node=None):
+        f, dest = self._sub_route(topic_filter, node)
+        return self.do_delete_route(f, dest)
+
+    def _sub_route(self, topic_filter, node):
+        node = self.node if node is None else node
+        tf, _ = parse(topic_filter)
+        if isinstance(tf, Share):
+            return tf.topic, (tf.group.decode(), node)
+        return tf, node
 
     def commit(self):
         if self._dirty:

@@ -42,6 +42,13 @@ def wildcard(words_or_topic) -> bool:
     return any(w in (PLUS, HASH) for w in ws)
 
 
+def filter(topic):  # noqa: A001 - the reference's name
+    """emqx_trie_search:filter/1 (emqx_trie_search.erl:136-140): the word list of a
+    wildcard filter, False for a filter without '+'/'#' (make_key/2 keeps those binary)."""
+    ws = filter_words(topic)
+    return ws if wildcard(ws) else False
+
+
 def join(words) -> bytes:
     """emqx_topic:join/1 (emqx_topic.erl:310-322) for word lists."""
     parts = []

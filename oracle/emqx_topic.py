@@ -73,6 +73,14 @@ def wildcard(t) -> bool:
     return False
 
 
+def trie_filter(topic: bytes):
+    """emqx_trie_search:filter/1 + filter_words/1 (emqx_trie_search.erl:136-140,358-366):
+    '+'/'#' become atoms, every other level (the empty one included) stays a binary;
+    False when no level is a wildcard."""
+    ws = ["+" if w == b"+" else "#" if w == b"#" else w for w in tokens(topic)]
+    return ws if wildcard(ws) else False
+
+
 def _match_words(n: list, f: list) -> bool:
     i = 0
     while True:

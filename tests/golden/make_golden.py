@@ -103,10 +103,25 @@ TOPIC_MISC = {
              ["@words:ab/+/#", "ab/+/#"],
              [[{"atom": "+"}, "a", {"atom": "#"}, "b", {"atom": ""}, {"atom": "+"}], {"error": "topic_invalid_#"}],
              [[{"atom": "+"}, "c", "#", "d", {"atom": ""}, {"atom": "+"}], {"error": "topic_invalid_#"}]],
-    # t_intersect :132-187 (first block)
-    "intersection": [["t/global/#", "t/+/1/+", "t/global/1/+"], ["t/global/#", "#", "t/global/#"],
-                     ["t/global/#", "t/global/#", "t/global/#"], ["$SYS/broker", "$SYS/+", "$SYS/broker"],
-                     ["$SYS/broker", "+/+", False], ["$SYS/broker", "#", False]],
+    # emqx_topic_SUITE intersection KATs, every assertion; t_intersect_commutes :148-181 is
+    # the argument swap, checked for every row by the tests
+    "intersection": [
+        # t_intersect :132-139
+        ["t/global/#", "t/+/1/+", "t/global/1/+"], ["t/global/#", "#", "t/global/#"],
+        ["t/global/#", "t/global/#", "t/global/#"], ["1/+/3/+/5/#", "+/2/+/4/+", "1/2/3/4/5"],
+        ["t/local/1/#", "t/local/+", "t/local/1"], ["t/global/#", "t/local/+", False],
+        ["t/local/1/+", "t/local/+", False],
+        # t_intersect_topic_wildcard :141-147
+        ["t/test/#", "t/test/1", "t/test/1"], ["t/test/1/1", "t/test/#", "t/test/1/1"],
+        ["t/test/1/1", "t/test/+", False], ["t/test/1/1", "t/test/1/1", "t/test/1/1"],
+        ["t/test/1", "t/test/2", False], ["t/test/1", "t/test/1/2", False],
+        # t_sys_intersect :183-187
+        ["$SYS/broker/#", "$SYS/+/+", "$SYS/broker/+"], ["$SYS/broker", "$SYS/+", "$SYS/broker"],
+        ["$SYS/broker", "+/+", False], ["$SYS/broker", "#", False]],
+    # emqx_trie_search_tests:filter_test_ :23-33 — filter/1: the key words of a wildcard
+    # filter (empty level stays <<>>), false for a filter without wildcards
+    "filter": [["sensor/+/metric//#", ["sensor", {"atom": "+"}, "metric", "", {"atom": "#"}]],
+               ["sensor/1/metric//42", False]],
     # t_prepend :240-245
     "prepend": [[None, "ab", "ab"], ["", "a/b", "a/b"], ["x/", "a/b", "x/a/b"], ["x/y", "a/b", "x/y/a/b"],
                 [{"atom": "+"}, "a/b", "+/a/b"]],
@@ -229,6 +244,12 @@ ROUTER_CASES = [
     {"name": "t_add_delete :80-86 (topics)", "steps": [
         ["add", "a/b/c", "node"], ["add", "a/b/c", "node"], ["add", "a/+/b", "node"],
         ["topics", ["a/+/b", "a/b/c"]], ["del", "a/b/c", "node"], ["del", "a/+/b", "node"], ["topics", []]]},
+    # t_queue_subscription :1120-1137: $queue/t/1 and $share/aa/t/1 are two routes on t/1
+    # (groups '$queue' and 'aa', emqx_topic:parse/1 :342-354; emqx_shared_sub.erl:450)
+    {"name": "emqx_shared_sub_SUITE t_queue_subscription :1120-1137", "steps": [
+        ["sub", "$queue/t/1", "node"], ["sub", "$share/aa/t/1", "node"],
+        ["count", "t/1", 2],
+        ["match", "t/1", [["t/1", ["$queue", "node"]], ["t/1", ["aa", "node"]]]]]},
     {"name": "emqx_shared_sub_SUITE two groups :1017-1052", "steps": [
         ["add", "t/1", ["g1", "node"]], ["add", "t/1", ["g2", "node"]],
         ["match", "t/1", [["t/1", ["g1", "node"]], ["t/1", ["g2", "node"]]]]]},

@@ -102,6 +102,68 @@ class OracleIndex:
         return keys[0] if keys else False
 
 
+class OracleRouter:
+    """emqx_router match_routes/1 over the brute-force emqx_topic:match/2 restatement:
+    the route table as a set of (filter, dest)."""
+
+    def __init__(self, node="node"):
+        self.node = node
+        self.routes = set()
+
+    def add_route(self, t, d):
+        self.routes.add((t.encode(), d))
+
+    def delete_route(self, t, d):
+        self.routes.discard((t.encode(), d))
+
+    def _sub(self, tf, node):
+        from oracle import emqx_topic as et
+        p, _ = et.parse(tf.encode())
+        return (p.topic, (p.group.decode(), node)) if isinstance(p, et.Share) else (p, node)
+
+    def subscribe(self, tf, node):
+        self.routes.add(self._sub(tf, node))
+
+    def unsubscribe(self, tf, node):
+        self.routes.discard(self._sub(tf, node))
+
+    def match_routes(self, topic):
+        from oracle import emqx_topic as et
+        tb = topic.encode()
+        return [(f, d) for f, d in self.routes if et.match(tb, f)]
+
+    def topics(self):
+        return list({f for f, _ in self.routes})
+
+
+def run_router_case(case, r):
+    """Replay one kat_router.json case against a Router-shaped object (GPU mirror
+    emqx_amd.router.Router or OracleRouter).  Steps: add/del/sub/unsub/match/count/topics."""
+    def dest(d):
+        return tuple(d) if isinstance(d, list) else d
+
+    for step in case["steps"]:
+        kind = step[0]
+        if kind == "add":
+            r.add_route(step[1], dest(step[2]))
+        elif kind == "del":
+            r.delete_route(step[1], dest(step[2]))
+        elif kind == "sub":
+            r.subscribe(step[1], step[2])
+        elif kind == "unsub":
+            r.unsubscribe(step[1], step[2])
+        elif kind == "match":
+            got = sorted(((bytes(f).decode(), d) for f, d in r.match_routes(step[1])), key=repr)
+            exp = sorted(((f, dest(d)) for f, d in step[2]), key=repr)
+            assert got == exp, (case["name"], step, got)
+        elif kind == "count":
+            assert len(r.match_routes(step[1])) == step[2], (case["name"], step)
+        elif kind == "topics":
+            assert sorted(bytes(t).decode() for t in r.topics()) == sorted(step[1]), (case["name"], step)
+        else:
+            raise ValueError(kind)
+
+
 def run_index_case(case, make_index, check):
     """Replay one kat_index.json case; `check(cond, msg)` reports failures."""
     ix = make_index()

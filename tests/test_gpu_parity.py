@@ -61,21 +61,25 @@ def test_index_kats_gpu(golden, mode):
 
 def test_router_kats_gpu(golden):
     from emqx_amd.router import Router
+    from tests.kat import run_router_case
     for case in golden("kat_router.json"):
-        r = Router(0, node="node")
-        for step in case["steps"]:
-            kind = step[0]
-            dest = (lambda d: tuple(d) if isinstance(d, list) else d)
-            if kind == "add":
-                r.add_route(step[1], dest(step[2]))
-            elif kind == "del":
-                r.delete_route(step[1], dest(step[2]))
-            elif kind == "match":
-                got = sorted(((f.decode(), d) for f, d in r.match_routes(step[1])), key=repr)
-                exp = sorted(((f, dest(d)) for f, d in step[2]), key=repr)
-                assert got == exp, (case["name"], step)
-            elif kind == "topics":
-                assert sorted(t.decode() for t in r.topics()) == sorted(step[1])
+        run_router_case(case, Router(0, node="node"))
+
+
+def test_filter_kats_key_form_gpu(golden):
+    """emqx_trie_search_tests:filter_test_ :23-33 through the engine: a wildcard filter's
+    key comes back as its word list (the empty level a binary), a filter without
+    wildcards as its binary (make_key/2, emqx_trie_search.erl:115-128)."""
+    from emqx_amd.topic_index import TopicIndex
+    ix = TopicIndex(0)
+    cases = golden("kat_topic.json")["filter"]
+    for n, (t, _) in enumerate(cases):
+        ix.insert(t.encode(), n)
+    for n, (t, exp) in enumerate(cases):
+        topic = t.replace("+", "x").replace("#", "y").encode()
+        keys = [k for k in ix.matches(topic, None, []) if k[1] == (n,)]
+        want = tuple(w["atom"] if isinstance(w, dict) else w.encode() for w in exp) if exp else t.encode()
+        assert keys == [(want, (n,))], (t, keys)
 
 
 def test_config_a_golden_sample_gpu(golden, mode):

@@ -62,6 +62,9 @@ def test_topic_misc_kats(golden):
         r = et.intersection(a.encode(), b.encode())
         assert r == (exp.encode() if exp else False), (a, b, r)
         assert et.intersection(b.encode(), a.encode()) == r  # commutative
+    assert len(g["intersection"]) == 17  # every assertion of t_intersect/_topic_wildcard/t_sys_intersect
+    for t, exp in g["filter"]:
+        assert et.trie_filter(t.encode()) == ([_atom(w) for w in exp] if exp else False), t
     for parent, w, exp in g["prepend"]:
         p = _atom(parent) if isinstance(parent, dict) else (parent.encode() if parent is not None else None)
         assert et.prepend(p, w.encode()) == exp.encode()
@@ -73,6 +76,18 @@ def test_topic_misc_kats(golden):
             assert et.parse(t.encode())[0] == et.Share(*(x.encode() for x in exp["share"]))
         else:
             assert et.parse(t.encode())[0] == exp.encode()
+
+
+def test_product_filter_kats(golden):
+    """emqx_trie_search_tests:filter_test_ :23-33 on the product's key classification
+    (make_key/2 keeps a filter without wildcards binary)."""
+    from emqx_amd import topic as pt
+    from emqx_amd.topic_index import make_key
+    for t, exp in golden("kat_topic.json")["filter"]:
+        want = [_atom(w) for w in exp] if exp else False
+        assert pt.filter(t.encode()) == want, t
+        k = make_key(t.encode(), 1)
+        assert k == ((tuple(want), (1,)) if want else (t.encode(), (1,)))
 
 
 def test_product_parse_agrees_with_oracle(golden):
@@ -100,6 +115,16 @@ def test_index_kats_on_trie_search_restatement(golden):
     for case in cases:
         run_index_case(case, OracleIndex, lambda c, m: c or errs.append(m))
     assert not errs, "\n".join(errs)
+
+
+def test_router_kats_on_oracle(golden):
+    """kat_router.json (emqx_router_SUITE, emqx_shared_sub_SUITE) on the brute-force
+    emqx_topic:match/2 restatement."""
+    from tests.kat import OracleRouter, run_router_case
+    cases = golden("kat_router.json")
+    assert any("t_queue_subscription" in c["name"] for c in cases)
+    for case in cases:
+        run_router_case(case, OracleRouter())
 
 
 # ---------------------------------------------------------------------- config A
