@@ -166,6 +166,52 @@ def cpu_info():
     return model
 
 
+def cpu_topology():
+    """What the CPU baseline can use on this host: logical CPUs, this process's affinity
+    set, the cgroup CPU quota (cpu.max, in CPUs; None if unlimited), the job's announced CPU
+    share (OMP_NUM_THREADS), sockets and threads per core from /proc/cpuinfo.  The baseline's
+    thread count is the smallest of affinity, quota and share (the CPUs this job may run on
+    at once; one thread per BEAM scheduler), unless --cpu-threads says otherwise."""
+    import math
+    info = {"logical_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "cgroup_quota_cpus": None,
+            "sockets": None, "threads_per_core": None}
+    for p in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(p).read().split()[:2]
+            if q != "max":
+                info["cgroup_quota_cpus"] = round(int(q) / int(per), 2)
+        except (OSError, ValueError):
+            pass
+    try:
+        phys, cores, sib = set(), None, None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k = k.strip()
+            if k == "physical id":
+                phys.add(v.strip())
+            elif k == "cpu cores" and cores is None:
+                cores = int(v)
+            elif k == "siblings" and sib is None:
+                sib = int(v)
+        info["sockets"] = len(phys) or None
+        if cores and sib:
+            info["threads_per_core"] = sib // cores
+    except (OSError, ValueError):
+        pass
+    # the job's CPU share as the pool announces it (OMP_NUM_THREADS: 16 per GPU on the box)
+    try:
+        info["job_share_cpus"] = int(os.environ["OMP_NUM_THREADS"])
+    except (KeyError, ValueError):
+        info["job_share_cpus"] = None
+    usable = info["affinity_cpus"]
+    if info["cgroup_quota_cpus"]:
+        usable = min(usable, max(1, math.floor(info["cgroup_quota_cpus"])))
+    if info["job_share_cpus"]:
+        usable = min(usable, info["job_share_cpus"])
+    info["usable_cpus"] = usable
+    return info
+
+
 def host_rss_gib():
     """Peak resident host memory of this rank (the engine's host master copy + workload)."""
     import resource
@@ -181,7 +227,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--batch", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work (s)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0: every CPU this process may use, see cpu_topology)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--batcher-seconds", type=float, default=2.0,
                     help="closed-loop load per publisher count through the batching aggregator (0: skip)")
@@ -227,25 +274,62 @@ def main():
     from emqx_amd import workloads
 
     # ---------------------------------------------------------------- build
+    # N = 1: one engine.  N > 1 (mode 1): rank 0 generates the workload and
+    # builds the ONE host master copy; every other rank gets a read replica of its device
+    # index (tm_image_export -> RCCL broadcast -> tm_replica_create) and its topic slice
+    # over the same group, so host memory and build work are one copy per node.
     t0 = time.time()
-    w = workloads.generate(args.config, scale=args.scale, n_topics=args.batch * world)
+    w = None
+    if rank == 0:
+        w = workloads.generate(args.config, scale=args.scale, n_topics=args.batch * world)
     t_gen = time.time() - t0
     t0 = time.time()
-    eng = N.Engine(local, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
-    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
-    eng.commit()
+    eng = None
+    if rank == 0:
+        eng = N.Engine(local, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4, record_patch=world > 1)
+        eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+        eng.commit()
     t_build = time.time() - t0
+    dev = torch.device("cuda", local)
+    image_s = None
+    if world > 1:
+        from emqx_amd.replica import EngineReplicaAdapter, ReplicatedIndex
+        t0 = time.time()
+        rix = ReplicatedIndex(EngineReplicaAdapter(local, eng), rank, world)
+        rix.start()
+        eng = rix.ad.eng
+        image_s = time.time() - t0
+        # topics: rank 0's whole batch to every rank, each keeps its slice (untimed)
+        tdev = dev if backend != "gloo" else torch.device("cpu")
+        sz = torch.tensor([len(w.t_bytes), len(w.t_off)] if rank == 0 else [0, 0], dtype=torch.int64, device=tdev)
+        dist.broadcast(sz, 0)
+        all_b = (torch.from_numpy(w.t_bytes).to(tdev) if rank == 0
+                 else torch.empty(int(sz[0].item()), dtype=torch.uint8, device=tdev))
+        all_o = (torch.from_numpy(w.t_off.view(np.int32)).to(tdev) if rank == 0
+                 else torch.empty(int(sz[1].item()), dtype=torch.int32, device=tdev))
+        dist.broadcast(all_b, 0)
+        dist.broadcast(all_o, 0)
+        all_b, all_o = all_b.to(dev), all_o.to(dev)
     st = eng.stats()
-    log(f"[rank {rank}] generated {w.n_keys} keys in {t_gen:.1f}s, engine build {t_build:.1f}s, "
-        f"nodes {st['n_nodes']}, words {st['n_words']}, index {st['device_bytes'] / 2**30:.2f} GiB")
+    log(f"[rank {rank}] {'generated ' + str(w.n_keys) + ' keys in ' + format(t_gen, '.1f') + 's, ' if w else ''}"
+        f"engine build {t_build:.1f}s{', replica image ' + format(image_s, '.1f') + 's' if image_s else ''}, "
+        f"keys {st['n_keys']}, nodes {st['n_nodes']}, words {st['n_words']}, "
+        f"index {st['device_bytes'] / 2**30:.2f} GiB, host RSS {host_rss_gib()} GiB")
 
     lo, hi = rank * args.batch, (rank + 1) * args.batch
-    tb, to = w.topic_slice(lo, hi)
     n = hi - lo
-    topic_bytes = int(to[-1])
-    dev = torch.device("cuda", local)
-    d_bytes = torch.from_numpy(tb).to(dev)
-    d_off = torch.from_numpy(to.view(np.int32)).to(dev)
+    if world > 1:
+        base = int(all_o[lo].item())
+        topic_bytes = int(all_o[hi].item()) - base
+        d_bytes = all_b[base:]
+        d_off = (all_o[lo:hi + 1] - base).contiguous()
+        tb, to = (w.topic_slice(lo, hi) if rank == 0 else (None, None))
+    else:
+        tb, to = w.topic_slice(lo, hi)
+        topic_bytes = int(to[-1])
+        d_bytes = torch.from_numpy(tb).to(dev)
+        d_off = torch.from_numpy(to.view(np.int32)).to(dev)
+    torch.cuda.synchronize()
     stream = torch.cuda.Stream(dev)  # kernels and timing events share this stream
     sp = stream.cuda_stream
 
@@ -370,6 +454,9 @@ def main():
     filt = filter_leg(args, w, eng, 20000) if rank == 0 and not args.profile else None
     inter = intersect_leg(w, tb, to) if rank == 0 and not args.profile else None
 
+    rss = torch.tensor([host_rss_gib()], dtype=torch.float64, device=dev if backend != "gloo" else "cpu")
+    if world > 1:
+        dist.all_reduce(rss, op=dist.ReduceOp.MAX)
     if rank == 0:
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
         prof = profiled_traffic(w.n_keys, n)
@@ -425,6 +512,10 @@ def main():
             "spill_topics": int(slow_topics),
             "build_s": round(t_build, 2),
             "host_peak_rss_gib": host_rss_gib(),
+            "host_peak_rss_gib_max_over_ranks": round(float(rss.item()), 2),
+            "replication": ({"mode": "one host master on rank 0, device image broadcast to replicas",
+                             "image_bytes": int(eng.image_size()), "image_s": round(image_s, 2)}
+                            if world > 1 else None),
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -469,25 +560,29 @@ def run_sharded(args):
     def step():
         return six.match_device(eng, d_bytes.data_ptr(), d_off.data_ptr(), n, tb)
 
+    six.prepare_device(eng, d_bytes.data_ptr(), d_off.data_ptr(), n, tb)  # sizes: untimed, collective
     for _ in range(max(1, args.warmup)):
-        off, ids = step()
+        off, ids, flags = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    lat = []
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t_start = time.perf_counter()
-    for _ in range(args.steps):
-        t1 = time.perf_counter()
-        off, ids = step()
-        torch.cuda.synchronize()
-        lat.append((time.perf_counter() - t1) * 1e3)
+    for k in range(args.steps):  # no host sync inside a step
+        evs[k][0].record()
+        off, ids, flags = step()
+        evs[k][1].record()
+    torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    lat = [a.elapsed_time(b) for a, b in evs]
     if world > 1:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if int(flags.item()):
+        raise RuntimeError("sharded step overflowed the sizes prepare_device fixed")
     matches = int(off[-1].item())
     if rank == 0:
         print(json.dumps({
@@ -693,7 +788,7 @@ def filter_leg(args, w, eng, q):
     dt = float(np.mean(ts))
     o, c, k, st = eng.match_filter_packed(qb, qo)
     total = int(c.sum())
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    threads = args.cpu_threads or cpu_topology()["usable_cpus"]
     ix = oracle_index(w)
     t0 = time.perf_counter()
     ix.count(qb, qo, algo=oracle.ALGO_FILTER, threads=threads)
@@ -800,7 +895,8 @@ def cpu_baseline(args, w, eng, tb, to, n):
     batch, and check the engine's results for that sample bit-exactly."""
     import oracle
     from emqx_amd import _native as N
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    topo = cpu_topology()
+    threads = args.cpu_threads or topo["usable_cpus"]
     t0 = time.time()
     ix = oracle_index(w)
     t_build = time.time() - t0
@@ -839,6 +935,8 @@ def cpu_baseline(args, w, eng, tb, to, n):
         "unit": "publishes/s",
         "cores": threads,
         "kind": "port",
+        "host": dict(topo, model=cpu_info(), threads_used=threads),
+        "value_1_thread": round(m1 / dt1, 1),
         "sample": f"{passes} pass(es) over {m} publishes ({dt:.1f} s) of the same batch vs the same {w.n_keys} keys; C++ restatement of "
                   f"emqx_trie_search over an Erlang-term-ordered key set (oracle/trie_search.cpp), "
                   f"{threads} threads on {cpu_info()}; 1 thread: {round(m1 / dt1, 1)} publishes/s "

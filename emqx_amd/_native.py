@@ -49,6 +49,9 @@ def shared_id(group: int, member: int) -> int:
 
 
 TM_CFG_FORCE_SLOW = 1
+TM_CFG_RECORD_PATCH = 2
+TM_RES_KEYS_OVERFLOW = 1
+TM_RES_IDS_OVERFLOW = 2
 
 # every symbol include/emqx_tm.h declares (tests check the .so exports them all)
 EXPORTS = (
@@ -56,7 +59,8 @@ EXPORTS = (
     "tm_commit_epoch", "tm_match_batch", "tm_match_device", "tm_device_sync",
     "tm_reserve_matches", "tm_key_info", "tm_key_ids", "tm_stats", "tm_debug_stats", "tm_debug_timing",
     "tm_result_ids_device", "tm_merge_shards_device", "tm_merge_shards", "tm_match_device_mode",
-    "tm_match_filter_batch", "tm_intersect_batch",
+    "tm_match_filter_batch", "tm_intersect_batch", "tm_result_ids_device_ex", "tm_image_size", "tm_image_export",
+    "tm_replica_create", "tm_replica_load", "tm_patch_size", "tm_patch_export", "tm_replica_apply_patch",
 )
 # every symbol include/emqx_tm_batcher.h declares
 BATCHER_EXPORTS = (
@@ -174,6 +178,14 @@ def load() -> C.CDLL:
     lib.tm_debug_timing.argtypes = [C.c_void_p, C.c_int, P(C.c_float)]
     lib.tm_debug_stats.argtypes = [C.c_void_p, C.c_int, P(C.c_uint64)]
     lib.tm_result_ids_device.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    lib.tm_result_ids_device_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.tm_image_size.argtypes = [C.c_void_p, P(C.c_uint64)]
+    lib.tm_image_export.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+    lib.tm_replica_create.argtypes = [P(tm_config), C.c_void_p, C.c_uint64, C.c_void_p, P(C.c_void_p)]
+    lib.tm_replica_load.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+    lib.tm_patch_size.argtypes = [C.c_void_p, P(C.c_uint64), P(C.c_int)]
+    lib.tm_patch_export.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+    lib.tm_replica_apply_patch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
     lib.tm_merge_shards_device.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64,
                                            C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     lib.tm_merge_shards.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
@@ -241,11 +253,11 @@ class Engine:
 
     def __init__(self, device: int = 0, *, force_slow: bool = False, reserve_keys: int = 0,
                  reserve_nodes: int = 0, reserve_matches: int = 0, seg_chunks: int = 0, edge_load_inv: int = 0,
-                 topics_per_wave: int = 0):
+                 topics_per_wave: int = 0, record_patch: bool = False, _image=None):
         self.lib = load()
         cfg = tm_config()
         cfg.device = device
-        cfg.flags = TM_CFG_FORCE_SLOW if force_slow else 0
+        cfg.flags = (TM_CFG_FORCE_SLOW if force_slow else 0) | (TM_CFG_RECORD_PATCH if record_patch else 0)
         cfg.reserve_keys = reserve_keys
         cfg.reserve_nodes = reserve_nodes
         cfg.reserve_matches = reserve_matches
@@ -253,11 +265,47 @@ class Engine:
         cfg.topics_per_wave = topics_per_wave
         cfg.edge_load_inv = edge_load_inv or int(os.environ.get("EMQX_TM_EDGE_LOAD_INV", "0"))
         h = C.c_void_p()
-        rc = self.lib.tm_create(C.byref(cfg), C.byref(h))
+        if _image is None:
+            rc = self.lib.tm_create(C.byref(cfg), C.byref(h))
+        else:  # (device pointer, bytes, stream) of a master's image on this device
+            rc = self.lib.tm_replica_create(C.byref(cfg), C.c_void_p(_image[0]), _image[1],
+                                            C.c_void_p(_image[2]) if _image[2] else None, C.byref(h))
         if rc != TM_OK:
             raise TMError(rc, "tm_create failed (no gfx950 HIP device visible?)")
         self.h = h
         self.device = device
+        self.replica = _image is not None
+
+    @classmethod
+    def replica_from_image(cls, device: int, d_image: int, nbytes: int, stream: int = 0, **kw) -> "Engine":
+        """A read replica (tm_replica_create) from a master's device image on `device`."""
+        return cls(device, _image=(d_image, nbytes, stream), **kw)
+
+    # ---- replicated mode: image + epoch patches (include/emqx_tm.h)
+    def image_size(self) -> int:
+        n = C.c_uint64()
+        self._check(self.lib.tm_image_size(self.h, C.byref(n)))
+        return n.value
+
+    def image_export(self, d_dst: int, cap: int, stream: int = 0):
+        self._check(self.lib.tm_image_export(self.h, C.c_void_p(d_dst), cap, C.c_void_p(stream) if stream else None))
+
+    def replica_load(self, d_image: int, nbytes: int, stream: int = 0):
+        self._check(self.lib.tm_replica_load(self.h, C.c_void_p(d_image), nbytes,
+                                             C.c_void_p(stream) if stream else None))
+
+    def patch_export(self):
+        """The last commit's device changes: (bytes as a uint8 array, full) — full means the
+        commit re-uploaded everything and replicas must reload from an image."""
+        n, full = C.c_uint64(), C.c_int()
+        self._check(self.lib.tm_patch_size(self.h, C.byref(n), C.byref(full)))
+        buf = np.zeros(n.value, dtype=np.uint8)
+        self._check(self.lib.tm_patch_export(self.h, buf.ctypes.data, n.value))
+        return buf, bool(full.value)
+
+    def apply_patch(self, patch: np.ndarray):
+        patch = np.ascontiguousarray(patch, dtype=np.uint8)
+        self._check(self.lib.tm_replica_apply_patch(self.h, patch.ctypes.data, len(patch)))
 
     def close(self):
         if getattr(self, "h", None):
@@ -458,6 +506,11 @@ class Engine:
         """Route ids of the last batch, topic-major, into device buffers (d_off: n+1 u32)."""
         self._check(self.lib.tm_result_ids_device(self.h, C.c_void_p(d_ids), ids_cap, C.c_void_p(d_off),
                                                   C.c_void_p(stream) if stream else None))
+
+    def result_ids_device_ex(self, d_ids: int, ids_cap: int, d_off: int, d_flags: int, stream: int = 0):
+        """result_ids_device + a device u32 of TM_RES_* overflow flags (no host sync)."""
+        self._check(self.lib.tm_result_ids_device_ex(self.h, C.c_void_p(d_ids), ids_cap, C.c_void_p(d_off),
+                                                     C.c_void_p(d_flags), C.c_void_p(stream) if stream else None))
 
     def merge_shards_device(self, G: int, n: int, d_counts: int, d_ids: int, stride: int, d_out_off: int,
                             d_out_ids: int, out_cap: int, stream: int = 0):

@@ -98,10 +98,14 @@ hipError_t launch_excl_scan(const uint32_t *in, uint64_t in_stride, uint32_t n, 
                             hipStream_t stream);
 // ids[dst_off[t] + k] = key_rec[2 * keys[src_off[t] + k]] (the id word of the key's
 // {id, order code} record) for k < cnt[t] (topics whose range
-// would pass `cap` are skipped).
+// would pass `cap`, or whose keys lie past the walk's arena `keys_cap`, are skipped).
+// flags (may be null): one u32 := RES_* bits, computed on the device from the walk's
+// cursor (requested keys) and dst_off[n].
+constexpr uint32_t RES_KEYS_OVERFLOW = 1, RES_IDS_OVERFLOW = 2;
 hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
                              const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
-                             uint64_t cap, hipStream_t stream);
+                             uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, uint32_t *flags,
+                             hipStream_t stream);
 // Concatenate G shards' topic-major results per topic.  roff: G*(n+1) u32, tot: n u32,
 // scratch: scan_scratch_words(n) u32 (work areas); off: n+1 u32 out; out: merged ids.
 hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,

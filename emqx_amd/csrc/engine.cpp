@@ -118,6 +118,60 @@ constexpr uint64_t MAX_EDGE_SLOTS = 1ull << 31;
 // Word table load <= 1/WORD_LOAD_INV (small: it sizes with the vocabulary, not the nodes).
 constexpr uint64_t WORD_LOAD_INV = 4;
 
+// Device arrays of the frozen index: what a device image holds and what an epoch patch
+// touches (replicated mode, tm_image_export / tm_replica_*).
+enum : uint32_t {
+    A_WTAB, A_WARENA, A_WORD_OFF, A_ETAB, A_SLOT_LIST, A_ARENA, A_ROOT, A_KEY_REC, A_KEY_NODE, A_KEY_BIN, A_KEY_DD,
+    A_N
+};
+constexpr uint32_t ARR_ELEM[A_N] = {16, 1, 4, 16, 4, 4, 16, 16, 4, 4, 1};
+
+// Epoch patch: what one delta commit changed on the device, as records a replica replays.
+enum : uint32_t { P_TAIL = 1, P_SCATTER = 2, P_WHOLE = 3 };
+struct PatchRec {
+    uint32_t kind, arr;
+    uint64_t count;  // elements
+    uint64_t a;      // P_TAIL: first element written; P_WHOLE: capacity (bytes) to allocate
+    uint64_t bytes;  // payload bytes following this record (8-byte padded)
+};
+constexpr uint64_t PATCH_MAGIC = 0x3148435441504d54ull, IMAGE_MAGIC = 0x31474d494d545845ull;
+struct PatchHdr {
+    uint64_t magic;
+    uint64_t epoch_from, epoch_to;
+    uint64_t wmask, emask, n_deep, n_live, n_records;
+    uint64_t full;  // the commit re-uploaded everything: replicas reload from an image
+};
+struct ImageHdr {
+    uint64_t magic;
+    uint64_t epoch, wmask, emask, n_deep, n_live, n_nodes, n_words;
+    uint64_t cap[A_N], used[A_N], off[A_N];
+};
+constexpr uint64_t IMAGE_ALIGN = 256;
+
+struct PatchLog {
+    bool on = false;   // tm_config.flags & TM_CFG_RECORD_PATCH
+    bool full = false;
+    uint64_t n = 0;
+    std::vector<uint8_t> buf;
+    void reset() {
+        full = false;
+        n = 0;
+        buf.clear();
+    }
+    void add(uint32_t kind, uint32_t arr, uint64_t count, uint64_t a, const void *p1, size_t n1,
+             const void *p2 = nullptr, size_t n2 = 0) {
+        if (!on || full) return;
+        const uint64_t pay = (n1 + n2 + 7) & ~7ull;
+        PatchRec r{kind, arr, count, a, pay};
+        const size_t at = buf.size();
+        buf.resize(at + sizeof r + pay, 0);
+        memcpy(&buf[at], &r, sizeof r);
+        if (n1) memcpy(&buf[at + sizeof r], p1, n1);
+        if (n2) memcpy(&buf[at + sizeof r + n1], p2, n2);
+        n++;
+    }
+};
+
 inline uint64_t next_pow2(uint64_t x) {
     uint64_t p = 1;
     while (p < x) p <<= 1;
@@ -260,10 +314,26 @@ struct tm_engine {
     hipStream_t last_stream = nullptr;  // stream of the last tm_match_device call
     uint32_t last_n = 0;                // topics of the last match batch
     bool stats_on = false;
+    PatchLog patch;          // master: the last commit's device changes (TM_CFG_RECORD_PATCH)
+    uint64_t patch_from = 0; // epoch the recorded patch applies to
+    bool replica = false;    // built from a device image: no host master copy, read-only
+    uint64_t rep_n_live = 0, rep_n_nodes = 0, rep_n_words = 0;
+    uint64_t dev_used[A_N] = {};  // bytes of each device array in use (image export)
     hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // around k_match_fast (tm_debug_timing)
     bool timing_on = false;
 
     uint64_t edge_load_inv() const { return cfg.edge_load_inv ? cfg.edge_load_inv : EDGE_LOAD_INV; }
+
+    DevBuf *arr_buf(uint32_t a) {
+        DevBuf *b[A_N] = {&d_wtab, &d_warena, &d_word_off, &d_etab, &d_slot_list, &d_arena,
+                          &d_root, &d_key_rec, &d_key_node, &d_key_bin, &d_key_dd};
+        return a < A_N ? b[a] : nullptr;
+    }
+    uint32_t arr_of(const DevBuf *d) {
+        for (uint32_t a = 0; a < A_N; a++)
+            if (arr_buf(a) == d) return a;
+        return A_N;
+    }
 
     // =====================================================================
     // words: a word of <= 8 bytes is its own key (zero-padded LE bytes); longer
@@ -775,6 +845,11 @@ struct tm_engine {
         size_t bytes = h.size() * sizeof(T);
         if ((e = d.ensure(std::max<size_t>(bytes * headroom_num / headroom_den, 4096)))) return e;
         if (bytes && (e = hipMemcpyAsync(d.p, h.data(), bytes, hipMemcpyHostToDevice, stream))) return e;
+        const uint32_t a = arr_of(&d);
+        if (a < A_N) {
+            dev_used[a] = bytes;
+            patch.add(P_WHOLE, a, bytes / ARR_ELEM[a], d.cap, h.data(), bytes);
+        }
         return hipSuccess;
     }
     template <class T>
@@ -782,12 +857,22 @@ struct tm_engine {
         if (h.size() <= dev_n) return hipSuccess;
         hipError_t e = hipMemcpyAsync(d.as<T>() + dev_n, h.data() + dev_n, (h.size() - dev_n) * sizeof(T),
                                       hipMemcpyHostToDevice, stream);
-        if (e == hipSuccess) dev_n = h.size();
+        if (e != hipSuccess) return e;
+        const uint32_t a = arr_of(&d);
+        if (a < A_N) {
+            patch.add(P_TAIL, a, (h.size() - dev_n) * sizeof(T) / ARR_ELEM[a], dev_n * sizeof(T) / ARR_ELEM[a],
+                      h.data() + dev_n, (h.size() - dev_n) * sizeof(T));
+            dev_used[a] = h.size() * sizeof(T);
+        }
+        dev_n = h.size();
         return e;
     }
 
     hipError_t upload_full() {
         hipError_t e;
+        patch.reset();
+        patch.full = true;  // replicas reload from an image
+        dev_used[A_ROOT] = sizeof(RootRec);
         if ((e = put(d_wtab, wtab, 1, 1))) return e;
         if ((e = put(d_warena, warena))) return e;
         warena_dev = warena.size();
@@ -844,6 +929,10 @@ struct tm_engine {
             key_dev_rec((uint32_t)dirty_kid[i], &rec[2 * i], &node[i], &bin[i], &dd[i]);
         }
         dirty_kid.clear();
+        patch.add(P_SCATTER, A_KEY_REC, n, 0, idx.data(), n * 8, rec.data(), n * 16);
+        patch.add(P_SCATTER, A_KEY_BIN, n, 0, idx.data(), n * 8, bin.data(), n * 4);
+        patch.add(P_SCATTER, A_KEY_NODE, n, 0, idx.data(), n * 8, node.data(), n * 4);
+        patch.add(P_SCATTER, A_KEY_DD, n, 0, idx.data(), n * 8, dd.data(), n);
         hipError_t e;
         if ((e = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e;
         if ((e = d_scatter_src.ensure(n * 16))) return e;
@@ -872,7 +961,8 @@ struct tm_engine {
 
     // dst[idx[i]] = src[i] for 16-byte records (edge slots, word slots, node records)
     template <class Rec16>
-    hipError_t scatter16(std::vector<uint64_t> &dirty, const std::vector<Rec16> &tab, void *dtab) {
+    hipError_t scatter16(std::vector<uint64_t> &dirty, const std::vector<Rec16> &tab, DevBuf &dbuf) {
+        void *dtab = dbuf.p;
         static_assert(sizeof(Rec16) == 16, "16-byte records");
         if (dirty.empty()) return hipSuccess;
         std::sort(dirty.begin(), dirty.end());
@@ -880,6 +970,7 @@ struct tm_engine {
         size_t n = dirty.size();
         std::vector<Rec16> src(n);
         for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
+        patch.add(P_SCATTER, arr_of(&dbuf), n, 0, dirty.data(), n * 8, src.data(), n * 16);
         hipError_t e;
         if ((e = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e;
         if ((e = d_scatter_src.ensure(n * 16))) return e;
@@ -893,13 +984,15 @@ struct tm_engine {
     }
 
     // dst[idx[i]] = src[i] for u32 entries (slot_list)
-    hipError_t scatter4(std::vector<uint64_t> &dirty, const std::vector<uint32_t> &tab, void *dtab) {
+    hipError_t scatter4(std::vector<uint64_t> &dirty, const std::vector<uint32_t> &tab, DevBuf &dbuf) {
+        void *dtab = dbuf.p;
         if (dirty.empty()) return hipSuccess;
         std::sort(dirty.begin(), dirty.end());
         dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
         size_t n = dirty.size();
         std::vector<uint32_t> src(n);
         for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
+        patch.add(P_SCATTER, arr_of(&dbuf), n, 0, dirty.data(), n * 8, src.data(), n * 4);
         hipError_t e;
         if ((e = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e;
         if ((e = d_scatter_src.ensure(n * 4))) return e;
@@ -924,14 +1017,15 @@ struct tm_engine {
         if (words_full) {
             if ((e = put(d_wtab, wtab, 1, 1))) return e;
             dirty_wslots.clear();
-        } else if ((e = scatter16(dirty_wslots, wtab, d_wtab.p))) {
+        } else if ((e = scatter16(dirty_wslots, wtab, d_wtab))) {
             return e;
         }
-        if ((e = scatter16(dirty_eslots, etab, d_etab.p))) return e;
-        if ((e = scatter4(dirty_lists, slot_list, d_slot_list.p))) return e;
+        if ((e = scatter16(dirty_eslots, etab, d_etab))) return e;
+        if ((e = scatter4(dirty_lists, slot_list, d_slot_list))) return e;
         if ((e = upload_key_ids_delta())) return e;
         if (root_dirty) {
             if ((e = hipMemcpyAsync(d_root.p, &root, sizeof(RootRec), hipMemcpyHostToDevice, stream))) return e;
+            patch.add(P_WHOLE, A_ROOT, 1, d_root.cap, &root, sizeof(RootRec));
         }
         return hipStreamSynchronize(stream);
     }
@@ -968,6 +1062,8 @@ struct tm_engine {
             return TM_ENOMEM;
         }
         const uint64_t t2 = now_us();
+        patch.reset();
+        patch_from = epoch;
         hipError_t e = need_full ? upload_full() : upload_delta();
         if (e != hipSuccess) {
             err = std::string("device upload failed: ") + hipGetErrorString(e);
@@ -1317,8 +1413,14 @@ __attribute__((visibility("hidden"))) int tmx_engine_device(const tm_engine *eng
 
 const char *tm_last_error(const tm_engine *eng) { return eng ? eng->err.c_str() : "null engine"; }
 
+static int replica_refuses(tm_engine *eng, const char *what) {
+    eng->err = std::string(what) + ": a replica is read-only and keeps no host copy of the keys (use the master)";
+    return TM_ESTATE;
+}
+
 int tm_apply(tm_engine *eng, const tm_op *ops, size_t n) {
     if (!eng || (n && !ops)) return TM_EINVAL;
+    if (eng->replica) return replica_refuses(eng, "tm_apply");
     for (size_t i = 0; i < n; i++) {
         const tm_op &o = ops[i];
         if ((o.op != TM_OP_ADD && o.op != TM_OP_DEL) || o.filter_len > 65535u || (o.filter_len && !o.filter)) {
@@ -1339,6 +1441,7 @@ int tm_apply_packed(tm_engine *eng, uint32_t op, const uint8_t *bytes, const uin
                     const uint32_t *flags, size_t n) {
     if (!eng || (n && (!off || !ids || (!bytes && off[n] > off[0])))) return TM_EINVAL;
     if (op != TM_OP_ADD && op != TM_OP_DEL) return TM_EINVAL;
+    if (eng->replica) return replica_refuses(eng, "tm_apply_packed");
     for (size_t i = 0; i < n; i++)
         if (off[i + 1] < off[i] || off[i + 1] - off[i] > 65535u) {
             eng->err = "tm_apply_packed: bad filter offsets";
@@ -1355,6 +1458,7 @@ int tm_apply_packed(tm_engine *eng, uint32_t op, const uint8_t *bytes, const uin
 
 int tm_commit_epoch(tm_engine *eng, uint64_t *epoch_out) {
     if (!eng) return TM_EINVAL;
+    if (eng->replica) return replica_refuses(eng, "tm_commit_epoch");
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     int rc = eng->commit();
     if (epoch_out) *epoch_out = eng->epoch;
@@ -1497,6 +1601,7 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
     out->n = n;
     // UNIQUE is reduced on the GPU unless a key is too deep for the device order code
     const bool dev_reduce = reduced_mode(mode) && (mode == TM_MATCH_AGGRE || eng->n_deep == 0);
+    if (reduced_mode(mode) && !dev_reduce && eng->replica) return replica_refuses(eng, "tm_match_batch (host UNIQUE)");
     eng->last_mode = (reduced_mode(mode) && !dev_reduce) ? TM_MATCH_ALL : mode;  // what the device holds
     if (n == 0) return TM_OK;
     // rebase offsets to 0
@@ -1708,6 +1813,11 @@ int tm_device_sync(tm_engine *eng) {
 }
 
 int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out, void *stream) {
+    return tm_result_ids_device_ex(eng, d_ids, ids_cap, d_off_out, nullptr, stream);
+}
+
+int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out, uint32_t *d_flags,
+                            void *stream) {
     if (!eng || !d_off_out || (ids_cap && !d_ids)) return TM_EINVAL;
     if (!eng->p_ctl) {
         eng->err = "tm_result_ids_device: no tm_match_device batch yet";
@@ -1721,7 +1831,8 @@ int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint
     const uint32_t *cnt = (red ? eng->d_ucnt : eng->d_outcnt).as<uint32_t>();
     TM_TRY_HIP(launch_excl_scan(cnt, 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s), TM_EDEVICE, "scan");
     TM_TRY_HIP(launch_result_ids(cnt, eng->d_outoff.as<uint32_t>(), eng->d_keys.as<uint32_t>(),
-                                 eng->d_key_rec.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, s),
+                                 eng->d_key_rec.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, eng->keys_cap,
+                                 (const unsigned long long *)(eng->p_ctl + CTL_CURSOR), d_flags, s),
                TM_EDEVICE, "result ids");
     return TM_OK;
 }
@@ -1792,6 +1903,7 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
                           tm_result *out) {
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
     if (mode != TM_MATCH_ALL && mode != TM_MATCH_UNIQUE && mode != TM_MATCH_FIRST) return TM_EINVAL;
+    if (eng->replica) return replica_refuses(eng, "tm_match_filter_batch");
     if (!eng->staged.empty()) {
         eng->err = "tm_match_filter_batch: staged ops not committed";
         return TM_ESTATE;
@@ -1969,12 +2081,12 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
     if (!eng || !out) return TM_EINVAL;
     memset(out, 0, sizeof(*out));
     out->epoch = eng->epoch;
-    out->n_keys = eng->n_live;
-    out->n_nodes = eng->node_parent.size();
-    out->n_words = eng->word_off.size();
-    out->edge_slots = eng->etab.size();
-    out->word_slots = eng->wtab.size();
-    out->list_words = eng->arena.size();
+    out->n_keys = eng->replica ? eng->rep_n_live : eng->n_live;
+    out->n_nodes = eng->replica ? eng->rep_n_nodes : eng->node_parent.size();
+    out->n_words = eng->replica ? eng->rep_n_words : eng->word_off.size();
+    out->edge_slots = eng->replica ? eng->emask + 1 : eng->etab.size();
+    out->word_slots = eng->replica ? eng->wmask + 1 : eng->wtab.size();
+    out->list_words = eng->replica ? eng->dev_used[A_ARENA] / 4 : eng->arena.size();
     out->device_bytes = eng->d_wtab.cap + eng->d_warena.cap + eng->d_word_off.cap + eng->d_etab.cap +
                         eng->d_slot_list.cap + eng->d_arena.cap + eng->d_root.cap;
     out->n_full_rebuilds = eng->n_full_rebuilds;
@@ -2019,6 +2131,230 @@ int tm_debug_timing(tm_engine *eng, int enable, float *ms_out) {
         TM_TRY_HIP(hipEventElapsedTime(ms_out, eng->ev_fast0, eng->ev_fast1), TM_EDEVICE, "elapsed");
     }
     eng->timing_on = enable != 0;
+    return TM_OK;
+}
+
+// ---- replicated mode: device image + epoch patches (DESIGN.md §6 mode 1) ----------
+static void image_layout(const tm_engine *eng, ImageHdr *h) {
+    memset(h, 0, sizeof *h);
+    h->magic = IMAGE_MAGIC;
+    h->epoch = eng->epoch;
+    h->wmask = eng->wmask;
+    h->emask = eng->emask;
+    h->n_deep = eng->n_deep;
+    h->n_live = eng->replica ? eng->rep_n_live : eng->n_live;
+    h->n_nodes = eng->replica ? eng->rep_n_nodes : eng->node_parent.size();
+    h->n_words = eng->replica ? eng->rep_n_words : eng->word_off.size();
+    const uint64_t nk = eng->keys.size();
+    const uint64_t used[A_N] = {eng->wtab.size() * 16, eng->warena_dev, eng->word_off_dev * 4, eng->etab.size() * 16,
+                                eng->slot_list.size() * 4, eng->arena_dev * 4, sizeof(RootRec), nk * 16, nk * 4, nk * 4,
+                                nk};
+    uint64_t at = (sizeof(ImageHdr) + IMAGE_ALIGN - 1) / IMAGE_ALIGN * IMAGE_ALIGN;
+    for (uint32_t a = 0; a < A_N; a++) {
+        const DevBuf *b = const_cast<tm_engine *>(eng)->arr_buf(a);
+        h->cap[a] = b->cap;
+        h->used[a] = eng->replica ? eng->dev_used[a] : std::min<uint64_t>(used[a], b->cap);
+        h->off[a] = at;
+        at += (h->used[a] + IMAGE_ALIGN - 1) / IMAGE_ALIGN * IMAGE_ALIGN;
+    }
+}
+
+static uint64_t image_bytes(const ImageHdr &h) {
+    uint64_t end = (sizeof(ImageHdr) + IMAGE_ALIGN - 1) / IMAGE_ALIGN * IMAGE_ALIGN;
+    for (uint32_t a = 0; a < A_N; a++) end = std::max(end, h.off[a] + (h.used[a] + IMAGE_ALIGN - 1) / IMAGE_ALIGN * IMAGE_ALIGN);
+    return end;
+}
+
+int tm_image_size(const tm_engine *eng, uint64_t *bytes) {
+    if (!eng || !bytes) return TM_EINVAL;
+    if (!eng->staged.empty()) return TM_ESTATE;
+    ImageHdr h;
+    image_layout(eng, &h);
+    *bytes = image_bytes(h);
+    return TM_OK;
+}
+
+int tm_image_export(tm_engine *eng, void *d_dst, uint64_t cap, void *stream) {
+    if (!eng || !d_dst) return TM_EINVAL;
+    if (!eng->staged.empty()) {
+        eng->err = "tm_image_export: staged ops not committed";
+        return TM_ESTATE;
+    }
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    ImageHdr h;
+    image_layout(eng, &h);
+    if (image_bytes(h) > cap) return TM_ENOMEM;
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    uint8_t *dst = (uint8_t *)d_dst;
+    for (uint32_t a = 0; a < A_N; a++)
+        if (h.used[a])
+            TM_TRY_HIP(hipMemcpyAsync(dst + h.off[a], eng->arr_buf(a)->p, h.used[a], hipMemcpyDeviceToDevice, s),
+                       TM_EDEVICE, "image D2D");
+    TM_TRY_HIP(hipMemcpyAsync(dst, &h, sizeof h, hipMemcpyHostToDevice, s), TM_EDEVICE, "image header");
+    TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "image sync");  // h is on this stack frame
+    return TM_OK;
+}
+
+int tm_replica_load(tm_engine *eng, const void *d_image, uint64_t bytes, void *stream) {
+    if (!eng || !d_image || bytes < sizeof(ImageHdr)) return TM_EINVAL;
+    if (!eng->replica) {
+        eng->err = "tm_replica_load: not a replica";
+        return TM_ESTATE;
+    }
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    ImageHdr h;
+    TM_TRY_HIP(hipMemcpyAsync(&h, d_image, sizeof h, hipMemcpyDeviceToHost, s), TM_EDEVICE, "image header");
+    TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "image sync");
+    if (h.magic != IMAGE_MAGIC || image_bytes(h) > bytes) {
+        eng->err = "tm_replica_load: not an engine image (or truncated)";
+        return TM_EINVAL;
+    }
+    const uint8_t *src = (const uint8_t *)d_image;
+    for (uint32_t a = 0; a < A_N; a++) {
+        if (h.used[a] > h.cap[a]) return TM_EINVAL;
+        DevBuf *b = eng->arr_buf(a);
+        b->release();
+        TM_TRY_HIP(b->ensure(std::max<uint64_t>(h.cap[a], 64)), TM_ENOMEM, "replica alloc");
+        if (h.used[a])
+            TM_TRY_HIP(hipMemcpyAsync(b->p, src + h.off[a], h.used[a], hipMemcpyDeviceToDevice, s), TM_EDEVICE,
+                       "image D2D");
+        eng->dev_used[a] = h.used[a];
+    }
+    TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "image sync");
+    eng->epoch = h.epoch;
+    eng->wmask = h.wmask;
+    eng->emask = h.emask;
+    eng->n_deep = h.n_deep;
+    eng->rep_n_live = h.n_live;
+    eng->rep_n_nodes = h.n_nodes;
+    eng->rep_n_words = h.n_words;
+    return TM_OK;
+}
+
+int tm_replica_create(const tm_config *cfg, const void *d_image, uint64_t bytes, void *stream, tm_engine **out) {
+    if (!out || !d_image) return TM_EINVAL;
+    *out = nullptr;
+    tm_config c = cfg ? *cfg : tm_config{};
+    c.flags &= ~TM_CFG_RECORD_PATCH;
+    c.reserve_keys = 1;
+    c.reserve_nodes = 1;
+    tm_engine *eng = nullptr;
+    int rc = tm_create(&c, &eng);
+    if (rc != TM_OK) return rc;
+    eng->replica = true;
+    // the replica keeps no host master copy
+    std::vector<WordSlot>().swap(eng->wtab);
+    std::vector<EdgeSlot>().swap(eng->etab);
+    std::vector<uint32_t>().swap(eng->slot_list);
+    std::vector<uint32_t>().swap(eng->slot_node);
+    std::vector<uint32_t>().swap(eng->kset);
+    if ((rc = tm_replica_load(eng, d_image, bytes, stream)) != TM_OK) {
+        tm_destroy(eng);
+        return rc;
+    }
+    *out = eng;
+    return TM_OK;
+}
+
+int tm_patch_size(const tm_engine *eng, uint64_t *bytes, int *full) {
+    if (!eng || !bytes) return TM_EINVAL;
+    if (!(eng->cfg.flags & TM_CFG_RECORD_PATCH)) return TM_ESTATE;
+    *bytes = sizeof(PatchHdr) + (eng->patch.full ? 0 : eng->patch.buf.size());
+    if (full) *full = eng->patch.full ? 1 : 0;
+    return TM_OK;
+}
+
+int tm_patch_export(const tm_engine *eng, void *dst, uint64_t cap) {
+    if (!eng || !dst) return TM_EINVAL;
+    if (!(eng->cfg.flags & TM_CFG_RECORD_PATCH)) return TM_ESTATE;
+    const uint64_t body = eng->patch.full ? 0 : eng->patch.buf.size();
+    if (cap < sizeof(PatchHdr) + body) return TM_ENOMEM;
+    PatchHdr h{PATCH_MAGIC, eng->patch_from, eng->epoch, eng->wmask, eng->emask, eng->n_deep, eng->n_live,
+               eng->patch.full ? 0 : eng->patch.n, eng->patch.full ? 1ull : 0ull};
+    memcpy(dst, &h, sizeof h);
+    if (body) memcpy((uint8_t *)dst + sizeof h, eng->patch.buf.data(), body);
+    return TM_OK;
+}
+
+int tm_replica_apply_patch(tm_engine *eng, const void *patch, uint64_t bytes) {
+    if (!eng || !patch || bytes < sizeof(PatchHdr)) return TM_EINVAL;
+    if (!eng->replica) {
+        eng->err = "tm_replica_apply_patch: not a replica";
+        return TM_ESTATE;
+    }
+    PatchHdr h;
+    memcpy(&h, patch, sizeof h);
+    if (h.magic != PATCH_MAGIC) return TM_EINVAL;
+    if (h.full) {
+        eng->err = "tm_replica_apply_patch: the master re-uploaded its whole index; reload from tm_image_export";
+        return TM_ESTATE;
+    }
+    if (h.epoch_from != eng->epoch) {
+        eng->err = "tm_replica_apply_patch: patch is for epoch " + std::to_string(h.epoch_from) + ", replica holds " +
+                   std::to_string(eng->epoch);
+        return TM_ESTATE;
+    }
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    hipStream_t s = eng->stream;
+    // validate every record before touching the device: a replica never half-applies
+    const uint8_t *p = (const uint8_t *)patch + sizeof h, *end = (const uint8_t *)patch + bytes;
+    for (uint64_t i = 0; i < h.n_records; i++) {
+        if (p + sizeof(PatchRec) > end) return TM_EINVAL;
+        PatchRec r;
+        memcpy(&r, p, sizeof r);
+        const uint64_t el = r.arr < A_N ? ARR_ELEM[r.arr] : 0;
+        if (!el || p + sizeof r + r.bytes > end) return TM_EINVAL;
+        const uint64_t need = r.kind == P_SCATTER ? r.count * (8 + el) : r.count * el;
+        if (need > r.bytes) return TM_EINVAL;
+        const DevBuf *b = eng->arr_buf(r.arr);
+        if (r.kind == P_TAIL && (r.a + r.count) * el > b->cap) return TM_EINVAL;
+        if (r.kind == P_WHOLE && r.count * el > r.a) return TM_EINVAL;
+        if (r.kind != P_TAIL && r.kind != P_SCATTER && r.kind != P_WHOLE) return TM_EINVAL;
+        p += sizeof r + r.bytes;
+    }
+    p = (const uint8_t *)patch + sizeof h;
+    for (uint64_t i = 0; i < h.n_records; i++) {
+        PatchRec r;
+        memcpy(&r, p, sizeof r);
+        const uint8_t *pay = p + sizeof r;
+        const uint64_t el = ARR_ELEM[r.arr];
+        DevBuf *b = eng->arr_buf(r.arr);
+        if (r.kind == P_TAIL) {
+            if (r.count)
+                TM_TRY_HIP(hipMemcpyAsync(b->as<uint8_t>() + r.a * el, pay, r.count * el, hipMemcpyHostToDevice, s),
+                           TM_EDEVICE, "patch H2D");
+            eng->dev_used[r.arr] = std::max<uint64_t>(eng->dev_used[r.arr], (r.a + r.count) * el);
+        } else if (r.kind == P_WHOLE) {
+            if (b->cap < r.a) {
+                b->release();
+                TM_TRY_HIP(b->ensure(r.a), TM_ENOMEM, "replica alloc");
+            }
+            if (r.count)
+                TM_TRY_HIP(hipMemcpyAsync(b->p, pay, r.count * el, hipMemcpyHostToDevice, s), TM_EDEVICE, "patch H2D");
+            eng->dev_used[r.arr] = r.count * el;
+        } else if (r.count) {
+            TM_TRY_HIP(eng->d_scatter_idx.ensure(r.count * 8), TM_ENOMEM, "alloc");
+            TM_TRY_HIP(eng->d_scatter_src.ensure(r.count * el), TM_ENOMEM, "alloc");
+            TM_TRY_HIP(hipMemcpyAsync(eng->d_scatter_idx.p, pay, r.count * 8, hipMemcpyHostToDevice, s), TM_EDEVICE,
+                       "patch H2D");
+            TM_TRY_HIP(hipMemcpyAsync(eng->d_scatter_src.p, pay + r.count * 8, r.count * el, hipMemcpyHostToDevice, s),
+                       TM_EDEVICE, "patch H2D");
+            const uint64_t *ix = eng->d_scatter_idx.as<uint64_t>();
+            hipError_t e = el == 16  ? launch_scatter16(b->as<uint4>(), ix, eng->d_scatter_src.as<uint4>(), r.count, s)
+                           : el == 4 ? launch_scatter4(b->as<uint32_t>(), ix, eng->d_scatter_src.as<uint32_t>(), r.count, s)
+                                     : launch_scatter1(b->as<uint8_t>(), ix, eng->d_scatter_src.as<uint8_t>(), r.count, s);
+            TM_TRY_HIP(e, TM_EDEVICE, "patch scatter");
+            TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "patch sync");  // scratch is reused by the next record
+        }
+        p += sizeof r + r.bytes;
+    }
+    TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "patch sync");
+    eng->epoch = h.epoch_to;
+    eng->wmask = h.wmask;
+    eng->emask = h.emask;
+    eng->n_deep = h.n_deep;
+    eng->rep_n_live = h.n_live;
     return TM_OK;
 }
 

@@ -109,15 +109,19 @@ hipError_t launch_excl_scan(const uint32_t *in, uint64_t in_stride, uint32_t n, 
 // consecutive keys per instruction.
 __global__ __launch_bounds__(64) void k_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
                                                    const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n,
-                                                   uint64_t *ids, uint64_t cap) {
+                                                   uint64_t *ids, uint64_t cap, uint64_t keys_cap,
+                                                   const unsigned long long *cursor) {
     const uint32_t lane = threadIdx.x;
     const uint32_t t = blockIdx.x * 64 + lane;
     uint32_t c = 0, so = 0, dofs = 0;
+    // the walk's arena overflowed: waves past the cap skipped their copy-out, nothing to read
+    if (cursor && *cursor > keys_cap) return;
     if (t < n) {
         c = cnt[t];
         so = src_off[t];
         dofs = dst_off[t];
         if ((uint64_t)dofs + c > cap) c = 0;  // caller's buffer too small: it re-sizes from d_off[n]
+        if ((uint64_t)so + c > keys_cap) c = 0;
     }
     const bool is_long = c > 8;
     if (!is_long) {
@@ -132,12 +136,28 @@ __global__ __launch_bounds__(64) void k_result_ids(const uint32_t *cnt, const ui
     }
 }
 
+// flags[0] = RES_KEYS_OVERFLOW if the walk asked for more keys than its arena holds,
+// | RES_IDS_OVERFLOW if the compacted ids passed the caller's buffer (dst_off[n] > cap).
+__global__ void k_result_flags(const unsigned long long *cursor, uint64_t keys_cap, const uint32_t *dst_off,
+                               uint32_t n, uint64_t cap, uint32_t *flags) {
+    if (threadIdx.x == 0)
+        flags[0] = (*cursor > keys_cap ? RES_KEYS_OVERFLOW : 0u) | ((uint64_t)dst_off[n] > cap ? RES_IDS_OVERFLOW : 0u);
+}
+
 hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
                              const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
-                             uint64_t cap, hipStream_t s) {
-    if (!n) return hipSuccess;
-    k_result_ids<<<(n + 63) / 64, 64, 0, s>>>(cnt, src_off, keys, key_rec, dst_off, n, ids, cap);
-    return hipGetLastError();
+                             uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, uint32_t *flags,
+                             hipStream_t s) {
+    if (n) {
+        k_result_ids<<<(n + 63) / 64, 64, 0, s>>>(cnt, src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap, cursor);
+        hipError_t e = hipGetLastError();
+        if (e) return e;
+    }
+    if (flags) {
+        k_result_flags<<<1, 64, 0, s>>>(cursor, keys_cap, dst_off, n, cap, flags);
+        return hipGetLastError();
+    }
+    return hipSuccess;
 }
 
 // ---------------------------------------------------------------------------

@@ -176,20 +176,21 @@ int synth_generate(const synth_params *pp, synth_out **out) {
     std::vector<std::string> lv;
     uint64_t next_id = 0;
     auto keep = [&](uint64_t id) { return p.shard_count <= 1 || shard_mix(id) % p.shard_count == p.shard_index; };
+    // The draws from r decide a filter's shape; its words come from its own stream tr.
+    // Only the level count (tr's first draw) is needed to replay r, so a filter whose
+    // ids all fall in other shards never builds its strings (same output, shards ~G x faster).
+    std::vector<uint32_t> plus_at;
     for (uint64_t i = 0; i < p.n_filters; i++) {
         uint64_t sseed = r.next();
         src_seed.push_back(sseed);
-        Rng tr(sseed);
-        gen_topic(lv, tr, p, z);
+        const uint32_t nl = p.min_levels + Rng(sseed).below(p.max_levels - p.min_levels + 1);  // gen_topic's first draw
         bool sys = p.p_sys_filter > 0 && r.uni() < p.p_sys_filter;
-        if (sys) {
-            lv.insert(lv.begin(), {"$SYS", "brokers", "emqx@n" + std::to_string(r.below(4))});
-        }
+        uint32_t sys_node = sys ? r.below(4) : 0;
         std::string f;
         bool hash = r.uni() < p.p_hash;
         bool plus = r.uni() < p.p_plus;
         if (hash && p.plus_hash_excl) plus = false;
-        size_t n = lv.size();
+        size_t n = nl + (sys ? 3 : 0);
         if (hash) {
             uint32_t d = p.min_hash_depth;
             if (wsum > 0) {
@@ -202,19 +203,26 @@ int synth_generate(const synth_params *pp, synth_out **out) {
             if (d > n) d = (uint32_t)n;
             n = d;
         }
+        plus_at.clear();
         if (plus) {
-            bool any = false;
             for (size_t k = 0; k < n; k++)
-                if (r.uni() < p.p_plus_level) {
-                    lv[k] = "+";
-                    any = true;
-                }
-            if (!any && n) lv[r.below((uint32_t)n)] = "+";
+                if (r.uni() < p.p_plus_level) plus_at.push_back((uint32_t)k);
+            if (plus_at.empty() && n) plus_at.push_back(r.below((uint32_t)n));
         }
-        f = joinv(lv, n);
-        if (hash) f += n ? "/#" : "#";
         uint32_t copies = 1;
         if ((hash || plus) && p.p_multi > 0 && r.uni() < p.p_multi) copies += 1 + r.below(p.multi_max ? p.multi_max : 1);
+        bool any_kept = false;
+        for (uint32_t c = 0; c < copies && !any_kept; c++) any_kept = keep(next_id + c);
+        if (!any_kept) {
+            next_id += copies;
+            continue;
+        }
+        Rng tr(sseed);
+        gen_topic(lv, tr, p, z);
+        if (sys) lv.insert(lv.begin(), {"$SYS", "brokers", "emqx@n" + std::to_string(sys_node)});
+        for (uint32_t k : plus_at) lv[k] = "+";
+        f = joinv(lv, n);
+        if (hash) f += n ? "/#" : "#";
         for (uint32_t c = 0; c < copies; c++, next_id++) {
             if (!keep(next_id)) continue;
             fb.insert(fb.end(), f.begin(), f.end());

@@ -131,14 +131,68 @@ class ShardedIndex:
         return off, merged, st
 
     # ---- device path (RCCL over xGMI)
-    def match_device(self, eng: "N.Engine", d_bytes: int, d_off: int, n: int, total_bytes: int):
-        """GPU path: local walk, ids compacted on device, RCCL all-gathers, device merge.
-        The engine calls and the torch ops between them all run on ONE torch stream (the
-        engine's own stream is non-blocking, so torch's legacy default stream would not
-        order after it); the caller's current stream waits for it before this returns.
-        Returns device tensors (off[n+1] i32, ids i64 holding u64 route ids)."""
+    def prepare_device(self, eng: "N.Engine", d_bytes: int, d_off: int, n: int, total_bytes: int,
+                       headroom: float = 1.25):
+        """Size this rank's output arena and the exchange stride from one synchronous run of
+        the batch (collective when world > 1).  Not part of the step: the step itself never
+        waits on the host; a later batch that outgrows these sizes is flagged on the device
+        (match_device's third result) and re-run by the caller after prepare_device."""
         import torch
         import torch.distributed as dist
+        dev = torch.device("cuda", torch.cuda.current_device())
+        torch.cuda.current_stream().synchronize()
+        r = eng.match_device(d_bytes, d_off, n, total_bytes, 0)
+        eng.device_sync()  # also sizes the chunk pools to this batch's demand
+        total = _read_u64(r.d_total)
+        eng.reserve_matches(int(total * headroom) + 1024)
+        t = torch.tensor([total], dtype=torch.int64, device=dev)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        self.stride = int(int(t.item()) * headroom) + 1024
+        return total
+
+    def local_device(self, eng: "N.Engine", d_bytes: int, d_off: int, n: int, total_bytes: int, sp: int):
+        """This rank's half of the step, queued on stream `sp` with no host sync: the walk,
+        then the route ids compacted topic-major (tm_result_ids_device_ex).  Returns
+        (cnt_ext i32[n+1]: per-topic counts + the TM_RES_* overflow flags, ids i64[stride])."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        eng.match_device(d_bytes, d_off, n, total_bytes, sp)
+        lo = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        ids = torch.empty(self.stride, dtype=torch.int64, device=dev)
+        cnt_ext = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        eng.result_ids_device_ex(ids.data_ptr(), self.stride, lo.data_ptr(), cnt_ext[n:].data_ptr(), sp)
+        torch.sub(lo[1:], lo[:-1], out=cnt_ext[:n])
+        return cnt_ext, ids
+
+    def merge_device(self, eng: "N.Engine", C_ext, Ids, G: int, n: int, sp: int):
+        """Concatenate G shards' slices per topic on the device.  C_ext: (G, n+1) i32 (counts
+        + flags rows), Ids: (G * stride) i64.  Returns (off i32[n+1], ids i64 buffer whose first
+        off[n] entries are the result, flags i32[1]: nonzero if any shard overflowed)."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        C = C_ext[:, :n].contiguous()
+        flags = C_ext[:, n].max().reshape(1)
+        out_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        cap = G * self.stride
+        out_ids = torch.empty(cap, dtype=torch.int64, device=dev)
+        eng.merge_shards_device(G, n, C.data_ptr(), Ids.data_ptr(), self.stride, out_off.data_ptr(),
+                                out_ids.data_ptr(), cap, sp)
+        return out_off, out_ids, flags
+
+    def match_device(self, eng: "N.Engine", d_bytes: int, d_off: int, n: int, total_bytes: int):
+        """GPU step: local walk, ids compacted on device, RCCL all-gathers of the counts and of
+        the ids (padded to the stride prepare_device fixed), device merge.  Nothing in it
+        waits on the host.  The engine calls and the torch ops between them run on ONE torch
+        stream (the engine's own stream is non-blocking, so torch's legacy default stream
+        would not order after it); the caller's current stream waits for it before this
+        returns.  Returns device tensors (off i32[n+1], ids i64 buffer holding off[n] u64
+        route ids, flags i32[1]); flags != 0 means a shard outgrew its sizes: call
+        prepare_device again and re-run the batch."""
+        import torch
+        import torch.distributed as dist
+        if getattr(self, "stride", None) is None:
+            self.prepare_device(eng, d_bytes, d_off, n, total_bytes)
         dev = torch.device("cuda", torch.cuda.current_device())
         caller = torch.cuda.current_stream()
         if getattr(self, "_stream", None) is None:
@@ -147,36 +201,19 @@ class ShardedIndex:
         s.wait_stream(caller)  # the topic batch was written on the caller's stream
         sp = s.cuda_stream
         with torch.cuda.stream(s):
-            r = eng.match_device(d_bytes, d_off, n, total_bytes, sp)
-            eng.device_sync()
-            total = _read_u64(r.d_total)
-            if total > r.keys_cap:
-                eng.reserve_matches(int(total * 1.1) + 1024)
-                r = eng.match_device(d_bytes, d_off, n, total_bytes, sp)
-                eng.device_sync()
-                total = _read_u64(r.d_total)
-            loc_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-            maxT = torch.tensor([total], dtype=torch.int64, device=dev)
+            cnt_ext, ids = self.local_device(eng, d_bytes, d_off, n, total_bytes, sp)
             if self.world > 1:
-                dist.all_reduce(maxT, op=dist.ReduceOp.MAX, group=self.group)
-            stride = max(int(maxT.item()), 1)
-            mine = torch.zeros(stride, dtype=torch.int64, device=dev)
-            eng.result_ids_device(mine.data_ptr(), stride, loc_off.data_ptr(), sp)
-            cnt = (loc_off[1:] - loc_off[:-1]).contiguous()
-            if self.world > 1:
-                C = torch.empty(self.world * n, dtype=torch.int32, device=dev)
-                dist.all_gather_into_tensor(C, cnt, group=self.group)
-                Ids = torch.empty(self.world * stride, dtype=torch.int64, device=dev)
-                dist.all_gather_into_tensor(Ids, mine, group=self.group)
+                C = torch.empty(self.world * (n + 1), dtype=torch.int32, device=dev)
+                dist.all_gather_into_tensor(C, cnt_ext, group=self.group)
+                Ids = torch.empty(self.world * self.stride, dtype=torch.int64, device=dev)
+                dist.all_gather_into_tensor(Ids, ids, group=self.group)
             else:  # one shard: the exchange is the identity
-                C, Ids = cnt, mine
-            out_total = int(C.to(torch.int64).sum().item())
-            out_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-            out_ids = torch.empty(max(out_total, 1), dtype=torch.int64, device=dev)
-            eng.merge_shards_device(self.world, n, C.data_ptr(), Ids.data_ptr(), stride, out_off.data_ptr(),
-                                    out_ids.data_ptr(), out_total, sp)
+                C, Ids = cnt_ext, ids
+            out = self.merge_device(eng, C.view(self.world, n + 1), Ids, self.world, n, sp)
         caller.wait_stream(s)
-        return out_off, out_ids[:out_total]
+        for t in out:
+            t.record_stream(caller)  # consumed on the caller's stream from here on
+        return out
 
 
 def _read_u64(ptr: int) -> int:

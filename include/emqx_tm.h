@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define TM_ABI_VERSION 4u
+#define TM_ABI_VERSION 5u
 
 /* status codes */
 #define TM_OK          0
@@ -96,7 +96,9 @@ extern "C" {
 #define TM_SHARED_ID(group, member) (TM_ID_SHARED | ((uint64_t)(group) << 32) | (uint32_t)(member))
 
 /* tm_config.flags */
-#define TM_CFG_FORCE_SLOW 1u  /* route every topic through the spill (slow) kernel: test aid */
+#define TM_CFG_FORCE_SLOW   1u  /* route every topic through the spill (slow) kernel: test aid */
+#define TM_CFG_RECORD_PATCH 2u  /* master of a replicated index: every commit records the device
+                                   changes it made as an epoch patch (tm_patch_export) */
 
 typedef struct tm_engine tm_engine;
 
@@ -225,6 +227,16 @@ int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap);
  * to a #route{}).  Asynchronous on `stream` (NULL: the batch's stream).  Topics whose ids
  * would pass ids_cap are left unwritten: size d_ids from *d_total. */
 int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off, void *stream);
+/* tm_result_ids_device that also reports, ON THE DEVICE, whether the result is complete, so
+ * a pipeline (the filter-sharded step, the batching aggregator) never waits on the host
+ * between the walk and the next stage: d_flags[0] (one u32) := TM_RES_KEYS_OVERFLOW when the
+ * walk asked for more keys than its output arena holds (*d_total > keys_cap: no ids are
+ * written; re-run after tm_reserve_matches), | TM_RES_IDS_OVERFLOW when d_off[n] > ids_cap;
+ * 0 when every id is in d_ids. */
+#define TM_RES_KEYS_OVERFLOW 1u
+#define TM_RES_IDS_OVERFLOW  2u
+int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off, uint32_t *d_flags,
+                            void *stream);
 
 /* Filter-sharded mode: G shards matched the same n topics against disjoint
  * key sets; shard r's compacted result (tm_result_ids_device) is counts[r*n .. r*n+n) and
@@ -238,6 +250,32 @@ int tm_merge_shards_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_
                            void *stream);
 int tm_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,
                     uint32_t *out_off, uint64_t *out_ids, uint64_t out_cap);
+
+/* Replicated mode (DESIGN.md §6 mode 1).  The reference keeps one full route table per node,
+ * replicated by mria (emqx_router.erl:133-162) and fed by one syncer per node
+ * (emqx_router_syncer.erl:244-280).  Here ONE master engine per node holds the host master
+ * copy and applies the route ops; every other GPU holds a READ REPLICA: the master's frozen
+ * device index, copied device to device (RCCL broadcast over xGMI, or a peer copy), with no
+ * host copy of its own.  Each commit's device changes travel as an epoch patch.
+ *   tm_image_size / tm_image_export  the committed device index as one contiguous image
+ *                                    (d_dst: device memory on the master's GPU; synchronous)
+ *   tm_replica_create                a read-only engine on cfg->device from an image there
+ *   tm_replica_load                  replace a replica's index with a newer image
+ *   tm_patch_size / tm_patch_export  (master built with TM_CFG_RECORD_PATCH) the last commit's
+ *                                    device changes as host bytes; *full = 1 when that commit
+ *                                    re-uploaded everything: send an image instead
+ *   tm_replica_apply_patch           replay a patch on a replica holding the epoch it was made
+ *                                    from (TM_ESTATE otherwise: reload from an image)
+ * A replica matches (tm_match_batch / tm_match_device*, tm_result_ids_device*) exactly like its
+ * master at the same epoch; writes, tm_match_filter_batch and key introspection return
+ * TM_ESTATE / TM_ENOTFOUND (route ids come back through tm_result_ids_device). */
+int tm_image_size(const tm_engine *eng, uint64_t *bytes);
+int tm_image_export(tm_engine *eng, void *d_dst, uint64_t cap, void *stream);
+int tm_replica_create(const tm_config *cfg, const void *d_image, uint64_t bytes, void *stream, tm_engine **out);
+int tm_replica_load(tm_engine *replica, const void *d_image, uint64_t bytes, void *stream);
+int tm_patch_size(const tm_engine *master, uint64_t *bytes, int *full);
+int tm_patch_export(const tm_engine *master, void *dst, uint64_t cap);
+int tm_replica_apply_patch(tm_engine *replica, const void *patch, uint64_t bytes);
 
 /* matches_filter/3: query i is a topic FILTER, bytes[off[i] .. off[i+1]).  Returns the keys
  * the reference's seek walk (emqx_trie_search.erl:192-258 with the filter-search clauses of

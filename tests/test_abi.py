@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert name in exported, name
         assert getattr(lib, name) is not None
-    assert lib.tm_abi_version() == 4
+    assert lib.tm_abi_version() == 5
     assert C.sizeof(N.tm_stats_t) == 15 * 8  # mirrors tm_stats_t in include/emqx_tm.h
 
 

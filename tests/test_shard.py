@@ -162,55 +162,116 @@ def test_sharded_gloo_world2_matches_unsharded_oracle():
         _same_sets(off2, ids2, eoff2, eids2)
 
 
+def _shard_engines_merged(parts, w_topics, oracle_w=None):
+    """GPU: one engine per shard workload in `parts` on cuda:0, each through the real
+    per-rank step (ShardedIndex.local_device: walk + tm_result_ids_device_ex, no host sync),
+    the all-gather replaced by stacking (what RCCL's all-gather produces), then the real
+    device merge (ShardedIndex.merge_device).  Returns host (off, ids, flags)."""
+    import torch
+    G = len(parts)
+    n = w_topics.n_topics
+    dev = torch.device("cuda", 0)
+    d_bytes = torch.from_numpy(w_topics.t_bytes).to(dev)
+    d_off = torch.from_numpy(w_topics.t_off.view(np.int32)).to(dev)
+    tb = int(w_topics.t_off[-1])
+    engs, sixs = [], []
+    for r, part in enumerate(parts):
+        eng = N.Engine(0)
+        eng.apply_packed(N.TM_OP_ADD, part.f_bytes, part.f_off, part.f_id)
+        eng.commit()
+        six = S.ShardedIndex(S.EngineShard(eng), r, G)
+        engs.append(eng)
+        sixs.append(six)
+    torch.cuda.synchronize()
+    stride = max(six.prepare_device(e, d_bytes.data_ptr(), d_off.data_ptr(), n, tb) for six, e in zip(sixs, engs))
+    stride = int(stride * 1.25) + 1024
+    cs, ids = [], []
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        for six, e in zip(sixs, engs):
+            six.stride = stride  # what prepare_device's all-reduce(max) gives every rank
+            c, i = six.local_device(e, d_bytes.data_ptr(), d_off.data_ptr(), n, tb, s.cuda_stream)
+            cs.append(c)
+            ids.append(i)
+        C = torch.stack(cs).contiguous()
+        Ids = torch.cat(ids)
+        off, out, flags = sixs[0].merge_device(engs[0], C, Ids, G, n, s.cuda_stream)
+    torch.cuda.synchronize()
+    o = off.cpu().numpy().view(np.uint32)
+    res = (o, out[:int(o[-1])].cpu().numpy().view(np.uint64), int(flags.item()),
+           C[:, :n].cpu().numpy().view(np.uint32), Ids.view(G, stride).cpu().numpy().view(np.uint64))
+    for e in engs:
+        e.close()
+    return res
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("G", [1, 2, 3])
 def test_sharded_device_merge_gpu(G):
-    import torch
     w = workloads.generate("B", scale=0.05, n_topics=20000)
-    n = w.n_topics
-    dev = torch.device("cuda", 0)
-    d_bytes = torch.from_numpy(w.t_bytes).to(dev)
-    d_off = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
-    engs, offs, idss, tots = [], [], [], []
+    parts = []
     for r in range(G):
-        eng = N.Engine(0)
-        six = S.ShardedIndex(S.EngineShard(eng), r, G)
-        six.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
-        six.commit()
-        res = eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, int(w.t_off[-1]), 0)
-        eng.device_sync()
-        total = S._read_u64(res.d_total)
-        if total > res.keys_cap:
-            eng.reserve_matches(total + 1024)
-            res = eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, int(w.t_off[-1]), 0)
-            eng.device_sync()
-        lo = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        ids = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
-        eng.result_ids_device(ids.data_ptr(), max(total, 1), lo.data_ptr(), 0)
-        torch.cuda.synchronize()
-        assert int(lo[-1].item()) == total
-        engs.append(eng)
-        offs.append(lo)
-        idss.append(ids)
-        tots.append(total)
-    stride = max(max(tots), 1)
-    C = torch.stack([(o[1:] - o[:-1]) for o in offs]).contiguous()
-    Ids = torch.zeros((G, stride), dtype=torch.int64, device=dev)
-    for r in range(G):
-        Ids[r, :tots[r]] = idss[r][:tots[r]]
-    out_total = sum(tots)
-    out_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
-    out_ids = torch.empty(max(out_total, 1), dtype=torch.int64, device=dev)
-    engs[0].merge_shards_device(G, n, C.data_ptr(), Ids.data_ptr(), stride, out_off.data_ptr(), out_ids.data_ptr(),
-                                out_total, 0)
-    torch.cuda.synchronize()
-    off = out_off.cpu().numpy().view(np.uint32)
-    ids = out_ids[:out_total].cpu().numpy().view(np.uint64)
+        mask = S.shard_of(w.f_id, G) == r
+        b, o, i, _ = S.select_keys(w.f_bytes, w.f_off, w.f_id, mask)
+        parts.append(workloads.Workload("B", b, o, i, w.t_bytes, w.t_off))
+    off, ids, flags, C, Ids = _shard_engines_merged(parts, w)
+    assert flags == 0
     ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
     eoff, eids, _ = ix.match(w.t_bytes, w.t_off)
     _same_sets(off, ids, eoff, eids)
     # the host merge of the same buffers agrees with the device merge
-    hoff, hids = N.merge_shards(C.cpu().numpy().view(np.uint32), Ids.cpu().numpy().view(np.uint64))
+    hoff, hids = N.merge_shards(C, Ids)
     assert np.array_equal(hoff, off) and np.array_equal(hids, ids)
-    for e in engs:
-        e.close()
+
+
+@pytest.mark.gpu
+def test_config_d_eight_shards_vs_oracle_gpu():
+    """BASELINE configs[3] (config D: 8-level B-generator filters hash-sharded 8 ways): the
+    eight shards exactly as csrc/synth.cpp generates them for ranks 0..7, each on its own
+    engine, merged on the device; compared with the oracle over ALL of D's keys at a scale
+    the oracle finishes in seconds."""
+    scale, nt = 0.002, 20000
+    full = workloads.generate("D", scale=scale, n_topics=nt)
+    parts = [workloads.generate("D", scale=scale, n_topics=nt, shard_count=8, shard_index=r) for r in range(8)]
+    assert sum(p.n_keys for p in parts) == full.n_keys
+    for p in parts:
+        assert np.array_equal(p.t_off, full.t_off) and np.array_equal(p.t_bytes, full.t_bytes)
+    off, ids, flags, _, _ = _shard_engines_merged(parts, full)
+    assert flags == 0
+    ix = oracle.OrderedIndex(full.f_bytes, full.f_off, full.f_id)
+    eoff, eids, _ = ix.match(full.t_bytes, full.t_off, threads=8)
+    assert int(eoff[-1]) > nt  # a real match load, not an empty result
+    _same_sets(off, ids, eoff, eids)
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_config_d_full_size_shard_properties_gpu():
+    """One full-size config-D shard (12.5 M of the 100 M keys: what one of 8 GPUs holds)
+    under a 200 K-publish batch: COUNT-mode counts equal ALL-mode counts, statuses agree,
+    FIRST finds a key exactly where ALL finds any, every id returned belongs to shard 0, and
+    a 2,000-topic sample is bit-exact against the oracle over this shard's keys."""
+    import torch
+    w = workloads.generate("D", scale=1.0, n_topics=200_000, shard_count=8, shard_index=0)
+    assert w.n_keys > 12_000_000
+    eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    off_a, cnt_a, keys_a, st_a = eng.match_packed(w.t_bytes, w.t_off, N.TM_MATCH_ALL)
+    _, cnt_c, _, st_c = eng.match_packed(w.t_bytes, w.t_off, N.TM_MATCH_COUNT)
+    _, cnt_f, _, st_f = eng.match_packed(w.t_bytes, w.t_off, N.TM_MATCH_FIRST)
+    assert np.array_equal(cnt_a, cnt_c) and np.array_equal(st_a, st_c) and np.array_equal(st_a, st_f)
+    assert np.array_equal(cnt_f, (cnt_a > 0).astype(cnt_f.dtype))
+    assert int(cnt_a.sum()) > w.n_topics
+    ids = eng.key_ids(keys_a)
+    assert (S.shard_of(ids, 8) == 0).all()
+    ps = 2000
+    sub = workloads.Workload("D", w.f_bytes, w.f_off, w.f_id, w.t_bytes, w.t_off[:ps + 1])
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    eo, eids, est = ix.match(sub.t_bytes, sub.t_off, threads=8)
+    assert np.array_equal(st_a[:ps], est)
+    for t in range(ps):
+        got = np.sort(ids[off_a[t]:off_a[t] + cnt_a[t]])
+        assert np.array_equal(got, eids[eo[t]:eo[t + 1]]), t
+    eng.close()
+    torch.cuda.synchronize()
