@@ -115,12 +115,13 @@ class tm_stats_t(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "epoch", "n_keys", "n_nodes", "n_words", "edge_slots", "word_slots", "list_words",
         "device_bytes", "n_full_rebuilds", "n_delta_commits", "n_slow_topics",
-        "commit_apply_us", "commit_lists_us", "commit_upload_us", "n_deep_keys")]
+        "commit_apply_us", "commit_lists_us", "commit_upload_us", "n_deep_keys", "n_filter_onepass",
+        "n_filter_twopass")]
 
 
 class tm_batcher_config(C.Structure):
     _fields_ = [("max_batch", C.c_uint32), ("max_wait_us", C.c_uint32), ("mode", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("delivery_threads", C.c_uint32)]
 
 
 class tm_batch_view(C.Structure):
@@ -539,9 +540,9 @@ class Batcher:
     Python batch matcher; the C-ABI's tm_batcher_create_fn)."""
 
     def __init__(self, engine: "Engine | None" = None, *, backend=None, max_batch: int = 0, max_wait_us: int = 0,
-                 mode: int = TM_MATCH_ALL):
+                 mode: int = TM_MATCH_ALL, delivery_threads: int = 0):
         self.lib = load()
-        cfg = tm_batcher_config(max_batch, max_wait_us, mode, 0)
+        cfg = tm_batcher_config(max_batch, max_wait_us, mode, delivery_threads)
         h = C.c_void_p()
         self._keep = []
         if engine is not None:

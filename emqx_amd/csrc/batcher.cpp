@@ -3,20 +3,30 @@
 // Reference behaviour it stands in for: emqx_broker:do_publish/1 calls
 // emqx_router:match_routes/1 once per publish, synchronously, in the publisher's own process
 // (apps/emqx/src/emqx_broker.erl:285-290, apps/emqx/src/emqx_router.erl:205-212).  Here many
-// publishers queue single topics; one worker thread cuts the queue into windows
-// (max_batch publishes or max_wait_us since the oldest, whichever comes first), runs ONE
-// engine batch per window and calls every publisher back with its own id list.  While it
-// runs a window, the next one fills.
+// publishers queue single topics and the aggregator answers each with its own id list, one
+// engine batch per WINDOW (max_batch publishes or max_wait_us since the oldest).
 //
-// The engine backend keeps the whole batch on the GPU until the ids are final:
-// tm_match_device_mode (walk + optional reducer) -> tm_result_ids_device (key handles ->
-// route ids, topic-major) -> one D2H of offsets, ids and statuses.
+// Pipeline (engine backend), three stages that overlap across consecutive windows:
+//   1. the cutter thread takes a window from the submission shards straight into a pinned
+//      staging slot and queues its whole GPU part on the compute stream: H2D of the topics,
+//      the walk (tm_match_device_mode), ids compacted topic-major (tm_result_ids_device), and
+//      D2H of the offsets, statuses and the batch's counter block;
+//   2. the completion thread waits for that, then copies the ids back on a separate copy
+//      stream (so window k's PCIe transfer overlaps window k+1's walk);
+//   3. the delivery threads call every publisher of the window back, in parallel (each
+//      thread owns a contiguous range of the window); the completion thread is one of them.
+// Two slots alternate, so window k+1 runs on the GPU while window k is delivered.
+// Submissions go to one of SHARDS queue shards (by submitting thread), so publishers that
+// resubmit from their callbacks do not all contend on one lock.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -25,6 +35,10 @@
 #include "../../include/emqx_tm_batcher.h"
 
 extern "C" int tmx_engine_device(const tm_engine *eng);  // engine.cpp, library-internal
+extern "C" int tmx_engine_grow_pools(tm_engine *eng, uint64_t seg_demand, uint64_t fr_demand);
+extern "C" void tmx_engine_pool_caps(const tm_engine *eng, uint64_t *seg_chunks, uint64_t *fr_chunks);
+extern "C" int tmx_result_ids32_device(tm_engine *eng, uint32_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
+                                       void *stream);
 
 namespace {
 
@@ -52,15 +66,29 @@ struct DBuf {
         if (p) (void)hipFree(p);
     }
 };
+// pinned host memory (engine backend: DMA-able), or plain memory for a custom backend
 struct HBuf {
     void *p = nullptr;
     size_t cap = 0;
-    hipError_t ensure(size_t bytes) {
-        if (bytes <= cap) return hipSuccess;
-        if (p) (void)hipHostFree(p);
+    bool pinned = true;
+    void drop() {
+        if (p) {
+            if (pinned) (void)hipHostFree(p);
+            else std::free(p);
+        }
         p = nullptr;
         cap = 0;
+    }
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        drop();
         size_t c = std::max<size_t>(bytes + bytes / 4, 4096);
+        if (!pinned) {
+            p = std::malloc(c);
+            if (!p) return hipErrorOutOfMemory;
+            cap = c;
+            return hipSuccess;
+        }
         hipError_t e = hipHostMalloc(&p, c, hipHostMallocDefault);
         if (e == hipSuccess) cap = c;
         return e;
@@ -69,137 +97,16 @@ struct HBuf {
     T *as() const {
         return (T *)p;
     }
-    ~HBuf() {
-        if (p) (void)hipHostFree(p);
-    }
+    ~HBuf() { drop(); }
 };
 
-#define BT_HIP(E)                              \
-    do {                                       \
+#define BT_HIP(E)                                 \
+    do {                                          \
         if ((E) != hipSuccess) return TM_EDEVICE; \
     } while (0)
 
-// tm_batch_fn over an engine.  Everything is queued on the backend's own stream and
-// the batch waits on it twice: once for the offsets / statuses / demand, once for the ids.
-// Host result buffers alternate between two slots, so a view stays valid until the
-// second-next call.
-struct EngineBackend {
-    tm_engine *eng;
-    int device;
-    hipStream_t stream = nullptr;
-    DBuf d_bytes, d_off, d_ids, d_off_out;
-    HBuf h_bytes, h_off, h_total;
-    struct Slot {
-        HBuf h_off_out, h_ids, h_status, h_cnt;
-        std::vector<uint32_t> cnt;
-        std::vector<uint64_t> ids;  // host path only
-    } slot[2];
-    uint32_t turn = 0;
-
-    ~EngineBackend() {
-        if (stream) (void)hipStreamDestroy(stream);
-    }
-
-    int run(const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode, tm_batch_view *v) {
-        Slot &S = slot[turn++ & 1];
-        BT_HIP(hipSetDevice(device));
-        if (!stream) BT_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        const uint64_t nbytes = (uint64_t)off[n] - off[0];
-        S.cnt.resize(n);
-        BT_HIP(S.h_status.ensure((size_t)n * 4 + 4));
-        BT_HIP(S.h_off_out.ensure((size_t)n * 4 + 4));
-        BT_HIP(S.h_cnt.ensure((size_t)n * 4 + 4));
-        BT_HIP(h_total.ensure(8));
-        BT_HIP(h_bytes.ensure(nbytes + 16));
-        BT_HIP(h_off.ensure((size_t)n * 4 + 4));
-        std::memcpy(h_bytes.p, bytes + off[0], nbytes);
-        for (uint32_t i = 0; i <= n; i++) h_off.as<uint32_t>()[i] = off[i] - off[0];
-        BT_HIP(d_bytes.ensure(nbytes + 16));
-        BT_HIP(d_off.ensure((size_t)n * 4 + 4));
-        BT_HIP(d_off_out.ensure((size_t)n * 4 + 4));
-        BT_HIP(hipMemcpyAsync(d_bytes.p, h_bytes.p, nbytes + 1, hipMemcpyHostToDevice, stream));
-        BT_HIP(hipMemcpyAsync(d_off.p, h_off.p, (size_t)n * 4 + 4, hipMemcpyHostToDevice, stream));
-        const bool ids_mode = mode != TM_MATCH_COUNT;
-        uint32_t *oo = S.h_off_out.as<uint32_t>();
-        tm_dev_result r;
-        int rc = 0;
-        for (int attempt = 0;; attempt++) {
-            rc = tm_match_device_mode(eng, (const uint8_t *)d_bytes.p, (const uint32_t *)d_off.p, n, nbytes, mode,
-                                      stream, &r);
-            if (rc == TM_ESTATE && mode == TM_MATCH_UNIQUE) return run_host(S, bytes, off, n, mode, v);
-            if (rc) return rc;
-            *h_total.as<uint64_t>() = 0;
-            if (ids_mode) {
-                // key handles -> ids, compacted topic-major; a batch past keys_cap is re-run
-                const uint64_t cap = mode == TM_MATCH_FIRST ? n : r.keys_cap;
-                BT_HIP(d_ids.ensure(cap * 8 + 8));
-                if ((rc = tm_result_ids_device(eng, (uint64_t *)d_ids.p, cap, (uint32_t *)d_off_out.p, stream)))
-                    return rc;
-                BT_HIP(hipMemcpyAsync(oo, d_off_out.p, (size_t)n * 4 + 4, hipMemcpyDeviceToHost, stream));
-                if (mode != TM_MATCH_FIRST)
-                    BT_HIP(hipMemcpyAsync(h_total.p, r.d_total, 8, hipMemcpyDeviceToHost, stream));
-            } else {
-                BT_HIP(hipMemcpyAsync(S.h_cnt.p, r.d_cnt, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
-            }
-            BT_HIP(hipMemcpyAsync(S.h_status.p, r.d_status, (size_t)n * 4, hipMemcpyDeviceToHost, stream));
-            if ((rc = tm_device_sync(eng))) return rc;  // waits on `stream`; sizes the engine's pools
-            const uint64_t total = *h_total.as<uint64_t>();
-            if (total <= r.keys_cap) break;
-            if (attempt || (rc = tm_reserve_matches(eng, total + total / 8 + 1024, 0))) return rc ? rc : TM_EDEVICE;
-        }
-        v->status = S.h_status.as<int32_t>();
-        if (!ids_mode) {
-            std::memset(oo, 0, (size_t)n * 4);
-            v->off = oo;
-            v->cnt = S.h_cnt.as<uint32_t>();
-            v->ids = nullptr;
-            return TM_OK;
-        }
-        const uint64_t got = oo[n];
-        BT_HIP(S.h_ids.ensure(got * 8 + 8));
-        if (got) {
-            BT_HIP(hipMemcpyAsync(S.h_ids.p, d_ids.p, got * 8, hipMemcpyDeviceToHost, stream));
-            BT_HIP(hipStreamSynchronize(stream));
-        }
-        for (uint32_t i = 0; i < n; i++) S.cnt[i] = oo[i + 1] - oo[i];
-        v->off = oo;
-        v->cnt = S.cnt.data();
-        v->ids = S.h_ids.as<uint64_t>();
-        return TM_OK;
-    }
-
-    // UNIQUE over keys deeper than the device order code: tm_match_batch reduces on the host
-    int run_host(Slot &S, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode, tm_batch_view *v) {
-        tm_result res;
-        int rc = tm_match_batch(eng, bytes, off, n, mode, &res);
-        if (rc) return rc;
-        std::vector<uint64_t> &ids = S.ids;
-        std::vector<uint32_t> &cnt = S.cnt;
-        ids.resize(res.total);
-        uint32_t *oo = S.h_off_out.as<uint32_t>();
-        uint64_t pos = 0;
-        for (uint32_t i = 0; i < n; i++) {
-            oo[i] = (uint32_t)pos;
-            cnt[i] = res.cnt[i];
-            if (res.cnt[i] && (rc = tm_key_ids(eng, res.keys + res.off[i], res.cnt[i], ids.data() + pos))) return rc;
-            pos += res.cnt[i];
-        }
-        oo[n] = (uint32_t)pos;
-        std::memcpy(S.h_status.p, res.status, (size_t)n * 4);
-        v->off = oo;
-        v->cnt = cnt.data();
-        v->ids = ids.data();
-        v->status = S.h_status.as<int32_t>();
-        return TM_OK;
-    }
-};
-
-int engine_batch(void *be, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode, tm_batch_view *out) {
-    return static_cast<EngineBackend *>(be)->run(bytes, off, n, mode, out);
-}
-
 struct Pending {
-    uint32_t off, len;  // the topic's bytes in the queue's byte buffer
+    uint32_t len;
     tm_match_cb cb;
     void *ctx;
     uint64_t t0;  // submit time (ns)
@@ -207,100 +114,476 @@ struct Pending {
 
 constexpr size_t LAT_RING = 65536;
 constexpr size_t QUEUE_BYTES_MAX = 1ull << 31;
+constexpr uint32_t SHARDS = 16;
+constexpr uint32_t NSLOT = 2;
+constexpr uint32_t CTL_BYTES = 32;  // the engine's per-launch counter block {total, slow, seg, fr}
+
+struct alignas(64) Shard {
+    std::mutex m;
+    std::vector<uint8_t> bytes;
+    std::vector<Pending> q;
+    std::atomic<uint32_t> n{0};  // q.size(), readable without the lock (the cutter's polls)
+};
+
+uint32_t shard_of_thread() {
+    static std::atomic<uint32_t> next{0};
+    thread_local uint32_t me = next.fetch_add(1) % SHARDS;
+    return me;
+}
+
+// One window in flight: its publishers, its host/device buffers and its result view.
+struct Slot {
+    enum State { FREE, BUSY } state = FREE;
+    std::vector<Pending> pubs;
+    uint32_t n = 0;
+    uint32_t mode = 0;
+    int rc = 0;
+    uint64_t t_enq = 0;
+    // engine backend
+    HBuf h_bytes, h_off, h_off_out, h_status, h_cnt, h_ids, h_ctl;
+    DBuf d_bytes, d_off, d_ids, d_off_out;
+    uint64_t nbytes = 0, ids_cap = 0, keys_cap = 0;
+    hipEvent_t ev = nullptr;
+    bool narrow = false;                // ids crossed PCIe as u32 (every id < 2^32); widened at delivery
+    bool host_done = false;             // the result was produced synchronously (custom / host path)
+    std::vector<uint32_t> cnt;          // per-publish counts
+    std::vector<uint64_t> ids_host;     // host-path ids
+    tm_batch_view v{};
+};
 
 }  // namespace
 
 struct tm_batcher {
     tm_batch_fn fn = nullptr;
     void *backend = nullptr;
-    EngineBackend *eb = nullptr;  // owned when the batcher runs over an engine
+    tm_engine *eng = nullptr;  // engine backend (else fn/backend)
     tm_batcher_config cfg{};
+    uint32_t n_delivery = 4;
 
-    std::mutex mu;  // queue, stats
-    std::condition_variable cv;
-    std::vector<uint8_t> qbytes;
-    std::vector<Pending> q;
-    bool stopping = false;
+    Shard shards[SHARDS];
+    std::mutex wake_mu;  // cutter sleep/wake
+    std::condition_variable wake_cv;
+    std::atomic<bool> stopping{false};
+    std::atomic<uint32_t> cutter_idle{0};  // 1 while the cutter sleeps on an empty queue
 
-    std::mutex eng_mu;  // backend calls vs tm_batcher_apply / tm_batcher_commit
+    std::mutex eng_mu;  // engine calls: enqueue of a window vs tm_batcher_apply / commit
+    hipStream_t s_comp = nullptr, s_copy = nullptr;
+    int device = 0;
 
-    std::thread worker;
+    Slot slot[NSLOT];
+    std::mutex slot_mu;  // slot states + completion FIFO
+    std::condition_variable slot_cv;
+    std::deque<uint32_t> fifo;  // slots queued for completion, in window order
+    bool cutter_done = false;   // under slot_mu
 
+    std::thread cutter, completer;
+    std::vector<std::thread> pool;
+    // delivery jobs: one window split in n_delivery + 1 ranges
+    std::mutex job_mu;
+    std::condition_variable job_cv, job_done_cv;
+    Slot *job_slot = nullptr;
+    uint64_t job_gen = 0;
+    uint32_t job_left = 0;
+    bool pool_stop = false;
+
+    std::mutex st_mu;  // stats
     uint64_t n_batches = 0, n_pub = 0, max_seen = 0, backend_ns = 0;
-    std::vector<uint32_t> lat_ns;  // ring of submit -> callback latencies (ns, saturating)
+    std::vector<uint32_t> lat_ns;
     size_t lat_pos = 0, lat_n = 0;
 
-    // One thread cuts windows, runs the backend and calls the publishers back.  (A
-    // separate delivery thread overlapping batch k's callbacks with batch k+1 was measured
-    // slower under closed-loop load: the population splits into two half-size windows and
-    // the fixed per-batch cost doubles)
-    void loop() {
-        std::vector<uint8_t> bbytes;
-        std::vector<Pending> batch;
-        std::vector<uint32_t> offs, lats;
-        std::unique_lock<std::mutex> lk(mu);
+    // ------------------------------------------------------------------ submit side
+    // No state shared by all submitters on this path: one shard lock (shards by submitting
+    // thread) and a read of the cutter's idle flag.
+    int submit(const uint8_t *topic, uint32_t len, tm_match_cb cb, void *ctx) {
+        const uint64_t t0 = now_ns();
+        Shard &sh = shards[shard_of_thread()];
+        {
+            std::lock_guard<std::mutex> g(sh.m);
+            // checked under the shard lock: the cutter's last pass over this shard comes after
+            // `stopping` is set, so a publish either lands before that pass or is refused here
+            if (stopping.load()) return TM_ESTATE;
+            if (sh.bytes.size() + len > QUEUE_BYTES_MAX / SHARDS) return TM_ENOMEM;  // back-pressure
+            sh.q.push_back(Pending{len, cb, ctx, t0});
+            sh.bytes.insert(sh.bytes.end(), topic, topic + len);
+            sh.n.store((uint32_t)sh.q.size(), std::memory_order_relaxed);
+        }
+        if (cutter_idle.load()) {
+            std::lock_guard<std::mutex> g(wake_mu);
+            wake_cv.notify_one();
+        }
+        return TM_OK;
+    }
+
+    uint64_t queued_now() const {
+        uint64_t n = 0;
+        for (const Shard &sh : shards) n += sh.n.load(std::memory_order_relaxed);
+        return n;
+    }
+
+    uint64_t oldest_t0() {
+        uint64_t t = ~0ull;
+        for (Shard &sh : shards) {
+            std::lock_guard<std::mutex> g(sh.m);
+            if (!sh.q.empty()) t = std::min(t, sh.q.front().t0);
+        }
+        return t;
+    }
+
+    // Move up to max_batch queued publishes into slot S (bytes into its pinned staging).
+    int take_window(Slot &S) {
+        S.pubs.clear();
+        uint64_t nb = 0;
+        // sizes first (the shards keep filling; we take what is there now)
+        for (Shard &sh : shards) {
+            std::lock_guard<std::mutex> g(sh.m);
+            nb += sh.bytes.size();
+        }
+        S.n = 0;
+        BT_HIP(S.h_bytes.ensure(nb + 64));
+        BT_HIP(S.h_off.ensure(((size_t)cfg.max_batch + 1) * 4));
+        uint8_t *dst = S.h_bytes.as<uint8_t>();
+        uint64_t at = 0, taken_bytes = 0;
+        static thread_local uint32_t rot = 0;
+        rot++;
+        for (uint32_t k = 0; k < SHARDS && S.pubs.size() < cfg.max_batch; k++) {
+            Shard &sh = shards[(rot + k) % SHARDS];
+            std::lock_guard<std::mutex> g(sh.m);
+            if (sh.q.empty()) continue;
+            size_t take = std::min<size_t>(sh.q.size(), cfg.max_batch - S.pubs.size());
+            uint64_t tb = 0;
+            for (size_t i = 0; i < take; i++) tb += sh.q[i].len;
+            if (at + tb > nb + 64) {  // grew since sizing: take what fits
+                take = 0;
+                tb = 0;
+                while (take < sh.q.size() && at + tb + sh.q[take].len <= nb + 64 && S.pubs.size() + take < cfg.max_batch)
+                    tb += sh.q[take++].len;
+            }
+            std::memcpy(dst + at, sh.bytes.data(), tb);
+            at += tb;
+            S.pubs.insert(S.pubs.end(), sh.q.begin(), sh.q.begin() + (ptrdiff_t)take);
+            sh.q.erase(sh.q.begin(), sh.q.begin() + (ptrdiff_t)take);
+            sh.bytes.erase(sh.bytes.begin(), sh.bytes.begin() + (ptrdiff_t)tb);
+            sh.n.store((uint32_t)sh.q.size(), std::memory_order_relaxed);
+            taken_bytes += tb;
+        }
+        (void)taken_bytes;
+        S.n = (uint32_t)S.pubs.size();
+        S.nbytes = at;
+        uint32_t *o = S.h_off.as<uint32_t>();
+        uint32_t pos = 0;
+        for (uint32_t i = 0; i < S.n; i++) {
+            o[i] = pos;
+            pos += S.pubs[i].len;
+        }
+        o[S.n] = pos;
+        return TM_OK;
+    }
+
+    // ------------------------------------------------------------------ engine backend
+    // Queue window S's GPU part on the compute stream.  Caller holds eng_mu.
+    int enqueue(Slot &S) {
+        const uint32_t n = S.n;
+        S.host_done = false;
+        BT_HIP(hipSetDevice(device));
+        BT_HIP(S.d_bytes.ensure(S.nbytes + 16));
+        BT_HIP(S.d_off.ensure((size_t)n * 4 + 4));
+        BT_HIP(S.d_off_out.ensure((size_t)n * 4 + 4));
+        BT_HIP(S.h_off_out.ensure((size_t)n * 4 + 4));
+        BT_HIP(S.h_status.ensure((size_t)n * 4 + 4));
+        BT_HIP(S.h_cnt.ensure((size_t)n * 4 + 4));
+        BT_HIP(S.h_ctl.ensure(CTL_BYTES));
+        if (!S.ev) BT_HIP(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+        BT_HIP(hipMemcpyAsync(S.d_bytes.p, S.h_bytes.p, S.nbytes + 1, hipMemcpyHostToDevice, s_comp));
+        BT_HIP(hipMemcpyAsync(S.d_off.p, S.h_off.p, (size_t)n * 4 + 4, hipMemcpyHostToDevice, s_comp));
+        tm_dev_result r;
+        int rc = tm_match_device_mode(eng, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes,
+                                      S.mode, s_comp, &r);
+        if (rc) return rc;
+        S.keys_cap = r.keys_cap;
+        std::memset(S.h_ctl.p, 0, CTL_BYTES);
+        // the batch's counter block (total, spills, pool demand): the next launch reuses it
+        BT_HIP(hipMemcpyAsync(S.h_ctl.p, r.d_total, CTL_BYTES, hipMemcpyDeviceToHost, s_comp));
+        if (S.mode == TM_MATCH_COUNT) {
+            BT_HIP(hipMemcpyAsync(S.h_cnt.p, r.d_cnt, (size_t)n * 4, hipMemcpyDeviceToHost, s_comp));
+        } else {
+            S.ids_cap = S.mode == TM_MATCH_FIRST ? n : r.keys_cap;
+            BT_HIP(S.d_ids.ensure(S.ids_cap * 8 + 8));
+            // u32 ids while they fit: half the PCIe bytes, the bottleneck of this path
+            rc = tmx_result_ids32_device(eng, (uint32_t *)S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp);
+            S.narrow = rc == TM_OK;
+            if (rc == TM_ESTATE)
+                rc = tm_result_ids_device(eng, (uint64_t *)S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp);
+            if (rc) return rc;
+            BT_HIP(hipMemcpyAsync(S.h_off_out.p, S.d_off_out.p, (size_t)n * 4 + 4, hipMemcpyDeviceToHost, s_comp));
+        }
+        BT_HIP(hipMemcpyAsync(S.h_status.p, r.d_status, (size_t)n * 4, hipMemcpyDeviceToHost, s_comp));
+        BT_HIP(hipEventRecord(S.ev, s_comp));
+        return TM_OK;
+    }
+
+    // UNIQUE over keys deeper than the device order code: tm_match_batch reduces on the host.
+    // Synchronous; copies the result into the slot (engine memory is reused by the next call).
+    int run_host(Slot &S) {
+        S.narrow = false;
+        BT_HIP(hipStreamSynchronize(s_comp));  // nothing of ours in flight on the engine
+        tm_result res;
+        int rc = tm_match_batch(eng, S.h_bytes.as<uint8_t>(), S.h_off.as<uint32_t>(), S.n, S.mode, &res);
+        if (rc) return rc;
+        S.ids_host.resize(res.total + 1);
+        S.cnt.resize(S.n);
+        BT_HIP(S.h_off_out.ensure((size_t)S.n * 4 + 4));
+        BT_HIP(S.h_status.ensure((size_t)S.n * 4 + 4));
+        uint32_t *oo = S.h_off_out.as<uint32_t>();
+        uint64_t pos = 0;
+        for (uint32_t i = 0; i < S.n; i++) {
+            oo[i] = (uint32_t)pos;
+            S.cnt[i] = res.cnt[i];
+            if (res.cnt[i] && (rc = tm_key_ids(eng, res.keys + res.off[i], res.cnt[i], S.ids_host.data() + pos)))
+                return rc;
+            pos += res.cnt[i];
+        }
+        oo[S.n] = (uint32_t)pos;
+        std::memcpy(S.h_status.p, res.status, (size_t)S.n * 4);
+        S.v = tm_batch_view{oo, S.cnt.data(), S.ids_host.data(), S.h_status.as<int32_t>()};
+        S.host_done = true;
+        return TM_OK;
+    }
+
+    // Completion of an engine window: counter block back -> maybe re-run -> ids D2H -> view.
+    int complete(Slot &S) {
+        if (S.host_done) return TM_OK;
+        BT_HIP(hipEventSynchronize(S.ev));
+        const uint64_t *ctl = S.h_ctl.as<uint64_t>();
+        const uint64_t total = ctl[0], seg = ctl[2], fr = ctl[3];
+        const bool over = (S.mode != TM_MATCH_COUNT && S.mode != TM_MATCH_FIRST) && total > S.keys_cap;
+        uint64_t seg_cap = 0, fr_cap = 0;
+        tmx_engine_pool_caps(eng, &seg_cap, &fr_cap);
+        if (over || seg > seg_cap || fr > fr_cap) {
+            // pools sized to the demand for later windows (only when short: the engine compares)
+            std::lock_guard<std::mutex> g(eng_mu);
+            BT_HIP(hipStreamSynchronize(s_comp));
+            int rc = tmx_engine_grow_pools(eng, seg, fr);
+            if (rc) return rc;
+            if (over) {  // output arena too small: grow to the demand, run this window again
+                if ((rc = tm_reserve_matches(eng, total + total / 8 + 1024, 0))) return rc;
+                if ((rc = enqueue(S))) return rc;
+                BT_HIP(hipEventSynchronize(S.ev));
+                if (S.h_ctl.as<uint64_t>()[0] > S.keys_cap) return TM_EDEVICE;
+            }
+        }
+        S.v.status = S.h_status.as<int32_t>();
+        if (S.mode == TM_MATCH_COUNT) {
+            uint32_t *oo = S.h_off_out.as<uint32_t>();
+            std::memset(oo, 0, (size_t)S.n * 4);
+            S.v.off = oo;
+            S.v.cnt = S.h_cnt.as<uint32_t>();
+            S.v.ids = nullptr;
+            return TM_OK;
+        }
+        const uint32_t *oo = S.h_off_out.as<uint32_t>();
+        const uint64_t got = oo[S.n];
+        const uint64_t w = S.narrow ? 4 : 8;
+        BT_HIP(S.h_ids.ensure(got * w + 8));
+        if (got) {
+            BT_HIP(hipMemcpyAsync(S.h_ids.p, S.d_ids.p, got * w, hipMemcpyDeviceToHost, s_copy));
+            BT_HIP(hipStreamSynchronize(s_copy));
+        }
+        S.cnt.resize(S.n);
+        for (uint32_t i = 0; i < S.n; i++) S.cnt[i] = oo[i + 1] - oo[i];
+        S.v.off = oo;
+        S.v.cnt = S.cnt.data();
+        S.v.ids = S.h_ids.as<uint64_t>();  // u32 words when narrow (deliver_range widens)
+        return TM_OK;
+    }
+
+    // ------------------------------------------------------------------ delivery
+    void deliver_range(Slot &S, uint32_t lo, uint32_t hi) {
+        std::vector<uint32_t> lats;
+        lats.reserve(hi - lo);
+        thread_local std::vector<uint64_t> wide;  // a narrowed window's ids, one publish at a time
+        const uint32_t *ids32 = S.narrow ? reinterpret_cast<const uint32_t *>(S.v.ids) : nullptr;
+        uint64_t now = 0;
+        for (uint32_t i = lo; i < hi; i++) {
+            const Pending &p = S.pubs[i];
+            if (S.rc < 0) {
+                p.cb(p.ctx, S.rc, nullptr, 0);
+            } else {
+                const int32_t st = S.v.status[i];
+                const uint32_t c = st == TM_TOPIC_OK ? S.v.cnt[i] : 0;
+                const uint64_t *ids = nullptr;
+                if (S.v.ids && c) {
+                    if (ids32) {
+                        if (wide.size() < c) wide.resize(c);
+                        const uint32_t *src = ids32 + S.v.off[i];
+                        for (uint32_t k = 0; k < c; k++) wide[k] = src[k];
+                        ids = wide.data();
+                    } else {
+                        ids = S.v.ids + S.v.off[i];
+                    }
+                }
+                p.cb(p.ctx, st, ids, c);
+            }
+            if (((i - lo) & 15) == 0) now = now_ns();  // one clock read per 16 callbacks
+            const uint64_t d = now > p.t0 ? now - p.t0 : 0;
+            lats.push_back(d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d);
+        }
+        std::lock_guard<std::mutex> g(st_mu);
+        for (uint32_t x : lats) {
+            lat_ns[lat_pos] = x;
+            lat_pos = (lat_pos + 1) % LAT_RING;
+        }
+        lat_n = std::min(LAT_RING, lat_n + lats.size());
+    }
+
+    uint32_t parts_for(uint32_t n) const {
+        // small windows are not worth waking the pool for
+        return std::max<uint32_t>(1, std::min<uint32_t>(n_delivery + 1, n / 256));
+    }
+
+    void pool_loop(uint32_t idx) {
+        uint64_t seen = 0;
         for (;;) {
-            cv.wait(lk, [&] { return stopping || !q.empty(); });
-            if (q.empty()) break;  // stopping and drained
-            const uint64_t deadline = q.front().t0 + (uint64_t)cfg.max_wait_us * 1000;
-            while (!stopping && q.size() < cfg.max_batch && qbytes.size() < QUEUE_BYTES_MAX / 2) {
+            Slot *S;
+            uint64_t gen;
+            {
+                std::unique_lock<std::mutex> lk(job_mu);
+                job_cv.wait(lk, [&] { return pool_stop || job_gen != seen; });
+                if (pool_stop) return;
+                seen = gen = job_gen;
+                S = job_slot;
+            }
+            const uint32_t parts = parts_for(S->n);
+            if (idx + 1 < parts) {  // part 0 is the completion thread's
+                const uint64_t lo = (uint64_t)S->n * (idx + 1) / parts, hi = (uint64_t)S->n * (idx + 2) / parts;
+                deliver_range(*S, (uint32_t)lo, (uint32_t)hi);
+            }
+            std::lock_guard<std::mutex> g(job_mu);
+            if (--job_left == 0) job_done_cv.notify_all();
+            (void)gen;
+        }
+    }
+
+    void deliver(Slot &S) {
+        const uint32_t parts = parts_for(S.n);
+        if (parts <= 1 || pool.empty()) {
+            deliver_range(S, 0, S.n);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(job_mu);
+            job_slot = &S;
+            job_left = (uint32_t)pool.size();
+            job_gen++;
+        }
+        job_cv.notify_all();
+        deliver_range(S, 0, (uint32_t)((uint64_t)S.n / parts));
+        std::unique_lock<std::mutex> lk(job_mu);
+        job_done_cv.wait(lk, [&] { return job_left == 0; });
+    }
+
+    // ------------------------------------------------------------------ threads
+    void cutter_loop() {
+        uint32_t next = 0;
+        for (;;) {
+            // a window: something queued, and (max_batch queued, or the oldest waited
+            // max_wait_us, or stopping)
+            uint64_t t_old;
+            {
+                std::unique_lock<std::mutex> lk(wake_mu);
+                bool quit = false;
+                for (;;) {
+                    const bool stop = stopping.load();  // before looking at the shards
+                    t_old = oldest_t0();
+                    if (t_old != ~0ull) break;
+                    if (stop) {
+                        quit = true;
+                        break;
+                    }
+                    // idle is published before the check above repeats under wake_mu, and a
+                    // submitter notifies under wake_mu: no wakeup is lost
+                    cutter_idle.store(1);
+                    if (oldest_t0() == ~0ull && !stopping.load()) wake_cv.wait(lk);
+                    cutter_idle.store(0);
+                }
+                if (quit) break;
+            }
+            const uint64_t deadline = t_old + (uint64_t)cfg.max_wait_us * 1000;
+            for (;;) {
+                if (stopping.load() || queued_now() >= cfg.max_batch) break;
                 const uint64_t t = now_ns();
                 if (t >= deadline) break;
-                cv.wait_for(lk, std::chrono::nanoseconds(deadline - t));
+                // polled: a submitter does not signal a filling window (that would put one
+                // shared write on every publish); the wait is bounded by the deadline anyway
+                const uint64_t nap = std::min<uint64_t>(deadline - t, 20000);
+                std::this_thread::sleep_for(std::chrono::nanoseconds(nap));
             }
-            batch.clear();
-            bbytes.clear();
-            batch.swap(q);
-            bbytes.swap(qbytes);
-            if (batch.size() > cfg.max_batch) {  // the tail waits for the next window
-                for (size_t i = cfg.max_batch; i < batch.size(); i++) {
-                    Pending p = batch[i];
-                    const uint8_t *src = bbytes.data() + p.off;
-                    p.off = (uint32_t)qbytes.size();
-                    qbytes.insert(qbytes.end(), src, src + p.len);
-                    q.push_back(p);
-                }
-                batch.resize(cfg.max_batch);
-            }
-            lk.unlock();
-
-            const uint32_t n = (uint32_t)batch.size();
-            offs.resize((size_t)n + 1);
-            for (uint32_t i = 0; i < n; i++) offs[i] = batch[i].off;  // contiguous, in queue order
-            offs[n] = batch[n - 1].off + batch[n - 1].len;
-            tm_batch_view v{};
-            const uint64_t tb = now_ns();
-            int rc;
+            // a free slot (slots complete in order, so the next one in turn)
+            Slot &S = slot[next];
             {
-                std::lock_guard<std::mutex> g(eng_mu);
-                rc = fn(backend, bbytes.data(), offs.data(), n, cfg.mode, &v);
+                std::unique_lock<std::mutex> lk(slot_mu);
+                slot_cv.wait(lk, [&] { return S.state == Slot::FREE; });
+                S.state = Slot::BUSY;
             }
-            const uint64_t te = now_ns();
-            lk.lock();  // counted before the callbacks: a caller woken by one sees its batch
-            n_batches++;
-            n_pub += n;
-            max_seen = std::max<uint64_t>(max_seen, n);
-            backend_ns += te - tb;
-            lk.unlock();
-            lats.resize(n);
-            for (uint32_t i = 0; i < n; i++) {
-                const Pending &p = batch[i];
-                if (rc < 0) {
-                    p.cb(p.ctx, rc, nullptr, 0);
+            S.rc = take_window(S);
+            S.mode = cfg.mode;
+            S.t_enq = now_ns();
+            if (S.rc == TM_OK && S.n) {
+                if (eng) {
+                    std::lock_guard<std::mutex> g(eng_mu);
+                    S.rc = enqueue(S);
+                    if (S.rc == TM_ESTATE && S.mode == TM_MATCH_UNIQUE) S.rc = run_host(S);
                 } else {
-                    const int32_t st = v.status[i];
-                    const uint32_t c = st == TM_TOPIC_OK ? v.cnt[i] : 0;
-                    p.cb(p.ctx, st, (v.ids && c) ? v.ids + v.off[i] : nullptr, c);
+                    // custom backend: synchronous; its view lives until its next call, which
+                    // the slot ordering below delays until this window is delivered
+                    std::lock_guard<std::mutex> g(eng_mu);
+                    S.rc = fn(backend, S.h_bytes.as<uint8_t>(), S.h_off.as<uint32_t>(), S.n, S.mode, &S.v);
+                    S.host_done = true;
+                    S.narrow = false;
                 }
-                const uint64_t d = now_ns() - p.t0;
-                lats[i] = d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
             }
-            lk.lock();
-            for (uint32_t i = 0; i < n; i++) {
-                lat_ns[lat_pos] = lats[i];
-                lat_pos = (lat_pos + 1) % LAT_RING;
+            {
+                std::lock_guard<std::mutex> g(slot_mu);
+                fifo.push_back(next);
             }
-            lat_n = std::min(LAT_RING, lat_n + n);
+            slot_cv.notify_all();
+            // a custom backend's view must be delivered before the next call: one slot at a time
+            next = eng ? (next + 1) % NSLOT : next;
+        }
+        {
+            std::lock_guard<std::mutex> g(slot_mu);
+            cutter_done = true;
+        }
+        slot_cv.notify_all();
+    }
+
+    void completer_loop() {
+        for (;;) {
+            uint32_t si;
+            {
+                std::unique_lock<std::mutex> lk(slot_mu);
+                slot_cv.wait(lk, [&] { return !fifo.empty() || cutter_done; });
+                if (fifo.empty()) break;
+                si = fifo.front();
+                fifo.pop_front();
+            }
+            Slot &S = slot[si];
+            if (S.rc == TM_OK && S.n && eng) S.rc = complete(S);
+            const uint64_t te = now_ns();
+            if (S.n) {
+                {
+                    std::lock_guard<std::mutex> g(st_mu);  // counted before the callbacks
+                    n_batches++;
+                    n_pub += S.n;
+                    max_seen = std::max<uint64_t>(max_seen, S.n);
+                    backend_ns += te - S.t_enq;
+                }
+                deliver(S);
+            }
+            {
+                std::lock_guard<std::mutex> g(slot_mu);
+                S.state = Slot::FREE;
+            }
+            slot_cv.notify_all();
         }
     }
 
@@ -309,10 +592,26 @@ struct tm_batcher {
         if (cfg.max_batch == 0) cfg.max_batch = 65536;
         if (cfg.max_wait_us == 0) cfg.max_wait_us = 200;
         if (cfg.mode > TM_MATCH_AGGRE) return TM_EINVAL;
+        n_delivery = cfg.delivery_threads ? cfg.delivery_threads - 1 : 3;
+        if (n_delivery > 63) return TM_EINVAL;
         lat_ns.assign(LAT_RING, 0);
+        if (!eng)
+            for (Slot &S : slot)
+                for (HBuf *h : {&S.h_bytes, &S.h_off, &S.h_off_out, &S.h_status, &S.h_cnt, &S.h_ids, &S.h_ctl})
+                    h->pinned = false;
+        if (eng) {
+            device = tmx_engine_device(eng);
+            if (hipSetDevice(device) != hipSuccess ||
+                hipStreamCreateWithFlags(&s_comp, hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithFlags(&s_copy, hipStreamNonBlocking) != hipSuccess)
+                return TM_EDEVICE;
+        }
         try {
-            worker = std::thread([this] { loop(); });
+            for (uint32_t i = 0; i < n_delivery; i++) pool.emplace_back([this, i] { pool_loop(i); });
+            completer = std::thread([this] { completer_loop(); });
+            cutter = std::thread([this] { cutter_loop(); });
         } catch (...) {
+            stop();
             return TM_ENOMEM;
         }
         return TM_OK;
@@ -320,21 +619,41 @@ struct tm_batcher {
 
     void stop() {
         {
-            std::lock_guard<std::mutex> g(mu);
+            std::lock_guard<std::mutex> g(wake_mu);
             stopping = true;
         }
-        cv.notify_all();
-        if (worker.joinable()) worker.join();
+        wake_cv.notify_all();
+        if (cutter.joinable()) cutter.join();
+        else {
+            std::lock_guard<std::mutex> g(slot_mu);
+            cutter_done = true;
+        }
+        slot_cv.notify_all();
+        if (completer.joinable()) completer.join();
+        {
+            std::lock_guard<std::mutex> g(job_mu);
+            pool_stop = true;
+        }
+        job_cv.notify_all();
+        for (std::thread &t : pool)
+            if (t.joinable()) t.join();
+        if (eng) {
+            (void)hipSetDevice(device);
+            for (Slot &S : slot)
+                if (S.ev) (void)hipEventDestroy(S.ev);
+            if (s_comp) (void)hipStreamDestroy(s_comp);
+            if (s_copy) (void)hipStreamDestroy(s_copy);
+        }
     }
 };
 
 extern "C" {
 
-int tm_batcher_create_fn(tm_batch_fn fn, void *backend, const tm_batcher_config *cfg, tm_batcher **out) {
-    if (!fn || !out) return TM_EINVAL;
-    *out = nullptr;
+static int batcher_new(tm_engine *eng, tm_batch_fn fn, void *backend, const tm_batcher_config *cfg,
+                       tm_batcher **out) {
     tm_batcher *b = new (std::nothrow) tm_batcher();
     if (!b) return TM_ENOMEM;
+    b->eng = eng;
     b->fn = fn;
     b->backend = backend;
     int rc = b->start(cfg);
@@ -346,42 +665,27 @@ int tm_batcher_create_fn(tm_batch_fn fn, void *backend, const tm_batcher_config 
     return TM_OK;
 }
 
+int tm_batcher_create_fn(tm_batch_fn fn, void *backend, const tm_batcher_config *cfg, tm_batcher **out) {
+    if (!fn || !out) return TM_EINVAL;
+    *out = nullptr;
+    return batcher_new(nullptr, fn, backend, cfg, out);
+}
+
 int tm_batcher_create(tm_engine *eng, const tm_batcher_config *cfg, tm_batcher **out) {
     if (!eng || !out) return TM_EINVAL;
-    EngineBackend *eb = new (std::nothrow) EngineBackend();
-    if (!eb) return TM_ENOMEM;
-    eb->eng = eng;
-    eb->device = tmx_engine_device(eng);
-    int rc = tm_batcher_create_fn(engine_batch, eb, cfg, out);
-    if (rc) {
-        delete eb;
-        return rc;
-    }
-    (*out)->eb = eb;
-    return TM_OK;
+    *out = nullptr;
+    return batcher_new(eng, nullptr, nullptr, cfg, out);
 }
 
 void tm_batcher_destroy(tm_batcher *b) {
     if (!b) return;
     b->stop();  // drains: every queued publish is matched and called back first
-    delete b->eb;
     delete b;
 }
 
 int tm_batcher_submit(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_match_cb cb, void *ctx) {
     if (!b || !cb || (len && !topic) || len > 65535) return TM_EINVAL;
-    const uint64_t t0 = now_ns();
-    bool wake;
-    {
-        std::lock_guard<std::mutex> g(b->mu);
-        if (b->stopping) return TM_ESTATE;
-        if (b->qbytes.size() + len > QUEUE_BYTES_MAX) return TM_ENOMEM;  // back-pressure
-        b->q.push_back(Pending{(uint32_t)b->qbytes.size(), len, cb, ctx, t0});
-        b->qbytes.insert(b->qbytes.end(), topic, topic + len);
-        wake = b->q.size() == 1 || b->q.size() >= b->cfg.max_batch;
-    }
-    if (wake) b->cv.notify_one();
-    return TM_OK;
+    return b->submit(topic, len, cb, ctx);
 }
 
 namespace {
@@ -421,23 +725,25 @@ int tm_batcher_match(tm_batcher *b, const uint8_t *topic, uint32_t len, uint64_t
 
 int tm_batcher_apply(tm_batcher *b, const tm_op *ops, size_t n) {
     if (!b) return TM_EINVAL;
-    if (!b->eb) return TM_ESTATE;
+    if (!b->eng) return TM_ESTATE;
     std::lock_guard<std::mutex> g(b->eng_mu);
-    return tm_apply(b->eb->eng, ops, n);
+    return tm_apply(b->eng, ops, n);
 }
 
 int tm_batcher_commit(tm_batcher *b, uint64_t *epoch_out) {
     if (!b) return TM_EINVAL;
-    if (!b->eb) return TM_ESTATE;
+    if (!b->eng) return TM_ESTATE;
     std::lock_guard<std::mutex> g(b->eng_mu);
-    return tm_commit_epoch(b->eb->eng, epoch_out);
+    // windows already queued on the GPU finish on the old epoch; the next one sees the new
+    if (hipSetDevice(b->device) != hipSuccess || hipStreamSynchronize(b->s_comp) != hipSuccess) return TM_EDEVICE;
+    return tm_commit_epoch(b->eng, epoch_out);
 }
 
 int tm_batcher_stats_get(tm_batcher *b, tm_batcher_stats *out) {
     if (!b || !out) return TM_EINVAL;
     std::vector<uint32_t> lat;
     {
-        std::lock_guard<std::mutex> g(b->mu);
+        std::lock_guard<std::mutex> g(b->st_mu);
         out->batches = b->n_batches;
         out->publishes = b->n_pub;
         out->max_batch_seen = b->max_seen;

@@ -25,6 +25,9 @@ struct MatchArgs {
     uint32_t force_slow;  // 1: every topic takes the spill kernel (test aid)
     uint32_t mode;        // MODE_ALL: every key; MODE_COUNT: counts only; MODE_FIRST: k_match_first
     uint32_t tpw;         // topics per wave of k_match_fast (pick_tpw)
+    uint32_t first_dfs;   // MODE_FIRST: 1 = lane-per-topic DFS (index holds keys deeper than the
+                          // 31-level order code), 0 = k_match_first_wave + k_first_slow
+    uint32_t _pad0;
     // frozen index
     const WordSlot *wtab;
     uint64_t wmask;
@@ -106,6 +109,10 @@ hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const
                              const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
                              uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, uint32_t *flags,
                              hipStream_t stream);
+// the same with the ids narrowed to u32 (every live id < 2^32): half the bytes to move
+hipError_t launch_result_ids32(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
+                               const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint32_t *ids,
+                               uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, hipStream_t stream);
 // Concatenate G shards' topic-major results per topic.  roff: G*(n+1) u32, tot: n u32,
 // scratch: scan_scratch_words(n) u32 (work areas); off: n+1 u32 out; out: merged ids.
 hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,

@@ -314,6 +314,7 @@ struct tm_engine {
     hipStream_t last_stream = nullptr;  // stream of the last tm_match_device call
     uint32_t last_n = 0;                // topics of the last match batch
     bool stats_on = false;
+    uint64_t max_id = 0;     // largest id ever added (ids fit u32 results while < 2^32)
     PatchLog patch;          // master: the last commit's device changes (TM_CFG_RECORD_PATCH)
     uint64_t patch_from = 0; // epoch the recorded patch applies to
     bool replica = false;    // built from a device image: no host master copy, read-only
@@ -654,6 +655,7 @@ struct tm_engine {
             keys[h] = KeyRec{node, kind, {0, 0, 0}, op.id};
             if (deep_shape(kind, depth)) n_deep++;
             id_add(h);
+            max_id = std::max(max_id, op.id);
             dirty_kid.push_back(h);
             kset[slot] = h;
             kset_used++;
@@ -1192,12 +1194,14 @@ struct tm_engine {
         std::vector<std::string> dict;   // sorted distinct literal words of the keys
         uint32_t K = 0;
         DevBuf d_kw, d_koff, d_kh;
-        DevBuf d_qw, d_qoff, d_qdollar, d_qstatus, d_cnt, d_off, d_out, d_scan;
+        DevBuf d_qw, d_qoff, d_qdollar, d_qstatus, d_cnt, d_off, d_out, d_scan, d_pool, d_ctl;
+        uint64_t out_want = 1 << 16, pool_want = 1024;  // one-pass sizes (from the demand seen)
         std::vector<uint32_t> qw, qoff, h_off, h_cnt, u_keys;
         std::vector<uint32_t> wcode;     // interned word id -> order code (NONE: not cached yet)
         PinBuf h_keys;                   // walk output (pinned: it can be GBs)
         std::vector<uint8_t> qdollar;
         std::vector<int32_t> qstatus;
+        uint64_t n_onepass = 0, n_twopass = 0;  // batches by path (tests / bench)
     } fx;
     // intersection/2 batches (filter_kernels.hip k_intersect)
     DevBuf d_ia, d_iaoff, d_ib, d_iboff, d_iout, d_ilen;
@@ -1341,6 +1345,7 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     tm_engine *eng = new (std::nothrow) tm_engine();
     if (!eng) return TM_ENOMEM;
     if (cfg) eng->cfg = *cfg;
+    eng->patch.on = (eng->cfg.flags & TM_CFG_RECORD_PATCH) != 0;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= eng->cfg.device || eng->cfg.device < 0) {
         delete eng;
@@ -1389,7 +1394,8 @@ void tm_destroy(tm_engine *eng) {
                       &eng->d_dd_wl_n, &eng->d_ukeys, &eng->d_ucnt,
                       &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
-                      &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan, &eng->d_ia, &eng->d_iaoff,
+                      &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan, &eng->fx.d_pool,
+                      &eng->fx.d_ctl, &eng->d_ia, &eng->d_iaoff,
                       &eng->d_ib, &eng->d_iboff, &eng->d_iout, &eng->d_ilen})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
@@ -1410,6 +1416,21 @@ void tm_destroy(tm_engine *eng) {
 
 // library-internal (batcher.cpp), not part of the C-ABI
 __attribute__((visibility("hidden"))) int tmx_engine_device(const tm_engine *eng) { return eng->cfg.device; }
+static int grow_pools(tm_engine *eng);
+// library-internal (batcher.cpp): size the chunk pools to a batch's demand (the counter
+// block the batcher copied back); no kernel of this engine may be in flight
+__attribute__((visibility("hidden"))) void tmx_engine_pool_caps(const tm_engine *eng, uint64_t *seg_chunks,
+                                                               uint64_t *fr_chunks) {
+    *seg_chunks = eng->cfg.seg_chunks ? ~0ull : eng->seg_chunks;  // fixed pools (test aid) never grow
+    *fr_chunks = eng->cfg.seg_chunks ? ~0ull : eng->fr_chunks;
+}
+__attribute__((visibility("hidden"))) int tmx_engine_grow_pools(tm_engine *eng, uint64_t seg_demand,
+                                                                uint64_t fr_demand) {
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    eng->seg_demand_last = seg_demand;
+    eng->fr_demand_last = fr_demand;
+    return grow_pools(eng);
+}
 
 const char *tm_last_error(const tm_engine *eng) { return eng ? eng->err.c_str() : "null engine"; }
 
@@ -1526,6 +1547,7 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     MatchArgs a{};
     a.mode = mode;
     a.tpw = pick_tpw(n, eng->cfg.topics_per_wave);
+    a.first_dfs = eng->n_deep ? 1u : 0u;
     a.key_bin = eng->d_key_bin.as<uint32_t>();
     a.bytes = d_bytes;
     a.off = d_off;
@@ -1837,6 +1859,24 @@ int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, u
     return TM_OK;
 }
 
+// library-internal (batcher.cpp): tm_result_ids_device with u32 ids, when every id ever
+// added is below 2^32 (TM_ESTATE otherwise)
+__attribute__((visibility("hidden"))) int tmx_result_ids32_device(tm_engine *eng, uint32_t *d_ids, uint64_t ids_cap,
+                                                                  uint32_t *d_off_out, void *stream) {
+    if (eng->max_id > 0xFFFFFFFFull || eng->replica) return TM_ESTATE;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    hipStream_t s = stream ? (hipStream_t)stream : (eng->last_stream ? eng->last_stream : eng->stream);
+    const uint32_t n = eng->last_n;
+    TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
+    const uint32_t *cnt = (reduced_mode(eng->last_mode) ? eng->d_ucnt : eng->d_outcnt).as<uint32_t>();
+    TM_TRY_HIP(launch_excl_scan(cnt, 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s), TM_EDEVICE, "scan");
+    TM_TRY_HIP(launch_result_ids32(cnt, eng->d_outoff.as<uint32_t>(), eng->d_keys.as<uint32_t>(),
+                                   eng->d_key_rec.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, eng->keys_cap,
+                                   (const unsigned long long *)(eng->p_ctl + CTL_CURSOR), s),
+               TM_EDEVICE, "result ids");
+    return TM_OK;
+}
+
 int tm_merge_shards_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_t *d_counts, const uint64_t *d_ids,
                            uint64_t stride, uint32_t *d_off_out, uint64_t *d_ids_out, uint64_t out_cap, void *stream) {
     if (!eng || G == 0 || !d_off_out || (n && (!d_counts || !d_ids)) || (out_cap && !d_ids_out)) return TM_EINVAL;
@@ -1973,30 +2013,76 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
     a.first = mode == TM_MATCH_FIRST;
     a.cnt = fx.d_cnt.as<uint32_t>();
     a.out_off = fx.d_off.as<uint32_t>();
-    TM_TRY_HIP(launch_filter_walk(a, 0, s), TM_EDEVICE, "k_filter_walk count");
-    TM_TRY_HIP(launch_excl_scan(a.cnt, 1, n, fx.d_off.as<uint32_t>(), fx.d_scan.as<uint32_t>(), s), TM_EDEVICE,
-               "scan");
     fx.h_off.resize((size_t)n + 1);
     fx.h_cnt.resize(n);
-    TM_TRY_HIP(hipMemcpyAsync(fx.h_off.data(), fx.d_off.p, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-               "D2H");
-    TM_TRY_HIP(hipMemcpyAsync(fx.h_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
-    TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk count");
-    // the device scan is u32: a batch whose walks return 4 Gi keys or more is refused
-    // before the emit pass could write past its offsets
     uint64_t total = 0;
-    for (uint32_t i = 0; i < n; i++) total += fx.h_cnt[i];
-    if (total >= 0xFFFFFFFFull) {
-        eng->err = "tm_match_filter_batch: the batch returns 4 Gi keys or more; split it";
-        return TM_ENOMEM;
-    }
-    TM_TRY_HIP(fx.h_keys.ensure(std::max<uint64_t>(total, 1) * 4), TM_ENOMEM, "pinned alloc");
-    if (total) {
-        TM_TRY_HIP(fx.d_out.ensure(total * 4), TM_ENOMEM, "alloc");
+    // One pass: the walk streams its keys into pooled chunks and copies them to a contiguous
+    // range reserved at its end.  Sized from the demand of earlier batches; a batch that does
+    // not fit takes the two-pass path below (count, scan, emit) and sizes the next one.
+    bool done = false;
+    {
+        const uint64_t pool = std::max<uint64_t>(fx.pool_want, (uint64_t)n + 1024);
+        const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(fx.out_want, 1 << 16), 0xFFFFFFF0ull);
+        TM_TRY_HIP(fx.d_pool.ensure(pool * FW_CHUNK * 4), TM_ENOMEM, "alloc filter pool");
+        TM_TRY_HIP(fx.d_out.ensure(cap * 4), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(fx.d_ctl.ensure(16), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(hipMemsetAsync(fx.d_ctl.p, 0, 16, s), TM_EDEVICE, "memset");
+        a.pool = fx.d_pool.as<uint32_t>();
+        a.pool_chunks = fx.d_pool.cap / (FW_CHUNK * 4);
         a.out = fx.d_out.as<uint32_t>();
-        TM_TRY_HIP(launch_filter_walk(a, 1, s), TM_EDEVICE, "k_filter_walk emit");
-        TM_TRY_HIP(hipMemcpyAsync(fx.h_keys.p, fx.d_out.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
-        TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk emit");
+        a.out_cap = fx.d_out.cap / 4;
+        a.ctl = fx.d_ctl.as<unsigned long long>();
+        uint64_t ctl[2] = {0, 0};
+        TM_TRY_HIP(launch_filter_walk(a, FW_ONEPASS, s), TM_EDEVICE, "k_filter_walk");
+        TM_TRY_HIP(hipMemcpyAsync(ctl, fx.d_ctl.p, 16, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(fx.h_off.data(), fx.d_off.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                   "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(fx.h_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                   "D2H");
+        TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk");
+        total = ctl[0];
+        if (total <= a.out_cap && ctl[1] <= a.pool_chunks) {
+            TM_TRY_HIP(fx.h_keys.ensure(std::max<uint64_t>(total, 1) * 4), TM_ENOMEM, "pinned alloc");
+            if (total) {
+                TM_TRY_HIP(hipMemcpyAsync(fx.h_keys.p, fx.d_out.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                           "D2H");
+                TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk");
+            }
+            done = true;
+        }
+        fx.n_onepass += done;
+    }
+    if (!done) {
+        fx.n_twopass++;
+        TM_TRY_HIP(launch_filter_walk(a, FW_COUNT, s), TM_EDEVICE, "k_filter_walk count");
+        TM_TRY_HIP(launch_excl_scan(a.cnt, 1, n, fx.d_off.as<uint32_t>(), fx.d_scan.as<uint32_t>(), s), TM_EDEVICE,
+                   "scan");
+        TM_TRY_HIP(hipMemcpyAsync(fx.h_off.data(), fx.d_off.p, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, s),
+                   TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(fx.h_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                   "D2H");
+        TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk count");
+        // the device scan is u32: a batch whose walks return 4 Gi keys or more is refused
+        // before the emit pass could write past its offsets
+        total = 0;
+        for (uint32_t i = 0; i < n; i++) total += fx.h_cnt[i];
+        if (total >= 0xFFFFFFFFull) {
+            eng->err = "tm_match_filter_batch: the batch returns 4 Gi keys or more; split it";
+            return TM_ENOMEM;
+        }
+        // the next batch's one-pass sizes: this demand with headroom (a query wastes at most
+        // one partly filled chunk)
+        fx.out_want = total + total / 4 + 1024;
+        fx.pool_want = (total / (FW_CHUNK - 1) + n) + (total / (FW_CHUNK - 1) + n) / 4 + 64;
+        TM_TRY_HIP(fx.h_keys.ensure(std::max<uint64_t>(total, 1) * 4), TM_ENOMEM, "pinned alloc");
+        if (total) {
+            TM_TRY_HIP(fx.d_out.ensure(total * 4), TM_ENOMEM, "alloc");
+            a.out = fx.d_out.as<uint32_t>();
+            TM_TRY_HIP(launch_filter_walk(a, FW_EMIT, s), TM_EDEVICE, "k_filter_walk emit");
+            TM_TRY_HIP(hipMemcpyAsync(fx.h_keys.p, fx.d_out.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                       "D2H");
+            TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk emit");
+        }
     }
     out->total = total;
     out->off = fx.h_off.data();
@@ -2096,6 +2182,8 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
     out->commit_lists_us = eng->commit_us[1];
     out->commit_upload_us = eng->commit_us[2];
     out->n_deep_keys = eng->n_deep;
+    out->n_filter_onepass = eng->fx.n_onepass;
+    out->n_filter_twopass = eng->fx.n_twopass;
     return TM_OK;
 }
 

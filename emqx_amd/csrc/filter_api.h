@@ -21,10 +21,18 @@ struct FilterArgs {
     const uint8_t *qdollar;  // 1: the first query word starts with '$' (base_init/1)
     const int32_t *qstatus;  // 0: walk; else skipped (count 0)
     uint32_t first;          // return_first: stop at the first hit
-    uint32_t *cnt;           // pass 0 out: n
-    const uint32_t *out_off; // pass 1 in: n (exclusive scan of cnt)
-    uint32_t *out;           // pass 1 out: key handles, per query in walk order
+    uint32_t *cnt;           // pass 0 out: n;  FW_ONEPASS out: n
+    uint32_t *out_off;       // pass 1 in: n (exclusive scan of cnt);  FW_ONEPASS out: n
+    uint32_t *out;           // pass 1 / FW_ONEPASS out: key handles, per query in walk order
+    // FW_ONEPASS: the walk streams its keys into linked chunks of FW_CHUNK words (word 0 = next
+    // chunk) from `pool`, then reserves its contiguous output range with one atomic and copies
+    uint32_t *pool;
+    uint64_t pool_chunks;
+    uint64_t out_cap;
+    unsigned long long *ctl;  // [0] output keys requested, [1] chunks requested (may pass the caps)
 };
+constexpr int FW_COUNT = 0, FW_EMIT = 1, FW_ONEPASS = 2;
+constexpr uint32_t FW_CHUNK = 256;  // u32 words per pool chunk (1 link + 255 keys)
 hipError_t launch_filter_walk(const FilterArgs &a, int pass, hipStream_t stream);
 // emqx_topic:intersection/2 per pair; out_len[i] = bytes, or one of:
 constexpr int32_t INTERSECT_FALSE = -1, INTERSECT_BADHASH = -2;

@@ -23,6 +23,7 @@ namespace tmx {
 namespace {
 
 constexpr uint32_t C_HASH = 0, C_PLUS = 1;
+constexpr uint32_t NONE_FW = 0xFFFFFFFFu;
 constexpr int R_FULL = 0, R_PREFIX = 1, R_LOWER = 2, R_SEEK = 3;
 
 // key j vs pre[0..np) ++ [w]: -1 / 0 / 1
@@ -132,7 +133,11 @@ __device__ __attribute__((always_inline)) inline int cmp_filter(const uint32_t (
 // `lower` or seeks, the sequential walk visits exactly those keys in order.  FULL keys
 // before that point are emitted in order (ballot + prefix popcount); then the wave stops
 // (lower / end of table), seeks (wave_seek), or moves on by 64.
-// pass 0: cnt[q] = keys the walk matches; pass 1: write their handles at out_off[q].
+// FW_COUNT: cnt[q] = keys the walk matches; FW_EMIT: write their handles at out_off[q].
+// FW_ONEPASS: one walk; keys go to the wave's chunk chain as they are met, then to a
+// contiguous range reserved at the end (out_off[q], cnt[q]).  A wave whose chunks or output
+// range do not fit the pool / out_cap leaves its query unwritten; the host sees the demand
+// in ctl and re-runs the batch (two-pass) after growing.
 __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
     const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
@@ -141,10 +146,22 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
     const uint32_t *W = a.qw + qb;
     const uint32_t K = a.K;
     uint32_t c = 0;  // wave-uniform
+    // FW_ONEPASS chunk chain (wave-uniform): head, current chunk, keys in the current chunk
+    constexpr uint32_t CK = FW_CHUNK - 1;
+    uint32_t head = NONE_FW, curc = NONE_FW, fill = CK;
+    bool short_pool = false;
+    auto new_chunk = [&]() -> uint32_t {  // wave-uniform; NONE_FW when the pool is exhausted
+        unsigned long long c0 = 0;
+        if (lane == 0) c0 = atomicAdd(&a.ctl[1], 1ull);
+        c0 = __shfl(c0, 0);
+        if (c0 >= a.pool_chunks) return NONE_FW;
+        if (lane == 0) a.pool[c0 * FW_CHUNK] = NONE_FW;
+        return (uint32_t)c0;
+    };
     if (WL && a.qstatus[q] == 0) {
         // base_init/1 (:160-163): a first word <<"$", _/bytes>> starts at next({[W0], {}})
         uint32_t idx = a.qdollar[q] ? wave_seek(a, 0, nullptr, 0, W[0], lane) : 0;
-        uint32_t *out = pass ? a.out + a.out_off[q] : nullptr;
+        uint32_t *out = pass == FW_EMIT ? a.out + a.out_off[q] : nullptr;
         const uint64_t below = (1ull << lane) - 1;
         uint32_t wr[8];  // the query's first 8 words (qw is padded by 8 words on the device)
 #pragma unroll
@@ -163,14 +180,38 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             const uint64_t stop = __ballot(r == R_LOWER || r == R_SEEK);
             const uint32_t fs = stop ? (uint32_t)__ffsll((long long)stop) - 1 : 64;
             const bool full = lane < fs && r == R_FULL;
-            const uint64_t fm = __ballot(full);
-            if (a.first && fm) {                 // return_first: the first key met
-                if (pass && lane == (uint32_t)__ffsll((long long)fm) - 1) out[0] = a.kh[j];
-                c = 1;
-                break;
+            uint64_t fm = __ballot(full);
+            if (a.first && fm) fm &= 0 - fm;  // return_first: the first key met only
+            const uint32_t nf = __popcll(fm);
+            if (pass == FW_ONEPASS && nf && !short_pool) {
+                // room in the current chunk for `room` keys; the rest go to a fresh chunk
+                const uint32_t room = CK - fill;
+                uint32_t nc = NONE_FW;
+                if (nf > room) {
+                    nc = new_chunk();
+                    if (nc == NONE_FW) short_pool = true;
+                    else if (curc == NONE_FW) head = nc;
+                    else if (lane == 0) a.pool[(uint64_t)curc * FW_CHUNK] = nc;  // link
+                }
+                if (!short_pool) {
+                    if ((fm >> lane) & 1ull) {
+                        const uint32_t rk = __popcll(fm & below);
+                        const uint64_t at = rk < room ? (uint64_t)curc * FW_CHUNK + 1 + fill + rk
+                                                      : (uint64_t)nc * FW_CHUNK + 1 + (rk - room);
+                        a.pool[at] = a.kh[j];
+                    }
+                    if (nf > room) {
+                        curc = nc;
+                        fill = nf - room;
+                    } else {
+                        fill += nf;
+                    }
+                }
+            } else if (pass == FW_EMIT && ((fm >> lane) & 1ull)) {
+                out[c + __popcll(fm & below)] = a.kh[j];  // match_add/2, walk order
             }
-            if (pass && full) out[c + __popcll(fm & below)] = a.kh[j];  // match_add/2, walk order
-            c += __popcll(fm);
+            c += nf;
+            if (a.first && nf) break;
             if (fs == 64) {                      // 64 x next(Cursor)
                 idx += 64;
                 continue;
@@ -183,7 +224,26 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             idx = wave_seek(a, ks + 1, a.kw + a.koff[ks], sp, sw, lane);
         }
     }
-    if (!pass && lane == 0) a.cnt[q] = c;
+    if (pass == FW_COUNT && lane == 0) a.cnt[q] = c;
+    if (pass == FW_ONEPASS) {
+        unsigned long long base = 0;
+        if (lane == 0 && c) base = atomicAdd(&a.ctl[0], (unsigned long long)c);
+        base = __shfl(base, 0);
+        if (lane == 0) {
+            a.cnt[q] = c;
+            a.out_off[q] = (uint32_t)base;
+        }
+        if (short_pool || base + c > a.out_cap) return;  // the host re-runs the batch
+        __threadfence_block();  // the chain's keys and links (other lanes' stores) before reading them
+        // copy the chain into [base, base + c): 255 keys per chunk, 64 lanes at a time
+        uint32_t ch = head;
+        for (uint32_t done = 0; done < c; done += CK) {
+            const uint32_t m = min(CK, c - done);
+            const uint32_t *src = a.pool + (uint64_t)ch * FW_CHUNK + 1;
+            for (uint32_t k = lane; k < m; k += 64) a.out[base + done + k] = src[k];
+            ch = a.pool[(uint64_t)ch * FW_CHUNK];
+        }
+    }
 }
 
 }  // namespace

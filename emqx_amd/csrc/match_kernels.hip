@@ -609,8 +609,13 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                 __syncthreads();
                 st_frch += got;
             }
+            // lanes write in scan order, so every lane before the first one that does not fit
+            // wrote all its entries and every lane after it writes none: the buffer's valid
+            // prefix ends at the first overflowing lane's position
+            const bool ovf = np && pp + np > cap;
+            const unsigned long long ovm = __ballot(ovf);
             if (np) {
-                if (pp + np <= cap) {
+                if (!ovf) {
 #pragma unroll
                     for (int k = 0; k < RPL; k++) {
                         if (q1[k]) fr_write(nxt, pp++, r1[k].child, tl[k] | q1[k]);
@@ -623,7 +628,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                         if (q1[k] || q2[k]) atomicOr(&L.spill, 1ull << tl[k]);
                 }
             }
-            nnext = min(nnext + tot_p, cap);
+            nnext = ovm ? __shfl(pp, __builtin_ctzll(ovm), WAVE) : nnext + tot_p;
 #pragma unroll
             for (int k = 0; k < RPL; k++) st_visit += (uint32_t)f1[k] + (uint32_t)f2[k];
         }
@@ -790,105 +795,487 @@ __global__ __launch_bounds__(WAVE) void k_match_slow(MatchArgs a) {
 
 
 // ---------------------------------------------------------------------------
-// k_match_first: emqx_topic_index:match/2 (return_first, emqx_trie_search.erl:171-178) —
-// the FIRST matching key in ETS term order, per topic; lane per topic.
+// FIRST: emqx_topic_index:match/2 (return_first, emqx_trie_search.erl:171-178) — the FIRST
+// matching key in ETS term order, per topic.
 //
 // Every key that matches topic T spells T's words at its literal levels, so two matching
-// keys differ only in WHERE they have '+' / '#' / the end of the list.  In Erlang term
-// order '#' < '+' < any binary and a shorter list sorts first, so the smallest matching
-// word-list key is the first one a depth-first walk meets when it tries, at each node:
-// the keys ending here (d == levels), then the node's "P/#" keys, then the '+' subtree,
-// then the literal subtree.  Equal word lists are one filter: the smallest id wins
-// ({ID} tuples).  {Binary, {ID}} keys sort after every list (emqx_trie_search.erl:381-389
-// finds them last), so one is the answer only when no word-list key matches.
+// keys differ only in WHERE they have '+' / '#' / the end of the list.  Their Erlang term
+// order is therefore the order of their shape codes (engine.cpp key_ord): per level END 0 <
+// '#' 1 < '+' 2 < literal 3 (a shorter list sorts first; atoms '#' < '+' < any binary), two
+// bits per level from bit 61 down; {Binary, {ID}} keys sort after every list (bit 62).  Equal
+// codes are one filter, and the node's list header holds its smallest-id keys ({ID} tuples).
+//
+// k_match_first_wave (index without keys deeper than 31 levels): the level-synchronous wave
+// walk of k_match_fast, with each frontier entry carrying its path's code prefix.  A
+// candidate (a node's '#' keys; at the last level its word-list and binary terminal keys)
+// has a code computed from that prefix alone; the wave keeps the smallest per topic (LDS
+// atomicMin), then the lane holding it records where its handle lives.  A frontier entry
+// whose prefix sorts after the best candidate cannot lead to a smaller key and is dropped,
+// so a walk ends as soon as nothing smaller can exist.  No key lists are copied.
+// k_first_dfs: lane per topic, depth-first in term order ('#' keys, then the '+' subtree,
+// then the literal one), stack in global scratch: any key depth, and the spill path.
+constexpr uint32_t FW_HANDLE = 0, FW_HASHLIST = 1, FW_ROOTHASH = 2;  // where the winner's handle lives
+constexpr uint64_t ORD_BIN_D = 1ull << 62;
+
+__device__ __forceinline__ uint32_t first_dfs_topic(const MatchArgs &a, const RootRec &R, uint32_t t) {
+    uint32_t dummy = 0;
+    auto byte_at = [&](uint32_t i) -> uint8_t { return a.bytes[i]; };
+    const uint32_t b = a.off[t], e = a.off[t + 1];
+    const uint64_t sbase = (uint64_t)(a.off[t] - a.off[0]) + 2ull * t;
+    uint32_t *wid = a.scratch_w + sbase;
+    uint64_t *stk = a.scratch_s + sbase;
+    const bool dollar = (e > b) && a.bytes[b] == '$';
+    uint32_t nl = 0;
+    for (uint32_t i = b;; ++i) {
+        const uint32_t st = i;
+        const uint64_t key = level_key(&i, e, byte_at);
+        wid[nl++] = word_lookup(a, key, i - st, st, byte_at, &dummy);
+        if (i >= e) break;
+    }
+    uint32_t best = NONE, bbest = NONE;
+    uint32_t sp = 0;
+    stk[sp++] = ROOT_MARK << 24;
+    while (sp) {
+        const uint64_t ent = stk[--sp];
+        const uint64_t slot = ent >> 24;
+        const uint32_t d = (uint32_t)(ent & 0xFFFFFF);
+        // the node's return_first candidates: its smallest-id {Binary,{ID}} term key,
+        // word-list term key and '#' key (list header, or the inline key)
+        uint32_t node, info, bloom, tb = NONE, tw = NONE, th = NONE;
+        if (slot == ROOT_MARK) {
+            node = ROOT_ID;
+            info = dollar ? (R.info & I_LIT) : R.info;
+            bloom = R.bloom;
+            if (!dollar && R.hash_cnt) th = a.arena[R.list_off - 3];
+        } else {
+            const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + slot);
+            node = (uint32_t)slot;
+            bloom = x.z;
+            info = x.w;
+            const uint32_t m = info_mode(info);
+            if (m == M_REC || m == M_CNT) {
+                const uint32_t lo = a.slot_list[node];
+                tb = a.arena[lo - 5];
+                tw = a.arena[lo - 4];
+                th = a.arena[lo - 3];
+            } else if (m == M_INLINE) {
+                const uint32_t k = info & I_KEY_MASK;
+                if (info & I_INL_HASH) th = k;
+                else if (a.key_bin[k]) tb = k;
+                else tw = k;
+            }
+        }
+        if (d == nl) {  // P + end of list, then P + '#'; binaries only if no list matches
+            if (tb != NONE) bbest = tb;  // only the all-literal path holds binary keys
+            best = tw != NONE ? tw : th;
+            if (best != NONE) break;
+            continue;
+        }
+        if (th != NONE) {  // P + '#'
+            best = th;
+            break;
+        }
+        // children: the '+' subtree before the literal one (pushed last, popped first)
+        const uint32_t need = probes_needed(info, bloom, wid[d]);
+        Rec r;
+        if ((need & DO_LIT) && edge_probe(a, node, wid[d], &r, &dummy)) stk[sp++] = ((uint64_t)r.child << 24) | (d + 1);
+        if ((need & DO_PLUS) && edge_probe(a, node, W_PLUS, &r, &dummy)) stk[sp++] = ((uint64_t)r.child << 24) | (d + 1);
+    }
+    return best == NONE ? bbest : best;
+}
+
+__device__ __forceinline__ bool topic_badarg(const MatchArgs &a, uint32_t t) {
+    const uint32_t b = a.off[t], e = a.off[t + 1];
+    bool badarg = false;
+    for (uint32_t i = b, st = b;; ++i) {
+        const bool end = i == e;
+        if (end || a.bytes[i] == '/') {
+            if (i - st == 1 && (a.bytes[st] == '+' || a.bytes[st] == '#')) badarg = true;
+            st = i + 1;
+            if (end) break;
+        }
+    }
+    return badarg;
+}
+
+// every topic, lane per topic (indexes holding keys deeper than the 31-level code)
 __global__ __launch_bounds__(WAVE) void k_match_first(MatchArgs a) {
     const RootRec R = *a.root;
     if (blockIdx.x == 0 && threadIdx.x < CTL_BYTES / 8) a.ctl_next[threadIdx.x] = 0ull;  // next launch's counters
-    uint32_t dummy = 0;
-    auto byte_at = [&](uint32_t i) -> uint8_t { return a.bytes[i]; };
     for (uint32_t t = blockIdx.x * WAVE + lane_id(); t < a.n; t += gridDim.x * WAVE) {
-        const uint32_t b = a.off[t], e = a.off[t + 1];
-        // badarg pre-scan (a level exactly "+" or "#")
-        bool badarg = false;
-        for (uint32_t i = b, st = b;; ++i) {
+        const bool badarg = topic_badarg(a, t);
+        a.out_off[t] = t;
+        a.status[t] = badarg ? 1 : 0;
+        const uint32_t k = badarg ? NONE : first_dfs_topic(a, R, t);
+        a.out_cnt[t] = k != NONE ? 1u : 0u;
+        a.keys[t] = k;
+    }
+}
+
+// the topics k_match_first_wave handed off (frontier pool exhausted, or the test aid)
+__global__ __launch_bounds__(WAVE) void k_first_slow(MatchArgs a) {
+    const uint32_t nslow = *a.slow_count;
+    const RootRec R = *a.root;
+    for (uint32_t idx = blockIdx.x * WAVE + lane_id(); idx < nslow; idx += gridDim.x * WAVE) {
+        const uint32_t t = a.slow_list[idx];
+        const uint32_t k = first_dfs_topic(a, R, t);
+        a.out_cnt[t] = k != NONE ? 1u : 0u;
+        a.keys[t] = k;
+    }
+}
+
+struct FirstLds {
+    uint8_t tb[TBCAP];
+    uint32_t fr_node[2][FCAP];
+    uint64_t fr_ord[2][FCAP];      // code prefix of the entry's path (levels < depth)
+    uint8_t fr_meta[2][FCAP];      // topic lane | DO_PLUS / DO_LIT
+    uint32_t fch[2][MAXF];         // overflow chunks (uint4 entries {node, meta, ord lo, ord hi})
+    uint32_t wid[2][WAVE];
+    uint32_t nlev[WAVE];
+    unsigned long long best[WAVE];  // smallest candidate code so far (~0: none)
+    unsigned long long win[WAVE];   // its handle, or where it lives: value | FW_* << 32
+    unsigned long long spill;
+    unsigned long long alive[2];
+};
+constexpr uint32_t FCH4 = FCH / 2;  // uint4 entries per overflow chunk (the pool is sized in uint2)
+
+__global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
+    __shared__ FirstLds L;
+    const uint32_t lane = lane_id();
+    const uint32_t t = blockIdx.x * a.tpw + lane;
+    const bool active = lane < a.tpw && t < a.n;
+    if (blockIdx.x == 0 && threadIdx.x < CTL_BYTES / 8) a.ctl_next[threadIdx.x] = 0ull;  // next launch's counters
+    uint4 *const pool4 = reinterpret_cast<uint4 *>(a.fr_pool);
+
+    // ---- stage the wave's topic bytes (as k_match_fast)
+    const uint32_t t0 = blockIdx.x * a.tpw;
+    const uint32_t wb0 = a.off[t0], wb1 = a.off[min(t0 + a.tpw, a.n)];
+    const uint32_t tbase = wb0 & ~15u;
+    const bool staged = ((reinterpret_cast<uintptr_t>(a.bytes) & 15u) == 0) && (wb1 - tbase <= (uint32_t)TBCAP);
+    if (staged) {
+        for (uint32_t j = lane * 16; tbase + j < wb1; j += WAVE * 16) {
+            if (tbase + j + 16 <= wb1) {
+                *reinterpret_cast<uint4 *>(&L.tb[j]) = *reinterpret_cast<const uint4 *>(a.bytes + tbase + j);
+            } else {
+                for (uint32_t k = 0; tbase + j + k < wb1; k++) L.tb[j + k] = a.bytes[tbase + j + k];
+            }
+        }
+        __syncthreads();
+    }
+    auto byte_at = [&](uint32_t i) -> uint8_t { return staged ? L.tb[i - tbase] : a.bytes[i]; };
+
+    bool badarg = false, dollar = false;
+    uint32_t nl = 0, b = 0, e = 0;
+    if (active) {
+        b = a.off[t];
+        e = a.off[t + 1];
+        dollar = (e > b) && byte_at(b) == '$';
+        uint32_t st = b;
+        for (uint32_t i = b;; ++i) {
             const bool end = i == e;
-            if (end || a.bytes[i] == '/') {
-                if (i - st == 1 && (a.bytes[st] == '+' || a.bytes[st] == '#')) badarg = true;
+            const uint8_t c = end ? (uint8_t)'/' : byte_at(i);
+            if (c == '/') {
+                if (i - st == 1 && (byte_at(st) == '+' || byte_at(st) == '#')) badarg = true;
+                nl++;
                 st = i + 1;
                 if (end) break;
             }
         }
-        a.out_off[t] = t;
-        a.status[t] = badarg ? 1 : 0;
-        if (badarg) {
-            a.out_cnt[t] = 0;
-            continue;
+    }
+    const bool spill0 = active && !badarg && a.force_slow;
+    const bool walk = active && !badarg && !spill0;
+    uint32_t cur_b = b;
+    L.nlev[lane] = nl;
+    L.best[lane] = ~0ull;
+    L.win[lane] = 0;
+    {
+        const unsigned long long sp0 = __ballot(spill0);
+        if (lane == 0) {
+            L.spill = sp0;
+            L.alive[0] = 0;
+            L.alive[1] = 0;
         }
-        const uint64_t sbase = (uint64_t)(a.off[t] - a.off[0]) + 2ull * t;
-        uint32_t *wid = a.scratch_w + sbase;
-        uint64_t *stk = a.scratch_s + sbase;
-        const bool dollar = (e > b) && a.bytes[b] == '$';
-        uint32_t nl = 0;
-        for (uint32_t i = b;; ++i) {
-            const uint32_t st = i;
-            const uint64_t key = level_key(&i, e, byte_at);
-            wid[nl++] = word_lookup(a, key, i - st, st, byte_at, &dummy);
-            if (i >= e) break;
+    }
+    uint32_t dummy = 0;
+    auto tokenize_next = [&](uint32_t slot) {
+        uint32_t i = cur_b;
+        const uint32_t st = i;
+        const uint64_t key = level_key(&i, e, byte_at);
+        L.wid[slot][lane] = word_lookup(a, key, i - st, st, byte_at, &dummy);
+        cur_b = i + 1;
+    };
+
+    // ---- root: a root '#' key (code '#' at level 0) is the smallest any topic can match
+    const RootRec R = *a.root;
+    if (walk) tokenize_next(0);
+    uint32_t nfr;
+    {
+        const bool rh = walk && !dollar && R.hash_cnt;
+        if (rh) {
+            L.best[lane] = 1ull << 60;
+            L.win[lane] = (unsigned long long)FW_ROOTHASH << 32;
         }
-        uint32_t best = NONE, bbest = NONE;
-        uint32_t sp = 0;
-        stk[sp++] = ROOT_MARK << 24;
-        while (sp) {
-            const uint64_t ent = stk[--sp];
-            const uint64_t slot = ent >> 24;
-            const uint32_t d = (uint32_t)(ent & 0xFFFFFF);
-            // the node's return_first candidates: its smallest-id {Binary,{ID}} term key,
-            // word-list term key and '#' key (list header, or the inline key)
-            uint32_t node, info, bloom, tb = NONE, tw = NONE, th = NONE;
-            if (slot == ROOT_MARK) {
-                node = ROOT_ID;
-                info = dollar ? (R.info & I_LIT) : R.info;
-                bloom = R.bloom;
-                if (!dollar && R.hash_cnt) th = a.arena[R.list_off - 3];
-            } else {
-                const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + slot);
-                node = (uint32_t)slot;
-                bloom = x.z;
-                info = x.w;
-                const uint32_t m = info_mode(info);
-                if (m == M_REC || m == M_CNT) {
-                    const uint32_t lo = a.slot_list[node];
-                    tb = a.arena[lo - 5];
-                    tw = a.arena[lo - 4];
-                    th = a.arena[lo - 3];
-                } else if (m == M_INLINE) {
-                    const uint32_t k = info & I_KEY_MASK;
-                    if (info & I_INL_HASH) th = k;
-                    else if (a.key_bin[k]) tb = k;
-                    else tw = k;
+        const uint32_t rinfo = dollar ? (R.info & I_LIT) : R.info;
+        const uint32_t m = (walk && !rh) ? probes_needed(rinfo, R.bloom, L.wid[0][lane]) : 0u;
+        const unsigned long long al0 = __ballot(m != 0);
+        if (lane == 0) L.alive[0] = al0;
+        uint32_t tot;
+        const uint32_t p2 = wave_excl_scan(m ? 1u : 0u, &tot);
+        if (m) {
+            L.fr_node[0][p2] = ROOT_ID;
+            L.fr_meta[0][p2] = (uint8_t)(lane | m);
+            L.fr_ord[0][p2] = 0ull;
+        }
+        nfr = tot;
+    }
+    __syncthreads();
+
+    uint32_t nfch[2] = {0, 0};
+    auto fr_read = [&](uint32_t lvl, uint32_t i, uint32_t &node, uint32_t &meta, uint64_t &ord) {
+        if (i < (uint32_t)FCAP) {
+            node = L.fr_node[lvl][i];
+            meta = L.fr_meta[lvl][i];
+            ord = L.fr_ord[lvl][i];
+        } else {
+            const uint32_t k = i - FCAP;
+            const uint4 v = pool4[(uint64_t)L.fch[lvl][k / FCH4] * FCH4 + k % FCH4];
+            node = v.x;
+            meta = v.y;
+            ord = ((uint64_t)v.w << 32) | v.z;
+        }
+    };
+    auto fr_write = [&](uint32_t lvl, uint32_t i, uint32_t node, uint32_t meta, uint64_t ord) {
+        if (i < (uint32_t)FCAP) {
+            L.fr_node[lvl][i] = node;
+            L.fr_meta[lvl][i] = (uint8_t)meta;
+            L.fr_ord[lvl][i] = ord;
+        } else {
+            const uint32_t k = i - FCAP;
+            pool4[(uint64_t)L.fch[lvl][k / FCH4] * FCH4 + k % FCH4] =
+                make_uint4(node, meta, (uint32_t)ord, (uint32_t)(ord >> 32));
+        }
+    };
+
+    // Without word-list keys deeper than the code (31 levels; '#' keys 30), only {Binary, {ID}}
+    // keys hang below depth 31, and only on the all-literal path: past depth 30 the walk
+    // follows that path alone (code prefix ALL_LIT) and looks for binary terminal keys.
+    constexpr uint64_t ALL_LIT = (1ull << 62) - 1;
+    for (uint32_t d = 0; nfr > 0; ++d) {
+        const uint32_t cur = d & 1, nxt = cur ^ 1;
+        if (walk && ((L.alive[cur] >> lane) & 1ull) && d + 1 < nl) tokenize_next(nxt);
+        if (lane == 0) L.alive[nxt] = 0;
+        __syncthreads();
+        uint32_t nnext = 0;
+        // a child at depth d+1 adds its level-d symbol ('+' 2, literal 3) at bit sh; its '#'
+        // keys have '#' (1) at level d+1, bit sh-2 (none when d == 30: no such keys)
+        const bool deep = d > 30;
+        const uint32_t sh = deep ? 0u : 60 - 2 * d;
+        const uint64_t hbit = (!deep && sh >= 2) ? 1ull << (sh - 2) : 0ull;
+        for (uint32_t base = 0; base < nfr; base += WAVE * RPL) {
+            uint32_t tl[RPL];
+            bool last[RPL], f1[RPL], f2[RPL];
+            Rec r1[RPL], r2[RPL];
+            uint64_t pre[RPL];
+            {
+                uint32_t node[RPL], w[RPL];
+                bool p1[RPL], p2[RPL];
+                uint64_t s1[RPL], s2[RPL];
+#pragma unroll
+                for (int k = 0; k < RPL; k++) {
+                    const uint32_t i = base + k * WAVE + lane;
+                    bool has = i < nfr;
+                    uint32_t meta = 0;
+                    node[k] = 0;
+                    pre[k] = 0;
+                    if (has) fr_read(cur, i, node[k], meta, pre[k]);
+                    tl[k] = meta & 63u;
+                    // nothing under this entry can sort before the topic's best candidate
+                    if (has && (L.best[tl[k]] < pre[k] || (deep && pre[k] != ALL_LIT))) has = false;
+                    w[k] = has ? L.wid[cur][tl[k]] : NONE;
+                    last[k] = has && (d + 1 == L.nlev[tl[k]]);
+                    p1[k] = has && (meta & DO_LIT);
+                    p2[k] = has && !deep && (meta & DO_PLUS);
+                    s1[k] = edge_hash(node[k], w[k]) & a.emask;
+                    s2[k] = edge_hash(node[k], W_PLUS) & a.emask;
+                    f1[k] = f2[k] = false;
+                }
+                for (;;) {
+                    bool any = false;
+#pragma unroll
+                    for (int k = 0; k < RPL; k++) any = any || p1[k] || p2[k];
+                    if (!any) break;
+                    uint4 x1[RPL], x2[RPL];
+#pragma unroll
+                    for (int k = 0; k < RPL; k++) {
+                        x1[k] = p1[k] ? *reinterpret_cast<const uint4 *>(a.etab + s1[k]) : make_uint4(NONE, 0, 0, 0);
+                        x2[k] = p2[k] ? *reinterpret_cast<const uint4 *>(a.etab + s2[k]) : make_uint4(NONE, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int k = 0; k < RPL; k++) {
+                        if (p1[k]) {
+                            if (x1[k].x == NONE) p1[k] = false;
+                            else if (x1[k].x == node[k] && x1[k].y == w[k]) {
+                                r1[k] = Rec{(uint32_t)s1[k], x1[k].z, x1[k].w};
+                                f1[k] = true;
+                                p1[k] = false;
+                            } else s1[k] = (s1[k] + 1) & a.emask;
+                        }
+                        if (p2[k]) {
+                            if (x2[k].x == NONE) p2[k] = false;
+                            else if (x2[k].x == node[k] && x2[k].y == W_PLUS) {
+                                r2[k] = Rec{(uint32_t)s2[k], x2[k].z, x2[k].w};
+                                f2[k] = true;
+                                p2[k] = false;
+                            } else s2[k] = (s2[k] + 1) & a.emask;
+                        }
+                    }
                 }
             }
-            if (d == nl) {  // P + end of list, then P + '#'; binaries only if no list matches
-                if (tb != NONE) bbest = tb;  // only the all-literal path holds binary keys
-                best = tw != NONE ? tw : th;
-                if (best != NONE) break;
-                continue;
+            // candidates of each found child (depth d+1): its '#' keys (code P'|'#' at level
+            // d+1) and, at the topic's last level, its word-list terminal keys (code P') and
+            // binary ones (after every list)
+            uint64_t cord[RPL][2][2];  // [entry][child][0: '#', 1: terminal] code (~0: none)
+            uint64_t cwin[RPL][2][2];
+#pragma unroll
+            for (int k = 0; k < RPL; k++) {
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    cord[k][c][0] = cord[k][c][1] = ~0ull;
+                    cwin[k][c][0] = cwin[k][c][1] = 0;
+                    const bool f = c ? f2[k] : f1[k];
+                    if (!f) continue;
+                    const Rec r = c ? r2[k] : r1[k];
+                    const uint64_t P = deep ? pre[k] : pre[k] | ((uint64_t)(c ? 2u : 3u) << sh);
+                    const uint32_t m = info_mode(r.info);
+                    uint32_t hc = 0, tcnt = 0, lo = 0;
+                    if (m == M_INLINE) {
+                        const uint32_t key = r.info & I_KEY_MASK;
+                        if (r.info & I_INL_HASH) {
+                            if (hbit) {
+                                cord[k][c][0] = P | hbit;
+                                cwin[k][c][0] = key;
+                            }
+                        } else if (last[k]) {
+                            cord[k][c][1] = a.key_bin[key] ? ORD_BIN_D : P;
+                            cwin[k][c][1] = key;
+                        }
+                    } else if (m == M_CNT) {
+                        hc = info_hash_cnt(r.info);
+                        tcnt = info_term_cnt(r.info);
+                    } else if (m == M_REC) {
+                        lo = a.slot_list[r.child];
+                        tcnt = a.arena[lo - 2];
+                        hc = a.arena[lo - 1];
+                    }
+                    if (hc && hbit) {
+                        cord[k][c][0] = P | hbit;
+                        cwin[k][c][0] = ((unsigned long long)FW_HASHLIST << 32) | r.child;
+                    }
+                    if (last[k] && tcnt) {  // which terminal kinds: the list header's min-id keys
+                        if (m == M_CNT) lo = a.slot_list[r.child];
+                        const uint32_t tw = a.arena[lo - 4], tb = a.arena[lo - 5];
+                        if (tw != NONE) {
+                            cord[k][c][1] = P;
+                            cwin[k][c][1] = tw;
+                        } else if (tb != NONE) {
+                            cord[k][c][1] = ORD_BIN_D;
+                            cwin[k][c][1] = tb;
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < 2; j++)
+                        if (cord[k][c][j] != ~0ull) atomicMin(&L.best[tl[k]], (unsigned long long)cord[k][c][j]);
+                }
             }
-            if (th != NONE) {  // P + '#'
-                best = th;
-                break;
+            __syncthreads();
+            // the lane holding a topic's smallest code records its handle (codes are unique
+            // per topic: the code and the topic's words determine the filter)
+#pragma unroll
+            for (int k = 0; k < RPL; k++)
+#pragma unroll
+                for (int c = 0; c < 2; c++)
+#pragma unroll
+                    for (int j = 0; j < 2; j++)
+                        if (cord[k][c][j] != ~0ull && cord[k][c][j] == L.best[tl[k]]) L.win[tl[k]] = cwin[k][c][j];
+            // next frontier: children still needing a probe whose prefix can still win
+            uint32_t q1[RPL], q2[RPL];
+            uint64_t P1[RPL], P2[RPL];
+            uint32_t np = 0;
+#pragma unroll
+            for (int k = 0; k < RPL; k++) {
+                const uint32_t wn = last[k] ? NONE : L.wid[nxt][tl[k]];
+                P1[k] = deep ? pre[k] : pre[k] | (3ull << sh);
+                P2[k] = deep ? pre[k] : pre[k] | (2ull << sh);
+                const unsigned long long bt = L.best[tl[k]];
+                // a child at depth d+1 > 30 matters only on the all-literal path (binary keys)
+                const bool deeper = !last[k] && (d + 1 <= 30 || P1[k] == ALL_LIT);
+                q1[k] = (f1[k] && deeper && !(bt < P1[k])) ? probes_needed(r1[k].info, r1[k].bloom, wn) : 0u;
+                q2[k] = (f2[k] && deeper && d + 1 <= 30 && !(bt < P2[k])) ? probes_needed(r2[k].info, r2[k].bloom, wn) : 0u;
+                np += (uint32_t)(q1[k] != 0) + (uint32_t)(q2[k] != 0);
             }
-            // children: the '+' subtree before the literal one (pushed last, popped first)
-            const uint32_t need = probes_needed(info, bloom, wid[d]);
-            Rec r;
-            if ((need & DO_LIT) && edge_probe(a, node, wid[d], &r, &dummy)) stk[sp++] = ((uint64_t)r.child << 24) | (d + 1);
-            if ((need & DO_PLUS) && edge_probe(a, node, W_PLUS, &r, &dummy)) stk[sp++] = ((uint64_t)r.child << 24) | (d + 1);
+            uint32_t tot_p;
+            uint32_t pp = nnext + wave_excl_scan(np, &tot_p);
+            uint32_t cap = FCAP + nfch[nxt] * FCH4;
+            if (nnext + tot_p > cap && nfch[nxt] < (uint32_t)MAXF) {
+                const uint32_t want = min((nnext + tot_p - FCAP + FCH4 - 1) / FCH4, (uint32_t)MAXF) - nfch[nxt];
+                unsigned long long c0 = 0;
+                if (lane == 0) c0 = atomicAdd(a.fr_cursor, (unsigned long long)want);
+                c0 = __shfl(c0, 0, WAVE);
+                const uint32_t got = c0 >= a.fr_chunks ? 0u : (uint32_t)min((unsigned long long)want, a.fr_chunks - c0);
+                if (lane < got) L.fch[nxt][nfch[nxt] + lane] = (uint32_t)(c0 + lane);
+                nfch[nxt] += got;
+                cap = FCAP + nfch[nxt] * FCH4;
+                __syncthreads();
+            }
+            const bool ovf = np && pp + np > cap;
+            const unsigned long long ovm = __ballot(ovf);
+            if (np) {
+                if (!ovf) {
+#pragma unroll
+                    for (int k = 0; k < RPL; k++) {
+                        if (q1[k]) fr_write(nxt, pp++, r1[k].child, tl[k] | q1[k], P1[k]);
+                        if (q2[k]) fr_write(nxt, pp++, r2[k].child, tl[k] | q2[k], P2[k]);
+                        if (q1[k] || q2[k]) atomicOr(&L.alive[nxt], 1ull << tl[k]);
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < RPL; k++)  // frontier overflow: those topics take the DFS
+                        if (q1[k] || q2[k]) atomicOr(&L.spill, 1ull << tl[k]);
+                }
+            }
+            nnext = ovm ? __shfl(pp, __builtin_ctzll(ovm), WAVE) : nnext + tot_p;
+            __syncthreads();
         }
-        if (best == NONE) best = bbest;
-        a.out_cnt[t] = best != NONE ? 1u : 0u;
-        a.keys[t] = best;
+        __syncthreads();
+        nfr = nnext;
+    }
+
+    // ---- results: the winner's handle (one more read for a '#' list), or the DFS for spills
+    const bool spill = active && !badarg && ((L.spill >> lane) & 1ull);
+    if (active) {
+        a.out_off[t] = t;
+        a.status[t] = badarg ? 1 : 0;
+        if (!spill) {
+            uint32_t k = NONE;
+            const unsigned long long wv = L.win[lane];
+            if (walk && L.best[lane] != ~0ull) {
+                const uint32_t kind = (uint32_t)(wv >> 32), v = (uint32_t)wv;
+                k = kind == FW_HANDLE ? v : kind == FW_ROOTHASH ? a.arena[R.list_off - 3] : a.arena[a.slot_list[v] - 3];
+            }
+            a.out_cnt[t] = k != NONE ? 1u : 0u;
+            a.keys[t] = k;
+        }
+    }
+    {
+        uint32_t tot_sp;
+        const uint32_t ps = wave_excl_scan(spill ? 1u : 0u, &tot_sp);
+        uint32_t sb = 0;
+        if (lane == 0 && tot_sp) sb = atomicAdd(a.slow_count, tot_sp);
+        sb = __shfl(sb, 0, WAVE);
+        if (spill) a.slow_list[sb + ps] = t;
     }
 }
+
 // ---------------------------------------------------------------------------
 __global__ void k_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -921,10 +1308,17 @@ hipError_t launch_match(const MatchArgs &a, hipStream_t s) {
     const unsigned grid = (unsigned)match_grid(a.n, a.tpw);
     if (a.mode == MODE_FIRST) {  // <= 1 key per topic at keys[t]; cursor stays 0
         if (a.ev_fast0 && (e = hipEventRecord(a.ev_fast0, s))) return e;
-        k_match_first<<<grid < 4096u ? grid : 4096u, WAVE, 0, s>>>(a);
+        if (a.first_dfs) {  // keys deeper than the 31-level code: lane-per-topic DFS
+            k_match_first<<<grid < 4096u ? grid : 4096u, WAVE, 0, s>>>(a);
+            if ((e = hipGetLastError())) return e;
+            if (a.ev_fast1 && (e = hipEventRecord(a.ev_fast1, s))) return e;
+            return hipSuccess;
+        }
+        k_match_first_wave<<<grid, WAVE, 0, s>>>(a);
         if ((e = hipGetLastError())) return e;
         if (a.ev_fast1 && (e = hipEventRecord(a.ev_fast1, s))) return e;
-        return hipSuccess;
+        k_first_slow<<<grid < 2048u ? grid : 2048u, WAVE, 0, s>>>(a);
+        return hipGetLastError();
     }
     if (a.ev_fast0 && (e = hipEventRecord(a.ev_fast0, s))) return e;
     if (a.stats) k_match_fast<true><<<grid, WAVE, 0, s>>>(a);

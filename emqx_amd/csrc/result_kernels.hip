@@ -107,9 +107,10 @@ hipError_t launch_excl_scan(const uint32_t *in, uint64_t in_stride, uint32_t n, 
 // key handles -> ids, topic-major.  One wave per 64 topics: lists of up to 8 keys are
 // copied by the topic's own lane; longer ones (hot '#' lists) by the whole wave, 64
 // consecutive keys per instruction.
+template <class IdT>
 __global__ __launch_bounds__(64) void k_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
                                                    const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n,
-                                                   uint64_t *ids, uint64_t cap, uint64_t keys_cap,
+                                                   IdT *ids, uint64_t cap, uint64_t keys_cap,
                                                    const unsigned long long *cursor) {
     const uint32_t lane = threadIdx.x;
     const uint32_t t = blockIdx.x * 64 + lane;
@@ -125,14 +126,14 @@ __global__ __launch_bounds__(64) void k_result_ids(const uint32_t *cnt, const ui
     }
     const bool is_long = c > 8;
     if (!is_long) {
-        for (uint32_t k = 0; k < c; k++) ids[(uint64_t)dofs + k] = key_rec[2ull * keys[(uint64_t)so + k]];
+        for (uint32_t k = 0; k < c; k++) ids[(uint64_t)dofs + k] = (IdT)key_rec[2ull * keys[(uint64_t)so + k]];
     }
     uint64_t longs = __ballot(is_long);
     while (longs) {
         const int l = __builtin_ctzll(longs);
         longs &= longs - 1;
         const uint32_t lc = __shfl(c, l, 64), ls = __shfl(so, l, 64), ld = __shfl(dofs, l, 64);
-        for (uint32_t k = lane; k < lc; k += 64) ids[(uint64_t)ld + k] = key_rec[2ull * keys[(uint64_t)ls + k]];
+        for (uint32_t k = lane; k < lc; k += 64) ids[(uint64_t)ld + k] = (IdT)key_rec[2ull * keys[(uint64_t)ls + k]];
     }
 }
 
@@ -144,12 +145,14 @@ __global__ void k_result_flags(const unsigned long long *cursor, uint64_t keys_c
         flags[0] = (*cursor > keys_cap ? RES_KEYS_OVERFLOW : 0u) | ((uint64_t)dst_off[n] > cap ? RES_IDS_OVERFLOW : 0u);
 }
 
-hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
-                             const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
-                             uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, uint32_t *flags,
-                             hipStream_t s) {
+template <class IdT>
+static hipError_t launch_result_ids_t(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
+                                      const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, IdT *ids,
+                                      uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, uint32_t *flags,
+                                      hipStream_t s) {
     if (n) {
-        k_result_ids<<<(n + 63) / 64, 64, 0, s>>>(cnt, src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap, cursor);
+        k_result_ids<IdT><<<(n + 63) / 64, 64, 0, s>>>(cnt, src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap,
+                                                       cursor);
         hipError_t e = hipGetLastError();
         if (e) return e;
     }
@@ -158,6 +161,19 @@ hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const
         return hipGetLastError();
     }
     return hipSuccess;
+}
+
+hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
+                             const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
+                             uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, uint32_t *flags,
+                             hipStream_t s) {
+    return launch_result_ids_t(cnt, src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap, cursor, flags, s);
+}
+
+hipError_t launch_result_ids32(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
+                               const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint32_t *ids,
+                               uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, hipStream_t s) {
+    return launch_result_ids_t(cnt, src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap, cursor, nullptr, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -174,6 +174,8 @@ typedef struct tm_stats_t {
     uint64_t commit_lists_us;
     uint64_t commit_upload_us;
     uint64_t n_deep_keys;   /* live word-list keys deeper than the device order code (31 levels) */
+    uint64_t n_filter_onepass;  /* tm_match_filter_batch batches walked once (keys chunked on device) */
+    uint64_t n_filter_twopass;  /* ... that needed the count + emit passes (output sized from them) */
 } tm_stats_t;
 
 /* lifecycle --------------------------------------------------------------- */

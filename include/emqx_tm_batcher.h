@@ -4,25 +4,28 @@
  * (apps/emqx/src/emqx_broker.erl:285-290) runs emqx_router:match_routes/1
  * (apps/emqx/src/emqx_router.erl:205-212) synchronously in the publishing process.  A GPU
  * wants one call per WINDOW of publishes, so this aggregator sits between the many
- * concurrent publishers and tm_match_*: publishers submit single topics, a worker thread
- * cuts the queue into batches, runs one engine batch per window and hands each publisher
- * its own id list (SURVEY.md §8 (b) "Who calls it", §8 (f) f3).
+ * concurrent publishers and tm_match_*: publishers submit single topics, a cutter thread
+ * cuts the queue into windows, runs one engine batch per window and delivery threads hand
+ * each publisher its own id list (SURVEY.md §8 (b) "Who calls it", §8 (f) f3).
  *
  *   window   a batch is dispatched when max_batch publishes are queued, or when the
  *            oldest queued publish has waited max_wait_us, or at tm_batcher_destroy
- *            (which drains the queue).  While a batch runs on the GPU the next one keeps
- *            filling, so under load batches grow by themselves.
+ *            (which drains the queue).  Two windows are in flight at once: while window
+ *            k+1 walks on the GPU, window k's ids cross PCIe and its publishers are called
+ *            back; under load windows grow by themselves.
  *   result   per publish: TM_TOPIC_OK with the ids of its matched keys (route dests,
  *            emqx_topic_index:get_id/1 of every key, emqx_topic_index.erl:87-89), or
  *            TM_BADARG with no ids (a level exactly "+" or "#": emqx_trie_search.erl:374-375),
  *            or a negative TM_E* status when the batch failed as a whole.  COUNT mode
  *            gives the count and no ids.
- *   writes   tm_batcher_apply / tm_batcher_commit serialise with the worker, so an epoch
- *            swaps only between batches: every batch sees exactly one committed epoch.
+ *   writes   tm_batcher_apply / tm_batcher_commit serialise with the cutter and wait for the
+ *            windows already on the GPU, so an epoch swaps only between windows: every
+ *            window sees exactly one committed epoch.
  *
  * Erlang binding: a NIF calls tm_batcher_submit with a callback that
  * enif_send()s the id list to the publishing pid, which waits in `receive`; the callback
- * runs on the worker thread and must not block.
+ * runs on a delivery thread (several run at once, each for different publishers) and must
+ * not block.
  */
 #ifndef EMQX_TM_BATCHER_H
 #define EMQX_TM_BATCHER_H
@@ -42,7 +45,8 @@ typedef struct tm_batcher_config {
     uint32_t max_batch;    /* publishes per engine batch (0 = 65536)              */
     uint32_t max_wait_us;  /* window bound from the oldest queued publish (0 = 200) */
     uint32_t mode;         /* TM_MATCH_ALL / UNIQUE / AGGRE / FIRST / COUNT        */
-    uint32_t reserved;
+    uint32_t delivery_threads; /* threads calling publishers back, the completion thread
+                                  included (0 = 4); each takes a contiguous share of a window */
 } tm_batcher_config;
 
 /* One publish's result; `ids` is valid only during the call. */
@@ -76,7 +80,7 @@ typedef struct tm_batcher_stats {
  * receive its writes through tm_batcher_apply / tm_batcher_commit while the batcher runs. */
 int  tm_batcher_create(tm_engine *eng, const tm_batcher_config *cfg, tm_batcher **out);
 int  tm_batcher_create_fn(tm_batch_fn fn, void *backend, const tm_batcher_config *cfg, tm_batcher **out);
-/* Drains the queue (every submitted publish gets its callback), then stops the worker. */
+/* Drains the queue (every submitted publish gets its callback), then stops the threads. */
 void tm_batcher_destroy(tm_batcher *b);
 
 /* Queue one publish (topic bytes are copied).  TM_ESTATE once destroy has begun. */
@@ -86,7 +90,7 @@ int tm_batcher_submit(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_matc
 int tm_batcher_match(tm_batcher *b, const uint8_t *topic, uint32_t len, uint64_t *ids, uint32_t cap,
                      uint32_t *n_out, int32_t *status);
 
-/* Engine writes, serialised with the worker (engine batchers only: TM_ESTATE otherwise). */
+/* Engine writes, serialised with the windows (engine batchers only: TM_ESTATE otherwise). */
 int tm_batcher_apply(tm_batcher *b, const tm_op *ops, size_t n);
 int tm_batcher_commit(tm_batcher *b, uint64_t *epoch_out);
 

@@ -209,3 +209,29 @@ def test_filter_walk_config_e_scaled():
     assert not st.any()
     bad = [q for q, g, e in zip(queries, got, exp) if g != e]
     assert not bad, bad[:5]
+
+
+def test_filter_walk_one_pass_and_two_pass_agree():
+    """The one-pass walk (keys chunked on the device, one output reservation per query) and
+    the count + emit passes give the same walks.  The first batch of a fresh engine is sized
+    for 64 Ki keys: a batch returning more takes the two-pass path, which sizes the next
+    batch for the one pass."""
+    w = workloads.generate("E", scale=0.2, n_topics=100)
+    filters = w.filters()
+    ids = [int(x) for x in w.f_id]
+    rng = random.Random(0x1F)
+    queries = [b"#", b"+/#"] + [b"/".join(f.split(b"/")[:2]) + b"/#" for f in rng.sample(filters, 600)]
+    eng = N.Engine(0)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    exp, st = _oracle_walks(filters, ids, [0] * len(filters), queries)
+    assert sum(len(e) for e in exp) > 1 << 16
+    got1 = _engine_walks(eng, queries)
+    s1 = eng.stats()
+    got2 = _engine_walks(eng, queries)
+    s2 = eng.stats()
+    assert s1["n_filter_twopass"] == 1 and s2["n_filter_onepass"] == s1["n_filter_onepass"] + 1
+    assert got1 == exp and got2 == exp
+    # a small batch after it: one pass
+    small = queries[2:50]
+    assert _engine_walks(eng, small) == exp[2:50]

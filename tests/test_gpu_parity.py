@@ -201,6 +201,91 @@ def test_first_mode_term_order_kats():
     assert first(b"q") == []
 
 
+def _random_shape_index(seed, n_filters=4000, n_topics=6000, levels=9, vocab=6):
+    """Filters over a tiny vocabulary with '+' and '#' at every depth (many matching keys of
+    every shape per topic: the FIRST walk's pruning decides between them), word-list and
+    binary exact keys, $-topics; topics of 1..levels levels."""
+    rng = np.random.default_rng(seed)
+    words = [b"w%d" % i for i in range(vocab)] + [b"", b"$s"]
+    ops = []
+    for i in range(n_filters):
+        nl = int(rng.integers(1, levels + 1))
+        ws = [words[int(rng.integers(0, vocab))] for _ in range(nl)]
+        for j in range(nl):
+            if rng.random() < 0.25:
+                ws[j] = b"+"
+        if rng.random() < 0.3:
+            ws = ws[:int(rng.integers(0, nl + 1))] + [b"#"]
+        f = b"/".join(ws)
+        fl = N.TM_KEY_WORDS if (b"+" not in ws and b"#" not in ws and rng.random() < 0.5) else 0
+        ops.append((N.TM_OP_ADD, f, int(rng.integers(0, 50)), fl))
+    topics = []
+    for _ in range(n_topics):
+        nl = int(rng.integers(1, levels + 1))
+        ts = [words[int(rng.integers(0, len(words)))] for _ in range(nl)]
+        topics.append(b"/".join(ts))
+    return ops, topics
+
+
+def _oracle_first(ops, topics):
+    keys = {}
+    for op, f, i, fl in ops:
+        keys[(f, i, fl)] = True
+    ks = sorted(keys)
+    ix = oracle.OrderedIndex.from_filters([k[0] for k in ks], [k[1] for k in ks], [k[2] for k in ks])
+    buf, off = N.pack_topics(topics)
+    return ix.match(buf, off, mode=oracle.MODE_FIRST, threads=8), (buf, off)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("variant", ["wave", "tpw4", "spill", "pool1"])
+def test_first_wave_vs_oracle_random_shapes(seed, variant):
+    """k_match_first_wave (term-order codes, pruning) == the oracle's return_first walk,
+    key for key, on indexes dense in '+' / '#' shapes; also at 4 topics per wave, with every
+    topic forced through the DFS spill kernel, and with the frontier pool exhausted (topics
+    hand off to k_first_slow mid-walk)."""
+    ops, topics = _random_shape_index(seed)
+    kw = {"wave": {}, "tpw4": {"topics_per_wave": 4}, "spill": {"force_slow": True},
+          "pool1": {"seg_chunks": 1, "topics_per_wave": 64}}[variant]
+    eng = _engine(**kw)
+    eng.apply(ops)
+    eng.commit()
+    assert eng.stats()["n_deep_keys"] == 0
+    exp, (buf, off) = _oracle_first(ops, topics)
+    _assert_same(_engine_sets(eng, buf, off, N.TM_MATCH_FIRST), exp, f"first {variant} seed {seed}")
+    eng.close()
+
+
+def test_first_deep_binary_and_deep_word_keys():
+    """Keys past the 31-level order code: a {Binary, {ID}} key 40 levels deep is found by the
+    wave walk (it follows the all-literal path past depth 30); a 35-level word-list key
+    switches the engine to the lane-per-topic DFS (n_deep > 0); both agree with the oracle."""
+    deep = b"/".join(b"L%d" % i for i in range(40))
+    base = [(N.TM_OP_ADD, deep, 1, 0), (N.TM_OP_ADD, b"L0/+/L2/#", 2, 0), (N.TM_OP_ADD, b"L0/L1/L2", 5, 0)]
+    extra = [(N.TM_OP_ADD, deep, 3, N.TM_KEY_WORDS), (N.TM_OP_ADD, b"/".join([b"+"] * 35), 4, 0)]
+    topics = [deep, b"L0/x/L2", b"/".join(b"L%d" % i for i in range(35)), b"L0/L1/L2/q", b"L0/L1/L2"]
+    for ops in (base, base + extra):
+        eng = _engine()
+        eng.apply(ops)
+        eng.commit()
+        assert (eng.stats()["n_deep_keys"] > 0) == (ops is not base)
+        exp, (buf, off) = _oracle_first(ops, topics)
+        _assert_same(_engine_sets(eng, buf, off, N.TM_MATCH_FIRST), exp, f"deep {len(ops)} keys")
+        eng.close()
+
+
+def test_first_edge_cases_vs_oracle(mode):
+    shallow = [f for f in EDGE_FILTERS if len(f.split(b"/")) <= 30]
+    for filters in (shallow, EDGE_FILTERS):
+        ops = [(N.TM_OP_ADD, f, i, 0) for i, f in enumerate(filters)]
+        eng = _engine(mode)
+        eng.apply(ops)
+        eng.commit()
+        exp, (buf, off) = _oracle_first(ops, EDGE_TOPICS)
+        _assert_same(_engine_sets(eng, buf, off, N.TM_MATCH_FIRST), exp, "first edge")
+        eng.close()
+
+
 # ------------------------------------------------------------- edge cases
 EDGE_FILTERS = [b"#", b"+", b"+/+", b"/#", b"/+", b"//", b"", b"a", b"a/#", b"a/+", b"a//b", b"a/+/+", b"+/#",
                 b"$SYS/#", b"$SYS/+", b"$SYS/brokers/+/clients/#", b"+/brokers/#", b"a/#/b", b"a/b#", b"a/b+",

@@ -183,7 +183,10 @@ def _shard_engines_merged(parts, w_topics, oracle_w=None):
         engs.append(eng)
         sixs.append(six)
     torch.cuda.synchronize()
-    stride = max(six.prepare_device(e, d_bytes.data_ptr(), d_off.data_ptr(), n, tb) for six, e in zip(sixs, engs))
+    # per-shard sizing run (the all-reduce(max) of prepare_device is taken here by hand:
+    # one process stands in for G ranks, no process group)
+    stride = max(S.ShardedIndex(S.EngineShard(e), 0, 1).prepare_device(e, d_bytes.data_ptr(), d_off.data_ptr(), n, tb)
+                 for e in engs)
     stride = int(stride * 1.25) + 1024
     cs, ids = [], []
     s = torch.cuda.Stream(dev)
@@ -240,7 +243,7 @@ def test_config_d_eight_shards_vs_oracle_gpu():
     assert flags == 0
     ix = oracle.OrderedIndex(full.f_bytes, full.f_off, full.f_id)
     eoff, eids, _ = ix.match(full.t_bytes, full.t_off, threads=8)
-    assert int(eoff[-1]) > nt  # a real match load, not an empty result
+    assert int(eoff[-1]) > nt // 4  # a real match load (about half the topics hit), not an empty result
     _same_sets(off, ids, eoff, eids)
 
 
