@@ -100,7 +100,7 @@ def batcher_load(eng, tb, to32, seconds):
                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                C.POINTER(C.c_double)]
     runs = []
-    dt = max(2, min(8, cpu_topology()["usable_cpus"] // 2))
+    dt = max(2, min(14, cpu_topology()["usable_cpus"] - 3))  # leave the cutter, completer and caller a CPU
     for pubs in (4096, 65536, 262144):
         b = N.Batcher(eng, max_batch=65536, max_wait_us=200, delivery_threads=dt)
         got, ids, errs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
@@ -114,7 +114,10 @@ def batcher_load(eng, tb, to32, seconds):
                      "ids_per_s": round(ids.value / el.value, 1),
                      "mean_batch": round(st["publishes"] / max(st["batches"], 1), 1),
                      "lat_p50_ms": round(st["lat_p50_us"] / 1e3, 3), "lat_p99_ms": round(st["lat_p99_us"] / 1e3, 3),
-                     "backend_frac": round(st["backend_us"] * 1e-6 / el.value, 3)})
+                     "backend_frac": round(st["backend_us"] * 1e-6 / el.value, 3),
+                     # share of the run's wall time each pipeline stage was busy (stages overlap)
+                     "stage_busy": {k: round(st[k + "_us"] * 1e-6 / el.value, 3)
+                                    for k in ("cut", "enqueue", "gpu_wait", "copy", "deliver")}})
     return {"api": f"tm_batcher_submit (max_batch 65536, max_wait 200 us, {dt} delivery threads)", "runs": runs,
             "note": "closed loop: each publisher resubmits from its result callback; ids copied to host per "
                     "window, two windows in flight (GPU walk of one overlaps PCIe + callbacks of the other)"}
@@ -235,6 +238,8 @@ def main():
     ap.add_argument("--batcher-seconds", type=float, default=2.0,
                     help="closed-loop load per publisher count through the batching aggregator (0: skip)")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no CPU baseline)")
+    ap.add_argument("--quick", action="store_true",
+                    help="development run: skip the CPU baseline and the matches_filter / intersection legs")
     ap.add_argument("--mode", choices=("replicated", "sharded"), default="replicated",
                     help="replicated trie, publishes data-parallel (default); or filters hash-sharded over "
                          "ranks with an RCCL all-gather merge (config D; DESIGN.md §6)")
@@ -450,11 +455,12 @@ def main():
     # ---------------------------------------------------------------- CPU baseline + parity sample
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile and not args.quick:
         cpu, parity = cpu_baseline(args, w, eng, tb, to, n)
     # the rest of the index API on the same engine, off the headline metric
-    filt = filter_leg(args, w, eng, 20000) if rank == 0 and not args.profile else None
-    inter = intersect_leg(w, tb, to) if rank == 0 and not args.profile else None
+    legs = rank == 0 and not args.profile and not args.quick
+    filt = filter_leg(args, w, eng, 20000) if legs else None
+    inter = intersect_leg(w, tb, to) if legs else None
 
     rss = torch.tensor([host_rss_gib()], dtype=torch.float64, device=dev if backend != "gloo" else "cpu")
     if world > 1:
@@ -797,7 +803,7 @@ def filter_leg(args, w, eng, q):
     dt_cpu = time.perf_counter() - t0
     ps = min(q, 20000)
     eo, eids, est, src = ix.match(qb, qo[:ps + 1], algo=oracle.ALGO_FILTER, with_src=True)
-    eng_ids = eng.key_ids(k[:int(o[ps - 1] + c[ps - 1])]) if ps else np.zeros(0, np.uint64)
+    eng_ids = eng.key_ids(k) if len(k) else np.zeros(0, np.uint64)  # ranges are in any order
     bad = 0
     for i in range(ps):
         if not np.array_equal(eng_ids[o[i]:o[i] + c[i]], w.f_id[src[eo[i]:eo[i + 1]]]):

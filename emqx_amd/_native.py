@@ -131,7 +131,8 @@ class tm_batch_view(C.Structure):
 class tm_batcher_stats(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("publishes", C.c_uint64), ("max_batch_seen", C.c_uint64),
                 ("backend_us", C.c_uint64), ("lat_p50_us", C.c_double), ("lat_p99_us", C.c_double),
-                ("lat_max_us", C.c_double)]
+                ("lat_max_us", C.c_double), ("cut_us", C.c_uint64), ("enqueue_us", C.c_uint64),
+                ("gpu_wait_us", C.c_uint64), ("copy_us", C.c_uint64), ("deliver_us", C.c_uint64)]
 
 
 tm_match_cb = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.POINTER(C.c_uint64), C.c_uint32)
@@ -489,10 +490,11 @@ class Engine:
 
     STAT_NAMES = ("node_visits", "edge_probes", "word_probes", "keys", "levels", "spilled_topics",
                   "segments", "chunk_flushes", "frontier_chunks", "node_records", "inline_keys",
-                  "cyc_prescan", "cyc_walk", "cyc_copyout")
+                  "cyc_prescan", "cyc_walk", "cyc_copyout", "hot_cyc_prescan", "hot_cyc_walk", "hot_cyc_copyout",
+                  "hot_waves")
 
     def debug_stats(self, enable: bool, read: bool = True):
-        out = (C.c_uint64 * 14)()
+        out = (C.c_uint64 * 18)()
         self._check(self.lib.tm_debug_stats(self.h, 1 if enable else 0, out if read else None))
         return list(out) if read else None
 

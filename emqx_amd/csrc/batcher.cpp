@@ -13,9 +13,10 @@
 //      D2H of the offsets, statuses and the batch's counter block;
 //   2. the completion thread waits for that, then copies the ids back on a separate copy
 //      stream (so window k's PCIe transfer overlaps window k+1's walk);
-//   3. the delivery threads call every publisher of the window back, in parallel (each
-//      thread owns a contiguous range of the window); the completion thread is one of them.
-// Two slots alternate, so window k+1 runs on the GPU while window k is delivered.
+//   3. the delivery thread and its pool call every publisher of the window back, in
+//      parallel (each thread owns a contiguous range of the window).
+// Three slots rotate: window k+2 is cut and walks on the GPU while window k+1's ids cross
+// PCIe and window k's publishers are called back.
 // Submissions go to one of SHARDS queue shards (by submitting thread), so publishers that
 // resubmit from their callbacks do not all contend on one lock.
 #include <hip/hip_runtime.h>
@@ -115,7 +116,7 @@ struct Pending {
 constexpr size_t LAT_RING = 65536;
 constexpr size_t QUEUE_BYTES_MAX = 1ull << 31;
 constexpr uint32_t SHARDS = 16;
-constexpr uint32_t NSLOT = 2;
+constexpr uint32_t NSLOT = 3;  // window k+2 cut / on the GPU, k+1 on PCIe, k being delivered
 constexpr uint32_t CTL_BYTES = 32;  // the engine's per-launch counter block {total, slow, seg, fr}
 
 struct alignas(64) Shard {
@@ -138,12 +139,19 @@ struct Slot {
     uint32_t n = 0;
     uint32_t mode = 0;
     int rc = 0;
-    uint64_t t_enq = 0;
+    uint64_t t_enq = 0, t_done = 0;
     // engine backend
     HBuf h_bytes, h_off, h_off_out, h_status, h_cnt, h_ids, h_ctl;
     DBuf d_bytes, d_off, d_ids, d_off_out;
     uint64_t nbytes = 0, ids_cap = 0, keys_cap = 0;
     hipEvent_t ev = nullptr;
+    // the ids cross PCIe in chunks (by publish range) and delivery starts on a chunk as soon
+    // as its copy is done, so a window's copy and its callbacks overlap
+    static constexpr uint32_t MAXCH = 8;
+    uint32_t nchunk = 1;
+    uint32_t chunk_lo[MAXCH + 1] = {};
+    hipEvent_t cev[MAXCH] = {};
+    bool cev_wait = false;              // chunk events to wait for before delivering
     bool narrow = false;                // ids crossed PCIe as u32 (every id < 2^32); widened at delivery
     bool host_done = false;             // the result was produced synchronously (custom / host path)
     std::vector<uint32_t> cnt;          // per-publish counts
@@ -173,21 +181,25 @@ struct tm_batcher {
     Slot slot[NSLOT];
     std::mutex slot_mu;  // slot states + completion FIFO
     std::condition_variable slot_cv;
-    std::deque<uint32_t> fifo;  // slots queued for completion, in window order
-    bool cutter_done = false;   // under slot_mu
+    std::deque<uint32_t> fifo;   // slots queued for completion, in window order
+    std::deque<uint32_t> dfifo;  // slots ready for delivery, in window order
+    bool cutter_done = false;    // under slot_mu
+    bool completer_done = false;
 
-    std::thread cutter, completer;
+    std::thread cutter, completer, deliverer;
     std::vector<std::thread> pool;
     // delivery jobs: one window split in n_delivery + 1 ranges
     std::mutex job_mu;
     std::condition_variable job_cv, job_done_cv;
     Slot *job_slot = nullptr;
+    uint32_t job_lo = 0, job_hi = 0;
     uint64_t job_gen = 0;
     uint32_t job_left = 0;
     bool pool_stop = false;
 
     std::mutex st_mu;  // stats
     uint64_t n_batches = 0, n_pub = 0, max_seen = 0, backend_ns = 0;
+    std::atomic<uint64_t> ns_cut{0}, ns_enq{0}, ns_gpu{0}, ns_copy{0}, ns_del{0};  // stage times
     std::vector<uint32_t> lat_ns;
     size_t lat_pos = 0, lat_n = 0;
 
@@ -351,8 +363,17 @@ struct tm_batcher {
 
     // Completion of an engine window: counter block back -> maybe re-run -> ids D2H -> view.
     int complete(Slot &S) {
-        if (S.host_done) return TM_OK;
+        if (S.host_done) {
+            S.nchunk = 1;
+            S.chunk_lo[0] = 0;
+            S.chunk_lo[1] = S.n;
+            S.cev_wait = false;
+            return TM_OK;
+        }
+        const uint64_t tw0 = now_ns();
         BT_HIP(hipEventSynchronize(S.ev));
+        const uint64_t tw1 = now_ns();
+        ns_gpu.fetch_add(tw1 - tw0, std::memory_order_relaxed);
         const uint64_t *ctl = S.h_ctl.as<uint64_t>();
         const uint64_t total = ctl[0], seg = ctl[2], fr = ctl[3];
         const bool over = (S.mode != TM_MATCH_COUNT && S.mode != TM_MATCH_FIRST) && total > S.keys_cap;
@@ -372,7 +393,11 @@ struct tm_batcher {
             }
         }
         S.v.status = S.h_status.as<int32_t>();
+        S.nchunk = 1;
+        S.chunk_lo[0] = 0;
+        S.chunk_lo[1] = S.n;
         if (S.mode == TM_MATCH_COUNT) {
+            S.cev_wait = false;
             uint32_t *oo = S.h_off_out.as<uint32_t>();
             std::memset(oo, 0, (size_t)S.n * 4);
             S.v.off = oo;
@@ -384,15 +409,30 @@ struct tm_batcher {
         const uint64_t got = oo[S.n];
         const uint64_t w = S.narrow ? 4 : 8;
         BT_HIP(S.h_ids.ensure(got * w + 8));
-        if (got) {
-            BT_HIP(hipMemcpyAsync(S.h_ids.p, S.d_ids.p, got * w, hipMemcpyDeviceToHost, s_copy));
-            BT_HIP(hipStreamSynchronize(s_copy));
+        // chunks of >= 1 MiB of ids, at most MAXCH, cut at publish boundaries
+        uint32_t nch = (uint32_t)std::min<uint64_t>(Slot::MAXCH, std::max<uint64_t>(1, got * w >> 20));
+        nch = std::max<uint32_t>(1, std::min<uint32_t>(nch, S.n));
+        S.chunk_lo[0] = 0;
+        for (uint32_t j = 1; j < nch; j++) {  // first publish whose ids start at or past j/nch
+            const uint64_t want = got * j / nch;
+            S.chunk_lo[j] = (uint32_t)(std::lower_bound(oo, oo + S.n, (uint32_t)want) - oo);
+            S.chunk_lo[j] = std::max(S.chunk_lo[j], S.chunk_lo[j - 1]);
+        }
+        S.chunk_lo[nch] = S.n;
+        S.nchunk = nch;
+        for (uint32_t j = 0; j < nch; j++) {
+            const uint64_t a = oo[S.chunk_lo[j]], b = oo[S.chunk_lo[j + 1]];
+            if (b > a)
+                BT_HIP(hipMemcpyAsync(S.h_ids.as<uint8_t>() + a * w, (const uint8_t *)S.d_ids.p + a * w, (b - a) * w,
+                                      hipMemcpyDeviceToHost, s_copy));
+            BT_HIP(hipEventRecord(S.cev[j], s_copy));
         }
         S.cnt.resize(S.n);
         for (uint32_t i = 0; i < S.n; i++) S.cnt[i] = oo[i + 1] - oo[i];
         S.v.off = oo;
         S.v.cnt = S.cnt.data();
         S.v.ids = S.h_ids.as<uint64_t>();  // u32 words when narrow (deliver_range widens)
+        S.cev_wait = true;
         return TM_OK;
     }
 
@@ -444,41 +484,57 @@ struct tm_batcher {
         uint64_t seen = 0;
         for (;;) {
             Slot *S;
-            uint64_t gen;
+            uint32_t lo, hi;
             {
                 std::unique_lock<std::mutex> lk(job_mu);
                 job_cv.wait(lk, [&] { return pool_stop || job_gen != seen; });
                 if (pool_stop) return;
-                seen = gen = job_gen;
+                seen = job_gen;
                 S = job_slot;
+                lo = job_lo;
+                hi = job_hi;
             }
-            const uint32_t parts = parts_for(S->n);
-            if (idx + 1 < parts) {  // part 0 is the completion thread's
-                const uint64_t lo = (uint64_t)S->n * (idx + 1) / parts, hi = (uint64_t)S->n * (idx + 2) / parts;
-                deliver_range(*S, (uint32_t)lo, (uint32_t)hi);
+            const uint32_t parts = parts_for(hi - lo);
+            if (idx + 1 < parts) {  // part 0 is the delivery thread's own
+                const uint64_t n = hi - lo;
+                deliver_range(*S, lo + (uint32_t)(n * (idx + 1) / parts), lo + (uint32_t)(n * (idx + 2) / parts));
             }
             std::lock_guard<std::mutex> g(job_mu);
             if (--job_left == 0) job_done_cv.notify_all();
-            (void)gen;
         }
     }
 
-    void deliver(Slot &S) {
-        const uint32_t parts = parts_for(S.n);
+    // publishes [lo, hi) of S, split over the delivery thread and its pool
+    void deliver_part(Slot &S, uint32_t lo, uint32_t hi) {
+        const uint32_t parts = parts_for(hi - lo);
         if (parts <= 1 || pool.empty()) {
-            deliver_range(S, 0, S.n);
+            deliver_range(S, lo, hi);
             return;
         }
         {
             std::lock_guard<std::mutex> g(job_mu);
             job_slot = &S;
+            job_lo = lo;
+            job_hi = hi;
             job_left = (uint32_t)pool.size();
             job_gen++;
         }
         job_cv.notify_all();
-        deliver_range(S, 0, (uint32_t)((uint64_t)S.n / parts));
+        deliver_range(S, lo, lo + (uint32_t)((uint64_t)(hi - lo) / parts));
         std::unique_lock<std::mutex> lk(job_mu);
         job_done_cv.wait(lk, [&] { return job_left == 0; });
+    }
+
+    // chunk by chunk, each as soon as its ids have landed
+    void deliver(Slot &S) {
+        for (uint32_t j = 0; j < S.nchunk; j++) {
+            if (S.cev_wait) {
+                const uint64_t t0 = now_ns();
+                if (hipEventSynchronize(S.cev[j]) != hipSuccess) S.rc = TM_EDEVICE;
+                ns_copy.fetch_add(now_ns() - t0, std::memory_order_relaxed);  // waited on PCIe
+            }
+            deliver_part(S, S.chunk_lo[j], S.chunk_lo[j + 1]);
+        }
     }
 
     // ------------------------------------------------------------------ threads
@@ -524,9 +580,11 @@ struct tm_batcher {
                 slot_cv.wait(lk, [&] { return S.state == Slot::FREE; });
                 S.state = Slot::BUSY;
             }
+            const uint64_t tc0 = now_ns();
             S.rc = take_window(S);
             S.mode = cfg.mode;
             S.t_enq = now_ns();
+            ns_cut.fetch_add(S.t_enq - tc0, std::memory_order_relaxed);
             if (S.rc == TM_OK && S.n) {
                 if (eng) {
                     std::lock_guard<std::mutex> g(eng_mu);
@@ -541,6 +599,7 @@ struct tm_batcher {
                     S.narrow = false;
                 }
             }
+            ns_enq.fetch_add(now_ns() - S.t_enq, std::memory_order_relaxed);
             {
                 std::lock_guard<std::mutex> g(slot_mu);
                 fifo.push_back(next);
@@ -556,6 +615,7 @@ struct tm_batcher {
         slot_cv.notify_all();
     }
 
+    // stage 2: the GPU part is done -> ids over PCIe (copy stream) -> to the delivery stage
     void completer_loop() {
         for (;;) {
             uint32_t si;
@@ -567,17 +627,48 @@ struct tm_batcher {
                 fifo.pop_front();
             }
             Slot &S = slot[si];
+            S.nchunk = 1;  // one chunk, nothing to wait for, unless complete() streams the ids
+            S.chunk_lo[0] = 0;
+            S.chunk_lo[1] = S.n;
+            S.cev_wait = false;
             if (S.rc == TM_OK && S.n && eng) S.rc = complete(S);
-            const uint64_t te = now_ns();
+            S.t_done = now_ns();
+            {
+                std::lock_guard<std::mutex> g(slot_mu);
+                dfifo.push_back(si);
+            }
+            slot_cv.notify_all();
+        }
+        {
+            std::lock_guard<std::mutex> g(slot_mu);
+            completer_done = true;
+        }
+        slot_cv.notify_all();
+    }
+
+    // stage 3: call the window's publishers back (with the delivery pool), free the slot
+    void deliverer_loop() {
+        for (;;) {
+            uint32_t si;
+            {
+                std::unique_lock<std::mutex> lk(slot_mu);
+                slot_cv.wait(lk, [&] { return !dfifo.empty() || completer_done; });
+                if (dfifo.empty()) break;
+                si = dfifo.front();
+                dfifo.pop_front();
+            }
+            Slot &S = slot[si];
             if (S.n) {
                 {
                     std::lock_guard<std::mutex> g(st_mu);  // counted before the callbacks
                     n_batches++;
                     n_pub += S.n;
                     max_seen = std::max<uint64_t>(max_seen, S.n);
-                    backend_ns += te - S.t_enq;
+                    backend_ns += S.t_done - S.t_enq;
                 }
+                const uint64_t td0 = now_ns();
                 deliver(S);
+                ns_del.fetch_add(now_ns() - td0, std::memory_order_relaxed);
             }
             {
                 std::lock_guard<std::mutex> g(slot_mu);
@@ -605,10 +696,14 @@ struct tm_batcher {
                 hipStreamCreateWithFlags(&s_comp, hipStreamNonBlocking) != hipSuccess ||
                 hipStreamCreateWithFlags(&s_copy, hipStreamNonBlocking) != hipSuccess)
                 return TM_EDEVICE;
+            for (Slot &S : slot)
+                for (hipEvent_t &e : S.cev)
+                    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return TM_EDEVICE;
         }
         try {
             for (uint32_t i = 0; i < n_delivery; i++) pool.emplace_back([this, i] { pool_loop(i); });
             completer = std::thread([this] { completer_loop(); });
+            deliverer = std::thread([this] { deliverer_loop(); });
             cutter = std::thread([this] { cutter_loop(); });
         } catch (...) {
             stop();
@@ -630,6 +725,12 @@ struct tm_batcher {
         }
         slot_cv.notify_all();
         if (completer.joinable()) completer.join();
+        else {
+            std::lock_guard<std::mutex> g(slot_mu);
+            completer_done = true;
+        }
+        slot_cv.notify_all();
+        if (deliverer.joinable()) deliverer.join();
         {
             std::lock_guard<std::mutex> g(job_mu);
             pool_stop = true;
@@ -639,8 +740,11 @@ struct tm_batcher {
             if (t.joinable()) t.join();
         if (eng) {
             (void)hipSetDevice(device);
-            for (Slot &S : slot)
+            for (Slot &S : slot) {
                 if (S.ev) (void)hipEventDestroy(S.ev);
+                for (hipEvent_t e : S.cev)
+                    if (e) (void)hipEventDestroy(e);
+            }
             if (s_comp) (void)hipStreamDestroy(s_comp);
             if (s_copy) (void)hipStreamDestroy(s_copy);
         }
@@ -748,6 +852,11 @@ int tm_batcher_stats_get(tm_batcher *b, tm_batcher_stats *out) {
         out->publishes = b->n_pub;
         out->max_batch_seen = b->max_seen;
         out->backend_us = b->backend_ns / 1000;
+        out->cut_us = b->ns_cut / 1000;
+        out->enqueue_us = b->ns_enq / 1000;
+        out->gpu_wait_us = b->ns_gpu / 1000;
+        out->copy_us = b->ns_copy / 1000;
+        out->deliver_us = b->ns_del / 1000;
         lat.assign(b->lat_ns.begin(), b->lat_ns.begin() + (ptrdiff_t)b->lat_n);
     }
     out->lat_p50_us = out->lat_p99_us = out->lat_max_us = 0;

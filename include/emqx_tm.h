@@ -112,7 +112,7 @@ typedef struct tm_config {
     uint32_t seg_chunks;          /* 0 = auto; else fixed size of the key-segment and
                                      frontier-overflow chunk pools (test aid: exhaustion
                                      routes topics to the spill kernel, results stay exact) */
-    uint32_t edge_load_inv;       /* edge-table load <= 1/edge_load_inv (0 = default 8): a wave
+    uint32_t edge_load_inv;       /* edge-table load <= 1/edge_load_inv (0 = default 16): a wave
                                      waits for its longest probe chain, so lower load shortens
                                      the walk at the price of HBM (16 B per slot) */
     uint32_t topics_per_wave;     /* 0 = by batch size (4..64); else 4, 8, 16, 32 or 64 */
@@ -318,13 +318,15 @@ int tm_key_info(const tm_engine *eng, uint32_t key, uint64_t *id, uint32_t *flag
 int tm_key_ids(const tm_engine *eng, const uint32_t *keys, size_t n, uint64_t *ids_out);
 int tm_stats(const tm_engine *eng, tm_stats_t *out);
 
-/* diagnostics: enable/disable device walk counters; when out14 != NULL, first
+/* diagnostics: enable/disable device walk counters; when out18 != NULL, first
  * read the counters accumulated since the last call: {node visits, edge-slot
  * probes, word-slot probes, keys emitted, topic levels, topics spilled to the
  * slow kernel, key segments, segment-chunk flushes, frontier overflow chunks,
- * list-header reads, keys emitted inline from edge slots, and the summed wave
- * cycles of the fast kernel's phases: stage+pre-scan, walk, copy-out}. */
-int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out14);
+ * list-header reads, keys emitted inline from edge slots, the summed wave
+ * cycles of the fast kernel's phases: stage+pre-scan, walk, copy-out; the same
+ * three phases summed over the waves holding a topic with more than 256 keys
+ * (under a hot '#' filter), and the number of such waves}. */
+int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out18);
 /* diagnostics: time the dominant kernel of the next match with HIP events on its
  * launch stream; enable=1 arms, then (after the match) enable=0 + ms_out reads. */
 int tm_debug_timing(tm_engine *eng, int enable, float *ms_out);

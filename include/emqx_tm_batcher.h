@@ -10,9 +10,9 @@
  *
  *   window   a batch is dispatched when max_batch publishes are queued, or when the
  *            oldest queued publish has waited max_wait_us, or at tm_batcher_destroy
- *            (which drains the queue).  Two windows are in flight at once: while window
- *            k+1 walks on the GPU, window k's ids cross PCIe and its publishers are called
- *            back; under load windows grow by themselves.
+ *            (which drains the queue).  Three windows are in flight at once: window k+2
+ *            walks on the GPU while window k+1's ids cross PCIe and window k's publishers
+ *            are called back; under load windows grow by themselves.
  *   result   per publish: TM_TOPIC_OK with the ids of its matched keys (route dests,
  *            emqx_topic_index:get_id/1 of every key, emqx_topic_index.erl:87-89), or
  *            TM_BADARG with no ids (a level exactly "+" or "#": emqx_trie_search.erl:374-375),
@@ -45,8 +45,8 @@ typedef struct tm_batcher_config {
     uint32_t max_batch;    /* publishes per engine batch (0 = 65536)              */
     uint32_t max_wait_us;  /* window bound from the oldest queued publish (0 = 200) */
     uint32_t mode;         /* TM_MATCH_ALL / UNIQUE / AGGRE / FIRST / COUNT        */
-    uint32_t delivery_threads; /* threads calling publishers back, the completion thread
-                                  included (0 = 4); each takes a contiguous share of a window */
+    uint32_t delivery_threads; /* threads calling publishers back (0 = 4); each takes a
+                                  contiguous share of a window */
 } tm_batcher_config;
 
 /* One publish's result; `ids` is valid only during the call. */
@@ -72,6 +72,9 @@ typedef struct tm_batcher_stats {
     uint64_t backend_us;        /* wall time inside the engine / backend, summed  */
     /* submit -> callback latency over the last (up to) 65536 publishes, microseconds */
     double   lat_p50_us, lat_p99_us, lat_max_us;
+    /* per pipeline stage, microseconds summed over windows: cutting a window from the queue,
+     * queueing its GPU part, waiting for the GPU part, its ids over PCIe, calling back */
+    uint64_t cut_us, enqueue_us, gpu_wait_us, copy_us, deliver_us;
 } tm_batcher_stats;
 
 /* Over an engine: batches go through tm_match_device_mode on the engine's device and the

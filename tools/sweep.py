@@ -30,9 +30,10 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 # same-process reference point.
 VARIANTS = {
     "base": ([], 0),
+    "nt": (["-DTM_NT_KEYS=1"], 0),
+    "rpl3": (["-DTM_RPL=3"], 0),
+    "nt16": (["-DTM_NT_KEYS=1"], 16),
     "tpw32": ([], 0, 32),
-    "tpw16": ([], 0, 16),
-    "tpw64": ([], 0, 64),
 }
 
 
@@ -50,7 +51,8 @@ def build(names):
                                                 text=True))
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wno-unused-function", *flags, os.path.join(CSRC, "engine.cpp"),
-               kern, os.path.join(CSRC, "result_kernels.hip"), os.path.join(CSRC, "filter_kernels.hip"), "-o", out]
+               os.path.join(CSRC, "batcher.cpp"), kern, os.path.join(CSRC, "result_kernels.hip"),
+               os.path.join(CSRC, "filter_kernels.hip"), "-o", out]
         procs.append((name, subprocess.Popen(cmd)))
         if len(procs) >= 4:
             n, p = procs.pop(0)
