@@ -193,9 +193,13 @@ struct tm_batcher {
     std::condition_variable job_cv, job_done_cv;
     Slot *job_slot = nullptr;
     uint32_t job_lo = 0, job_hi = 0;
-    uint64_t job_gen = 0;
-    uint32_t job_left = 0;
-    bool pool_stop = false;
+    // a job is published by bumping job_gen (release) after its fields are set; pool threads
+    // spin on it a little before sleeping, and the delivery thread spins on job_left, so a
+    // hand-off costs about a microsecond instead of a futex wake-up
+    std::atomic<uint64_t> job_gen{0};
+    std::atomic<uint32_t> job_left{0};
+    std::atomic<uint32_t> sleepers{0};
+    std::atomic<bool> pool_stop{false};
 
     std::mutex st_mu;  // stats
     uint64_t n_batches = 0, n_pub = 0, max_seen = 0, backend_ns = 0;
@@ -409,8 +413,8 @@ struct tm_batcher {
         const uint64_t got = oo[S.n];
         const uint64_t w = S.narrow ? 4 : 8;
         BT_HIP(S.h_ids.ensure(got * w + 8));
-        // chunks of >= 1 MiB of ids, at most MAXCH, cut at publish boundaries
-        uint32_t nch = (uint32_t)std::min<uint64_t>(Slot::MAXCH, std::max<uint64_t>(1, got * w >> 20));
+        // chunks of >= 2 MiB of ids, at most MAXCH, cut at publish boundaries
+        uint32_t nch = (uint32_t)std::min<uint64_t>(Slot::MAXCH, std::max<uint64_t>(1, got * w >> 21));
         nch = std::max<uint32_t>(1, std::min<uint32_t>(nch, S.n));
         S.chunk_lo[0] = 0;
         for (uint32_t j = 1; j < nch; j++) {  // first publish whose ids start at or past j/nch
@@ -445,6 +449,7 @@ struct tm_batcher {
         uint64_t now = 0;
         for (uint32_t i = lo; i < hi; i++) {
             const Pending &p = S.pubs[i];
+            if (i + 8 < hi) __builtin_prefetch(S.pubs[i + 8].ctx);  // the caller's per-publish state
             if (S.rc < 0) {
                 p.cb(p.ctx, S.rc, nullptr, 0);
             } else {
@@ -480,27 +485,35 @@ struct tm_batcher {
         return std::max<uint32_t>(1, std::min<uint32_t>(n_delivery + 1, n / 256));
     }
 
+    static constexpr int SPIN = 256;  // polls (a few microseconds) before sleeping: the CPUs are a quota
+
     void pool_loop(uint32_t idx) {
         uint64_t seen = 0;
         for (;;) {
-            Slot *S;
-            uint32_t lo, hi;
-            {
+            int spins = 0;
+            while (job_gen.load(std::memory_order_acquire) == seen && !pool_stop.load(std::memory_order_relaxed)) {
+                if (++spins < SPIN) {
+                    __builtin_ia32_pause();
+                    continue;
+                }
                 std::unique_lock<std::mutex> lk(job_mu);
-                job_cv.wait(lk, [&] { return pool_stop || job_gen != seen; });
-                if (pool_stop) return;
-                seen = job_gen;
-                S = job_slot;
-                lo = job_lo;
-                hi = job_hi;
+                sleepers.fetch_add(1);
+                job_cv.wait(lk, [&] { return pool_stop.load() || job_gen.load() != seen; });
+                sleepers.fetch_sub(1);
             }
+            if (pool_stop.load()) return;
+            seen = job_gen.load(std::memory_order_acquire);
+            Slot *S = job_slot;
+            const uint32_t lo = job_lo, hi = job_hi;
             const uint32_t parts = parts_for(hi - lo);
             if (idx + 1 < parts) {  // part 0 is the delivery thread's own
                 const uint64_t n = hi - lo;
                 deliver_range(*S, lo + (uint32_t)(n * (idx + 1) / parts), lo + (uint32_t)(n * (idx + 2) / parts));
             }
-            std::lock_guard<std::mutex> g(job_mu);
-            if (--job_left == 0) job_done_cv.notify_all();
+            if (job_left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                std::lock_guard<std::mutex> g(job_mu);
+                job_done_cv.notify_all();
+            }
         }
     }
 
@@ -511,18 +524,25 @@ struct tm_batcher {
             deliver_range(S, lo, hi);
             return;
         }
-        {
+        job_slot = &S;
+        job_lo = lo;
+        job_hi = hi;
+        job_left.store((uint32_t)pool.size(), std::memory_order_relaxed);
+        job_gen.fetch_add(1, std::memory_order_acq_rel);
+        if (sleepers.load()) {
             std::lock_guard<std::mutex> g(job_mu);
-            job_slot = &S;
-            job_lo = lo;
-            job_hi = hi;
-            job_left = (uint32_t)pool.size();
-            job_gen++;
+            job_cv.notify_all();
         }
-        job_cv.notify_all();
         deliver_range(S, lo, lo + (uint32_t)((uint64_t)(hi - lo) / parts));
-        std::unique_lock<std::mutex> lk(job_mu);
-        job_done_cv.wait(lk, [&] { return job_left == 0; });
+        int spins = 0;
+        while (job_left.load(std::memory_order_acquire) != 0) {
+            if (++spins < SPIN) {
+                __builtin_ia32_pause();
+                continue;
+            }
+            std::unique_lock<std::mutex> lk(job_mu);
+            job_done_cv.wait(lk, [&] { return job_left.load() == 0; });
+        }
     }
 
     // chunk by chunk, each as soon as its ids have landed
@@ -733,7 +753,7 @@ struct tm_batcher {
         if (deliverer.joinable()) deliverer.join();
         {
             std::lock_guard<std::mutex> g(job_mu);
-            pool_stop = true;
+            pool_stop.store(true);
         }
         job_cv.notify_all();
         for (std::thread &t : pool)

@@ -228,3 +228,19 @@ def test_closed_loop_loadgen_over_python_backend():
     assert s["publishes"] == got.value and s["batches"] < got.value
     per = [len(_expect(t)) for t in (b"a/b", b"x/y/z", b"a", b"$SYS/a")]
     assert ids.value <= max(per) * got.value
+
+
+def test_batcher_pipeline_under_thread_sanitizer():
+    """tests/native/batcher_tsan: the aggregator's threads (cutter, completion, delivery
+    pool) and sharded submission under ThreadSanitizer, 8,192 closed-loop publishers over
+    a custom backend (no device)."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "batcher_tsan")
+    if not os.path.exists(exe):
+        pytest.fail("tests/native/batcher_tsan not built (run __graft_entry__.build())")
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 report_signal_unsafe=0")
+    p = subprocess.run([exe, "8192", "16", "1", "4"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "ThreadSanitizer" not in p.stderr, p.stderr[-3000:]
+    assert '"errors": 0' in p.stdout
