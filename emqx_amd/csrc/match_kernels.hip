@@ -32,7 +32,10 @@
 namespace tmx {
 
 constexpr int WAVE = 64;
-constexpr int FCAP = 256;        // frontier entries per wave per depth held in LDS
+#ifndef TM_FCAP
+#define TM_FCAP 384  // 256 -> 384: fewer frontier overflows to HBM chunks for 2 fewer waves per CU (0.889 -> 0.868 ms); 512 loses more occupancy than it saves
+#endif
+constexpr int FCAP = TM_FCAP;    // frontier entries per wave per depth held in LDS
 constexpr int FCH = FR_CHUNK;    // frontier entries per global overflow chunk
 constexpr int MAXF = 32;         // overflow chunks per frontier buffer per wave
 #ifndef TM_SCAP

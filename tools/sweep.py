@@ -30,9 +30,10 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 # same-process reference point.
 VARIANTS = {
     "base": ([], 0),
-    "nt": (["-DTM_NT_KEYS=1"], 0),
-    "rpl3": (["-DTM_RPL=3"], 0),
-    "nt16": (["-DTM_NT_KEYS=1"], 16),
+    "tb2560": (["-DTM_TBCAP=2560"], 0),
+    "tb2560_f448": (["-DTM_TBCAP=2560", "-DTM_FCAP=448"], 0),
+    "scap96": (["-DTM_SCAP=96"], 0),
+    "fcap320": (["-DTM_FCAP=320"], 0),
     "tpw32": ([], 0, 32),
 }
 
