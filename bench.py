@@ -120,7 +120,8 @@ def batcher_load(eng, tb, to32, seconds):
                                     for k in ("cut", "enqueue", "gpu_wait", "copy", "deliver")}})
     return {"api": f"tm_batcher_submit (max_batch 65536, max_wait 200 us, {dt} delivery threads)", "runs": runs,
             "note": "closed loop: each publisher resubmits from its result callback; ids copied to host per "
-                    "window, two windows in flight (GPU walk of one overlaps PCIe + callbacks of the other)"}
+                    "window as u32 in chunks; four windows in flight (GPU walk / PCIe / callbacks); "
+                    "stage_busy: share of wall time each stage worked (copy and deliver: per delivery thread)"}
 
 
 def gather_roof(walk, kernel_ms):

@@ -13,9 +13,13 @@
 //      D2H of the offsets, statuses and the batch's counter block;
 //   2. the completion thread waits for that, then copies the ids back on a separate copy
 //      stream (so window k's PCIe transfer overlaps window k+1's walk);
-//   3. the delivery thread and its pool call every publisher of the window back, in
-//      parallel (each thread owns a contiguous range of the window).
-// Three slots rotate: window k+2 is cut and walks on the GPU while window k+1's ids cross
+//   3. the delivery threads call the publishers back: the completion thread splits each
+//      window into publish ranges (per PCIe chunk) on one work queue, and every delivery
+//      thread takes the next range, waits for its chunk's copy if it has not landed, and
+//      calls that range back.  No thread waits for another: a window's slot is freed by
+//      whichever thread finishes its last range, and the next window's ranges are taken
+//      while stragglers of this one still run.
+// Four slots rotate: window k+3 is cut and walks on the GPU while earlier windows' ids cross
 // PCIe and window k's publishers are called back.
 // Submissions go to one of SHARDS queue shards (by submitting thread), so publishers that
 // resubmit from their callbacks do not all contend on one lock.
@@ -116,8 +120,16 @@ struct Pending {
 constexpr size_t LAT_RING = 65536;
 constexpr size_t QUEUE_BYTES_MAX = 1ull << 31;
 constexpr uint32_t SHARDS = 16;
-constexpr uint32_t NSLOT = 3;  // window k+2 cut / on the GPU, k+1 on PCIe, k being delivered
-constexpr uint32_t CTL_BYTES = 32;  // the engine's per-launch counter block {total, slow, seg, fr}
+#ifndef TM_NSLOT
+#define TM_NSLOT 4
+#endif
+// windows in flight: k+3 cut / on the GPU, k+2 and k+1 on PCIe or waiting, k being delivered.
+// A fourth slot lets the next window be cut while delivery still holds one (65,536 closed-loop
+// publishers: 39 -> 44 M publishes/s)
+constexpr uint32_t NSLOT = TM_NSLOT;
+constexpr uint32_t CTL_BYTES = 32;
+// the threads that wait on these sleep in the driver instead of spinning a CPU of the quota
+constexpr unsigned EV_FLAGS = hipEventDisableTiming | hipEventBlockingSync;  // the engine's per-launch counter block {total, slow, seg, fr}
 
 struct alignas(64) Shard {
     std::mutex m;
@@ -151,6 +163,8 @@ struct Slot {
     uint32_t nchunk = 1;
     uint32_t chunk_lo[MAXCH + 1] = {};
     hipEvent_t cev[MAXCH] = {};
+    std::atomic<uint8_t> chunk_ready[MAXCH] = {};  // cev[j] has been waited for by some thread
+    std::atomic<uint32_t> parts_left{0};           // delivery ranges not yet called back
     bool cev_wait = false;              // chunk events to wait for before delivering
     bool narrow = false;                // ids crossed PCIe as u32 (every id < 2^32); widened at delivery
     bool host_done = false;             // the result was produced synchronously (custom / host path)
@@ -182,24 +196,20 @@ struct tm_batcher {
     std::mutex slot_mu;  // slot states + completion FIFO
     std::condition_variable slot_cv;
     std::deque<uint32_t> fifo;   // slots queued for completion, in window order
-    std::deque<uint32_t> dfifo;  // slots ready for delivery, in window order
     bool cutter_done = false;    // under slot_mu
-    bool completer_done = false;
 
-    std::thread cutter, completer, deliverer;
-    std::vector<std::thread> pool;
-    // delivery jobs: one window split in n_delivery + 1 ranges
-    std::mutex job_mu;
-    std::condition_variable job_cv, job_done_cv;
-    Slot *job_slot = nullptr;
-    uint32_t job_lo = 0, job_hi = 0;
-    // a job is published by bumping job_gen (release) after its fields are set; pool threads
-    // spin on it a little before sleeping, and the delivery thread spins on job_left, so a
-    // hand-off costs about a microsecond instead of a futex wake-up
-    std::atomic<uint64_t> job_gen{0};
-    std::atomic<uint32_t> job_left{0};
-    std::atomic<uint32_t> sleepers{0};
-    std::atomic<bool> pool_stop{false};
+    std::thread cutter, completer;
+    std::vector<std::thread> workers;  // delivery threads
+    // delivery work: publish ranges of the windows, in window order
+    struct Work {
+        uint32_t slot, chunk, lo, hi;
+    };
+    std::mutex work_mu;
+    std::condition_variable work_cv;
+    std::deque<Work> work;
+    std::atomic<uint32_t> work_n{0};     // work.size(), polled without the lock
+    std::atomic<uint32_t> sleepers{0};   // delivery threads blocked on work_cv
+    bool work_closed = false;            // under work_mu: no more ranges will come
 
     std::mutex st_mu;  // stats
     uint64_t n_batches = 0, n_pub = 0, max_seen = 0, backend_ns = 0;
@@ -308,7 +318,7 @@ struct tm_batcher {
         BT_HIP(S.h_status.ensure((size_t)n * 4 + 4));
         BT_HIP(S.h_cnt.ensure((size_t)n * 4 + 4));
         BT_HIP(S.h_ctl.ensure(CTL_BYTES));
-        if (!S.ev) BT_HIP(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+        if (!S.ev) BT_HIP(hipEventCreateWithFlags(&S.ev, EV_FLAGS));
         BT_HIP(hipMemcpyAsync(S.d_bytes.p, S.h_bytes.p, S.nbytes + 1, hipMemcpyHostToDevice, s_comp));
         BT_HIP(hipMemcpyAsync(S.d_off.p, S.h_off.p, (size_t)n * 4 + 4, hipMemcpyHostToDevice, s_comp));
         tm_dev_result r;
@@ -441,7 +451,7 @@ struct tm_batcher {
     }
 
     // ------------------------------------------------------------------ delivery
-    void deliver_range(Slot &S, uint32_t lo, uint32_t hi) {
+    void deliver_range(Slot &S, uint32_t lo, uint32_t hi, int rc) {
         std::vector<uint32_t> lats;
         lats.reserve(hi - lo);
         thread_local std::vector<uint64_t> wide;  // a narrowed window's ids, one publish at a time
@@ -450,8 +460,8 @@ struct tm_batcher {
         for (uint32_t i = lo; i < hi; i++) {
             const Pending &p = S.pubs[i];
             if (i + 8 < hi) __builtin_prefetch(S.pubs[i + 8].ctx);  // the caller's per-publish state
-            if (S.rc < 0) {
-                p.cb(p.ctx, S.rc, nullptr, 0);
+            if (rc < 0) {
+                p.cb(p.ctx, rc, nullptr, 0);
             } else {
                 const int32_t st = S.v.status[i];
                 const uint32_t c = st == TM_TOPIC_OK ? S.v.cnt[i] : 0;
@@ -480,80 +490,77 @@ struct tm_batcher {
         lat_n = std::min(LAT_RING, lat_n + lats.size());
     }
 
-    uint32_t parts_for(uint32_t n) const {
-        // small windows are not worth waking the pool for
-        return std::max<uint32_t>(1, std::min<uint32_t>(n_delivery + 1, n / 256));
-    }
-
     static constexpr int SPIN = 256;  // polls (a few microseconds) before sleeping: the CPUs are a quota
+    static constexpr uint32_t MIN_RANGE = 256;  // publishes: smaller ranges are not worth a hand-off
 
-    void pool_loop(uint32_t idx) {
-        uint64_t seen = 0;
-        for (;;) {
-            int spins = 0;
-            while (job_gen.load(std::memory_order_acquire) == seen && !pool_stop.load(std::memory_order_relaxed)) {
-                if (++spins < SPIN) {
-                    __builtin_ia32_pause();
-                    continue;
-                }
-                std::unique_lock<std::mutex> lk(job_mu);
-                sleepers.fetch_add(1);
-                job_cv.wait(lk, [&] { return pool_stop.load() || job_gen.load() != seen; });
-                sleepers.fetch_sub(1);
-            }
-            if (pool_stop.load()) return;
-            seen = job_gen.load(std::memory_order_acquire);
-            Slot *S = job_slot;
-            const uint32_t lo = job_lo, hi = job_hi;
-            const uint32_t parts = parts_for(hi - lo);
-            if (idx + 1 < parts) {  // part 0 is the delivery thread's own
-                const uint64_t n = hi - lo;
-                deliver_range(*S, lo + (uint32_t)(n * (idx + 1) / parts), lo + (uint32_t)(n * (idx + 2) / parts));
-            }
-            if (job_left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
-                std::lock_guard<std::mutex> g(job_mu);
-                job_done_cv.notify_all();
-            }
+    // Queue window S's delivery: each chunk cut into ranges, about one per delivery thread.
+    void post_delivery(uint32_t si) {
+        Slot &S = slot[si];
+        const uint32_t nthreads = (uint32_t)workers.size();
+        std::vector<Work> ws;
+        for (uint32_t j = 0; j < S.nchunk; j++) {
+            const uint32_t lo = S.chunk_lo[j], hi = S.chunk_lo[j + 1];
+            S.chunk_ready[j].store(S.cev_wait ? 0 : 1, std::memory_order_relaxed);
+            if (hi <= lo) continue;
+            const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(nthreads, (hi - lo) / MIN_RANGE));
+            for (uint32_t k = 0; k < parts; k++)
+                ws.push_back(Work{si, j, lo + (uint32_t)((uint64_t)(hi - lo) * k / parts),
+                                  lo + (uint32_t)((uint64_t)(hi - lo) * (k + 1) / parts)});
         }
-    }
-
-    // publishes [lo, hi) of S, split over the delivery thread and its pool
-    void deliver_part(Slot &S, uint32_t lo, uint32_t hi) {
-        const uint32_t parts = parts_for(hi - lo);
-        if (parts <= 1 || pool.empty()) {
-            deliver_range(S, lo, hi);
+        if (ws.empty()) {
+            free_slot(S);
             return;
         }
-        job_slot = &S;
-        job_lo = lo;
-        job_hi = hi;
-        job_left.store((uint32_t)pool.size(), std::memory_order_relaxed);
-        job_gen.fetch_add(1, std::memory_order_acq_rel);
-        if (sleepers.load()) {
-            std::lock_guard<std::mutex> g(job_mu);
-            job_cv.notify_all();
+        S.parts_left.store((uint32_t)ws.size(), std::memory_order_release);
+        {
+            std::lock_guard<std::mutex> g(work_mu);
+            work.insert(work.end(), ws.begin(), ws.end());
+            work_n.store((uint32_t)work.size(), std::memory_order_release);
         }
-        deliver_range(S, lo, lo + (uint32_t)((uint64_t)(hi - lo) / parts));
-        int spins = 0;
-        while (job_left.load(std::memory_order_acquire) != 0) {
-            if (++spins < SPIN) {
-                __builtin_ia32_pause();
-                continue;
-            }
-            std::unique_lock<std::mutex> lk(job_mu);
-            job_done_cv.wait(lk, [&] { return job_left.load() == 0; });
-        }
+        if (sleepers.load()) work_cv.notify_all();
     }
 
-    // chunk by chunk, each as soon as its ids have landed
-    void deliver(Slot &S) {
-        for (uint32_t j = 0; j < S.nchunk; j++) {
-            if (S.cev_wait) {
+    void free_slot(Slot &S) {
+        {
+            std::lock_guard<std::mutex> g(slot_mu);
+            S.state = Slot::FREE;
+        }
+        slot_cv.notify_all();
+    }
+
+    // the next range, or false once the queue is closed and empty
+    bool next_work(Work &w) {
+        for (int spins = 0; spins < SPIN && work_n.load(std::memory_order_acquire) == 0; spins++)
+            __builtin_ia32_pause();
+        std::unique_lock<std::mutex> lk(work_mu);
+        if (work.empty()) {
+            sleepers.fetch_add(1);
+            work_cv.wait(lk, [&] { return !work.empty() || work_closed; });
+            sleepers.fetch_sub(1);
+            if (work.empty()) return false;
+        }
+        w = work.front();
+        work.pop_front();
+        work_n.store((uint32_t)work.size(), std::memory_order_release);
+        return true;
+    }
+
+    void worker_loop() {
+        Work w;
+        while (next_work(w)) {
+            Slot &S = slot[w.slot];
+            int rc = S.rc;
+            if (!S.chunk_ready[w.chunk].load(std::memory_order_acquire)) {
+                // several threads may wait on one chunk's copy at once; each returns when it lands
                 const uint64_t t0 = now_ns();
-                if (hipEventSynchronize(S.cev[j]) != hipSuccess) S.rc = TM_EDEVICE;
+                if (hipEventSynchronize(S.cev[w.chunk]) != hipSuccess) rc = TM_EDEVICE;
+                else S.chunk_ready[w.chunk].store(1, std::memory_order_release);
                 ns_copy.fetch_add(now_ns() - t0, std::memory_order_relaxed);  // waited on PCIe
             }
-            deliver_part(S, S.chunk_lo[j], S.chunk_lo[j + 1]);
+            const uint64_t td0 = now_ns();
+            deliver_range(S, w.lo, w.hi, rc);
+            ns_del.fetch_add(now_ns() - td0, std::memory_order_relaxed);
+            if (S.parts_left.fetch_sub(1, std::memory_order_acq_rel) == 1) free_slot(S);
         }
     }
 
@@ -653,49 +660,20 @@ struct tm_batcher {
             S.cev_wait = false;
             if (S.rc == TM_OK && S.n && eng) S.rc = complete(S);
             S.t_done = now_ns();
-            {
-                std::lock_guard<std::mutex> g(slot_mu);
-                dfifo.push_back(si);
+            if (S.n) {
+                std::lock_guard<std::mutex> g(st_mu);  // counted before the callbacks
+                n_batches++;
+                n_pub += S.n;
+                max_seen = std::max<uint64_t>(max_seen, S.n);
+                backend_ns += S.t_done - S.t_enq;
             }
-            slot_cv.notify_all();
+            post_delivery(si);
         }
         {
-            std::lock_guard<std::mutex> g(slot_mu);
-            completer_done = true;
+            std::lock_guard<std::mutex> g(work_mu);
+            work_closed = true;
         }
-        slot_cv.notify_all();
-    }
-
-    // stage 3: call the window's publishers back (with the delivery pool), free the slot
-    void deliverer_loop() {
-        for (;;) {
-            uint32_t si;
-            {
-                std::unique_lock<std::mutex> lk(slot_mu);
-                slot_cv.wait(lk, [&] { return !dfifo.empty() || completer_done; });
-                if (dfifo.empty()) break;
-                si = dfifo.front();
-                dfifo.pop_front();
-            }
-            Slot &S = slot[si];
-            if (S.n) {
-                {
-                    std::lock_guard<std::mutex> g(st_mu);  // counted before the callbacks
-                    n_batches++;
-                    n_pub += S.n;
-                    max_seen = std::max<uint64_t>(max_seen, S.n);
-                    backend_ns += S.t_done - S.t_enq;
-                }
-                const uint64_t td0 = now_ns();
-                deliver(S);
-                ns_del.fetch_add(now_ns() - td0, std::memory_order_relaxed);
-            }
-            {
-                std::lock_guard<std::mutex> g(slot_mu);
-                S.state = Slot::FREE;
-            }
-            slot_cv.notify_all();
-        }
+        work_cv.notify_all();
     }
 
     int start(const tm_batcher_config *c) {
@@ -703,8 +681,8 @@ struct tm_batcher {
         if (cfg.max_batch == 0) cfg.max_batch = 65536;
         if (cfg.max_wait_us == 0) cfg.max_wait_us = 200;
         if (cfg.mode > TM_MATCH_AGGRE) return TM_EINVAL;
-        n_delivery = cfg.delivery_threads ? cfg.delivery_threads - 1 : 3;
-        if (n_delivery > 63) return TM_EINVAL;
+        n_delivery = cfg.delivery_threads ? cfg.delivery_threads : 4;
+        if (n_delivery > 64) return TM_EINVAL;
         lat_ns.assign(LAT_RING, 0);
         if (!eng)
             for (Slot &S : slot)
@@ -718,12 +696,11 @@ struct tm_batcher {
                 return TM_EDEVICE;
             for (Slot &S : slot)
                 for (hipEvent_t &e : S.cev)
-                    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return TM_EDEVICE;
+                    if (hipEventCreateWithFlags(&e, EV_FLAGS) != hipSuccess) return TM_EDEVICE;
         }
         try {
-            for (uint32_t i = 0; i < n_delivery; i++) pool.emplace_back([this, i] { pool_loop(i); });
+            for (uint32_t i = 0; i < n_delivery; i++) workers.emplace_back([this] { worker_loop(); });
             completer = std::thread([this] { completer_loop(); });
-            deliverer = std::thread([this] { deliverer_loop(); });
             cutter = std::thread([this] { cutter_loop(); });
         } catch (...) {
             stop();
@@ -745,18 +722,12 @@ struct tm_batcher {
         }
         slot_cv.notify_all();
         if (completer.joinable()) completer.join();
-        else {
-            std::lock_guard<std::mutex> g(slot_mu);
-            completer_done = true;
-        }
-        slot_cv.notify_all();
-        if (deliverer.joinable()) deliverer.join();
         {
-            std::lock_guard<std::mutex> g(job_mu);
-            pool_stop.store(true);
+            std::lock_guard<std::mutex> g(work_mu);
+            work_closed = true;
         }
-        job_cv.notify_all();
-        for (std::thread &t : pool)
+        work_cv.notify_all();
+        for (std::thread &t : workers)  // they drain the queue before they see it closed
             if (t.joinable()) t.join();
         if (eng) {
             (void)hipSetDevice(device);
@@ -875,8 +846,9 @@ int tm_batcher_stats_get(tm_batcher *b, tm_batcher_stats *out) {
         out->cut_us = b->ns_cut / 1000;
         out->enqueue_us = b->ns_enq / 1000;
         out->gpu_wait_us = b->ns_gpu / 1000;
-        out->copy_us = b->ns_copy / 1000;
-        out->deliver_us = b->ns_del / 1000;
+        const uint64_t nt = std::max<size_t>(1, b->workers.size());  // per delivery thread
+        out->copy_us = b->ns_copy / 1000 / nt;
+        out->deliver_us = b->ns_del / 1000 / nt;
         lat.assign(b->lat_ns.begin(), b->lat_ns.begin() + (ptrdiff_t)b->lat_n);
     }
     out->lat_p50_us = out->lat_p99_us = out->lat_max_us = 0;

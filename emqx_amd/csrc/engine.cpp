@@ -324,6 +324,13 @@ struct tm_engine {
     uint64_t dev_used[A_N] = {};  // bytes of each device array in use (image export)
     hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // around k_match_fast (tm_debug_timing)
     bool timing_on = false;
+    // pipelined tm_match_batch: a copy stream, per-half events, the counter blocks' landing
+    // place, and the last such batch's keys per topic (sizes the next one's buffers)
+    hipStream_t s_pipe = nullptr;
+    hipEvent_t ev_pk[2] = {}, ev_pd[2] = {};
+    PinBuf h_pctl;
+    double pipe_kpt = 0;
+    bool dev_batch = true;  // the device holds the last batch whole (tm_result_ids_device*)
 
     uint64_t edge_load_inv() const { return cfg.edge_load_inv ? cfg.edge_load_inv : EDGE_LOAD_INV; }
 
@@ -1412,6 +1419,11 @@ void tm_destroy(tm_engine *eng) {
         b->release();
     if (eng->ev_fast0) (void)hipEventDestroy(eng->ev_fast0);
     if (eng->ev_fast1) (void)hipEventDestroy(eng->ev_fast1);
+    if (eng->s_pipe) (void)hipStreamSynchronize(eng->s_pipe);
+    for (hipEvent_t e : {eng->ev_pk[0], eng->ev_pk[1], eng->ev_pd[0], eng->ev_pd[1]})
+        if (e) (void)hipEventDestroy(e);
+    eng->h_pctl.release();
+    if (eng->s_pipe) (void)hipStreamDestroy(eng->s_pipe);
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
     delete eng;
 }
@@ -1544,8 +1556,11 @@ static int grow_pools(tm_engine *eng) {
     return TM_OK;
 }
 
+// `obase`: the batch's per-topic results go to d_outoff/d_outcnt/d_status + obase; `keys`,
+// `keys_cap`: its key output (default: the whole arena)
 static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
-                                hipStream_t s, uint32_t mode = MODE_ALL) {
+                                hipStream_t s, uint32_t mode = MODE_ALL, uint32_t obase = 0, uint32_t *keys = nullptr,
+                                uint64_t keys_cap = 0) {
     MatchArgs a{};
     a.mode = mode;
     a.tpw = pick_tpw(n, eng->cfg.topics_per_wave);
@@ -1564,11 +1579,11 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.emask = eng->emask;
     a.root = eng->d_root.as<RootRec>();
     a.arena = eng->d_arena.as<uint32_t>();
-    a.out_off = eng->d_outoff.as<uint32_t>();
-    a.out_cnt = eng->d_outcnt.as<uint32_t>();
-    a.status = eng->d_status.as<int32_t>();
-    a.keys = eng->d_keys.as<uint32_t>();
-    a.keys_cap = eng->keys_cap;
+    a.out_off = eng->d_outoff.as<uint32_t>() + obase;
+    a.out_cnt = eng->d_outcnt.as<uint32_t>() + obase;
+    a.status = eng->d_status.as<int32_t>() + obase;
+    a.keys = keys ? keys : eng->d_keys.as<uint32_t>();
+    a.keys_cap = keys ? keys_cap : eng->keys_cap;
     eng->ctl_cur ^= 1u;
     eng->p_ctl = eng->d_ctl.as<uint8_t>() + eng->ctl_cur * CTL_BYTES;
     a.cursor = (unsigned long long *)(eng->p_ctl + CTL_CURSOR);
@@ -1611,6 +1626,151 @@ static int enqueue_reduce(tm_engine *eng, uint32_t mode, uint32_t n, hipStream_t
     return TM_OK;
 }
 
+
+// Host batches of TM_MATCH_ALL with at least 2 * PIPE_SUB topics run as sub-batches of
+// about PIPE_SUB topics on two streams: sub-batch j+1 is staged, copied in and walked while
+// sub-batch j's keys cross PCIe.  The keys D2H (PCIe) is the bound of this path, so the
+// walk, the staging and the H2D hide behind it.
+constexpr uint32_t PIPE_SUB = 262144;
+constexpr uint32_t PIPE_MAXSUB = 8;
+
+static int match_batch_pipelined(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n,
+                                 tm_result *out) {
+    const uint32_t base = off[0];
+    const uint64_t nbytes = (uint64_t)off[n] - base;
+    const uint32_t S = std::max<uint32_t>(2, std::min<uint32_t>(PIPE_MAXSUB, n / PIPE_SUB));
+    uint32_t b[PIPE_MAXSUB + 1];
+    for (uint32_t j = 0; j <= S; j++) b[j] = (uint32_t)((uint64_t)n * j / S);
+    int rc = ensure_batch(eng, n, nbytes);
+    if (rc) return rc;
+    TM_TRY_HIP(eng->h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->h_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->d_bytes.ensure(nbytes + 16), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->h_outoff.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->h_outcnt.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->h_status.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->h_pctl.ensure(2 * CTL_BYTES), TM_ENOMEM, "pinned alloc");
+    if (!eng->s_pipe) {
+        TM_TRY_HIP(hipStreamCreateWithFlags(&eng->s_pipe, hipStreamNonBlocking), TM_EDEVICE, "stream");
+        for (hipEvent_t *e : {&eng->ev_pk[0], &eng->ev_pk[1], &eng->ev_pd[0], &eng->ev_pd[1]})
+            TM_TRY_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming), TM_EDEVICE, "event");
+    }
+    // each half of the key arena holds one sub-batch; sized from the last pipelined batch
+    const uint64_t est_sub = (uint64_t)(eng->pipe_kpt * (double)(n / S + 1) * 1.15) + 4096;
+    if (eng->keys_cap < 2 * est_sub) {
+        TM_TRY_HIP(eng->d_keys.ensure(2 * est_sub * 4), TM_ENOMEM, "alloc keys");
+        eng->keys_cap = 2 * est_sub;
+    }
+    uint64_t hc = eng->keys_cap / 2;
+    TM_TRY_HIP(eng->h_keys.ensure((size_t)(eng->pipe_kpt * (double)n * 1.1) * 4 + 4), TM_ENOMEM, "pinned alloc");
+    hipStream_t s = eng->stream, c = eng->s_pipe;
+    uint8_t *hb8 = eng->h_bytes.as<uint8_t>(), *hctl = eng->h_pctl.as<uint8_t>();
+    uint32_t *ho = eng->h_off.as<uint32_t>();
+    uint64_t hb[PIPE_MAXSUB] = {}, hbase = 0, seg_d = 0, fr_d = 0, slow = 0;
+
+    auto stage = [&](uint32_t j) -> int {  // sub-batch j's topics into pinned memory, then H2D
+        const uint32_t lo = b[j], hi = b[j + 1];
+        const uint64_t blo = off[lo] - base, bhi = off[hi] - base;
+        if (bhi > blo) memcpy(hb8 + blo, bytes + base + blo, bhi - blo);
+        for (uint32_t i = lo; i <= hi; i++) ho[i] = off[i] - base;
+        if (bhi > blo)
+            TM_TRY_HIP(hipMemcpyAsync(eng->d_bytes.as<uint8_t>() + blo, hb8 + blo, bhi - blo, hipMemcpyHostToDevice, s),
+                       TM_EDEVICE, "H2D");
+        TM_TRY_HIP(hipMemcpyAsync(eng->d_off.as<uint32_t>() + lo, ho + lo, ((size_t)hi - lo + 1) * 4,
+                                  hipMemcpyHostToDevice, s),
+                   TM_EDEVICE, "H2D");
+        return TM_OK;
+    };
+    auto walk = [&](uint32_t j) -> int {  // sub-batch j walks into key half j % 2
+        const uint32_t lo = b[j], hi = b[j + 1], h = j & 1;
+        if (j >= 2) TM_TRY_HIP(hipStreamWaitEvent(s, eng->ev_pd[h], 0), TM_EDEVICE, "wait");  // half's last D2H
+        eng->last_n = hi - lo;
+        TM_TRY_HIP(enqueue_match(eng, eng->d_bytes.as<uint8_t>(), eng->d_off.as<uint32_t>() + lo, hi - lo, s, MODE_ALL,
+                                 lo, eng->d_keys.as<uint32_t>() + h * hc, hc),
+                   TM_EDEVICE, "kernel launch");
+        TM_TRY_HIP(hipMemcpyAsync(hctl + h * CTL_BYTES, eng->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                   "D2H");
+        TM_TRY_HIP(hipEventRecord(eng->ev_pk[h], s), TM_EDEVICE, "event");
+        return TM_OK;
+    };
+    // sub-batch j's walk is done: its keys and per-topic results D2H on the copy stream
+    // (1: its key half was too small)
+    auto finish = [&](uint32_t j) -> int {
+        const uint32_t lo = b[j], hi = b[j + 1], h = j & 1;
+        TM_TRY_HIP(hipEventSynchronize(eng->ev_pk[h]), TM_EDEVICE, "match kernels");
+        const uint8_t *ctl = hctl + h * CTL_BYTES;
+        const uint64_t total = *(const uint64_t *)ctl;
+        if (total > hc) return 1;
+        slow += *(const uint32_t *)(ctl + 8);
+        seg_d = std::max(seg_d, *(const uint64_t *)(ctl + 16));
+        fr_d = std::max(fr_d, *(const uint64_t *)(ctl + 24));
+        if ((hbase + total) * 4 + 4 > eng->h_keys.cap) {  // more keys than estimated: grow, keeping what landed
+            TM_TRY_HIP(hipStreamSynchronize(c), TM_EDEVICE, "D2H");
+            PinBuf nb;
+            TM_TRY_HIP(nb.ensure((hbase + total) * 8 + 4), TM_ENOMEM, "pinned alloc");
+            if (hbase) memcpy(nb.p, eng->h_keys.p, hbase * 4);
+            std::swap(nb.p, eng->h_keys.p);
+            std::swap(nb.cap, eng->h_keys.cap);
+            nb.release();
+        }
+        TM_TRY_HIP(hipStreamWaitEvent(c, eng->ev_pk[h], 0), TM_EDEVICE, "wait");
+        if (total)
+            TM_TRY_HIP(hipMemcpyAsync(eng->h_keys.as<uint32_t>() + hbase, eng->d_keys.as<uint32_t>() + h * hc, total * 4,
+                                      hipMemcpyDeviceToHost, c),
+                       TM_EDEVICE, "D2H");
+        for (std::pair<PinBuf *, DevBuf *> pr : {std::make_pair(&eng->h_outoff, &eng->d_outoff),
+                                                 std::make_pair(&eng->h_outcnt, &eng->d_outcnt),
+                                                 std::make_pair(&eng->h_status, &eng->d_status)})
+            TM_TRY_HIP(hipMemcpyAsync(pr.first->as<uint32_t>() + lo, pr.second->as<uint32_t>() + lo,
+                                      ((size_t)hi - lo) * 4, hipMemcpyDeviceToHost, c),
+                       TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipEventRecord(eng->ev_pd[h], c), TM_EDEVICE, "event");
+        hb[j] = hbase;
+        hbase += total;
+        return TM_OK;
+    };
+
+    if ((rc = stage(0)) || (rc = walk(0))) return rc;
+    for (uint32_t j = 0; j < S; j++) {
+        if (j + 1 < S && ((rc = stage(j + 1)) || (rc = walk(j + 1)))) return rc;
+        rc = finish(j);
+        if (rc == 1) {
+            // the half was short: drain, grow both halves past this sub-batch's demand, walk
+            // it (and the one queued behind it, whose output the move discards) again
+            const uint64_t need = *(const uint64_t *)(hctl + (j & 1) * CTL_BYTES);
+            TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "sync");
+            TM_TRY_HIP(hipStreamSynchronize(c), TM_EDEVICE, "sync");
+            const uint64_t want = 2 * (need + need / 8 + 1024);
+            TM_TRY_HIP(eng->d_keys.ensure(want * 4), TM_ENOMEM, "alloc keys");
+            eng->keys_cap = want;
+            hc = want / 2;
+            if ((rc = walk(j)) || (j + 1 < S && (rc = walk(j + 1)))) return rc;
+            rc = finish(j);
+            if (rc == 1) return TM_EDEVICE;  // cannot happen: the half now holds the demand
+        }
+        if (rc) return rc;
+    }
+    TM_TRY_HIP(hipStreamSynchronize(c), TM_EDEVICE, "D2H");
+    // sub-batch offsets are relative to its own keys: rebase onto the joined array
+    uint32_t *oo = eng->h_outoff.as<uint32_t>();
+    for (uint32_t j = 1; j < S; j++)
+        for (uint32_t i = b[j]; i < b[j + 1]; i++) oo[i] += (uint32_t)hb[j];
+    eng->n_slow_last = slow;
+    eng->seg_demand_last = seg_d;
+    eng->fr_demand_last = fr_d;
+    if ((rc = grow_pools(eng))) return rc;
+    eng->pipe_kpt = (double)hbase / n;
+    eng->dev_batch = false;  // the device holds sub-batches, not this batch
+    eng->last_n = 0;
+    out->total = hbase;
+    out->off = oo;
+    out->cnt = eng->h_outcnt.as<uint32_t>();
+    out->keys = eng->h_keys.as<uint32_t>();
+    out->status = eng->h_status.as<int32_t>();
+    return TM_OK;
+}
+
 int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
                    tm_result *out) {
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
@@ -1628,6 +1788,9 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
     if (reduced_mode(mode) && !dev_reduce && eng->replica) return replica_refuses(eng, "tm_match_batch (host UNIQUE)");
     eng->last_mode = (reduced_mode(mode) && !dev_reduce) ? TM_MATCH_ALL : mode;  // what the device holds
     if (n == 0) return TM_OK;
+    if (mode == TM_MATCH_ALL && n >= 2 * PIPE_SUB)
+        return match_batch_pipelined(eng, bytes, off, n, out);
+    eng->dev_batch = true;
     // rebase offsets to 0
     uint32_t base = off[0];
     uint64_t nbytes = (uint64_t)off[n] - base;
@@ -1807,6 +1970,7 @@ int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t 
     }
     TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s, kmode), TM_EDEVICE, "kernel launch");
     eng->last_mode = mode;
+    eng->dev_batch = true;
     if (reduced_mode(mode) && (rc = enqueue_reduce(eng, mode, n, s))) return rc;
     out->n = n;
     out->d_off = eng->d_outoff.as<uint32_t>();
@@ -1843,8 +2007,8 @@ int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint
 int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out, uint32_t *d_flags,
                             void *stream) {
     if (!eng || !d_off_out || (ids_cap && !d_ids)) return TM_EINVAL;
-    if (!eng->p_ctl) {
-        eng->err = "tm_result_ids_device: no tm_match_device batch yet";
+    if (!eng->p_ctl || !eng->dev_batch) {
+        eng->err = "tm_result_ids_device: no tm_match_device batch since the last (pipelined) tm_match_batch";
         return TM_ESTATE;
     }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
@@ -1865,7 +2029,7 @@ int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, u
 // added is below 2^32 (TM_ESTATE otherwise)
 __attribute__((visibility("hidden"))) int tmx_result_ids32_device(tm_engine *eng, uint32_t *d_ids, uint64_t ids_cap,
                                                                   uint32_t *d_off_out, void *stream) {
-    if (eng->max_id > 0xFFFFFFFFull || eng->replica) return TM_ESTATE;
+    if (eng->max_id > 0xFFFFFFFFull || eng->replica || !eng->dev_batch) return TM_ESTATE;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     hipStream_t s = stream ? (hipStream_t)stream : (eng->last_stream ? eng->last_stream : eng->stream);
     const uint32_t n = eng->last_n;

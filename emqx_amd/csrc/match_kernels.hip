@@ -33,7 +33,7 @@ namespace tmx {
 
 constexpr int WAVE = 64;
 #ifndef TM_FCAP
-#define TM_FCAP 384  // 256 -> 384: fewer frontier overflows to HBM chunks for 2 fewer waves per CU (0.889 -> 0.868 ms); 512 loses more occupancy than it saves
+#define TM_FCAP 448  // 256 -> 448 with the topic stage at 2.5 KiB: fewer frontier overflows to HBM chunks at 14 waves/CU (0.889 -> 0.848 ms)
 #endif
 constexpr int FCAP = TM_FCAP;    // frontier entries per wave per depth held in LDS
 constexpr int FCH = FR_CHUNK;    // frontier entries per global overflow chunk
@@ -42,7 +42,7 @@ constexpr int MAXF = 32;         // overflow chunks per frontier buffer per wave
 #define TM_SCAP 128
 #endif
 #ifndef TM_TBCAP
-#define TM_TBCAP 3072
+#define TM_TBCAP 2560
 #endif
 #ifndef TM_MIN_WAVES
 #define TM_MIN_WAVES 1

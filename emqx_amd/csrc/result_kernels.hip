@@ -16,6 +16,8 @@
 // All of it is byte movement: coalesced where the layout allows, HBM-bound.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "device_api.h"
 
 namespace tmx {
@@ -104,36 +106,51 @@ hipError_t launch_excl_scan(const uint32_t *in, uint64_t in_stride, uint32_t n, 
 }
 
 // ---------------------------------------------------------------------------
-// key handles -> ids, topic-major.  One wave per 64 topics: lists of up to 8 keys are
-// copied by the topic's own lane; longer ones (hot '#' lists) by the whole wave, 64
-// consecutive keys per instruction.
+// key handles -> ids, topic-major, flat over the OUTPUT: a block owns RI_BLK consecutive
+// output positions (grid-stride over blocks of them), finds the topics that cover them
+// (binary search of dst_off, narrowed to the block's first..last topic), and each thread
+// maps its positions independently: ids[q] = id(keys[src_off[t] + q - dst_off[t]]).  Every
+// thread has RI_PER independent gathers, whatever the mix of list lengths (one lane per
+// topic left a 16 K-topic batch with a few hundred waves walking 2,000-key lists serially).
+constexpr uint32_t RI_T = 256, RI_PER = 16, RI_BLK = RI_T * RI_PER;
+
+__device__ __forceinline__ uint32_t topic_of(const uint32_t *dst_off, uint32_t lo, uint32_t hi, uint64_t q) {
+    // the last t in [lo, hi] with dst_off[t] <= q (dst_off[lo] <= q holds)
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo + 1) / 2;
+        if (dst_off[mid] <= q) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
 template <class IdT>
-__global__ __launch_bounds__(64) void k_result_ids(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
-                                                   const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n,
-                                                   IdT *ids, uint64_t cap, uint64_t keys_cap,
-                                                   const unsigned long long *cursor) {
-    const uint32_t lane = threadIdx.x;
-    const uint32_t t = blockIdx.x * 64 + lane;
-    uint32_t c = 0, so = 0, dofs = 0;
+__global__ __launch_bounds__(RI_T) void k_result_ids(const uint32_t *src_off, const uint32_t *keys,
+                                                     const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n,
+                                                     IdT *ids, uint64_t cap, uint64_t keys_cap,
+                                                     const unsigned long long *cursor) {
     // the walk's arena overflowed: waves past the cap skipped their copy-out, nothing to read
     if (cursor && *cursor > keys_cap) return;
-    if (t < n) {
-        c = cnt[t];
-        so = src_off[t];
-        dofs = dst_off[t];
-        if ((uint64_t)dofs + c > cap) c = 0;  // caller's buffer too small: it re-sizes from d_off[n]
-        if ((uint64_t)so + c > keys_cap) c = 0;
-    }
-    const bool is_long = c > 8;
-    if (!is_long) {
-        for (uint32_t k = 0; k < c; k++) ids[(uint64_t)dofs + k] = (IdT)key_rec[2ull * keys[(uint64_t)so + k]];
-    }
-    uint64_t longs = __ballot(is_long);
-    while (longs) {
-        const int l = __builtin_ctzll(longs);
-        longs &= longs - 1;
-        const uint32_t lc = __shfl(c, l, 64), ls = __shfl(so, l, 64), ld = __shfl(dofs, l, 64);
-        for (uint32_t k = lane; k < lc; k += 64) ids[(uint64_t)ld + k] = (IdT)key_rec[2ull * keys[(uint64_t)ls + k]];
+    const uint64_t lim = min((uint64_t)dst_off[n], cap);  // topics past the caller's cap stay unwritten
+    __shared__ uint32_t s_t0, s_t1;
+    for (uint64_t q0 = (uint64_t)blockIdx.x * RI_BLK; q0 < lim; q0 += (uint64_t)gridDim.x * RI_BLK) {
+        const uint64_t q1 = min(q0 + RI_BLK, lim);
+        __syncthreads();  // the previous block-range is done with s_t0 / s_t1
+        if (threadIdx.x == 0) {
+            s_t0 = topic_of(dst_off, 0, n, q0);
+            s_t1 = topic_of(dst_off, s_t0, n, q1 - 1);
+        }
+        __syncthreads();
+        uint32_t t = s_t0;
+        const uint32_t t1 = s_t1;
+#pragma unroll 4
+        for (uint32_t i = 0; i < RI_PER; i++) {
+            const uint64_t q = q0 + (uint64_t)i * RI_T + threadIdx.x;
+            if (q >= q1) break;
+            t = topic_of(dst_off, t, t1, q);  // positions rise with i: start from the last topic
+            const uint64_t src = (uint64_t)src_off[t] + (q - dst_off[t]);
+            if (src < keys_cap) ids[q] = (IdT)key_rec[2ull * keys[src]];
+        }
     }
 }
 
@@ -150,9 +167,12 @@ static hipError_t launch_result_ids_t(const uint32_t *cnt, const uint32_t *src_o
                                       const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, IdT *ids,
                                       uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, uint32_t *flags,
                                       hipStream_t s) {
-    if (n) {
-        k_result_ids<IdT><<<(n + 63) / 64, 64, 0, s>>>(cnt, src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap,
-                                                       cursor);
+    (void)cnt;  // dst_off is its scan
+    if (n && cap) {
+        // sized from the caller's cap (the result's size is on the device): surplus blocks exit
+        const uint64_t blocks = std::min<uint64_t>((cap + RI_BLK - 1) / RI_BLK, 2048);
+        k_result_ids<IdT><<<(uint32_t)blocks, RI_T, 0, s>>>(src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap,
+                                                            cursor);
         hipError_t e = hipGetLastError();
         if (e) return e;
     }

@@ -55,6 +55,31 @@ def _key_order(key):
     return (fk, term_key(ident))
 
 
+def words_topic_bytes(words) -> bytes:
+    """A pre-split topic (matches/3 takes `[word()]`, emqx_trie_search.erl:182,369-370) as
+    the bytes of a topic filter with the same walk.  A word list is used as is: no badarg
+    check, so '+' / '#' atoms act as wildcards of the topic (compare/3's filter-search
+    clauses, :292-300), and the final match_topics/4 step (:381-389) adds nothing, since a
+    list never equals or sorts above a binary key: a word-list topic matches exactly what
+    matches_filter/3 of the same words matches.
+
+    Words the byte form cannot carry are refused (ValueError): one containing '/', and the
+    binaries <<"+">> / <<"#">> (plain words in a list, wildcards once joined).  Standing in
+    another word for them is not exact: the reference's walk decides `lower` (stop) by the
+    term order of the words (:325-332), so the stand-in would have to sort exactly where the
+    original does among the index's words."""
+    out = []
+    for w in words:
+        if isinstance(w, str) and w in (PLUS, HASH):  # the atoms
+            out.append(w.encode())
+            continue
+        wb = w.encode() if isinstance(w, str) else bytes(w)
+        if b"/" in wb or wb in (b"+", b"#"):
+            raise ValueError(f"word {wb!r} has no byte form (contains '/' or is a binary '+'/'#')")
+        out.append(wb)
+    return b"/".join(out)
+
+
 class TopicIndex:
     def __init__(self, device: int = 0, engine: N.Engine | None = None, **engine_kw):
         self.eng = engine or N.Engine(device, **engine_kw)
@@ -62,6 +87,7 @@ class TopicIndex:
         self._terms: list = []      # u64 -> term
         self._records: dict = {}    # key -> record
         self._dirty = False
+        self._max_word = 0          # longest filter word ever inserted (word-list topics)
 
     @classmethod
     def new(cls, device: int = 0, **kw) -> "TopicIndex":
@@ -90,6 +116,7 @@ class TopicIndex:
     # ---- writes: insert/4, delete/3
     def insert(self, filt, ident, record=b"", tab=None) -> bool:
         fb, flags = self._filter_bytes(filt)
+        self._max_word = max(self._max_word, max(len(w) for w in fb.split(b"/")))
         self.eng.apply([(N.TM_OP_ADD, fb, self._id(ident), flags)])
         self._records[make_key(filt, ident)] = record
         self._dirty = True
@@ -118,16 +145,33 @@ class TopicIndex:
 
     def matches_batch(self, topics, opts=()) -> list:
         """Batched matches/3: one list of keys per topic; BadArg instances for
-        topics with a '+'/'#' level."""
+        topics with a '+'/'#' level.  A topic may also be a word list (words_topic_bytes)."""
         self.commit()
-        handles = self.eng.match(topics, N.TM_MATCH_ALL)
-        out = []
-        for hs in handles:
+        topics = list(topics)
+        wl = [i for i, t in enumerate(topics) if isinstance(t, (list, tuple))]
+        out = [None] * len(topics)
+        if wl:
+            empty = [i for i in wl if not topics[i]]
+            byw = [i for i in wl if topics[i]]
+            if byw:
+                for i, r in zip(byw, self.matches_filter_batch([words_topic_bytes(topics[i]) for i in byw], opts)):
+                    out[i] = r
+            if empty:
+                # [] words: only the root '#' filter compares match_full against them (:282-290;
+                # every longer filter is `lower`, :333-340); a one-level unknown word reaches
+                # exactly '#', '+' and '+/#', of which '#' is kept
+                root = self.matches_filter_batch([b"\xff" * (self._max_word + 1)], ())[0]
+                keys = [k for k in root if isinstance(k[0], tuple) and k[0] == (HASH,)]
+                for i in empty:
+                    out[i] = self._reduce(keys, opts)
+        rest = [i for i in range(len(topics)) if out[i] is None]
+        handles = self.eng.match([topics[i] for i in rest], N.TM_MATCH_ALL) if rest else []
+        for i, hs in zip(rest, handles):
             if hs is None:
-                out.append(BadArg("badarg"))
+                out[i] = BadArg("badarg")
                 continue
             keys = [self._key_of(h) for h in hs]
-            out.append(self._reduce(keys, opts))
+            out[i] = self._reduce(keys, opts)
         return out
 
     @staticmethod

@@ -194,7 +194,11 @@ int tm_commit_epoch(tm_engine *eng, uint64_t *epoch_out);
 
 /* reads ------------------------------------------------------------------- */
 /* Host buffers in, host result out (H2D + kernels + D2H inside).
- * Topic i is bytes[off[i] .. off[i+1]); `off` has n+1 entries. */
+ * Topic i is bytes[off[i] .. off[i+1]); `off` has n+1 entries.  TM_MATCH_ALL batches of
+ * 524,288 topics or more are pipelined: sub-batches of about 262,144 topics on two streams,
+ * each one's staging, H2D and walk overlapping the previous one's D2H (PCIe is this path's
+ * bound).  The device then holds sub-batch results, not the batch: tm_result_ids_device*
+ * refuse (TM_ESTATE) until the next tm_match_device* call. */
 int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off,
                    uint32_t n, uint32_t mode, tm_result *out);
 /* Device buffers in, device result out, asynchronous on the engine's stream
@@ -222,7 +226,7 @@ int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t 
                          uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out);
 int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap);
 
-/* Route ids of the last match batch (all keys, TM_MATCH_ALL), compacted topic-major on
+/* Route ids of the last tm_match_device* batch (all keys, TM_MATCH_ALL), compacted topic-major on
  * the device: topic i's ids are d_ids[d_off[i] .. d_off[i+1]); d_off has n+1 entries and
  * d_off[n] = *d_total.  This is get_id/1 (emqx_topic_index.erl:87-89) applied on the GPU to
  * every key, in the topic order a caller expects (emqx_router.erl:648-649 maps each key

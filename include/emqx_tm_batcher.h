@@ -10,9 +10,9 @@
  *
  *   window   a batch is dispatched when max_batch publishes are queued, or when the
  *            oldest queued publish has waited max_wait_us, or at tm_batcher_destroy
- *            (which drains the queue).  Three windows are in flight at once: window k+2
- *            walks on the GPU while window k+1's ids cross PCIe and window k's publishers
- *            are called back; under load windows grow by themselves.
+ *            (which drains the queue).  Four windows are in flight at once: window k+3
+ *            walks on the GPU while earlier windows' ids cross PCIe and window k's
+ *            publishers are called back; under load windows grow by themselves.
  *   result   per publish: TM_TOPIC_OK with the ids of its matched keys (route dests,
  *            emqx_topic_index:get_id/1 of every key, emqx_topic_index.erl:87-89), or
  *            TM_BADARG with no ids (a level exactly "+" or "#": emqx_trie_search.erl:374-375),
@@ -24,8 +24,9 @@
  *
  * Erlang binding: a NIF calls tm_batcher_submit with a callback that
  * enif_send()s the id list to the publishing pid, which waits in `receive`; the callback
- * runs on a delivery thread (several run at once, each for different publishers) and must
- * not block.
+ * runs on a delivery thread (several run at once, each for different publishes) and must
+ * not block.  Callbacks of different publishes may run in any order; a publisher with one
+ * publish in flight (emqx_broker:publish/1 is synchronous) sees its results in order.
  */
 #ifndef EMQX_TM_BATCHER_H
 #define EMQX_TM_BATCHER_H
@@ -45,8 +46,9 @@ typedef struct tm_batcher_config {
     uint32_t max_batch;    /* publishes per engine batch (0 = 65536)              */
     uint32_t max_wait_us;  /* window bound from the oldest queued publish (0 = 200) */
     uint32_t mode;         /* TM_MATCH_ALL / UNIQUE / AGGRE / FIRST / COUNT        */
-    uint32_t delivery_threads; /* threads calling publishers back (0 = 4); each takes a
-                                  contiguous share of a window */
+    uint32_t delivery_threads; /* threads calling publishers back (0 = 4); they take
+                                  ranges of a window from one queue, so a thread that is
+                                  slow (or descheduled) never holds the others */
 } tm_batcher_config;
 
 /* One publish's result; `ids` is valid only during the call. */
@@ -73,7 +75,8 @@ typedef struct tm_batcher_stats {
     /* submit -> callback latency over the last (up to) 65536 publishes, microseconds */
     double   lat_p50_us, lat_p99_us, lat_max_us;
     /* per pipeline stage, microseconds summed over windows: cutting a window from the queue,
-     * queueing its GPU part, waiting for the GPU part, its ids over PCIe, calling back */
+     * queueing its GPU part, waiting for the GPU part; then, averaged over the delivery
+     * threads: waiting for ids still on PCIe, calling back */
     uint64_t cut_us, enqueue_us, gpu_wait_us, copy_us, deliver_us;
 } tm_batcher_stats;
 

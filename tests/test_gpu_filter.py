@@ -235,3 +235,24 @@ def test_filter_walk_one_pass_and_two_pass_agree():
     # a small batch after it: one pass
     small = queries[2:50]
     assert _engine_walks(eng, small) == exp[2:50]
+
+
+def test_topic_index_word_list_topics():
+    """matches/3 with a pre-split topic (emqx_trie_search.erl:182,369-370) through the
+    mirror: the engine's filter walk of the joined words, against the literal restatement
+    walking the list itself; [] reaches only the root '#' keys (compare/3 :282-290, :333-340)."""
+    from emqx_amd.topic_index import TopicIndex
+    tab = TopicIndex(0)
+    fs = ["a/+", "a/b/#", "#", "+/b", "a/b", "$SYS/#", "+", "+/+/c"]
+    for i, f in enumerate(fs, 1):
+        tab.insert(f.encode(), i)
+    tab.insert([b"a", b"b"], 20)  # a word-list key without wildcards
+    rix = RefIndex([f.encode() for f in fs] + [b"a/b"], list(range(1, 9)) + [20], [0] * 8 + [1])
+    for ws in ([b"a", b"b"], [b"a", "+"], ["+", b"b"], [b"$SYS", b"x"], [b"x", b"y", b"c"], [b"a", "#"], []):
+        got = [(k[0] if isinstance(k[0], tuple) else k[0], k[1][0]) for k in tab.matches(ws)]
+        exp = [(tuple(w), i) for w, i in ref_matches_filter(rix, ws)]
+        assert sorted(got, key=repr) == sorted(exp, key=repr), ws
+    # a binary exact key never matches a word-list topic (match_topics/4, :381-389) ...
+    assert (b"a/b", (5,)) not in tab.matches([b"a", b"b"])
+    # ... but does match the same topic as a binary
+    assert (b"a/b", (5,)) in tab.matches(b"a/b")

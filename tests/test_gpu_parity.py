@@ -108,6 +108,26 @@ def test_config_parity(name, scale, nt, mode):
         assert eng.stats()["n_slow_topics"] == 0
 
 
+def test_host_batch_pipelined_vs_oracle(mode):
+    """tm_match_batch at >= 2 x 262,144 topics runs as sub-batches on two streams (each
+    sub-batch's walk overlaps the previous one's D2H, engine.cpp match_batch_pipelined):
+    the joined result is the oracle's.  The first call starts with key halves far too small
+    (no estimate yet), so it also takes the grow-and-rewalk path; the repeat uses the
+    estimate.  Afterwards the device holds no single batch: tm_result_ids_device refuses."""
+    w = workloads.generate("C", scale=0.02, n_topics=800_000)
+    eng = _engine(mode)
+    _load(eng, w)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    exp = ix.match(w.t_bytes, w.t_off, threads=8)
+    _assert_same(_engine_sets(eng, w.t_bytes, w.t_off), exp, "pipelined")
+    _assert_same(_engine_sets(eng, w.t_bytes, w.t_off), exp, "pipelined (repeat)")
+    import torch
+    ids = torch.zeros(16, dtype=torch.int64, device="cuda:0")
+    lo = torch.zeros(16, dtype=torch.int32, device="cuda:0")
+    with pytest.raises(N.TMError):
+        eng.result_ids_device(ids.data_ptr(), 16, lo.data_ptr())
+
+
 @pytest.mark.parametrize("tpw", [4, 16, 64])
 @pytest.mark.parametrize("name,scale,nt", [("A", 1.0, 50_000), ("C", 0.02, 50_000), ("E", 0.1, 50_000)])
 def test_config_parity_topics_per_wave(name, scale, nt, tpw):

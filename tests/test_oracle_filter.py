@@ -84,8 +84,8 @@ def compare(F, W, pos):
 def ref_matches_filter(ix: RefIndex, q: bytes):
     """search/3 with topic_filter set (:192-228): returns the accumulator as the reference
     would, i.e. the matched keys in REVERSE walk order."""
-    W = _words(q)
-    w0 = W[0]
+    W = list(q) if isinstance(q, (list, tuple)) else _words(q)  # a word list is taken as is (:359-360)
+    w0 = W[0] if W else None
     base = [w0] if isinstance(w0, bytes) and w0.startswith(b"$") else []  # base_init/1 :160-163
     cur = ix.next(ix.base(base))
     acc = []
@@ -215,3 +215,42 @@ def test_filter_search_mid_hash_is_badarg():
     q = np.frombuffer(b"#/y\0", dtype=np.uint8)
     off, got, st = ix.match(q, np.array([0, 3], dtype=np.uint32), algo=oracle.ALGO_FILTER)
     assert list(st) == [1] and off[-1] == 0
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_word_list_topics_map_to_filter_search(seed):
+    """matches/3 of a pre-split topic (emqx_trie_search.erl:182,369-370): the literal
+    restatement walks the word list as given (no badarg; '+'/'#' atoms are wildcards of the
+    topic); the mirror hands the engine words_topic_bytes(...) through matches_filter, which
+    the oracle's filter walk answers here.  Both must agree key by key.  Words with no byte
+    form (<<"+">>, <<"#">>, words with '/') are refused."""
+    from emqx_amd.topic_index import words_topic_bytes
+    rng = random.Random(100 + seed)
+    svocab = ["a", "b", "c", "$SYS", ""]
+    vocab = [v.encode() for v in svocab]
+    filters, ids, wf = _rand_set(rng, 300, svocab)
+    rix = RefIndex(filters, ids, wf)
+    odd = [b"zz", b"$x", b"\xff"]
+    for w in (b"+", b"#", b"a/b"):
+        with pytest.raises(ValueError):
+            words_topic_bytes([b"a", w])
+    topics = []
+    for _ in range(300):
+        n = rng.randint(1, 5)
+        ws = []
+        for k in range(n):
+            r = rng.random()
+            if r < 0.1:
+                ws.append("+")
+            elif r < 0.15 and k == n - 1:
+                ws.append("#")
+            elif r < 0.35:
+                ws.append(rng.choice(odd))
+            else:
+                ws.append(rng.choice(vocab))
+        topics.append(ws)
+    qs = [words_topic_bytes(t) for t in topics]
+    got = oracle_matches_filter(filters, ids, wf, qs)
+    for t, q, g in zip(topics, qs, got):
+        exp = [(tuple(ws), i) for ws, i in ref_matches_filter(rix, t)]
+        assert g == exp[::-1], (t, q)

@@ -1,0 +1,58 @@
+"""Batcher sweep on one GPU (bench tooling): config C engine, closed-loop publishers through
+tm_batcher_submit for each (publishers, delivery threads, max_wait_us) given, one JSON line
+each.  Usage: python tools/batcher_gpu.py P:T:W [P:T:W ...]"""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import numpy as np
+
+    from emqx_amd import _native as N
+    from emqx_amd import workloads as W
+    t0 = time.time()
+    w = W.generate("C", scale=float(os.environ.get("SCALE", "1.0")), n_topics=1_000_000)
+    eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    print(f"engine ready in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    tb = np.ascontiguousarray(w.t_bytes, dtype=np.uint8)
+    to32 = np.ascontiguousarray(w.t_off, dtype=np.uint32)
+    lg = C.CDLL(os.path.join(ROOT, "tools", "libtm_loadgen.so"))
+    lg.loadgen_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double,
+                               C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                               C.POINTER(C.c_double)]
+    if os.environ.get("HOSTPATH"):  # tm_match_batch with host buffers, 1 M publishes per call
+        eng.match_packed_view(tb, to32)
+        ts = []
+        for _ in range(8):
+            t1 = time.perf_counter()
+            r = eng.match_packed_view(tb, to32)
+            ts.append(time.perf_counter() - t1)
+        print(json.dumps({"host_path_ms": [round(t * 1e3, 2) for t in ts], "keys": int(r.total),
+                          "publishes_per_s": round(len(to32) / 1 / min(ts) if False else (len(to32) - 1) / float(np.median(ts)))}),
+              flush=True)
+    for spec in sys.argv[1:]:
+        pubs, th, wait = (int(x) for x in spec.split(":"))
+        b = N.Batcher(eng, max_batch=65536, max_wait_us=wait, delivery_threads=th)
+        got, ids, errs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
+        rc = lg.loadgen_run(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, 2.0, C.byref(got),
+                            C.byref(ids), C.byref(errs), C.byref(el))
+        st = b.stats()
+        b.close()
+        print(json.dumps({"publishers": pubs, "threads": th, "max_wait_us": wait, "rc": rc, "errors": errs.value,
+                          "publishes_per_s": round(got.value / el.value), "ids_per_publish": round(ids.value / max(got.value, 1), 1),
+                          "mean_batch": round(st["publishes"] / max(st["batches"], 1), 1),
+                          "p50_ms": round(st["lat_p50_us"] / 1e3, 3), "p99_ms": round(st["lat_p99_us"] / 1e3, 3),
+                          "busy": {k: round(st[k + "_us"] * 1e-6 / el.value, 3)
+                                   for k in ("cut", "enqueue", "gpu_wait", "copy", "deliver")}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

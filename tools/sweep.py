@@ -30,11 +30,11 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 # same-process reference point.
 VARIANTS = {
     "base": ([], 0),
-    "tb2560": (["-DTM_TBCAP=2560"], 0),
     "tb2560_f448": (["-DTM_TBCAP=2560", "-DTM_FCAP=448"], 0),
-    "scap96": (["-DTM_SCAP=96"], 0),
-    "fcap320": (["-DTM_FCAP=320"], 0),
-    "tpw32": ([], 0, 32),
+    "tb2048_f512": (["-DTM_TBCAP=2048", "-DTM_FCAP=512"], 0),
+    "tb2304_f480": (["-DTM_TBCAP=2304", "-DTM_FCAP=480"], 0),
+    "tb2048_f576": (["-DTM_TBCAP=2048", "-DTM_FCAP=576"], 0),
+    "tb1792_f544": (["-DTM_TBCAP=1792", "-DTM_FCAP=544"], 0),
 }
 
 
