@@ -65,6 +65,9 @@ constexpr uint32_t DO_PLUS = 0x80u, DO_LIT = 0x40u;  // frontier meta: probes th
 #ifndef TM_QMED
 #define TM_QMED 2  // a "medium" list is at most TM_QMED group-iterations long
 #endif
+#ifndef TM_PRELOOK
+#define TM_PRELOOK 10  // levels whose word ids are looked up in the pre-scan, all in flight together
+#endif
 #ifndef TM_CP_UNROLL
 #define TM_CP_UNROLL 8
 #endif
@@ -173,6 +176,90 @@ __device__ __forceinline__ uint32_t probes_needed(uint32_t info, uint32_t bloom,
     if ((info & I_LIT) && w != NONE && (bloom & bloom_bit(w))) m |= DO_LIT;
     return m;
 }
+
+#if TM_PRELOOK
+// Pre-scan of one topic (lane = topic) with its first TM_PRELOOK levels tokenised and their
+// word-table probes issued together: one round trip instead of one per level inside the
+// walk, which then takes level d's word id from registers (deeper levels are tokenised as
+// the walk reaches them, from byte pre_b).  Also counts the levels (nl) and finds badarg.
+// In: a, b, e, byte_at.  Out: widr[TM_PRELOOK], nl, badarg, pre_b; PROBES counts slot reads.
+// A macro, expanded in place in both wave kernels: as an inlined helper function the
+// compiler gave k_match_fast 134 VGPRs instead of 115 (3 waves per SIMD instead of 4).
+#define TM_PRESCAN_PRELOOK(PROBES)                                                                  \
+    do {                                                                                            \
+        uint64_t key[TM_PRELOOK], sl[TM_PRELOOK];                                                   \
+        uint32_t tag[TM_PRELOOK], wst[TM_PRELOOK];                                                  \
+        uint4 x[TM_PRELOOK];                                                                        \
+        uint32_t i = b;                                                                             \
+    _Pragma("unroll")                                                                               \
+        for (int l = 0; l < TM_PRELOOK; l++) {                                                      \
+            widr[l] = NONE;                                                                         \
+            tag[l] = NONE;  /* no such level */                                                     \
+            if (i <= e) {  /* level l exists and starts at byte i */                                \
+                wst[l] = i;                                                                         \
+                key[l] = level_key(&i, e, byte_at);                                                 \
+                const uint32_t len = i - wst[l];                                                    \
+                if (len == 1 && (key[l] == '+' || key[l] == '#')) badarg = true;                    \
+                tag[l] = len > 8 ? (len | W_LONG) : len;                                            \
+                sl[l] = word_slot_hash(key[l], tag[l]) & a.wmask;                                   \
+                x[l] = *reinterpret_cast<const uint4 *>(a.wtab + sl[l]);                            \
+                (PROBES)++;                                                                         \
+                nl++;                                                                               \
+                i++;                                                                                \
+            }                                                                                       \
+        }                                                                                           \
+        pre_b = i;                                                                                  \
+  /* resolve the probes (collision chains and long-word byte checks are rare) */                    \
+    _Pragma("unroll")                                                                               \
+        for (int l = 0; l < TM_PRELOOK; l++) {                                                      \
+            if (tag[l] == NONE) continue;                                                           \
+            uint4 y = x[l];                                                                         \
+            for (;;) {                                                                              \
+                if (y.w == NONE) break;                                                             \
+                if (y.z == tag[l] && y.x == (uint32_t)key[l] && y.y == (uint32_t)(key[l] >> 32)) {  \
+                    const uint32_t len = tag[l] & ~W_LONG;                                          \
+                    if (len <= 8) {                                                                 \
+                        widr[l] = y.w;                                                              \
+                        break;                                                                      \
+                    }                                                                               \
+                    const uint8_t *w = a.warena + a.word_off[y.w];                                  \
+                    bool eq = true;                                                                 \
+                    for (uint32_t k = 0; k < len && eq; k++) eq = byte_at(wst[l] + k) == w[k];      \
+                    if (eq) {                                                                       \
+                        widr[l] = y.w;                                                              \
+                        break;                                                                      \
+                    }                                                                               \
+                }                                                                                   \
+                sl[l] = (sl[l] + 1) & a.wmask;                                                      \
+                y = *reinterpret_cast<const uint4 *>(a.wtab + sl[l]);                               \
+                (PROBES)++;                                                                         \
+            }                                                                                       \
+        }                                                                                           \
+        if (pre_b <= e) {  /* levels past TM_PRELOOK: count them and check for badarg */            \
+            uint32_t st = pre_b;                                                                    \
+            for (uint32_t i2 = pre_b;; ++i2) {                                                      \
+                const bool end = i2 == e;                                                           \
+                const uint8_t c = end ? (uint8_t)'/' : byte_at(i2);                                 \
+                if (c == '/') {                                                                     \
+                    if (i2 - st == 1 && (byte_at(st) == '+' || byte_at(st) == '#')) badarg = true;  \
+                    nl++;                                                                           \
+                    st = i2 + 1;                                                                    \
+                    if (end) break;                                                                 \
+                }                                                                                   \
+            }                                                                                       \
+        }                                                                                           \
+                                                                                                    \
+    } while (0)
+
+// widr[lv] for a wave-uniform lv < TM_PRELOOK (static register indices, no scratch)
+__device__ __forceinline__ uint32_t prelook_word(const uint32_t (&widr)[TM_PRELOOK], uint32_t lv) {
+    uint32_t v = NONE;
+#pragma unroll
+    for (int l = 0; l < TM_PRELOOK; l++)
+        if (lv == (uint32_t)l) v = widr[l];
+    return v;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // fast kernel: one wavefront (= one 64-thread workgroup) per 64 topics
@@ -338,6 +425,16 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     // ---- 1. pre-scan (lane = topic): levels, badarg, '$'
     bool badarg = false, dollar = false;
     uint32_t nl = 0, b = 0, e = 0;
+#if TM_PRELOOK
+    uint32_t widr[TM_PRELOOK];  // word ids of the first TM_PRELOOK levels
+    uint32_t pre_b = 0;         // byte where level TM_PRELOOK starts
+    if (active) {
+        b = a.off[t];
+        e = a.off[t + 1];
+        dollar = (e > b) && byte_at(b) == '$';
+        TM_PRESCAN_PRELOOK(st_wprobe);
+    }
+#else
     if (active) {
         b = a.off[t];
         e = a.off[t + 1];
@@ -354,9 +451,14 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
             }
         }
     }
+#endif
     const bool spill0 = active && !badarg && a.force_slow;
     const bool walk = active && !badarg && !spill0;
+#if TM_PRELOOK
+    uint32_t cur_b = pre_b;  // byte offset where level TM_PRELOOK starts (tokenised in the walk)
+#else
     uint32_t cur_b = b;  // byte offset where this lane's topic's next level starts
+#endif
     L.nlev[lane] = nl;
     L.cnt[lane] = 0;
     {
@@ -369,7 +471,15 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     }
 
     // tokenise one level of this lane's topic (the cursor walks left to right)
-    auto tokenize_next = [&](uint32_t slot) {
+    // level lv's word id into L.wid[slot] (lv is wave-uniform)
+    auto level_word = [&](uint32_t slot, uint32_t lv) {
+#if TM_PRELOOK
+        if (lv < (uint32_t)TM_PRELOOK) {
+            L.wid[slot][lane] = prelook_word(widr, lv);
+            return;
+        }
+#endif
+        (void)lv;
         uint32_t i = cur_b;
         const uint32_t st = i;
         const uint64_t key = level_key(&i, e, byte_at);
@@ -379,7 +489,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
 
     // ---- 2. root: emit "#" keys (not for '$' topics), seed the frontier
     const RootRec R = *a.root;
-    if (walk) tokenize_next(0);  // level 0
+    if (walk) level_word(0, 0);  // level 0
     uint32_t nseg = 0, nchunk = 0;  // wave-uniform
     uint32_t nfr;
     {
@@ -436,7 +546,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
         const uint32_t cur = d & 1, nxt = cur ^ 1;
         // 3a. tokenise level d+1 ahead for topics that are still alive and go deeper:
         //     the children pushed at this depth are filtered with it (bloom)
-        if (walk && ((L.alive[cur] >> lane) & 1ull) && d + 1 < nl) tokenize_next(nxt);
+        if (walk && ((L.alive[cur] >> lane) & 1ull) && d + 1 < nl) level_word(nxt, d + 1);
         if (lane == 0) L.alive[nxt] = 0;
         __syncthreads();
         // 3b. expand the frontier, WAVE * RPL entries per round (RPL per lane, so each
@@ -991,6 +1101,18 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
 
     bool badarg = false, dollar = false;
     uint32_t nl = 0, b = 0, e = 0;
+    uint32_t dummy = 0;
+#if TM_PRELOOK
+    uint32_t widr[TM_PRELOOK];
+    uint32_t pre_b = 0;
+    if (active) {
+        b = a.off[t];
+        e = a.off[t + 1];
+        dollar = (e > b) && byte_at(b) == '$';
+        TM_PRESCAN_PRELOOK(dummy);
+    }
+    uint32_t cur_b = pre_b;
+#else
     if (active) {
         b = a.off[t];
         e = a.off[t + 1];
@@ -1007,9 +1129,10 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
             }
         }
     }
+    uint32_t cur_b = b;
+#endif
     const bool spill0 = active && !badarg && a.force_slow;
     const bool walk = active && !badarg && !spill0;
-    uint32_t cur_b = b;
     L.nlev[lane] = nl;
     L.best[lane] = ~0ull;
     L.win[lane] = 0;
@@ -1021,8 +1144,14 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
             L.alive[1] = 0;
         }
     }
-    uint32_t dummy = 0;
-    auto tokenize_next = [&](uint32_t slot) {
+    auto level_word = [&](uint32_t slot, uint32_t lv) {  // level lv's word id (lv wave-uniform)
+#if TM_PRELOOK
+        if (lv < (uint32_t)TM_PRELOOK) {
+            L.wid[slot][lane] = prelook_word(widr, lv);
+            return;
+        }
+#endif
+        (void)lv;
         uint32_t i = cur_b;
         const uint32_t st = i;
         const uint64_t key = level_key(&i, e, byte_at);
@@ -1032,7 +1161,7 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
 
     // ---- root: a root '#' key (code '#' at level 0) is the smallest any topic can match
     const RootRec R = *a.root;
-    if (walk) tokenize_next(0);
+    if (walk) level_word(0, 0);
     uint32_t nfr;
     {
         const bool rh = walk && !dollar && R.hash_cnt;
@@ -1087,7 +1216,7 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
     constexpr uint64_t ALL_LIT = (1ull << 62) - 1;
     for (uint32_t d = 0; nfr > 0; ++d) {
         const uint32_t cur = d & 1, nxt = cur ^ 1;
-        if (walk && ((L.alive[cur] >> lane) & 1ull) && d + 1 < nl) tokenize_next(nxt);
+        if (walk && ((L.alive[cur] >> lane) & 1ull) && d + 1 < nl) level_word(nxt, d + 1);
         if (lane == 0) L.alive[nxt] = 0;
         __syncthreads();
         uint32_t nnext = 0;

@@ -29,7 +29,10 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 # "head": the committed match_kernels.hip (git HEAD) with the working tree's engine, as the
 # same-process reference point.
 VARIANTS = {
+    "head": ([], 0),  # match_kernels.hip as committed (git HEAD)
     "base": ([], 0),
+    "base2": ([], 0),  # the same build again: run-to-run noise and the digest's self-check
+    "nopre": (["-DTM_PRELOOK=0"], 0),
     "tb2560_f448": (["-DTM_TBCAP=2560", "-DTM_FCAP=448"], 0),
     "tb2048_f512": (["-DTM_TBCAP=2048", "-DTM_FCAP=512"], 0),
     "tb2304_f480": (["-DTM_TBCAP=2304", "-DTM_FCAP=480"], 0),
@@ -76,6 +79,7 @@ def run(args):
     stream = torch.cuda.Stream(dev)
     import importlib
     results = []
+    digests = []
     for name in args.variants:
         lib = os.path.join(VDIR, f"libemqx_tm_{name}.so")
         os.environ["EMQX_TM_LIB"] = lib
@@ -83,6 +87,7 @@ def run(args):
         importlib.reload(_native)
         N = _native
         t0 = time.time()
+        print(f"variant {name}: building the index", file=sys.stderr, flush=True)
         v = VARIANTS[name]
         eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4, edge_load_inv=v[1],
                        topics_per_wave=v[2] if len(v) > 2 else 0)
@@ -104,9 +109,10 @@ def run(args):
         eng.device_sync()
         torch.cuda.synchronize()
         eng.debug_stats(True, read=False)
-        step()
+        r = step()  # this launch's result (reserve_matches above re-allocated the key arena)
         torch.cuda.synchronize()
         walk = dict(zip(N.Engine.STAT_NAMES, [int(x) for x in eng.debug_stats(False)]))
+        digest = _topic_digest(eng, r, n, _read_u64(r.d_total), sp)
         eng.debug_stats(False, read=False)
         kms = []
         for _ in range(args.steps):
@@ -125,12 +131,35 @@ def run(args):
                "batch_ms": round(bms, 4), "keys": walk["keys"], "edge_probes": walk["edge_probes"],
                "word_probes": walk["word_probes"], "edge_slots": st["edge_slots"], "build_s": round(tbuild, 1),
                "cyc": [walk["cyc_prescan"], walk["cyc_walk"], walk["cyc_copyout"]]}
+        if digests:
+            rec["same_keys_per_topic"] = bool(torch.equal(digest, digests[0]))
+        digests.append(digest)
         print(json.dumps(rec), flush=True)
         results.append(rec)
         eng.close()
         del eng
     keys = {r["keys"] for r in results}
     print(json.dumps({"consistent_key_counts": len(keys) == 1}), flush=True)
+
+
+def _topic_digest(eng, r, n, total, stream):
+    """Per topic: the count and the sum of a hash of its route ids (order-independent; key
+    handles are build-specific, ids are not), from tm_result_ids_device on the device."""
+    import torch
+    if total > r.keys_cap:
+        raise RuntimeError(f"batch overflowed its key arena ({total} > {r.keys_cap})")
+    dev = torch.device("cuda", 0)
+    ids = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+    off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    eng.result_ids_device(ids.data_ptr(), ids.numel(), off.data_ptr(), stream)
+    eng.device_sync()
+    torch.cuda.synchronize()
+    o = off.long() & 0xFFFFFFFF
+    h = (ids[:total] * 0x9E3779B97F4A7C15) >> 16
+    cs = torch.zeros(total + 1, dtype=torch.int64, device=dev)
+    cs[1:] = torch.cumsum(h, 0)
+    return torch.stack([o[1:] - o[:-1], cs[o[1:]] - cs[o[:-1]]])
 
 
 def _read_u64(ptr):
