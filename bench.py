@@ -252,6 +252,8 @@ def main():
     ap.add_argument("--filter-search", type=int, default=0, metavar="Q",
                     help="matches_filter/3 run: Q topic-filter queries (the config's own filters, "
                          "generalised) walked on the GPU (tm_match_filter_batch), oracle beside it")
+    ap.add_argument("--filter-kinds", default="", help="development: comma list of query kinds to keep "
+                    "(0 stored filters, 1 one level '+', 2 prefix + '#')")
     args = ap.parse_args()
     if args.filter_search:
         return run_filter(args)
@@ -752,7 +754,7 @@ def oracle_index(w):
     return _ORACLE_IX[id(w)]
 
 
-def filter_queries(w, q, seed=0xF11):
+def filter_queries(w, q, seed=0xF11, kinds=None):
     """Q topic filters from the workload's own filters: a third as stored, a third with one
     level turned '+', a third cut to a deep prefix (at most 2 levels off) + '#' (valid
     filters: '#' only last; shallow '#' queries would return most of the index)."""
@@ -760,6 +762,10 @@ def filter_queries(w, q, seed=0xF11):
     nf = len(w.f_id)
     pick = rng.integers(0, nf, q)
     kind = rng.integers(0, 3, q)
+    if kinds:  # development: only these query kinds (0 stored, 1 one '+', 2 prefix + '#')
+        keep = np.isin(kind, kinds)
+        pick, kind = pick[keep], kind[keep]
+        q = len(pick)
     out = []
     for j, k in zip(pick, kind):
         ws = bytes(w.f_bytes[w.f_off[j]:w.f_off[j + 1]]).split(b"/")
@@ -782,7 +788,7 @@ def filter_leg(args, w, eng, q):
     after the per-epoch index build; the oracle's restatement (oracle/trie_search.cpp
     ALGO_FILTER) timed on the same queries; walk order compared on a sample."""
     import oracle
-    qb, qo = filter_queries(w, q)
+    qb, qo = filter_queries(w, q, kinds=[int(x) for x in args.filter_kinds.split(",")] if args.filter_kinds else None)
     qo = np.ascontiguousarray(qo, dtype=np.uint32)
     t0 = time.perf_counter()
     eng.match_filter_view(qb, qo[:2])  # first call after the commit builds the index

@@ -1203,7 +1203,7 @@ struct tm_engine {
         std::vector<std::string> dict;   // sorted distinct literal words of the keys
         uint32_t K = 0;
         DevBuf d_kw, d_koff, d_kh;
-        DevBuf d_qw, d_qoff, d_qdollar, d_qstatus, d_cnt, d_off, d_out, d_scan, d_pool, d_ctl;
+        DevBuf d_qw, d_qoff, d_qdollar, d_qstatus, d_cnt, d_off, d_out, d_scan, d_pool, d_ctl, d_jobs, d_krec;
         uint64_t out_want = 1 << 16, pool_want = 1024;  // one-pass sizes (from the demand seen)
         std::vector<uint32_t> qw, qoff, h_off, h_cnt, u_keys;
         std::vector<uint32_t> wcode;     // interned word id -> order code (NONE: not cached yet)
@@ -1310,15 +1310,25 @@ struct tm_engine {
             kh[j] = lk[i];
         }
         kw.insert(kw.end(), 8, 0u);  // k_filter_walk preloads 8 words of a key unconditionally
+        // fixed-stride records {length, first FW_REC_WORDS codes}: a compare reads one 32-B
+        // record instead of koff and then the words (one round trip instead of two)
+        std::vector<uint32_t> krec(std::max<size_t>(lk.size(), 1) * 8, 0u);
+        for (size_t j = 0; j < lk.size(); j++) {
+            const uint32_t b = koff[j], L = koff[j + 1] - b;
+            krec[j * 8] = L;
+            for (uint32_t i = 0; i < std::min<uint32_t>(L, FW_REC_WORDS); i++) krec[j * 8 + 1 + i] = kw[b + i];
+        }
         fx.K = (uint32_t)lk.size();
         hipError_t e;
-        if ((e = fx.d_kw.ensure(std::max<size_t>(kw.size(), 1) * 4)) != hipSuccess ||
+        if ((e = fx.d_krec.ensure(krec.size() * 4)) != hipSuccess ||
+            (e = fx.d_kw.ensure(std::max<size_t>(kw.size(), 1) * 4)) != hipSuccess ||
             (e = fx.d_koff.ensure(koff.size() * 4)) != hipSuccess ||
             (e = fx.d_kh.ensure(std::max<size_t>(kh.size(), 1) * 4)) != hipSuccess) {
             err = std::string("matches_filter index alloc: ") + hipGetErrorString(e);
             return TM_ENOMEM;
         }
-        if ((!kw.empty() && (e = hipMemcpy(fx.d_kw.p, kw.data(), kw.size() * 4, hipMemcpyHostToDevice))) ||
+        if ((e = hipMemcpy(fx.d_krec.p, krec.data(), krec.size() * 4, hipMemcpyHostToDevice)) ||
+            (!kw.empty() && (e = hipMemcpy(fx.d_kw.p, kw.data(), kw.size() * 4, hipMemcpyHostToDevice))) ||
             (e = hipMemcpy(fx.d_koff.p, koff.data(), koff.size() * 4, hipMemcpyHostToDevice)) ||
             (!kh.empty() && (e = hipMemcpy(fx.d_kh.p, kh.data(), kh.size() * 4, hipMemcpyHostToDevice)))) {
             err = std::string("matches_filter index upload: ") + hipGetErrorString(e);
@@ -1404,7 +1414,7 @@ void tm_destroy(tm_engine *eng) {
                       &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
                       &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan, &eng->fx.d_pool,
-                      &eng->fx.d_ctl, &eng->d_ia, &eng->d_iaoff,
+                      &eng->fx.d_ctl, &eng->fx.d_jobs, &eng->fx.d_krec, &eng->d_ia, &eng->d_iaoff,
                       &eng->d_ib, &eng->d_iboff, &eng->d_iout, &eng->d_ilen})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
@@ -2168,6 +2178,7 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
                "H2D");
     FilterArgs a{};
     a.kw = fx.d_kw.as<uint32_t>();
+    a.krec = fx.d_krec.as<uint4>();
     a.koff = fx.d_koff.as<uint32_t>();
     a.kh = fx.d_kh.as<uint32_t>();
     a.K = fx.K;
@@ -2191,16 +2202,22 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
         const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(fx.out_want, 1 << 16), 0xFFFFFFF0ull);
         TM_TRY_HIP(fx.d_pool.ensure(pool * FW_CHUNK * 4), TM_ENOMEM, "alloc filter pool");
         TM_TRY_HIP(fx.d_out.ensure(cap * 4), TM_ENOMEM, "alloc");
-        TM_TRY_HIP(fx.d_ctl.ensure(16), TM_ENOMEM, "alloc");
-        TM_TRY_HIP(hipMemsetAsync(fx.d_ctl.p, 0, 16, s), TM_EDEVICE, "memset");
+        TM_TRY_HIP(fx.d_ctl.ensure(24), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(hipMemsetAsync(fx.d_ctl.p, 0, 24, s), TM_EDEVICE, "memset");
+        // bulk copy jobs: ranges of more than FW_BULK keys, all inside the output
+        const uint64_t jobs = cap / FW_BULK + 64;
+        TM_TRY_HIP(fx.d_jobs.ensure(jobs * sizeof(uint4)), TM_ENOMEM, "alloc filter jobs");
         a.pool = fx.d_pool.as<uint32_t>();
         a.pool_chunks = fx.d_pool.cap / (FW_CHUNK * 4);
         a.out = fx.d_out.as<uint32_t>();
         a.out_cap = fx.d_out.cap / 4;
         a.ctl = fx.d_ctl.as<unsigned long long>();
-        uint64_t ctl[2] = {0, 0};
+        a.jobs = fx.d_jobs.as<uint4>();
+        a.jobs_cap = fx.d_jobs.cap / sizeof(uint4);
+        uint64_t ctl[3] = {0, 0, 0};
         TM_TRY_HIP(launch_filter_walk(a, FW_ONEPASS, s), TM_EDEVICE, "k_filter_walk");
-        TM_TRY_HIP(hipMemcpyAsync(ctl, fx.d_ctl.p, 16, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+        TM_TRY_HIP(launch_filter_bulk(a, s), TM_EDEVICE, "k_filter_bulk");
+        TM_TRY_HIP(hipMemcpyAsync(ctl, fx.d_ctl.p, 24, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
         TM_TRY_HIP(hipMemcpyAsync(fx.h_off.data(), fx.d_off.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                    "D2H");
         TM_TRY_HIP(hipMemcpyAsync(fx.h_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
@@ -2237,9 +2254,9 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
             return TM_ENOMEM;
         }
         // the next batch's one-pass sizes: this demand with headroom (a query wastes at most
-        // one partly filled chunk)
+        // one partly filled chunk; a chunk holds FW_CHUNK / 2 - 1 ranges)
         fx.out_want = total + total / 4 + 1024;
-        fx.pool_want = (total / (FW_CHUNK - 1) + n) + (total / (FW_CHUNK - 1) + n) / 4 + 64;
+        fx.pool_want = (total / (FW_CHUNK / 2 - 1) + n) + (total / (FW_CHUNK / 2 - 1) + n) / 4 + 64;
         TM_TRY_HIP(fx.h_keys.ensure(std::max<uint64_t>(total, 1) * 4), TM_ENOMEM, "pinned alloc");
         if (total) {
             TM_TRY_HIP(fx.d_out.ensure(total * 4), TM_ENOMEM, "alloc");

@@ -13,6 +13,7 @@ namespace tmx {
 struct FilterArgs {
     const uint32_t *kw;    // order codes of every key's words, keys back to back
     const uint32_t *koff;  // K+1: key j's words are kw[koff[j] .. koff[j+1])
+    const uint4 *krec;     // 2 per key: {length, words 0 .. FW_REC_WORDS-1 (0-padded)}
     const uint32_t *kh;    // K: key handle of sorted key j
     uint32_t K;
     uint32_t n;            // queries
@@ -24,16 +25,26 @@ struct FilterArgs {
     uint32_t *cnt;           // pass 0 out: n;  FW_ONEPASS out: n
     uint32_t *out_off;       // pass 1 in: n (exclusive scan of cnt);  FW_ONEPASS out: n
     uint32_t *out;           // pass 1 / FW_ONEPASS out: key handles, per query in walk order
-    // FW_ONEPASS: the walk streams its keys into linked chunks of FW_CHUNK words (word 0 = next
-    // chunk) from `pool`, then reserves its contiguous output range with one atomic and copies
+    // FW_ONEPASS: the walk streams its matches as ranges {first sorted key, count} into linked
+    // chunks of FW_CHUNK u32 words (entry 0's .x = next chunk) from `pool`, then reserves its
+    // contiguous output range with one atomic and expands the ranges into it; ranges longer
+    // than FW_BULK keys become jobs of k_filter_bulk (all CUs copy them)
     uint32_t *pool;
     uint64_t pool_chunks;
     uint64_t out_cap;
-    unsigned long long *ctl;  // [0] output keys requested, [1] chunks requested (may pass the caps)
+    unsigned long long *ctl;  // [0] output keys requested, [1] chunks requested (may pass the caps),
+                              // [2] bulk jobs
+    uint4 *jobs;              // FW_ONEPASS: {src sorted key, dst, count (<= FW_JOB), 0}
+    uint64_t jobs_cap;
 };
 constexpr int FW_COUNT = 0, FW_EMIT = 1, FW_ONEPASS = 2;
-constexpr uint32_t FW_CHUNK = 256;  // u32 words per pool chunk (1 link + 255 keys)
+constexpr uint32_t FW_CHUNK = 256;   // u32 words per pool chunk (1 link entry + 127 ranges of 2 words)
+constexpr uint32_t FW_BULK = 4096;   // ranges longer than this are copied by k_filter_bulk
+constexpr uint32_t FW_JOB = 8192;    // keys per k_filter_bulk job (a long range is split)
+constexpr uint32_t FW_REC_WORDS = 7; // key words held in the fixed-stride record
 hipError_t launch_filter_walk(const FilterArgs &a, int pass, hipStream_t stream);
+// FW_ONEPASS's bulk copies (after launch_filter_walk, same stream; reads the job count on device)
+hipError_t launch_filter_bulk(const FilterArgs &a, hipStream_t stream);
 // emqx_topic:intersection/2 per pair; out_len[i] = bytes, or one of:
 constexpr int32_t INTERSECT_FALSE = -1, INTERSECT_BADHASH = -2;
 hipError_t launch_intersect(const uint8_t *a, const uint32_t *a_off, const uint8_t *b, const uint32_t *b_off,

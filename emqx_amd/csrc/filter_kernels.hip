@@ -26,31 +26,64 @@ constexpr uint32_t C_HASH = 0, C_PLUS = 1;
 constexpr uint32_t NONE_FW = 0xFFFFFFFFu;
 constexpr int R_FULL = 0, R_PREFIX = 1, R_LOWER = 2, R_SEEK = 3;
 
-// key j vs pre[0..np) ++ [w]: -1 / 0 / 1
-__device__ inline int cmp_key_seek(const FilterArgs &a, uint32_t j, const uint32_t *pre, uint32_t np, uint32_t w) {
-    const uint32_t b = a.koff[j], L = a.koff[j + 1] - b;
-    const uint32_t *k = a.kw + b;
-    for (uint32_t i = 0; i < np; i++) {
-        if (i == L) return -1;
-        const uint32_t x = k[i];
-        if (x != pre[i]) return x < pre[i] ? -1 : 1;
-    }
-    if (np == L) return -1;
-    const uint32_t x = k[np];
-    if (x != w) return x < w ? -1 : 1;
-    return L == np + 1 ? 0 : 1;
+constexpr uint32_t RW = FW_REC_WORDS;
+
+// key j's record: its length and first RW words (0-padded)
+__device__ __forceinline__ uint32_t load_rec(const FilterArgs &a, uint32_t j, uint32_t (&kr)[RW]) {
+    const uint4 r0 = a.krec[2 * (uint64_t)j], r1 = a.krec[2 * (uint64_t)j + 1];
+    kr[0] = r0.y;
+    kr[1] = r0.z;
+    kr[2] = r0.w;
+    kr[3] = r1.x;
+    kr[4] = r1.y;
+    kr[5] = r1.z;
+    kr[6] = r1.w;
+    return r0.x;
 }
 
-// next({pre ++ [w], {}}) among keys [lo, K): the first key >= the probe, found by the whole
+// The seek probe {first np words of key ks ++ [w], {}}: the first RW prefix words in registers
+// (taken from key ks's record, which the wave already holds), the rest read from kw.
+struct Probe {
+    uint32_t pr[RW];
+    uint32_t ks, np, w;
+};
+
+// key j vs the probe: -1 / 0 / 1.  One record load: the compare is one round trip unless
+// the prefix is longer than the record.
+__device__ inline int cmp_key_seek(const FilterArgs &a, uint32_t j, const Probe &pb) {
+    uint32_t kr[RW];
+    const uint32_t L = load_rec(a, j, kr);
+    uint32_t xn = 0;  // the key's word at position np (when np < RW)
+#pragma unroll
+    for (int i = 0; i < (int)RW; i++) {
+        if ((uint32_t)i < pb.np) {
+            if ((uint32_t)i == L) return -1;
+            if (kr[i] != pb.pr[i]) return kr[i] < pb.pr[i] ? -1 : 1;
+        }
+        if ((uint32_t)i == pb.np) xn = kr[i];
+    }
+    if (pb.np > RW) {
+        const uint32_t *k = a.kw + a.koff[j], *pre = a.kw + a.koff[pb.ks];
+        for (uint32_t i = RW; i < pb.np; i++) {
+            if (i == L) return -1;
+            if (k[i] != pre[i]) return k[i] < pre[i] ? -1 : 1;
+        }
+    }
+    if (pb.np == L) return -1;
+    const uint32_t x = pb.np < RW ? xn : a.kw[a.koff[j] + pb.np];
+    if (x != pb.w) return x < pb.w ? -1 : 1;
+    return L == pb.np + 1 ? 0 : 1;
+}
+
+// next(probe) among keys [lo, K): the first key >= the probe, found by the whole
 // wave.  Gallop: lane L probes lo + 2^L - 1 (lane 32 lies past any K < 2^32), which
 // brackets the answer; then 64-ary narrowing, each round probing 64 evenly spaced keys
 // (a range of K keys takes about log64(K) rounds).  Wave-uniform result.
-__device__ uint32_t wave_seek(const FilterArgs &a, uint32_t lo, const uint32_t *pre, uint32_t np, uint32_t w,
-                              uint32_t lane) {
+__device__ uint32_t wave_seek(const FilterArgs &a, uint32_t lo, const Probe &pb, uint32_t lane) {
     const uint64_t K = a.K;
     if (lo >= K) return (uint32_t)K;
     const uint64_t p = lane < 33 ? (uint64_t)lo + ((1ull << lane) - 1) : ~0ull;
-    const bool ge = p >= K || cmp_key_seek(a, (uint32_t)p, pre, np, w) >= 0;
+    const bool ge = p >= K || cmp_key_seek(a, (uint32_t)p, pb) >= 0;
     const uint32_t g = (uint32_t)__ffsll((long long)__ballot(ge)) - 1;  // lane 32 is always ge
     if (g == 0) return lo;
     // invariant: every key below l is < the probe; key h is >= it (or h == K)
@@ -58,7 +91,7 @@ __device__ uint32_t wave_seek(const FilterArgs &a, uint32_t lo, const uint32_t *
     while (l < h) {
         const uint64_t step = (h - l + 63) / 64;
         const uint64_t x = l + lane * step;
-        const bool xge = x >= h || cmp_key_seek(a, (uint32_t)x, pre, np, w) >= 0;
+        const bool xge = x >= h || cmp_key_seek(a, (uint32_t)x, pb) >= 0;
         const uint64_t m = __ballot(xge);
         if (!m) {
             l = l + 63 * step + 1;
@@ -92,7 +125,10 @@ __device__ uint32_t wave_seek(const FilterArgs &a, uint32_t lo, const uint32_t *
             return R_LOWER;                                                                    \
         }                                                                                      \
         const uint32_t w_ = (W_);                                                              \
-        if (WL - pos_ == 1 && w_ == C_HASH) return R_FULL; /* (_, ['#'], _) */                 \
+        if (WL - pos_ == 1 && w_ == C_HASH) { /* (_, ['#'], _) */                             \
+            qh = pos_;                                                                         \
+            return R_FULL;                                                                     \
+        }                                                                                      \
         if (w_ != C_PLUS) { /* ([_|TF], ['+'|TW], Pos) continues */                            \
             if (f_ == C_PLUS) { /* (['+'|TF], [HW|TW], Pos) */                                 \
                 lp = (int)pos_;                                                                \
@@ -113,20 +149,47 @@ __device__ uint32_t wave_seek(const FilterArgs &a, uint32_t lo, const uint32_t *
         }                                                                                      \
     }
 
-// compare/3 for a filter search.  The first 8 words of the key (fr) and of the query (wr)
-// come preloaded in registers and the first 8 positions are unrolled (static indices keep
-// them in registers), so a compare is not a chain of dependent loads.
-__device__ __attribute__((always_inline)) inline int cmp_filter(const uint32_t (&fr)[8], const uint32_t *F,
-                                                                uint32_t FL, const uint32_t (&wr)[8],
+// compare/3 for a filter search.  The key's record (fr: its first RW words) and the query's
+// first 8 words (wr) come preloaded in registers and the first RW positions are unrolled
+// (static indices keep them in registers), so a compare is one record load.  qh := the position
+// when the result is match_full by the query's last-level '#' (else left unchanged).
+__device__ __attribute__((always_inline)) inline int cmp_filter(const uint32_t (&fr)[RW], const FilterArgs &a,
+                                                                uint32_t j, uint32_t FL, const uint32_t (&wr)[8],
                                                                 const uint32_t *W, uint32_t WL, uint32_t &spos,
-                                                                uint32_t &sword) {
+                                                                uint32_t &sword, uint32_t &qh) {
     int lp = -1;
     uint32_t lpw = 0;
 #pragma unroll
-    for (uint32_t p = 0; p < 8; p++) CMP_STEP(p, fr[p], wr[p])
-    for (uint32_t p = 8;; p++) CMP_STEP(p, F[p], W[p])
+    for (uint32_t p = 0; p < RW; p++) CMP_STEP(p, fr[p], wr[p])
+    const uint32_t *F = a.kw + a.koff[j];  // past the record: the key's words in kw
+    for (uint32_t p = RW;; p++) CMP_STEP(p, F[p], W[p])
 }
 #undef CMP_STEP
+
+// src[0..m) -> dst[0..m) by the 64 lanes of a wave, 8 loads in flight per lane
+__device__ void copy_keys(const uint32_t *src, uint32_t *dst, uint32_t m, uint32_t lane) {
+    for (uint32_t k0 = lane; k0 < m; k0 += 64 * 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (k0 + u * 64 < m) v[u] = src[k0 + u * 64];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (k0 + u * 64 < m) dst[k0 + u * 64] = v[u];
+    }
+}
+
+// exclusive prefix sum over the 64 lanes; *total gets the wave sum
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total, uint32_t lane) {
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    *total = __shfl(x, 63, 64);
+    return x - v;
+}
 
 // One wave per query.  The walk moves to the next key after match_full / match_prefix, so
 // the 64 lanes compare keys idx .. idx+63 at once: up to the first key that compares
@@ -146,21 +209,57 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
     const uint32_t *W = a.qw + qb;
     const uint32_t K = a.K;
     uint32_t c = 0;  // wave-uniform
-    // FW_ONEPASS chunk chain (wave-uniform): head, current chunk, keys in the current chunk
-    constexpr uint32_t CK = FW_CHUNK - 1;
-    uint32_t head = NONE_FW, curc = NONE_FW, fill = CK;
+    // FW_ONEPASS chain of ranges (wave-uniform): head, current chunk, ranges in the current chunk
+    constexpr uint32_t CE = FW_CHUNK / 2 - 1;  // ranges per chunk (entry 0 is the link)
+    uint2 *const pool2 = reinterpret_cast<uint2 *>(a.pool);
+    uint32_t head = NONE_FW, curc = NONE_FW, fill = CE, nent = 0;
     bool short_pool = false;
     auto new_chunk = [&]() -> uint32_t {  // wave-uniform; NONE_FW when the pool is exhausted
         unsigned long long c0 = 0;
         if (lane == 0) c0 = atomicAdd(&a.ctl[1], 1ull);
         c0 = __shfl(c0, 0);
         if (c0 >= a.pool_chunks) return NONE_FW;
-        if (lane == 0) a.pool[c0 * FW_CHUNK] = NONE_FW;
+        if (lane == 0) pool2[c0 * (FW_CHUNK / 2)] = make_uint2(NONE_FW, 0u);
         return (uint32_t)c0;
+    };
+    // append one range per lane in `em` (this lane's is {src, len}), in lane order
+    auto chain_put = [&](uint64_t em, uint32_t src, uint32_t len) {
+        const uint32_t ne = __popcll(em);
+        if (!ne || short_pool) return;
+        const uint32_t room = CE - fill;
+        uint32_t nc = NONE_FW;
+        if (ne > room) {
+            nc = new_chunk();
+            if (nc == NONE_FW) {
+                short_pool = true;
+                return;
+            }
+            if (curc == NONE_FW) head = nc;
+            else if (lane == 0) pool2[(uint64_t)curc * (FW_CHUNK / 2)] = make_uint2(nc, 0u);  // link
+        }
+        if ((em >> lane) & 1ull) {
+            const uint32_t rk = __popcll(em & ((1ull << lane) - 1));
+            const uint64_t at = rk < room ? (uint64_t)curc * (FW_CHUNK / 2) + 1 + fill + rk
+                                          : (uint64_t)nc * (FW_CHUNK / 2) + 1 + (rk - room);
+            pool2[at] = make_uint2(src, len);
+        }
+        if (ne > room) {
+            curc = nc;
+            fill = ne - room;
+        } else {
+            fill += ne;
+        }
+        nent += ne;
     };
     if (WL && a.qstatus[q] == 0) {
         // base_init/1 (:160-163): a first word <<"$", _/bytes>> starts at next({[W0], {}})
-        uint32_t idx = a.qdollar[q] ? wave_seek(a, 0, nullptr, 0, W[0], lane) : 0;
+        uint32_t idx = 0;
+        if (a.qdollar[q]) {
+            Probe pb{};
+            pb.np = 0;
+            pb.w = W[0];
+            idx = wave_seek(a, 0, pb, lane);
+        }
         uint32_t *out = pass == FW_EMIT ? a.out + a.out_off[q] : nullptr;
         const uint64_t below = (1ull << lane) - 1;
         uint32_t wr[8];  // the query's first 8 words (qw is padded by 8 words on the device)
@@ -169,49 +268,61 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
         while (idx < K) {
             const uint32_t j = idx + lane;
             int r = R_LOWER;  // past the end of the table: the walk stops there
-            uint32_t spos = 0, sword = 0;
+            uint32_t spos = 0, sword = 0, qh = NONE_FW;
+            uint32_t fr[RW] = {};
             if (j < K && j >= idx) {
-                const uint32_t b = a.koff[j];
-                uint32_t fr[8];  // independent loads (kw is padded by 8 words on the device)
-#pragma unroll
-                for (int i = 0; i < 8; i++) fr[i] = a.kw[b + i];
-                r = cmp_filter(fr, a.kw + b, a.koff[j + 1] - b, wr, W, WL, spos, sword);
+                const uint32_t FL = load_rec(a, j, fr);
+                r = cmp_filter(fr, a, j, FL, wr, W, WL, spos, sword, qh);
             }
+            // the probe of a seek or run end from lane l: key idx+l's record words, no loads
+            auto probe_from = [&](uint32_t l, uint32_t np, uint32_t w) {
+                Probe pb;
+#pragma unroll
+                for (int i = 0; i < (int)RW; i++) pb.pr[i] = __shfl(fr[i], l);
+                pb.ks = idx + l;
+                pb.np = np;
+                pb.w = w;
+                return pb;
+            };
             const uint64_t stop = __ballot(r == R_LOWER || r == R_SEEK);
             const uint32_t fs = stop ? (uint32_t)__ffsll((long long)stop) - 1 : 64;
-            const bool full = lane < fs && r == R_FULL;
+            // A key that is match_full by the query's last-level '#' at position p starts a run:
+            // every following key with the same first p words is match_full too (the compare
+            // reads nothing else of them), and those keys are contiguous in term order.
+            const uint64_t runm = __ballot(lane < fs && qh != NONE_FW);
+            const uint32_t rl = runm ? (uint32_t)__ffsll((long long)runm) - 1 : 64;
+            const uint32_t lim = min(fs, rl);
+            const bool full = lane < lim && r == R_FULL;
             uint64_t fm = __ballot(full);
             if (a.first && fm) fm &= 0 - fm;  // return_first: the first key met only
             const uint32_t nf = __popcll(fm);
-            if (pass == FW_ONEPASS && nf && !short_pool) {
-                // room in the current chunk for `room` keys; the rest go to a fresh chunk
-                const uint32_t room = CK - fill;
-                uint32_t nc = NONE_FW;
-                if (nf > room) {
-                    nc = new_chunk();
-                    if (nc == NONE_FW) short_pool = true;
-                    else if (curc == NONE_FW) head = nc;
-                    else if (lane == 0) a.pool[(uint64_t)curc * FW_CHUNK] = nc;  // link
-                }
-                if (!short_pool) {
-                    if ((fm >> lane) & 1ull) {
-                        const uint32_t rk = __popcll(fm & below);
-                        const uint64_t at = rk < room ? (uint64_t)curc * FW_CHUNK + 1 + fill + rk
-                                                      : (uint64_t)nc * FW_CHUNK + 1 + (rk - room);
-                        a.pool[at] = a.kh[j];
-                    }
-                    if (nf > room) {
-                        curc = nc;
-                        fill = nf - room;
-                    } else {
-                        fill += nf;
-                    }
-                }
+            if (pass == FW_ONEPASS) {
+                // consecutive FULL lanes form one range: {first key, run length}
+                const bool st0 = ((fm >> lane) & 1ull) && (lane == 0 || !((fm >> (lane - 1)) & 1ull));
+                const uint64_t sm = __ballot(st0);
+                const uint64_t rest = ~(fm >> lane);  // 0 only at lane 0 with all 64 lanes FULL
+                const uint32_t rlen = st0 ? (rest ? (uint32_t)__ffsll((long long)rest) - 1 : 64u) : 0u;
+                chain_put(sm, j, rlen);
             } else if (pass == FW_EMIT && ((fm >> lane) & 1ull)) {
                 out[c + __popcll(fm & below)] = a.kh[j];  // match_add/2, walk order
             }
             c += nf;
             if (a.first && nf) break;
+            if (rl < fs) {
+                // the run [rs, E): E = next({first p words of key rs ++ [+inf], {}})
+                const uint32_t rs = idx + rl, p = __shfl(qh, rl);
+                const uint32_t E = a.first ? rs + 1 : wave_seek(a, rs + 1, probe_from(rl, p, NONE_FW), lane);
+                const uint32_t m = E - rs;
+                if (pass == FW_EMIT) {
+                    copy_keys(a.kh + rs, out + c, m, lane);
+                } else if (pass == FW_ONEPASS) {
+                    chain_put(1ull, rs, m);
+                }
+                c += m;
+                if (a.first) break;
+                idx = E;
+                continue;
+            }
             if (fs == 64) {                      // 64 x next(Cursor)
                 idx += 64;
                 continue;
@@ -221,7 +332,7 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             if (rs == R_LOWER || ks >= K) break;  // lower, or '$end_of_table'
             // seek/3: next({first spos words of key ks ++ [sword], {}})
             const uint32_t sp = __shfl(spos, fs), sw = __shfl(sword, fs);
-            idx = wave_seek(a, ks + 1, a.kw + a.koff[ks], sp, sw, lane);
+            idx = wave_seek(a, ks + 1, probe_from(fs, sp, sw), lane);
         }
     }
     if (pass == FW_COUNT && lane == 0) a.cnt[q] = c;
@@ -234,19 +345,72 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             a.out_off[q] = (uint32_t)base;
         }
         if (short_pool || base + c > a.out_cap) return;  // the host re-runs the batch
-        __threadfence_block();  // the chain's keys and links (other lanes' stores) before reading them
-        // copy the chain into [base, base + c): 255 keys per chunk, 64 lanes at a time
-        uint32_t ch = head;
-        for (uint32_t done = 0; done < c; done += CK) {
-            const uint32_t m = min(CK, c - done);
-            const uint32_t *src = a.pool + (uint64_t)ch * FW_CHUNK + 1;
-            for (uint32_t k = lane; k < m; k += 64) a.out[base + done + k] = src[k];
-            ch = a.pool[(uint64_t)ch * FW_CHUNK];
+        __threadfence_block();  // the chain's ranges and links (other lanes' stores) before reading them
+        // expand the ranges into [base, base + c), chunk by chunk: ranges of up to 8 keys by
+        // their lane, longer ones by the wave, longer than FW_BULK keys by k_filter_bulk
+        uint32_t ch = head, pos = 0;
+        for (uint32_t cb = 0; cb < nent; cb += CE) {
+            const uint32_t m = min(CE, nent - cb);
+            const uint2 *ent = pool2 + (uint64_t)ch * (FW_CHUNK / 2) + 1;
+            for (uint32_t e0 = 0; e0 < m; e0 += 64) {
+                uint2 r = e0 + lane < m ? ent[e0 + lane] : make_uint2(0u, 0u);
+                uint32_t tot;
+                const uint32_t d = (uint32_t)base + pos + wave_excl_scan(r.y, &tot, lane);
+                pos += tot;
+                if (d + (uint64_t)r.y > base + c) r.y = 0;  // never write past the range (a bad
+                                                            // chain shows as a parity failure)
+                if (r.y <= 8) {
+                    for (uint32_t k = 0; k < r.y; k++) a.out[d + k] = a.kh[r.x + k];
+                }
+                bool queued = false;
+                if (r.y > FW_BULK) {  // FW_JOB keys per job
+                    const uint32_t nj = (r.y + FW_JOB - 1) / FW_JOB;
+                    const unsigned long long jn = atomicAdd(&a.ctl[2], (unsigned long long)nj);
+                    if (jn + nj <= a.jobs_cap) {
+                        for (uint32_t u = 0; u < nj; u++)
+                            a.jobs[jn + u] = make_uint4(r.x + u * FW_JOB, d + u * FW_JOB, min(FW_JOB, r.y - u * FW_JOB), 0u);
+                        queued = true;
+                    }
+                }
+                uint64_t wv = __ballot(r.y > 8 && !queued);  // the wave copies these one by one
+                while (wv) {
+                    const uint32_t l = (uint32_t)__ffsll((long long)wv) - 1;
+                    wv &= wv - 1;
+                    copy_keys(a.kh + __shfl(r.x, l), a.out + __shfl(d, l), __shfl(r.y, l), lane);
+                }
+            }
+            if (cb + CE < nent) ch = pool2[(uint64_t)ch * (FW_CHUNK / 2)].x;  // next chunk
+        }
+    }
+}
+
+// FW_ONEPASS's long ranges, split into jobs of at most FW_JOB keys: a block per job
+__global__ __launch_bounds__(256) void k_filter_bulk(FilterArgs a) {
+    const unsigned long long nj = min(a.ctl[2], (unsigned long long)a.jobs_cap);
+    for (unsigned long long jn = blockIdx.x; jn < nj; jn += gridDim.x) {
+        uint4 jb = a.jobs[jn];
+        if (jb.y + (uint64_t)jb.z > a.out_cap) jb.z = 0;  // never write past the output
+        const uint32_t *src = a.kh + jb.x;
+        uint32_t *dst = a.out + jb.y;
+        for (uint32_t k0 = threadIdx.x; k0 < jb.z; k0 += 256 * 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (k0 + u * 256 < jb.z) v[u] = src[k0 + u * 256];
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (k0 + u * 256 < jb.z) dst[k0 + u * 256] = v[u];
         }
     }
 }
 
 }  // namespace
+
+hipError_t launch_filter_bulk(const FilterArgs &a, hipStream_t stream) {
+    if (!a.n || !a.jobs_cap) return hipSuccess;
+    hipLaunchKernelGGL(k_filter_bulk, dim3(4096), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_filter_walk(const FilterArgs &a, int pass, hipStream_t stream) {
     if (!a.n) return hipSuccess;

@@ -256,3 +256,29 @@ def test_topic_index_word_list_topics():
     assert (b"a/b", (5,)) not in tab.matches([b"a", b"b"])
     # ... but does match the same topic as a binary
     assert (b"a/b", (5,)) in tab.matches(b"a/b")
+
+
+def test_filter_walk_long_full_steps_and_bulk_ranges():
+    """Steps where all 64 keys are match_full without a query '#' (70,000 copies of one
+    word-list filter under different ids: the one-pass chain stores them as 64-key ranges), and
+    '#'-query runs longer than FW_BULK keys (copied by k_filter_bulk), through both the
+    two-pass path (the first batch: more than the 64 Ki keys a fresh engine sizes for) and
+    the one-pass path (the second), walk order against the oracle."""
+    filters = [b"d/e"] * 70000 + [b"d/f"] * 5000 + [b"d/+"] * 300 + [b"d/e/g"] * 9000 + [b"x/#"] * 10
+    ids = list(range(1, len(filters) + 1))
+    wf = [1] * len(filters)  # word-list keys: {Binary, {ID}} keys end a filter search
+    queries = [b"d/e", b"d/+", b"+/e", b"d/#", b"#", b"+/+", b"d/e/#", b"x/y", b"d/+/g"]
+    eng = N.Engine(0)
+    _load(eng, filters, ids, wf)
+    exp, st = _oracle_walks(filters, ids, wf, queries)
+    assert not st.any() and sum(len(e) for e in exp) > 1 << 16
+    got1 = _engine_walks(eng, queries)
+    got2 = _engine_walks(eng, queries)
+    s = eng.stats()
+    assert s["n_filter_twopass"] >= 1 and s["n_filter_onepass"] >= 1
+    for q, g1, g2, e in zip(queries, got1, got2, exp):
+        assert g1 == e, q
+        assert g2 == e, q
+    first = _engine_walks(eng, queries, N.TM_MATCH_FIRST)
+    exp_first, _ = _oracle_walks(filters, ids, wf, queries, oracle.MODE_FIRST)
+    assert first == exp_first
