@@ -654,7 +654,7 @@ def run_churn(args):
     live_f = list(fl)
     live_id = w.f_id.astype(np.uint64).copy()
     next_id = int(live_id.max()) + 1
-    commit_ms, match_ms, nops, phases = [], [], [], []
+    commit_ms, match_ms, nops, phases, full_eps = [], [], [], [], []
 
     def pack(fs, ids):
         off = np.zeros(len(fs) + 1, dtype=np.uint64)
@@ -679,6 +679,7 @@ def run_churn(args):
         db, do, di = pack(del_f, del_id)
         ab, ao, ai = pack(add_f, add_id)
         torch.cuda.synchronize()
+        n_full_before = int(eng.stats()["n_full_rebuilds"])
         t0 = time.perf_counter()
         eng.apply_packed(N.TM_OP_DEL, db, do, di)
         eng.apply_packed(N.TM_OP_ADD, ab, ao, ai)
@@ -696,6 +697,7 @@ def run_churn(args):
         live_id = np.concatenate([live_id[keep], add_id])
         if ep >= args.warmup:
             cs = eng.stats()
+            full_eps.append(int(cs["n_full_rebuilds"]) > n_full_before)
             phases.append((cs["commit_apply_us"], cs["commit_lists_us"], cs["commit_upload_us"]))
             commit_ms.append((t1 - t0) * 1e3)
             match_ms.append(e0.elapsed_time(e1))
@@ -723,6 +725,9 @@ def run_churn(args):
         "match_ms_p50": round(float(np.percentile(match_ms, 50)), 4),
         "publishes_per_s_incl_commit": round(n * len(match_ms) / ((np.sum(match_ms) + np.sum(commit_ms)) * 1e-3), 1),
         "full_rebuilds": st["n_full_rebuilds"], "delta_commits": st["n_delta_commits"],
+        "commit_ms_per_epoch": [round(x, 2) for x in commit_ms],
+        "commit_phase_ms_per_epoch": [[round(x / 1e3, 2) for x in ph] for ph in phases],
+        "full_rebuild_epochs": [i for i, f in enumerate(full_eps) if f],
         "build_s": round(t_build, 2),
         "host_peak_rss_gib": host_rss_gib(),
         "parity": {"sampled_topics": ps, "mismatches": int(bad), "oracle": "oracle/trie_search.cpp"},

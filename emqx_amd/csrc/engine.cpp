@@ -200,6 +200,7 @@ struct tm_engine {
     uint64_t n_edges = 0;
     std::vector<uint32_t> node_parent, node_word, node_slot;
     std::vector<NodeList> node_list;  // terminal list of every node (host numbering)
+    std::vector<uint32_t> node_cap;   // keys the node's arena list has room for (>= its count)
     std::vector<uint32_t> slot_node;  // slot -> host node (NONE for empty slots)
     std::vector<uint32_t> slot_list;  // slot -> first key of the node's list (device copy)
     RootRec root{0, 0, 0, 0};
@@ -279,6 +280,8 @@ struct tm_engine {
     std::vector<std::pair<uint32_t, uint32_t>> lv_scratch;  // classify(): (start, len) per level
     std::vector<Delta> deltas;
     std::vector<uint64_t> dirty_eslots, dirty_wslots, dirty_lists;
+    std::vector<uint64_t> dirty_arena;  // arena words already on the device, rewritten in place
+    uint64_t n_grows = 0;               // device arrays moved to a larger buffer by a delta commit
     bool root_dirty = true;
     bool need_full = true;  // full device upload at next commit
     bool words_full = false;  // word table rehashed: re-upload it whole at next commit
@@ -474,6 +477,7 @@ struct tm_engine {
         node_word.push_back(word);
         node_slot.push_back(NONE);
         node_list.push_back(NodeList{0, 0, 0});
+        node_cap.push_back(0);
         const uint32_t pd = dev_id(parent);
         s = edge_place(pd, word);
         etab[s] = EdgeSlot{pd, word, 0, 0};
@@ -774,12 +778,14 @@ struct tm_engine {
     }
 
     // Append one list (header, term keys, hash keys) to the arena.
-    NodeList append_list(const uint32_t *terms, uint32_t tc, const uint32_t *hashes, uint32_t hc) {
+    // cap >= tc + hc keys are reserved (the slack lets later epochs edit the list in place).
+    NodeList append_list(const uint32_t *terms, uint32_t tc, const uint32_t *hashes, uint32_t hc, uint32_t cap = 0) {
         if (tc + hc == 0) return NodeList{0, 0, 0};
         arena.resize(arena.size() + LIST_HDR);
         const uint32_t off = (uint32_t)arena.size();
         arena.insert(arena.end(), terms, terms + tc);
         arena.insert(arena.end(), hashes, hashes + hc);
+        if (cap > tc + hc) arena.resize(arena.size() + (cap - tc - hc), 0u);
         write_header(off, terms, tc, hashes, hc);
         return NodeList{off, tc, hc};
     }
@@ -811,8 +817,10 @@ struct tm_engine {
             if (k.kind == K_HASH) arena[hfill[k.node]++] = (uint32_t)h;
             else arena[tfill[k.node]++] = (uint32_t)h;
         }
+        node_cap.assign(nn, 0);
         for (size_t v = 0; v < nn; v++) {
             node_list[v] = NodeList{pos[v], tcnt[v], hcnt[v]};
+            node_cap[v] = tcnt[v] + hcnt[v];
             if (pos[v]) write_header(pos[v], &arena[pos[v]], tcnt[v], &arena[pos[v] + tcnt[v]], hcnt[v]);
             refresh_info((uint32_t)v);
         }
@@ -843,8 +851,24 @@ struct tm_engine {
                     if (it != Lst.end()) Lst.erase(it);
                 }
             }
-            arena_garbage += r.term_cnt + r.hash_cnt + (r.term_cnt + r.hash_cnt ? LIST_HDR : 0);
-            node_list[node] = append_list(terms.data(), (uint32_t)terms.size(), hashes.data(), (uint32_t)hashes.size());
+            const uint32_t tc = (uint32_t)terms.size(), hc = (uint32_t)hashes.size(), cap = node_cap[node];
+            if (r.list_off && tc + hc && tc + hc <= cap) {
+                // fits the list's room: rewrite it in place (header + keys), so the churn of a
+                // long list (a hot '#' prefix's subscribers) leaves no garbage behind
+                uint32_t *dst = &arena[r.list_off];
+                std::copy(terms.begin(), terms.end(), dst);
+                std::copy(hashes.begin(), hashes.end(), dst + tc);
+                write_header(r.list_off, terms.data(), tc, hashes.data(), hc);
+                for (uint64_t w = r.list_off - LIST_HDR; w < (uint64_t)r.list_off + tc + hc; w++)
+                    if (w < arena_dev) dirty_arena.push_back(w);
+                node_list[node] = NodeList{r.list_off, tc, hc};
+            } else {
+                arena_garbage += cap + (r.list_off ? LIST_HDR : 0);
+                // lists of 16 keys or more get a quarter more room when they move
+                const uint32_t room = tc + hc >= 16 ? tc + hc + (tc + hc) / 4 : tc + hc;
+                node_list[node] = append_list(terms.data(), tc, hashes.data(), hc, room);
+                node_cap[node] = tc + hc ? room : 0;
+            }
             refresh_info(node);
             i = j;
         }
@@ -1016,15 +1040,45 @@ struct tm_engine {
         return hipStreamSynchronize(stream);
     }
 
+    // A grow-only array that outgrew its device buffer moves to one 1.5x its size: its device
+    // contents are copied on the device and only the tail then crosses PCIe (round 1
+    // re-uploaded the whole index, edge table included: a 70 ms commit at config E).  Replicas
+    // get the array whole (P_WHOLE with the new capacity) ahead of the tail.
+    template <class T>
+    hipError_t grow(DevBuf &d, const std::vector<T> &h, size_t dev_n) {
+        if (h.size() * sizeof(T) <= d.cap) return hipSuccess;
+        DevBuf nb;
+        hipError_t e = nb.ensure(std::max<size_t>(h.size() * sizeof(T) * 3 / 2, 4096));
+        if (e) return e;
+        if (dev_n && (e = hipMemcpyAsync(nb.p, d.p, dev_n * sizeof(T), hipMemcpyDeviceToDevice, stream))) {
+            nb.release();
+            return e;
+        }
+        if ((e = hipStreamSynchronize(stream))) {
+            nb.release();
+            return e;
+        }
+        d.release();
+        d.p = nb.p;
+        d.cap = nb.cap;
+        nb.p = nullptr;
+        const uint32_t a = arr_of(&d);
+        if (a < A_N) patch.add(P_WHOLE, a, dev_n * sizeof(T) / ARR_ELEM[a], d.cap, h.data(), dev_n * sizeof(T));
+        n_grows++;
+        return hipSuccess;
+    }
+
     hipError_t upload_delta() {
         hipError_t e;
-        // arrays that only grow: append the tail, or re-upload everything when full
-        if (warena.size() > d_warena.cap || arena.size() * sizeof(uint32_t) > d_arena.cap ||
-            word_off.size() * sizeof(uint32_t) > d_word_off.cap)
-            return upload_full();
+        // arrays that only grow: append the tail (moving the array to a larger buffer first
+        // when it no longer fits)
+        if ((e = grow(d_warena, warena, warena_dev))) return e;
+        if ((e = grow(d_word_off, word_off, word_off_dev))) return e;
+        if ((e = grow(d_arena, arena, arena_dev))) return e;
         if ((e = put_tail(d_warena, warena, warena_dev))) return e;
         if ((e = put_tail(d_word_off, word_off, word_off_dev))) return e;
         if ((e = put_tail(d_arena, arena, arena_dev))) return e;
+        if ((e = scatter4(dirty_arena, arena, d_arena))) return e;  // lists rewritten in place
         if (words_full) {
             if ((e = put(d_wtab, wtab, 1, 1))) return e;
             dirty_wslots.clear();
@@ -1091,6 +1145,7 @@ struct tm_engine {
         dirty_eslots.clear();
         dirty_wslots.clear();
         dirty_lists.clear();
+        dirty_arena.clear();
         for (uint32_t h : free_pending) free_keys.push_back(h);
         free_pending.clear();
         epoch++;
@@ -1392,6 +1447,7 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     eng->node_slot.push_back(NONE);
     eng->node_list.reserve(rn);
     eng->node_list.push_back(NodeList{0, 0, 0});
+    eng->node_cap.push_back(0);
     eng->edge_rehash(std::min<uint64_t>(next_pow2(std::max<uint64_t>(rn * eng->edge_load_inv(), 1024)), MAX_EDGE_SLOTS));
     eng->kset_rehash(next_pow2(std::max<uint64_t>(rk * 2, 1024)));
     eng->keys.reserve(rk);
