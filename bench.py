@@ -401,6 +401,9 @@ def main():
     kernel_ms = float(np.mean(kms))
     eng.device_sync()
     slow_topics = eng.stats()["n_slow_topics"]
+    # N > 1: every replica matches the master's first topics too; their per-topic route-id
+    # digests must equal rank 0's (the master's own parity vs the oracle is checked at N = 1)
+    replica_parity = replica_check(eng, all_b, all_o, min(20000, n), dev, backend, sp, world) if world > 1 else None
 
     # ---------------------------------------------------------------- latency vs batch size
     # (not the metric: the batching window's trade-off); rank 0 only
@@ -520,6 +523,7 @@ def main():
             "intersection": inter,
             "cpu_baseline": cpu,
             "parity": parity,
+            "replica_parity": replica_parity,
             "spill_topics": int(slow_topics),
             "build_s": round(t_build, 2),
             "host_peak_rss_gib": host_rss_gib(),
@@ -732,6 +736,36 @@ def run_churn(args):
         "host_peak_rss_gib": host_rss_gib(),
         "parity": {"sampled_topics": ps, "mismatches": int(bad), "oracle": "oracle/trie_search.cpp"},
     }), flush=True)
+
+
+def replica_check(eng, all_b, all_o, s, dev, backend, sp, world):
+    """Collective: match topics [0, s) of the whole batch on every rank and compare each
+    rank's per-topic (count, sum of a hash of the route ids) with rank 0's."""
+    import torch
+    import torch.distributed as dist
+    d_off = all_o[:s + 1].contiguous()
+    r = eng.match_device(all_b.data_ptr(), d_off.data_ptr(), s, int(all_o[s].item()), sp)
+    eng.device_sync()
+    total = _read_u64(r.d_total)
+    if total > r.keys_cap:
+        raise RuntimeError("replica check: output arena overflow")
+    ids = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+    off = torch.empty(s + 1, dtype=torch.int32, device=dev)
+    eng.result_ids_device(ids.data_ptr(), ids.numel(), off.data_ptr(), sp)
+    eng.device_sync()
+    torch.cuda.synchronize()
+    o = off.long() & 0xFFFFFFFF
+    h = (ids[:total] * 0x9E3779B97F4A7C15) >> 16
+    cs = torch.zeros(total + 1, dtype=torch.int64, device=dev)
+    cs[1:] = torch.cumsum(h, 0)
+    dig = torch.stack([o[1:] - o[:-1], cs[o[1:]] - cs[o[:-1]]])
+    if backend == "gloo":
+        dig = dig.cpu()
+    got = [torch.empty_like(dig) for _ in range(world)]
+    dist.all_gather(got, dig)
+    return {"sampled_topics": s, "ranks": world, "matched_keys": int(o[-1].item()),
+            "ranks_differing_from_master": [i for i, g in enumerate(got) if not torch.equal(g, got[0])],
+            "compared": "per topic: route-id count and the sum of a hash of the ids"}
 
 
 def _read_u64(ptr):
