@@ -49,7 +49,8 @@ def algorithmic_bytes(st, topic_bytes, n):
             + 16 * st["node_records"] + 4 * arena_keys + 4 * st["keys"] + 12 * n)
 
 
-KERNEL_SRCS = ("emqx_amd/csrc/match_kernels.hip", "emqx_amd/csrc/layout.h", "emqx_amd/csrc/device_api.h")
+KERNEL_SRCS = ("emqx_amd/csrc/match_kernels.hip", "emqx_amd/csrc/layout.h", "emqx_amd/csrc/device_api.h",
+               "emqx_amd/csrc/wave.h")
 
 
 def kernel_src_sha():

@@ -22,7 +22,8 @@ def _newer(out, srcs):
 def build(force: bool = False, verbose: bool = True):
     tm = os.path.join(HERE, "libemqx_tm.so")
     srcs = [os.path.join(CSRC, f) for f in ("engine.cpp", "batcher.cpp", "match_kernels.hip",
-                                            "result_kernels.hip", "filter_kernels.hip", "layout.h", "device_api.h", "filter_api.h")]
+                                            "result_kernels.hip", "filter_kernels.hip", "layout.h", "device_api.h", "filter_api.h",
+                                            "wave.h")]
     srcs += [os.path.join(os.path.dirname(HERE), "include", h) for h in ("emqx_tm.h", "emqx_tm_batcher.h")]
     if force or not _newer(tm, srcs):
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",

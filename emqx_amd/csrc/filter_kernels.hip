@@ -17,6 +17,7 @@
 #include <algorithm>
 
 #include "filter_api.h"
+#include "wave.h"
 
 namespace tmx {
 
@@ -181,13 +182,9 @@ __device__ void copy_keys(const uint32_t *src, uint32_t *dst, uint32_t m, uint32
 
 // exclusive prefix sum over the 64 lanes; *total gets the wave sum
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total, uint32_t lane) {
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= (uint32_t)d) x += y;
-    }
-    *total = __shfl(x, 63, 64);
+    (void)lane;
+    const uint32_t x = wave_incl_scan_dpp(v);
+    *total = lane_value(x, 63);
     return x - v;
 }
 
@@ -278,7 +275,7 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             auto probe_from = [&](uint32_t l, uint32_t np, uint32_t w) {
                 Probe pb;
 #pragma unroll
-                for (int i = 0; i < (int)RW; i++) pb.pr[i] = __shfl(fr[i], l);
+                for (int i = 0; i < (int)RW; i++) pb.pr[i] = lane_value(fr[i], l);
                 pb.ks = idx + l;
                 pb.np = np;
                 pb.w = w;
@@ -310,7 +307,7 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             if (a.first && nf) break;
             if (rl < fs) {
                 // the run [rs, E): E = next({first p words of key rs ++ [+inf], {}})
-                const uint32_t rs = idx + rl, p = __shfl(qh, rl);
+                const uint32_t rs = idx + rl, p = lane_value(qh, rl);
                 const uint32_t E = a.first ? rs + 1 : wave_seek(a, rs + 1, probe_from(rl, p, NONE_FW), lane);
                 const uint32_t m = E - rs;
                 if (pass == FW_EMIT) {
@@ -327,11 +324,11 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
                 idx += 64;
                 continue;
             }
-            const int rs = __shfl(r, fs);
+            const int rs = (int)lane_value((uint32_t)r, fs);
             const uint32_t ks = idx + fs;
             if (rs == R_LOWER || ks >= K) break;  // lower, or '$end_of_table'
             // seek/3: next({first spos words of key ks ++ [sword], {}})
-            const uint32_t sp = __shfl(spos, fs), sw = __shfl(sword, fs);
+            const uint32_t sp = lane_value(spos, fs), sw = lane_value(sword, fs);
             idx = wave_seek(a, ks + 1, probe_from(fs, sp, sw), lane);
         }
     }
@@ -376,7 +373,7 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
                 while (wv) {
                     const uint32_t l = (uint32_t)__ffsll((long long)wv) - 1;
                     wv &= wv - 1;
-                    copy_keys(a.kh + __shfl(r.x, l), a.out + __shfl(d, l), __shfl(r.y, l), lane);
+                    copy_keys(a.kh + lane_value(r.x, l), a.out + lane_value(d, l), lane_value(r.y, l), lane);
                 }
             }
             if (cb + CE < nent) ch = pool2[(uint64_t)ch * (FW_CHUNK / 2)].x;  // next chunk

@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include "device_api.h"
+#include "wave.h"
 
 namespace tmx {
 
@@ -91,8 +92,15 @@ constexpr int CP_SHORT = 8;                 // lists up to this long are copied 
 // wave helpers
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (WAVE - 1); }
 
+#ifndef TM_DPP_SCAN
+#define TM_DPP_SCAN 1  // wave scans on DPP lane moves (wave.h) instead of ds_bpermute round trips
+#endif
 // exclusive prefix sum over the 64 lanes; *total gets the wave sum
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
+#if TM_DPP_SCAN
+    const uint32_t x = wave_incl_scan_dpp(v);
+    *total = lane_value(x, WAVE - 1);
+#else
     uint32_t x = v;
     const uint32_t lane = lane_id();
 #pragma unroll
@@ -101,6 +109,7 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total) 
         if (lane >= (uint32_t)d) x += y;
     }
     *total = __shfl(x, WAVE - 1, WAVE);
+#endif
     return x - v;
 }
 
@@ -753,7 +762,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                         if (q1[k] || q2[k]) atomicOr(&L.spill, 1ull << tl[k]);
                 }
             }
-            nnext = ovm ? __shfl(pp, __builtin_ctzll(ovm), WAVE) : nnext + tot_p;
+            nnext = ovm ? __builtin_amdgcn_readlane(pp, __builtin_ctzll(ovm)) : nnext + tot_p;
 #pragma unroll
             for (int k = 0; k < RPL; k++) st_visit += (uint32_t)f1[k] + (uint32_t)f2[k];
         }
@@ -1397,7 +1406,7 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
                         if (q1[k] || q2[k]) atomicOr(&L.spill, 1ull << tl[k]);
                 }
             }
-            nnext = ovm ? __shfl(pp, __builtin_ctzll(ovm), WAVE) : nnext + tot_p;
+            nnext = ovm ? __builtin_amdgcn_readlane(pp, __builtin_ctzll(ovm)) : nnext + tot_p;
             __syncthreads();
         }
         __syncthreads();

@@ -19,6 +19,7 @@
 #include <algorithm>
 
 #include "device_api.h"
+#include "wave.h"
 
 namespace tmx {
 
@@ -31,12 +32,7 @@ constexpr int SCAN_B = SCAN_T * SCAN_V;  // values per scan block
 // Values are counts whose total stays below 2^32 (a batch's key count).
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *sh, uint32_t *total) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= (uint32_t)d) x += y;
-    }
+    const uint32_t x = wave_incl_scan_dpp(v);
     if (lane == 63) sh[wid] = x;
     __syncthreads();
     uint32_t base = 0, tot = 0;
@@ -315,16 +311,12 @@ __global__ __launch_bounds__(64) void k_dd_pass(uint32_t mode, const uint32_t *c
         o = off[t];
         if ((uint64_t)o + c > keys_cap) c = 0;  // overflowed batch: the caller re-runs it
     }
-    uint32_t x = c;  // inclusive scan over the wave
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x += y;
-    }
+    const uint32_t x = wave_incl_scan_dpp(c);  // inclusive scan over the wave
     s_start[lane + 1] = x;
     if (lane == 0) s_start[0] = 0;
     s_off[lane] = o;
     s_nflag[lane] = 0;
-    const uint32_t total = __shfl(x, 63);
+    const uint32_t total = lane_value(x, 63);
     __syncthreads();
     const uint8_t bit = dd_bit(mode);
     // the 64 topics' lists as one sequence, 64 * DDP_U keys per round; a lane's key index

@@ -9,7 +9,7 @@ ARGS="--profile --steps 4 --warmup 1 $*"
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 # which kernel source these counters belong to (bench.py only reports a matching profile)
-sha256sum emqx_amd/csrc/match_kernels.hip emqx_amd/csrc/layout.h emqx_amd/csrc/device_api.h > "$OUT/src.sha"
+sha256sum emqx_amd/csrc/match_kernels.hip emqx_amd/csrc/layout.h emqx_amd/csrc/device_api.h emqx_amd/csrc/wave.h > "$OUT/src.sha"
 run() {  # name, rocprof args...
   local name=$1; shift
   timeout -s KILL 240 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o "$name" -- \

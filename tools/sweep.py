@@ -33,6 +33,7 @@ VARIANTS = {
     "base": ([], 0),
     "base2": ([], 0),  # the same build again: run-to-run noise and the digest's self-check
     "nopre": (["-DTM_PRELOOK=0"], 0),
+    "nodpp": (["-DTM_DPP_SCAN=0"], 0),
     "tb2560_f448": (["-DTM_TBCAP=2560", "-DTM_FCAP=448"], 0),
     "tb2048_f512": (["-DTM_TBCAP=2048", "-DTM_FCAP=512"], 0),
     "tb2304_f480": (["-DTM_TBCAP=2304", "-DTM_FCAP=480"], 0),
