@@ -49,11 +49,10 @@ struct Probe {
     uint32_t ks, np, w;
 };
 
-// key j vs the probe: -1 / 0 / 1.  One record load: the compare is one round trip unless
-// the prefix is longer than the record.
-__device__ inline int cmp_key_seek(const FilterArgs &a, uint32_t j, const Probe &pb) {
-    uint32_t kr[RW];
-    const uint32_t L = load_rec(a, j, kr);
+// key j (its record kr, length L already in registers) vs the probe: -1 / 0 / 1.  Memory
+// is read only when the prefix is longer than the record.
+__device__ inline int cmp_rec_probe(const FilterArgs &a, uint32_t j, const uint32_t (&kr)[RW], uint32_t L,
+                                    const Probe &pb) {
     uint32_t xn = 0;  // the key's word at position np (when np < RW)
 #pragma unroll
     for (int i = 0; i < (int)RW; i++) {
@@ -74,6 +73,13 @@ __device__ inline int cmp_key_seek(const FilterArgs &a, uint32_t j, const Probe 
     const uint32_t x = pb.np < RW ? xn : a.kw[a.koff[j] + pb.np];
     if (x != pb.w) return x < pb.w ? -1 : 1;
     return L == pb.np + 1 ? 0 : 1;
+}
+
+// key j vs the probe: one record load (a round trip), then the compare in registers
+__device__ inline int cmp_key_seek(const FilterArgs &a, uint32_t j, const Probe &pb) {
+    uint32_t kr[RW];
+    const uint32_t L = load_rec(a, j, kr);
+    return cmp_rec_probe(a, j, kr, L, pb);
 }
 
 // next(probe) among keys [lo, K): the first key >= the probe, found by the whole
@@ -267,10 +273,21 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             int r = R_LOWER;  // past the end of the table: the walk stops there
             uint32_t spos = 0, sword = 0, qh = NONE_FW;
             uint32_t fr[RW] = {};
-            if (j < K && j >= idx) {
-                const uint32_t FL = load_rec(a, j, fr);
+            uint32_t FL = 0;
+            const bool inr = j < K && j >= idx;
+            if (inr) {
+                FL = load_rec(a, j, fr);
                 r = cmp_filter(fr, a, j, FL, wr, W, WL, spos, sword, qh);
             }
+            // next(probe) from key lo = idx + from + 1: the lanes past `from` already hold
+            // their records, so a target inside this window costs no memory round trip;
+            // past it, the wave searches from idx + 64 (keys past K count as the end)
+            auto seek_from = [&](uint32_t from, const Probe &pb) -> uint32_t {
+                const bool ge = lane > from && (!inr || cmp_rec_probe(a, j, fr, FL, pb) >= 0);
+                const uint64_t gm = __ballot(ge);
+                if (gm) return min(idx + (uint32_t)__ffsll((long long)gm) - 1, K);
+                return wave_seek(a, idx + 64, pb, lane);
+            };
             // the probe of a seek or run end from lane l: key idx+l's record words, no loads
             auto probe_from = [&](uint32_t l, uint32_t np, uint32_t w) {
                 Probe pb;
@@ -308,7 +325,7 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             if (rl < fs) {
                 // the run [rs, E): E = next({first p words of key rs ++ [+inf], {}})
                 const uint32_t rs = idx + rl, p = lane_value(qh, rl);
-                const uint32_t E = a.first ? rs + 1 : wave_seek(a, rs + 1, probe_from(rl, p, NONE_FW), lane);
+                const uint32_t E = a.first ? rs + 1 : seek_from(rl, probe_from(rl, p, NONE_FW));
                 const uint32_t m = E - rs;
                 if (pass == FW_EMIT) {
                     copy_keys(a.kh + rs, out + c, m, lane);
@@ -329,7 +346,7 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             if (rs == R_LOWER || ks >= K) break;  // lower, or '$end_of_table'
             // seek/3: next({first spos words of key ks ++ [sword], {}})
             const uint32_t sp = lane_value(spos, fs), sw = lane_value(sword, fs);
-            idx = wave_seek(a, ks + 1, probe_from(fs, sp, sw), lane);
+            idx = seek_from(fs, probe_from(fs, sp, sw));
         }
     }
     if (pass == FW_COUNT && lane == 0) a.cnt[q] = c;

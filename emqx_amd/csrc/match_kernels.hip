@@ -34,7 +34,7 @@ namespace tmx {
 
 constexpr int WAVE = 64;
 #ifndef TM_FCAP
-#define TM_FCAP 448  // 256 -> 448 with the topic stage at 2.5 KiB: fewer frontier overflows to HBM chunks at 14 waves/CU (0.889 -> 0.848 ms)
+#define TM_FCAP 384  // with a 2 KiB topic stage: 10,016 B of LDS per wave, 16 waves/CU (the VGPR limit too); 448 / 2.5 KiB (14 waves) was best before the DPP scans
 #endif
 constexpr int FCAP = TM_FCAP;    // frontier entries per wave per depth held in LDS
 constexpr int FCH = FR_CHUNK;    // frontier entries per global overflow chunk
@@ -43,7 +43,7 @@ constexpr int MAXF = 32;         // overflow chunks per frontier buffer per wave
 #define TM_SCAP 128
 #endif
 #ifndef TM_TBCAP
-#define TM_TBCAP 2560
+#define TM_TBCAP 2048
 #endif
 #ifndef TM_MIN_WAVES
 #define TM_MIN_WAVES 1
@@ -92,6 +92,9 @@ constexpr int CP_SHORT = 8;                 // lists up to this long are copied 
 // wave helpers
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (WAVE - 1); }
 
+#ifndef TM_ALIVE_REG
+#define TM_ALIVE_REG 1  // k_match_fast: topics alive at this / the next depth in registers (DPP OR) not LDS atomics
+#endif
 #ifndef TM_DPP_SCAN
 #define TM_DPP_SCAN 1  // wave scans on DPP lane moves (wave.h) instead of ds_bpermute round trips
 #endif
@@ -500,6 +503,9 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     const RootRec R = *a.root;
     if (walk) level_word(0, 0);  // level 0
     uint32_t nseg = 0, nchunk = 0;  // wave-uniform
+#if TM_ALIVE_REG
+    unsigned long long alive_c = 0;  // wave-uniform: topics with frontier entries at this depth
+#endif
     uint32_t nfr;
     {
         const bool em = walk && !dollar && R.hash_cnt;
@@ -515,6 +521,9 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
         const uint32_t m = walk ? probes_needed(rinfo, R.bloom, L.wid[0][lane]) : 0u;
         const unsigned long long al0 = __ballot(m != 0);
         if (lane == 0) L.alive[0] = al0;
+#if TM_ALIVE_REG
+        alive_c = al0;
+#endif
         const uint32_t p2 = wave_excl_scan(m ? 1u : 0u, &tot);
         if (m) {
             L.fr_node[0][p2] = ROOT_ID;
@@ -555,8 +564,13 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
         const uint32_t cur = d & 1, nxt = cur ^ 1;
         // 3a. tokenise level d+1 ahead for topics that are still alive and go deeper:
         //     the children pushed at this depth are filtered with it (bloom)
+#if TM_ALIVE_REG
+        if (walk && ((alive_c >> lane) & 1ull) && d + 1 < nl) level_word(nxt, d + 1);
+        unsigned long long alive_n = 0;  // wave-uniform
+#else
         if (walk && ((L.alive[cur] >> lane) & 1ull) && d + 1 < nl) level_word(nxt, d + 1);
         if (lane == 0) L.alive[nxt] = 0;
+#endif
         __syncthreads();
         // 3b. expand the frontier, WAVE * RPL entries per round (RPL per lane, so each
         //     lane has up to 2 * RPL independent probes in flight)
@@ -754,7 +768,9 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                     for (int k = 0; k < RPL; k++) {
                         if (q1[k]) fr_write(nxt, pp++, r1[k].child, tl[k] | q1[k]);
                         if (q2[k]) fr_write(nxt, pp++, r2[k].child, tl[k] | q2[k]);
+#if !TM_ALIVE_REG
                         if (q1[k] || q2[k]) atomicOr(&L.alive[nxt], 1ull << tl[k]);
+#endif
                     }
                 } else {
 #pragma unroll
@@ -763,11 +779,25 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                 }
             }
             nnext = ovm ? __builtin_amdgcn_readlane(pp, __builtin_ctzll(ovm)) : nnext + tot_p;
+#if TM_ALIVE_REG
+            {
+                unsigned long long my = 0;
+                if (np && !ovf) {
+#pragma unroll
+                    for (int k = 0; k < RPL; k++)
+                        if (q1[k] || q2[k]) my |= 1ull << tl[k];
+                }
+                alive_n |= wave_or64_dpp(my);
+            }
+#endif
 #pragma unroll
             for (int k = 0; k < RPL; k++) st_visit += (uint32_t)f1[k] + (uint32_t)f2[k];
         }
         __syncthreads();
         nfr = nnext;
+#if TM_ALIVE_REG
+        alive_c = alive_n;
+#endif
     }
 
     if constexpr (STATS) ts2 = __builtin_amdgcn_s_memtime();

@@ -19,6 +19,20 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t x) {
     return x;
 }
 
+// OR of x over the 64 lanes (the same DPP moves; the result is read from lane 63)
+__device__ __forceinline__ uint32_t wave_or_dpp(uint32_t x) {
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);
+    x |= __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);
+    return __builtin_amdgcn_readlane(x, 63);
+}
+__device__ __forceinline__ uint64_t wave_or64_dpp(uint64_t x) {
+    return ((uint64_t)wave_or_dpp((uint32_t)(x >> 32)) << 32) | wave_or_dpp((uint32_t)x);
+}
+
 // value of x in lane l (l wave-uniform): v_readlane, no LDS
 __device__ __forceinline__ uint32_t lane_value(uint32_t x, uint32_t l) { return __builtin_amdgcn_readlane(x, l); }
 

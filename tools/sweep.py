@@ -34,6 +34,15 @@ VARIANTS = {
     "base2": ([], 0),  # the same build again: run-to-run noise and the digest's self-check
     "nopre": (["-DTM_PRELOOK=0"], 0),
     "nodpp": (["-DTM_DPP_SCAN=0"], 0),
+    "alive": (["-DTM_ALIVE_REG=1"], 0),
+    "rpl3": (["-DTM_RPL=3"], 0),
+    "tb2048_f384": (["-DTM_TBCAP=2048", "-DTM_FCAP=384"], 0),
+    "tb2048_f352": (["-DTM_TBCAP=2048", "-DTM_FCAP=352"], 0),
+    "alive_tb2048_f384": (["-DTM_ALIVE_REG=1", "-DTM_TBCAP=2048", "-DTM_FCAP=384"], 0),
+    "w20": (["-DTM_TBCAP=1536", "-DTM_FCAP=320", "-DTM_SCAP=96", "-DTM_MIN_WAVES=5"], 0),
+    "f416": (["-DTM_FCAP=416"], 0),
+    "s96": (["-DTM_SCAP=96"], 0),
+    "noalive": (["-DTM_ALIVE_REG=0"], 0),
     "tb2560_f448": (["-DTM_TBCAP=2560", "-DTM_FCAP=448"], 0),
     "tb2048_f512": (["-DTM_TBCAP=2048", "-DTM_FCAP=512"], 0),
     "tb2304_f480": (["-DTM_TBCAP=2304", "-DTM_FCAP=480"], 0),
