@@ -83,10 +83,18 @@ class ReplicatedIndex:
             return torch.device("cpu")
         return self.ad.tensor_device()
 
+    CHUNK = 1 << 30  # bytes per broadcast call: a 20 GiB image goes as 1 GiB pieces
+
     def _bcast(self, t):
         import torch.distributed as dist
         if self.world > 1:
-            dist.broadcast(t, src=0, group=self.group)
+            flat = t.view(-1)
+            if flat.numel() * flat.element_size() <= self.CHUNK:
+                dist.broadcast(t, src=0, group=self.group)
+            else:  # keep every collective's element count well inside 32 bits
+                step = self.CHUNK // flat.element_size()
+                for i in range(0, flat.numel(), step):
+                    dist.broadcast(flat[i:i + step], src=0, group=self.group)
         return t
 
     def _send_image(self):

@@ -77,8 +77,10 @@ class FakeAdapter:
         return [ids[o[t]:o[t + 1]].tolist() for t in range(len(topics))]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, chunk=0):
     import torch.distributed as dist
+    if chunk:
+        ReplicatedIndex.CHUNK = chunk  # images and patches cross in many pieces
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -110,12 +112,15 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_replicated_gloo_world2_protocol():
+@pytest.mark.parametrize("chunk", [0, 64])
+def test_replicated_gloo_world2_protocol(chunk):
+    """chunk 64: every broadcast larger than 64 bytes goes as 64-byte pieces, the path a
+    20 GiB image takes in 1 GiB pieces."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, chunk)) for r in range(2)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=240) for _ in ps], key=lambda r: r[0])
