@@ -43,6 +43,12 @@ VARIANTS = {
     "f416": (["-DTM_FCAP=416"], 0),
     "s96": (["-DTM_SCAP=96"], 0),
     "noalive": (["-DTM_ALIVE_REG=0"], 0),
+    "rpl1": (["-DTM_RPL=1"], 0),
+    "cpu4": (["-DTM_CP_UNROLL=4"], 0),
+    "cpu16": (["-DTM_CP_UNROLL=16"], 0),
+    "qcopy16": (["-DTM_QCOPY=16"], 0),
+    "qcopy4": (["-DTM_QCOPY=4"], 0),
+    "el32": ([], 32),
     "tb2560_f448": (["-DTM_TBCAP=2560", "-DTM_FCAP=448"], 0),
     "tb2048_f512": (["-DTM_TBCAP=2048", "-DTM_FCAP=512"], 0),
     "tb2304_f480": (["-DTM_TBCAP=2304", "-DTM_FCAP=480"], 0),
