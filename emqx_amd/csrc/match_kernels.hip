@@ -1098,11 +1098,15 @@ __global__ __launch_bounds__(WAVE) void k_first_slow(MatchArgs a) {
     }
 }
 
+#ifndef TM_FCAP_FIRST
+#define TM_FCAP_FIRST 256  // k_match_first_wave's frontier entries per depth in LDS (13 B each: node, code, meta); 256: 10,776 B, 15 waves/CU (0.567 -> 0.509 ms vs 384)
+#endif
+constexpr int FCAP_F = TM_FCAP_FIRST;
 struct FirstLds {
     uint8_t tb[TBCAP];
-    uint32_t fr_node[2][FCAP];
-    uint64_t fr_ord[2][FCAP];      // code prefix of the entry's path (levels < depth)
-    uint8_t fr_meta[2][FCAP];      // topic lane | DO_PLUS / DO_LIT
+    uint32_t fr_node[2][FCAP_F];
+    uint64_t fr_ord[2][FCAP_F];      // code prefix of the entry's path (levels < depth)
+    uint8_t fr_meta[2][FCAP_F];      // topic lane | DO_PLUS / DO_LIT
     uint32_t fch[2][MAXF];         // overflow chunks (uint4 entries {node, meta, ord lo, ord hi})
     uint32_t wid[2][WAVE];
     uint32_t nlev[WAVE];
@@ -1202,6 +1206,9 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
     const RootRec R = *a.root;
     if (walk) level_word(0, 0);
     uint32_t nfr;
+#if TM_ALIVE_REG
+    unsigned long long alive_c = 0;  // wave-uniform: topics with frontier entries at this depth
+#endif
     {
         const bool rh = walk && !dollar && R.hash_cnt;
         if (rh) {
@@ -1212,6 +1219,9 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
         const uint32_t m = (walk && !rh) ? probes_needed(rinfo, R.bloom, L.wid[0][lane]) : 0u;
         const unsigned long long al0 = __ballot(m != 0);
         if (lane == 0) L.alive[0] = al0;
+#if TM_ALIVE_REG
+        alive_c = al0;
+#endif
         uint32_t tot;
         const uint32_t p2 = wave_excl_scan(m ? 1u : 0u, &tot);
         if (m) {
@@ -1225,12 +1235,12 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
 
     uint32_t nfch[2] = {0, 0};
     auto fr_read = [&](uint32_t lvl, uint32_t i, uint32_t &node, uint32_t &meta, uint64_t &ord) {
-        if (i < (uint32_t)FCAP) {
+        if (i < (uint32_t)FCAP_F) {
             node = L.fr_node[lvl][i];
             meta = L.fr_meta[lvl][i];
             ord = L.fr_ord[lvl][i];
         } else {
-            const uint32_t k = i - FCAP;
+            const uint32_t k = i - FCAP_F;
             const uint4 v = pool4[(uint64_t)L.fch[lvl][k / FCH4] * FCH4 + k % FCH4];
             node = v.x;
             meta = v.y;
@@ -1238,12 +1248,12 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
         }
     };
     auto fr_write = [&](uint32_t lvl, uint32_t i, uint32_t node, uint32_t meta, uint64_t ord) {
-        if (i < (uint32_t)FCAP) {
+        if (i < (uint32_t)FCAP_F) {
             L.fr_node[lvl][i] = node;
             L.fr_meta[lvl][i] = (uint8_t)meta;
             L.fr_ord[lvl][i] = ord;
         } else {
-            const uint32_t k = i - FCAP;
+            const uint32_t k = i - FCAP_F;
             pool4[(uint64_t)L.fch[lvl][k / FCH4] * FCH4 + k % FCH4] =
                 make_uint4(node, meta, (uint32_t)ord, (uint32_t)(ord >> 32));
         }
@@ -1255,8 +1265,13 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
     constexpr uint64_t ALL_LIT = (1ull << 62) - 1;
     for (uint32_t d = 0; nfr > 0; ++d) {
         const uint32_t cur = d & 1, nxt = cur ^ 1;
+#if TM_ALIVE_REG
+        if (walk && ((alive_c >> lane) & 1ull) && d + 1 < nl) level_word(nxt, d + 1);
+        unsigned long long alive_n = 0;  // wave-uniform
+#else
         if (walk && ((L.alive[cur] >> lane) & 1ull) && d + 1 < nl) level_word(nxt, d + 1);
         if (lane == 0) L.alive[nxt] = 0;
+#endif
         __syncthreads();
         uint32_t nnext = 0;
         // a child at depth d+1 adds its level-d symbol ('+' 2, literal 3) at bit sh; its '#'
@@ -1408,16 +1423,16 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
             }
             uint32_t tot_p;
             uint32_t pp = nnext + wave_excl_scan(np, &tot_p);
-            uint32_t cap = FCAP + nfch[nxt] * FCH4;
+            uint32_t cap = FCAP_F + nfch[nxt] * FCH4;
             if (nnext + tot_p > cap && nfch[nxt] < (uint32_t)MAXF) {
-                const uint32_t want = min((nnext + tot_p - FCAP + FCH4 - 1) / FCH4, (uint32_t)MAXF) - nfch[nxt];
+                const uint32_t want = min((nnext + tot_p - FCAP_F + FCH4 - 1) / FCH4, (uint32_t)MAXF) - nfch[nxt];
                 unsigned long long c0 = 0;
                 if (lane == 0) c0 = atomicAdd(a.fr_cursor, (unsigned long long)want);
                 c0 = __shfl(c0, 0, WAVE);
                 const uint32_t got = c0 >= a.fr_chunks ? 0u : (uint32_t)min((unsigned long long)want, a.fr_chunks - c0);
                 if (lane < got) L.fch[nxt][nfch[nxt] + lane] = (uint32_t)(c0 + lane);
                 nfch[nxt] += got;
-                cap = FCAP + nfch[nxt] * FCH4;
+                cap = FCAP_F + nfch[nxt] * FCH4;
                 __syncthreads();
             }
             const bool ovf = np && pp + np > cap;
@@ -1428,7 +1443,9 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
                     for (int k = 0; k < RPL; k++) {
                         if (q1[k]) fr_write(nxt, pp++, r1[k].child, tl[k] | q1[k], P1[k]);
                         if (q2[k]) fr_write(nxt, pp++, r2[k].child, tl[k] | q2[k], P2[k]);
+#if !TM_ALIVE_REG
                         if (q1[k] || q2[k]) atomicOr(&L.alive[nxt], 1ull << tl[k]);
+#endif
                     }
                 } else {
 #pragma unroll
@@ -1437,10 +1454,24 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
                 }
             }
             nnext = ovm ? __builtin_amdgcn_readlane(pp, __builtin_ctzll(ovm)) : nnext + tot_p;
+#if TM_ALIVE_REG
+            {
+                unsigned long long my = 0;
+                if (np && !ovf) {
+#pragma unroll
+                    for (int k = 0; k < RPL; k++)
+                        if (q1[k] || q2[k]) my |= 1ull << tl[k];
+                }
+                alive_n |= wave_or64_dpp(my);
+            }
+#endif
             __syncthreads();
         }
         __syncthreads();
         nfr = nnext;
+#if TM_ALIVE_REG
+        alive_c = alive_n;
+#endif
     }
 
     // ---- results: the winner's handle (one more read for a '#' list), or the DFS for spills

@@ -44,6 +44,9 @@ VARIANTS = {
     "s96": (["-DTM_SCAP=96"], 0),
     "noalive": (["-DTM_ALIVE_REG=0"], 0),
     "rpl1": (["-DTM_RPL=1"], 0),
+    "ff256": (["-DTM_FCAP_FIRST=256"], 0),
+    "ff192": (["-DTM_FCAP_FIRST=192"], 0),
+    "noalive_first": (["-DTM_ALIVE_REG=0"], 0),
     "cpu4": (["-DTM_CP_UNROLL=4"], 0),
     "cpu16": (["-DTM_CP_UNROLL=16"], 0),
     "qcopy16": (["-DTM_QCOPY=16"], 0),
@@ -113,6 +116,8 @@ def run(args):
         sp = stream.cuda_stream
 
         def step():
+            if args.mode == "first":  # return_first (k_match_first_wave)
+                return eng.match_device_mode(d_bytes.data_ptr(), d_off.data_ptr(), n, int(to[-1]), N.TM_MATCH_FIRST, sp)
             return eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, int(to[-1]), sp)
 
         r = step()
@@ -128,7 +133,7 @@ def run(args):
         r = step()  # this launch's result (reserve_matches above re-allocated the key arena)
         torch.cuda.synchronize()
         walk = dict(zip(N.Engine.STAT_NAMES, [int(x) for x in eng.debug_stats(False)]))
-        digest = _topic_digest(eng, r, n, _read_u64(r.d_total), sp)
+        digest = _topic_digest(eng, r, n, _read_u64(r.d_total), sp) if args.mode == "all" else None
         eng.debug_stats(False, read=False)
         kms = []
         for _ in range(args.steps):
@@ -147,9 +152,10 @@ def run(args):
                "batch_ms": round(bms, 4), "keys": walk["keys"], "edge_probes": walk["edge_probes"],
                "word_probes": walk["word_probes"], "edge_slots": st["edge_slots"], "build_s": round(tbuild, 1),
                "cyc": [walk["cyc_prescan"], walk["cyc_walk"], walk["cyc_copyout"]]}
-        if digests:
-            rec["same_keys_per_topic"] = bool(torch.equal(digest, digests[0]))
-        digests.append(digest)
+        if digest is not None:
+            if digests:
+                rec["same_keys_per_topic"] = bool(torch.equal(digest, digests[0]))
+            digests.append(digest)
         print(json.dumps(rec), flush=True)
         results.append(rec)
         eng.close()
@@ -195,6 +201,7 @@ if __name__ == "__main__":
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--batch", type=int, default=1_000_000)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--mode", choices=("all", "first"), default="all")
     a = ap.parse_args()
     if a.cmd == "build":
         build(a.variants)
