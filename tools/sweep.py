@@ -44,6 +44,10 @@ VARIANTS = {
     "s96": (["-DTM_SCAP=96"], 0),
     "noalive": (["-DTM_ALIVE_REG=0"], 0),
     "rpl1": (["-DTM_RPL=1"], 0),
+    "r1p4_f256s96": (["-DTM_RPL=1", "-DTM_PRELOOK=4", "-DTM_FCAP=256", "-DTM_SCAP=96"], 0),
+    "r1p6_f256s96": (["-DTM_RPL=1", "-DTM_PRELOOK=6", "-DTM_FCAP=256", "-DTM_SCAP=96"], 0),
+    "r1p4_f192s64": (["-DTM_RPL=1", "-DTM_PRELOOK=4", "-DTM_FCAP=192", "-DTM_SCAP=64"], 0),
+    "r1p10": (["-DTM_RPL=1", "-DTM_PRELOOK=10"], 0),
     "ff256": (["-DTM_FCAP_FIRST=256"], 0),
     "ff192": (["-DTM_FCAP_FIRST=192"], 0),
     "noalive_first": (["-DTM_ALIVE_REG=0"], 0),
