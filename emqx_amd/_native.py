@@ -61,6 +61,7 @@ EXPORTS = (
     "tm_result_ids_device", "tm_merge_shards_device", "tm_merge_shards", "tm_match_device_mode",
     "tm_match_filter_batch", "tm_intersect_batch", "tm_result_ids_device_ex", "tm_image_size", "tm_image_export",
     "tm_replica_create", "tm_replica_load", "tm_patch_size", "tm_patch_export", "tm_replica_apply_patch",
+    "tm_discard_staged", "tm_result_release", "tm_match_batch_runs", "tm_runs_release",
 )
 # every symbol include/emqx_tm_batcher.h declares
 BATCHER_EXPORTS = (
@@ -75,7 +76,7 @@ class tm_config(C.Structure):
         ("reserve_keys", C.c_uint32), ("reserve_nodes", C.c_uint32),
         ("reserve_topics", C.c_uint32), ("reserve_matches", C.c_uint32),
         ("seg_chunks", C.c_uint32), ("edge_load_inv", C.c_uint32),
-        ("topics_per_wave", C.c_uint32), ("reserved", C.c_uint32 * 1),
+        ("topics_per_wave", C.c_uint32), ("max_nodes", C.c_uint32), ("max_list_words", C.c_uint32),
     ]
 
 
@@ -116,7 +117,18 @@ class tm_stats_t(C.Structure):
         "epoch", "n_keys", "n_nodes", "n_words", "edge_slots", "word_slots", "list_words",
         "device_bytes", "n_full_rebuilds", "n_delta_commits", "n_slow_topics",
         "commit_apply_us", "commit_lists_us", "commit_upload_us", "n_deep_keys", "n_filter_onepass",
-        "n_filter_twopass")]
+        "n_filter_twopass", "commit_stall_us", "n_commits_refused", "n_staged")]
+
+
+class tm_span(C.Structure):
+    _fields_ = [("ids", C.c_void_p), ("n", C.c_uint64)]
+
+
+class tm_runs_result(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("_pad", C.c_uint32), ("epoch", C.c_uint64), ("total_ids", C.c_uint64),
+                ("total_spans", C.c_uint64), ("span_off", C.POINTER(C.c_uint32)), ("span_cnt", C.POINTER(C.c_uint32)),
+                ("spans", C.POINTER(tm_span)),
+                ("kcnt", C.POINTER(C.c_uint32)), ("status", C.POINTER(C.c_int32))]
 
 
 class tm_batcher_config(C.Structure):
@@ -163,6 +175,10 @@ def load() -> C.CDLL:
     lib.tm_apply_packed.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_size_t]
     lib.tm_commit_epoch.argtypes = [C.c_void_p, P(C.c_uint64)]
+    lib.tm_discard_staged.argtypes = [C.c_void_p, P(C.c_uint64)]
+    lib.tm_result_release.argtypes = [C.c_void_p]
+    lib.tm_match_batch_runs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, P(tm_runs_result)]
+    lib.tm_runs_release.argtypes = [C.c_void_p]
     lib.tm_match_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, P(tm_result)]
     lib.tm_intersect_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                        P(tm_intersect_result)]
@@ -255,7 +271,8 @@ class Engine:
 
     def __init__(self, device: int = 0, *, force_slow: bool = False, reserve_keys: int = 0,
                  reserve_nodes: int = 0, reserve_matches: int = 0, seg_chunks: int = 0, edge_load_inv: int = 0,
-                 topics_per_wave: int = 0, record_patch: bool = False, _image=None):
+                 topics_per_wave: int = 0, record_patch: bool = False, max_nodes: int = 0,
+                 max_list_words: int = 0, _image=None):
         self.lib = load()
         cfg = tm_config()
         cfg.device = device
@@ -265,6 +282,8 @@ class Engine:
         cfg.reserve_matches = reserve_matches
         cfg.seg_chunks = seg_chunks
         cfg.topics_per_wave = topics_per_wave
+        cfg.max_nodes = max_nodes
+        cfg.max_list_words = max_list_words
         cfg.edge_load_inv = edge_load_inv or int(os.environ.get("EMQX_TM_EDGE_LOAD_INV", "0"))
         h = C.c_void_p()
         if _image is None:
@@ -361,6 +380,16 @@ class Engine:
         self._check(self.lib.tm_commit_epoch(self.h, C.byref(ep)))
         return ep.value
 
+    def discard_staged(self) -> int:
+        """Drop every staged op (tm_discard_staged); returns how many."""
+        n = C.c_uint64()
+        self._check(self.lib.tm_discard_staged(self.h, C.byref(n)))
+        return n.value
+
+    def result_release(self):
+        """Free this thread's host result buffers (tm_result_release)."""
+        self._check(self.lib.tm_result_release(self.h))
+
     # ---- reads
     def match_packed(self, buf: np.ndarray, off: np.ndarray, mode: int = TM_MATCH_ALL):
         """Match a packed batch; returns (off, cnt, keys, status) numpy copies."""
@@ -447,6 +476,44 @@ class Engine:
         self._check(self.lib.tm_match_batch(self.h, buf.ctypes.data, off.ctypes.data, len(off) - 1, mode,
                                             C.byref(res)))
         return res
+
+    def match_runs_view(self, buf: np.ndarray, off: np.ndarray) -> tm_runs_result:
+        """tm_match_batch_runs without copying: spans into the engine's host id arena, under this
+        thread's read lease until its next runs call or runs_release()."""
+        res = tm_runs_result()
+        self._check(self.lib.tm_match_batch_runs(self.h, buf.ctypes.data, off.ctypes.data, len(off) - 1,
+                                                 C.byref(res)))
+        return res
+
+    def match_runs(self, buf: np.ndarray, off: np.ndarray):
+        """tm_match_batch_runs, expanded: (off u32[n+1], ids u64, kcnt u32[n], status i32[n]).
+        Topic i's ids are ids[off[i]:off[i+1]] (the multiset tm_match_batch + key ids gives)."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        n = len(off) - 1
+        res = self.match_runs_view(buf, off)
+        try:
+            if n == 0:
+                return np.zeros(1, np.uint32), np.zeros(0, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.int32)
+            kcnt = np.ctypeslib.as_array(res.kcnt, shape=(n,)).copy()
+            st = np.ctypeslib.as_array(res.status, shape=(n,)).copy()
+            soff = np.ctypeslib.as_array(res.span_off, shape=(n,)).copy()
+            scnt = np.ctypeslib.as_array(res.span_cnt, shape=(n,)).copy()
+            ids = np.zeros(int(res.total_ids), dtype=np.uint64)
+            o = np.zeros(n + 1, dtype=np.uint32)
+            np.cumsum(kcnt, out=o[1:])
+            for i in range(n):
+                at = int(o[i])
+                for j in range(int(soff[i]), int(soff[i]) + int(scnt[i])):
+                    sp = res.spans[j]
+                    k = int(sp.n)
+                    if k:
+                        ids[at:at + k] = np.ctypeslib.as_array(C.cast(sp.ids, C.POINTER(C.c_uint64)), shape=(k,))
+                    at += k
+                assert at == int(o[i + 1]), "spans of a topic disagree with its id count"
+            return o, ids, kcnt, st
+        finally:
+            self._check(self.lib.tm_runs_release(self.h))
 
     def match(self, topics, mode: int = TM_MATCH_ALL):
         """List of topics -> list of key-handle lists (None for badarg topics)."""

@@ -44,6 +44,8 @@ extern "C" int tmx_engine_grow_pools(tm_engine *eng, uint64_t seg_demand, uint64
 extern "C" void tmx_engine_pool_caps(const tm_engine *eng, uint64_t *seg_chunks, uint64_t *fr_chunks);
 extern "C" int tmx_result_ids32_device(tm_engine *eng, uint32_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
                                        void *stream);
+extern "C" void tmx_engine_lock(tm_engine *eng);
+extern "C" void tmx_engine_unlock(tm_engine *eng);
 
 namespace {
 
@@ -188,7 +190,7 @@ struct tm_batcher {
     std::atomic<bool> stopping{false};
     std::atomic<uint32_t> cutter_idle{0};  // 1 while the cutter sleeps on an empty queue
 
-    std::mutex eng_mu;  // engine calls: enqueue of a window vs tm_batcher_apply / commit
+    std::mutex eng_mu;  // the cutter's enqueue vs a re-run from the completion thread
     hipStream_t s_comp = nullptr, s_copy = nullptr;
     int device = 0;
 
@@ -306,8 +308,16 @@ struct tm_batcher {
     }
 
     // ------------------------------------------------------------------ engine backend
-    // Queue window S's GPU part on the compute stream.  Caller holds eng_mu.
+    // Queue window S's GPU part on the compute stream.  Caller holds eng_mu.  The engine's
+    // device lock is held across the whole sequence, so no other caller's batch (a direct
+    // tm_match_device on the same engine) lands between the walk and the reads of its result.
     int enqueue(Slot &S) {
+        tmx_engine_lock(eng);
+        const int rc = enqueue_locked(S);
+        tmx_engine_unlock(eng);
+        return rc;
+    }
+    int enqueue_locked(Slot &S) {
         const uint32_t n = S.n;
         S.host_done = false;
         BT_HIP(hipSetDevice(device));
@@ -818,19 +828,19 @@ int tm_batcher_match(tm_batcher *b, const uint8_t *topic, uint32_t len, uint64_t
     return w.status < 0 ? w.status : TM_OK;
 }
 
+// The engine is safe under concurrent callers (include/emqx_tm.h "Threading"): writes go
+// straight to it, and its commit publishes only between the windows' device work (the
+// windows already queued finish on the old epoch; the next one sees the new).  These two are
+// kept for callers that hold only the batcher.
 int tm_batcher_apply(tm_batcher *b, const tm_op *ops, size_t n) {
     if (!b) return TM_EINVAL;
     if (!b->eng) return TM_ESTATE;
-    std::lock_guard<std::mutex> g(b->eng_mu);
     return tm_apply(b->eng, ops, n);
 }
 
 int tm_batcher_commit(tm_batcher *b, uint64_t *epoch_out) {
     if (!b) return TM_EINVAL;
     if (!b->eng) return TM_ESTATE;
-    std::lock_guard<std::mutex> g(b->eng_mu);
-    // windows already queued on the GPU finish on the old epoch; the next one sees the new
-    if (hipSetDevice(b->device) != hipSuccess || hipStreamSynchronize(b->s_comp) != hipSuccess) return TM_EDEVICE;
     return tm_commit_epoch(b->eng, epoch_out);
 }
 

@@ -9,6 +9,11 @@
 namespace tmx {
 
 constexpr uint32_t MODE_ALL = 0, MODE_COUNT = 1, MODE_FIRST = 2;  // MatchArgs.mode
+// MODE_RUNS: instead of copying keys, every key segment the walk found (a run of consecutive
+// arena keys, or one inline key) is written as a host span {const uint64_t *ids, uint64_t n}
+// (include/emqx_tm.h tm_span): keys points at uint4 spans, keys_cap counts spans, cursor
+// counts spans, out_cnt[t] = topic t's spans, out_kcnt[t] = its keys.
+constexpr uint32_t MODE_RUNS = 3;
 constexpr int SEG_CHUNK = 128;  // key segments per global chunk (16 B each)
 constexpr int SEG_MAXCHUNK = 128;  // segment chunks one wave may flush (its list lives in HBM)
 constexpr int FR_CHUNK = 256;   // frontier entries per global overflow chunk (8 B each)
@@ -45,6 +50,10 @@ struct MatchArgs {
     int32_t *status;
     uint32_t *keys;
     uint64_t keys_cap;
+    // MODE_RUNS
+    uint32_t *out_kcnt;
+    uint64_t span_arena;  // host address of the id arena: an arena run at src spans span_arena + 8 * src
+    uint64_t span_keys;   // host address of key handle 0's id: key h's id is at span_keys + 16 * h
     unsigned long long *cursor;  // keys requested so far (may exceed keys_cap)
     // the counters (cursor, slow_count, seg_cursor, fr_cursor) share one CTL_BYTES block;
     // the launch zeroes the block the next launch will use (no memsets before a batch)

@@ -16,12 +16,18 @@
 // from it (SURVEY.md §5 checkpoint/resume).
 #include <hip/hip_runtime.h>
 
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <unordered_map>
+#include <unordered_set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -109,6 +115,32 @@ struct PinBuf {
     template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
+// One set of per-batch device buffers and the counters sized from its batches' demand.
+struct BatchBufs {
+    DevBuf d_bytes, d_off, d_outoff, d_outcnt, d_status, d_keys, d_slow_list, d_scr_w, d_scr_s, d_seg_pool, d_fr_pool,
+        d_wave_chunks;
+    DevBuf d_ukeys, d_ucnt;     // UNIQUE / AGGRE: reducer scratch at the result's offsets; reduced counts
+    DevBuf d_dd_wl, d_dd_wl_n;  // k_dd_pass -> k_dedupe worklist
+    DevBuf d_kcnt, d_rcur;      // runs: ids per topic; the batch's span cursor (shared by its sub-batches)
+    // A launch's counters live in one 32-B block {cursor u64, slow_count u32 (+pad),
+    // seg_cursor u64, fr_cursor u64}.  Two blocks alternate: each launch zeroes the block
+    // the NEXT launch will use, so no memset launches precede a batch.
+    DevBuf d_ctl;
+    uint8_t *p_ctl = nullptr;  // the last launch's block
+    uint32_t ctl_cur = 0;
+    uint64_t keys_cap = 0, seg_chunks = 0, fr_chunks = 0, ukeys_cap = 0;
+    uint64_t seg_demand_last = 0, fr_demand_last = 0;
+    uint32_t last_n = 0;     // topics of the last batch
+    uint32_t last_mode = 0;  // TM_MATCH_* of the last batch
+    bool dev_batch = true;   // the device holds the last batch whole (tm_result_ids_device*)
+    void release() {
+        for (DevBuf *b : {&d_bytes, &d_off, &d_outoff, &d_outcnt, &d_status, &d_keys, &d_slow_list, &d_scr_w, &d_scr_s,
+                          &d_seg_pool, &d_fr_pool, &d_wave_chunks, &d_ukeys, &d_ucnt, &d_dd_wl, &d_dd_wl_n, &d_kcnt,
+                          &d_rcur, &d_ctl})
+            b->release();
+    }
+};
+
 // Edge table load <= 1/EDGE_LOAD_INV.  A wave waits for the longest of its ~256
 // concurrent probe chains, so short chains (low load) matter more than table size:
 // 1/16 walks config C 3.4 % faster than 1/8 (0.912 -> 0.881 ms) for 16 GiB of HBM instead
@@ -141,11 +173,14 @@ struct PatchHdr {
     uint64_t magic;
     uint64_t epoch_from, epoch_to;
     uint64_t wmask, emask, n_deep, n_live, n_records;
-    uint64_t full;  // the commit re-uploaded everything: replicas reload from an image
+    uint64_t full;   // the commit re-uploaded everything: replicas reload from an image
+    uint64_t nonce;  // the master's identity: a replica applies patches of its own master only
+    uint64_t max_id;
 };
 struct ImageHdr {
     uint64_t magic;
     uint64_t epoch, wmask, emask, n_deep, n_live, n_nodes, n_words;
+    uint64_t nonce, max_id;
     uint64_t cap[A_N], used[A_N], off[A_N];
 };
 constexpr uint64_t IMAGE_ALIGN = 256;
@@ -180,12 +215,102 @@ inline uint64_t next_pow2(uint64_t x) {
     return p;
 }
 
+// tm_last_error(): the calling thread's last failure (several threads may call one engine at
+// once, so one shared message would be overwritten by another thread's call).
+std::string &tl_err() {
+    thread_local std::string s;
+    return s;
+}
+struct ErrSlot {
+    ErrSlot &operator=(std::string s) {
+        tl_err() = std::move(s);
+        return *this;
+    }
+    ErrSlot &operator=(const char *s) {
+        tl_err() = s;
+        return *this;
+    }
+    const char *c_str() const { return tl_err().c_str(); }
+};
+
+// Host results of the calls that return host memory (tm_match_batch, tm_match_filter_batch,
+// tm_intersect_batch, tm_match_batch_runs): one set per calling thread, so a result stays valid
+// until the same thread's next such call however many threads share the engine.
+struct HostOut {
+    PinBuf h_outoff, h_outcnt, h_status, h_keys;
+    std::vector<uint32_t> pp_off, pp_cnt, pp_keys;
+    // matches_filter/3
+    std::vector<uint32_t> f_off, f_cnt, f_ukeys;
+    std::vector<int32_t> f_status;
+    PinBuf f_keys;
+    // intersection/2
+    std::vector<uint64_t> ix_off;
+    std::vector<int32_t> ix_len;
+    std::vector<uint8_t> ix_bytes;
+    // runs (tm_match_batch_runs)
+    PinBuf r_off, r_cnt, r_kcnt, r_status, r_runs;
+    std::vector<tm_span> spans;
+    std::vector<uint32_t> span_off;
+    uint64_t lease_epoch = 0;
+    bool lease = false;  // holds a read lease on the host id arena (tm_match_batch_runs)
+    void release() {
+        for (PinBuf *b : {&h_outoff, &h_outcnt, &h_status, &h_keys, &f_keys, &r_off, &r_cnt, &r_kcnt, &r_status, &r_runs})
+            b->release();
+        std::vector<uint32_t>().swap(pp_off);
+        std::vector<uint32_t>().swap(pp_cnt);
+        std::vector<uint32_t>().swap(pp_keys);
+        std::vector<uint32_t>().swap(f_off);
+        std::vector<uint32_t>().swap(f_cnt);
+        std::vector<uint32_t>().swap(f_ukeys);
+        std::vector<int32_t>().swap(f_status);
+        std::vector<uint64_t>().swap(ix_off);
+        std::vector<int32_t>().swap(ix_len);
+        std::vector<uint8_t>().swap(ix_bytes);
+        std::vector<tm_span>().swap(spans);
+        std::vector<uint32_t>().swap(span_off);
+    }
+};
+
+// What the match path reads of the index besides the device buffers: set only when a commit
+// PUBLISHES (under mu_dev), so a match never sees a table mask of a host table that a commit
+// running on another thread has already rehashed but not yet uploaded.
+struct DevView {
+    uint64_t epoch = 0;
+    uint64_t wmask = 0, emask = 0;
+    uint64_t n_deep = 0;
+    uint64_t max_id = 0;
+    uint64_t n_live = 0, n_nodes = 0, n_words = 0;
+};
+
 }  // namespace
 
 struct tm_engine {
     tm_config cfg{};
-    std::string err;
-    uint64_t epoch = 0;
+    ErrSlot err;
+    uint64_t epoch = 0;  // host master epoch (== dv.epoch after every successful publish)
+
+    // ---- locks (DESIGN.md §1 "Threading").  Order: mu_commit -> (leases) -> mu_host -> mu_dev
+    // -> mu_stage / mu_out.
+    //   mu_commit one commit at a time (only a commit changes the host copy, so its read-only
+    //             pre-check needs no other lock)
+    //   mu_stage  the staged op list (tm_apply never waits for a match or a commit)
+    //   mu_host   the host master copy: commit's host phase, key introspection, the
+    //             matches_filter index, host-side UNIQUE
+    //   mu_dev    the device: index buffers, batch buffers, streams, DevView (every match)
+    // A commit holds mu_host for its host phase and takes mu_dev only to publish: a delta's
+    // scatters, or the pointer swap of a full rebuild built off to the side (standby image).
+    std::mutex mu_commit, mu_stage, mu_host, mu_out;
+    std::recursive_mutex mu_dev;
+    DevView dv;
+    // streams that ran work reading the index since the last publish, with an event recorded
+    // after that work: a publish makes its own stream wait on them before writing in place
+    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+    std::unordered_map<std::thread::id, std::unique_ptr<HostOut>> outs;
+    // read leases on the host id arena (runs results): a commit's host phase waits for them
+    std::mutex lease_mu;
+    std::condition_variable lease_cv;
+    uint64_t n_leases = 0;
+    bool lease_block = false;
 
     // ---- words (interner + device word table mirror)
     std::vector<WordSlot> wtab;
@@ -209,6 +334,38 @@ struct tm_engine {
     std::vector<uint32_t> arena;
     uint64_t arena_garbage = 0;
     size_t arena_dev = 0;  // words already on device
+    // Host id arena: arena_id[i] = id of the key handle arena[i] (key positions only), so a run
+    // of the arena is a span of route ids (tm_match_batch_runs).  One fixed virtual reservation
+    // (MAP_NORESERVE, touched as it fills), so spans stay valid while the arena grows.
+    uint64_t *arena_id = nullptr;
+    uint64_t arena_id_res = 0;  // entries reserved
+    void ids_of(uint64_t lo, uint64_t hi) {  // refresh arena_id over key positions [lo, hi)
+        if (!arena_id) return;
+        if (hi > arena_id_res) {  // past the reservation: only until the compaction this forces
+            ids_stale = true;
+            hi = arena_id_res;
+        }
+        for (uint64_t i = lo; i < hi; i++) arena_id[i] = keys[arena[i]].id;
+    }
+    bool ids_stale = false;
+    bool reserve_ids() {  // a virtual reservation of the budget (halved until the OS grants it)
+        uint64_t want = std::min<uint64_t>(std::max<uint64_t>(arena_budget() + 16, 1ull << 16), 1ull << 32);
+        while (want >= (1ull << 12)) {
+            void *p = mmap(nullptr, want * 8, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+            if (p != MAP_FAILED) {
+                arena_id = (uint64_t *)p;
+                arena_id_res = want;
+                return true;
+            }
+            want /= 2;
+        }
+        return false;
+    }
+    void release_ids() {
+        if (arena_id) munmap(arena_id, arena_id_res * 8);
+        arena_id = nullptr;
+        arena_id_res = 0;
+    }
 
     // ---- keys
     std::vector<KeyRec> keys;
@@ -296,34 +453,35 @@ struct tm_engine {
     DevBuf d_key_dd;                  // key handle -> KDD_* flags (u8; which keys k_dedupe must table)
     std::vector<uint64_t> dirty_kid;  // handles (re)assigned since the last upload
     uint64_t n_deep = 0;              // live word-list keys too deep for the 64-bit order code
-    DevBuf d_ukeys, d_ucnt;           // UNIQUE / AGGRE: reducer scratch at the result's offsets; reduced counts
-    DevBuf d_dd_wl, d_dd_wl_n;        // k_dd_pass -> k_dedupe worklist
-    uint64_t ukeys_cap = 0;
-    uint32_t last_mode = 0;           // TM_MATCH_* of the last batch
     DevBuf d_res_scan, d_mrg_roff, d_mrg_tot;  // scratch of tm_result_ids_device / tm_merge_shards_device
-    // batch buffers
-    DevBuf d_bytes, d_off, d_outoff, d_outcnt, d_status, d_keys, d_slow_list, d_scr_w, d_scr_s, d_stats,
-        d_seg_pool, d_fr_pool, d_wave_chunks;
-    // A launch's counters live in one 32-B block {cursor u64, slow_count u32 (+pad),
-    // seg_cursor u64, fr_cursor u64}.  Two blocks alternate: each launch zeroes the block
-    // the NEXT launch will use, so no memset launches precede a batch.
-    DevBuf d_ctl;
-    uint8_t *p_ctl = nullptr;  // the last launch's block
-    uint32_t ctl_cur = 0;
-    uint64_t keys_cap = 0, seg_chunks = 0, fr_chunks = 0;
-    PinBuf h_bytes, h_off, h_outoff, h_outcnt, h_status, h_keys, h_cursor;
-    std::vector<uint32_t> pp_off, pp_cnt, pp_keys;  // post-processed results
+    DevBuf d_stats;
+    // Batch buffers: one set for the device-result calls (tm_match_device*, whose result the
+    // engine keeps until the next such call) and one for the host-result calls (tm_match_batch*,
+    // synchronous), so a host call from one thread never overwrites another thread's pending
+    // device result.  `bb` is the set of the call in progress (under mu_dev).
+    BatchBufs bb_dev, bb_host;
+    BatchBufs *bb = &bb_dev;
+    double runs_spt = 4.0;     // spans per topic of the last runs batch (sizes the next)
+    PinBuf h_rctl;             // runs: per sub-batch {span cursor, counter block}
+    PinBuf h_bytes, h_off, h_cursor;
     hipStream_t stream = nullptr;
-    uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0, seg_demand_last = 0, fr_demand_last = 0;
+    hipStream_t s_build = nullptr;  // a full rebuild's standby upload (beside the matches)
+    hipEvent_t ev_chain = nullptr;  // orders a device match after the previous one's stream
+    uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0;
     uint64_t commit_us[3] = {0, 0, 0};  // last commit: apply / lists / upload (tm_stats)
+    uint64_t commit_stall_us = 0;       // last commit: matches held back while it published
+    uint64_t n_commits_refused = 0;     // commits refused for capacity (ops kept staged)
+    uint64_t staged_count() {
+        std::lock_guard<std::mutex> g(mu_stage);
+        return staged.size();
+    }
     hipStream_t last_stream = nullptr;  // stream of the last tm_match_device call
-    uint32_t last_n = 0;                // topics of the last match batch
     bool stats_on = false;
     uint64_t max_id = 0;     // largest id ever added (ids fit u32 results while < 2^32)
     PatchLog patch;          // master: the last commit's device changes (TM_CFG_RECORD_PATCH)
     uint64_t patch_from = 0; // epoch the recorded patch applies to
     bool replica = false;    // built from a device image: no host master copy, read-only
-    uint64_t rep_n_live = 0, rep_n_nodes = 0, rep_n_words = 0;
+    uint64_t master_nonce = 0;  // random per master engine; a replica holds its master's
     uint64_t dev_used[A_N] = {};  // bytes of each device array in use (image export)
     hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // around k_match_fast (tm_debug_timing)
     bool timing_on = false;
@@ -333,9 +491,100 @@ struct tm_engine {
     hipEvent_t ev_pk[2] = {}, ev_pd[2] = {};
     PinBuf h_pctl;
     double pipe_kpt = 0;
-    bool dev_batch = true;  // the device holds the last batch whole (tm_result_ids_device*)
 
     uint64_t edge_load_inv() const { return cfg.edge_load_inv ? cfg.edge_load_inv : EDGE_LOAD_INV; }
+    uint64_t node_budget() const {  // trie nodes below the root
+        const uint64_t hard = MAX_EDGE_SLOTS / 2;
+        return cfg.max_nodes ? std::min<uint64_t>(cfg.max_nodes, hard) : hard;
+    }
+    uint64_t arena_budget() const {  // list offsets are u32; the host id arena's reservation
+        const uint64_t hard = arena_id_res ? std::min<uint64_t>(0xFFFFFFF0ull, arena_id_res - 16) : 0xFFFFFFF0ull;
+        return cfg.max_list_words ? std::min<uint64_t>(cfg.max_list_words, hard) : hard;
+    }
+
+    HostOut &out() {  // the calling thread's host results
+        std::lock_guard<std::mutex> g(mu_out);
+        std::unique_ptr<HostOut> &p = outs[std::this_thread::get_id()];
+        if (!p) p.reset(new HostOut());
+        return *p;
+    }
+
+    // ---- ordering of device work (under mu_dev)
+    // index-reading work was queued on s: remember it (a publish waits for it)
+    hipError_t note_use(hipStream_t s) {
+        for (auto &u : uses)
+            if (u.first == s) return hipEventRecord(u.second, s);
+        hipEvent_t ev;
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e) return e;
+        uses.push_back({s, ev});
+        return hipEventRecord(ev, s);
+    }
+    // make `s` wait (on the device) for every recorded use
+    hipError_t wait_uses(hipStream_t s) {
+        for (auto &u : uses)
+            if (u.first != s) {
+                hipError_t e = hipStreamWaitEvent(s, u.second, 0);
+                if (e) return e;
+            }
+        return hipSuccess;
+    }
+    // the host waits for every recorded use and the engine stream (before buffers are freed)
+    hipError_t quiesce() {
+        for (auto &u : uses) {
+            hipError_t e = hipEventSynchronize(u.second);
+            if (e) return e;
+        }
+        return stream ? hipStreamSynchronize(stream) : hipSuccess;
+    }
+    // A device match about to run on s reuses the batch buffers of the previous one (which ran
+    // on last_stream): order s after everything queued on last_stream so far, which includes
+    // the previous caller's reads of its result.
+    hipError_t chain_after_last(hipStream_t s) {
+        if (!last_stream || last_stream == s) return hipSuccess;
+        hipError_t e;
+        if (!ev_chain && (e = hipEventCreateWithFlags(&ev_chain, hipEventDisableTiming))) return e;
+        if ((e = hipEventRecord(ev_chain, last_stream))) return e;
+        return hipStreamWaitEvent(s, ev_chain, 0);
+    }
+
+    // a batch buffer that must grow: in-flight work may still use it, so drain first
+    hipError_t grow_buf(DevBuf &b, size_t bytes) {
+        if (bytes <= b.cap && b.p) return hipSuccess;
+        hipError_t e = quiesce();
+        return e ? e : b.ensure(bytes);
+    }
+
+    // ---- read leases on the host id arena (tm_match_batch_runs)
+    void lease_take(HostOut &o) {
+        if (o.lease) return;
+        std::unique_lock<std::mutex> lk(lease_mu);
+        lease_cv.wait(lk, [&] { return !lease_block; });
+        n_leases++;
+        o.lease = true;
+    }
+    void lease_drop(HostOut &o) {
+        if (!o.lease) return;
+        {
+            std::lock_guard<std::mutex> g(lease_mu);
+            n_leases--;
+            o.lease = false;
+        }
+        lease_cv.notify_all();
+    }
+    // a commit's host phase: no new leases, wait for the held ones (writer preference)
+    void leases_block() {
+        std::unique_lock<std::mutex> lk(lease_mu);
+        lease_block = true;
+        lease_cv.wait(lk, [&] { return n_leases == 0; });
+    }
+    void leases_unblock() {
+        {
+            std::lock_guard<std::mutex> g(lease_mu);
+            lease_block = false;
+        }
+        lease_cv.notify_all();
+    }
 
     DevBuf *arr_buf(uint32_t a) {
         DevBuf *b[A_N] = {&d_wtab, &d_warena, &d_word_off, &d_etab, &d_slot_list, &d_arena,
@@ -645,10 +894,10 @@ struct tm_engine {
         return (kind == K_EXACT_WORDS || kind == K_WILD) && depth > 31;
     }
 
-    void apply_one(const StagedOp &op, uint32_t hint_node = ROOT, uint32_t hint_depth = 0) {
+    void apply_one(const StagedOp &op, const uint8_t *ob, uint32_t hint_node = ROOT, uint32_t hint_depth = 0) {
         uint8_t kind;
         uint32_t node, depth = 0;
-        const uint8_t *fp = stage_bytes.data() + op.off;
+        const uint8_t *fp = ob + op.off;
         if (op.op == TM_OP_ADD) {
             classify(fp, op.len, op.flags, true, &kind, &node, &depth, hint_node, hint_depth);
             if (kind == K_DEAD) {
@@ -706,24 +955,35 @@ struct tm_engine {
     // per level); the ops then apply in order, each walk starting at its resolved prefix.
     // A prefix stays valid while ops apply (nodes are only ever added), and an op whose
     // path appears only during this epoch resumes from where resolution stopped.
-    void apply_staged() {
-        const size_t n = staged.size();
+    // nwalk[i]: levels of the trie path an ADD creates or reuses (0: no path).
+    void resolve_all(const std::vector<StagedOp> &ops, const uint8_t *ob, std::vector<uint32_t> &hnode,
+                     std::vector<uint32_t> &hdepth, std::vector<uint32_t> &nwalk) const {
+        const size_t n = ops.size();
+        auto one = [&](size_t i, std::vector<std::pair<uint32_t, uint32_t>> &lv) {
+            const uint8_t *f = ob + ops[i].off;
+            resolve_prefix(f, ops[i].len, lv, &hnode[i], &hdepth[i]);
+            if (ops[i].op != TM_OP_ADD) return;
+            // a '#' before the last level: a dead key, no path; a final '#': the path stops above it
+            int hash_pos = -1;
+            for (size_t k = 0; k < lv.size() && hash_pos < 0; k++)
+                if (lv[k].second == 1 && f[lv[k].first] == '#') hash_pos = (int)k;
+            if (hash_pos >= 0 && hash_pos != (int)lv.size() - 1) nwalk[i] = 0;
+            else nwalk[i] = (uint32_t)(hash_pos >= 0 ? lv.size() - 1 : lv.size());
+        };
         const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-        const unsigned nt = (n_edges == 0 || n < 4096) ? 1u : (unsigned)std::min<size_t>(hw, n / 2048);
+        const unsigned nt = n < 4096 ? 1u : (unsigned)std::min<size_t>(hw, n / 2048);
         if (nt <= 1) {
-            for (const StagedOp &op : staged) apply_one(op);
+            std::vector<std::pair<uint32_t, uint32_t>> lv;
+            for (size_t i = 0; i < n; i++) one(i, lv);
             return;
         }
-        std::vector<uint32_t> hnode(n), hdepth(n);
         std::vector<std::thread> th;
         for (unsigned k = 0; k < nt; k++)
             th.emplace_back([&, k] {
                 std::vector<std::pair<uint32_t, uint32_t>> lv;
-                for (size_t i = k; i < n; i += nt)
-                    resolve_prefix(stage_bytes.data() + staged[i].off, staged[i].len, lv, &hnode[i], &hdepth[i]);
+                for (size_t i = k; i < n; i += nt) one(i, lv);
             });
         for (auto &t : th) t.join();
-        for (size_t i = 0; i < n; i++) apply_one(staged[i], hnode[i], hdepth[i]);
     }
 
     // Recompute a node's emission bits from its list (and keep its I_PLUS/I_LIT):
@@ -787,12 +1047,14 @@ struct tm_engine {
         arena.insert(arena.end(), hashes, hashes + hc);
         if (cap > tc + hc) arena.resize(arena.size() + (cap - tc - hc), 0u);
         write_header(off, terms, tc, hashes, hc);
+        ids_of(off, (uint64_t)off + tc + hc);
         return NodeList{off, tc, hc};
     }
 
     // Rebuild the whole arena from the key table (counting sort by node).
     void rebuild_arena() {
         need_full = true;  // everything is re-uploaded: no dirty tracking
+        ids_stale = false;
         size_t nn = node_parent.size();
         std::vector<uint32_t> tcnt(nn, 0), hcnt(nn, 0);
         for (size_t h = 0; h < keys.size(); h++) {
@@ -821,7 +1083,10 @@ struct tm_engine {
         for (size_t v = 0; v < nn; v++) {
             node_list[v] = NodeList{pos[v], tcnt[v], hcnt[v]};
             node_cap[v] = tcnt[v] + hcnt[v];
-            if (pos[v]) write_header(pos[v], &arena[pos[v]], tcnt[v], &arena[pos[v] + tcnt[v]], hcnt[v]);
+            if (pos[v]) {
+                write_header(pos[v], &arena[pos[v]], tcnt[v], &arena[pos[v] + tcnt[v]], hcnt[v]);
+                ids_of(pos[v], (uint64_t)pos[v] + tcnt[v] + hcnt[v]);
+            }
             refresh_info((uint32_t)v);
         }
         arena_garbage = 0;
@@ -859,6 +1124,7 @@ struct tm_engine {
                 std::copy(terms.begin(), terms.end(), dst);
                 std::copy(hashes.begin(), hashes.end(), dst + tc);
                 write_header(r.list_off, terms.data(), tc, hashes.data(), hc);
+                ids_of(r.list_off, (uint64_t)r.list_off + tc + hc);
                 for (uint64_t w = r.list_off - LIST_HDR; w < (uint64_t)r.list_off + tc + hc; w++)
                     if (w < arena_dev) dirty_arena.push_back(w);
                 node_list[node] = NodeList{r.list_off, tc, hc};
@@ -874,17 +1140,30 @@ struct tm_engine {
         }
     }
 
+    // ---- device upload.  Every allocation of a publish comes before its first in-place
+    // write, and a replaced buffer is allocated before the old one is freed, so a publish that
+    // fails (out of HBM) leaves the device holding the previous epoch intact.
+
+    // Replace array a's device buffer with one holding h (headroom num/den), allocated first.
     template <class T>
-    hipError_t put(DevBuf &d, const std::vector<T> &h, size_t headroom_num = 3, size_t headroom_den = 2) {
-        hipError_t e;
-        size_t bytes = h.size() * sizeof(T);
-        if ((e = d.ensure(std::max<size_t>(bytes * headroom_num / headroom_den, 4096)))) return e;
-        if (bytes && (e = hipMemcpyAsync(d.p, h.data(), bytes, hipMemcpyHostToDevice, stream))) return e;
-        const uint32_t a = arr_of(&d);
-        if (a < A_N) {
-            dev_used[a] = bytes;
-            patch.add(P_WHOLE, a, bytes / ARR_ELEM[a], d.cap, h.data(), bytes);
+    hipError_t replace_whole(DevBuf &d, uint32_t a, const std::vector<T> &h, size_t num = 3, size_t den = 2) {
+        const size_t bytes = h.size() * sizeof(T);
+        DevBuf nb;
+        hipError_t e = nb.ensure(std::max<size_t>(bytes * num / den, 4096));
+        if (e) return e;
+        if (bytes && (e = hipMemcpyAsync(nb.p, h.data(), bytes, hipMemcpyHostToDevice, stream))) {
+            nb.release();
+            return e;
         }
+        if ((e = hipStreamSynchronize(stream))) {
+            nb.release();
+            return e;
+        }
+        std::swap(d.p, nb.p);
+        std::swap(d.cap, nb.cap);
+        nb.release();
+        dev_used[a] = bytes;
+        patch.add(P_WHOLE, a, bytes / ARR_ELEM[a], d.cap, h.data(), bytes);
         return hipSuccess;
     }
     template <class T>
@@ -903,26 +1182,6 @@ struct tm_engine {
         return e;
     }
 
-    hipError_t upload_full() {
-        hipError_t e;
-        patch.reset();
-        patch.full = true;  // replicas reload from an image
-        dev_used[A_ROOT] = sizeof(RootRec);
-        if ((e = put(d_wtab, wtab, 1, 1))) return e;
-        if ((e = put(d_warena, warena))) return e;
-        warena_dev = warena.size();
-        if ((e = put(d_word_off, word_off))) return e;
-        word_off_dev = word_off.size();
-        if ((e = put(d_etab, etab, 1, 1))) return e;
-        if ((e = put(d_slot_list, slot_list, 1, 1))) return e;
-        if ((e = put(d_arena, arena))) return e;
-        arena_dev = arena.size();
-        if ((e = d_root.ensure(sizeof(RootRec)))) return e;
-        if ((e = hipMemcpyAsync(d_root.p, &root, sizeof(RootRec), hipMemcpyHostToDevice, stream))) return e;
-        if ((e = upload_key_ids_full())) return e;
-        return hipStreamSynchronize(stream);
-    }
-
     // key handle -> {id, order code}, device node slot, binary flag
     void key_dev_rec(uint32_t h, uint64_t *rec, uint32_t *node, uint32_t *bin, uint8_t *dd) const {
         const KeyRec &k = keys[h];
@@ -933,26 +1192,83 @@ struct tm_engine {
         *bin = k.kind == K_EXACT_BIN ? 1u : 0u;
         *dd = (uint8_t)(((k._p[0] & KR_MULTI) ? KDD_MULTI : 0) | ((k.id & TM_ID_SHARED) ? KDD_SHARED : 0));
     }
+    struct KeyArrays {
+        std::vector<uint64_t> rec;
+        std::vector<uint32_t> node, bin;
+        std::vector<uint8_t> dd;
+    };
+    void key_arrays(KeyArrays &k) const {
+        k.rec.resize(keys.size() * 2);
+        k.node.resize(keys.size());
+        k.bin.resize(keys.size());
+        k.dd.resize(keys.size());
+        for (size_t h = 0; h < keys.size(); h++) key_dev_rec((uint32_t)h, &k.rec[2 * h], &k.node[h], &k.bin[h], &k.dd[h]);
+    }
 
-    hipError_t upload_key_ids_full() {
-        std::vector<uint64_t> rec(keys.size() * 2);
-        std::vector<uint32_t> node(keys.size()), bin(keys.size());
-        std::vector<uint8_t> dd(keys.size());
-        for (size_t h = 0; h < keys.size(); h++) key_dev_rec((uint32_t)h, &rec[2 * h], &node[h], &bin[h], &dd[h]);
-        dirty_kid.clear();
-        hipError_t e = put(d_key_rec, rec);
+    // Full publish into a STANDBY image: every array is uploaded into fresh buffers on s_build
+    // while matches keep running on the current image (mu_dev is not held); then, under
+    // mu_dev, the in-flight matches drain and the buffers swap.  At config C that is ~20 GiB
+    // uploaded beside the match path; the match path stalls only for the swap.
+    template <class T>
+    static hipError_t stage_to(DevBuf &d, const std::vector<T> &h, hipStream_t s, uint64_t *used, size_t num = 3,
+                               size_t den = 2) {
+        const size_t bytes = h.size() * sizeof(T);
+        hipError_t e = d.ensure(std::max<size_t>(bytes * num / den, 4096));
         if (e) return e;
-        if ((e = put(d_key_node, node))) return e;
-        if ((e = put(d_key_bin, bin))) return e;
-        if ((e = put(d_key_dd, dd))) return e;
-        return hipStreamSynchronize(stream);  // the staging vectors die at scope exit
+        if (bytes && (e = hipMemcpyAsync(d.p, h.data(), bytes, hipMemcpyHostToDevice, s))) return e;
+        *used = bytes;
+        return hipSuccess;
+    }
+    uint64_t last_swap_us = 0;  // mu_dev held by the last full publish's swap (tm_stats)
+    hipError_t publish_full() {
+        patch.reset();
+        patch.full = true;  // replicas reload from an image
+        DevBuf sb[A_N];
+        uint64_t used[A_N] = {};
+        KeyArrays ka;
+        key_arrays(ka);
+        hipStream_t s = s_build;
+        hipError_t e;
+        auto fail = [&](hipError_t err) {
+            (void)hipStreamSynchronize(s);
+            for (DevBuf &b : sb) b.release();
+            return err;
+        };
+        if ((e = stage_to(sb[A_WTAB], wtab, s, &used[A_WTAB], 1, 1)) || (e = stage_to(sb[A_WARENA], warena, s, &used[A_WARENA])) ||
+            (e = stage_to(sb[A_WORD_OFF], word_off, s, &used[A_WORD_OFF])) ||
+            (e = stage_to(sb[A_ETAB], etab, s, &used[A_ETAB], 1, 1)) ||
+            (e = stage_to(sb[A_SLOT_LIST], slot_list, s, &used[A_SLOT_LIST], 1, 1)) ||
+            (e = stage_to(sb[A_ARENA], arena, s, &used[A_ARENA])) || (e = stage_to(sb[A_KEY_REC], ka.rec, s, &used[A_KEY_REC])) ||
+            (e = stage_to(sb[A_KEY_NODE], ka.node, s, &used[A_KEY_NODE])) ||
+            (e = stage_to(sb[A_KEY_BIN], ka.bin, s, &used[A_KEY_BIN])) ||
+            (e = stage_to(sb[A_KEY_DD], ka.dd, s, &used[A_KEY_DD])) || (e = sb[A_ROOT].ensure(sizeof(RootRec))) ||
+            (e = hipMemcpyAsync(sb[A_ROOT].p, &root, sizeof(RootRec), hipMemcpyHostToDevice, s)))
+            return fail(e);
+        used[A_ROOT] = sizeof(RootRec);
+        if ((e = hipStreamSynchronize(s))) return fail(e);
+        {
+            std::lock_guard<std::recursive_mutex> g(mu_dev);
+            const uint64_t t0 = now_us();
+            if ((e = quiesce())) return fail(e);  // matches in flight finish on the old image
+            for (uint32_t a = 0; a < A_N; a++) {
+                DevBuf *d = arr_buf(a);
+                std::swap(d->p, sb[a].p);
+                std::swap(d->cap, sb[a].cap);
+                dev_used[a] = used[a];
+            }
+            warena_dev = warena.size();
+            word_off_dev = word_off.size();
+            arena_dev = arena.size();
+            dirty_kid.clear();
+            set_view();
+            last_swap_us = now_us() - t0;
+        }
+        for (DevBuf &b : sb) b.release();  // the previous image: nothing in flight reads it
+        return hipSuccess;
     }
 
     hipError_t upload_key_ids_delta() {
         if (dirty_kid.empty()) return hipSuccess;
-        if (keys.size() * 16 > d_key_rec.cap || keys.size() * sizeof(uint32_t) > d_key_bin.cap ||
-            keys.size() * sizeof(uint32_t) > d_key_node.cap || keys.size() > d_key_dd.cap)
-            return upload_key_ids_full();
         std::sort(dirty_kid.begin(), dirty_kid.end());
         dirty_kid.erase(std::unique(dirty_kid.begin(), dirty_kid.end()), dirty_kid.end());
         const size_t n = dirty_kid.size();
@@ -968,9 +1284,11 @@ struct tm_engine {
         patch.add(P_SCATTER, A_KEY_BIN, n, 0, idx.data(), n * 8, bin.data(), n * 4);
         patch.add(P_SCATTER, A_KEY_NODE, n, 0, idx.data(), n * 8, node.data(), n * 4);
         patch.add(P_SCATTER, A_KEY_DD, n, 0, idx.data(), n * 8, dd.data(), n);
+        // handles past the arrays' used part (inside their capacity) extend it
+        const uint64_t top = idx[n - 1] + 1;
+        for (uint32_t a : {A_KEY_REC, A_KEY_BIN, A_KEY_NODE, A_KEY_DD})
+            dev_used[a] = std::max<uint64_t>(dev_used[a], top * ARR_ELEM[a]);
         hipError_t e;
-        if ((e = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e;
-        if ((e = d_scatter_src.ensure(n * 16))) return e;
         if ((e = hipMemcpyAsync(d_scatter_idx.p, idx.data(), n * 8, hipMemcpyHostToDevice, stream))) return e;
         if ((e = hipMemcpyAsync(d_scatter_src.p, rec.data(), n * 16, hipMemcpyHostToDevice, stream))) return e;
         if ((e = launch_scatter16(d_key_rec.as<uint4>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint4>(), n,
@@ -1007,8 +1325,6 @@ struct tm_engine {
         for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
         patch.add(P_SCATTER, arr_of(&dbuf), n, 0, dirty.data(), n * 8, src.data(), n * 16);
         hipError_t e;
-        if ((e = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e;
-        if ((e = d_scatter_src.ensure(n * 16))) return e;
         if ((e = hipMemcpyAsync(d_scatter_idx.p, dirty.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, stream)))
             return e;
         if ((e = hipMemcpyAsync(d_scatter_src.p, src.data(), n * 16, hipMemcpyHostToDevice, stream))) return e;
@@ -1029,8 +1345,6 @@ struct tm_engine {
         for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
         patch.add(P_SCATTER, arr_of(&dbuf), n, 0, dirty.data(), n * 8, src.data(), n * 4);
         hipError_t e;
-        if ((e = d_scatter_idx.ensure(n * sizeof(uint64_t)))) return e;
-        if ((e = d_scatter_src.ensure(n * 4))) return e;
         if ((e = hipMemcpyAsync(d_scatter_idx.p, dirty.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, stream)))
             return e;
         if ((e = hipMemcpyAsync(d_scatter_src.p, src.data(), n * 4, hipMemcpyHostToDevice, stream))) return e;
@@ -1068,23 +1382,39 @@ struct tm_engine {
         return hipSuccess;
     }
 
+    // Delta publish, under mu_dev after quiesce().  Phase 1 allocates (moves of grown arrays,
+    // key arrays that outgrew their buffers, the word table after a rehash, the scatter
+    // staging); phase 2 writes in place.  A failure in phase 1 leaves the previous epoch whole.
     hipError_t upload_delta() {
         hipError_t e;
-        // arrays that only grow: append the tail (moving the array to a larger buffer first
-        // when it no longer fits)
+        // phase 1
         if ((e = grow(d_warena, warena, warena_dev))) return e;
         if ((e = grow(d_word_off, word_off, word_off_dev))) return e;
         if ((e = grow(d_arena, arena, arena_dev))) return e;
+        if (keys.size() * 16 > d_key_rec.cap || keys.size() * sizeof(uint32_t) > d_key_bin.cap ||
+            keys.size() * sizeof(uint32_t) > d_key_node.cap || keys.size() > d_key_dd.cap) {
+            KeyArrays ka;
+            key_arrays(ka);
+            if ((e = replace_whole(d_key_rec, A_KEY_REC, ka.rec)) || (e = replace_whole(d_key_node, A_KEY_NODE, ka.node)) ||
+                (e = replace_whole(d_key_bin, A_KEY_BIN, ka.bin)) || (e = replace_whole(d_key_dd, A_KEY_DD, ka.dd)))
+                return e;
+            dirty_kid.clear();
+        }
+        if (words_full) {
+            if ((e = replace_whole(d_wtab, A_WTAB, wtab, 1, 1))) return e;
+            dirty_wslots.clear();
+        }
+        size_t mx = 0;
+        for (const std::vector<uint64_t> *v : {&dirty_arena, &dirty_wslots, &dirty_eslots, &dirty_lists, &dirty_kid})
+            mx = std::max(mx, v->size());
+        if ((e = d_scatter_idx.ensure(std::max<size_t>(mx, 1) * sizeof(uint64_t)))) return e;
+        if ((e = d_scatter_src.ensure(std::max<size_t>(mx, 1) * 16))) return e;
+        // phase 2
         if ((e = put_tail(d_warena, warena, warena_dev))) return e;
         if ((e = put_tail(d_word_off, word_off, word_off_dev))) return e;
         if ((e = put_tail(d_arena, arena, arena_dev))) return e;
         if ((e = scatter4(dirty_arena, arena, d_arena))) return e;  // lists rewritten in place
-        if (words_full) {
-            if ((e = put(d_wtab, wtab, 1, 1))) return e;
-            dirty_wslots.clear();
-        } else if ((e = scatter16(dirty_wslots, wtab, d_wtab))) {
-            return e;
-        }
+        if ((e = scatter16(dirty_wslots, wtab, d_wtab))) return e;
         if ((e = scatter16(dirty_eslots, etab, d_etab))) return e;
         if ((e = scatter4(dirty_lists, slot_list, d_slot_list))) return e;
         if ((e = upload_key_ids_delta())) return e;
@@ -1101,43 +1431,159 @@ struct tm_engine {
             .count();
     }
 
-    int commit() {
-        const uint64_t t0 = now_us();
-        apply_staged();
-        if (edge_full) {
-            err = "edge table full: more trie nodes than MAX_EDGE_SLOTS / 2 (shard the filters over more GPUs); "
-                  "the engine is unusable and must be recreated";
+    // ---------------------------------------------------------------------
+    // Capacity check of an epoch's ops BEFORE anything changes (a refused commit keeps its ops
+    // staged and the engine serving the previous epoch: emqx_router_syncer.erl:269-277).
+    // hnode/hdepth: the deepest existing node on each op's path; nwalk: the levels its key
+    // hangs at (0 for ops that create no node: deletes, dead filters).
+    int capacity_check(const std::vector<StagedOp> &ops, const uint8_t *ob, const std::vector<uint32_t> &hdepth,
+                       const std::vector<uint32_t> &nwalk) {
+        uint64_t upper = 0, adds = 0;
+        for (size_t i = 0; i < ops.size(); i++)
+            if (ops[i].op == TM_OP_ADD) {
+                adds++;
+                if (nwalk[i] > hdepth[i]) upper += nwalk[i] - hdepth[i];
+            }
+        // the arena after a compaction: every live key once, one header per node with keys
+        const uint64_t keys_after = n_live + adds;
+        auto arena_need = [&](uint64_t nn) { return keys_after + LIST_HDR * std::min(keys_after, n_edges + 1 + nn); };
+        uint64_t new_nodes = upper;
+        if (n_edges + upper > node_budget() || arena_need(upper) > arena_budget()) {
+            // exact: a new node is named by its filter's byte prefix (its words)
+            std::unordered_set<std::string> fresh;
+            std::vector<std::pair<uint32_t, uint32_t>> lv;
+            for (size_t i = 0; i < ops.size(); i++) {
+                if (ops[i].op != TM_OP_ADD || nwalk[i] <= hdepth[i]) continue;
+                const uint8_t *f = ob + ops[i].off;
+                lv.clear();
+                uint32_t st = 0;
+                for (uint32_t j = 0; j <= ops[i].len; j++)
+                    if (j == ops[i].len || f[j] == '/') {
+                        lv.push_back({st, j - st});
+                        st = j + 1;
+                    }
+                for (uint32_t k = hdepth[i]; k < nwalk[i]; k++)
+                    fresh.emplace((const char *)f, lv[k].first + lv[k].second);
+            }
+            new_nodes = fresh.size();
+        }
+        if (n_edges + new_nodes > node_budget()) {
+            err = "commit refused: " + std::to_string(n_edges + new_nodes) + " trie nodes > budget " +
+                  std::to_string(node_budget()) +
+                  " (ops kept staged; the previous epoch keeps serving; shard the filters or raise max_nodes)";
             return TM_ENOMEM;
         }
-        staged.clear();
-        stage_bytes.clear();
+        if (arena_need(new_nodes) > arena_budget()) {
+            err = "commit refused: the terminal-list arena would pass its budget of " + std::to_string(arena_budget()) +
+                  " words (ops kept staged; the previous epoch keeps serving)";
+            return TM_ENOMEM;
+        }
+        return TM_OK;
+    }
+
+    // Ops whose commit failed go back to the front of the staged list (ahead of ops staged
+    // by other threads meanwhile), so a retry applies everything in the original order.
+    void restage(std::vector<StagedOp> &ops, std::vector<uint8_t> &ob) {
+        std::lock_guard<std::mutex> g(mu_stage);
+        const uint64_t base = ob.size();
+        for (StagedOp &o : staged) o.off += base;
+        ob.insert(ob.end(), stage_bytes.begin(), stage_bytes.end());
+        ops.insert(ops.end(), staged.begin(), staged.end());
+        staged.swap(ops);
+        stage_bytes.swap(ob);
+    }
+
+    // Publish the host copy's changes to the device.  Delta: scatter in place under mu_dev,
+    // after every use already queued.  Full: upload into a standby image on s_build while
+    // matches keep running on the current one, then swap under mu_dev.
+    hipError_t publish(bool full) {
+        if (full) {
+            hipError_t e = publish_full();
+            if (!e) commit_stall_us = last_swap_us;
+            return e;
+        }
+        std::lock_guard<std::recursive_mutex> g(mu_dev);
+        const uint64_t t0 = now_us();
+        hipError_t e = quiesce();  // in-flight matches read what this writes in place
+        if (!e) e = upload_delta();
+        if (!e) set_view();
+        commit_stall_us = now_us() - t0;
+        return e;
+    }
+    void set_view() {  // under mu_dev
+        dv.epoch = epoch;
+        dv.wmask = wmask;
+        dv.emask = emask;
+        dv.n_deep = n_deep;
+        dv.max_id = max_id;
+        dv.n_live = n_live;
+        dv.n_nodes = node_parent.size();
+        dv.n_words = word_off.size();
+    }
+
+    int commit(HostOut *me) {  // caller holds mu_commit
+        std::vector<StagedOp> ops;
+        std::vector<uint8_t> ob;
+        {
+            std::lock_guard<std::mutex> g(mu_stage);
+            ops.swap(staged);
+            ob.swap(stage_bytes);
+        }
+        const uint64_t t0 = now_us();
+        const size_t n = ops.size();
+        std::vector<uint32_t> hnode(n, ROOT), hdepth(n, 0), nwalk(n, 0);
+        resolve_all(ops, ob.data(), hnode, hdepth, nwalk);
+        int rc = capacity_check(ops, ob.data(), hdepth, nwalk);
+        if (rc) {
+            restage(ops, ob);
+            n_commits_refused++;
+            return rc;
+        }
+        // host phase: runs results read the host id arena and key table, so none may be held
+        if (me) lease_drop(*me);
+        leases_block();  // before mu_host: a lease holder may still read the host copy meanwhile
+        struct Unblock {
+            tm_engine *e;
+            ~Unblock() { e->leases_unblock(); }
+        } unblock{this};
+        std::lock_guard<std::mutex> gh(mu_host);
+        for (size_t i = 0; i < n; i++) apply_one(ops[i], ob.data(), hnode[i], hdepth[i]);
+        if (edge_full) {  // cannot happen after capacity_check; never serve a half-applied trie
+            err = "internal: edge table overflow past the capacity check";
+            return TM_EDEVICE;
+        }
         const uint64_t t1 = now_us();
         bool full = need_full || deltas.size() > std::max<uint64_t>(n_live / 8, 1u << 16);
         if (full) {
             rebuild_arena();
         } else if (!deltas.empty()) {
             apply_deltas();
-            if (arena_garbage > std::max<uint64_t>(arena.size() / 2, 1u << 20)) rebuild_arena();
+            if (arena_garbage > std::max<uint64_t>(arena.size() / 2, 1u << 20) || arena.size() > arena_budget() ||
+                ids_stale)
+                rebuild_arena();
         }
         deltas.clear();
-        if (arena.size() >= 0xFFFFFFF0ull) {  // list offsets are u32
-            edge_full = true;
-            err = "terminal-list arena beyond 4 Gi entries (shard the filters over more GPUs); "
-                  "the engine is unusable and must be recreated";
-            return TM_ENOMEM;
-        }
         const uint64_t t2 = now_us();
         patch.reset();
         patch_from = epoch;
-        hipError_t e = need_full ? upload_full() : upload_delta();
+        const bool was_full = need_full;
+        epoch++;
+        hipError_t e = publish(need_full);
         if (e != hipSuccess) {
-            err = std::string("device upload failed: ") + hipGetErrorString(e);
-            return TM_EDEVICE;
+            // the device still holds the previous epoch, intact (allocations come before any
+            // in-place write); the host copy has advanced: the next commit re-uploads it whole
+            epoch--;
+            need_full = true;
+            patch.reset();
+            patch.full = true;
+            err = std::string("device upload failed (the previous epoch keeps serving; the next commit "
+                              "uploads the index again): ") + hipGetErrorString(e);
+            return e == hipErrorOutOfMemory ? TM_ENOMEM : TM_EDEVICE;
         }
         commit_us[0] = t1 - t0;
         commit_us[1] = t2 - t1;
         commit_us[2] = now_us() - t2;
-        if (need_full) n_full_rebuilds++;
+        if (was_full) n_full_rebuilds++;
         else n_delta_commits++;
         need_full = false;
         words_full = false;
@@ -1148,7 +1594,6 @@ struct tm_engine {
         dirty_arena.clear();
         for (uint32_t h : free_pending) free_keys.push_back(h);
         free_pending.clear();
-        epoch++;
         return TM_OK;
     }
 
@@ -1260,18 +1705,13 @@ struct tm_engine {
         DevBuf d_kw, d_koff, d_kh;
         DevBuf d_qw, d_qoff, d_qdollar, d_qstatus, d_cnt, d_off, d_out, d_scan, d_pool, d_ctl, d_jobs, d_krec;
         uint64_t out_want = 1 << 16, pool_want = 1024;  // one-pass sizes (from the demand seen)
-        std::vector<uint32_t> qw, qoff, h_off, h_cnt, u_keys;
+        std::vector<uint32_t> qw, qoff;
         std::vector<uint32_t> wcode;     // interned word id -> order code (NONE: not cached yet)
-        PinBuf h_keys;                   // walk output (pinned: it can be GBs)
         std::vector<uint8_t> qdollar;
-        std::vector<int32_t> qstatus;
         uint64_t n_onepass = 0, n_twopass = 0;  // batches by path (tests / bench)
     } fx;
     // intersection/2 batches (filter_kernels.hip k_intersect)
     DevBuf d_ia, d_iaoff, d_ib, d_iboff, d_iout, d_ilen;
-    std::vector<uint64_t> ix_off;
-    std::vector<int32_t> ix_len;
-    std::vector<uint8_t> ix_bytes;
 
     static void split_words(const uint8_t *p, size_t n, std::vector<std::pair<size_t, size_t>> &out) {
         out.clear();
@@ -1420,6 +1860,8 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     if (!eng) return TM_ENOMEM;
     if (cfg) eng->cfg = *cfg;
     eng->patch.on = (eng->cfg.flags & TM_CFG_RECORD_PATCH) != 0;
+    eng->master_nonce = mix64((uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() ^
+                              (uint64_t)(uintptr_t)eng) | 1ull;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= eng->cfg.device || eng->cfg.device < 0) {
         delete eng;
@@ -1432,9 +1874,14 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
         return TM_EDEVICE;  // kernels are built for gfx950 only
     }
     if (hipSetDevice(eng->cfg.device) != hipSuccess ||
-        hipStreamCreateWithFlags(&eng->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete eng;
+        hipStreamCreateWithFlags(&eng->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&eng->s_build, hipStreamNonBlocking) != hipSuccess) {
+        tm_destroy(eng);
         return TM_EDEVICE;
+    }
+    if (!eng->reserve_ids()) {
+        tm_destroy(eng);
+        return TM_ENOMEM;
     }
     uint64_t rk = eng->cfg.reserve_keys ? eng->cfg.reserve_keys : 1024;
     uint64_t rn = eng->cfg.reserve_nodes ? eng->cfg.reserve_nodes : rk * 4;
@@ -1452,7 +1899,11 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     eng->kset_rehash(next_pow2(std::max<uint64_t>(rk * 2, 1024)));
     eng->keys.reserve(rk);
     eng->need_full = true;
-    int rc = eng->commit();  // empty epoch 1: device tables exist from the start
+    int rc;
+    {
+        std::lock_guard<std::mutex> g(eng->mu_commit);
+        rc = eng->commit(nullptr);  // empty epoch 1: device tables exist from the start
+    }
     if (rc != TM_OK) {
         tm_destroy(eng);
         return rc;
@@ -1464,25 +1915,27 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
 void tm_destroy(tm_engine *eng) {
     if (!eng) return;
     (void)hipSetDevice(eng->cfg.device);
-    if (eng->stream) (void)hipStreamSynchronize(eng->stream);
-    for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_dd_wl,
-                      &eng->d_dd_wl_n, &eng->d_ukeys, &eng->d_ucnt,
-                      &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
+    (void)eng->quiesce();
+    if (eng->s_build) (void)hipStreamSynchronize(eng->s_build);
+    for (auto &u : eng->uses) (void)hipEventDestroy(u.second);
+    eng->uses.clear();
+    if (eng->ev_chain) (void)hipEventDestroy(eng->ev_chain);
+    for (auto &o : eng->outs) o.second->release();
+    eng->outs.clear();
+    eng->release_ids();
+    eng->bb_dev.release();
+    eng->bb_host.release();
+    eng->h_rctl.release();
+    for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
                       &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan, &eng->fx.d_pool,
                       &eng->fx.d_ctl, &eng->fx.d_jobs, &eng->fx.d_krec, &eng->d_ia, &eng->d_iaoff,
                       &eng->d_ib, &eng->d_iboff, &eng->d_iout, &eng->d_ilen})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
-                      &eng->d_arena, &eng->d_scatter_idx,
-                      &eng->d_scatter_src, &eng->d_bytes, &eng->d_off, &eng->d_outoff, &eng->d_outcnt,
-                      &eng->d_status, &eng->d_keys, &eng->d_ctl, &eng->d_slow_list,
-                      &eng->d_scr_w, &eng->d_scr_s, &eng->d_stats, &eng->d_seg_pool,
-                      &eng->d_fr_pool, &eng->d_wave_chunks})
+                      &eng->d_arena, &eng->d_scatter_idx, &eng->d_scatter_src, &eng->d_stats})
         b->release();
-    for (PinBuf *b : {&eng->h_bytes, &eng->h_off, &eng->h_outoff, &eng->h_outcnt, &eng->h_status, &eng->h_keys,
-                      &eng->h_cursor, &eng->fx.h_keys})
-        b->release();
+    for (PinBuf *b : {&eng->h_bytes, &eng->h_off, &eng->h_cursor}) b->release();
     if (eng->ev_fast0) (void)hipEventDestroy(eng->ev_fast0);
     if (eng->ev_fast1) (void)hipEventDestroy(eng->ev_fast1);
     if (eng->s_pipe) (void)hipStreamSynchronize(eng->s_pipe);
@@ -1490,6 +1943,7 @@ void tm_destroy(tm_engine *eng) {
         if (e) (void)hipEventDestroy(e);
     eng->h_pctl.release();
     if (eng->s_pipe) (void)hipStreamDestroy(eng->s_pipe);
+    if (eng->s_build) (void)hipStreamDestroy(eng->s_build);
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
     delete eng;
 }
@@ -1501,16 +1955,26 @@ static int grow_pools(tm_engine *eng);
 // block the batcher copied back); no kernel of this engine may be in flight
 __attribute__((visibility("hidden"))) void tmx_engine_pool_caps(const tm_engine *eng, uint64_t *seg_chunks,
                                                                uint64_t *fr_chunks) {
-    *seg_chunks = eng->cfg.seg_chunks ? ~0ull : eng->seg_chunks;  // fixed pools (test aid) never grow
-    *fr_chunks = eng->cfg.seg_chunks ? ~0ull : eng->fr_chunks;
+    std::lock_guard<std::recursive_mutex> g(const_cast<tm_engine *>(eng)->mu_dev);
+    const_cast<tm_engine *>(eng)->bb = const_cast<BatchBufs *>(&eng->bb_dev);
+    *seg_chunks = eng->cfg.seg_chunks ? ~0ull : eng->bb->seg_chunks;  // fixed pools (test aid) never grow
+    *fr_chunks = eng->cfg.seg_chunks ? ~0ull : eng->bb->fr_chunks;
 }
 __attribute__((visibility("hidden"))) int tmx_engine_grow_pools(tm_engine *eng, uint64_t seg_demand,
                                                                 uint64_t fr_demand) {
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    eng->bb = &eng->bb_dev;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
-    eng->seg_demand_last = seg_demand;
-    eng->fr_demand_last = fr_demand;
+    eng->bb->seg_demand_last = seg_demand;
+    eng->bb->fr_demand_last = fr_demand;
     return grow_pools(eng);
 }
+
+// library-internal (batcher.cpp): hold the engine's device lock across a window's whole
+// enqueue (walk, id compaction, the D2H of its results), so no other caller's batch lands
+// between them
+__attribute__((visibility("hidden"))) void tmx_engine_lock(tm_engine *eng) { eng->mu_dev.lock(); }
+__attribute__((visibility("hidden"))) void tmx_engine_unlock(tm_engine *eng) { eng->mu_dev.unlock(); }
 
 const char *tm_last_error(const tm_engine *eng) { return eng ? eng->err.c_str() : "null engine"; }
 
@@ -1529,6 +1993,7 @@ int tm_apply(tm_engine *eng, const tm_op *ops, size_t n) {
             return TM_EINVAL;
         }
     }
+    std::lock_guard<std::mutex> g(eng->mu_stage);
     eng->staged.reserve(eng->staged.size() + n);
     for (size_t i = 0; i < n; i++) {
         const tm_op &o = ops[i];
@@ -1548,6 +2013,7 @@ int tm_apply_packed(tm_engine *eng, uint32_t op, const uint8_t *bytes, const uin
             eng->err = "tm_apply_packed: bad filter offsets";
             return TM_EINVAL;
         }
+    std::lock_guard<std::mutex> g(eng->mu_stage);
     eng->staged.reserve(eng->staged.size() + n);
     uint64_t base = eng->stage_bytes.size();
     if (n) eng->stage_bytes.insert(eng->stage_bytes.end(), bytes + off[0], bytes + off[n]);
@@ -1561,46 +2027,77 @@ int tm_commit_epoch(tm_engine *eng, uint64_t *epoch_out) {
     if (!eng) return TM_EINVAL;
     if (eng->replica) return replica_refuses(eng, "tm_commit_epoch");
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
-    int rc = eng->commit();
+    std::lock_guard<std::mutex> g(eng->mu_commit);
+    HostOut *me = nullptr;
+    {
+        std::lock_guard<std::mutex> go(eng->mu_out);
+        auto it = eng->outs.find(std::this_thread::get_id());
+        if (it != eng->outs.end()) me = it->second.get();
+    }
+    int rc = eng->commit(me);
     if (epoch_out) *epoch_out = eng->epoch;
     return rc;
 }
 
+int tm_discard_staged(tm_engine *eng, uint64_t *n_out) {
+    if (!eng) return TM_EINVAL;
+    std::lock_guard<std::mutex> g(eng->mu_stage);
+    if (n_out) *n_out = eng->staged.size();
+    eng->staged.clear();
+    eng->stage_bytes.clear();
+    return TM_OK;
+}
+
+int tm_result_release(tm_engine *eng) {
+    if (!eng) return TM_EINVAL;
+    std::unique_ptr<HostOut> mine;
+    {
+        std::lock_guard<std::mutex> g(eng->mu_out);
+        auto it = eng->outs.find(std::this_thread::get_id());
+        if (it == eng->outs.end()) return TM_OK;
+        mine = std::move(it->second);
+        eng->outs.erase(it);
+    }
+    eng->lease_drop(*mine);
+    mine->release();
+    return TM_OK;
+}
+
 // Size the batch buffers for n topics / `bytes` topic bytes.
 static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
-    TM_TRY_HIP(eng->d_outoff.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_outcnt.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_status.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_slow_list.ensure((size_t)n * 4 + 4), TM_ENOMEM, "alloc");
-    if (!eng->d_ctl.p) {
-        TM_TRY_HIP(eng->d_ctl.ensure(2 * CTL_BYTES), TM_ENOMEM, "alloc");
-        TM_TRY_HIP(hipMemset(eng->d_ctl.p, 0, 2 * CTL_BYTES), TM_EDEVICE, "memset");  // both blocks start at 0
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_outoff, (size_t)n * 4 + 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_outcnt, (size_t)n * 4 + 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_status, (size_t)n * 4 + 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_slow_list, (size_t)n * 4 + 4), TM_ENOMEM, "alloc");
+    if (!eng->bb->d_ctl.p) {
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_ctl, 2 * CTL_BYTES), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(hipMemset(eng->bb->d_ctl.p, 0, 2 * CTL_BYTES), TM_EDEVICE, "memset");  // both blocks start at 0
     }
-    TM_TRY_HIP(eng->d_stats.ensure(256), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_scr_w.ensure((bytes + 2ull * n + 2) * 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_scr_s.ensure((bytes + 2ull * n + 2) * 8), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_wave_chunks.ensure(match_grid(n, pick_tpw(n, eng->cfg.topics_per_wave)) * SEG_MAXCHUNK * 4 + 4),
+    TM_TRY_HIP(eng->grow_buf(eng->d_stats, 256), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_scr_w, (bytes + 2ull * n + 2) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_scr_s, (bytes + 2ull * n + 2) * 8), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_wave_chunks, match_grid(n, pick_tpw(n, eng->cfg.topics_per_wave)) * SEG_MAXCHUNK * 4 + 4),
                TM_ENOMEM, "alloc");
     {
         // chunk pool for waves whose staged key segments overflow LDS
         uint64_t want = eng->cfg.seg_chunks ? eng->cfg.seg_chunks : std::max<uint64_t>(1024, ((uint64_t)n + 63) / 64 * 8);
-        if (want > eng->seg_chunks) {
-            TM_TRY_HIP(eng->d_seg_pool.ensure(want * SEG_CHUNK * sizeof(uint4)), TM_ENOMEM, "alloc seg pool");
-            eng->seg_chunks = want;
+        if (want > eng->bb->seg_chunks) {
+            TM_TRY_HIP(eng->grow_buf(eng->bb->d_seg_pool, want * SEG_CHUNK * sizeof(uint4)), TM_ENOMEM, "alloc seg pool");
+            eng->bb->seg_chunks = want;
         }
     }
     {
         // frontier overflow pool (waves whose per-depth frontier exceeds LDS)
         uint64_t want = eng->cfg.seg_chunks ? eng->cfg.seg_chunks : std::max<uint64_t>(1024, ((uint64_t)n + 63) / 64 * 4);
-        if (want > eng->fr_chunks) {
-            TM_TRY_HIP(eng->d_fr_pool.ensure(want * FR_CHUNK * sizeof(uint2)), TM_ENOMEM, "alloc frontier pool");
-            eng->fr_chunks = want;
+        if (want > eng->bb->fr_chunks) {
+            TM_TRY_HIP(eng->grow_buf(eng->bb->d_fr_pool, want * FR_CHUNK * sizeof(uint2)), TM_ENOMEM, "alloc frontier pool");
+            eng->bb->fr_chunks = want;
         }
     }
-    if (eng->keys_cap == 0) {
+    if (eng->bb->keys_cap == 0) {
         uint64_t want = eng->cfg.reserve_matches ? eng->cfg.reserve_matches : std::max<uint64_t>(n * 8ull, 1 << 16);
-        TM_TRY_HIP(eng->d_keys.ensure(want * 4), TM_ENOMEM, "alloc");
-        eng->keys_cap = want;
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, want * 4), TM_ENOMEM, "alloc");
+        eng->bb->keys_cap = want;
     }
     return TM_OK;
 }
@@ -1609,15 +2106,15 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
 // stay exact); size them to the observed demand for the next batch.
 static int grow_pools(tm_engine *eng) {
     if (eng->cfg.seg_chunks) return TM_OK;  // fixed by the caller (test aid)
-    if (eng->seg_demand_last > eng->seg_chunks) {
-        uint64_t want = eng->seg_demand_last + eng->seg_demand_last / 4 + 64;
-        TM_TRY_HIP(eng->d_seg_pool.ensure(want * SEG_CHUNK * sizeof(uint4)), TM_ENOMEM, "alloc seg pool");
-        eng->seg_chunks = want;
+    if (eng->bb->seg_demand_last > eng->bb->seg_chunks) {
+        uint64_t want = eng->bb->seg_demand_last + eng->bb->seg_demand_last / 4 + 64;
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_seg_pool, want * SEG_CHUNK * sizeof(uint4)), TM_ENOMEM, "alloc seg pool");
+        eng->bb->seg_chunks = want;
     }
-    if (eng->fr_demand_last > eng->fr_chunks) {
-        uint64_t want = eng->fr_demand_last + eng->fr_demand_last / 4 + 64;
-        TM_TRY_HIP(eng->d_fr_pool.ensure(want * FR_CHUNK * sizeof(uint2)), TM_ENOMEM, "alloc frontier pool");
-        eng->fr_chunks = want;
+    if (eng->bb->fr_demand_last > eng->bb->fr_chunks) {
+        uint64_t want = eng->bb->fr_demand_last + eng->bb->fr_demand_last / 4 + 64;
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_fr_pool, want * FR_CHUNK * sizeof(uint2)), TM_ENOMEM, "alloc frontier pool");
+        eng->bb->fr_chunks = want;
     }
     return TM_OK;
 }
@@ -1626,45 +2123,50 @@ static int grow_pools(tm_engine *eng) {
 // `keys_cap`: its key output (default: the whole arena)
 static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                                 hipStream_t s, uint32_t mode = MODE_ALL, uint32_t obase = 0, uint32_t *keys = nullptr,
-                                uint64_t keys_cap = 0) {
+                                uint64_t keys_cap = 0, unsigned long long *cursor = nullptr) {
     MatchArgs a{};
     a.mode = mode;
     a.tpw = pick_tpw(n, eng->cfg.topics_per_wave);
-    a.first_dfs = eng->n_deep ? 1u : 0u;
+    a.first_dfs = eng->dv.n_deep ? 1u : 0u;
     a.key_bin = eng->d_key_bin.as<uint32_t>();
     a.bytes = d_bytes;
     a.off = d_off;
     a.n = n;
     a.force_slow = (eng->cfg.flags & TM_CFG_FORCE_SLOW) ? 1u : 0u;
     a.wtab = eng->d_wtab.as<WordSlot>();
-    a.wmask = eng->wmask;
+    a.wmask = eng->dv.wmask;
     a.warena = eng->d_warena.as<uint8_t>();
     a.word_off = eng->d_word_off.as<uint32_t>();
     a.etab = eng->d_etab.as<EdgeSlot>();
     a.slot_list = eng->d_slot_list.as<uint32_t>();
-    a.emask = eng->emask;
+    a.emask = eng->dv.emask;
     a.root = eng->d_root.as<RootRec>();
     a.arena = eng->d_arena.as<uint32_t>();
-    a.out_off = eng->d_outoff.as<uint32_t>() + obase;
-    a.out_cnt = eng->d_outcnt.as<uint32_t>() + obase;
-    a.status = eng->d_status.as<int32_t>() + obase;
-    a.keys = keys ? keys : eng->d_keys.as<uint32_t>();
-    a.keys_cap = keys ? keys_cap : eng->keys_cap;
-    eng->ctl_cur ^= 1u;
-    eng->p_ctl = eng->d_ctl.as<uint8_t>() + eng->ctl_cur * CTL_BYTES;
-    a.cursor = (unsigned long long *)(eng->p_ctl + CTL_CURSOR);
-    a.ctl_next = (unsigned long long *)(eng->d_ctl.as<uint8_t>() + (eng->ctl_cur ^ 1u) * CTL_BYTES);
-    a.slow_list = eng->d_slow_list.as<uint32_t>();
-    a.slow_count = (uint32_t *)(eng->p_ctl + CTL_SLOW);
-    a.scratch_w = eng->d_scr_w.as<uint32_t>();
-    a.scratch_s = eng->d_scr_s.as<uint64_t>();
-    a.seg_pool = eng->d_seg_pool.as<uint4>();
-    a.seg_chunks = eng->seg_chunks;
-    a.seg_cursor = (unsigned long long *)(eng->p_ctl + CTL_SEG);
-    a.wave_chunks = eng->d_wave_chunks.as<uint32_t>();
-    a.fr_pool = eng->d_fr_pool.as<uint2>();
-    a.fr_chunks = eng->fr_chunks;
-    a.fr_cursor = (unsigned long long *)(eng->p_ctl + CTL_FR);
+    a.out_off = eng->bb->d_outoff.as<uint32_t>() + obase;
+    a.out_cnt = eng->bb->d_outcnt.as<uint32_t>() + obase;
+    a.status = eng->bb->d_status.as<int32_t>() + obase;
+    a.keys = keys ? keys : eng->bb->d_keys.as<uint32_t>();
+    a.keys_cap = keys ? keys_cap : eng->bb->keys_cap;
+    eng->bb->ctl_cur ^= 1u;
+    eng->bb->p_ctl = eng->bb->d_ctl.as<uint8_t>() + eng->bb->ctl_cur * CTL_BYTES;
+    a.cursor = cursor ? cursor : (unsigned long long *)(eng->bb->p_ctl + CTL_CURSOR);
+    if (mode == MODE_RUNS) {
+        a.out_kcnt = eng->bb->d_kcnt.as<uint32_t>() + obase;
+        a.span_arena = (uint64_t)(uintptr_t)eng->arena_id;
+        a.span_keys = eng->keys.empty() ? 0 : (uint64_t)(uintptr_t)&eng->keys[0].id;
+    }
+    a.ctl_next = (unsigned long long *)(eng->bb->d_ctl.as<uint8_t>() + (eng->bb->ctl_cur ^ 1u) * CTL_BYTES);
+    a.slow_list = eng->bb->d_slow_list.as<uint32_t>();
+    a.slow_count = (uint32_t *)(eng->bb->p_ctl + CTL_SLOW);
+    a.scratch_w = eng->bb->d_scr_w.as<uint32_t>();
+    a.scratch_s = eng->bb->d_scr_s.as<uint64_t>();
+    a.seg_pool = eng->bb->d_seg_pool.as<uint4>();
+    a.seg_chunks = eng->bb->seg_chunks;
+    a.seg_cursor = (unsigned long long *)(eng->bb->p_ctl + CTL_SEG);
+    a.wave_chunks = eng->bb->d_wave_chunks.as<uint32_t>();
+    a.fr_pool = eng->bb->d_fr_pool.as<uint2>();
+    a.fr_chunks = eng->bb->fr_chunks;
+    a.fr_cursor = (unsigned long long *)(eng->bb->p_ctl + CTL_FR);
     a.stats = eng->stats_on ? eng->d_stats.as<unsigned long long>() : nullptr;
     a.ev_fast0 = eng->timing_on ? eng->ev_fast0 : nullptr;
     a.ev_fast1 = eng->timing_on ? eng->ev_fast1 : nullptr;
@@ -1676,18 +2178,18 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
 static bool reduced_mode(uint32_t mode) { return mode == TM_MATCH_UNIQUE || mode == TM_MATCH_AGGRE; }
 
 static int enqueue_reduce(tm_engine *eng, uint32_t mode, uint32_t n, hipStream_t s) {
-    if (eng->ukeys_cap < eng->keys_cap) {
-        TM_TRY_HIP(eng->d_ukeys.ensure(eng->keys_cap * 4), TM_ENOMEM, "alloc reduced keys");
-        eng->ukeys_cap = eng->keys_cap;
+    if (eng->bb->ukeys_cap < eng->bb->keys_cap) {
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_ukeys, eng->bb->keys_cap * 4), TM_ENOMEM, "alloc reduced keys");
+        eng->bb->ukeys_cap = eng->bb->keys_cap;
     }
-    TM_TRY_HIP(eng->d_ucnt.ensure((uint64_t)n * 4 + 4), TM_ENOMEM, "alloc reduced counts");
-    TM_TRY_HIP(eng->d_dd_wl.ensure((uint64_t)n * 8), TM_ENOMEM, "alloc reducer worklist");
-    TM_TRY_HIP(eng->d_dd_wl_n.ensure(4), TM_ENOMEM, "alloc reducer worklist");
-    TM_TRY_HIP(launch_dedupe(mode == TM_MATCH_UNIQUE ? DD_UNIQUE : DD_AGGRE, eng->d_outcnt.as<uint32_t>(),
-                             eng->d_outoff.as<uint32_t>(), eng->d_keys.as<uint32_t>(), eng->keys_cap,
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_ucnt, (uint64_t)n * 4 + 4), TM_ENOMEM, "alloc reduced counts");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_dd_wl, (uint64_t)n * 8), TM_ENOMEM, "alloc reducer worklist");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_dd_wl_n, 4), TM_ENOMEM, "alloc reducer worklist");
+    TM_TRY_HIP(launch_dedupe(mode == TM_MATCH_UNIQUE ? DD_UNIQUE : DD_AGGRE, eng->bb->d_outcnt.as<uint32_t>(),
+                             eng->bb->d_outoff.as<uint32_t>(), eng->bb->d_keys.as<uint32_t>(), eng->bb->keys_cap,
                              eng->d_key_rec.as<uint64_t>(), eng->d_key_node.as<uint32_t>(),
-                             eng->d_key_dd.as<uint8_t>(), n, eng->d_ucnt.as<uint32_t>(), eng->d_ukeys.as<uint32_t>(),
-                             eng->d_dd_wl.as<uint2>(), eng->d_dd_wl_n.as<uint32_t>(), s),
+                             eng->d_key_dd.as<uint8_t>(), n, eng->bb->d_ucnt.as<uint32_t>(), eng->bb->d_ukeys.as<uint32_t>(),
+                             eng->bb->d_dd_wl.as<uint2>(), eng->bb->d_dd_wl_n.as<uint32_t>(), s),
                TM_EDEVICE, "dedupe");
     return TM_OK;
 }
@@ -1700,7 +2202,7 @@ static int enqueue_reduce(tm_engine *eng, uint32_t mode, uint32_t n, hipStream_t
 constexpr uint32_t PIPE_SUB = 262144;
 constexpr uint32_t PIPE_MAXSUB = 8;
 
-static int match_batch_pipelined(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n,
+static int match_batch_pipelined(tm_engine *eng, HostOut &o, const uint8_t *bytes, const uint32_t *off, uint32_t n,
                                  tm_result *out) {
     const uint32_t base = off[0];
     const uint64_t nbytes = (uint64_t)off[n] - base;
@@ -1711,11 +2213,11 @@ static int match_batch_pipelined(tm_engine *eng, const uint8_t *bytes, const uin
     if (rc) return rc;
     TM_TRY_HIP(eng->h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(eng->h_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->d_bytes.ensure(nbytes + 16), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->h_outoff.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->h_outcnt.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->h_status.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_bytes, nbytes + 16), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_off, ((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(o.h_outoff.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(o.h_outcnt.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(o.h_status.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(eng->h_pctl.ensure(2 * CTL_BYTES), TM_ENOMEM, "pinned alloc");
     if (!eng->s_pipe) {
         TM_TRY_HIP(hipStreamCreateWithFlags(&eng->s_pipe, hipStreamNonBlocking), TM_EDEVICE, "stream");
@@ -1724,12 +2226,12 @@ static int match_batch_pipelined(tm_engine *eng, const uint8_t *bytes, const uin
     }
     // each half of the key arena holds one sub-batch; sized from the last pipelined batch
     const uint64_t est_sub = (uint64_t)(eng->pipe_kpt * (double)(n / S + 1) * 1.15) + 4096;
-    if (eng->keys_cap < 2 * est_sub) {
-        TM_TRY_HIP(eng->d_keys.ensure(2 * est_sub * 4), TM_ENOMEM, "alloc keys");
-        eng->keys_cap = 2 * est_sub;
+    if (eng->bb->keys_cap < 2 * est_sub) {
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, 2 * est_sub * 4), TM_ENOMEM, "alloc keys");
+        eng->bb->keys_cap = 2 * est_sub;
     }
-    uint64_t hc = eng->keys_cap / 2;
-    TM_TRY_HIP(eng->h_keys.ensure((size_t)(eng->pipe_kpt * (double)n * 1.1) * 4 + 4), TM_ENOMEM, "pinned alloc");
+    uint64_t hc = eng->bb->keys_cap / 2;
+    TM_TRY_HIP(o.h_keys.ensure((size_t)(eng->pipe_kpt * (double)n * 1.1) * 4 + 4), TM_ENOMEM, "pinned alloc");
     hipStream_t s = eng->stream, c = eng->s_pipe;
     uint8_t *hb8 = eng->h_bytes.as<uint8_t>(), *hctl = eng->h_pctl.as<uint8_t>();
     uint32_t *ho = eng->h_off.as<uint32_t>();
@@ -1741,9 +2243,9 @@ static int match_batch_pipelined(tm_engine *eng, const uint8_t *bytes, const uin
         if (bhi > blo) memcpy(hb8 + blo, bytes + base + blo, bhi - blo);
         for (uint32_t i = lo; i <= hi; i++) ho[i] = off[i] - base;
         if (bhi > blo)
-            TM_TRY_HIP(hipMemcpyAsync(eng->d_bytes.as<uint8_t>() + blo, hb8 + blo, bhi - blo, hipMemcpyHostToDevice, s),
+            TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_bytes.as<uint8_t>() + blo, hb8 + blo, bhi - blo, hipMemcpyHostToDevice, s),
                        TM_EDEVICE, "H2D");
-        TM_TRY_HIP(hipMemcpyAsync(eng->d_off.as<uint32_t>() + lo, ho + lo, ((size_t)hi - lo + 1) * 4,
+        TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_off.as<uint32_t>() + lo, ho + lo, ((size_t)hi - lo + 1) * 4,
                                   hipMemcpyHostToDevice, s),
                    TM_EDEVICE, "H2D");
         return TM_OK;
@@ -1751,11 +2253,11 @@ static int match_batch_pipelined(tm_engine *eng, const uint8_t *bytes, const uin
     auto walk = [&](uint32_t j) -> int {  // sub-batch j walks into key half j % 2
         const uint32_t lo = b[j], hi = b[j + 1], h = j & 1;
         if (j >= 2) TM_TRY_HIP(hipStreamWaitEvent(s, eng->ev_pd[h], 0), TM_EDEVICE, "wait");  // half's last D2H
-        eng->last_n = hi - lo;
-        TM_TRY_HIP(enqueue_match(eng, eng->d_bytes.as<uint8_t>(), eng->d_off.as<uint32_t>() + lo, hi - lo, s, MODE_ALL,
-                                 lo, eng->d_keys.as<uint32_t>() + h * hc, hc),
+        eng->bb->last_n = hi - lo;
+        TM_TRY_HIP(enqueue_match(eng, eng->bb->d_bytes.as<uint8_t>(), eng->bb->d_off.as<uint32_t>() + lo, hi - lo, s, MODE_ALL,
+                                 lo, eng->bb->d_keys.as<uint32_t>() + h * hc, hc),
                    TM_EDEVICE, "kernel launch");
-        TM_TRY_HIP(hipMemcpyAsync(hctl + h * CTL_BYTES, eng->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+        TM_TRY_HIP(hipMemcpyAsync(hctl + h * CTL_BYTES, eng->bb->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                    "D2H");
         TM_TRY_HIP(hipEventRecord(eng->ev_pk[h], s), TM_EDEVICE, "event");
         return TM_OK;
@@ -1771,23 +2273,23 @@ static int match_batch_pipelined(tm_engine *eng, const uint8_t *bytes, const uin
         slow += *(const uint32_t *)(ctl + 8);
         seg_d = std::max(seg_d, *(const uint64_t *)(ctl + 16));
         fr_d = std::max(fr_d, *(const uint64_t *)(ctl + 24));
-        if ((hbase + total) * 4 + 4 > eng->h_keys.cap) {  // more keys than estimated: grow, keeping what landed
+        if ((hbase + total) * 4 + 4 > o.h_keys.cap) {  // more keys than estimated: grow, keeping what landed
             TM_TRY_HIP(hipStreamSynchronize(c), TM_EDEVICE, "D2H");
             PinBuf nb;
             TM_TRY_HIP(nb.ensure((hbase + total) * 8 + 4), TM_ENOMEM, "pinned alloc");
-            if (hbase) memcpy(nb.p, eng->h_keys.p, hbase * 4);
-            std::swap(nb.p, eng->h_keys.p);
-            std::swap(nb.cap, eng->h_keys.cap);
+            if (hbase) memcpy(nb.p, o.h_keys.p, hbase * 4);
+            std::swap(nb.p, o.h_keys.p);
+            std::swap(nb.cap, o.h_keys.cap);
             nb.release();
         }
         TM_TRY_HIP(hipStreamWaitEvent(c, eng->ev_pk[h], 0), TM_EDEVICE, "wait");
         if (total)
-            TM_TRY_HIP(hipMemcpyAsync(eng->h_keys.as<uint32_t>() + hbase, eng->d_keys.as<uint32_t>() + h * hc, total * 4,
+            TM_TRY_HIP(hipMemcpyAsync(o.h_keys.as<uint32_t>() + hbase, eng->bb->d_keys.as<uint32_t>() + h * hc, total * 4,
                                       hipMemcpyDeviceToHost, c),
                        TM_EDEVICE, "D2H");
-        for (std::pair<PinBuf *, DevBuf *> pr : {std::make_pair(&eng->h_outoff, &eng->d_outoff),
-                                                 std::make_pair(&eng->h_outcnt, &eng->d_outcnt),
-                                                 std::make_pair(&eng->h_status, &eng->d_status)})
+        for (std::pair<PinBuf *, DevBuf *> pr : {std::make_pair(&o.h_outoff, &eng->bb->d_outoff),
+                                                 std::make_pair(&o.h_outcnt, &eng->bb->d_outcnt),
+                                                 std::make_pair(&o.h_status, &eng->bb->d_status)})
             TM_TRY_HIP(hipMemcpyAsync(pr.first->as<uint32_t>() + lo, pr.second->as<uint32_t>() + lo,
                                       ((size_t)hi - lo) * 4, hipMemcpyDeviceToHost, c),
                        TM_EDEVICE, "D2H");
@@ -1808,8 +2310,8 @@ static int match_batch_pipelined(tm_engine *eng, const uint8_t *bytes, const uin
             TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "sync");
             TM_TRY_HIP(hipStreamSynchronize(c), TM_EDEVICE, "sync");
             const uint64_t want = 2 * (need + need / 8 + 1024);
-            TM_TRY_HIP(eng->d_keys.ensure(want * 4), TM_ENOMEM, "alloc keys");
-            eng->keys_cap = want;
+            TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, want * 4), TM_ENOMEM, "alloc keys");
+            eng->bb->keys_cap = want;
             hc = want / 2;
             if ((rc = walk(j)) || (j + 1 < S && (rc = walk(j + 1)))) return rc;
             rc = finish(j);
@@ -1819,21 +2321,21 @@ static int match_batch_pipelined(tm_engine *eng, const uint8_t *bytes, const uin
     }
     TM_TRY_HIP(hipStreamSynchronize(c), TM_EDEVICE, "D2H");
     // sub-batch offsets are relative to its own keys: rebase onto the joined array
-    uint32_t *oo = eng->h_outoff.as<uint32_t>();
+    uint32_t *oo = o.h_outoff.as<uint32_t>();
     for (uint32_t j = 1; j < S; j++)
         for (uint32_t i = b[j]; i < b[j + 1]; i++) oo[i] += (uint32_t)hb[j];
     eng->n_slow_last = slow;
-    eng->seg_demand_last = seg_d;
-    eng->fr_demand_last = fr_d;
+    eng->bb->seg_demand_last = seg_d;
+    eng->bb->fr_demand_last = fr_d;
     if ((rc = grow_pools(eng))) return rc;
     eng->pipe_kpt = (double)hbase / n;
-    eng->dev_batch = false;  // the device holds sub-batches, not this batch
-    eng->last_n = 0;
+    eng->bb->dev_batch = false;  // the device holds sub-batches, not this batch
+    eng->bb->last_n = 0;
     out->total = hbase;
     out->off = oo;
-    out->cnt = eng->h_outcnt.as<uint32_t>();
-    out->keys = eng->h_keys.as<uint32_t>();
-    out->status = eng->h_status.as<int32_t>();
+    out->cnt = o.h_outcnt.as<uint32_t>();
+    out->keys = o.h_keys.as<uint32_t>();
+    out->status = o.h_status.as<int32_t>();
     return TM_OK;
 }
 
@@ -1841,22 +2343,24 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
                    tm_result *out) {
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
     if (mode > TM_MATCH_AGGRE) return TM_EINVAL;
-    if (eng->edge_full) return TM_ESTATE;
-    if (!eng->staged.empty()) {
-        eng->err = "tm_match_batch: staged ops not committed";
-        return TM_ESTATE;
-    }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    // UNIQUE may reduce on the host (keys deeper than the device order code): term order of
+    // keys needs the host copy, so that mode also holds mu_host (taken before mu_dev)
+    std::unique_lock<std::mutex> gh(eng->mu_host, std::defer_lock);
+    if (mode == TM_MATCH_UNIQUE && !eng->replica) gh.lock();
+    std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+    eng->bb = &eng->bb_host;
+    HostOut &o = eng->out();
     memset(out, 0, sizeof(*out));
     out->n = n;
     // UNIQUE is reduced on the GPU unless a key is too deep for the device order code
-    const bool dev_reduce = reduced_mode(mode) && (mode == TM_MATCH_AGGRE || eng->n_deep == 0);
+    const bool dev_reduce = reduced_mode(mode) && (mode == TM_MATCH_AGGRE || eng->dv.n_deep == 0);
     if (reduced_mode(mode) && !dev_reduce && eng->replica) return replica_refuses(eng, "tm_match_batch (host UNIQUE)");
-    eng->last_mode = (reduced_mode(mode) && !dev_reduce) ? TM_MATCH_ALL : mode;  // what the device holds
+    eng->bb->last_mode = (reduced_mode(mode) && !dev_reduce) ? TM_MATCH_ALL : mode;  // what the device holds
     if (n == 0) return TM_OK;
     if (mode == TM_MATCH_ALL && n >= 2 * PIPE_SUB)
-        return match_batch_pipelined(eng, bytes, off, n, out);
-    eng->dev_batch = true;
+        return match_batch_pipelined(eng, o, bytes, off, n, out);
+    eng->bb->dev_batch = true;
     // rebase offsets to 0
     uint32_t base = off[0];
     uint64_t nbytes = (uint64_t)off[n] - base;
@@ -1864,65 +2368,65 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
     if (rc) return rc;
     TM_TRY_HIP(eng->h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(eng->h_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->d_bytes.ensure(nbytes + 16), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_bytes, nbytes + 16), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_off, ((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
     if (nbytes) memcpy(eng->h_bytes.p, bytes + base, nbytes);
     uint32_t *ho = eng->h_off.as<uint32_t>();
     for (uint32_t i = 0; i <= n; i++) ho[i] = off[i] - base;
     hipStream_t s = eng->stream;
-    TM_TRY_HIP(hipMemcpyAsync(eng->d_bytes.p, eng->h_bytes.p, nbytes + 1, hipMemcpyHostToDevice, s), TM_EDEVICE,
+    TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_bytes.p, eng->h_bytes.p, nbytes + 1, hipMemcpyHostToDevice, s), TM_EDEVICE,
                "H2D");
-    TM_TRY_HIP(hipMemcpyAsync(eng->d_off.p, ho, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
+    TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_off.p, ho, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
     TM_TRY_HIP(eng->h_cursor.ensure(64), TM_ENOMEM, "pinned alloc");
     // FIRST runs k_match_first (<= 1 key per topic); COUNT skips the key copy-out
     const uint32_t kmode = mode == TM_MATCH_FIRST ? MODE_FIRST : (mode == TM_MATCH_COUNT ? MODE_COUNT : MODE_ALL);
-    if (kmode == MODE_FIRST && eng->keys_cap < n) {
-        TM_TRY_HIP(eng->d_keys.ensure((uint64_t)n * 4), TM_ENOMEM, "alloc keys");
-        eng->keys_cap = n;
+    if (kmode == MODE_FIRST && eng->bb->keys_cap < n) {
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, (uint64_t)n * 4), TM_ENOMEM, "alloc keys");
+        eng->bb->keys_cap = n;
     }
     for (int attempt = 0; attempt < 2; attempt++) {
-        eng->last_n = n;
-        TM_TRY_HIP(enqueue_match(eng, eng->d_bytes.as<uint8_t>(), eng->d_off.as<uint32_t>(), n, s, kmode), TM_EDEVICE,
+        eng->bb->last_n = n;
+        TM_TRY_HIP(enqueue_match(eng, eng->bb->d_bytes.as<uint8_t>(), eng->bb->d_off.as<uint32_t>(), n, s, kmode), TM_EDEVICE,
                    "kernel launch");
         // the counter block has the host layout: cursor @0, slow_count @8, seg @16, fr @24
-        TM_TRY_HIP(hipMemcpyAsync(eng->h_cursor.p, eng->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+        TM_TRY_HIP(hipMemcpyAsync(eng->h_cursor.p, eng->bb->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                    "D2H");
         TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "match kernels");
         uint64_t total = *eng->h_cursor.as<uint64_t>();
         eng->n_slow_last = *(uint32_t *)((uint8_t *)eng->h_cursor.p + 8);
-        eng->seg_demand_last = *(uint64_t *)((uint8_t *)eng->h_cursor.p + 16);
-        eng->fr_demand_last = *(uint64_t *)((uint8_t *)eng->h_cursor.p + 24);
-        if (kmode != MODE_ALL || total <= eng->keys_cap) break;
+        eng->bb->seg_demand_last = *(uint64_t *)((uint8_t *)eng->h_cursor.p + 16);
+        eng->bb->fr_demand_last = *(uint64_t *)((uint8_t *)eng->h_cursor.p + 24);
+        if (kmode != MODE_ALL || total <= eng->bb->keys_cap) break;
         // output arena too small: grow to the demand and run again (once suffices:
         // the cursor counts every key the batch asked for)
         uint64_t want = total + total / 8 + 1024;
-        TM_TRY_HIP(eng->d_keys.ensure(want * 4), TM_ENOMEM, "alloc keys");
-        eng->keys_cap = want;
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, want * 4), TM_ENOMEM, "alloc keys");
+        eng->bb->keys_cap = want;
     }
     uint64_t total = kmode == MODE_ALL ? *eng->h_cursor.as<uint64_t>() : (kmode == MODE_FIRST ? n : 0);
     if (dev_reduce && (rc = enqueue_reduce(eng, mode, n, s))) return rc;
-    TM_TRY_HIP(eng->h_outoff.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->h_outcnt.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->h_status.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->h_keys.ensure(total * 4 + 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(hipMemcpyAsync(eng->h_outoff.p, eng->d_outoff.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+    TM_TRY_HIP(o.h_outoff.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(o.h_outcnt.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(o.h_status.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(o.h_keys.ensure(total * 4 + 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(hipMemcpyAsync(o.h_outoff.p, eng->bb->d_outoff.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                "D2H");
-    TM_TRY_HIP(hipMemcpyAsync(eng->h_outcnt.p, (dev_reduce ? eng->d_ucnt : eng->d_outcnt).p, (size_t)n * 4,
+    TM_TRY_HIP(hipMemcpyAsync(o.h_outcnt.p, (dev_reduce ? eng->bb->d_ucnt : eng->bb->d_outcnt).p, (size_t)n * 4,
                               hipMemcpyDeviceToHost, s),
                TM_EDEVICE, "D2H");
-    TM_TRY_HIP(hipMemcpyAsync(eng->h_status.p, eng->d_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+    TM_TRY_HIP(hipMemcpyAsync(o.h_status.p, eng->bb->d_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                "D2H");
     if (total)
-        TM_TRY_HIP(hipMemcpyAsync(eng->h_keys.p, eng->d_keys.p, total * 4,
+        TM_TRY_HIP(hipMemcpyAsync(o.h_keys.p, eng->bb->d_keys.p, total * 4,
                                   hipMemcpyDeviceToHost, s),
                    TM_EDEVICE, "D2H");
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "D2H");
     if ((rc = grow_pools(eng))) return rc;
     out->total = total;
-    out->off = eng->h_outoff.as<uint32_t>();
-    out->cnt = eng->h_outcnt.as<uint32_t>();
-    out->keys = eng->h_keys.as<uint32_t>();
-    out->status = eng->h_status.as<int32_t>();
+    out->off = o.h_outoff.as<uint32_t>();
+    out->cnt = o.h_outcnt.as<uint32_t>();
+    out->keys = o.h_keys.as<uint32_t>();
+    out->status = o.h_status.as<int32_t>();
     if (mode == TM_MATCH_ALL) return TM_OK;
     if (dev_reduce) {  // reduced lists sit at the full result's offsets, with gaps
         uint64_t t = 0;
@@ -1931,44 +2435,44 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
         return TM_OK;
     }
     if (mode == TM_MATCH_COUNT) {  // counts only: no keys
-        eng->pp_off.assign(n, 0);
-        out->off = eng->pp_off.data();
+        o.pp_off.assign(n, 0);
+        out->off = o.pp_off.data();
         out->keys = nullptr;
         out->total = 0;
         return TM_OK;
     }
     if (mode == TM_MATCH_FIRST) {  // k_match_first wrote topic i's key (if any) at keys[i]: compact
-        eng->pp_off.resize(n);
-        eng->pp_keys.clear();
+        o.pp_off.resize(n);
+        o.pp_keys.clear();
         for (uint32_t i = 0; i < n; i++) {
-            eng->pp_off[i] = (uint32_t)eng->pp_keys.size();
-            if (out->cnt[i]) eng->pp_keys.push_back(out->keys[i]);
+            o.pp_off[i] = (uint32_t)o.pp_keys.size();
+            if (out->cnt[i]) o.pp_keys.push_back(out->keys[i]);
         }
-        out->off = eng->pp_off.data();
-        out->keys = eng->pp_keys.data();
-        out->total = eng->pp_keys.size();
+        out->off = o.pp_off.data();
+        out->keys = o.pp_keys.data();
+        out->total = o.pp_keys.size();
         return TM_OK;
     }
 
     // UNIQUE with a key deeper than the device order code: reduce each topic's set under
     // ETS term order here.
-    eng->pp_off.resize(n);
-    eng->pp_cnt.resize(n);
-    eng->pp_keys.clear();
+    o.pp_off.resize(n);
+    o.pp_cnt.resize(n);
+    o.pp_keys.clear();
     std::vector<uint32_t> tmp;
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t *ks = out->keys + out->off[i];
         uint32_t c = out->cnt[i];
-        eng->pp_off[i] = (uint32_t)eng->pp_keys.size();
+        o.pp_off[i] = (uint32_t)o.pp_keys.size();
         if (c == 0) {
-            eng->pp_cnt[i] = 0;
+            o.pp_cnt[i] = 0;
             continue;
         }
         tmp.assign(ks, ks + c);
         std::sort(tmp.begin(), tmp.end(), [&](uint32_t a, uint32_t b) { return eng->cmp_keys(a, b) < 0; });
         if (mode == TM_MATCH_FIRST) {
-            eng->pp_keys.push_back(tmp[0]);
-            eng->pp_cnt[i] = 1;
+            o.pp_keys.push_back(tmp[0]);
+            o.pp_cnt[i] = 1;
         } else {
             // maps:put in ascending walk order: the last (greatest) key per id wins,
             // maps:values/1 returns them ordered by id (small maps are sorted).
@@ -1982,23 +2486,25 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
                 else best[ins.first->second].second = k;
             }
             std::sort(best.begin(), best.end());
-            for (auto &p : best) eng->pp_keys.push_back(p.second);
-            eng->pp_cnt[i] = (uint32_t)best.size();
+            for (auto &p : best) o.pp_keys.push_back(p.second);
+            o.pp_cnt[i] = (uint32_t)best.size();
         }
     }
-    out->off = eng->pp_off.data();
-    out->cnt = eng->pp_cnt.data();
-    out->keys = eng->pp_keys.data();
-    out->total = eng->pp_keys.size();
+    out->off = o.pp_off.data();
+    out->cnt = o.pp_cnt.data();
+    out->keys = o.pp_keys.data();
+    out->total = o.pp_keys.size();
     return TM_OK;
 }
 
 int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap) {
     if (!eng) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
-    if (keys_cap > eng->keys_cap) {
-        TM_TRY_HIP(eng->d_keys.ensure(keys_cap * 4), TM_ENOMEM, "alloc keys");
-        eng->keys_cap = keys_cap;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    eng->bb = &eng->bb_dev;  // the tm_match_device* path (host calls size their own output)
+    if (keys_cap > eng->bb->keys_cap) {
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, keys_cap * 4), TM_ENOMEM, "alloc keys");
+        eng->bb->keys_cap = keys_cap;
     }
     (void)topics_cap;
     return TM_OK;
@@ -2012,55 +2518,57 @@ int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_of
 int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                          uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out) {
     if (mode > TM_MATCH_AGGRE) return TM_EINVAL;
-    if (!eng || eng->edge_full) return eng ? TM_ESTATE : TM_EINVAL;
-    if (mode == TM_MATCH_UNIQUE && eng->n_deep) {
+    if (!eng || !out || !d_off || (n && !d_bytes)) return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    eng->bb = &eng->bb_dev;
+    if (mode == TM_MATCH_UNIQUE && eng->dv.n_deep) {
         eng->err = "tm_match_device_mode: UNIQUE with filters deeper than 31 levels is host-only (tm_match_batch)";
         return TM_ESTATE;
     }
-    if (!eng || !out || !d_off || (n && !d_bytes)) return TM_EINVAL;
-    if (!eng->staged.empty()) {
-        eng->err = "tm_match_device: staged ops not committed";
-        return TM_ESTATE;
-    }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    // the batch buffers are reused: after everything queued behind the previous batch
+    TM_TRY_HIP(eng->chain_after_last(s), TM_EDEVICE, "stream order");
     // total_bytes = d_off[n] - d_off[0] sizes the spill kernel's scratch
     int rc = ensure_batch(eng, n, total_bytes);
     if (rc) return rc;
-    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
     eng->last_stream = s;
-    eng->last_n = n;
+    eng->bb->last_n = n;
     const uint32_t kmode = mode == TM_MATCH_FIRST ? MODE_FIRST : (mode == TM_MATCH_COUNT ? MODE_COUNT : MODE_ALL);
-    if (kmode == MODE_FIRST && eng->keys_cap < n) {
-        TM_TRY_HIP(eng->d_keys.ensure((uint64_t)n * 4), TM_ENOMEM, "alloc keys");
-        eng->keys_cap = n;
+    if (kmode == MODE_FIRST && eng->bb->keys_cap < n) {
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, (uint64_t)n * 4), TM_ENOMEM, "alloc keys");
+        eng->bb->keys_cap = n;
     }
     TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s, kmode), TM_EDEVICE, "kernel launch");
-    eng->last_mode = mode;
-    eng->dev_batch = true;
+    eng->bb->last_mode = mode;
+    eng->bb->dev_batch = true;
     if (reduced_mode(mode) && (rc = enqueue_reduce(eng, mode, n, s))) return rc;
+    TM_TRY_HIP(eng->note_use(s), TM_EDEVICE, "event");
     out->n = n;
-    out->d_off = eng->d_outoff.as<uint32_t>();
-    out->d_cnt = (reduced_mode(mode) ? eng->d_ucnt : eng->d_outcnt).as<uint32_t>();
-    out->d_keys = eng->d_keys.as<uint32_t>();  // reduced modes compact in place
-    out->d_status = eng->d_status.as<int32_t>();
-    out->d_total = (uint64_t *)(eng->p_ctl + CTL_CURSOR);
-    out->keys_cap = eng->keys_cap;
+    out->d_off = eng->bb->d_outoff.as<uint32_t>();
+    out->d_cnt = (reduced_mode(mode) ? eng->bb->d_ucnt : eng->bb->d_outcnt).as<uint32_t>();
+    out->d_keys = eng->bb->d_keys.as<uint32_t>();  // reduced modes compact in place
+    out->d_status = eng->bb->d_status.as<int32_t>();
+    out->d_total = (uint64_t *)(eng->bb->p_ctl + CTL_CURSOR);
+    out->keys_cap = eng->bb->keys_cap;
     return TM_OK;
 }
 
 int tm_device_sync(tm_engine *eng) {
     if (!eng) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    eng->bb = &eng->bb_dev;
     hipStream_t s = eng->last_stream ? eng->last_stream : eng->stream;
     TM_TRY_HIP(eng->h_cursor.ensure(64), TM_ENOMEM, "pinned alloc");
     uint8_t *h = (uint8_t *)eng->h_cursor.p;
-    if (eng->p_ctl)
-        TM_TRY_HIP(hipMemcpyAsync(h, eng->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+    if (eng->bb->p_ctl)
+        TM_TRY_HIP(hipMemcpyAsync(h, eng->bb->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "sync");
-    if (eng->p_ctl) {
+    if (eng->bb->p_ctl) {
         eng->n_slow_last = *(uint32_t *)(h + 8);
-        eng->seg_demand_last = *(uint64_t *)(h + 16);
-        eng->fr_demand_last = *(uint64_t *)(h + 24);
+        eng->bb->seg_demand_last = *(uint64_t *)(h + 16);
+        eng->bb->fr_demand_last = *(uint64_t *)(h + 24);
         return grow_pools(eng);
     }
     return TM_OK;
@@ -2073,21 +2581,24 @@ int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint
 int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out, uint32_t *d_flags,
                             void *stream) {
     if (!eng || !d_off_out || (ids_cap && !d_ids)) return TM_EINVAL;
-    if (!eng->p_ctl || !eng->dev_batch) {
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    eng->bb = &eng->bb_dev;
+    if (!eng->bb->p_ctl || !eng->bb->dev_batch) {
         eng->err = "tm_result_ids_device: no tm_match_device batch since the last (pipelined) tm_match_batch";
         return TM_ESTATE;
     }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     hipStream_t s = stream ? (hipStream_t)stream : (eng->last_stream ? eng->last_stream : eng->stream);
-    const uint32_t n = eng->last_n;
+    const uint32_t n = eng->bb->last_n;
     TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
-    const bool red = reduced_mode(eng->last_mode);
-    const uint32_t *cnt = (red ? eng->d_ucnt : eng->d_outcnt).as<uint32_t>();
+    const bool red = reduced_mode(eng->bb->last_mode);
+    const uint32_t *cnt = (red ? eng->bb->d_ucnt : eng->bb->d_outcnt).as<uint32_t>();
     TM_TRY_HIP(launch_excl_scan(cnt, 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s), TM_EDEVICE, "scan");
-    TM_TRY_HIP(launch_result_ids(cnt, eng->d_outoff.as<uint32_t>(), eng->d_keys.as<uint32_t>(),
-                                 eng->d_key_rec.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, eng->keys_cap,
-                                 (const unsigned long long *)(eng->p_ctl + CTL_CURSOR), d_flags, s),
+    TM_TRY_HIP(launch_result_ids(cnt, eng->bb->d_outoff.as<uint32_t>(), eng->bb->d_keys.as<uint32_t>(),
+                                 eng->d_key_rec.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, eng->bb->keys_cap,
+                                 (const unsigned long long *)(eng->bb->p_ctl + CTL_CURSOR), d_flags, s),
                TM_EDEVICE, "result ids");
+    TM_TRY_HIP(eng->note_use(s), TM_EDEVICE, "event");
     return TM_OK;
 }
 
@@ -2095,17 +2606,20 @@ int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, u
 // added is below 2^32 (TM_ESTATE otherwise)
 __attribute__((visibility("hidden"))) int tmx_result_ids32_device(tm_engine *eng, uint32_t *d_ids, uint64_t ids_cap,
                                                                   uint32_t *d_off_out, void *stream) {
-    if (eng->max_id > 0xFFFFFFFFull || eng->replica || !eng->dev_batch) return TM_ESTATE;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    eng->bb = &eng->bb_dev;
+    if (eng->dv.max_id > 0xFFFFFFFFull || eng->replica || !eng->bb->dev_batch) return TM_ESTATE;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     hipStream_t s = stream ? (hipStream_t)stream : (eng->last_stream ? eng->last_stream : eng->stream);
-    const uint32_t n = eng->last_n;
+    const uint32_t n = eng->bb->last_n;
     TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
-    const uint32_t *cnt = (reduced_mode(eng->last_mode) ? eng->d_ucnt : eng->d_outcnt).as<uint32_t>();
+    const uint32_t *cnt = (reduced_mode(eng->bb->last_mode) ? eng->bb->d_ucnt : eng->bb->d_outcnt).as<uint32_t>();
     TM_TRY_HIP(launch_excl_scan(cnt, 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s), TM_EDEVICE, "scan");
-    TM_TRY_HIP(launch_result_ids32(cnt, eng->d_outoff.as<uint32_t>(), eng->d_keys.as<uint32_t>(),
-                                   eng->d_key_rec.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, eng->keys_cap,
-                                   (const unsigned long long *)(eng->p_ctl + CTL_CURSOR), s),
+    TM_TRY_HIP(launch_result_ids32(cnt, eng->bb->d_outoff.as<uint32_t>(), eng->bb->d_keys.as<uint32_t>(),
+                                   eng->d_key_rec.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, eng->bb->keys_cap,
+                                   (const unsigned long long *)(eng->bb->p_ctl + CTL_CURSOR), s),
                TM_EDEVICE, "result ids");
+    TM_TRY_HIP(eng->note_use(s), TM_EDEVICE, "event");
     return TM_OK;
 }
 
@@ -2113,6 +2627,7 @@ int tm_merge_shards_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_
                            uint64_t stride, uint32_t *d_off_out, uint64_t *d_ids_out, uint64_t out_cap, void *stream) {
     if (!eng || G == 0 || !d_off_out || (n && (!d_counts || !d_ids)) || (out_cap && !d_ids_out)) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
     TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->d_mrg_roff.ensure((uint64_t)G * (n + 1) * 4), TM_ENOMEM, "alloc");
@@ -2151,6 +2666,7 @@ int tm_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64
 int tm_key_info(const tm_engine *eng, uint32_t key, uint64_t *id, uint32_t *flags, uint8_t *buf, uint32_t cap,
                 uint32_t *len) {
     if (!eng) return TM_EINVAL;
+    std::lock_guard<std::mutex> g(const_cast<tm_engine *>(eng)->mu_host);
     if (key >= eng->keys.size() || eng->keys[key].kind == K_FREE) return TM_ENOTFOUND;
     const KeyRec &k = eng->keys[key];
     if (id) *id = k.id;
@@ -2163,6 +2679,7 @@ int tm_key_info(const tm_engine *eng, uint32_t key, uint64_t *id, uint32_t *flag
 
 int tm_key_ids(const tm_engine *eng, const uint32_t *keys, size_t n, uint64_t *ids_out) {
     if (!eng || (n && (!keys || !ids_out))) return TM_EINVAL;
+    std::lock_guard<std::mutex> g(const_cast<tm_engine *>(eng)->mu_host);
     for (size_t i = 0; i < n; i++) {
         uint32_t k = keys[i];
         if (k >= eng->keys.size() || eng->keys[k].kind == K_FREE) return TM_ENOTFOUND;
@@ -2176,11 +2693,11 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
     if (mode != TM_MATCH_ALL && mode != TM_MATCH_UNIQUE && mode != TM_MATCH_FIRST) return TM_EINVAL;
     if (eng->replica) return replica_refuses(eng, "tm_match_filter_batch");
-    if (!eng->staged.empty()) {
-        eng->err = "tm_match_filter_batch: staged ops not committed";
-        return TM_ESTATE;
-    }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    // the walk's key index is built from the host copy (mu_host); it runs on the engine stream
+    std::lock_guard<std::mutex> gh(eng->mu_host);
+    std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+    HostOut &o = eng->out();
     memset(out, 0, sizeof(*out));
     out->n = n;
     if (n == 0) return TM_OK;
@@ -2191,7 +2708,7 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
     fx.qw.clear();
     fx.qoff.assign(1, 0);
     fx.qdollar.assign(n, 0);
-    fx.qstatus.assign(n, TM_TOPIC_OK);
+    o.f_status.assign(n, TM_TOPIC_OK);
     std::vector<std::pair<size_t, size_t>> lv;
     for (uint32_t i = 0; i < n; i++) {
         const char *t = (const char *)bytes + off[i];
@@ -2199,7 +2716,7 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
         tm_engine::split_words((const uint8_t *)t, tl, lv);
         for (size_t j = 0; j < lv.size(); j++) {
             uint32_t c = tm_engine::fx_level(t + lv[j].first, lv[j].second);
-            if (c == 0 && j + 1 < lv.size()) fx.qstatus[i] = TM_BADARG;  // '#' before the last level
+            if (c == 0 && j + 1 < lv.size()) o.f_status[i] = TM_BADARG;  // '#' before the last level
             if (c == NONE) {  // a literal: through the interner's hash table when it knows the word
                 const uint8_t *wp = (const uint8_t *)t + lv[j].first;
                 const uint32_t wl = (uint32_t)lv[j].second, wid = eng->word_lookup(wp, wl);
@@ -2230,7 +2747,7 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
     TM_TRY_HIP(hipMemcpyAsync(fx.d_qoff.p, fx.qoff.data(), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s), TM_EDEVICE,
                "H2D");
     TM_TRY_HIP(hipMemcpyAsync(fx.d_qdollar.p, fx.qdollar.data(), n, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
-    TM_TRY_HIP(hipMemcpyAsync(fx.d_qstatus.p, fx.qstatus.data(), (size_t)n * 4, hipMemcpyHostToDevice, s), TM_EDEVICE,
+    TM_TRY_HIP(hipMemcpyAsync(fx.d_qstatus.p, o.f_status.data(), (size_t)n * 4, hipMemcpyHostToDevice, s), TM_EDEVICE,
                "H2D");
     FilterArgs a{};
     a.kw = fx.d_kw.as<uint32_t>();
@@ -2246,8 +2763,8 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
     a.first = mode == TM_MATCH_FIRST;
     a.cnt = fx.d_cnt.as<uint32_t>();
     a.out_off = fx.d_off.as<uint32_t>();
-    fx.h_off.resize((size_t)n + 1);
-    fx.h_cnt.resize(n);
+    o.f_off.resize((size_t)n + 1);
+    o.f_cnt.resize(n);
     uint64_t total = 0;
     // One pass: the walk streams its keys into pooled chunks and copies them to a contiguous
     // range reserved at its end.  Sized from the demand of earlier batches; a batch that does
@@ -2274,16 +2791,16 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
         TM_TRY_HIP(launch_filter_walk(a, FW_ONEPASS, s), TM_EDEVICE, "k_filter_walk");
         TM_TRY_HIP(launch_filter_bulk(a, s), TM_EDEVICE, "k_filter_bulk");
         TM_TRY_HIP(hipMemcpyAsync(ctl, fx.d_ctl.p, 24, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
-        TM_TRY_HIP(hipMemcpyAsync(fx.h_off.data(), fx.d_off.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+        TM_TRY_HIP(hipMemcpyAsync(o.f_off.data(), fx.d_off.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                    "D2H");
-        TM_TRY_HIP(hipMemcpyAsync(fx.h_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+        TM_TRY_HIP(hipMemcpyAsync(o.f_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                    "D2H");
         TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk");
         total = ctl[0];
         if (total <= a.out_cap && ctl[1] <= a.pool_chunks) {
-            TM_TRY_HIP(fx.h_keys.ensure(std::max<uint64_t>(total, 1) * 4), TM_ENOMEM, "pinned alloc");
+            TM_TRY_HIP(o.f_keys.ensure(std::max<uint64_t>(total, 1) * 4), TM_ENOMEM, "pinned alloc");
             if (total) {
-                TM_TRY_HIP(hipMemcpyAsync(fx.h_keys.p, fx.d_out.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                TM_TRY_HIP(hipMemcpyAsync(o.f_keys.p, fx.d_out.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                            "D2H");
                 TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk");
             }
@@ -2296,15 +2813,15 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
         TM_TRY_HIP(launch_filter_walk(a, FW_COUNT, s), TM_EDEVICE, "k_filter_walk count");
         TM_TRY_HIP(launch_excl_scan(a.cnt, 1, n, fx.d_off.as<uint32_t>(), fx.d_scan.as<uint32_t>(), s), TM_EDEVICE,
                    "scan");
-        TM_TRY_HIP(hipMemcpyAsync(fx.h_off.data(), fx.d_off.p, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, s),
+        TM_TRY_HIP(hipMemcpyAsync(o.f_off.data(), fx.d_off.p, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, s),
                    TM_EDEVICE, "D2H");
-        TM_TRY_HIP(hipMemcpyAsync(fx.h_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+        TM_TRY_HIP(hipMemcpyAsync(o.f_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                    "D2H");
         TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk count");
         // the device scan is u32: a batch whose walks return 4 Gi keys or more is refused
         // before the emit pass could write past its offsets
         total = 0;
-        for (uint32_t i = 0; i < n; i++) total += fx.h_cnt[i];
+        for (uint32_t i = 0; i < n; i++) total += o.f_cnt[i];
         if (total >= 0xFFFFFFFFull) {
             eng->err = "tm_match_filter_batch: the batch returns 4 Gi keys or more; split it";
             return TM_ENOMEM;
@@ -2313,32 +2830,32 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
         // one partly filled chunk; a chunk holds FW_CHUNK / 2 - 1 ranges)
         fx.out_want = total + total / 4 + 1024;
         fx.pool_want = (total / (FW_CHUNK / 2 - 1) + n) + (total / (FW_CHUNK / 2 - 1) + n) / 4 + 64;
-        TM_TRY_HIP(fx.h_keys.ensure(std::max<uint64_t>(total, 1) * 4), TM_ENOMEM, "pinned alloc");
+        TM_TRY_HIP(o.f_keys.ensure(std::max<uint64_t>(total, 1) * 4), TM_ENOMEM, "pinned alloc");
         if (total) {
             TM_TRY_HIP(fx.d_out.ensure(total * 4), TM_ENOMEM, "alloc");
             a.out = fx.d_out.as<uint32_t>();
             TM_TRY_HIP(launch_filter_walk(a, FW_EMIT, s), TM_EDEVICE, "k_filter_walk emit");
-            TM_TRY_HIP(hipMemcpyAsync(fx.h_keys.p, fx.d_out.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+            TM_TRY_HIP(hipMemcpyAsync(o.f_keys.p, fx.d_out.p, total * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                        "D2H");
             TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk emit");
         }
     }
     out->total = total;
-    out->off = fx.h_off.data();
-    out->cnt = fx.h_cnt.data();
-    out->keys = fx.h_keys.as<uint32_t>();
-    out->status = fx.qstatus.data();
+    out->off = o.f_off.data();
+    out->cnt = o.f_cnt.data();
+    out->keys = o.f_keys.as<uint32_t>();
+    out->status = o.f_status.data();
     if (mode == TM_MATCH_UNIQUE) {
         // match_add/2 into a map (:350-352): the last key per id in walk order wins;
         // maps:values/1 lists them by id
-        fx.u_keys.clear();
+        o.f_ukeys.clear();
         std::vector<std::pair<uint64_t, uint32_t>> best;
         std::unordered_map<uint64_t, size_t> at;
         for (uint32_t i = 0; i < n; i++) {
             best.clear();
             at.clear();
-            for (uint32_t k = fx.h_off[i]; k < fx.h_off[i] + fx.h_cnt[i]; k++) {
-                const uint32_t h = fx.h_keys.as<uint32_t>()[k];
+            for (uint32_t k = o.f_off[i]; k < o.f_off[i] + o.f_cnt[i]; k++) {
+                const uint32_t h = o.f_keys.as<uint32_t>()[k];
                 const uint64_t id = eng->keys[h].id;
                 auto it = at.find(id);
                 if (it == at.end()) {
@@ -2349,12 +2866,12 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
                 }
             }
             std::sort(best.begin(), best.end());
-            fx.h_off[i] = (uint32_t)fx.u_keys.size();
-            fx.h_cnt[i] = (uint32_t)best.size();
-            for (auto &b : best) fx.u_keys.push_back(b.second);
+            o.f_off[i] = (uint32_t)o.f_ukeys.size();
+            o.f_cnt[i] = (uint32_t)best.size();
+            for (auto &b : best) o.f_ukeys.push_back(b.second);
         }
-        out->total = fx.u_keys.size();
-        out->keys = fx.u_keys.data();
+        out->total = o.f_ukeys.size();
+        out->keys = o.f_ukeys.data();
     }
     return TM_OK;
 }
@@ -2364,6 +2881,8 @@ int tm_intersect_batch(tm_engine *eng, const uint8_t *a, const uint32_t *a_off, 
     if (!eng || !out || (n && (!a_off || !b_off || (!a && a_off[n] > a_off[0]) || (!b && b_off[n] > b_off[0]))))
         return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    HostOut &o = eng->out();
     memset(out, 0, sizeof(*out));
     out->n = n;
     if (n == 0) return TM_OK;
@@ -2388,27 +2907,29 @@ int tm_intersect_batch(tm_engine *eng, const uint8_t *a, const uint32_t *a_off, 
     TM_TRY_HIP(launch_intersect(eng->d_ia.as<uint8_t>(), eng->d_iaoff.as<uint32_t>(), eng->d_ib.as<uint8_t>(),
                                 eng->d_iboff.as<uint32_t>(), n, eng->d_iout.as<uint8_t>(), eng->d_ilen.as<int32_t>(), s),
                TM_EDEVICE, "k_intersect");
-    eng->ix_len.resize(n);
-    eng->ix_bytes.resize(cap + 1);
-    TM_TRY_HIP(hipMemcpyAsync(eng->ix_len.data(), eng->d_ilen.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+    o.ix_len.resize(n);
+    o.ix_bytes.resize(cap + 1);
+    TM_TRY_HIP(hipMemcpyAsync(o.ix_len.data(), eng->d_ilen.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
                "D2H");
-    TM_TRY_HIP(hipMemcpyAsync(eng->ix_bytes.data(), eng->d_iout.p, cap, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+    TM_TRY_HIP(hipMemcpyAsync(o.ix_bytes.data(), eng->d_iout.p, cap, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_intersect");
-    eng->ix_off.resize(n);
-    for (uint32_t i = 0; i < n; i++) eng->ix_off[i] = (uint64_t)ao[i] + bo[i] + i;
-    out->off = eng->ix_off.data();
-    out->len = eng->ix_len.data();
-    out->bytes = eng->ix_bytes.data();
+    o.ix_off.resize(n);
+    for (uint32_t i = 0; i < n; i++) o.ix_off[i] = (uint64_t)ao[i] + bo[i] + i;
+    out->off = o.ix_off.data();
+    out->len = o.ix_len.data();
+    out->bytes = o.ix_bytes.data();
     return TM_OK;
 }
 
 int tm_stats(const tm_engine *eng, tm_stats_t *out) {
     if (!eng || !out) return TM_EINVAL;
+    std::lock_guard<std::mutex> gh(const_cast<tm_engine *>(eng)->mu_host);
+    std::lock_guard<std::recursive_mutex> gd(const_cast<tm_engine *>(eng)->mu_dev);
     memset(out, 0, sizeof(*out));
-    out->epoch = eng->epoch;
-    out->n_keys = eng->replica ? eng->rep_n_live : eng->n_live;
-    out->n_nodes = eng->replica ? eng->rep_n_nodes : eng->node_parent.size();
-    out->n_words = eng->replica ? eng->rep_n_words : eng->word_off.size();
+    out->epoch = eng->dv.epoch;
+    out->n_keys = eng->replica ? eng->dv.n_live : eng->n_live;
+    out->n_nodes = eng->replica ? eng->dv.n_nodes : eng->node_parent.size();
+    out->n_words = eng->replica ? eng->dv.n_words : eng->word_off.size();
     out->edge_slots = eng->replica ? eng->emask + 1 : eng->etab.size();
     out->word_slots = eng->replica ? eng->wmask + 1 : eng->wtab.size();
     out->list_words = eng->replica ? eng->dev_used[A_ARENA] / 4 : eng->arena.size();
@@ -2423,6 +2944,9 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
     out->n_deep_keys = eng->n_deep;
     out->n_filter_onepass = eng->fx.n_onepass;
     out->n_filter_twopass = eng->fx.n_twopass;
+    out->commit_stall_us = eng->commit_stall_us;
+    out->n_commits_refused = eng->n_commits_refused;
+    out->n_staged = const_cast<tm_engine *>(eng)->staged_count();
     return TM_OK;
 }
 
@@ -2433,6 +2957,7 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
 int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out18) {
     if (!eng) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     TM_TRY_HIP(eng->d_stats.ensure(256), TM_ENOMEM, "alloc");
     if (out18) {
         TM_TRY_HIP(hipDeviceSynchronize(), TM_EDEVICE, "sync");
@@ -2449,6 +2974,7 @@ int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out18) {
 int tm_debug_timing(tm_engine *eng, int enable, float *ms_out) {
     if (!eng) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     if (!eng->ev_fast0) {
         TM_TRY_HIP(hipEventCreate(&eng->ev_fast0), TM_EDEVICE, "event");
         TM_TRY_HIP(hipEventCreate(&eng->ev_fast1), TM_EDEVICE, "event");
@@ -2462,25 +2988,25 @@ int tm_debug_timing(tm_engine *eng, int enable, float *ms_out) {
 }
 
 // ---- replicated mode: device image + epoch patches (DESIGN.md §6 mode 1) ----------
+// Every array's used bytes come from dev_used (kept by each upload and scatter), and the
+// counts from the published view: the image is the epoch the device serves (mu_dev).
 static void image_layout(const tm_engine *eng, ImageHdr *h) {
     memset(h, 0, sizeof *h);
     h->magic = IMAGE_MAGIC;
-    h->epoch = eng->epoch;
-    h->wmask = eng->wmask;
-    h->emask = eng->emask;
-    h->n_deep = eng->n_deep;
-    h->n_live = eng->replica ? eng->rep_n_live : eng->n_live;
-    h->n_nodes = eng->replica ? eng->rep_n_nodes : eng->node_parent.size();
-    h->n_words = eng->replica ? eng->rep_n_words : eng->word_off.size();
-    const uint64_t nk = eng->keys.size();
-    const uint64_t used[A_N] = {eng->wtab.size() * 16, eng->warena_dev, eng->word_off_dev * 4, eng->etab.size() * 16,
-                                eng->slot_list.size() * 4, eng->arena_dev * 4, sizeof(RootRec), nk * 16, nk * 4, nk * 4,
-                                nk};
+    h->epoch = eng->dv.epoch;
+    h->wmask = eng->dv.wmask;
+    h->emask = eng->dv.emask;
+    h->n_deep = eng->dv.n_deep;
+    h->n_live = eng->dv.n_live;
+    h->n_nodes = eng->dv.n_nodes;
+    h->n_words = eng->dv.n_words;
+    h->nonce = eng->master_nonce;
+    h->max_id = eng->dv.max_id;
     uint64_t at = (sizeof(ImageHdr) + IMAGE_ALIGN - 1) / IMAGE_ALIGN * IMAGE_ALIGN;
     for (uint32_t a = 0; a < A_N; a++) {
         const DevBuf *b = const_cast<tm_engine *>(eng)->arr_buf(a);
         h->cap[a] = b->cap;
-        h->used[a] = eng->replica ? eng->dev_used[a] : std::min<uint64_t>(used[a], b->cap);
+        h->used[a] = std::min<uint64_t>(eng->dev_used[a], b->cap);
         h->off[a] = at;
         at += (h->used[a] + IMAGE_ALIGN - 1) / IMAGE_ALIGN * IMAGE_ALIGN;
     }
@@ -2494,7 +3020,7 @@ static uint64_t image_bytes(const ImageHdr &h) {
 
 int tm_image_size(const tm_engine *eng, uint64_t *bytes) {
     if (!eng || !bytes) return TM_EINVAL;
-    if (!eng->staged.empty()) return TM_ESTATE;
+    std::lock_guard<std::recursive_mutex> g(const_cast<tm_engine *>(eng)->mu_dev);
     ImageHdr h;
     image_layout(eng, &h);
     *bytes = image_bytes(h);
@@ -2503,15 +3029,13 @@ int tm_image_size(const tm_engine *eng, uint64_t *bytes) {
 
 int tm_image_export(tm_engine *eng, void *d_dst, uint64_t cap, void *stream) {
     if (!eng || !d_dst) return TM_EINVAL;
-    if (!eng->staged.empty()) {
-        eng->err = "tm_image_export: staged ops not committed";
-        return TM_ESTATE;
-    }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     ImageHdr h;
     image_layout(eng, &h);
     if (image_bytes(h) > cap) return TM_ENOMEM;
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    if (s != eng->stream) TM_TRY_HIP(eng->wait_uses(s), TM_EDEVICE, "stream order");
     uint8_t *dst = (uint8_t *)d_dst;
     for (uint32_t a = 0; a < A_N; a++)
         if (h.used[a])
@@ -2529,6 +3053,7 @@ int tm_replica_load(tm_engine *eng, const void *d_image, uint64_t bytes, void *s
         return TM_ESTATE;
     }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
     ImageHdr h;
     TM_TRY_HIP(hipMemcpyAsync(&h, d_image, sizeof h, hipMemcpyDeviceToHost, s), TM_EDEVICE, "image header");
@@ -2537,25 +3062,43 @@ int tm_replica_load(tm_engine *eng, const void *d_image, uint64_t bytes, void *s
         eng->err = "tm_replica_load: not an engine image (or truncated)";
         return TM_EINVAL;
     }
+    for (uint32_t a = 0; a < A_N; a++)
+        if (h.used[a] > h.cap[a]) return TM_EINVAL;
+    // the new image goes into fresh buffers first: a failed load keeps the old one serving
+    DevBuf nb[A_N];
     const uint8_t *src = (const uint8_t *)d_image;
     for (uint32_t a = 0; a < A_N; a++) {
-        if (h.used[a] > h.cap[a]) return TM_EINVAL;
-        DevBuf *b = eng->arr_buf(a);
-        b->release();
-        TM_TRY_HIP(b->ensure(std::max<uint64_t>(h.cap[a], 64)), TM_ENOMEM, "replica alloc");
-        if (h.used[a])
-            TM_TRY_HIP(hipMemcpyAsync(b->p, src + h.off[a], h.used[a], hipMemcpyDeviceToDevice, s), TM_EDEVICE,
-                       "image D2D");
-        eng->dev_used[a] = h.used[a];
+        hipError_t e = nb[a].ensure(std::max<uint64_t>(h.cap[a], 64));
+        if (!e && h.used[a]) e = hipMemcpyAsync(nb[a].p, src + h.off[a], h.used[a], hipMemcpyDeviceToDevice, s);
+        if (e) {
+            (void)hipStreamSynchronize(s);
+            for (DevBuf &b : nb) b.release();
+            eng->err = std::string("tm_replica_load: ") + hipGetErrorString(e);
+            return e == hipErrorOutOfMemory ? TM_ENOMEM : TM_EDEVICE;
+        }
     }
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "image sync");
+    TM_TRY_HIP(eng->quiesce(), TM_EDEVICE, "drain");  // matches in flight finish on the old image
+    for (uint32_t a = 0; a < A_N; a++) {
+        DevBuf *b = eng->arr_buf(a);
+        std::swap(b->p, nb[a].p);
+        std::swap(b->cap, nb[a].cap);
+        nb[a].release();
+        eng->dev_used[a] = h.used[a];
+    }
     eng->epoch = h.epoch;
     eng->wmask = h.wmask;
     eng->emask = h.emask;
     eng->n_deep = h.n_deep;
-    eng->rep_n_live = h.n_live;
-    eng->rep_n_nodes = h.n_nodes;
-    eng->rep_n_words = h.n_words;
+    eng->master_nonce = h.nonce;
+    eng->dv.epoch = h.epoch;
+    eng->dv.wmask = h.wmask;
+    eng->dv.emask = h.emask;
+    eng->dv.n_deep = h.n_deep;
+    eng->dv.max_id = h.max_id;
+    eng->dv.n_live = h.n_live;
+    eng->dv.n_nodes = h.n_nodes;
+    eng->dv.n_words = h.n_words;
     return TM_OK;
 }
 
@@ -2576,6 +3119,7 @@ int tm_replica_create(const tm_config *cfg, const void *d_image, uint64_t bytes,
     std::vector<uint32_t>().swap(eng->slot_list);
     std::vector<uint32_t>().swap(eng->slot_node);
     std::vector<uint32_t>().swap(eng->kset);
+    eng->release_ids();
     if ((rc = tm_replica_load(eng, d_image, bytes, stream)) != TM_OK) {
         tm_destroy(eng);
         return rc;
@@ -2587,6 +3131,7 @@ int tm_replica_create(const tm_config *cfg, const void *d_image, uint64_t bytes,
 int tm_patch_size(const tm_engine *eng, uint64_t *bytes, int *full) {
     if (!eng || !bytes) return TM_EINVAL;
     if (!(eng->cfg.flags & TM_CFG_RECORD_PATCH)) return TM_ESTATE;
+    std::lock_guard<std::mutex> g(const_cast<tm_engine *>(eng)->mu_host);
     *bytes = sizeof(PatchHdr) + (eng->patch.full ? 0 : eng->patch.buf.size());
     if (full) *full = eng->patch.full ? 1 : 0;
     return TM_OK;
@@ -2595,10 +3140,11 @@ int tm_patch_size(const tm_engine *eng, uint64_t *bytes, int *full) {
 int tm_patch_export(const tm_engine *eng, void *dst, uint64_t cap) {
     if (!eng || !dst) return TM_EINVAL;
     if (!(eng->cfg.flags & TM_CFG_RECORD_PATCH)) return TM_ESTATE;
+    std::lock_guard<std::mutex> g(const_cast<tm_engine *>(eng)->mu_host);
     const uint64_t body = eng->patch.full ? 0 : eng->patch.buf.size();
     if (cap < sizeof(PatchHdr) + body) return TM_ENOMEM;
     PatchHdr h{PATCH_MAGIC, eng->patch_from, eng->epoch, eng->wmask, eng->emask, eng->n_deep, eng->n_live,
-               eng->patch.full ? 0 : eng->patch.n, eng->patch.full ? 1ull : 0ull};
+               eng->patch.full ? 0 : eng->patch.n, eng->patch.full ? 1ull : 0ull, eng->master_nonce, eng->max_id};
     memcpy(dst, &h, sizeof h);
     if (body) memcpy((uint8_t *)dst + sizeof h, eng->patch.buf.data(), body);
     return TM_OK;
@@ -2610,9 +3156,14 @@ int tm_replica_apply_patch(tm_engine *eng, const void *patch, uint64_t bytes) {
         eng->err = "tm_replica_apply_patch: not a replica";
         return TM_ESTATE;
     }
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     PatchHdr h;
     memcpy(&h, patch, sizeof h);
     if (h.magic != PATCH_MAGIC) return TM_EINVAL;
+    if (h.nonce != eng->master_nonce) {
+        eng->err = "tm_replica_apply_patch: the patch comes from another master than the replica's image";
+        return TM_ESTATE;
+    }
     if (h.full) {
         eng->err = "tm_replica_apply_patch: the master re-uploaded its whole index; reload from tm_image_export";
         return TM_ESTATE;
@@ -2624,22 +3175,37 @@ int tm_replica_apply_patch(tm_engine *eng, const void *patch, uint64_t bytes) {
     }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     hipStream_t s = eng->stream;
-    // validate every record before touching the device: a replica never half-applies
+    // validate every record before touching the device: a replica never half-applies, and no
+    // record may write past the buffer it targets (capacities as they will be at that record)
+    uint64_t cap_at[A_N];
+    for (uint32_t a = 0; a < A_N; a++) cap_at[a] = eng->arr_buf(a)->cap;
     const uint8_t *p = (const uint8_t *)patch + sizeof h, *end = (const uint8_t *)patch + bytes;
     for (uint64_t i = 0; i < h.n_records; i++) {
         if (p + sizeof(PatchRec) > end) return TM_EINVAL;
         PatchRec r;
         memcpy(&r, p, sizeof r);
         const uint64_t el = r.arr < A_N ? ARR_ELEM[r.arr] : 0;
-        if (!el || p + sizeof r + r.bytes > end) return TM_EINVAL;
+        if (!el || r.bytes > (uint64_t)(end - p) - sizeof r) return TM_EINVAL;
+        if (r.kind != P_TAIL && r.kind != P_SCATTER && r.kind != P_WHOLE) return TM_EINVAL;
+        if (r.count > (1ull << 40)) return TM_EINVAL;
         const uint64_t need = r.kind == P_SCATTER ? r.count * (8 + el) : r.count * el;
         if (need > r.bytes) return TM_EINVAL;
-        const DevBuf *b = eng->arr_buf(r.arr);
-        if (r.kind == P_TAIL && (r.a + r.count) * el > b->cap) return TM_EINVAL;
-        if (r.kind == P_WHOLE && r.count * el > r.a) return TM_EINVAL;
-        if (r.kind != P_TAIL && r.kind != P_SCATTER && r.kind != P_WHOLE) return TM_EINVAL;
+        if (r.kind == P_TAIL && (r.a + r.count) * el > cap_at[r.arr]) return TM_EINVAL;
+        if (r.kind == P_WHOLE) {
+            if (r.count * el > r.a) return TM_EINVAL;
+            cap_at[r.arr] = std::max(cap_at[r.arr], r.a);
+        }
+        if (r.kind == P_SCATTER) {
+            const uint8_t *ix = p + sizeof r;
+            for (uint64_t k = 0; k < r.count; k++) {
+                uint64_t idx;
+                memcpy(&idx, ix + k * 8, 8);
+                if ((idx + 1) * el > cap_at[r.arr]) return TM_EINVAL;
+            }
+        }
         p += sizeof r + r.bytes;
     }
+    TM_TRY_HIP(eng->quiesce(), TM_EDEVICE, "drain");  // replica matches in flight read these arrays
     p = (const uint8_t *)patch + sizeof h;
     for (uint64_t i = 0; i < h.n_records; i++) {
         PatchRec r;
@@ -2654,6 +3220,7 @@ int tm_replica_apply_patch(tm_engine *eng, const void *patch, uint64_t bytes) {
             eng->dev_used[r.arr] = std::max<uint64_t>(eng->dev_used[r.arr], (r.a + r.count) * el);
         } else if (r.kind == P_WHOLE) {
             if (b->cap < r.a) {
+                TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "patch sync");
                 b->release();
                 TM_TRY_HIP(b->ensure(r.a), TM_ENOMEM, "replica alloc");
             }
@@ -2672,6 +3239,15 @@ int tm_replica_apply_patch(tm_engine *eng, const void *patch, uint64_t bytes) {
                            : el == 4 ? launch_scatter4(b->as<uint32_t>(), ix, eng->d_scatter_src.as<uint32_t>(), r.count, s)
                                      : launch_scatter1(b->as<uint8_t>(), ix, eng->d_scatter_src.as<uint8_t>(), r.count, s);
             TM_TRY_HIP(e, TM_EDEVICE, "patch scatter");
+            uint64_t top = 0;
+            for (uint64_t k = 0; k < r.count; k++) {
+                uint64_t idx;
+                memcpy(&idx, pay + k * 8, 8);
+                top = std::max(top, idx + 1);
+            }
+            // a scatter past the used part (new key handles inside the capacity) extends it, so
+            // an image exported from this replica carries them
+            eng->dev_used[r.arr] = std::max<uint64_t>(eng->dev_used[r.arr], top * el);
             TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "patch sync");  // scratch is reused by the next record
         }
         p += sizeof r + r.bytes;
@@ -2681,7 +3257,200 @@ int tm_replica_apply_patch(tm_engine *eng, const void *patch, uint64_t bytes) {
     eng->wmask = h.wmask;
     eng->emask = h.emask;
     eng->n_deep = h.n_deep;
-    eng->rep_n_live = h.n_live;
+    eng->dv.epoch = h.epoch_to;
+    eng->dv.wmask = h.wmask;
+    eng->dv.emask = h.emask;
+    eng->dv.n_deep = h.n_deep;
+    eng->dv.max_id = h.max_id;
+    eng->dv.n_live = h.n_live;
+    return TM_OK;
+}
+
+// Is p host memory the device can DMA from directly (pinned / registered)?
+static bool host_pinned(const void *p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
+// memcpy of a large range on several threads (staging a batch into pinned memory)
+static void par_memcpy(void *dst, const void *src, size_t n) {
+    const size_t per = 8u << 20;
+    const unsigned nt = (unsigned)std::min<size_t>(8, (n + per - 1) / per);
+    if (nt <= 1) {
+        if (n) memcpy(dst, src, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < nt; k++)
+        th.emplace_back([=] {
+            const size_t a = n * k / nt, b = n * (k + 1) / nt;
+            memcpy((uint8_t *)dst + a, (const uint8_t *)src + a, b - a);
+        });
+    for (auto &t : th) t.join();
+}
+
+// tm_match_batch_runs: sub-batches of about RUNS_SUB topics walk in MODE_RUNS on the engine
+// stream, one after the other, reserving spans from one cursor (so each sub-batch's spans are
+// one contiguous range); while sub-batch j+1 is staged and walked, sub-batch j's spans and
+// per-topic arrays cross PCIe on the copy stream.
+constexpr uint32_t RUNS_SUB = 131072;
+constexpr uint32_t RUNS_MAXSUB = 16;
+
+int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, tm_runs_result *out) {
+    if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
+    if (eng->replica) return replica_refuses(eng, "tm_match_batch_runs (spans point into the host id arena)");
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    HostOut &o = eng->out();
+    eng->lease_drop(o);  // the previous result of this thread ends here
+    eng->lease_take(o);  // waits while a commit changes the host copy
+    std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+    eng->bb = &eng->bb_host;
+    memset(out, 0, sizeof(*out));
+    out->n = n;
+    out->epoch = eng->dv.epoch;
+    if (n == 0) return TM_OK;
+    const uint32_t base = off[0];
+    const uint64_t nbytes = (uint64_t)off[n] - base;
+    const uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(RUNS_MAXSUB, n / RUNS_SUB));
+    uint32_t b[RUNS_MAXSUB + 1];
+    for (uint32_t j = 0; j <= S; j++) b[j] = (uint32_t)((uint64_t)n * j / S);
+    int rc = ensure_batch(eng, n, nbytes);
+    if (rc) return rc;
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_bytes, nbytes + 16), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_off, ((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_kcnt, (size_t)n * 4 + 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_rcur, 64), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->h_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->h_rctl.ensure((size_t)RUNS_MAXSUB * 64), TM_ENOMEM, "pinned alloc");
+    for (PinBuf *pb : {&o.r_off, &o.r_cnt, &o.r_kcnt, &o.r_status})
+        TM_TRY_HIP(pb->ensure((size_t)n * 4 + 4), TM_ENOMEM, "pinned alloc");
+    const bool direct = host_pinned(bytes + base);  // DMA straight from the caller's batch
+    if (!direct) TM_TRY_HIP(eng->h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
+    if (!eng->s_pipe) {
+        TM_TRY_HIP(hipStreamCreateWithFlags(&eng->s_pipe, hipStreamNonBlocking), TM_EDEVICE, "stream");
+        for (hipEvent_t *e : {&eng->ev_pk[0], &eng->ev_pk[1], &eng->ev_pd[0], &eng->ev_pd[1]})
+            TM_TRY_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming), TM_EDEVICE, "event");
+    }
+    hipStream_t s = eng->stream, c = eng->s_pipe;
+    eng->bb->last_n = 0;
+    eng->bb->dev_batch = false;  // the device result is in span form, not keys
+    uint32_t *ho = eng->h_off.as<uint32_t>();
+    uint8_t *hb = direct ? nullptr : eng->h_bytes.as<uint8_t>();
+    uint64_t *rctl = eng->h_rctl.as<uint64_t>();  // per sub-batch: [0] span cursor, [1..4] counter block
+
+    for (int attempt = 0; attempt < 2; attempt++) {
+        const uint64_t cap = std::max<uint64_t>(65536, (uint64_t)(eng->runs_spt * 1.3 * n) + 4096);
+        if (eng->bb->d_keys.cap < cap * 16) {
+            TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, cap * 16), TM_ENOMEM, "alloc spans");
+            eng->bb->keys_cap = eng->bb->d_keys.cap / 4;
+        }
+        const uint64_t span_cap = eng->bb->d_keys.cap / 16;
+        TM_TRY_HIP(o.r_runs.ensure(span_cap * 16), TM_ENOMEM, "pinned alloc");
+        TM_TRY_HIP(hipMemsetAsync(eng->bb->d_rcur.p, 0, 8, s), TM_EDEVICE, "memset");
+        unsigned long long *cur = eng->bb->d_rcur.as<unsigned long long>();
+        auto stage = [&](uint32_t j) -> int {
+            const uint32_t lo = b[j], hi = b[j + 1];
+            const uint64_t blo = off[lo] - base, bhi = off[hi] - base;
+            for (uint32_t i = lo; i <= hi; i++) ho[i] = off[i] - base;
+            const uint8_t *src = bytes + base + blo;
+            if (!direct) {
+                par_memcpy(hb + blo, src, bhi - blo);
+                src = hb + blo;
+            }
+            if (bhi > blo)
+                TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_bytes.as<uint8_t>() + blo, src, bhi - blo, hipMemcpyHostToDevice, s),
+                           TM_EDEVICE, "H2D");
+            TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_off.as<uint32_t>() + lo, ho + lo, ((size_t)hi - lo + 1) * 4,
+                                      hipMemcpyHostToDevice, s),
+                       TM_EDEVICE, "H2D");
+            return TM_OK;
+        };
+        auto walk = [&](uint32_t j) -> int {
+            const uint32_t lo = b[j], hi = b[j + 1], h = j & 1;
+            TM_TRY_HIP(enqueue_match(eng, eng->bb->d_bytes.as<uint8_t>(), eng->bb->d_off.as<uint32_t>() + lo, hi - lo, s,
+                                     MODE_RUNS, lo, eng->bb->d_keys.as<uint32_t>(), span_cap, cur),
+                       TM_EDEVICE, "kernel launch");
+            TM_TRY_HIP(hipMemcpyAsync(rctl + 8 * j, cur, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+            TM_TRY_HIP(hipMemcpyAsync(rctl + 8 * j + 1, eng->bb->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                       "D2H");
+            TM_TRY_HIP(hipEventRecord(eng->ev_pk[h], s), TM_EDEVICE, "event");
+            return TM_OK;
+        };
+        uint64_t prev = 0, slow = 0, seg_d = 0, fr_d = 0;
+        bool over = false;
+        auto finish = [&](uint32_t j) -> int {  // sub-batch j walked: its results cross PCIe
+            const uint32_t lo = b[j], hi = b[j + 1], h = j & 1;
+            TM_TRY_HIP(hipEventSynchronize(eng->ev_pk[h]), TM_EDEVICE, "match kernels");
+            const uint64_t c_j = rctl[8 * j];
+            slow += (uint32_t)rctl[8 * j + 2];
+            seg_d = std::max(seg_d, rctl[8 * j + 3]);
+            fr_d = std::max(fr_d, rctl[8 * j + 4]);
+            if (c_j > span_cap) {
+                over = true;
+                prev = c_j;
+                return TM_OK;
+            }
+            TM_TRY_HIP(hipStreamWaitEvent(c, eng->ev_pk[h], 0), TM_EDEVICE, "wait");
+            if (c_j > prev)
+                TM_TRY_HIP(hipMemcpyAsync(o.r_runs.as<uint8_t>() + prev * 16, eng->bb->d_keys.as<uint8_t>() + prev * 16,
+                                          (c_j - prev) * 16, hipMemcpyDeviceToHost, c),
+                           TM_EDEVICE, "D2H");
+            for (std::pair<PinBuf *, DevBuf *> pr :
+                 {std::make_pair(&o.r_off, &eng->bb->d_outoff), std::make_pair(&o.r_cnt, &eng->bb->d_outcnt),
+                  std::make_pair(&o.r_kcnt, &eng->bb->d_kcnt), std::make_pair(&o.r_status, &eng->bb->d_status)})
+                TM_TRY_HIP(hipMemcpyAsync(pr.first->as<uint32_t>() + lo, pr.second->as<uint32_t>() + lo,
+                                          ((size_t)hi - lo) * 4, hipMemcpyDeviceToHost, c),
+                           TM_EDEVICE, "D2H");
+            prev = c_j;
+            return TM_OK;
+        };
+        if ((rc = stage(0)) || (rc = walk(0))) return rc;
+        for (uint32_t j = 0; j < S; j++) {
+            if (j + 1 < S && ((rc = stage(j + 1)) || (rc = walk(j + 1)))) return rc;
+            if ((rc = finish(j))) return rc;
+            if (over) break;
+        }
+        TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "sync");
+        TM_TRY_HIP(hipStreamSynchronize(c), TM_EDEVICE, "D2H");
+        eng->n_slow_last = slow;
+        eng->bb->seg_demand_last = seg_d;
+        eng->bb->fr_demand_last = fr_d;
+        if ((rc = grow_pools(eng))) return rc;
+        if (over) {  // more spans than estimated: size from the demand seen so far, run again
+            uint32_t done = 0;
+            for (uint32_t j = 0; j < S; j++)
+                if (rctl[8 * j] >= prev) {
+                    done = b[j + 1];
+                    break;
+                }
+            eng->runs_spt = std::max(eng->runs_spt * 2, (double)prev / std::max<uint32_t>(done, 1));
+            continue;
+        }
+        eng->runs_spt = (double)prev / n;
+        uint64_t tot = 0;
+        const uint32_t *kc = o.r_kcnt.as<uint32_t>();
+        for (uint32_t i = 0; i < n; i++) tot += kc[i];
+        out->total_ids = tot;
+        out->total_spans = prev;
+        out->span_off = o.r_off.as<uint32_t>();
+        out->span_cnt = o.r_cnt.as<uint32_t>();
+        out->spans = o.r_runs.as<tm_span>();
+        out->kcnt = kc;
+        out->status = o.r_status.as<int32_t>();
+        return TM_OK;
+    }
+    eng->err = "tm_match_batch_runs: span output still short after resizing";
+    return TM_EDEVICE;
+}
+
+int tm_runs_release(tm_engine *eng) {
+    if (!eng) return TM_EINVAL;
+    HostOut &o = eng->out();
+    eng->lease_drop(o);
     return TM_OK;
 }
 

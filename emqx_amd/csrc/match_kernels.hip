@@ -403,7 +403,25 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
     __syncthreads();
 }
 
-template <bool STATS>
+// MODE_RUNS copy-out: every segment of the wave becomes one host span of its topic (no key is
+// read or written: the consumer reads the ids from the engine's host id arena).
+__device__ __forceinline__ void emit_spans(const MatchArgs &a, const WaveLds &L, const uint4 *seg, uint32_t ns) {
+    uint4 *spans = reinterpret_cast<uint4 *>(a.keys);
+    for (uint32_t j = lane_id(); j < ns; j += WAVE) {
+        const uint4 g = seg[j];
+        if (!g.y || ((L.spill >> (g.w & 0x3Fu)) & 1ull)) continue;  // spilled: the slow kernel owns it
+        uint64_t p;
+        if (g.w & SEG_INLINE) {
+            p = a.span_keys + 16ull * g.x;
+        } else {
+            const uint32_t src = (g.w & SEG_NODE) ? a.slot_list[g.x] + (g.w >> SEG_SKIP_SHIFT) : g.x;
+            p = a.span_arena + 8ull * src;
+        }
+        spans[L.tbase[g.w & 0x3Fu] + g.z] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), g.y, 0u);
+    }
+}
+
+template <bool STATS, bool RUNS>
 __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) {
     __shared__ WaveLds L;
     uint32_t *const wchunks = a.wave_chunks + (uint64_t)blockIdx.x * MAXCHUNK;  // this wave's flushed chunks
@@ -473,6 +491,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
 #endif
     L.nlev[lane] = nl;
     L.cnt[lane] = 0;
+    if constexpr (RUNS) L.tbase[lane] = 0;  // RUNS: keys of the topic during the walk (cnt counts spans)
     {
         const unsigned long long sp0 = __ballot(spill0);
         if (lane == 0) {
@@ -513,7 +532,12 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
         const uint32_t pos = wave_excl_scan(em ? 1u : 0u, &tot);
         if (em) {
             L.seg[pos] = make_uint4(R.list_off, R.hash_cnt, 0u, lane);
-            L.cnt[lane] = R.hash_cnt;
+            if constexpr (RUNS) {
+                L.cnt[lane] = 1;
+                L.tbase[lane] = R.hash_cnt;
+            } else {
+                L.cnt[lane] = R.hash_cnt;
+            }
         }
         nseg = tot;
         st_seg += em;
@@ -698,7 +722,16 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
 #pragma unroll
                 for (int k = 0; k < RPL; k++) {
                     auto put = [&](uint32_t src, uint32_t cnt, uint32_t fl2) {
-                        const uint4 g = make_uint4(src, cnt, cnt ? atomicAdd(&L.cnt[tl[k]], cnt) : 0u, tl[k] | fl2);
+                        uint32_t rel = 0;
+                        if (cnt) {
+                            if constexpr (RUNS) {
+                                atomicAdd(&L.tbase[tl[k]], cnt);
+                                rel = atomicAdd(&L.cnt[tl[k]], 1u);
+                            } else {
+                                rel = atomicAdd(&L.cnt[tl[k]], cnt);
+                            }
+                        }
+                        const uint4 g = make_uint4(src, cnt, rel, tl[k] | fl2);
                         if (!direct) L.seg[ps] = g;
                         else if (dok) a.seg_pool[(uint64_t)dc0 * SCAP + ps] = g;
                         else atomicOr(&L.spill, 1ull << tl[k]);  // pool exhausted: topic spills
@@ -804,6 +837,8 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     // ---- 4. reserve this wave's output with one atomic; per-topic results
     const bool spill = active && !badarg && ((L.spill >> lane) & 1ull);
     const uint32_t my = (walk && !spill) ? L.cnt[lane] : 0u;
+    uint32_t my_keys = 0;
+    if constexpr (RUNS) my_keys = (walk && !spill) ? L.tbase[lane] : 0u;
     uint32_t total;
     const uint32_t excl = wave_excl_scan(my, &total);
     unsigned long long gb = 0;
@@ -815,6 +850,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
         a.status[t] = badarg ? 1 : 0;
         a.out_off[t] = spill ? 0u : (uint32_t)(gb + excl);
         a.out_cnt[t] = my;
+        if constexpr (RUNS) a.out_kcnt[t] = my_keys;
     }
     {
         uint32_t tot_sp;
@@ -827,7 +863,12 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     __syncthreads();
 
     // ---- 5. load-balanced expansion: staged segments, then flushed chunks
-    if (!overflow && total && a.mode == MODE_ALL) {
+    if constexpr (RUNS) {
+        if (!overflow && total) {
+            emit_spans(a, L, L.seg, nseg);
+            for (uint32_t c = 0; c < nchunk; ++c) emit_spans(a, L, a.seg_pool + (uint64_t)wchunks[c] * SCAP, SCAP);
+        }
+    } else if (!overflow && total && a.mode == MODE_ALL) {
         expand_segments(a, L, nseg);
         for (uint32_t c = 0; c < nchunk; ++c) {
             const uint4 *src = a.seg_pool + (uint64_t)wchunks[c] * SCAP;
@@ -876,6 +917,16 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
 // Stack entry: slot index (40 bits; ROOT_MARK for the root) | depth (24 bits).
 constexpr uint64_t ROOT_MARK = (1ull << 40) - 1;
 
+// one key of a topic the spill kernel walks: the key handle, or (MODE_RUNS) a one-key span
+__device__ __forceinline__ void out_key(const MatchArgs &a, uint32_t *out, uint32_t i, uint32_t key) {
+    if (a.mode == MODE_RUNS) {
+        const uint64_t p = a.span_keys + 16ull * key;
+        reinterpret_cast<uint4 *>(out)[i] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), 1u, 0u);
+    } else {
+        out[i] = key;
+    }
+}
+
 template <bool WRITE>
 __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_t *wid, uint64_t *stk, uint32_t nl,
                              bool dollar, uint32_t *out, uint32_t *probes, uint32_t *visits) {
@@ -904,18 +955,18 @@ __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_
                 hc = a.arena[lo - 1];
             } else if (m == M_INLINE && ((info & I_INL_HASH) || d == nl)) {
                 // the node's only key, inline in the slot
-                if (WRITE) out[count] = info & I_KEY_MASK;
+                if (WRITE) out_key(a, out, count, info & I_KEY_MASK);
                 count++;
             }
         }
         (*visits)++;
         // "P/#" keys match at P and below
         if (WRITE)
-            for (uint32_t k = 0; k < hc; k++) out[count + k] = a.arena[lo + tc + k];
+            for (uint32_t k = 0; k < hc; k++) out_key(a, out, count + k, a.arena[lo + tc + k]);
         count += hc;
         if (d == nl) {
             if (WRITE)
-                for (uint32_t k = 0; k < tc; k++) out[count + k] = a.arena[lo + k];
+                for (uint32_t k = 0; k < tc; k++) out_key(a, out, count + k, a.arena[lo + k]);
             count += tc;
             continue;
         }
@@ -955,8 +1006,13 @@ __global__ __launch_bounds__(WAVE) void k_match_slow(MatchArgs a) {
         a.out_cnt[t] = c;
         a.status[t] = 0;
         st_keys += c;
-        if (a.mode == MODE_ALL && pos + c <= a.keys_cap)
+        if (a.mode == MODE_RUNS) {
+            a.out_kcnt[t] = c;
+            if (pos + c <= a.keys_cap)  // spans are 4 u32 each
+                dfs_walk<true>(a, R, wid, stk, nl, dollar, a.keys + 4 * pos, &st_probe, &st_visit);
+        } else if (a.mode == MODE_ALL && pos + c <= a.keys_cap) {
             dfs_walk<true>(a, R, wid, stk, nl, dollar, a.keys + pos, &st_probe, &st_visit);
+        }
     }
     if constexpr (STATS) {
         // levels were already counted by the fast kernel's pre-scan
@@ -1545,8 +1601,13 @@ hipError_t launch_match(const MatchArgs &a, hipStream_t s) {
         return hipGetLastError();
     }
     if (a.ev_fast0 && (e = hipEventRecord(a.ev_fast0, s))) return e;
-    if (a.stats) k_match_fast<true><<<grid, WAVE, 0, s>>>(a);
-    else k_match_fast<false><<<grid, WAVE, 0, s>>>(a);
+    if (a.mode == MODE_RUNS) {
+        if (a.stats) k_match_fast<true, true><<<grid, WAVE, 0, s>>>(a);
+        else k_match_fast<false, true><<<grid, WAVE, 0, s>>>(a);
+    } else {
+        if (a.stats) k_match_fast<true, false><<<grid, WAVE, 0, s>>>(a);
+        else k_match_fast<false, false><<<grid, WAVE, 0, s>>>(a);
+    }
     if ((e = hipGetLastError())) return e;
     if (a.ev_fast1 && (e = hipEventRecord(a.ev_fast1, s))) return e;
     // spill kernel: fixed grid, grid-stride over the device-side spill list

@@ -38,9 +38,28 @@
  *   - Ops are staged by tm_apply and become visible atomically at tm_commit_epoch
  *     (one delta epoch).  Within one epoch the LAST op per key wins, the rule of
  *     emqx_router_syncer:merge_route_op/2.  A match batch always sees exactly one
- *     committed epoch (stronger than ETS' per-key atomicity).
- *   - One engine drives one GPU (tm_config.device) and owns one HIP stream; calls
- *     on one engine must be serialised by the caller (the NIF holds a lock).
+ *     committed epoch (stronger than ETS' per-key atomicity).  Staged ops are invisible to
+ *     matches until their commit: a match never fails because writes are pending.
+ *   - Failed commits (emqx_router_syncer.erl:269-277 keeps a failed batch's stash and
+ *     retries it): a commit that would exceed a capacity (trie nodes, terminal-list arena;
+ *     tm_config.max_nodes / max_list_words lower them) returns TM_ENOMEM BEFORE changing
+ *     anything: its ops stay staged (in order, ahead of any staged since), matches keep
+ *     serving the previous epoch, and the next tm_commit_epoch retries them
+ *     (tm_discard_staged drops them instead).  A commit whose device upload fails after the
+ *     host copy advanced returns TM_ENOMEM / TM_EDEVICE with the device still holding the
+ *     previous epoch intact; the next commit uploads the whole index again.
+ *   - Threading.  One engine drives one GPU (tm_config.device).  Every entry point may be
+ *     called from any number of threads at once, in any mix (the reference index is a
+ *     public, read_concurrency ETS table written by any process, emqx_topic_index.erl:41-42;
+ *     emqx_router.erl:141-160).  Inside: staging never waits for matches or commits; a
+ *     commit's host work (the trie, the lists, and a full rebuild's upload into a standby
+ *     device image) runs beside the matches, which wait only while the commit publishes
+ *     (a delta's in-place scatters, or the pointer swap of a standby image).  Host results
+ *     (tm_result, tm_runs_result, tm_intersect_result) belong to the calling thread: valid
+ *     until that thread's next call of the same kind.  Device results (tm_dev_result) belong
+ *     to the engine: valid until the next tm_match_device* call from ANY thread, which the
+ *     engine orders after everything already queued on the previous call's stream (keep
+ *     that stream alive until then).  tm_last_error() is per thread.
  */
 #ifndef EMQX_TM_H
 #define EMQX_TM_H
@@ -52,7 +71,7 @@
 extern "C" {
 #endif
 
-#define TM_ABI_VERSION 5u
+#define TM_ABI_VERSION 6u
 
 /* status codes */
 #define TM_OK          0
@@ -116,7 +135,9 @@ typedef struct tm_config {
                                      waits for its longest probe chain, so lower load shortens
                                      the walk at the price of HBM (16 B per slot) */
     uint32_t topics_per_wave;     /* 0 = by batch size (4..64); else 4, 8, 16, 32 or 64 */
-    uint32_t reserved[1];
+    uint32_t max_nodes;           /* trie-node budget (0 = the edge table's limit, 2^30): a commit
+                                     that would pass it fails with TM_ENOMEM, ops kept staged */
+    uint32_t max_list_words;      /* terminal-list arena budget in u32 words (0 = 2^32 - 16) */
 } tm_config;
 
 typedef struct tm_op {
@@ -176,6 +197,10 @@ typedef struct tm_stats_t {
     uint64_t n_deep_keys;   /* live word-list keys deeper than the device order code (31 levels) */
     uint64_t n_filter_onepass;  /* tm_match_filter_batch batches walked once (keys chunked on device) */
     uint64_t n_filter_twopass;  /* ... that needed the count + emit passes (output sized from them) */
+    uint64_t commit_stall_us;   /* last commit: how long matches were held back while it published
+                                   (a delta's in-place scatters; a full rebuild's standby swap) */
+    uint64_t n_commits_refused; /* commits refused for capacity, ops kept staged               */
+    uint64_t n_staged;          /* ops staged now (not yet committed)                          */
 } tm_stats_t;
 
 /* lifecycle --------------------------------------------------------------- */
@@ -191,6 +216,11 @@ int tm_apply(tm_engine *eng, const tm_op *ops, size_t n);
 int tm_apply_packed(tm_engine *eng, uint32_t op, const uint8_t *bytes, const uint64_t *off,
                     const uint64_t *ids, const uint32_t *flags, size_t n);
 int tm_commit_epoch(tm_engine *eng, uint64_t *epoch_out);
+/* Drop every staged op (e.g. a batch a capacity error refused); *n_out = ops dropped. */
+int tm_discard_staged(tm_engine *eng, uint64_t *n_out);
+/* Free the calling thread's host result buffers (tm_result / tm_intersect_result / runs) and
+ * end its runs lease; results it still points to become invalid. */
+int tm_result_release(tm_engine *eng);
 
 /* reads ------------------------------------------------------------------- */
 /* Host buffers in, host result out (H2D + kernels + D2H inside).
@@ -201,6 +231,39 @@ int tm_commit_epoch(tm_engine *eng, uint64_t *epoch_out);
  * refuse (TM_ESTATE) until the next tm_match_device* call. */
 int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off,
                    uint32_t n, uint32_t mode, tm_result *out);
+
+/* Runs form of tm_match_batch (TM_MATCH_ALL), for callers that consume route ids on the host
+ * (emqx_broker:do_publish/1 -> match_routes/1, emqx_broker.erl:285-290; emqx_router.erl:648-649
+ * turns each key into a #route{}).  The walk already knows each topic's matches as a few runs
+ * of consecutive keys of the terminal-list arena; only those runs cross PCIe (16 B each, vs
+ * 4 B per key), and each run is a span of the engine's HOST id arena: topic i's ids are the
+ * concatenation of spans[span_off[i] .. span_off[i] + span_cnt[i]), kcnt[i] ids in all, in
+ * unspecified order (the same multiset tm_match_batch + tm_key_ids gives).  The GPU writes
+ * the spans themselves (host addresses), so the host does no per-key or per-run work: a
+ * consumer reads each id once, where it builds its reply.  Zero-copy: the spans point
+ * into engine memory that the calling thread holds a READ LEASE on until its next
+ * tm_match_batch_runs, tm_runs_release or tm_result_release; a commit's host phase waits for
+ * every lease (release promptly; a thread's own commit first ends its own lease).  Master
+ * engines only (a replica keeps no host copy: TM_ESTATE). */
+typedef struct tm_span {
+    const uint64_t *ids;
+    uint64_t        n;
+} tm_span;
+typedef struct tm_runs_result {
+    uint32_t        n;
+    uint32_t        _pad;
+    uint64_t        epoch;        /* the committed epoch matched        */
+    uint64_t        total_ids;    /* sum of kcnt[]                      */
+    uint64_t        total_spans;
+    const uint32_t *span_off;     /* n entries                          */
+    const uint32_t *span_cnt;     /* n entries                          */
+    const tm_span  *spans;
+    const uint32_t *kcnt;         /* n entries: ids of topic i          */
+    const int32_t  *status;       /* n entries: TM_TOPIC_OK / TM_BADARG */
+} tm_runs_result;
+int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n,
+                        tm_runs_result *out);
+int tm_runs_release(tm_engine *eng);
 /* Device buffers in, device result out, asynchronous on the engine's stream
  * (or on `stream` if non-NULL: a hipStream_t).  The engine's own stream is
  * non-blocking: work the caller queues on other streams (including the legacy

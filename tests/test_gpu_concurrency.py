@@ -1,0 +1,305 @@
+"""The C-ABI under concurrent callers, and commit failure semantics.
+
+Reference behaviour: the index is a public, read_concurrency ETS table that any process
+writes while others match (apps/emqx/src/emqx_topic_index.erl:41-42; the route tables,
+apps/emqx/src/emqx_router.erl:141-160); a failed syncer batch keeps its stash, the table
+keeps serving and the batch is retried (apps/emqx/src/emqx_router_syncer.erl:269-277).
+Here every call may come from any thread (include/emqx_tm.h "Threading"); each batch sees
+exactly ONE committed epoch (checked bit-exactly against that epoch's oracle); a commit that
+would pass a capacity is refused before anything changes."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from emqx_amd import _native as N
+from emqx_amd import workloads
+
+pytestmark = pytest.mark.gpu
+
+
+def _epochs(w, n_epochs, rng, big_epoch=None):
+    """Key sets of successive epochs (a set of (filter, id)) and the ops between them."""
+    filters = w.filters()
+    live = {(f, int(i)) for f, i in zip(filters, w.f_id.tolist())}
+    sets, opss = [frozenset(live)], []
+    next_id = int(w.f_id.max()) + 1
+    for e in range(n_epochs):
+        order = sorted(live)
+        k = len(order) // 5 if e == big_epoch else max(2, len(order) // 50)
+        ops = []
+        for j in rng.choice(len(order), size=k, replace=False):
+            f, i = order[int(j)]
+            ops.append((N.TM_OP_DEL, f, i))
+            live.discard((f, i))
+        for _ in range(k):
+            f = filters[int(rng.integers(len(filters)))]
+            r = rng.random()
+            f = f + b"/#" if r < 0.3 else (b"+/" + f if r < 0.4 else f)
+            ops.append((N.TM_OP_ADD, f, next_id))
+            live.add((f, next_id))
+            next_id += 1
+        opss.append(ops)
+        sets.append(frozenset(live))
+    return sets, opss
+
+
+def _hip():
+    # torch's HIP runtime (conftest imports torch first; same soname, so this is that library)
+    lib = N.C.CDLL("libamdhip64.so")
+    lib.hipMemcpyAsync.argtypes = [N.C.c_void_p, N.C.c_void_p, N.C.c_size_t, N.C.c_int, N.C.c_void_p]
+    return lib
+
+
+def _expected(keyset, t_bytes, t_off):
+    lf, li = zip(*sorted(keyset))
+    return oracle.OrderedIndex.from_filters(list(lf), list(li)).match(t_bytes, t_off)
+
+
+def test_concurrent_matches_and_writes_see_one_epoch_each():
+    """Four threads at once on one engine: a writer stages each epoch's ops from two threads
+    and commits (a delta epoch, and one epoch big enough for a full rebuild into a standby
+    image); three readers loop over the runs form (ids of the epoch it reports), the key form
+    (counts, bracketed by tm_stats epochs) and the device form on a torch stream.  Every
+    result must equal one epoch's oracle result, and no reader goes back in time."""
+    rng = np.random.default_rng(0xC0C0)
+    w = workloads.generate("E", scale=0.02, n_topics=4000)
+    sets, opss = _epochs(w, 6, rng, big_epoch=3)
+    exp = [_expected(s, w.t_bytes, w.t_off) for s in sets]
+    exp_cnt = [np.diff(e[0]).astype(np.int64) for e in exp]
+    eng = N.Engine(0)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    base_epoch = eng.commit()
+    errors, seen = [], {"runs": set(), "keys": set(), "dev": set()}
+    done = threading.Event()
+
+    def fail(msg):
+        errors.append(msg)
+        done.set()
+
+    def reader_runs():
+        last = -1
+        while not done.is_set():
+            res = eng.match_runs_view(w.t_bytes, w.t_off)
+            e = int(res.epoch) - base_epoch
+            n = len(w.t_off) - 1
+            try:
+                if not 0 <= e < len(exp) or e < last:
+                    return fail(f"runs: epoch {e} after {last}")
+                last = e
+                eo, eids, est = exp[e]
+                kc = np.ctypeslib.as_array(res.kcnt, shape=(n,))
+                if not np.array_equal(kc.astype(np.int64), exp_cnt[e]):
+                    return fail(f"runs: counts differ from epoch {e}")
+                so = np.ctypeslib.as_array(res.span_off, shape=(n,))
+                sc = np.ctypeslib.as_array(res.span_cnt, shape=(n,))
+                for i in range(0, n, 37):  # a sample of topics, id for id
+                    got = []
+                    for j in range(int(so[i]), int(so[i]) + int(sc[i])):
+                        sp = res.spans[j]
+                        got += np.ctypeslib.as_array(N.C.cast(sp.ids, N.C.POINTER(N.C.c_uint64)),
+                                                     shape=(int(sp.n),)).tolist()
+                    if sorted(got) != eids[eo[i]:eo[i + 1]].tolist():
+                        return fail(f"runs: topic {i} differs from epoch {e}")
+                seen["runs"].add(e)
+            finally:
+                eng.lib.tm_runs_release(eng.h)
+
+    def reader_keys():
+        last = -1
+        while not done.is_set():
+            e0 = eng.stats()["epoch"] - base_epoch
+            off, cnt, keys, st = eng.match_packed(w.t_bytes, w.t_off)
+            e1 = eng.stats()["epoch"] - base_epoch
+            c = cnt.astype(np.int64)
+            hit = [e for e in range(max(e0, last, 0), e1 + 1) if np.array_equal(c, exp_cnt[e])]
+            if not hit:
+                return fail(f"keys: counts match no epoch in [{e0}, {e1}]")
+            last = hit[0]
+            seen["keys"].add(hit[0])
+
+    def reader_device():
+        dev = torch.device("cuda:0")
+        s = torch.cuda.Stream(device=dev)
+        tb = torch.from_numpy(np.asarray(w.t_bytes)).to(dev)
+        to = torch.from_numpy(np.asarray(w.t_off).astype(np.int32)).to(dev)
+        n = len(w.t_off) - 1
+        nbytes = int(w.t_off[-1] - w.t_off[0])
+        last = -1
+        while not done.is_set():
+            e0 = eng.stats()["epoch"] - base_epoch
+            with torch.cuda.stream(s):
+                r = eng.match_device_mode(tb.data_ptr(), to.data_ptr(), n, nbytes, N.TM_MATCH_COUNT, s.cuda_stream)
+                cnt = torch.empty(n, dtype=torch.int32, device=dev)
+                # read the engine-owned counts on the same stream, before the next device call
+                _hip().hipMemcpyAsync(N.C.c_void_p(cnt.data_ptr()), N.C.c_void_p(r.d_cnt), N.C.c_size_t(4 * n), 3,
+                                      N.C.c_void_p(s.cuda_stream))
+                s.synchronize()
+            e1 = eng.stats()["epoch"] - base_epoch
+            c = cnt.cpu().numpy().astype(np.int64)
+            hit = [e for e in range(max(e0, last, 0), e1 + 1) if np.array_equal(c, exp_cnt[e])]
+            if not hit:
+                return fail(f"device: counts match no epoch in [{e0}, {e1}]")
+            last = hit[0]
+            seen["dev"].add(hit[0])
+
+    def writer():
+        try:
+            for e, ops in enumerate(opss):
+                half = len(ops) // 2
+                # stage from two threads (each keeps its own op order; the halves touch disjoint keys)
+                t = threading.Thread(target=eng.apply, args=(ops[half:],))
+                dels = [o for o in ops[:half]]
+                t.start()
+                eng.apply(dels)
+                t.join()
+                eng.commit()
+                threading.Event().wait(0.05)
+        except Exception as ex:  # noqa: BLE001
+            fail(f"writer: {ex!r}")
+        finally:
+            threading.Event().wait(0.1)
+            done.set()
+
+    ths = [threading.Thread(target=f) for f in (reader_runs, reader_keys, reader_device)]
+    for t in ths:
+        t.start()
+    writer()
+    for t in ths:
+        t.join(timeout=60)
+    assert not errors, errors[:3]
+    # the last epoch is what everything serves at the end
+    assert eng.stats()["epoch"] - base_epoch == len(opss)
+    o, ids, kcnt, st = eng.match_runs(w.t_bytes, w.t_off)
+    assert np.array_equal(kcnt.astype(np.int64), exp_cnt[-1])
+    assert eng.stats()["n_full_rebuilds"] >= 2
+    assert all(seen.values()), seen
+    eng.close()
+
+
+def test_capacity_refusal_keeps_serving_and_keeps_ops_staged():
+    """A commit past the node budget is refused BEFORE anything changes: matches keep
+    returning the previous epoch, the ops stay staged (a retry fails the same way), ops
+    staged afterwards queue behind them, and after tm_discard_staged a smaller commit
+    succeeds."""
+    eng = N.Engine(0, max_nodes=64)
+    base = [(N.TM_OP_ADD, b"a/b/%d" % i, i) for i in range(20)] + [(N.TM_OP_ADD, b"a/#", 100)]
+    eng.apply(base)
+    e1 = eng.commit()
+    topics = [b"a/b/3", b"a/b/19", b"a/x", b"z/z/z"]
+    before = [sorted(eng.key_ids(np.array(k, dtype=np.uint32)).tolist()) for k in eng.match(topics)]
+    assert before == [[3, 100], [19, 100], [100], []]
+    big = [(N.TM_OP_ADD, b"z/%d/q" % i, 1000 + i) for i in range(40)]  # 80 new nodes > 64
+    eng.apply(big)
+    for _ in range(2):
+        with pytest.raises(N.TMError) as ex:
+            eng.commit()
+        assert ex.value.rc == N.TM_ENOMEM
+        s = eng.stats()
+        assert s["epoch"] == e1 and s["n_staged"] == len(big)
+        now = [sorted(eng.key_ids(np.array(k, dtype=np.uint32)).tolist()) for k in eng.match(topics)]
+        assert now == before
+        o, ids, kcnt, st = eng.match_runs(*N.pack_topics(topics))
+        assert [sorted(ids[o[i]:o[i + 1]].tolist()) for i in range(4)] == before
+    eng.apply([(N.TM_OP_ADD, b"a/b/3", 777)])  # staged behind the refused ops
+    assert eng.stats()["n_staged"] == len(big) + 1 and eng.stats()["n_commits_refused"] == 2
+    assert eng.discard_staged() == len(big) + 1
+    eng.apply([(N.TM_OP_ADD, b"z/z/z", 5), (N.TM_OP_DEL, b"a/b/19", 19)])
+    e2 = eng.commit()
+    assert e2 == e1 + 1
+    after = [sorted(eng.key_ids(np.array(k, dtype=np.uint32)).tolist()) for k in eng.match(topics)]
+    assert after == [[3, 100], [100], [100], [5]]
+    eng.close()
+
+
+def test_arena_budget_refusal_then_retry_after_deletes():
+    """The list-arena budget: an epoch whose keys would not fit even after a compaction is
+    refused with its ops kept staged and the previous epoch serving; a smaller epoch that fits
+    only after the engine compacts its arena (the moved list's slack would pass the budget)
+    then commits."""
+    eng = N.Engine(0, max_list_words=4096)
+    eng.apply([(N.TM_OP_ADD, b"t/#", i) for i in range(1000)])
+    e1 = eng.commit()
+    adds = [(N.TM_OP_ADD, b"t/#", 10000 + i) for i in range(4000)]
+    eng.apply(adds)
+    with pytest.raises(N.TMError):
+        eng.commit()
+    assert eng.stats()["epoch"] == e1
+    assert len(eng.match([b"t/x"])[0]) == 1000
+    eng.discard_staged()
+    eng.apply(adds[:1500])
+    e2 = eng.commit()
+    assert e2 == e1 + 1 and len(eng.match([b"t/x"])[0]) == 2500
+    eng.close()
+
+
+def test_commit_waits_for_an_async_match_on_another_stream():
+    """a commit that rewrites lists in place must not tear a walk still
+    in flight on the caller's stream.  Queue tm_match_device on a torch stream, commit in-place
+    edits right away, then read the result: it is the pre-commit epoch's, exactly."""
+    dev = torch.device("cuda:0")
+    w = workloads.generate("C", scale=0.005, n_topics=20000)
+    eng = N.Engine(0)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    filters = w.filters()
+    ix0 = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    eo, eids, est = ix0.match(w.t_bytes, w.t_off)
+    s = torch.cuda.Stream(device=dev)
+    tb = torch.from_numpy(np.asarray(w.t_bytes)).to(dev)
+    to = torch.from_numpy(np.asarray(w.t_off).astype(np.int32)).to(dev)
+    n = len(w.t_off) - 1
+    # deletes inside long '#' lists: rewritten in place (room kept), not moved
+    hot = [i for i, f in enumerate(filters) if f.endswith(b"/#")][:400]
+    ops = [(N.TM_OP_DEL, filters[i], int(w.f_id[i])) for i in hot]
+    for rep in range(3):
+        with torch.cuda.stream(s):
+            eng.match_device(tb.data_ptr(), to.data_ptr(), n, int(w.t_off[-1] - w.t_off[0]), s.cuda_stream)
+            d_ids = torch.empty(int(eids.size) + 16, dtype=torch.int64, device=dev)
+            d_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            eng.result_ids_device(d_ids.data_ptr(), d_ids.numel(), d_off.data_ptr(), s.cuda_stream)
+        if rep == 0:
+            eng.apply(ops)
+            eng.commit()  # must wait for the walk and the id pass queued on `s`
+        s.synchronize()
+        off = d_off.cpu().numpy().astype(np.int64)
+        ids = d_ids.cpu().numpy().view(np.uint64)
+        if rep == 0:
+            ref_off, ref_ids = eo, eids
+        else:
+            keep = np.ones(len(filters), dtype=bool)
+            keep[hot] = False
+            f2 = [filters[i] for i in range(len(filters)) if keep[i]]
+            ref_off, ref_ids, _ = oracle.OrderedIndex.from_filters(f2, w.f_id[keep]).match(w.t_bytes, w.t_off)
+        assert np.array_equal(np.diff(off), np.diff(ref_off).astype(np.int64)), rep
+        for i in range(0, n, 13):
+            assert np.array_equal(np.sort(ids[off[i]:off[i + 1]]), ref_ids[ref_off[i]:ref_off[i + 1]]), (rep, i)
+    eng.close()
+
+
+def test_last_error_is_per_thread():
+    """tm_last_error() reports the CALLING thread's last failure: two threads failing in
+    different calls on one engine each read their own message."""
+    import ctypes as C
+    eng = N.Engine(0)
+    hdr = np.zeros(4096, dtype=np.uint8)
+    a_failed, b_failed = threading.Event(), threading.Event()
+    got = {}
+
+    def thread_a():
+        eng.lib.tm_replica_apply_patch(eng.h, hdr.ctypes.data, len(hdr))  # "...apply_patch: not a replica"
+        a_failed.set()
+        b_failed.wait(10)
+        got["a"] = eng.lib.tm_last_error(eng.h)
+
+    t = threading.Thread(target=thread_a)
+    t.start()
+    a_failed.wait(10)
+    assert eng.lib.tm_replica_load(eng.h, C.c_void_p(hdr.ctypes.data), len(hdr), None) == N.TM_ESTATE
+    b_failed.set()
+    t.join()
+    assert b"apply_patch" in got["a"], got
+    assert b"tm_replica_load" in eng.lib.tm_last_error(eng.h)
+    eng.close()
