@@ -88,30 +88,45 @@ def profiled_traffic(workload_keys, batch, any_config=False):
     return best
 
 
+def _loadgen():
+    import ctypes as C
+    lg = C.CDLL(os.path.join(ROOT, "tools", "libtm_loadgen.so"))
+    lg.loadgen_run2.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double, C.c_int,
+                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+    lg.spans_checksum.restype = C.c_uint64
+    lg.spans_checksum.argtypes = [C.c_void_p, C.c_uint32]
+    return lg
+
+
 def batcher_load(eng, tb, to32, seconds):
     """End to end through the batching aggregator (include/emqx_tm_batcher.h): P concurrent
     publishers, each with one publish in flight (tools/loadgen.cpp), each publish answered
-    with its own route ids on the host.  Not the metric: the per-publish latency a broker
-    process would see, and the rate once the ids leave the GPU."""
+    with its own route ids on the host, every id read once by the callback (a checksum, as a
+    NIF building its reply reads each id).  Not the metric: the per-publish latency a broker
+    process would see, and the rate once the results leave the GPU.  Default transport: runs
+    (the walk's spans of the engine's host id arena cross PCIe); `ids` rows ship the ids."""
     import ctypes as C
 
     from emqx_amd import _native as N
-    lg = C.CDLL(os.path.join(ROOT, "tools", "libtm_loadgen.so"))
-    lg.loadgen_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double,
-                               C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
-                               C.POINTER(C.c_double)]
+    lg = _loadgen()
     runs = []
     dt = max(2, min(14, cpu_topology()["usable_cpus"] - 3))  # leave the cutter, completer and caller a CPU
-    for pubs in (4096, 65536, 262144):
-        b = N.Batcher(eng, max_batch=65536, max_wait_us=200, delivery_threads=dt)
-        got, ids, errs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
-        rc = lg.loadgen_run(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, seconds, C.byref(got),
-                            C.byref(ids), C.byref(errs), C.byref(el))
+    plan = [(4096, N.TM_TRANSPORT_AUTO, 0), (65536, N.TM_TRANSPORT_AUTO, 0), (262144, N.TM_TRANSPORT_AUTO, 0),
+            (65536, N.TM_TRANSPORT_AUTO, 1), (65536, N.TM_TRANSPORT_IDS, 0)]
+    for pubs, transport, spans in plan:
+        b = N.Batcher(eng, max_batch=65536, max_wait_us=200, delivery_threads=dt, transport=transport)
+        got, ids, errs, cs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
+        rc = lg.loadgen_run2(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, seconds, spans,
+                             C.byref(got), C.byref(ids), C.byref(errs), C.byref(cs), C.byref(el))
         st = b.stats()
         b.close()
         if rc != 0 or errs.value:
             raise RuntimeError(f"batcher load failed: rc {rc}, {errs.value} failed publishes")
-        runs.append({"publishers": pubs, "publishes_per_s": round(got.value / el.value, 1),
+        runs.append({"publishers": pubs,
+                     "transport": "runs" if transport != N.TM_TRANSPORT_IDS else "ids (u32 over PCIe)",
+                     "callback": "spans (tm_batcher_submit_spans)" if spans else "id list (tm_batcher_submit)",
+                     "publishes_per_s": round(got.value / el.value, 1),
                      "ids_per_s": round(ids.value / el.value, 1),
                      "mean_batch": round(st["publishes"] / max(st["batches"], 1), 1),
                      "lat_p50_ms": round(st["lat_p50_us"] / 1e3, 3), "lat_p99_ms": round(st["lat_p99_us"] / 1e3, 3),
@@ -120,9 +135,65 @@ def batcher_load(eng, tb, to32, seconds):
                      "stage_busy": {k: round(st[k + "_us"] * 1e-6 / el.value, 3)
                                     for k in ("cut", "enqueue", "gpu_wait", "copy", "deliver")}})
     return {"api": f"tm_batcher_submit (max_batch 65536, max_wait 200 us, {dt} delivery threads)", "runs": runs,
-            "note": "closed loop: each publisher resubmits from its result callback; ids copied to host per "
-                    "window as u32 in chunks; four windows in flight (GPU walk / PCIe / callbacks); "
+            "note": "closed loop: each publisher resubmits from its result callback, which reads every id once; "
+                    "four windows in flight (GPU walk / PCIe / callbacks); runs transport: spans cross PCIe and "
+                    "replies are read from the host id arena (one span: zero-copy; several: gathered); "
                     "stage_busy: share of wall time each stage worked (copy and deliver: per delivery thread)"}
+
+
+def host_runs_leg(eng, tb, to32, n, w, reps=10):
+    """SURVEY §8(d)'s protocol on the runs form: H2D of the topics + walk + D2H of the spans
+    and per-topic arrays + the host view (tm_match_batch_runs), with the batch in pinned
+    memory as an aggregator holds it (and from pageable memory, staged by the engine); the
+    same plus a read of every id (tools/loadgen.cpp spans_checksum, 8 threads).  Parity: the
+    ids of the first 20,000 topics vs the oracle."""
+    import ctypes as C
+
+    import torch
+    lg = _loadgen()
+    pin = torch.empty(len(tb), dtype=torch.uint8, pin_memory=True)
+    pin.numpy()[:] = tb
+    pinned = pin.numpy()
+    out = {"api": "tm_match_batch_runs", "batch": n}
+    for name, buf in (("pinned", pinned), ("pageable", tb)):
+        eng.match_runs_view(buf, to32)
+        eng.lib.tm_runs_release(eng.h)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            eng.match_runs_view(buf, to32)
+            ts.append(time.perf_counter() - t0)
+            eng.lib.tm_runs_release(eng.h)
+        dt = float(np.mean(ts))
+        out[name] = {"ms_per_batch": round(dt * 1e3, 3), "p50_ms": round(float(np.percentile(ts, 50)) * 1e3, 3),
+                     "p99_ms": round(float(np.percentile(ts, 99)) * 1e3, 3), "publishes_per_s": round(n / dt, 1)}
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        res = eng.match_runs_view(pinned, to32)
+        lg.spans_checksum(C.byref(res), 8)
+        ts.append(time.perf_counter() - t0)
+        eng.lib.tm_runs_release(eng.h)
+    dt = float(np.mean(ts))
+    out["pinned_read_every_id"] = {"ms_per_batch": round(dt * 1e3, 3), "publishes_per_s": round(n / dt, 1),
+                                   "threads": 8}
+    res = eng.match_runs_view(pinned, to32)
+    out["spans_per_batch"] = int(res.total_spans)
+    out["ids_per_batch"] = int(res.total_ids)
+    out["d2h_bytes"] = int(res.total_spans) * 16 + 16 * n
+    eng.lib.tm_runs_release(eng.h)
+    ps = min(n, 20000)
+    o, ids, kcnt, st = eng.match_runs(tb, to32[:ps + 1])
+    eo, eids, est = oracle_index(w).match(tb, to32[:ps + 1], threads=16)
+    bad = sum(1 for i in range(ps) if not np.array_equal(np.sort(ids[o[i]:o[i + 1]]), eids[eo[i]:eo[i + 1]]))
+    bad += int(np.sum(st != est))
+    out["parity"] = {"sampled_topics": ps, "mismatches": int(bad), "oracle": "oracle/trie_search.cpp"}
+    out["note"] = ("spans of the engine's host id arena (16 B each) cross PCIe instead of 4 B per key; the host view "
+                   "is the spans themselves (the GPU writes their host addresses); pinned: the caller's batch is DMA'd "
+                   "directly")
+    if bad:
+        log(f"PARITY FAILURE (runs): {bad}/{ps} topics differ")
+    return out
 
 
 def gather_roof(walk, kernel_ms):
@@ -283,6 +354,7 @@ def main():
 
     from emqx_amd import _native as N
     from emqx_amd import workloads
+    lib_sha = N.check_build()  # the mapped library is the one built from these sources
 
     # ---------------------------------------------------------------- build
     # N = 1: one engine.  N > 1 (mode 1): rank 0 generates the workload and
@@ -410,6 +482,7 @@ def main():
     # (not the metric: the batching window's trade-off); rank 0 only
     lat_sweep = []
     host_path = None
+    host_runs = None
     batcher = None
     mode_rates = {}
     if rank == 0 and not args.profile:
@@ -457,6 +530,7 @@ def main():
                      "publishes_per_s": round(n / dt, 1),
                      "note": "H2D of the topics + kernels + D2H of every key + host result view; "
                              "bounded by PCIe D2H of the keys"}
+        host_runs = host_runs_leg(eng, tb, to32, n, w)
         batcher = batcher_load(eng, tb, to32, args.batcher_seconds) if args.batcher_seconds > 0 else None
 
     # ---------------------------------------------------------------- CPU baseline + parity sample
@@ -468,6 +542,12 @@ def main():
     legs = rank == 0 and not args.profile and not args.quick
     filt = filter_leg(args, w, eng, 20000) if legs else None
     inter = intersect_leg(w, tb, to) if legs else None
+    # BASELINE.md's other per-config rows (E churn, B), and a forced full rebuild of the headline
+    # index with matches running beside it (after every parity check on this engine)
+    extra = legs and world == 1
+    rebuild = rebuild_leg(eng, w, d_bytes, d_off, n, topic_bytes, dev) if extra else None
+    churn = churn_leg("E", 1.0, 1_000_000, 5, 1) if extra else None
+    cfg_b = config_leg("B", 1_000_000) if extra else None
 
     rss = torch.tensor([host_rss_gib()], dtype=torch.float64, device=dev if backend != "gloo" else "cpu")
     if world > 1:
@@ -518,14 +598,20 @@ def main():
             "gather": gather_roof(walk, kernel_ms),
             "latency_vs_batch": lat_sweep,
             "host_path": host_path,
+            "host_path_runs": host_runs,
             "batcher": batcher,
             "other_modes": mode_rates,
             "matches_filter": filt,
             "intersection": inter,
+            "rebuild_under_load": rebuild,
+            "churn_E": churn,
+            "config_B": cfg_b,
             "cpu_baseline": cpu,
             "parity": parity,
             "replica_parity": replica_parity,
             "spill_topics": int(slow_topics),
+            "library": {"path": os.path.relpath(N.LIB_PATH, ROOT), "src_sha": lib_sha,
+                        "build_info": N.load().tm_build_info().decode()},
             "build_s": round(t_build, 2),
             "host_peak_rss_gib": host_rss_gib(),
             "host_peak_rss_gib_max_over_ranks": round(float(rss.item()), 2),
@@ -629,6 +715,14 @@ def _new_filter(f, n):
 
 
 def run_churn(args):
+    """--churn EPOCHS: the churn leg alone, as its own JSON line."""
+    cfg = args.config if args.config != "C" else "E"
+    r = churn_leg(cfg, args.scale, args.batch, args.churn, args.warmup)
+    print(json.dumps(dict({"metric": "delta-epoch churn: route ops/s committed + matched publishes/s between epochs"},
+                          **r)), flush=True)
+
+
+def churn_leg(cfg, scale, batch, epochs, warmup):
     """Live subscribe/unsubscribe churn (BASELINE configs[4]): every epoch deletes 1% of the
     live route keys and adds 1% new ones (half are new dests on existing filters, like a
     $share group joining: emqx_shared_sub.erl:450; half new filter strings), commits them as
@@ -638,10 +732,8 @@ def run_churn(args):
     import torch
 
     from emqx_amd import _native as N
-    from emqx_amd import shard as S
     from emqx_amd import workloads
-    cfg = args.config if args.config != "C" else "E"
-    w = workloads.generate(cfg, scale=args.scale, n_topics=args.batch)
+    w = workloads.generate(cfg, scale=scale, n_topics=batch)
     dev = torch.device("cuda", 0)
     eng = N.Engine(0, reserve_keys=w.n_keys * 2, reserve_nodes=w.n_keys * 8)
     t0 = time.time()
@@ -670,7 +762,7 @@ def run_churn(args):
     eng.device_sync()
     tot = _read_u64(r.d_total)
     eng.reserve_matches(int(tot * 1.5) + 1024)
-    for ep in range(args.warmup + args.churn):
+    for ep in range(warmup + epochs):
         k = max(1, len(live_id) // 100)
         dsel = rng.choice(len(live_id), size=k, replace=False)
         keep = np.ones(len(live_id), dtype=bool)
@@ -700,10 +792,10 @@ def run_churn(args):
             raise RuntimeError("output arena overflow during churn bench")
         live_f = [f for f, kk in zip(live_f, keep) if kk] + add_f
         live_id = np.concatenate([live_id[keep], add_id])
-        if ep >= args.warmup:
+        if ep >= warmup:
             cs = eng.stats()
             full_eps.append(int(cs["n_full_rebuilds"]) > n_full_before)
-            phases.append((cs["commit_apply_us"], cs["commit_lists_us"], cs["commit_upload_us"]))
+            phases.append((cs["commit_apply_us"], cs["commit_lists_us"], cs["commit_upload_us"], cs["commit_stall_us"]))
             commit_ms.append((t1 - t0) * 1e3)
             match_ms.append(e0.elapsed_time(e1))
             nops.append(2 * k)
@@ -717,26 +809,171 @@ def run_churn(args):
     ids = eng.key_ids(keys)
     bad = sum(not np.array_equal(np.sort(ids[off[i]:off[i] + cnt[i]]), eids[eo[i]:eo[i + 1]]) for i in range(ps))
     st = eng.stats()
-    print(json.dumps({
-        "metric": "delta-epoch churn: route ops/s committed + matched publishes/s between epochs",
-        "config": {"workload": f"{cfg} (scale {args.scale}): {w.n_keys} initial route keys, 1% adds + 1% deletes "
+    eng.close()
+    return {
+        "config": {"workload": f"{cfg} (scale {scale}): {w.n_keys} initial route keys, 1% adds + 1% deletes "
                                f"per epoch", "publishes_per_batch": n},
-        "epochs": args.churn, "ops_per_epoch": int(np.mean(nops)),
+        "epochs": epochs, "ops_per_epoch": int(np.mean(nops)),
         "commit_ms_p50": round(float(np.percentile(commit_ms, 50)), 3),
         "commit_ms_p99": round(float(np.percentile(commit_ms, 99)), 3),
+        "commit_stall_ms_p50": round(float(np.percentile([x[3] for x in phases], 50)) / 1e3, 3),
         "commit_phase_ms_p50": dict(zip(("apply", "lists", "upload"),
-                                        (round(float(x) / 1e3, 3) for x in np.percentile(np.array(phases), 50, axis=0)))),
+                                        (round(float(x) / 1e3, 3)
+                                         for x in np.percentile(np.array(phases)[:, :3], 50, axis=0)))),
         "route_ops_per_s": round(float(np.sum(nops) / (np.sum(commit_ms) * 1e-3)), 1),
         "match_ms_p50": round(float(np.percentile(match_ms, 50)), 4),
         "publishes_per_s_incl_commit": round(n * len(match_ms) / ((np.sum(match_ms) + np.sum(commit_ms)) * 1e-3), 1),
         "full_rebuilds": st["n_full_rebuilds"], "delta_commits": st["n_delta_commits"],
         "commit_ms_per_epoch": [round(x, 2) for x in commit_ms],
-        "commit_phase_ms_per_epoch": [[round(x / 1e3, 2) for x in ph] for ph in phases],
+        "commit_phase_ms_per_epoch": [[round(x / 1e3, 2) for x in ph[:3]] for ph in phases],
         "full_rebuild_epochs": [i for i, f in enumerate(full_eps) if f],
         "build_s": round(t_build, 2),
         "host_peak_rss_gib": host_rss_gib(),
         "parity": {"sampled_topics": ps, "mismatches": int(bad), "oracle": "oracle/trie_search.cpp"},
-    }), flush=True)
+    }
+
+
+def config_leg(cfg, batch, steps=20):
+    """BASELINE.md's per-config row for another config on one GPU: device-resident batches of
+    `batch` publishes (tm_match_device), p50/p99 batch latency, k_match_fast time, HBM bytes
+    (algorithmic), the runs host path, and a 20,000-topic parity sample vs the oracle."""
+    import torch
+
+    from emqx_amd import _native as N
+    from emqx_amd import workloads
+    t0 = time.time()
+    w = workloads.generate(cfg, n_topics=batch)
+    eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    t_build = time.time() - t0
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    sp = stream.cuda_stream
+    n = w.n_topics
+    tbytes = int(w.t_off[-1])
+    d_bytes = torch.from_numpy(w.t_bytes).to(dev)
+    d_off = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
+
+    def step():
+        return eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, tbytes, sp)
+
+    r = step()
+    eng.device_sync()
+    total = _read_u64(r.d_total)
+    if total > r.keys_cap:
+        eng.reserve_matches(int(total * 1.1) + 1024)
+        step()
+        eng.device_sync()
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    eng.debug_stats(True, read=False)
+    step()
+    torch.cuda.synchronize()
+    walk = dict(zip(N.Engine.STAT_NAMES, [int(x) for x in eng.debug_stats(False)]))
+    eng.debug_stats(False, read=False)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    lat = [a.elapsed_time(b) for a, b in evs]
+    kms = []
+    for _ in range(5):
+        eng.timing(True)
+        step()
+        torch.cuda.synchronize()
+        kms.append(eng.timing(False))
+    kernel_ms = float(np.mean(kms))
+    alg = algorithmic_bytes(walk, tbytes, n)
+    to32 = np.ascontiguousarray(w.t_off, dtype=np.uint32)
+    runs = host_runs_leg(eng, w.t_bytes, to32, n, w, reps=5)
+    eng.close()
+    return {"config": {"workload": f"{cfg}: {w.n_keys} route keys", "route_keys": w.n_keys, "publishes_per_batch": n,
+                       "matches_per_batch": int(walk["keys"])},
+            "publishes_per_s": round(n * steps / el, 1), "ms_per_batch": round(el / steps * 1e3, 4),
+            "p50_batch_ms": round(float(np.percentile(lat, 50)), 4),
+            "p99_batch_ms": round(float(np.percentile(lat, 99)), 4),
+            "kernel_ms": round(kernel_ms, 4), "kernel_publishes_per_s": round(n / (kernel_ms * 1e-3), 1),
+            "roofline": {"bound": "hbm", "achieved": round(alg / (kernel_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(alg / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "algorithmic_bytes_per_launch": int(alg)},
+            "host_path_runs": {k: runs[k] for k in ("pinned", "pageable", "pinned_read_every_id", "parity")},
+            "build_s": round(t_build, 2)}
+
+
+def rebuild_leg(eng, w, d_bytes, d_off, n, topic_bytes, dev, frac=0.13):
+    """A forced FULL rebuild at the headline scale, with matches running beside it: one epoch
+    deletes `frac` of the route keys and re-adds the same keys (last op per key wins, so the key
+    set is unchanged but 2 x frac of it are deltas: past n_live / 8, a full rebuild: every list
+    rebuilt, the whole index uploaded into a standby image, then swapped).  A second thread keeps
+    matching batches of 131,072 publishes on its own stream; their latency during the commit,
+    against before it, is the stall the match path sees (plus tm_stats.commit_stall_us: how long
+    the swap held matches back).  A compaction takes the same path."""
+    import threading
+
+    import torch
+
+    from emqx_amd import _native as N
+    rng = np.random.default_rng(0xB1D)
+    k = int(len(w.f_id) * frac)
+    sel = np.sort(rng.choice(len(w.f_id), size=k, replace=False))
+    lens = (w.f_off[sel + 1] - w.f_off[sel]).astype(np.uint64)
+    off = np.zeros(k + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    idx = np.concatenate([np.arange(int(w.f_off[j]), int(w.f_off[j + 1])) for j in sel]) if k else np.zeros(0, np.int64)
+    fb = np.ascontiguousarray(w.f_bytes[idx])
+    ids = np.ascontiguousarray(w.f_id[sel])
+    s2 = torch.cuda.Stream(dev)
+    m = min(n, 131072)
+    lat = []
+    stop = threading.Event()
+
+    def matcher():
+        while not stop.is_set():
+            t0 = time.perf_counter()
+            eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), m, int(topic_bytes_m), s2.cuda_stream)
+            s2.synchronize()
+            lat.append((t0, time.perf_counter() - t0))
+
+    topic_bytes_m = int(d_off[m].item())
+    th = threading.Thread(target=matcher)
+    th.start()
+    time.sleep(0.5)
+    n_full0 = eng.stats()["n_full_rebuilds"]
+    t0 = time.perf_counter()
+    eng.apply_packed(N.TM_OP_DEL, fb, off, ids)
+    eng.apply_packed(N.TM_OP_ADD, fb, off, ids)
+    eng.commit()
+    t1 = time.perf_counter()
+    time.sleep(0.3)
+    stop.set()
+    th.join()
+    st = eng.stats()
+    before = [d for t, d in lat if t < t0]
+    during = [d for t, d in lat if t0 <= t < t1]
+    return {"ops": 2 * k, "full_rebuild": int(st["n_full_rebuilds"]) > int(n_full0),
+            "commit_s": round(t1 - t0, 3),
+            "commit_phase_s": {"apply": round(st["commit_apply_us"] / 1e6, 3),
+                               "lists": round(st["commit_lists_us"] / 1e6, 3),
+                               "upload_standby": round(st["commit_upload_us"] / 1e6, 3)},
+            "matches_held_back_ms": round(st["commit_stall_us"] / 1e3, 3),
+            "concurrent_match_batch": m,
+            "concurrent_batches_during_commit": len(during),
+            "match_ms_before": {"p50": round(float(np.percentile(before, 50)) * 1e3, 3) if before else None,
+                                "max": round(float(np.max(before)) * 1e3, 3) if before else None},
+            "match_ms_during_commit": {"p50": round(float(np.percentile(during, 50)) * 1e3, 3) if during else None,
+                                       "p99": round(float(np.percentile(during, 99)) * 1e3, 3) if during else None,
+                                       "max": round(float(np.max(during)) * 1e3, 3) if during else None},
+            "note": "one epoch re-keys a share of the route keys (deleted and re-added: the same key set, all of them "
+                    "deltas) so the commit takes the full-rebuild path; the index is uploaded into a standby device "
+                    "image while the second thread keeps matching; match latency is wall time per batch incl. "
+                    "the host call"}
 
 
 def replica_check(eng, all_b, all_o, s, dev, backend, sp, world):

@@ -61,12 +61,12 @@ EXPORTS = (
     "tm_result_ids_device", "tm_merge_shards_device", "tm_merge_shards", "tm_match_device_mode",
     "tm_match_filter_batch", "tm_intersect_batch", "tm_result_ids_device_ex", "tm_image_size", "tm_image_export",
     "tm_replica_create", "tm_replica_load", "tm_patch_size", "tm_patch_export", "tm_replica_apply_patch",
-    "tm_discard_staged", "tm_result_release", "tm_match_batch_runs", "tm_runs_release",
+    "tm_discard_staged", "tm_result_release", "tm_match_batch_runs", "tm_runs_release", "tm_build_info",
 )
 # every symbol include/emqx_tm_batcher.h declares
 BATCHER_EXPORTS = (
     "tm_batcher_create", "tm_batcher_create_fn", "tm_batcher_destroy", "tm_batcher_submit", "tm_batcher_match",
-    "tm_batcher_apply", "tm_batcher_commit", "tm_batcher_stats_get",
+    "tm_batcher_apply", "tm_batcher_commit", "tm_batcher_stats_get", "tm_batcher_submit_spans",
 )
 
 
@@ -133,7 +133,10 @@ class tm_runs_result(C.Structure):
 
 class tm_batcher_config(C.Structure):
     _fields_ = [("max_batch", C.c_uint32), ("max_wait_us", C.c_uint32), ("mode", C.c_uint32),
-                ("delivery_threads", C.c_uint32)]
+                ("delivery_threads", C.c_uint32), ("transport", C.c_uint32)]
+
+
+TM_TRANSPORT_AUTO, TM_TRANSPORT_IDS, TM_TRANSPORT_RUNS = 0, 1, 2
 
 
 class tm_batch_view(C.Structure):
@@ -148,6 +151,7 @@ class tm_batcher_stats(C.Structure):
 
 
 tm_match_cb = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.POINTER(C.c_uint64), C.c_uint32)
+tm_spans_cb = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_void_p, C.c_uint32, C.c_uint64)
 tm_batch_fn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32, C.c_uint32,
                           C.POINTER(tm_batch_view))
 
@@ -166,6 +170,7 @@ def load() -> C.CDLL:
     lib = C.CDLL(LIB_PATH)
     P = C.POINTER
     lib.tm_abi_version.restype = C.c_uint32
+    lib.tm_build_info.restype = C.c_char_p
     lib.tm_create.argtypes = [P(tm_config), P(C.c_void_p)]
     lib.tm_destroy.argtypes = [C.c_void_p]
     lib.tm_destroy.restype = None
@@ -209,13 +214,14 @@ def load() -> C.CDLL:
     lib.tm_merge_shards.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
                                     C.c_void_p, C.c_uint64]
     for name in EXPORTS:
-        if name not in ("tm_destroy", "tm_last_error", "tm_abi_version"):
+        if name not in ("tm_destroy", "tm_last_error", "tm_abi_version", "tm_build_info"):
             getattr(lib, name).restype = C.c_int
     lib.tm_batcher_create.argtypes = [C.c_void_p, P(tm_batcher_config), P(C.c_void_p)]
     lib.tm_batcher_create_fn.argtypes = [tm_batch_fn, C.c_void_p, P(tm_batcher_config), P(C.c_void_p)]
     lib.tm_batcher_destroy.argtypes = [C.c_void_p]
     lib.tm_batcher_destroy.restype = None
     lib.tm_batcher_submit.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, tm_match_cb, C.c_void_p]
+    lib.tm_batcher_submit_spans.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, tm_spans_cb, C.c_void_p]
     lib.tm_batcher_match.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, P(C.c_uint32),
                                      P(C.c_int32)]
     lib.tm_batcher_apply.argtypes = [C.c_void_p, P(tm_op), C.c_size_t]
@@ -226,6 +232,22 @@ def load() -> C.CDLL:
             getattr(lib, name).restype = C.c_int
     _lib = lib
     return lib
+
+
+def build_sha() -> str:
+    """The source hash the loaded library was built from (tm_build_info)."""
+    info = load().tm_build_info().decode()
+    return dict(kv.split("=", 1) for kv in info.split()).get("src_sha", "")
+
+
+def check_build():
+    """Fail loudly when the library does not match the sources next to it."""
+    from emqx_amd.build import src_sha
+    have, want = build_sha(), src_sha()
+    if have != want:
+        raise RuntimeError(f"{LIB_PATH} was built from other sources (src_sha {have[:12]} != {want[:12]}): "
+                           "run __graft_entry__.build()")
+    return have
 
 
 def merge_shards(counts: np.ndarray, ids: np.ndarray):
@@ -609,9 +631,9 @@ class Batcher:
     Python batch matcher; the C-ABI's tm_batcher_create_fn)."""
 
     def __init__(self, engine: "Engine | None" = None, *, backend=None, max_batch: int = 0, max_wait_us: int = 0,
-                 mode: int = TM_MATCH_ALL, delivery_threads: int = 0):
+                 mode: int = TM_MATCH_ALL, delivery_threads: int = 0, transport: int = TM_TRANSPORT_AUTO):
         self.lib = load()
-        cfg = tm_batcher_config(max_batch, max_wait_us, mode, delivery_threads)
+        cfg = tm_batcher_config(max_batch, max_wait_us, mode, delivery_threads, transport)
         h = C.c_void_p()
         self._keep = []
         if engine is not None:

@@ -19,14 +19,54 @@ def _newer(out, srcs):
     return os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(s) for s in srcs)
 
 
+TM_SRCS = ("emqx_amd/csrc/engine.cpp", "emqx_amd/csrc/batcher.cpp", "emqx_amd/csrc/match_kernels.hip",
+           "emqx_amd/csrc/result_kernels.hip", "emqx_amd/csrc/filter_kernels.hip", "emqx_amd/csrc/layout.h",
+           "emqx_amd/csrc/device_api.h", "emqx_amd/csrc/filter_api.h", "emqx_amd/csrc/wave.h", "include/emqx_tm.h",
+           "include/emqx_tm_batcher.h")
+
+
+def src_sha() -> str:
+    """sha256 over the product library's sources (path + content of each): embedded in the
+    library at build time (tm_build_info), compared by build(), smoke() and bench.py."""
+    import hashlib
+    root = os.path.dirname(HERE)
+    h = hashlib.sha256()
+    for f in TM_SRCS:
+        h.update(f.encode() + b"\0")
+        h.update(open(os.path.join(root, f), "rb").read())
+    return h.hexdigest()
+
+
+def built_sha(lib_path: str):
+    """The source hash a built libemqx_tm.so carries (None if it has none or cannot load).
+    Read in a child process: loading the HIP library here would pin it in this process."""
+    import subprocess
+    if not os.path.exists(lib_path):
+        return None
+    code = ("import ctypes,sys; l=ctypes.CDLL(sys.argv[1]); l.tm_build_info.restype=ctypes.c_char_p; "
+            "print(l.tm_build_info().decode())")
+    try:
+        out = subprocess.run([sys.executable, "-c", code, lib_path], capture_output=True, text=True, timeout=120)
+    except (OSError, subprocess.SubprocessError):
+        return None
+    for tok in out.stdout.split():
+        if tok.startswith("src_sha="):
+            return tok[len("src_sha="):]
+    return None
+
+
 def build(force: bool = False, verbose: bool = True):
     tm = os.path.join(HERE, "libemqx_tm.so")
     srcs = [os.path.join(CSRC, f) for f in ("engine.cpp", "batcher.cpp", "match_kernels.hip",
                                             "result_kernels.hip", "filter_kernels.hip", "layout.h", "device_api.h", "filter_api.h",
                                             "wave.h")]
     srcs += [os.path.join(os.path.dirname(HERE), "include", h) for h in ("emqx_tm.h", "emqx_tm_batcher.h")]
-    if force or not _newer(tm, srcs):
+    sha = src_sha()
+    # rebuilt whenever the library's embedded source hash differs from the sources' (not mtimes:
+    # the tree travels to the GPU box with its built library)
+    if force or built_sha(tm) != sha:
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+               f'-DTM_SRC_SHA="{sha}"',
                "-Wno-unused-function", os.path.join(CSRC, "engine.cpp"), os.path.join(CSRC, "batcher.cpp"),
                os.path.join(CSRC, "match_kernels.hip"),
                os.path.join(CSRC, "result_kernels.hip"), os.path.join(CSRC, "filter_kernels.hip"), "-o", tm]

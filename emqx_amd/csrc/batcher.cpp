@@ -46,6 +46,17 @@ extern "C" int tmx_result_ids32_device(tm_engine *eng, uint32_t *d_ids, uint64_t
                                        void *stream);
 extern "C" void tmx_engine_lock(tm_engine *eng);
 extern "C" void tmx_engine_unlock(tm_engine *eng);
+extern "C" int tmx_batch_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                                      uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out);
+extern "C" int tmx_result_ids64_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
+                                       void *stream);
+extern "C" int tmx_batch_match_runs(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                                    uint64_t total_bytes, void *stream, void *d_spans, uint64_t spans_cap,
+                                    uint32_t *d_soff, uint32_t *d_scnt, uint32_t *d_kcnt, int32_t *d_status,
+                                    unsigned long long *d_cursor, const void **d_ctl_out);
+extern "C" void tmx_lease_take(tm_engine *eng);
+extern "C" void tmx_lease_drop(tm_engine *eng);
+extern "C" int tmx_engine_is_replica(const tm_engine *eng);
 
 namespace {
 
@@ -114,7 +125,8 @@ struct HBuf {
 
 struct Pending {
     uint32_t len;
-    tm_match_cb cb;
+    tm_match_cb cb;    // id-list callback, or
+    tm_spans_cb scb;   // span callback (tm_batcher_submit_spans)
     void *ctx;
     uint64_t t0;  // submit time (ns)
 };
@@ -173,6 +185,13 @@ struct Slot {
     std::vector<uint32_t> cnt;          // per-publish counts
     std::vector<uint64_t> ids_host;     // host-path ids
     tm_batch_view v{};
+    // runs transport (TM_MATCH_ALL on a master engine): the walk's spans of the engine's host
+    // id arena cross PCIe instead of the ids; the window holds a read lease until delivered
+    bool runs = false, leased = false;
+    DBuf d_spans, d_soff, d_scnt, d_kcnt, d_st, d_cur;
+    HBuf h_spans, h_soff, h_scnt, h_kcnt;
+    uint64_t spans_cap = 0;
+    const void *d_ctl = nullptr;
 };
 
 }  // namespace
@@ -191,6 +210,8 @@ struct tm_batcher {
     std::atomic<uint32_t> cutter_idle{0};  // 1 while the cutter sleeps on an empty queue
 
     std::mutex eng_mu;  // the cutter's enqueue vs a re-run from the completion thread
+    double spans_per_pub = 4.0;  // runs transport: spans per publish of recent windows (sizes the next)
+    bool runs_ok = false;        // runs transport in use (TM_MATCH_ALL windows of a master engine)
     hipStream_t s_comp = nullptr, s_copy = nullptr;
     int device = 0;
 
@@ -222,7 +243,7 @@ struct tm_batcher {
     // ------------------------------------------------------------------ submit side
     // No state shared by all submitters on this path: one shard lock (shards by submitting
     // thread) and a read of the cutter's idle flag.
-    int submit(const uint8_t *topic, uint32_t len, tm_match_cb cb, void *ctx) {
+    int submit(const uint8_t *topic, uint32_t len, tm_match_cb cb, tm_spans_cb scb, void *ctx) {
         const uint64_t t0 = now_ns();
         Shard &sh = shards[shard_of_thread()];
         {
@@ -231,7 +252,7 @@ struct tm_batcher {
             // `stopping` is set, so a publish either lands before that pass or is refused here
             if (stopping.load()) return TM_ESTATE;
             if (sh.bytes.size() + len > QUEUE_BYTES_MAX / SHARDS) return TM_ENOMEM;  // back-pressure
-            sh.q.push_back(Pending{len, cb, ctx, t0});
+            sh.q.push_back(Pending{len, cb, scb, ctx, t0});
             sh.bytes.insert(sh.bytes.end(), topic, topic + len);
             sh.n.store((uint32_t)sh.q.size(), std::memory_order_relaxed);
         }
@@ -320,6 +341,7 @@ struct tm_batcher {
     int enqueue_locked(Slot &S) {
         const uint32_t n = S.n;
         S.host_done = false;
+        if (S.runs) return enqueue_runs(S);
         BT_HIP(hipSetDevice(device));
         BT_HIP(S.d_bytes.ensure(S.nbytes + 16));
         BT_HIP(S.d_off.ensure((size_t)n * 4 + 4));
@@ -332,8 +354,8 @@ struct tm_batcher {
         BT_HIP(hipMemcpyAsync(S.d_bytes.p, S.h_bytes.p, S.nbytes + 1, hipMemcpyHostToDevice, s_comp));
         BT_HIP(hipMemcpyAsync(S.d_off.p, S.h_off.p, (size_t)n * 4 + 4, hipMemcpyHostToDevice, s_comp));
         tm_dev_result r;
-        int rc = tm_match_device_mode(eng, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes,
-                                      S.mode, s_comp, &r);
+        int rc = tmx_batch_match_device(eng, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes,
+                                        S.mode, s_comp, &r);
         if (rc) return rc;
         S.keys_cap = r.keys_cap;
         std::memset(S.h_ctl.p, 0, CTL_BYTES);
@@ -348,12 +370,84 @@ struct tm_batcher {
             rc = tmx_result_ids32_device(eng, (uint32_t *)S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp);
             S.narrow = rc == TM_OK;
             if (rc == TM_ESTATE)
-                rc = tm_result_ids_device(eng, (uint64_t *)S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp);
+                rc = tmx_result_ids64_device(eng, (uint64_t *)S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp);
             if (rc) return rc;
             BT_HIP(hipMemcpyAsync(S.h_off_out.p, S.d_off_out.p, (size_t)n * 4 + 4, hipMemcpyDeviceToHost, s_comp));
         }
         BT_HIP(hipMemcpyAsync(S.h_status.p, r.d_status, (size_t)n * 4, hipMemcpyDeviceToHost, s_comp));
         BT_HIP(hipEventRecord(S.ev, s_comp));
+        return TM_OK;
+    }
+
+    // Runs transport: the walk writes the window's spans and per-publish arrays into the slot;
+    // the counters (span cursor, pool demand) and the per-publish arrays come back on the
+    // compute stream, the spans themselves on the copy stream once their count is known.
+    int enqueue_runs(Slot &S) {
+        const uint32_t n = S.n;
+        BT_HIP(hipSetDevice(device));
+        BT_HIP(S.d_bytes.ensure(S.nbytes + 16));
+        BT_HIP(S.d_off.ensure((size_t)n * 4 + 4));
+        for (DBuf *d : {&S.d_soff, &S.d_scnt, &S.d_kcnt, &S.d_st}) BT_HIP(d->ensure((size_t)n * 4 + 4));
+        BT_HIP(S.d_cur.ensure(64));
+        for (HBuf *h : {&S.h_soff, &S.h_scnt, &S.h_kcnt, &S.h_status}) BT_HIP(h->ensure((size_t)n * 4 + 4));
+        BT_HIP(S.h_ctl.ensure(64));
+        if (!S.ev) BT_HIP(hipEventCreateWithFlags(&S.ev, EV_FLAGS));
+        const uint64_t want = std::max<uint64_t>(4096, (uint64_t)(spans_per_pub * 1.5 * n) + 1024);
+        if (S.spans_cap < want) {
+            BT_HIP(S.d_spans.ensure(want * 16));
+            S.spans_cap = S.d_spans.cap / 16;
+        }
+        BT_HIP(hipMemcpyAsync(S.d_bytes.p, S.h_bytes.p, S.nbytes + 1, hipMemcpyHostToDevice, s_comp));
+        BT_HIP(hipMemcpyAsync(S.d_off.p, S.h_off.p, (size_t)n * 4 + 4, hipMemcpyHostToDevice, s_comp));
+        int rc = tmx_batch_match_runs(eng, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, s_comp,
+                                      S.d_spans.p, S.spans_cap, (uint32_t *)S.d_soff.p, (uint32_t *)S.d_scnt.p,
+                                      (uint32_t *)S.d_kcnt.p, (int32_t *)S.d_st.p, (unsigned long long *)S.d_cur.p,
+                                      &S.d_ctl);
+        if (rc) return rc;
+        // h_ctl: [0] spans reserved, [1..4] the launch's counter block {-, slow, seg, fr}
+        BT_HIP(hipMemcpyAsync(S.h_ctl.p, S.d_cur.p, 8, hipMemcpyDeviceToHost, s_comp));
+        BT_HIP(hipMemcpyAsync(S.h_ctl.as<uint8_t>() + 8, S.d_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s_comp));
+        BT_HIP(hipMemcpyAsync(S.h_soff.p, S.d_soff.p, (size_t)n * 4, hipMemcpyDeviceToHost, s_comp));
+        BT_HIP(hipMemcpyAsync(S.h_scnt.p, S.d_scnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s_comp));
+        BT_HIP(hipMemcpyAsync(S.h_kcnt.p, S.d_kcnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s_comp));
+        BT_HIP(hipMemcpyAsync(S.h_status.p, S.d_st.p, (size_t)n * 4, hipMemcpyDeviceToHost, s_comp));
+        BT_HIP(hipEventRecord(S.ev, s_comp));
+        return TM_OK;
+    }
+
+    int complete_runs(Slot &S) {
+        const uint64_t tw0 = now_ns();
+        BT_HIP(hipEventSynchronize(S.ev));
+        ns_gpu.fetch_add(now_ns() - tw0, std::memory_order_relaxed);
+        const uint64_t *ctl = S.h_ctl.as<uint64_t>();
+        uint64_t total = ctl[0];
+        const uint64_t seg = ctl[3], fr = ctl[4];
+        uint64_t seg_cap = 0, fr_cap = 0;
+        tmx_engine_pool_caps(eng, &seg_cap, &fr_cap);
+        const bool over = total > S.spans_cap;
+        if (over || seg > seg_cap || fr > fr_cap) {
+            std::lock_guard<std::mutex> g(eng_mu);
+            BT_HIP(hipStreamSynchronize(s_comp));
+            int rc = tmx_engine_grow_pools(eng, seg, fr);
+            if (rc) return rc;
+            if (over) {  // more spans than the window's buffer: grow to the demand, run again
+                spans_per_pub = std::max(spans_per_pub, (double)total / std::max<uint32_t>(S.n, 1));
+                if ((rc = enqueue(S))) return rc;
+                BT_HIP(hipEventSynchronize(S.ev));
+                total = S.h_ctl.as<uint64_t>()[0];
+                if (total > S.spans_cap) return TM_EDEVICE;
+            }
+        }
+        spans_per_pub = 0.9 * spans_per_pub + 0.1 * ((double)total / std::max<uint32_t>(S.n, 1));
+        BT_HIP(S.h_spans.ensure(total * 16 + 16));
+        S.nchunk = 1;
+        S.chunk_lo[0] = 0;
+        S.chunk_lo[1] = S.n;
+        BT_HIP(hipStreamWaitEvent(s_copy, S.ev, 0));
+        if (total) BT_HIP(hipMemcpyAsync(S.h_spans.p, S.d_spans.p, total * 16, hipMemcpyDeviceToHost, s_copy));
+        BT_HIP(hipEventRecord(S.cev[0], s_copy));
+        S.cev_wait = true;
+        S.v.status = S.h_status.as<int32_t>();
         return TM_OK;
     }
 
@@ -394,6 +488,7 @@ struct tm_batcher {
             S.cev_wait = false;
             return TM_OK;
         }
+        if (S.runs) return complete_runs(S);
         const uint64_t tw0 = now_ns();
         BT_HIP(hipEventSynchronize(S.ev));
         const uint64_t tw1 = now_ns();
@@ -461,9 +556,53 @@ struct tm_batcher {
     }
 
     // ------------------------------------------------------------------ delivery
+    // one publish's reply: its own id list (gathered from its spans when it has several), or
+    // the spans themselves for a span callback
+    static void reply(const Pending &p, int32_t st, const tm_span *sp, uint32_t ns, uint64_t nids) {
+        thread_local std::vector<uint64_t> flat;
+        if (p.scb) {
+            p.scb(p.ctx, st, sp, ns, nids);
+            return;
+        }
+        if (ns == 1) {  // zero-copy: one run of the id arena
+            p.cb(p.ctx, st, sp[0].ids, (uint32_t)nids);
+            return;
+        }
+        if (flat.size() < nids) flat.resize(nids);
+        uint64_t at = 0;
+        for (uint32_t j = 0; j < ns; j++) {
+            std::memcpy(flat.data() + at, sp[j].ids, sp[j].n * 8);
+            at += sp[j].n;
+        }
+        p.cb(p.ctx, st, nids ? flat.data() : nullptr, (uint32_t)nids);
+    }
+
     void deliver_range(Slot &S, uint32_t lo, uint32_t hi, int rc) {
         std::vector<uint32_t> lats;
         lats.reserve(hi - lo);
+        if (S.runs && rc >= 0) {
+            const tm_span *spans = S.h_spans.as<tm_span>();
+            const uint32_t *so = S.h_soff.as<uint32_t>(), *sc = S.h_scnt.as<uint32_t>(), *kc = S.h_kcnt.as<uint32_t>();
+            const int32_t *stv = S.h_status.as<int32_t>();
+            uint64_t now = 0;
+            for (uint32_t i = lo; i < hi; i++) {
+                const Pending &p = S.pubs[i];
+                if (i + 8 < hi) __builtin_prefetch(S.pubs[i + 8].ctx);
+                const int32_t st = stv[i];
+                if (st == TM_TOPIC_OK) reply(p, st, spans + so[i], sc[i], kc[i]);
+                else reply(p, st, nullptr, 0, 0);
+                if (((i - lo) & 15) == 0) now = now_ns();
+                const uint64_t d = now > p.t0 ? now - p.t0 : 0;
+                lats.push_back(d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d);
+            }
+            std::lock_guard<std::mutex> g(st_mu);
+            for (uint32_t x : lats) {
+                lat_ns[lat_pos] = x;
+                lat_pos = (lat_pos + 1) % LAT_RING;
+            }
+            lat_n = std::min(LAT_RING, lat_n + lats.size());
+            return;
+        }
         thread_local std::vector<uint64_t> wide;  // a narrowed window's ids, one publish at a time
         const uint32_t *ids32 = S.narrow ? reinterpret_cast<const uint32_t *>(S.v.ids) : nullptr;
         uint64_t now = 0;
@@ -471,7 +610,8 @@ struct tm_batcher {
             const Pending &p = S.pubs[i];
             if (i + 8 < hi) __builtin_prefetch(S.pubs[i + 8].ctx);  // the caller's per-publish state
             if (rc < 0) {
-                p.cb(p.ctx, rc, nullptr, 0);
+                if (p.scb) p.scb(p.ctx, rc, nullptr, 0, 0);
+                else p.cb(p.ctx, rc, nullptr, 0);
             } else {
                 const int32_t st = S.v.status[i];
                 const uint32_t c = st == TM_TOPIC_OK ? S.v.cnt[i] : 0;
@@ -486,7 +626,12 @@ struct tm_batcher {
                         ids = S.v.ids + S.v.off[i];
                     }
                 }
-                p.cb(p.ctx, st, ids, c);
+                if (p.scb) {
+                    const tm_span one{ids, c};
+                    p.scb(p.ctx, st, c ? &one : nullptr, c ? 1u : 0u, c);
+                } else {
+                    p.cb(p.ctx, st, ids, c);
+                }
             }
             if (((i - lo) & 15) == 0) now = now_ns();  // one clock read per 16 callbacks
             const uint64_t d = now > p.t0 ? now - p.t0 : 0;
@@ -531,6 +676,10 @@ struct tm_batcher {
     }
 
     void free_slot(Slot &S) {
+        if (S.leased) {  // the window's spans are delivered: a commit may change the id arena now
+            S.leased = false;
+            tmx_lease_drop(eng);
+        }
         {
             std::lock_guard<std::mutex> g(slot_mu);
             S.state = Slot::FREE;
@@ -618,12 +767,18 @@ struct tm_batcher {
                 S.state = Slot::BUSY;
             }
             const uint64_t tc0 = now_ns();
+            S.runs = false;
             S.rc = take_window(S);
             S.mode = cfg.mode;
             S.t_enq = now_ns();
             ns_cut.fetch_add(S.t_enq - tc0, std::memory_order_relaxed);
             if (S.rc == TM_OK && S.n) {
                 if (eng) {
+                    S.runs = runs_ok && S.mode == TM_MATCH_ALL;
+                    if (S.runs) {  // leases come before any engine lock (include/emqx_tm.h)
+                        tmx_lease_take(eng);
+                        S.leased = true;
+                    }
                     std::lock_guard<std::mutex> g(eng_mu);
                     S.rc = enqueue(S);
                     if (S.rc == TM_ESTATE && S.mode == TM_MATCH_UNIQUE) S.rc = run_host(S);
@@ -699,6 +854,8 @@ struct tm_batcher {
                 for (HBuf *h : {&S.h_bytes, &S.h_off, &S.h_off_out, &S.h_status, &S.h_cnt, &S.h_ids, &S.h_ctl})
                     h->pinned = false;
         if (eng) {
+            runs_ok = cfg.transport != TM_TRANSPORT_IDS && !tmx_engine_is_replica(eng);
+            if (cfg.transport == TM_TRANSPORT_RUNS && !runs_ok) return TM_ESTATE;
             device = tmx_engine_device(eng);
             if (hipSetDevice(device) != hipSuccess ||
                 hipStreamCreateWithFlags(&s_comp, hipStreamNonBlocking) != hipSuccess ||
@@ -790,7 +947,12 @@ void tm_batcher_destroy(tm_batcher *b) {
 
 int tm_batcher_submit(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_match_cb cb, void *ctx) {
     if (!b || !cb || (len && !topic) || len > 65535) return TM_EINVAL;
-    return b->submit(topic, len, cb, ctx);
+    return b->submit(topic, len, cb, nullptr, ctx);
+}
+
+int tm_batcher_submit_spans(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_spans_cb cb, void *ctx) {
+    if (!b || !cb || (len && !topic) || len > 65535) return TM_EINVAL;
+    return b->submit(topic, len, nullptr, cb, ctx);
 }
 
 namespace {

@@ -133,6 +133,7 @@ struct BatchBufs {
     uint32_t last_n = 0;     // topics of the last batch
     uint32_t last_mode = 0;  // TM_MATCH_* of the last batch
     bool dev_batch = true;   // the device holds the last batch whole (tm_result_ids_device*)
+    hipStream_t last_stream = nullptr;  // stream of the last batch (the next one is ordered after it)
     void release() {
         for (DevBuf *b : {&d_bytes, &d_off, &d_outoff, &d_outcnt, &d_status, &d_keys, &d_slow_list, &d_scr_w, &d_scr_s,
                           &d_seg_pool, &d_fr_pool, &d_wave_chunks, &d_ukeys, &d_ucnt, &d_dd_wl, &d_dd_wl_n, &d_kcnt,
@@ -459,7 +460,7 @@ struct tm_engine {
     // engine keeps until the next such call) and one for the host-result calls (tm_match_batch*,
     // synchronous), so a host call from one thread never overwrites another thread's pending
     // device result.  `bb` is the set of the call in progress (under mu_dev).
-    BatchBufs bb_dev, bb_host;
+    BatchBufs bb_dev, bb_host, bb_batch;  // bb_batch: the batching aggregator's windows (batcher.cpp)
     BatchBufs *bb = &bb_dev;
     double runs_spt = 4.0;     // spans per topic of the last runs batch (sizes the next)
     PinBuf h_rctl;             // runs: per sub-batch {span cursor, counter block}
@@ -475,7 +476,6 @@ struct tm_engine {
         std::lock_guard<std::mutex> g(mu_stage);
         return staged.size();
     }
-    hipStream_t last_stream = nullptr;  // stream of the last tm_match_device call
     bool stats_on = false;
     uint64_t max_id = 0;     // largest id ever added (ids fit u32 results while < 2^32)
     PatchLog patch;          // master: the last commit's device changes (TM_CFG_RECORD_PATCH)
@@ -541,10 +541,10 @@ struct tm_engine {
     // on last_stream): order s after everything queued on last_stream so far, which includes
     // the previous caller's reads of its result.
     hipError_t chain_after_last(hipStream_t s) {
-        if (!last_stream || last_stream == s) return hipSuccess;
+        if (!bb->last_stream || bb->last_stream == s) return hipSuccess;
         hipError_t e;
         if (!ev_chain && (e = hipEventCreateWithFlags(&ev_chain, hipEventDisableTiming))) return e;
-        if ((e = hipEventRecord(ev_chain, last_stream))) return e;
+        if ((e = hipEventRecord(ev_chain, bb->last_stream))) return e;
         return hipStreamWaitEvent(s, ev_chain, 0);
     }
 
@@ -556,21 +556,27 @@ struct tm_engine {
     }
 
     // ---- read leases on the host id arena (tm_match_batch_runs)
-    void lease_take(HostOut &o) {
-        if (o.lease) return;
+    void lease_take_raw() {
         std::unique_lock<std::mutex> lk(lease_mu);
         lease_cv.wait(lk, [&] { return !lease_block; });
         n_leases++;
+    }
+    void lease_drop_raw() {
+        {
+            std::lock_guard<std::mutex> g(lease_mu);
+            n_leases--;
+        }
+        lease_cv.notify_all();
+    }
+    void lease_take(HostOut &o) {
+        if (o.lease) return;
+        lease_take_raw();
         o.lease = true;
     }
     void lease_drop(HostOut &o) {
         if (!o.lease) return;
-        {
-            std::lock_guard<std::mutex> g(lease_mu);
-            n_leases--;
-            o.lease = false;
-        }
-        lease_cv.notify_all();
+        o.lease = false;
+        lease_drop_raw();
     }
     // a commit's host phase: no new leases, wait for the held ones (writer preference)
     void leases_block() {
@@ -1853,6 +1859,15 @@ extern "C" {
 
 uint32_t tm_abi_version(void) { return TM_ABI_VERSION; }
 
+#ifndef TM_SRC_SHA
+#define TM_SRC_SHA "unknown"
+#endif
+const char *tm_build_info(void) {
+    static const std::string info =
+        std::string("src_sha=") + TM_SRC_SHA + " abi=" + std::to_string(TM_ABI_VERSION) + " arch=gfx950";
+    return info.c_str();
+}
+
 int tm_create(const tm_config *cfg, tm_engine **out) {
     if (!out) return TM_EINVAL;
     *out = nullptr;
@@ -1925,6 +1940,7 @@ void tm_destroy(tm_engine *eng) {
     eng->release_ids();
     eng->bb_dev.release();
     eng->bb_host.release();
+    eng->bb_batch.release();
     eng->h_rctl.release();
     for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
@@ -1956,14 +1972,14 @@ static int grow_pools(tm_engine *eng);
 __attribute__((visibility("hidden"))) void tmx_engine_pool_caps(const tm_engine *eng, uint64_t *seg_chunks,
                                                                uint64_t *fr_chunks) {
     std::lock_guard<std::recursive_mutex> g(const_cast<tm_engine *>(eng)->mu_dev);
-    const_cast<tm_engine *>(eng)->bb = const_cast<BatchBufs *>(&eng->bb_dev);
+    const_cast<tm_engine *>(eng)->bb = const_cast<BatchBufs *>(&eng->bb_batch);
     *seg_chunks = eng->cfg.seg_chunks ? ~0ull : eng->bb->seg_chunks;  // fixed pools (test aid) never grow
     *fr_chunks = eng->cfg.seg_chunks ? ~0ull : eng->bb->fr_chunks;
 }
 __attribute__((visibility("hidden"))) int tmx_engine_grow_pools(tm_engine *eng, uint64_t seg_demand,
                                                                 uint64_t fr_demand) {
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
-    eng->bb = &eng->bb_dev;
+    eng->bb = &eng->bb_batch;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     eng->bb->seg_demand_last = seg_demand;
     eng->bb->fr_demand_last = fr_demand;
@@ -2121,9 +2137,15 @@ static int grow_pools(tm_engine *eng) {
 
 // `obase`: the batch's per-topic results go to d_outoff/d_outcnt/d_status + obase; `keys`,
 // `keys_cap`: its key output (default: the whole arena)
+// per-topic outputs of a batch in buffers the caller owns (the aggregator's windows)
+struct TopicOut {
+    uint32_t *off, *cnt, *kcnt;
+    int32_t *status;
+};
 static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                                 hipStream_t s, uint32_t mode = MODE_ALL, uint32_t obase = 0, uint32_t *keys = nullptr,
-                                uint64_t keys_cap = 0, unsigned long long *cursor = nullptr) {
+                                uint64_t keys_cap = 0, unsigned long long *cursor = nullptr,
+                                const TopicOut *to = nullptr) {
     MatchArgs a{};
     a.mode = mode;
     a.tpw = pick_tpw(n, eng->cfg.topics_per_wave);
@@ -2154,6 +2176,12 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
         a.out_kcnt = eng->bb->d_kcnt.as<uint32_t>() + obase;
         a.span_arena = (uint64_t)(uintptr_t)eng->arena_id;
         a.span_keys = eng->keys.empty() ? 0 : (uint64_t)(uintptr_t)&eng->keys[0].id;
+    }
+    if (to) {
+        a.out_off = to->off;
+        a.out_cnt = to->cnt;
+        a.out_kcnt = to->kcnt;
+        a.status = to->status;
     }
     a.ctl_next = (unsigned long long *)(eng->bb->d_ctl.as<uint8_t>() + (eng->bb->ctl_cur ^ 1u) * CTL_BYTES);
     a.slow_list = eng->bb->d_slow_list.as<uint32_t>();
@@ -2515,12 +2543,12 @@ int tm_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_of
     return tm_match_device_mode(eng, d_bytes, d_off, n, total_bytes, TM_MATCH_ALL, stream, out);
 }
 
-int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
-                         uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out) {
+static int match_device_impl(tm_engine *eng, BatchBufs *set, const uint8_t *d_bytes, const uint32_t *d_off,
+                             uint32_t n, uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out) {
     if (mode > TM_MATCH_AGGRE) return TM_EINVAL;
     if (!eng || !out || !d_off || (n && !d_bytes)) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
-    eng->bb = &eng->bb_dev;
+    eng->bb = set;
     if (mode == TM_MATCH_UNIQUE && eng->dv.n_deep) {
         eng->err = "tm_match_device_mode: UNIQUE with filters deeper than 31 levels is host-only (tm_match_batch)";
         return TM_ESTATE;
@@ -2532,7 +2560,7 @@ int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t 
     // total_bytes = d_off[n] - d_off[0] sizes the spill kernel's scratch
     int rc = ensure_batch(eng, n, total_bytes);
     if (rc) return rc;
-    eng->last_stream = s;
+    eng->bb->last_stream = s;
     eng->bb->last_n = n;
     const uint32_t kmode = mode == TM_MATCH_FIRST ? MODE_FIRST : (mode == TM_MATCH_COUNT ? MODE_COUNT : MODE_ALL);
     if (kmode == MODE_FIRST && eng->bb->keys_cap < n) {
@@ -2554,12 +2582,24 @@ int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t 
     return TM_OK;
 }
 
+int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                         uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out) {
+    return eng ? match_device_impl(eng, &eng->bb_dev, d_bytes, d_off, n, total_bytes, mode, stream, out) : TM_EINVAL;
+}
+// library-internal (batcher.cpp): the same on the aggregator's own buffer set, so its windows
+// never disturb a direct tm_match_device caller's pending result
+__attribute__((visibility("hidden"))) int tmx_batch_match_device(tm_engine *eng, const uint8_t *d_bytes,
+                                                                 const uint32_t *d_off, uint32_t n, uint64_t total_bytes,
+                                                                 uint32_t mode, void *stream, tm_dev_result *out) {
+    return match_device_impl(eng, &eng->bb_batch, d_bytes, d_off, n, total_bytes, mode, stream, out);
+}
+
 int tm_device_sync(tm_engine *eng) {
     if (!eng) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     eng->bb = &eng->bb_dev;
-    hipStream_t s = eng->last_stream ? eng->last_stream : eng->stream;
+    hipStream_t s = eng->bb->last_stream ? eng->bb->last_stream : eng->stream;
     TM_TRY_HIP(eng->h_cursor.ensure(64), TM_ENOMEM, "pinned alloc");
     uint8_t *h = (uint8_t *)eng->h_cursor.p;
     if (eng->bb->p_ctl)
@@ -2578,17 +2618,17 @@ int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint
     return tm_result_ids_device_ex(eng, d_ids, ids_cap, d_off_out, nullptr, stream);
 }
 
-int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out, uint32_t *d_flags,
-                            void *stream) {
+static int result_ids_impl(tm_engine *eng, BatchBufs *set, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
+                           uint32_t *d_flags, void *stream) {
     if (!eng || !d_off_out || (ids_cap && !d_ids)) return TM_EINVAL;
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
-    eng->bb = &eng->bb_dev;
+    eng->bb = set;
     if (!eng->bb->p_ctl || !eng->bb->dev_batch) {
         eng->err = "tm_result_ids_device: no tm_match_device batch since the last (pipelined) tm_match_batch";
         return TM_ESTATE;
     }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
-    hipStream_t s = stream ? (hipStream_t)stream : (eng->last_stream ? eng->last_stream : eng->stream);
+    hipStream_t s = stream ? (hipStream_t)stream : (eng->bb->last_stream ? eng->bb->last_stream : eng->stream);
     const uint32_t n = eng->bb->last_n;
     TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
     const bool red = reduced_mode(eng->bb->last_mode);
@@ -2602,15 +2642,24 @@ int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, u
     return TM_OK;
 }
 
+int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out, uint32_t *d_flags,
+                            void *stream) {
+    return eng ? result_ids_impl(eng, &eng->bb_dev, d_ids, ids_cap, d_off_out, d_flags, stream) : TM_EINVAL;
+}
+__attribute__((visibility("hidden"))) int tmx_result_ids64_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap,
+                                                                  uint32_t *d_off_out, void *stream) {
+    return result_ids_impl(eng, &eng->bb_batch, d_ids, ids_cap, d_off_out, nullptr, stream);
+}
+
 // library-internal (batcher.cpp): tm_result_ids_device with u32 ids, when every id ever
 // added is below 2^32 (TM_ESTATE otherwise)
 __attribute__((visibility("hidden"))) int tmx_result_ids32_device(tm_engine *eng, uint32_t *d_ids, uint64_t ids_cap,
                                                                   uint32_t *d_off_out, void *stream) {
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
-    eng->bb = &eng->bb_dev;
+    eng->bb = &eng->bb_batch;
     if (eng->dv.max_id > 0xFFFFFFFFull || eng->replica || !eng->bb->dev_batch) return TM_ESTATE;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
-    hipStream_t s = stream ? (hipStream_t)stream : (eng->last_stream ? eng->last_stream : eng->stream);
+    hipStream_t s = stream ? (hipStream_t)stream : (eng->bb->last_stream ? eng->bb->last_stream : eng->stream);
     const uint32_t n = eng->bb->last_n;
     TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
     const uint32_t *cnt = (reduced_mode(eng->bb->last_mode) ? eng->bb->d_ucnt : eng->bb->d_outcnt).as<uint32_t>();
@@ -3446,6 +3495,39 @@ int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *of
     eng->err = "tm_match_batch_runs: span output still short after resizing";
     return TM_EDEVICE;
 }
+
+// library-internal (batcher.cpp): a window in runs form, every output in the window's own
+// buffers: spans (uint4 = tm_span) at d_spans, reserved from *d_cursor (zeroed here);
+// per-topic span offset / span count / id count / status.  *d_ctl_out: the launch's counter
+// block (pool demand).  The caller holds a lease (tmx_lease_take) until the spans are used.
+__attribute__((visibility("hidden"))) int tmx_batch_match_runs(tm_engine *eng, const uint8_t *d_bytes,
+                                                               const uint32_t *d_off, uint32_t n, uint64_t total_bytes,
+                                                               void *stream, void *d_spans, uint64_t spans_cap,
+                                                               uint32_t *d_soff, uint32_t *d_scnt, uint32_t *d_kcnt,
+                                                               int32_t *d_status, unsigned long long *d_cursor,
+                                                               const void **d_ctl_out) {
+    if (eng->replica) return TM_ESTATE;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    eng->bb = &eng->bb_batch;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    TM_TRY_HIP(eng->chain_after_last(s), TM_EDEVICE, "stream order");
+    int rc = ensure_batch(eng, n, total_bytes);
+    if (rc) return rc;
+    eng->bb->last_stream = s;
+    eng->bb->last_n = n;
+    eng->bb->dev_batch = false;  // no key-form result in this set
+    TM_TRY_HIP(hipMemsetAsync(d_cursor, 0, 8, s), TM_EDEVICE, "memset");
+    const TopicOut to{d_soff, d_scnt, d_kcnt, d_status};
+    TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s, MODE_RUNS, 0, (uint32_t *)d_spans, spans_cap, d_cursor, &to),
+               TM_EDEVICE, "kernel launch");
+    TM_TRY_HIP(eng->note_use(s), TM_EDEVICE, "event");
+    *d_ctl_out = eng->bb->p_ctl;
+    return TM_OK;
+}
+__attribute__((visibility("hidden"))) void tmx_lease_take(tm_engine *eng) { eng->lease_take_raw(); }
+__attribute__((visibility("hidden"))) void tmx_lease_drop(tm_engine *eng) { eng->lease_drop_raw(); }
+__attribute__((visibility("hidden"))) int tmx_engine_is_replica(const tm_engine *eng) { return eng->replica ? 1 : 0; }
 
 int tm_runs_release(tm_engine *eng) {
     if (!eng) return TM_EINVAL;

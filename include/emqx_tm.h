@@ -205,6 +205,9 @@ typedef struct tm_stats_t {
 
 /* lifecycle --------------------------------------------------------------- */
 uint32_t    tm_abi_version(void);
+/* "src_sha=<sha256 of the library's sources> abi=<n> arch=gfx950": ties a built library to the
+ * sources it was built from (emqx_amd/build.py src_sha). */
+const char *tm_build_info(void);
 int         tm_create(const tm_config *cfg, tm_engine **out);
 void        tm_destroy(tm_engine *eng);
 const char *tm_last_error(const tm_engine *eng);

@@ -18,9 +18,15 @@
  *            TM_BADARG with no ids (a level exactly "+" or "#": emqx_trie_search.erl:374-375),
  *            or a negative TM_E* status when the batch failed as a whole.  COUNT mode
  *            gives the count and no ids.
- *   writes   tm_batcher_apply / tm_batcher_commit serialise with the cutter and wait for the
- *            windows already on the GPU, so an epoch swaps only between windows: every
- *            window sees exactly one committed epoch.
+ *   transport  TM_MATCH_ALL windows on a master engine travel as RUNS (tm_match_batch_runs):
+ *            the walk's spans of the engine's host id arena cross PCIe, not the ids, and each
+ *            publish's reply is read straight from the arena (one span: zero-copy; several:
+ *            gathered by the delivery thread).  A window holds a read lease on the arena from
+ *            its enqueue until its last callback returns; a commit waits for those leases, so
+ *            every window sees exactly one committed epoch.  Other modes, and replicas, ship
+ *            the ids (u32 while every id fits).
+ *   writes   any thread may write the engine directly (tm_apply / tm_commit_epoch are safe
+ *            beside the aggregator); tm_batcher_apply / tm_batcher_commit are the same calls.
  *
  * Erlang binding: a NIF calls tm_batcher_submit with a callback that
  * enif_send()s the id list to the publishing pid, which waits in `receive`; the callback
@@ -49,10 +55,19 @@ typedef struct tm_batcher_config {
     uint32_t delivery_threads; /* threads calling publishers back (0 = 4); they take
                                   ranges of a window from one queue, so a thread that is
                                   slow (or descheduled) never holds the others */
+    uint32_t transport;    /* TM_TRANSPORT_AUTO (runs for TM_MATCH_ALL on a master engine, ids
+                              otherwise), TM_TRANSPORT_IDS, TM_TRANSPORT_RUNS (TM_ESTATE on a
+                              replica) */
 } tm_batcher_config;
+#define TM_TRANSPORT_AUTO 0u
+#define TM_TRANSPORT_IDS  1u
+#define TM_TRANSPORT_RUNS 2u
 
 /* One publish's result; `ids` is valid only during the call. */
 typedef void (*tm_match_cb)(void *ctx, int32_t status, const uint64_t *ids, uint32_t n);
+/* The same as spans (ids = the concatenation of spans[0 .. nspans), nids in all), valid only
+ * during the call: a NIF builds its reply list straight from the engine's id arena. */
+typedef void (*tm_spans_cb)(void *ctx, int32_t status, const tm_span *spans, uint32_t nspans, uint64_t nids);
 
 /* A batch matcher other than an engine (e.g. a filter-sharded index): match topics
  * bytes[off[i] .. off[i+1]) for i < n and fill `out` with memory the backend owns until
@@ -91,6 +106,8 @@ void tm_batcher_destroy(tm_batcher *b);
 
 /* Queue one publish (topic bytes are copied).  TM_ESTATE once destroy has begun. */
 int tm_batcher_submit(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_match_cb cb, void *ctx);
+/* tm_batcher_submit with a span callback (no copy of the ids on the host at all). */
+int tm_batcher_submit_spans(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_spans_cb cb, void *ctx);
 /* Blocking form: waits for the publish's batch.  Copies up to `cap` ids, *n_out = the
  * full count (> cap means truncated), *status = the publish's status. */
 int tm_batcher_match(tm_batcher *b, const uint8_t *topic, uint32_t len, uint64_t *ids, uint32_t cap,

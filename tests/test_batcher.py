@@ -152,8 +152,11 @@ def test_count_mode_and_write_calls_need_an_engine():
 
 # ------------------------------------------------------------------ GPU: over a real engine
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [N.TM_MATCH_ALL, N.TM_MATCH_COUNT, N.TM_MATCH_FIRST])
-def test_gpu_batcher_over_engine_vs_oracle(mode):
+@pytest.mark.parametrize("mode,transport", [(N.TM_MATCH_ALL, N.TM_TRANSPORT_AUTO), (N.TM_MATCH_ALL, N.TM_TRANSPORT_IDS),
+                                            (N.TM_MATCH_COUNT, N.TM_TRANSPORT_AUTO),
+                                            (N.TM_MATCH_FIRST, N.TM_TRANSPORT_AUTO)],
+                         ids=["all-runs", "all-ids", "count", "first"])
+def test_gpu_batcher_over_engine_vs_oracle(mode, transport):
     from emqx_amd import workloads
     import oracle
     w = workloads.generate("A", scale=0.3, n_topics=3000)
@@ -163,7 +166,7 @@ def test_gpu_batcher_over_engine_vs_oracle(mode):
     ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
     eoff, eids, est = ix.match(w.t_bytes, w.t_off)
     topics = w.topics()
-    b = N.Batcher(eng, max_batch=512, max_wait_us=500, mode=mode)
+    b = N.Batcher(eng, max_batch=512, max_wait_us=500, mode=mode, transport=transport)
     bad = []
 
     def worker(k):
@@ -244,3 +247,118 @@ def test_batcher_pipeline_under_thread_sanitizer():
     assert p.returncode == 0, p.stderr[-3000:]
     assert "ThreadSanitizer" not in p.stderr, p.stderr[-3000:]
     assert '"errors": 0' in p.stdout
+
+
+@pytest.mark.gpu
+def test_gpu_batcher_span_callbacks_vs_oracle():
+    """tm_batcher_submit_spans: each publish gets spans of the engine's id arena (runs
+    transport) whose concatenation is its oracle id set; on the ids transport, one span."""
+    from emqx_amd import workloads
+    import oracle
+    w = workloads.generate("C", scale=0.003, n_topics=2000)
+    eng = N.Engine(0)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    eoff, eids, est = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id).match(w.t_bytes, w.t_off)
+    topics = w.topics()
+    lib = N.load()
+    for transport in (N.TM_TRANSPORT_RUNS, N.TM_TRANSPORT_IDS):
+        b = N.Batcher(eng, max_batch=256, max_wait_us=300, transport=transport)
+        got, done = {}, threading.Semaphore(0)
+
+        def cb(ctx, status, spans, ns, nids):
+            sp = C.cast(spans, C.POINTER(N.tm_span)) if ns else None
+            ids = []
+            for j in range(ns):
+                ids += np.ctypeslib.as_array(C.cast(sp[j].ids, C.POINTER(C.c_uint64)), shape=(int(sp[j].n),)).tolist()
+            got[ctx] = (status, sorted(ids), nids)
+            done.release()
+
+        fn = N.tm_spans_cb(cb)
+        for i, t in enumerate(topics):
+            assert lib.tm_batcher_submit_spans(b.h, t, len(t), fn, C.c_void_p(i + 1)) == 0
+        for _ in topics:
+            assert done.acquire(timeout=30)
+        b.close()
+        for i in range(len(topics)):
+            st, ids, nids = got[i + 1]
+            assert st == est[i] and ids == eids[eoff[i]:eoff[i + 1]].tolist() and nids == len(ids), (transport, i)
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_batcher_beside_direct_writers_and_device_callers():
+    """The engine is shared: while 16 threads publish through the batcher (runs transport:
+    windows hold read leases), another thread writes and commits the ENGINE directly, and
+    another runs tm_match_device calls.  Every reply equals the oracle result of one committed
+    epoch, and replies never go back to an older epoch for a publisher."""
+    from emqx_amd import workloads
+    import oracle
+    import torch
+    w = workloads.generate("A", scale=0.3, n_topics=1500)
+    filters = w.filters()
+    eng = N.Engine(0)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    rng = np.random.default_rng(77)
+    live = {(f, int(i)) for f, i in zip(filters, w.f_id.tolist())}
+    sets, opss, nid = [frozenset(live)], [], 10 ** 6
+    for e in range(4):
+        order = sorted(live)
+        ops = []
+        for j in rng.choice(len(order), size=40, replace=False):
+            ops.append((N.TM_OP_DEL,) + order[int(j)])
+            live.discard(order[int(j)])
+        for _ in range(40):
+            f = filters[int(rng.integers(len(filters)))] + (b"/#" if rng.random() < 0.5 else b"")
+            ops.append((N.TM_OP_ADD, f, nid))
+            live.add((f, nid))
+            nid += 1
+        opss.append(ops)
+        sets.append(frozenset(live))
+    exp = []
+    for ks in sets:
+        lf, li = zip(*sorted(ks))
+        o, ids, st = oracle.OrderedIndex.from_filters(list(lf), list(li)).match(w.t_bytes, w.t_off)
+        exp.append([ids[o[i]:o[i + 1]].tolist() for i in range(len(o) - 1)])
+    topics = w.topics()
+    b = N.Batcher(eng, max_batch=256, max_wait_us=300)
+    stop, bad = threading.Event(), []
+
+    def publisher(k):
+        last = 0
+        i = k
+        while not stop.is_set():
+            st, ids = b.match(topics[i % len(topics)])
+            e = [x for x in range(last, len(exp)) if sorted(ids) == exp[x][i % len(topics)]]
+            if not e:
+                bad.append((k, i))
+                return
+            last = e[0]
+            i += 16
+
+    def device_caller():
+        dev = torch.device("cuda:0")
+        s = torch.cuda.Stream(device=dev)
+        tb = torch.from_numpy(w.t_bytes).to(dev)
+        to = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
+        while not stop.is_set():
+            with torch.cuda.stream(s):
+                eng.match_device_mode(tb.data_ptr(), to.data_ptr(), len(topics), int(w.t_off[-1]), N.TM_MATCH_COUNT,
+                                      s.cuda_stream)
+            s.synchronize()
+
+    th = [threading.Thread(target=publisher, args=(k,)) for k in range(16)] + [threading.Thread(target=device_caller)]
+    for t in th:
+        t.start()
+    for ops in opss:
+        time.sleep(0.05)
+        eng.apply(ops)
+        eng.commit()
+    time.sleep(0.1)
+    stop.set()
+    for t in th:
+        t.join(timeout=60)
+    b.close()
+    eng.close()
+    assert not bad, bad[:5]

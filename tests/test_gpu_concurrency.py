@@ -247,6 +247,7 @@ def test_commit_waits_for_an_async_match_on_another_stream():
     filters = w.filters()
     ix0 = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
     eo, eids, est = ix0.match(w.t_bytes, w.t_off)
+    eng.reserve_matches(int(eids.size * 1.2) + 1024)  # the device output arena holds the whole batch
     s = torch.cuda.Stream(device=dev)
     tb = torch.from_numpy(np.asarray(w.t_bytes)).to(dev)
     to = torch.from_numpy(np.asarray(w.t_off).astype(np.int32)).to(dev)

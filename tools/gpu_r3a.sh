@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
-timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_runs.py tests/test_gpu_concurrency.py > gpurun_out/r3a_new.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_concurrency.py tests/test_batcher.py -m gpu > gpurun_out/r3a_new.log 2>&1
 rc=$?
 echo "new tests rc=$rc"
 [ $rc -ne 0 ] && exit $rc
