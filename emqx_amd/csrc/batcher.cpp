@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <chrono>
 #include <condition_variable>
@@ -55,6 +56,7 @@ extern "C" int tmx_batch_match_runs(tm_engine *eng, const uint8_t *d_bytes, cons
                                     uint32_t *d_soff, uint32_t *d_scnt, uint32_t *d_kcnt, int32_t *d_status,
                                     unsigned long long *d_cursor, const void **d_ctl_out);
 extern "C" void tmx_lease_take(tm_engine *eng);
+extern "C" int tmx_batch_reserve_matches(tm_engine *eng, uint64_t keys_cap);
 extern "C" void tmx_lease_drop(tm_engine *eng);
 extern "C" int tmx_engine_is_replica(const tm_engine *eng);
 
@@ -211,6 +213,12 @@ struct tm_batcher {
 
     std::mutex eng_mu;  // the cutter's enqueue vs a re-run from the completion thread
     double spans_per_pub = 4.0;  // runs transport: spans per publish of recent windows (sizes the next)
+    std::atomic<bool> reported{false};  // the first failed window is reported on stderr (once)
+    void report(const char *stage, int rc) {
+        if (rc >= 0 || reported.exchange(true)) return;
+        std::fprintf(stderr, "tm_batcher: a window failed in %s: rc %d (%s)\n", stage, rc,
+                     eng ? tm_last_error(eng) : "custom backend");
+    }
     bool runs_ok = false;        // runs transport in use (TM_MATCH_ALL windows of a master engine)
     hipStream_t s_comp = nullptr, s_copy = nullptr;
     int device = 0;
@@ -505,7 +513,7 @@ struct tm_batcher {
             int rc = tmx_engine_grow_pools(eng, seg, fr);
             if (rc) return rc;
             if (over) {  // output arena too small: grow to the demand, run this window again
-                if ((rc = tm_reserve_matches(eng, total + total / 8 + 1024, 0))) return rc;
+                if ((rc = tmx_batch_reserve_matches(eng, total + total / 8 + 1024))) return rc;
                 if ((rc = enqueue(S))) return rc;
                 BT_HIP(hipEventSynchronize(S.ev));
                 if (S.h_ctl.as<uint64_t>()[0] > S.keys_cap) return TM_EDEVICE;
@@ -585,9 +593,18 @@ struct tm_batcher {
             const uint32_t *so = S.h_soff.as<uint32_t>(), *sc = S.h_scnt.as<uint32_t>(), *kc = S.h_kcnt.as<uint32_t>();
             const int32_t *stv = S.h_status.as<int32_t>();
             uint64_t now = 0;
+            // the id arena is read at random places (a span's start, an inline key's id): start
+            // the loads of a few publishes ahead so the replies do not wait on each miss in turn
+            constexpr uint32_t PF = 6;
+            auto prefetch = [&](uint32_t i) {
+                const uint32_t b = so[i], e = b + std::min<uint32_t>(sc[i], 4);
+                for (uint32_t j = b; j < e; j++) __builtin_prefetch(spans[j].ids);
+            };
+            for (uint32_t i = lo; i < std::min(hi, lo + PF); i++) prefetch(i);
             for (uint32_t i = lo; i < hi; i++) {
                 const Pending &p = S.pubs[i];
                 if (i + 8 < hi) __builtin_prefetch(S.pubs[i + 8].ctx);
+                if (i + PF < hi) prefetch(i + PF);
                 const int32_t st = stv[i];
                 if (st == TM_TOPIC_OK) reply(p, st, spans + so[i], sc[i], kc[i]);
                 else reply(p, st, nullptr, 0, 0);
@@ -781,6 +798,7 @@ struct tm_batcher {
                     }
                     std::lock_guard<std::mutex> g(eng_mu);
                     S.rc = enqueue(S);
+                    report("enqueue", S.rc);
                     if (S.rc == TM_ESTATE && S.mode == TM_MATCH_UNIQUE) S.rc = run_host(S);
                 } else {
                     // custom backend: synchronous; its view lives until its next call, which
@@ -823,7 +841,10 @@ struct tm_batcher {
             S.chunk_lo[0] = 0;
             S.chunk_lo[1] = S.n;
             S.cev_wait = false;
-            if (S.rc == TM_OK && S.n && eng) S.rc = complete(S);
+            if (S.rc == TM_OK && S.n && eng) {
+                S.rc = complete(S);
+                report("completion", S.rc);
+            }
             S.t_done = now_ns();
             if (S.n) {
                 std::lock_guard<std::mutex> g(st_mu);  // counted before the callbacks

@@ -234,6 +234,66 @@ struct ErrSlot {
     const char *c_str() const { return tl_err().c_str(); }
 };
 
+// A few resident threads that split large host copies (staging a pageable batch into pinned
+// memory): thread start-up per copy would cost more than the copy of one sub-batch.
+struct CopyPool {
+    std::mutex m;
+    std::condition_variable cv, done_cv;
+    std::vector<std::thread> th;
+    struct Job {
+        uint8_t *dst;
+        const uint8_t *src;
+        size_t n;
+    };
+    std::vector<Job> q;
+    size_t pending = 0;
+    bool stop = false;
+    void start(unsigned n) {
+        for (unsigned k = 0; k < n; k++)
+            th.emplace_back([this] {
+                std::unique_lock<std::mutex> lk(m);
+                for (;;) {
+                    cv.wait(lk, [&] { return stop || !q.empty(); });
+                    if (stop && q.empty()) return;
+                    Job j = q.back();
+                    q.pop_back();
+                    lk.unlock();
+                    memcpy(j.dst, j.src, j.n);
+                    lk.lock();
+                    if (--pending == 0) done_cv.notify_all();
+                }
+            });
+    }
+    void copy(void *dst, const void *src, size_t n) {
+        const size_t per = 2u << 20;
+        const size_t parts = std::min<size_t>(th.size() + 1, (n + per - 1) / per);
+        if (parts <= 1 || th.empty()) {
+            if (n) memcpy(dst, src, n);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(m);
+            for (size_t k = 1; k < parts; k++) {
+                const size_t a = n * k / parts, b = n * (k + 1) / parts;
+                q.push_back(Job{(uint8_t *)dst + a, (const uint8_t *)src + a, b - a});
+                pending++;
+            }
+        }
+        cv.notify_all();
+        memcpy(dst, src, n / parts);  // this thread takes the first part
+        std::unique_lock<std::mutex> lk(m);
+        done_cv.wait(lk, [&] { return pending == 0; });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto &t : th) t.join();
+    }
+};
+
 // Host results of the calls that return host memory (tm_match_batch, tm_match_filter_batch,
 // tm_intersect_batch, tm_match_batch_runs): one set per calling thread, so a result stays valid
 // until the same thread's next such call however many threads share the engine.
@@ -467,6 +527,9 @@ struct tm_engine {
     PinBuf h_bytes, h_off, h_cursor;
     hipStream_t stream = nullptr;
     hipStream_t s_build = nullptr;  // a full rebuild's standby upload (beside the matches)
+    hipStream_t s_h2d = nullptr;    // tm_match_batch_runs: topic H2D beside the walks
+    hipEvent_t ev_h2d[16] = {};
+    CopyPool copier;
     hipEvent_t ev_chain = nullptr;  // orders a device match after the previous one's stream
     uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0;
     uint64_t commit_us[3] = {0, 0, 0};  // last commit: apply / lists / upload (tm_stats)
@@ -1960,6 +2023,10 @@ void tm_destroy(tm_engine *eng) {
     eng->h_pctl.release();
     if (eng->s_pipe) (void)hipStreamDestroy(eng->s_pipe);
     if (eng->s_build) (void)hipStreamDestroy(eng->s_build);
+    if (eng->s_h2d) (void)hipStreamSynchronize(eng->s_h2d);
+    for (hipEvent_t e : eng->ev_h2d)
+        if (e) (void)hipEventDestroy(e);
+    if (eng->s_h2d) (void)hipStreamDestroy(eng->s_h2d);
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
     delete eng;
 }
@@ -2145,10 +2212,10 @@ struct TopicOut {
 static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                                 hipStream_t s, uint32_t mode = MODE_ALL, uint32_t obase = 0, uint32_t *keys = nullptr,
                                 uint64_t keys_cap = 0, unsigned long long *cursor = nullptr,
-                                const TopicOut *to = nullptr) {
+                                const TopicOut *to = nullptr, uint32_t tpw = 0) {
     MatchArgs a{};
     a.mode = mode;
-    a.tpw = pick_tpw(n, eng->cfg.topics_per_wave);
+    a.tpw = pick_tpw(n, tpw ? tpw : eng->cfg.topics_per_wave);
     a.first_dfs = eng->dv.n_deep ? 1u : 0u;
     a.key_bin = eng->d_key_bin.as<uint32_t>();
     a.bytes = d_bytes;
@@ -3346,8 +3413,13 @@ static void par_memcpy(void *dst, const void *src, size_t n) {
 // stream, one after the other, reserving spans from one cursor (so each sub-batch's spans are
 // one contiguous range); while sub-batch j+1 is staged and walked, sub-batch j's spans and
 // per-topic arrays cross PCIe on the copy stream.
-constexpr uint32_t RUNS_SUB = 131072;
+constexpr uint32_t RUNS_SUB = 262144;
 constexpr uint32_t RUNS_MAXSUB = 16;
+// development knobs (tools/prof_runs.py sweeps): sub-batch size and topics per wave
+static uint32_t env_u32(const char *name, uint32_t dflt) {
+    const char *v = getenv(name);
+    return v && *v ? (uint32_t)strtoul(v, nullptr, 10) : dflt;
+}
 
 int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, tm_runs_result *out) {
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
@@ -3364,11 +3436,24 @@ int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *of
     if (n == 0) return TM_OK;
     const uint32_t base = off[0];
     const uint64_t nbytes = (uint64_t)off[n] - base;
-    const uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(RUNS_MAXSUB, n / RUNS_SUB));
+    const uint32_t runs_sub = std::max<uint32_t>(4096, env_u32("EMQX_TM_RUNS_SUB", RUNS_SUB));
+    // 64 topics per wave from 131,072-topic sub-batches on (262,144: 1.845 vs 1.904 ms per 1 M at config C)
+    const uint32_t runs_tpw_knob = env_u32("EMQX_TM_RUNS_TPW", 0);
+    auto runs_tpw_of = [&](uint32_t sub) -> uint32_t { return runs_tpw_knob ? runs_tpw_knob : (sub >= 131072 ? 64u : 0u); };
+    const uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(RUNS_MAXSUB, n / runs_sub));
     uint32_t b[RUNS_MAXSUB + 1];
     for (uint32_t j = 0; j <= S; j++) b[j] = (uint32_t)((uint64_t)n * j / S);
     int rc = ensure_batch(eng, n, nbytes);
     if (rc) return rc;
+    {  // every sub-batch's grid must fit the per-wave chunk lists (sized for the whole batch above)
+        uint64_t g = 0;
+        for (uint32_t j = 0; j < S; j++)
+        {
+            const uint32_t sub = b[j + 1] - b[j], t = runs_tpw_of(sub);
+            g = std::max<uint64_t>(g, match_grid(sub, pick_tpw(sub, t ? t : eng->cfg.topics_per_wave)));
+        }
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_wave_chunks, g * SEG_MAXCHUNK * 4 + 4), TM_ENOMEM, "alloc");
+    }
     TM_TRY_HIP(eng->grow_buf(eng->bb->d_bytes, nbytes + 16), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->grow_buf(eng->bb->d_off, ((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->grow_buf(eng->bb->d_kcnt, (size_t)n * 4 + 4), TM_ENOMEM, "alloc");
@@ -3384,7 +3469,12 @@ int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *of
         for (hipEvent_t *e : {&eng->ev_pk[0], &eng->ev_pk[1], &eng->ev_pd[0], &eng->ev_pd[1]})
             TM_TRY_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming), TM_EDEVICE, "event");
     }
-    hipStream_t s = eng->stream, c = eng->s_pipe;
+    if (!eng->s_h2d) {
+        TM_TRY_HIP(hipStreamCreateWithFlags(&eng->s_h2d, hipStreamNonBlocking), TM_EDEVICE, "stream");
+        for (hipEvent_t &e : eng->ev_h2d) TM_TRY_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), TM_EDEVICE, "event");
+    }
+    if (!direct && eng->copier.th.empty()) eng->copier.start(3);
+    hipStream_t s = eng->stream, c = eng->s_pipe, hq = eng->s_h2d;
     eng->bb->last_n = 0;
     eng->bb->dev_batch = false;  // the device result is in span form, not keys
     uint32_t *ho = eng->h_off.as<uint32_t>();
@@ -3407,21 +3497,25 @@ int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *of
             for (uint32_t i = lo; i <= hi; i++) ho[i] = off[i] - base;
             const uint8_t *src = bytes + base + blo;
             if (!direct) {
-                par_memcpy(hb + blo, src, bhi - blo);
+                eng->copier.copy(hb + blo, src, bhi - blo);
                 src = hb + blo;
             }
+            // on their own stream: sub-batch j+1's topics cross PCIe while sub-batch j walks
             if (bhi > blo)
-                TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_bytes.as<uint8_t>() + blo, src, bhi - blo, hipMemcpyHostToDevice, s),
+                TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_bytes.as<uint8_t>() + blo, src, bhi - blo, hipMemcpyHostToDevice, hq),
                            TM_EDEVICE, "H2D");
             TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_off.as<uint32_t>() + lo, ho + lo, ((size_t)hi - lo + 1) * 4,
-                                      hipMemcpyHostToDevice, s),
+                                      hipMemcpyHostToDevice, hq),
                        TM_EDEVICE, "H2D");
+            TM_TRY_HIP(hipEventRecord(eng->ev_h2d[j], hq), TM_EDEVICE, "event");
             return TM_OK;
         };
         auto walk = [&](uint32_t j) -> int {
             const uint32_t lo = b[j], hi = b[j + 1], h = j & 1;
+            TM_TRY_HIP(hipStreamWaitEvent(s, eng->ev_h2d[j], 0), TM_EDEVICE, "wait");
             TM_TRY_HIP(enqueue_match(eng, eng->bb->d_bytes.as<uint8_t>(), eng->bb->d_off.as<uint32_t>() + lo, hi - lo, s,
-                                     MODE_RUNS, lo, eng->bb->d_keys.as<uint32_t>(), span_cap, cur),
+                                     MODE_RUNS, lo, eng->bb->d_keys.as<uint32_t>(), span_cap, cur, nullptr,
+                                     runs_tpw_of(hi - lo)),
                        TM_EDEVICE, "kernel launch");
             TM_TRY_HIP(hipMemcpyAsync(rctl + 8 * j, cur, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
             TM_TRY_HIP(hipMemcpyAsync(rctl + 8 * j + 1, eng->bb->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE,
@@ -3463,6 +3557,7 @@ int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *of
             if ((rc = finish(j))) return rc;
             if (over) break;
         }
+        TM_TRY_HIP(hipStreamSynchronize(hq), TM_EDEVICE, "sync");
         TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "sync");
         TM_TRY_HIP(hipStreamSynchronize(c), TM_EDEVICE, "D2H");
         eng->n_slow_last = slow;
@@ -3523,6 +3618,17 @@ __attribute__((visibility("hidden"))) int tmx_batch_match_runs(tm_engine *eng, c
                TM_EDEVICE, "kernel launch");
     TM_TRY_HIP(eng->note_use(s), TM_EDEVICE, "event");
     *d_ctl_out = eng->bb->p_ctl;
+    return TM_OK;
+}
+// library-internal (batcher.cpp): tm_reserve_matches for the aggregator's buffer set
+__attribute__((visibility("hidden"))) int tmx_batch_reserve_matches(tm_engine *eng, uint64_t keys_cap) {
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    eng->bb = &eng->bb_batch;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    if (keys_cap > eng->bb->keys_cap) {
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, keys_cap * 4), TM_ENOMEM, "alloc keys");
+        eng->bb->keys_cap = keys_cap;
+    }
     return TM_OK;
 }
 __attribute__((visibility("hidden"))) void tmx_lease_take(tm_engine *eng) { eng->lease_take_raw(); }
