@@ -52,6 +52,14 @@ class EngineReplicaAdapter:
         buf, full = self.eng.patch_export()
         return buf, full
 
+    def epoch(self) -> int:
+        return int(self.eng.stats()["epoch"])
+
+    @staticmethod
+    def patch_epoch_from(buf) -> int:
+        """The epoch a patch applies on (PatchHdr.epoch_from, engine.cpp)."""
+        return int(np.frombuffer(bytes(buf[8:16]), dtype=np.uint64)[0]) if len(buf) >= 16 else -1
+
     # replica side
     def load_image(self, t):
         import torch
@@ -71,6 +79,7 @@ class ReplicatedIndex:
     def __init__(self, adapter, rank: int, world: int, group=None):
         self.ad, self.rank, self.world, self.group = adapter, rank, world, group
         self.bytes_sent = 0  # image + patch bytes broadcast by the master (diagnostics)
+        self.shipped = None  # master: the epoch every replica holds (the last one shipped)
 
     @property
     def is_master(self) -> bool:
@@ -118,22 +127,37 @@ class ReplicatedIndex:
 
     def start(self):
         """Collective: every replica receives the master's current image."""
+        if self.is_master:
+            self.shipped = self.ad.epoch()
         self._send_image()
 
+    SYNC_PATCH, SYNC_IMAGE, SYNC_NONE = 0, 1, 2
+
     def sync(self):
-        """Collective, after the master's commit: ship that epoch's patch (or, after a full
-        rebuild, the whole image) to every replica."""
+        """Collective: bring every replica to the master's committed epoch.  One commit since
+        the last sync ships that commit's patch; a full rebuild, or more than one commit
+        (a patch only applies on the epoch it was made from), ships the whole image; no
+        commit ships nothing.  Returns the SYNC_* kind that was shipped."""
         import torch
         dev = self._dev()
         if self.is_master:
-            buf, full = self.ad.patch()
-            hdr = torch.tensor([len(buf), 1 if full else 0], dtype=torch.int64, device=dev)
+            cur = self.ad.epoch()
+            buf, kind = None, self.SYNC_NONE
+            if cur != self.shipped:
+                buf, full = self.ad.patch()
+                kind = (self.SYNC_IMAGE if full or self.ad.patch_epoch_from(buf) != self.shipped
+                        else self.SYNC_PATCH)
+            hdr = torch.tensor([len(buf) if kind == self.SYNC_PATCH else 0, kind], dtype=torch.int64, device=dev)
+            self.shipped = cur
         else:
             hdr = torch.zeros(2, dtype=torch.int64, device=dev)
         self._bcast(hdr)
-        n, full = int(hdr[0].item()), bool(hdr[1].item())
-        if full:
-            return self._send_image()
+        n, kind = int(hdr[0].item()), int(hdr[1].item())
+        if kind == self.SYNC_NONE:
+            return kind
+        if kind == self.SYNC_IMAGE:
+            self._send_image()
+            return kind
         if self.is_master:
             t = torch.from_numpy(buf).to(dev)
         else:
@@ -143,3 +167,4 @@ class ReplicatedIndex:
             self.bytes_sent += n * (self.world - 1)
         else:
             self.ad.apply_patch(t.cpu().numpy())
+        return kind

@@ -125,3 +125,43 @@ class OrderedIndex:
         self.lib.ots_match(self.h, tb.ctypes.data, to.ctypes.data, n, algo, mode, threads, 1, cnt.ctypes.data,
                            C.byref(cs))
         return cnt, cs.value
+
+
+INTERSECT_FALSE, INTERSECT_BADHASH = -1, -2
+
+
+def intersect_packed(a_buf, a_off, b_buf, b_off, threads=1):
+    """emqx_topic:intersection/2 over packed pairs (C++ restatement, trie_search.cpp
+    ots_intersect): -> (lens i32[n]: result length, INTERSECT_FALSE or INTERSECT_BADHASH;
+    starts u64[n]; out u8 buffer), pair i's result at out[starts[i]: starts[i] + lens[i]]."""
+    lib = load()
+    lib.ots_intersect.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p,
+                                  C.c_void_p]
+    ab = np.ascontiguousarray(a_buf, dtype=np.uint8)
+    ao = np.ascontiguousarray(a_off, dtype=np.uint32)
+    bb = np.ascontiguousarray(b_buf, dtype=np.uint8)
+    bo = np.ascontiguousarray(b_off, dtype=np.uint32)
+    n = len(ao) - 1
+    out = np.zeros(int(ao[-1]) + int(bo[-1]) + 16, dtype=np.uint8)
+    lens = np.zeros(max(n, 1), dtype=np.int32)
+    lib.ots_intersect(ab.ctypes.data, ao.ctypes.data, bb.ctypes.data, bo.ctypes.data, n, threads, out.ctypes.data,
+                      lens.ctypes.data)
+    return lens[:n], ao[:n].astype(np.uint64) + bo[:n].astype(np.uint64), out
+
+
+def intersect(pairs, threads=1):
+    """intersection/2 per (a, b) bytes pair: bytes, False, or the string 'badhash' where
+    join/1 raises error('topic_invalid_#')."""
+    def pack(ts):
+        off = np.zeros(len(ts) + 1, dtype=np.uint32)
+        if ts:
+            off[1:] = np.cumsum([len(t) for t in ts])
+        return np.frombuffer(b"".join(ts) + b"\0" * 16, dtype=np.uint8), off
+    ab, ao = pack([p[0] for p in pairs])
+    bb, bo = pack([p[1] for p in pairs])
+    lens, starts, out = intersect_packed(ab, ao, bb, bo, threads)
+    raw = out.tobytes()
+    res = []
+    for L, s in zip(lens.tolist(), starts.tolist()):
+        res.append(False if L == INTERSECT_FALSE else "badhash" if L == INTERSECT_BADHASH else raw[s:s + L])
+    return res

@@ -475,3 +475,111 @@ const uint32_t *ots_res_src(void *r) { return ((Results *)r)->flat_src.data(); }
 void ots_res_free(void *r) { delete (Results *)r; }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// emqx_topic:intersection/2 (apps/emqx/src/emqx_topic.erl:111-151) + join/1 (:310-322),
+// restated over byte words ('+' / '#' are the wildcard levels, every other level -- the
+// empty one included -- a literal compared bytewise).  The C++ CPU baseline of the
+// intersection leg (bench.py) and its parity checker over whole batches.
+// Per pair: out_len[i] = result length, -1 = false, -2 = error('topic_invalid_#') from
+// join/1; the result bytes at out + a_off[i] + b_off[i] (room: both inputs' lengths + 1).
+namespace {
+struct W {
+    const uint8_t *p;
+    uint32_t n;
+    bool plus() const { return n == 1 && p[0] == '+'; }
+    bool hash() const { return n == 1 && p[0] == '#'; }
+    bool wild() const { return plus() || hash(); }
+    bool eq(const W &o) const { return n == o.n && std::memcmp(p, o.p, n) == 0; }
+};
+void words_of(const uint8_t *p, uint32_t n, std::vector<W> &out) {
+    out.clear();
+    uint32_t st = 0;
+    for (uint32_t i = 0; i <= n; i++)
+        if (i == n || p[i] == '/') {
+            out.push_back(W{p + st, i - st});
+            st = i + 1;
+        }
+}
+const W PLUS_W{(const uint8_t *)"+", 1};
+// intersect/2 (:128-151): false, or the intersection's words
+bool intersect_words(const std::vector<W> &a, const std::vector<W> &b, std::vector<W> &r) {
+    r.clear();
+    size_t i = 0, j = 0;
+    for (;;) {
+        const size_t ra = a.size() - i, rb = b.size() - j;
+        if (rb == 1 && b[j].hash()) {  // intersect(Words, ['#']) -> Words
+            r.insert(r.end(), a.begin() + i, a.end());
+            return true;
+        }
+        if (ra == 1 && a[i].hash()) {  // intersect(['#'], Words) -> Words
+            r.insert(r.end(), b.begin() + j, b.end());
+            return true;
+        }
+        if (ra == 1 && rb == 1 && b[j].plus()) {  // intersect([W], ['+']) -> [W]
+            r.push_back(a[i]);
+            return true;
+        }
+        if (ra == 1 && rb == 1 && a[i].plus()) {  // intersect(['+'], [W]) -> [W]
+            r.push_back(b[j]);
+            return true;
+        }
+        if (ra && rb) {
+            const W &x = a[i], &y = b[j];
+            if (x.wild() && y.wild()) r.push_back(x.eq(y) ? x : PLUS_W);
+            else if (x.eq(y)) r.push_back(x);
+            else if (x.wild()) r.push_back(y);
+            else if (y.wild()) r.push_back(x);
+            else return false;
+            i++;
+            j++;
+            continue;
+        }
+        return ra == 0 && rb == 0;  // intersect([], []) -> []; anything else -> false
+    }
+}
+bool dollar_first(const std::vector<W> &w) { return w[0].n && w[0].p[0] == '$' && !w[0].wild(); }
+}  // namespace
+
+extern "C" void ots_intersect(const uint8_t *a_buf, const uint32_t *a_off, const uint8_t *b_buf, const uint32_t *b_off,
+                              uint64_t n, int nthreads, uint8_t *out, int32_t *out_len) {
+    std::atomic<uint64_t> next{0};
+    if (nthreads < 1) nthreads = 1;
+    auto worker = [&]() {
+        std::vector<W> a, b, r;
+        for (;;) {
+            const uint64_t lo = next.fetch_add(4096);
+            if (lo >= n) break;
+            const uint64_t hi = std::min<uint64_t>(lo + 4096, n);
+            for (uint64_t i = lo; i < hi; i++) {
+                words_of(a_buf + a_off[i], a_off[i + 1] - a_off[i], a);
+                words_of(b_buf + b_off[i], b_off[i + 1] - b_off[i], b);
+                // '$'-topics never intersect a filter whose first level is a wildcard (:113-118)
+                if ((dollar_first(a) && b[0].wild()) || (dollar_first(b) && a[0].wild()) ||
+                    !intersect_words(a, b, r)) {
+                    out_len[i] = -1;
+                    continue;
+                }
+                bool bad = false;  // join/1: '#' anywhere but last
+                for (size_t k = 0; k + 1 < r.size(); k++)
+                    if (r[k].hash()) bad = true;
+                if (bad) {
+                    out_len[i] = -2;
+                    continue;
+                }
+                uint8_t *o = out + (uint64_t)a_off[i] + b_off[i];
+                uint32_t len = 0;
+                for (size_t k = 0; k < r.size(); k++) {
+                    if (k) o[len++] = '/';
+                    std::memcpy(o + len, r[k].p, r[k].n);
+                    len += r[k].n;
+                }
+                out_len[i] = (int32_t)len;
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int k = 1; k < nthreads; k++) th.emplace_back(worker);
+    worker();
+    for (auto &t : th) t.join();
+}

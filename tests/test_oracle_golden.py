@@ -223,3 +223,31 @@ def test_property_trie_restatement_vs_python_match(topics, pats, sys_first):
     for i, t in enumerate(topics):
         exp = [k for k, f in enumerate(filters) if et.match(t, f)]
         assert ids[o[i]:o[i + 1]].tolist() == exp, (t, filters)
+
+
+def test_intersection_cpp_restatement_vs_python_and_kats(golden):
+    """oracle/trie_search.cpp ots_intersect (the intersection leg's C++ CPU baseline and
+    whole-batch checker) against the reference's 17 KATs and the Python restatement."""
+    import random
+
+    import oracle
+    g = golden("kat_topic.json")
+    kats = [(a.encode(), b.encode()) for a, b, _ in g["intersection"]]
+    got = oracle.intersect(kats + [(b, a) for a, b in kats])
+    for (a, b, exp), r, r2 in zip(g["intersection"], got, got[len(kats):]):
+        assert r == (exp.encode() if exp else False), (a, b, r)
+        assert r2 == r
+    rng = random.Random(7)
+    vocab = [b"a", b"b", b"", b"+", b"#", b"$SYS", b"$x", b"c/d"]
+    pairs = [(b"/".join(rng.choice(vocab) for _ in range(rng.randint(1, 5))),
+              b"/".join(rng.choice(vocab) for _ in range(rng.randint(1, 5)))) for _ in range(20000)]
+    pairs += [(b"", b""), (b"#", b""), (b"+", b""), (b"a/#", b"#/b"), (b"#/a", b"#/a")]
+
+    def py(a, b):
+        try:
+            return et.intersection(a, b)
+        except et.TopicError:
+            return "badhash"
+    got = oracle.intersect(pairs, threads=4)
+    for (a, b), r in zip(pairs, got):
+        assert r == py(a, b), (a, b, r)

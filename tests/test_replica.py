@@ -41,6 +41,7 @@ class FakeAdapter:
         self.full_next = False
         self.master = master
         self.images, self.patches = 0, 0
+        self.ep = 1
 
     def tensor_device(self):
         import torch
@@ -51,6 +52,14 @@ class FakeAdapter:
             (self.keys.add if op == "add" else self.keys.discard)((f, i))
         self.pending = ops
         self.full_next = full
+        self.ep += 1
+
+    def epoch(self):
+        return self.ep
+
+    @staticmethod
+    def patch_epoch_from(buf):
+        return json.loads(bytes(buf))["from"]
 
     def export_image(self):
         import torch
@@ -58,14 +67,15 @@ class FakeAdapter:
         return torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy())
 
     def patch(self):
-        return np.frombuffer(json.dumps(self.pending).encode(), dtype=np.uint8).copy(), self.full_next
+        b = json.dumps({"from": self.ep - 1, "ops": self.pending}).encode()
+        return np.frombuffer(b, dtype=np.uint8).copy(), self.full_next
 
     def load_image(self, t):
         self.keys = {tuple(k) for k in json.loads(bytes(t.numpy()))}
         self.images += 1
 
     def apply_patch(self, buf):
-        for op, f, i in json.loads(bytes(buf)):
+        for op, f, i in json.loads(bytes(buf))["ops"]:
             (self.keys.add if op == "add" else self.keys.discard)((f, i))
         self.patches += 1
 
@@ -104,6 +114,14 @@ def _worker(rank, world, port, q, chunk=0):
             ad.commit([("add", "a/#", 10**6 + 2)], full=True)
         rix.sync()
         out.append(ad.match(topics))
+        # two commits between syncs: the second's patch does not apply on the replicas'
+        # epoch, so the image goes instead; then a sync with no commit ships nothing
+        if rank == 0:
+            ad.commit([("add", "b/+", 10**6 + 3)])
+            ad.commit([("del", "#", 10**6)])
+        kinds = [rix.sync(), rix.sync()]
+        out.append(ad.match(topics))
+        out.append(kinds)
         q.put((rank, out, ad.images, ad.patches, rix.bytes_sent, None))
     except Exception:  # pragma: no cover - reported to the parent
         import traceback
@@ -130,7 +148,8 @@ def test_replicated_gloo_world2_protocol(chunk):
         assert r[5] is None, r[5]
     (_, m_out, _, _, sent, _), (_, r_out, images, patches, _, _) = res
     assert r_out == m_out  # the replica answers exactly as the master, every epoch
-    assert images == 2 and patches == 1  # start + full rebuild; one delta epoch
+    assert images == 3 and patches == 1  # start + full rebuild + two-commit sync; one delta epoch
+    assert r_out[-1] == [ReplicatedIndex.SYNC_IMAGE, ReplicatedIndex.SYNC_NONE]
     assert sent > 0
     assert any(len(x) for x in m_out[1]) and m_out[1] != m_out[0]
 
