@@ -136,7 +136,7 @@ def batcher_load(eng, tb, to32, seconds):
                                     for k in ("cut", "enqueue", "gpu_wait", "copy", "deliver")}})
     return {"api": f"tm_batcher_submit (max_batch 65536, max_wait 200 us, {dt} delivery threads)", "runs": runs,
             "note": "closed loop: each publisher resubmits from its result callback, which reads every id once; "
-                    "four windows in flight (GPU walk / PCIe / callbacks); runs transport: spans cross PCIe and "
+                    "six windows in flight (GPU walk / PCIe / callbacks); runs transport: spans cross PCIe and "
                     "replies are read from the host id arena (one span: zero-copy; several: gathered); "
                     "stage_busy: share of wall time each stage worked (copy and deliver: per delivery thread)"}
 
@@ -316,6 +316,9 @@ def main():
     ap.add_argument("--mode", choices=("replicated", "sharded"), default="replicated",
                     help="replicated trie, publishes data-parallel (default); or filters hash-sharded over "
                          "ranks with an RCCL all-gather merge (config D; DESIGN.md §6)")
+    ap.add_argument("--exchange", choices=("padded", "exact", "local"), default="padded",
+                    help="sharded mode: padded all-gather (no host sync), exact all-gather-v by grouped "
+                         "send/recv, or local (each rank D2H's its own shard lists, no collective)")
     ap.add_argument("--shard-of", type=int, default=0, metavar="G",
                     help="sharded mode on one process: hold shard 0 of a G-way split (per-GPU share of G GPUs)")
     ap.add_argument("--churn", type=int, default=0, metavar="EPOCHS",
@@ -438,6 +441,7 @@ def main():
     eng.debug_stats(True, read=False)
     step()
     torch.cuda.synchronize()
+    by_depth = eng.depth_stats()  # per walk depth: probes, wave cycles, frontier, round trips
     walk = dict(zip(N.Engine.STAT_NAMES, [int(x) for x in eng.debug_stats(False)]))
     alg_bytes = algorithmic_bytes(walk, topic_bytes, n)
     eng.debug_stats(False, read=False)
@@ -594,6 +598,7 @@ def main():
                                    f"is tallied at half), L2 hit {prof[1]['l2_hit_rate']:.3f}")
                 if prof else "no PMC profile of this kernel source under profiles/",
                 "walk": walk,
+                "walk_by_depth": by_depth,
             },
             "gather": gather_roof(walk, kernel_ms),
             "latency_vs_batch": lat_sweep,
@@ -653,39 +658,63 @@ def run_sharded(args):
     eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)  # already this shard's keys only
     eng.commit()
     log(f"[rank {rank}] shard {rank}/{nshards}: {w.n_keys} keys, build {time.time() - t0:.1f}s")
-    six = S.ShardedIndex(S.EngineShard(eng), rank, world)
+    six = S.ShardedIndex(S.EngineShard(eng), rank, world, exchange=args.exchange)
     n = w.n_topics
     d_bytes = torch.from_numpy(w.t_bytes).to(dev)
     d_off = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
     tb = int(w.t_off[-1])
 
-    def step():
-        return six.match_device(eng, d_bytes.data_ptr(), d_off.data_ptr(), n, tb)
+    def timed(exchange, steps, warmup):
+        """(elapsed s over `steps` steps, per-step event ms, last result) of one exchange"""
+        for _ in range(max(1, warmup)):
+            out = six.match_device(eng, d_bytes.data_ptr(), d_off.data_ptr(), n, tb, exchange=exchange)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        t_start = time.perf_counter()
+        for k in range(steps):  # padded: no host sync inside a step (DESIGN.md §6)
+            evs[k][0].record()
+            out = six.match_device(eng, d_bytes.data_ptr(), d_off.data_ptr(), n, tb, exchange=exchange)
+            evs[k][1].record()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t_start
+        if world > 1:
+            dist.barrier()
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        if int(out[2].max().item()):
+            raise RuntimeError("sharded step overflowed the sizes prepare_device fixed")
+        return el, [a.elapsed_time(b) for a, b in evs], out
 
     six.prepare_device(eng, d_bytes.data_ptr(), d_off.data_ptr(), n, tb)  # sizes: untimed, collective
-    for _ in range(max(1, args.warmup)):
-        off, ids, flags = step()
-    torch.cuda.synchronize()
+    elapsed, lat, out = timed(args.exchange, args.steps, args.warmup)
+    matches = int(out[0][-1].item())
+    local_total = int(six.shard.eng.stats()["n_keys"])  # keys on this rank
+    # the exchange variants side by side (SURVEY.md §8(e): "report both"), shorter runs
+    G = nshards
+    hdr_b = (n + 2) * 4
+    variants = {}
+    for ex in S.EXCHANGES:
+        el, lt, o = timed(ex, max(5, args.steps // 2), 2)
+        m_own = int(o[0][-1].item()) if ex == "local" else None
+        variants[ex] = {"ms_per_step": round(el / max(5, args.steps // 2) * 1e3, 4),
+                        "publishes_per_s": round(n * max(5, args.steps // 2) / el, 1),
+                        "p99_batch_ms": round(float(np.percentile(lt, 99)), 4)}
+        if ex == "local":
+            variants[ex]["own_matches"] = m_own
+            variants[ex]["d2h_bytes"] = hdr_b + m_own * six.id_bytes
+    own = variants["local"]["own_matches"]
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t_start = time.perf_counter()
-    for k in range(args.steps):  # no host sync inside a step
-        evs[k][0].record()
-        off, ids, flags = step()
-        evs[k][1].record()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    lat = [a.elapsed_time(b) for a, b in evs]
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    if int(flags.item()):
-        raise RuntimeError("sharded step overflowed the sizes prepare_device fixed")
-    matches = int(off[-1].item())
+        wire = {"measured_last_step": six.wire_bytes}
+    else:  # one rank holding 1/G: what a G-rank exchange would move into each rank
+        wire = {"model": f"{G}-rank exchange from this shard's sizes (every shard assumed to match as many)",
+                "padded": (G - 1) * (six.stride * six.id_bytes + hdr_b),
+                "exact": (G - 1) * (own * six.id_bytes + hdr_b), "local": 0,
+                "bound_(G-1)/G*sumM*4": int((G - 1) / G * (G * own) * 4),
+                "exact_ids_only": (G - 1) * own * six.id_bytes}
     if rank == 0:
         print(json.dumps({
             "metric": METRIC, "value": round(n * args.steps / elapsed, 1), "unit": "publishes/s",
@@ -694,11 +723,13 @@ def run_sharded(args):
             "vs_baseline": None, "dtype": "u32",
             "data": f"synthetic (seeded generator, emqx_amd/workloads.py config {args.config}, scale {args.scale})",
             "config": {"workload": f"{args.config} filter-sharded {nshards} ways over {world} rank(s): "
-                                   f"{w.n_keys} keys on rank 0",
+                                   f"{local_total} keys on rank 0",
                        "publishes_per_step": n, "matches_per_step": matches,
-                       "parallelism": f"filter hash-shard x{world}, RCCL all-gather merge"},
+                       "parallelism": f"filter hash-shard x{world}, exchange {args.exchange}"},
             "p50_batch_ms": round(float(np.percentile(lat, 50)), 4),
             "p99_batch_ms": round(float(np.percentile(lat, 99)), 4),
+            "id_bytes_on_wire": six.id_bytes, "stride_ids": six.stride,
+            "wire_bytes_per_rank": wire, "exchanges": variants,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -871,6 +902,7 @@ def config_leg(cfg, batch, steps=20):
     eng.debug_stats(True, read=False)
     step()
     torch.cuda.synchronize()
+    by_depth = eng.depth_stats()  # per walk depth: probes, wave cycles, frontier, round trips
     walk = dict(zip(N.Engine.STAT_NAMES, [int(x) for x in eng.debug_stats(False)]))
     eng.debug_stats(False, read=False)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]

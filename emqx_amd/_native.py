@@ -62,6 +62,7 @@ EXPORTS = (
     "tm_match_filter_batch", "tm_intersect_batch", "tm_result_ids_device_ex", "tm_image_size", "tm_image_export",
     "tm_replica_create", "tm_replica_load", "tm_patch_size", "tm_patch_export", "tm_replica_apply_patch",
     "tm_discard_staged", "tm_result_release", "tm_match_batch_runs", "tm_runs_release", "tm_build_info",
+    "tm_match_ids_device", "tm_merge_shard_ids_device", "tm_debug_depth_stats",
 )
 # every symbol include/emqx_tm_batcher.h declares
 BATCHER_EXPORTS = (
@@ -200,8 +201,13 @@ def load() -> C.CDLL:
     lib.tm_stats.argtypes = [C.c_void_p, P(tm_stats_t)]
     lib.tm_debug_timing.argtypes = [C.c_void_p, C.c_int, P(C.c_float)]
     lib.tm_debug_stats.argtypes = [C.c_void_p, C.c_int, P(C.c_uint64)]
+    lib.tm_debug_depth_stats.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.tm_result_ids_device.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     lib.tm_result_ids_device_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.tm_match_ids_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
+                                        C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.tm_merge_shard_ids_device.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p,
+                                              C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     lib.tm_image_size.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.tm_image_export.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     lib.tm_replica_create.argtypes = [P(tm_config), C.c_void_p, C.c_uint64, C.c_void_p, P(C.c_void_p)]
@@ -582,6 +588,15 @@ class Engine:
                   "cyc_prescan", "cyc_walk", "cyc_copyout", "hot_cyc_prescan", "hot_cyc_walk", "hot_cyc_copyout",
                   "hot_waves")
 
+    def depth_stats(self):
+        """Per walk depth (tm_debug_depth_stats): list of dicts {depth, edge_probes, cycles,
+        frontier, round_trips} for the depths the walk reached (read before debug_stats)."""
+        out = (C.c_uint64 * 64)()
+        self._check(self.lib.tm_debug_depth_stats(self.h, out))
+        v = list(out)
+        return [{"depth": d, "edge_probes": v[d], "cycles": v[16 + d], "frontier": v[32 + d], "round_trips": v[48 + d]}
+                for d in range(16) if v[32 + d]]
+
     def debug_stats(self, enable: bool, read: bool = True):
         out = (C.c_uint64 * 18)()
         self._check(self.lib.tm_debug_stats(self.h, 1 if enable else 0, out if read else None))
@@ -603,6 +618,25 @@ class Engine:
         """result_ids_device + a device u32 of TM_RES_* overflow flags (no host sync)."""
         self._check(self.lib.tm_result_ids_device_ex(self.h, C.c_void_p(d_ids), ids_cap, C.c_void_p(d_off),
                                                      C.c_void_p(d_flags), C.c_void_p(stream) if stream else None))
+
+    def match_ids_device(self, d_bytes: int, d_off: int, n: int, total_bytes: int, id_bytes: int, d_ids: int,
+                         ids_cap: int, d_off_out: int, d_flags: int = 0, stream: int = 0):
+        """tm_match_ids_device: the walk writes route ids (id_bytes 4 or 8) and they are compacted
+        topic-major into d_ids, offsets (n+1) into d_off_out, TM_RES_* flags into d_flags."""
+        self._check(self.lib.tm_match_ids_device(self.h, C.c_void_p(d_bytes), C.c_void_p(d_off), n, total_bytes,
+                                                 id_bytes, C.c_void_p(d_ids), ids_cap, C.c_void_p(d_off_out),
+                                                 C.c_void_p(d_flags) if d_flags else None,
+                                                 C.c_void_p(stream) if stream else None))
+
+    def merge_shard_ids_device(self, G: int, n: int, d_roff: int, roff_stride: int, d_ids: int, id_bytes: int,
+                               bases, d_out_off: int, d_out_ids: int, out_cap: int, stream: int = 0):
+        """tm_merge_shard_ids_device: rank r's offsets row at d_roff + r*roff_stride (u32), its ids
+        at d_ids + bases[r] elements of id_bytes; merged u64 ids + n+1 offsets out."""
+        b = (C.c_uint64 * G)(*[int(x) for x in bases])
+        self._check(self.lib.tm_merge_shard_ids_device(self.h, G, n, C.c_void_p(d_roff), roff_stride,
+                                                       C.c_void_p(d_ids), id_bytes, b, C.c_void_p(d_out_off),
+                                                       C.c_void_p(d_out_ids), out_cap,
+                                                       C.c_void_p(stream) if stream else None))
 
     def merge_shards_device(self, G: int, n: int, d_counts: int, d_ids: int, stride: int, d_out_off: int,
                             d_out_ids: int, out_cap: int, stream: int = 0):

@@ -85,7 +85,7 @@ def build(force: bool = False, verbose: bool = True):
     lsrc = [os.path.join(os.path.dirname(HERE), "tools", "loadgen.cpp"),
             os.path.join(os.path.dirname(HERE), "include", "emqx_tm_batcher.h")]
     if force or not _newer(lg, lsrc):
-        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", lsrc[0], "-o", lg, tm, "-Wl,-rpath,$ORIGIN/../emqx_amd"]
+        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", lsrc[0], "-o", lg, tm, "-Wl,-rpath,$ORIGIN/../emqx_amd"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)

@@ -19,7 +19,7 @@
 //      calls that range back.  No thread waits for another: a window's slot is freed by
 //      whichever thread finishes its last range, and the next window's ranges are taken
 //      while stragglers of this one still run.
-// Four slots rotate: window k+3 is cut and walks on the GPU while earlier windows' ids cross
+// Six slots rotate: the newest window is cut and walks on the GPU while earlier windows' ids cross
 // PCIe and window k's publishers are called back.
 // Submissions go to one of SHARDS queue shards (by submitting thread), so publishers that
 // resubmit from their callbacks do not all contend on one lock.
@@ -51,6 +51,9 @@ extern "C" int tmx_batch_match_device(tm_engine *eng, const uint8_t *d_bytes, co
                                       uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out);
 extern "C" int tmx_result_ids64_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
                                        void *stream);
+extern "C" int tmx_batch_match_ids(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                                   uint64_t total_bytes, uint32_t id_bytes, void *d_ids, uint64_t ids_cap,
+                                   uint32_t *d_off_out, void *stream, tm_dev_result *out);
 extern "C" int tmx_batch_match_runs(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                                     uint64_t total_bytes, void *stream, void *d_spans, uint64_t spans_cap,
                                     uint32_t *d_soff, uint32_t *d_scnt, uint32_t *d_kcnt, int32_t *d_status,
@@ -62,10 +65,32 @@ extern "C" int tmx_engine_is_replica(const tm_engine *eng);
 
 namespace {
 
+// The aggregator stamps every publish (submit -> callback latency), so its clock is on the
+// per-publish path: the TSC (invariant on the hosts this runs on; Linux uses it as the
+// clocksource there) read in ~7 ns, against ~18 ns for steady_clock's vDSO call, scaled to
+// nanoseconds by a calibration against steady_clock the first time it is used.
+struct TscClock {
+    uint64_t tsc0 = 0;
+    double ns_per_tick = 1.0;
+    TscClock() {
+        using clk = std::chrono::steady_clock;
+        const auto c0 = clk::now();
+        tsc0 = __builtin_ia32_rdtsc();
+        std::this_thread::sleep_for(std::chrono::milliseconds(3));
+        const auto c1 = clk::now();
+        const uint64_t t1 = __builtin_ia32_rdtsc();
+        const double ns = (double)std::chrono::duration_cast<std::chrono::nanoseconds>(c1 - c0).count();
+        if (t1 > tsc0 && ns > 0) ns_per_tick = ns / (double)(t1 - tsc0);
+    }
+};
+const TscClock &tsc_clock() {
+    static const TscClock c;
+    return c;
+}
 uint64_t now_ns() {
-    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-               std::chrono::steady_clock::now().time_since_epoch())
-        .count();
+    const TscClock &c = tsc_clock();
+    const uint64_t t = __builtin_ia32_rdtsc();
+    return t > c.tsc0 ? (uint64_t)((double)(t - c.tsc0) * c.ns_per_tick) : 0;
 }
 
 // grow-only device / pinned buffers
@@ -137,12 +162,15 @@ constexpr size_t LAT_RING = 65536;
 constexpr size_t QUEUE_BYTES_MAX = 1ull << 31;
 constexpr uint32_t SHARDS = 16;
 #ifndef TM_NSLOT
-#define TM_NSLOT 4
+#define TM_NSLOT 6
 #endif
-// windows in flight: k+3 cut / on the GPU, k+2 and k+1 on PCIe or waiting, k being delivered.
-// A fourth slot lets the next window be cut while delivery still holds one (65,536 closed-loop
-// publishers: 39 -> 44 M publishes/s)
+// windows in flight: the newest cut / on the GPU, older ones on PCIe or waiting, the oldest being
+// delivered.  Round 2: a fourth slot let the next window be cut while delivery still held one
+// (65,536 closed-loop publishers: 39 -> 44 M publishes/s); round 3, span callbacks: 4 slots
+// 42.7, 6 slots 48.7, 8 slots 40.7 M publishes/s (smaller windows: the cutter's share grows),
+// profiles/r03_batcher_sweep.jsonl
 constexpr uint32_t NSLOT = TM_NSLOT;
+constexpr uint32_t NSLOT_MAX = 8;  // EMQX_TM_NSLOT (development knob) may raise it up to this
 constexpr uint32_t CTL_BYTES = 32;
 // the threads that wait on these sleep in the driver instead of spinning a CPU of the quota
 constexpr unsigned EV_FLAGS = hipEventDisableTiming | hipEventBlockingSync;  // the engine's per-launch counter block {total, slow, seg, fr}
@@ -223,7 +251,8 @@ struct tm_batcher {
     hipStream_t s_comp = nullptr, s_copy = nullptr;
     int device = 0;
 
-    Slot slot[NSLOT];
+    Slot slot[NSLOT_MAX];
+    uint32_t nslot = NSLOT;
     std::mutex slot_mu;  // slot states + completion FIFO
     std::condition_variable slot_cv;
     std::deque<uint32_t> fifo;   // slots queued for completion, in window order
@@ -362,6 +391,28 @@ struct tm_batcher {
         BT_HIP(hipMemcpyAsync(S.d_bytes.p, S.h_bytes.p, S.nbytes + 1, hipMemcpyHostToDevice, s_comp));
         BT_HIP(hipMemcpyAsync(S.d_off.p, S.h_off.p, (size_t)n * 4 + 4, hipMemcpyHostToDevice, s_comp));
         tm_dev_result r;
+        if (S.mode == TM_MATCH_ALL) {
+            // the walk writes the route ids itself (u32 while every id fits), compacted
+            // topic-major: no key handles, no separate id pass (tm_match_ids_device)
+            S.ids_cap = std::max<uint64_t>(S.ids_cap, std::max<uint64_t>((uint64_t)n * 8, 1 << 16));
+            BT_HIP(S.d_ids.ensure(S.ids_cap * 8 + 8));
+            S.narrow = true;
+            int rc = tmx_batch_match_ids(eng, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, 4,
+                                         S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp, &r);
+            if (rc == TM_ESTATE) {
+                S.narrow = false;
+                rc = tmx_batch_match_ids(eng, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, 8,
+                                         S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp, &r);
+            }
+            if (rc) return rc;
+            S.keys_cap = std::min(r.keys_cap, S.ids_cap);
+            std::memset(S.h_ctl.p, 0, CTL_BYTES);
+            BT_HIP(hipMemcpyAsync(S.h_ctl.p, r.d_total, CTL_BYTES, hipMemcpyDeviceToHost, s_comp));
+            BT_HIP(hipMemcpyAsync(S.h_off_out.p, S.d_off_out.p, (size_t)n * 4 + 4, hipMemcpyDeviceToHost, s_comp));
+            BT_HIP(hipMemcpyAsync(S.h_status.p, r.d_status, (size_t)n * 4, hipMemcpyDeviceToHost, s_comp));
+            BT_HIP(hipEventRecord(S.ev, s_comp));
+            return TM_OK;
+        }
         int rc = tmx_batch_match_device(eng, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes,
                                         S.mode, s_comp, &r);
         if (rc) return rc;
@@ -513,7 +564,11 @@ struct tm_batcher {
             int rc = tmx_engine_grow_pools(eng, seg, fr);
             if (rc) return rc;
             if (over) {  // output arena too small: grow to the demand, run this window again
-                if ((rc = tmx_batch_reserve_matches(eng, total + total / 8 + 1024))) return rc;
+                const uint64_t want = total + total / 8 + 1024;
+                // a TM_MATCH_ALL window's walk writes ids: u64 ones take two words of the arena
+                const uint64_t words = S.mode == TM_MATCH_ALL && !S.narrow ? 2 * want : want;
+                if ((rc = tmx_batch_reserve_matches(eng, words))) return rc;
+                if (S.mode == TM_MATCH_ALL) S.ids_cap = std::max(S.ids_cap, want);
                 if ((rc = enqueue(S))) return rc;
                 BT_HIP(hipEventSynchronize(S.ev));
                 if (S.h_ctl.as<uint64_t>()[0] > S.keys_cap) return TM_EDEVICE;
@@ -816,7 +871,7 @@ struct tm_batcher {
             }
             slot_cv.notify_all();
             // a custom backend's view must be delivered before the next call: one slot at a time
-            next = eng ? (next + 1) % NSLOT : next;
+            next = eng ? (next + 1) % nslot : next;
         }
         {
             std::lock_guard<std::mutex> g(slot_mu);
@@ -870,6 +925,7 @@ struct tm_batcher {
         n_delivery = cfg.delivery_threads ? cfg.delivery_threads : 4;
         if (n_delivery > 64) return TM_EINVAL;
         lat_ns.assign(LAT_RING, 0);
+        if (const char *e = std::getenv("EMQX_TM_NSLOT")) nslot = std::max(2u, std::min(NSLOT_MAX, (uint32_t)std::atoi(e)));
         if (!eng)
             for (Slot &S : slot)
                 for (HBuf *h : {&S.h_bytes, &S.h_off, &S.h_off_out, &S.h_status, &S.h_cnt, &S.h_ids, &S.h_ctl})

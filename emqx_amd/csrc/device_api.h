@@ -14,6 +14,11 @@ constexpr uint32_t MODE_ALL = 0, MODE_COUNT = 1, MODE_FIRST = 2;  // MatchArgs.m
 // (include/emqx_tm.h tm_span): keys points at uint4 spans, keys_cap counts spans, cursor
 // counts spans, out_cnt[t] = topic t's spans, out_kcnt[t] = its keys.
 constexpr uint32_t MODE_RUNS = 3;
+// MODE_IDS32 / MODE_IDS64: the copy-out writes each key's route id (key_rec[2h], the id word of
+// its {id, order code} record) instead of its handle, as u32 (every id < 2^32) or u64: keys
+// points at the caller's id buffer, keys_cap counts ids (emqx_router:match_to_route/1,
+// apps/emqx/src/emqx_router.erl:648-649, fused into the walk: no separate k_result_ids pass).
+constexpr uint32_t MODE_IDS32 = 4, MODE_IDS64 = 5;
 constexpr int SEG_CHUNK = 128;  // key segments per global chunk (16 B each)
 constexpr int SEG_MAXCHUNK = 128;  // segment chunks one wave may flush (its list lives in HBM)
 constexpr int FR_CHUNK = 256;   // frontier entries per global overflow chunk (8 B each)
@@ -44,6 +49,7 @@ struct MatchArgs {
     const RootRec *root;
     const uint32_t *arena;
     const uint32_t *key_bin;   // key handle -> 1 for {Binary, {ID}} keys (sort after word lists)
+    const uint64_t *key_rec;   // MODE_IDS*: 2 u64 per key handle {id, order code}
     // results
     uint32_t *out_off;
     uint32_t *out_cnt;
@@ -76,7 +82,8 @@ struct MatchArgs {
     // probes, [2] word-slot probes, [3] keys emitted, [4] topic levels,
     // [5] topics spilled, [6] key segments, [7] segment-chunk flushes,
     // [8] frontier overflow chunks, [9] node-record reads, [10] keys emitted inline
-    // (fast kernel only for [5]-[10])
+    // (fast kernel only for [5]-[10]); [32 + d], [48 + d], [64 + d], [80 + d]: per walk depth
+    // d (15 = 15 and deeper) edge probes, wave cycles, frontier entries, probe round trips
     unsigned long long *stats;
     // optional: events recorded around k_match_fast on the launch stream
     hipEvent_t ev_fast0, ev_fast1;
@@ -122,6 +129,18 @@ hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const
 hipError_t launch_result_ids32(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
                                const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint32_t *ids,
                                uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, hipStream_t stream);
+// The same copy without the gather: src already holds ids of id_bytes (4 or 8) each, laid
+// out as the walk wrote them (MODE_IDS*); ids[dst_off[t] + k] = src[src_off[t] + k].
+hipError_t launch_compact_ids(uint32_t id_bytes, const uint32_t *src_off, const void *src, const uint32_t *dst_off,
+                              uint32_t n, void *ids, uint64_t cap, uint64_t src_cap, const unsigned long long *cursor,
+                              uint32_t *flags, hipStream_t stream);
+// Concatenate G shards' topic-major compacted ids per topic (tm_merge_shard_ids_device):
+// roff G rows (stride roff_stride) of n+1 per-rank exclusive scans, rank r's ids (id_bytes
+// each) at ids + base[r] elements; off: n+1 merged scan out; out: merged u64 ids.
+constexpr uint32_t MERGE_MAX_G = 64;
+hipError_t launch_merge_shard_ids(uint32_t G, uint32_t n, const uint32_t *roff, uint64_t roff_stride, const void *ids,
+                                  uint32_t id_bytes, const uint64_t *base, uint32_t *off, uint64_t *out, uint64_t cap,
+                                  hipStream_t stream);
 // Concatenate G shards' topic-major results per topic.  roff: G*(n+1) u32, tot: n u32,
 // scratch: scan_scratch_words(n) u32 (work areas); off: n+1 u32 out; out: merged ids.
 hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,

@@ -170,6 +170,8 @@ struct PatchRec {
     uint64_t bytes;  // payload bytes following this record (8-byte padded)
 };
 constexpr uint64_t PATCH_MAGIC = 0x3148435441504d54ull, IMAGE_MAGIC = 0x31474d494d545845ull;
+constexpr size_t STATS_BYTES = 96 * 8;  // walk counters (device_api.h MatchArgs.stats)
+
 struct PatchHdr {
     uint64_t magic;
     uint64_t epoch_from, epoch_to;
@@ -2156,7 +2158,7 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
         TM_TRY_HIP(eng->grow_buf(eng->bb->d_ctl, 2 * CTL_BYTES), TM_ENOMEM, "alloc");
         TM_TRY_HIP(hipMemset(eng->bb->d_ctl.p, 0, 2 * CTL_BYTES), TM_EDEVICE, "memset");  // both blocks start at 0
     }
-    TM_TRY_HIP(eng->grow_buf(eng->d_stats, 256), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->d_stats, STATS_BYTES), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->grow_buf(eng->bb->d_scr_w, (bytes + 2ull * n + 2) * 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->grow_buf(eng->bb->d_scr_s, (bytes + 2ull * n + 2) * 8), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->grow_buf(eng->bb->d_wave_chunks, match_grid(n, pick_tpw(n, eng->cfg.topics_per_wave)) * SEG_MAXCHUNK * 4 + 4),
@@ -2218,6 +2220,7 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.tpw = pick_tpw(n, tpw ? tpw : eng->cfg.topics_per_wave);
     a.first_dfs = eng->dv.n_deep ? 1u : 0u;
     a.key_bin = eng->d_key_bin.as<uint32_t>();
+    a.key_rec = eng->d_key_rec.as<uint64_t>();
     a.bytes = d_bytes;
     a.off = d_off;
     a.n = n;
@@ -2739,6 +2742,81 @@ __attribute__((visibility("hidden"))) int tmx_result_ids32_device(tm_engine *eng
     return TM_OK;
 }
 
+static int match_ids_impl(tm_engine *eng, BatchBufs *set, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                          uint64_t total_bytes, uint32_t id_bytes, void *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
+                          uint32_t *d_flags, void *stream, tm_dev_result *out) {
+    if (!eng || !d_off || (n && !d_bytes) || !d_off_out || (ids_cap && !d_ids) || (id_bytes != 4 && id_bytes != 8))
+        return TM_EINVAL;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    eng->bb = set;
+    if (id_bytes == 4 && eng->dv.max_id > 0xFFFFFFFFull) {
+        eng->err = "tm_match_ids_device: an id of this index does not fit 32 bits";
+        return TM_ESTATE;
+    }
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    TM_TRY_HIP(eng->chain_after_last(s), TM_EDEVICE, "stream order");
+    int rc = ensure_batch(eng, n, total_bytes);
+    if (rc) return rc;
+    eng->bb->last_stream = s;
+    eng->bb->last_n = n;
+    // the walk writes its ids wave-ordered into the batch's key buffer (as many u32 words per
+    // id as id_bytes needs), then one pass copies them topic-major into the caller's buffer
+    const uint64_t cap = eng->bb->keys_cap / (id_bytes / 4);
+    const uint32_t kmode = id_bytes == 4 ? MODE_IDS32 : MODE_IDS64;
+    TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s, kmode, 0, eng->bb->d_keys.as<uint32_t>(), cap),
+               TM_EDEVICE, "kernel launch");
+    eng->bb->last_mode = TM_MATCH_ALL;
+    eng->bb->dev_batch = false;  // the key buffer holds ids now: no tm_result_ids_device on it
+    TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(launch_excl_scan(eng->bb->d_outcnt.as<uint32_t>(), 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s),
+               TM_EDEVICE, "scan");
+    TM_TRY_HIP(launch_compact_ids(id_bytes, eng->bb->d_outoff.as<uint32_t>(), eng->bb->d_keys.p, d_off_out, n, d_ids,
+                                  ids_cap, cap, (const unsigned long long *)(eng->bb->p_ctl + CTL_CURSOR), d_flags, s),
+               TM_EDEVICE, "compact ids");
+    TM_TRY_HIP(eng->note_use(s), TM_EDEVICE, "event");
+    if (out) {  // the walk's own per-topic arrays and counter block (library-internal callers)
+        out->n = n;
+        out->d_off = eng->bb->d_outoff.as<uint32_t>();
+        out->d_cnt = eng->bb->d_outcnt.as<uint32_t>();
+        out->d_keys = nullptr;
+        out->d_status = eng->bb->d_status.as<int32_t>();
+        out->d_total = (uint64_t *)(eng->bb->p_ctl + CTL_CURSOR);
+        out->keys_cap = cap;
+    }
+    return TM_OK;
+}
+
+int tm_match_ids_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                        uint64_t total_bytes, uint32_t id_bytes, void *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
+                        uint32_t *d_flags, void *stream) {
+    return eng ? match_ids_impl(eng, &eng->bb_dev, d_bytes, d_off, n, total_bytes, id_bytes, d_ids, ids_cap, d_off_out,
+                                d_flags, stream, nullptr)
+               : TM_EINVAL;
+}
+// library-internal (batcher.cpp): the same on the aggregator's own buffer set
+__attribute__((visibility("hidden"))) int tmx_batch_match_ids(tm_engine *eng, const uint8_t *d_bytes,
+                                                              const uint32_t *d_off, uint32_t n, uint64_t total_bytes,
+                                                              uint32_t id_bytes, void *d_ids, uint64_t ids_cap,
+                                                              uint32_t *d_off_out, void *stream, tm_dev_result *out) {
+    return match_ids_impl(eng, &eng->bb_batch, d_bytes, d_off, n, total_bytes, id_bytes, d_ids, ids_cap, d_off_out,
+                          nullptr, stream, out);
+}
+
+int tm_merge_shard_ids_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_t *d_roff, uint64_t roff_stride,
+                              const void *d_ids, uint32_t id_bytes, const uint64_t *base, uint32_t *d_out_off,
+                              uint64_t *d_out_ids, uint64_t out_cap, void *stream) {
+    if (!eng || G == 0 || G > MERGE_MAX_G || !d_roff || !base || !d_out_off || roff_stride < (uint64_t)n + 1 ||
+        (id_bytes != 4 && id_bytes != 8) || (out_cap && (!d_out_ids || !d_ids)))
+        return TM_EINVAL;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    TM_TRY_HIP(launch_merge_shard_ids(G, n, d_roff, roff_stride, d_ids, id_bytes, base, d_out_off, d_out_ids, out_cap, s),
+               TM_EDEVICE, "merge");
+    return TM_OK;
+}
+
 int tm_merge_shards_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_t *d_counts, const uint64_t *d_ids,
                            uint64_t stride, uint32_t *d_off_out, uint64_t *d_ids_out, uint64_t out_cap, void *stream) {
     if (!eng || G == 0 || !d_off_out || (n && (!d_counts || !d_ids)) || (out_cap && !d_ids_out)) return TM_EINVAL;
@@ -3074,13 +3152,24 @@ int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out18) {
     if (!eng) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
-    TM_TRY_HIP(eng->d_stats.ensure(256), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->d_stats.ensure(STATS_BYTES), TM_ENOMEM, "alloc");
     if (out18) {
         TM_TRY_HIP(hipDeviceSynchronize(), TM_EDEVICE, "sync");
         TM_TRY_HIP(hipMemcpy(out18, eng->d_stats.p, 18 * 8, hipMemcpyDeviceToHost), TM_EDEVICE, "D2H");
     }
-    TM_TRY_HIP(hipMemset(eng->d_stats.p, 0, 256), TM_EDEVICE, "memset");
+    TM_TRY_HIP(hipMemset(eng->d_stats.p, 0, STATS_BYTES), TM_EDEVICE, "memset");
     eng->stats_on = enable != 0;
+    return TM_OK;
+}
+
+int tm_debug_depth_stats(tm_engine *eng, uint64_t *out64) {
+    if (!eng || !out64) return TM_EINVAL;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    TM_TRY_HIP(eng->d_stats.ensure(STATS_BYTES), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(hipDeviceSynchronize(), TM_EDEVICE, "sync");
+    TM_TRY_HIP(hipMemcpy(out64, (const uint8_t *)eng->d_stats.p + 32 * 8, 64 * 8, hipMemcpyDeviceToHost), TM_EDEVICE,
+               "D2H");
     return TM_OK;
 }
 

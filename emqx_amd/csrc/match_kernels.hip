@@ -84,6 +84,44 @@ __device__ __forceinline__ void put_key(uint32_t *p, uint32_t k) {
     *p = k;
 #endif
 }
+// what k_match_fast's copy-out writes per key (template parameter OUT)
+constexpr int O_KEYS = 0, O_RUNS = 1, O_IDS32 = 2, O_IDS64 = 3;
+__device__ __forceinline__ void put_id32(uint32_t *p, uint32_t v) {
+#if TM_NT_KEYS
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void put_id64(uint64_t *p, uint64_t v) {
+#if TM_NT_KEYS
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+// keys loaded from the arena -> what the output holds: the handles, or (MODE_IDS*) their ids
+// (all gathers of the unrolled group are issued before the first store)
+template <int OUT, int U>
+__device__ __forceinline__ void store_group(const MatchArgs &a, uint64_t dst0, uint32_t stride, const uint32_t (&key)[U],
+                                            uint32_t nvalid) {
+    if constexpr (OUT == O_KEYS) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if ((uint32_t)u < nvalid) put_key(&a.keys[dst0 + (uint64_t)u * stride], key[u]);
+    } else {
+        uint64_t id[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if ((uint32_t)u < nvalid) id[u] = a.key_rec[2ull * key[u]];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if ((uint32_t)u < nvalid) {
+                if constexpr (OUT == O_IDS32) put_id32(&a.keys[dst0 + (uint64_t)u * stride], (uint32_t)id[u]);
+                else put_id64(reinterpret_cast<uint64_t *>(a.keys) + dst0 + (uint64_t)u * stride, id[u]);
+            }
+    }
+}
 constexpr int RPL = TM_RPL;                 // frontier entries per lane per round
 constexpr int CP_UNROLL = TM_CP_UNROLL;     // arena loads in flight per lane, long lists
 constexpr int CP_SHORT = 8;                 // lists up to this long are copied by one lane
@@ -300,6 +338,7 @@ struct WaveLds {
 // single inline keys) are copied by the lane that holds them; long ones (hot '#'
 // filters with thousands of subscribers) are queued and copied by the whole wave, 64
 // consecutive keys per instruction, CP_UNROLL instructions in flight.
+template <int OUT>
 __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, uint32_t ns) {
     const uint32_t lane = lane_id();
     uint32_t nlong = 0;  // wave-uniform; long segment indices are queued in L.seg_scan
@@ -321,15 +360,14 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
         if (!is_long && g.y) {
             const uint32_t dst = L.tbase[g.w & 0xFFu] + g.z;
             if (g.w & SEG_INLINE) {
-                put_key(&a.keys[dst], g.x);
+                const uint32_t one[1] = {g.x};
+                store_group<OUT, 1>(a, dst, 1, one, 1);
             } else {
                 uint32_t key[CP_SHORT];
 #pragma unroll
                 for (int k = 0; k < CP_SHORT; k++)
                     if ((uint32_t)k < g.y) key[k] = a.arena[g.x + k];
-#pragma unroll
-                for (int k = 0; k < CP_SHORT; k++)
-                    if ((uint32_t)k < g.y) put_key(&a.keys[dst + k], key[k]);
+                store_group<OUT, CP_SHORT>(a, dst, 1, key, g.y);
             }
         }
 #if TM_QCOPY
@@ -368,11 +406,8 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
                         const uint32_t k = k0 + u * GRP;
                         if (k < g.y) key[u] = a.arena[g.x + k];
                     }
-#pragma unroll
-                    for (int u = 0; u < CP_UNROLL; u++) {
-                        const uint32_t k = k0 + u * GRP;
-                        if (k < g.y) put_key(&a.keys[dst + k], key[u]);
-                    }
+                    // keys k0, k0 + GRP, ... are valid while below g.y
+                    store_group<OUT, CP_UNROLL>(a, (uint64_t)dst + k0, GRP, key, (g.y - k0 + GRP - 1) / GRP);
                 }
             }
         }
@@ -393,11 +428,7 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
                 const uint32_t k = k0 + u * WAVE;
                 if (k < g.y) key[u] = a.arena[g.x + k];
             }
-#pragma unroll
-            for (int u = 0; u < CP_UNROLL; u++) {
-                const uint32_t k = k0 + u * WAVE;
-                if (k < g.y) put_key(&a.keys[dst + k], key[u]);
-            }
+            store_group<OUT, CP_UNROLL>(a, (uint64_t)dst + k0, WAVE, key, (g.y - k0 + WAVE - 1) / WAVE);
         }
     }
     __syncthreads();
@@ -421,8 +452,9 @@ __device__ __forceinline__ void emit_spans(const MatchArgs &a, const WaveLds &L,
     }
 }
 
-template <bool STATS, bool RUNS>
+template <bool STATS, int OUT>
 __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) {
+    constexpr bool RUNS = OUT == O_RUNS;
     __shared__ WaveLds L;
     uint32_t *const wchunks = a.wave_chunks + (uint64_t)blockIdx.x * MAXCHUNK;  // this wave's flushed chunks
     const uint32_t lane = lane_id();
@@ -586,6 +618,11 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     // ---- 3. level-synchronous walk
     for (uint32_t d = 0; nfr > 0; ++d) {
         const uint32_t cur = d & 1, nxt = cur ^ 1;
+        // STATS build: per-depth edge probes, wave cycles, frontier entries and probe round
+        // trips (wave-level iterations of the dependent probe loop), tm_debug_depth_stats
+        uint32_t dp_probe = 0, dp_rt = 0;
+        uint64_t dp_t0 = 0;
+        if constexpr (STATS) dp_t0 = __builtin_amdgcn_s_memtime();
         // 3a. tokenise level d+1 ahead for topics that are still alive and go deeper:
         //     the children pushed at this depth are filtered with it (bloom)
 #if TM_ALIVE_REG
@@ -635,7 +672,9 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                         x1[k] = p1[k] ? *reinterpret_cast<const uint4 *>(a.etab + s1[k]) : make_uint4(NONE, 0, 0, 0);
                         x2[k] = p2[k] ? *reinterpret_cast<const uint4 *>(a.etab + s2[k]) : make_uint4(NONE, 0, 0, 0);
                         st_probe += (uint32_t)p1[k] + (uint32_t)p2[k];
+                        if constexpr (STATS) dp_probe += (uint32_t)p1[k] + (uint32_t)p2[k];
                     }
+                    if constexpr (STATS) dp_rt++;
 #pragma unroll
                     for (int k = 0; k < RPL; k++) {
                         if (p1[k]) {
@@ -827,6 +866,17 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
             for (int k = 0; k < RPL; k++) st_visit += (uint32_t)f1[k] + (uint32_t)f2[k];
         }
         __syncthreads();
+        if constexpr (STATS) {
+            const uint32_t dd = d < 15u ? d : 15u;
+            const uint64_t pv = wave_sum64(dp_probe);
+            const uint64_t dt = __builtin_amdgcn_s_memtime() - dp_t0;
+            if (lane == 0) {
+                atomicAdd(&a.stats[32 + dd], (unsigned long long)pv);
+                atomicAdd(&a.stats[48 + dd], (unsigned long long)dt);
+                atomicAdd(&a.stats[64 + dd], (unsigned long long)nfr);
+                atomicAdd(&a.stats[80 + dd], (unsigned long long)dp_rt);
+            }
+        }
         nfr = nnext;
 #if TM_ALIVE_REG
         alive_c = alive_n;
@@ -868,13 +918,13 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
             emit_spans(a, L, L.seg, nseg);
             for (uint32_t c = 0; c < nchunk; ++c) emit_spans(a, L, a.seg_pool + (uint64_t)wchunks[c] * SCAP, SCAP);
         }
-    } else if (!overflow && total && a.mode == MODE_ALL) {
-        expand_segments(a, L, nseg);
+    } else if (!overflow && total && (OUT != O_KEYS || a.mode == MODE_ALL)) {
+        expand_segments<OUT>(a, L, nseg);
         for (uint32_t c = 0; c < nchunk; ++c) {
             const uint4 *src = a.seg_pool + (uint64_t)wchunks[c] * SCAP;
             for (uint32_t j = lane; j < (uint32_t)SCAP; j += WAVE) L.seg[j] = src[j];
             __syncthreads();
-            expand_segments(a, L, SCAP);
+            expand_segments<OUT>(a, L, SCAP);
         }
     }
 
@@ -917,19 +967,24 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
 // Stack entry: slot index (40 bits; ROOT_MARK for the root) | depth (24 bits).
 constexpr uint64_t ROOT_MARK = (1ull << 40) - 1;
 
-// one key of a topic the spill kernel walks: the key handle, or (MODE_RUNS) a one-key span
-__device__ __forceinline__ void out_key(const MatchArgs &a, uint32_t *out, uint32_t i, uint32_t key) {
+// one key of a topic the spill kernel walks, output slot i: the key handle, (MODE_RUNS) a
+// one-key span, or (MODE_IDS*) its route id
+__device__ __forceinline__ void out_key(const MatchArgs &a, uint64_t i, uint32_t key) {
     if (a.mode == MODE_RUNS) {
         const uint64_t p = a.span_keys + 16ull * key;
-        reinterpret_cast<uint4 *>(out)[i] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), 1u, 0u);
+        reinterpret_cast<uint4 *>(a.keys)[i] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), 1u, 0u);
+    } else if (a.mode == MODE_IDS32) {
+        a.keys[i] = (uint32_t)a.key_rec[2ull * key];
+    } else if (a.mode == MODE_IDS64) {
+        reinterpret_cast<uint64_t *>(a.keys)[i] = a.key_rec[2ull * key];
     } else {
-        out[i] = key;
+        a.keys[i] = key;
     }
 }
 
 template <bool WRITE>
 __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_t *wid, uint64_t *stk, uint32_t nl,
-                             bool dollar, uint32_t *out, uint32_t *probes, uint32_t *visits) {
+                             bool dollar, uint64_t out, uint32_t *probes, uint32_t *visits) {
     uint32_t sp = 0, count = 0;
     stk[sp++] = ROOT_MARK << 24;
     while (sp) {
@@ -955,18 +1010,18 @@ __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_
                 hc = a.arena[lo - 1];
             } else if (m == M_INLINE && ((info & I_INL_HASH) || d == nl)) {
                 // the node's only key, inline in the slot
-                if (WRITE) out_key(a, out, count, info & I_KEY_MASK);
+                if (WRITE) out_key(a, out + count, info & I_KEY_MASK);
                 count++;
             }
         }
         (*visits)++;
         // "P/#" keys match at P and below
         if (WRITE)
-            for (uint32_t k = 0; k < hc; k++) out_key(a, out, count + k, a.arena[lo + tc + k]);
+            for (uint32_t k = 0; k < hc; k++) out_key(a, out + count + k, a.arena[lo + tc + k]);
         count += hc;
         if (d == nl) {
             if (WRITE)
-                for (uint32_t k = 0; k < tc; k++) out_key(a, out, count + k, a.arena[lo + k]);
+                for (uint32_t k = 0; k < tc; k++) out_key(a, out + count + k, a.arena[lo + k]);
             count += tc;
             continue;
         }
@@ -1000,19 +1055,15 @@ __global__ __launch_bounds__(WAVE) void k_match_slow(MatchArgs a) {
             if (i >= e) break;
         }
         uint32_t dummy_v = 0, dummy_p = 0;
-        const uint32_t c = dfs_walk<false>(a, R, wid, stk, nl, dollar, nullptr, &dummy_p, &dummy_v);
+        const uint32_t c = dfs_walk<false>(a, R, wid, stk, nl, dollar, 0, &dummy_p, &dummy_v);
         const unsigned long long pos = atomicAdd(a.cursor, (unsigned long long)c);
         a.out_off[t] = (uint32_t)pos;
         a.out_cnt[t] = c;
         a.status[t] = 0;
         st_keys += c;
-        if (a.mode == MODE_RUNS) {
-            a.out_kcnt[t] = c;
-            if (pos + c <= a.keys_cap)  // spans are 4 u32 each
-                dfs_walk<true>(a, R, wid, stk, nl, dollar, a.keys + 4 * pos, &st_probe, &st_visit);
-        } else if (a.mode == MODE_ALL && pos + c <= a.keys_cap) {
-            dfs_walk<true>(a, R, wid, stk, nl, dollar, a.keys + pos, &st_probe, &st_visit);
-        }
+        if (a.mode == MODE_RUNS) a.out_kcnt[t] = c;
+        if (a.mode != MODE_COUNT && pos + c <= a.keys_cap)  // output slots: keys, spans or ids
+            dfs_walk<true>(a, R, wid, stk, nl, dollar, pos, &st_probe, &st_visit);
     }
     if constexpr (STATS) {
         // levels were already counted by the fast kernel's pre-scan
@@ -1602,11 +1653,15 @@ hipError_t launch_match(const MatchArgs &a, hipStream_t s) {
     }
     if (a.ev_fast0 && (e = hipEventRecord(a.ev_fast0, s))) return e;
     if (a.mode == MODE_RUNS) {
-        if (a.stats) k_match_fast<true, true><<<grid, WAVE, 0, s>>>(a);
-        else k_match_fast<false, true><<<grid, WAVE, 0, s>>>(a);
+        if (a.stats) k_match_fast<true, O_RUNS><<<grid, WAVE, 0, s>>>(a);
+        else k_match_fast<false, O_RUNS><<<grid, WAVE, 0, s>>>(a);
+    } else if (a.mode == MODE_IDS32) {
+        k_match_fast<false, O_IDS32><<<grid, WAVE, 0, s>>>(a);
+    } else if (a.mode == MODE_IDS64) {
+        k_match_fast<false, O_IDS64><<<grid, WAVE, 0, s>>>(a);
     } else {
-        if (a.stats) k_match_fast<true, false><<<grid, WAVE, 0, s>>>(a);
-        else k_match_fast<false, false><<<grid, WAVE, 0, s>>>(a);
+        if (a.stats) k_match_fast<true, O_KEYS><<<grid, WAVE, 0, s>>>(a);
+        else k_match_fast<false, O_KEYS><<<grid, WAVE, 0, s>>>(a);
     }
     if ((e = hipGetLastError())) return e;
     if (a.ev_fast1 && (e = hipEventRecord(a.ev_fast1, s))) return e;

@@ -120,8 +120,10 @@ __device__ __forceinline__ uint32_t topic_of(const uint32_t *dst_off, uint32_t l
     return lo;
 }
 
-template <class IdT>
-__global__ __launch_bounds__(RI_T) void k_result_ids(const uint32_t *src_off, const uint32_t *keys,
+// GATHER: src holds key handles and ids[q] = key_rec[2 * handle]; otherwise src already holds
+// the ids (the walk wrote them, MODE_IDS*) and this is a pure topic-major compaction copy.
+template <class IdT, bool GATHER>
+__global__ __launch_bounds__(RI_T) void k_result_ids(const uint32_t *src_off, const void *src,
                                                      const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n,
                                                      IdT *ids, uint64_t cap, uint64_t keys_cap,
                                                      const unsigned long long *cursor) {
@@ -144,8 +146,11 @@ __global__ __launch_bounds__(RI_T) void k_result_ids(const uint32_t *src_off, co
             const uint64_t q = q0 + (uint64_t)i * RI_T + threadIdx.x;
             if (q >= q1) break;
             t = topic_of(dst_off, t, t1, q);  // positions rise with i: start from the last topic
-            const uint64_t src = (uint64_t)src_off[t] + (q - dst_off[t]);
-            if (src < keys_cap) ids[q] = (IdT)key_rec[2ull * keys[src]];
+            const uint64_t j = (uint64_t)src_off[t] + (q - dst_off[t]);
+            if (j < keys_cap) {
+                if constexpr (GATHER) ids[q] = (IdT)key_rec[2ull * static_cast<const uint32_t *>(src)[j]];
+                else ids[q] = static_cast<const IdT *>(src)[j];
+            }
         }
     }
 }
@@ -158,17 +163,15 @@ __global__ void k_result_flags(const unsigned long long *cursor, uint64_t keys_c
         flags[0] = (*cursor > keys_cap ? RES_KEYS_OVERFLOW : 0u) | ((uint64_t)dst_off[n] > cap ? RES_IDS_OVERFLOW : 0u);
 }
 
-template <class IdT>
-static hipError_t launch_result_ids_t(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
-                                      const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, IdT *ids,
-                                      uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, uint32_t *flags,
-                                      hipStream_t s) {
-    (void)cnt;  // dst_off is its scan
+template <class IdT, bool GATHER>
+static hipError_t launch_result_ids_t(const uint32_t *src_off, const void *src, const uint64_t *key_rec,
+                                      const uint32_t *dst_off, uint32_t n, IdT *ids, uint64_t cap, uint64_t keys_cap,
+                                      const unsigned long long *cursor, uint32_t *flags, hipStream_t s) {
     if (n && cap) {
         // sized from the caller's cap (the result's size is on the device): surplus blocks exit
         const uint64_t blocks = std::min<uint64_t>((cap + RI_BLK - 1) / RI_BLK, 2048);
-        k_result_ids<IdT><<<(uint32_t)blocks, RI_T, 0, s>>>(src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap,
-                                                            cursor);
+        k_result_ids<IdT, GATHER><<<(uint32_t)blocks, RI_T, 0, s>>>(src_off, src, key_rec, dst_off, n, ids, cap,
+                                                                    keys_cap, cursor);
         hipError_t e = hipGetLastError();
         if (e) return e;
     }
@@ -183,13 +186,26 @@ hipError_t launch_result_ids(const uint32_t *cnt, const uint32_t *src_off, const
                              const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint64_t *ids,
                              uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, uint32_t *flags,
                              hipStream_t s) {
-    return launch_result_ids_t(cnt, src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap, cursor, flags, s);
+    (void)cnt;  // dst_off is its scan
+    return launch_result_ids_t<uint64_t, true>(src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap, cursor, flags, s);
 }
 
 hipError_t launch_result_ids32(const uint32_t *cnt, const uint32_t *src_off, const uint32_t *keys,
                                const uint64_t *key_rec, const uint32_t *dst_off, uint32_t n, uint32_t *ids,
                                uint64_t cap, uint64_t keys_cap, const unsigned long long *cursor, hipStream_t s) {
-    return launch_result_ids_t(cnt, src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap, cursor, nullptr, s);
+    (void)cnt;
+    return launch_result_ids_t<uint32_t, true>(src_off, keys, key_rec, dst_off, n, ids, cap, keys_cap, cursor, nullptr,
+                                               s);
+}
+
+hipError_t launch_compact_ids(uint32_t id_bytes, const uint32_t *src_off, const void *src, const uint32_t *dst_off,
+                              uint32_t n, void *ids, uint64_t cap, uint64_t src_cap, const unsigned long long *cursor,
+                              uint32_t *flags, hipStream_t s) {
+    if (id_bytes == 4)
+        return launch_result_ids_t<uint32_t, false>(src_off, src, nullptr, dst_off, n, (uint32_t *)ids, cap, src_cap,
+                                                    cursor, flags, s);
+    return launch_result_ids_t<uint64_t, false>(src_off, src, nullptr, dst_off, n, (uint64_t *)ids, cap, src_cap, cursor,
+                                                flags, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -237,6 +253,77 @@ hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, c
     if ((e = launch_excl_scan(tot, 1, n, off, scratch, s))) return e;
     if (!n) return hipSuccess;
     k_merge<<<(n + 63) / 64, 64, 0, s>>>(counts, ids, stride, roff, off, G, n, out, cap);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// shard merge over topic-major compacted ids (tm_merge_shard_ids_device).  roff: G rows of
+// n+1 (rank r's exclusive scan of its per-topic counts, i.e. its own d_off_out), rank r's ids
+// at ids + base[r].  The merged exclusive scan is the column sum of the rows' scans, so no
+// scan is launched: off[t] = sum_r roff_r[t].  Then one output-parallel pass: position q of
+// topic t takes the k-th id of the topic's concatenation over ranks 0..G-1.
+struct ShardBases {
+    uint64_t b[MERGE_MAX_G];
+};
+
+__global__ void k_roff_colsum(const uint32_t *roff, uint64_t stride, uint32_t G, uint32_t n, uint32_t *off) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > n) return;
+    uint32_t s = 0;
+    for (uint32_t r = 0; r < G; r++) s += roff[(uint64_t)r * stride + t];
+    off[t] = s;
+}
+
+template <class IdT>
+__global__ __launch_bounds__(RI_T) void k_merge_flat(const uint32_t *roff, uint64_t stride, uint32_t G, uint32_t n,
+                                                     const IdT *ids, ShardBases base, const uint32_t *off,
+                                                     uint64_t *out, uint64_t cap) {
+    const uint64_t lim = min((uint64_t)off[n], cap);  // topics past the caller's cap stay unwritten
+    __shared__ uint32_t s_t0, s_t1;
+    for (uint64_t q0 = (uint64_t)blockIdx.x * RI_BLK; q0 < lim; q0 += (uint64_t)gridDim.x * RI_BLK) {
+        const uint64_t q1 = min(q0 + RI_BLK, lim);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            s_t0 = topic_of(off, 0, n, q0);
+            s_t1 = topic_of(off, s_t0, n, q1 - 1);
+        }
+        __syncthreads();
+        uint32_t t = s_t0;
+        const uint32_t t1 = s_t1;
+#pragma unroll 4
+        for (uint32_t i = 0; i < RI_PER; i++) {
+            const uint64_t q = q0 + (uint64_t)i * RI_T + threadIdx.x;
+            if (q >= q1) break;
+            t = topic_of(off, t, t1, q);
+            uint32_t k = (uint32_t)(q - off[t]);
+            for (uint32_t r = 0; r < G; r++) {
+                const uint32_t a = roff[(uint64_t)r * stride + t], c = roff[(uint64_t)r * stride + t + 1] - a;
+                if (k < c) {
+                    out[q] = (uint64_t)ids[base.b[r] + a + k];
+                    break;
+                }
+                k -= c;
+            }
+        }
+    }
+}
+
+hipError_t launch_merge_shard_ids(uint32_t G, uint32_t n, const uint32_t *roff, uint64_t roff_stride, const void *ids,
+                                  uint32_t id_bytes, const uint64_t *base, uint32_t *off, uint64_t *out, uint64_t cap,
+                                  hipStream_t s) {
+    if (G == 0 || G > MERGE_MAX_G) return hipErrorInvalidValue;
+    ShardBases b{};
+    for (uint32_t r = 0; r < G; r++) b.b[r] = base[r];
+    k_roff_colsum<<<(n + 1 + 255) / 256, 256, 0, s>>>(roff, roff_stride, G, n, off);
+    hipError_t e = hipGetLastError();
+    if (e || !n || !cap) return e;
+    const uint64_t blocks = std::min<uint64_t>((cap + RI_BLK - 1) / RI_BLK, 2048);
+    if (id_bytes == 4)
+        k_merge_flat<uint32_t><<<(uint32_t)blocks, RI_T, 0, s>>>(roff, roff_stride, G, n, (const uint32_t *)ids, b, off,
+                                                                 out, cap);
+    else
+        k_merge_flat<uint64_t><<<(uint32_t)blocks, RI_T, 0, s>>>(roff, roff_stride, G, n, (const uint64_t *)ids, b, off,
+                                                                 out, cap);
     return hipGetLastError();
 }
 

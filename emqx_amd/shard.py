@@ -6,16 +6,17 @@ the filter set outgrows one GPU's budget, this mode splits the route keys instea
 
   * key (filter, id) lives on rank shard_of(id) = splitmix64(id) % G, for adds and deletes
     alike, so a delete always reaches the shard that holds its key;
-  * every rank matches the WHOLE topic batch against its shard;
-  * one exchange step merges the per-shard results: an all-gather of per-topic counts,
-    then an all-gather of each rank's topic-major route ids (padded to the largest
-    rank's total), then a per-topic concatenation (tm_merge_shards[_device]).  Shards
-    are disjoint, so nothing is deduplicated, exactly like one unsharded walk.
+  * every rank matches the WHOLE topic batch against its shard; the walk writes route ids
+    (u32 while they fit) compacted topic-major (tm_match_ids_device);
+  * one exchange step (ShardedIndex docstring: padded / exact / local) and a per-topic
+    concatenation (tm_merge_shard_ids_device).  Shards are disjoint, so nothing is
+    deduplicated, exactly like one unsharded walk.
 
 On GPUs the exchange runs over RCCL (backend "nccl") on device tensors and the merge is
-the HIP kernel behind tm_merge_shards_device.  On CPU (gloo) the host path runs: local
-host results, all-gather over gloo, host merge (tm_merge_shards).  The per-shard matcher
-is any object with apply_packed / commit / match_ids; the product one is EngineShard.
+the HIP kernel behind tm_merge_shard_ids_device.  On CPU (gloo) the host path runs: local
+host results, the same exchange over gloo, the host form of the merge
+(merge_shard_ids_host).  The per-shard matcher is any object with apply_packed / commit /
+match_ids; the product one is EngineShard.
 """
 from __future__ import annotations
 
@@ -61,6 +62,34 @@ def select_keys(buf, off, ids, mask, flags=None):
     return nbuf, noff, ids[mask], nfl
 
 
+EXCHANGES = ("padded", "exact", "local")
+
+
+def merge_shard_ids_host(H, ids, bases, n: int):
+    """Host form of the device merge (tm_merge_shard_ids_device, result_kernels.hip
+    k_merge_flat): H (G, n+2) u32 rows [topic-major offsets (n+1) | flags], rank r's ids at
+    ids[bases[r]:].  Returns (off u32[n+1], merged u64 ids): topic t's ids are the
+    concatenation of its slices from rank 0..G-1."""
+    H = np.asarray(H).view(np.uint32).reshape(len(bases), -1)
+    ids = np.asarray(ids)
+    G = len(bases)
+    roff = H[:, :n + 1].astype(np.int64)
+    cnt = np.diff(roff, axis=1)
+    off = roff.sum(0)
+    out = np.zeros(int(off[-1]), dtype=np.uint64)
+    before = np.zeros(n, dtype=np.int64)  # ids of ranks < r in each topic
+    for r in range(G):
+        c = cnt[r]
+        tot = int(c.sum())
+        if tot:
+            t_of = np.repeat(np.arange(n), c)
+            k = np.arange(tot) - np.repeat(roff[r, :-1] - roff[r, 0], c)
+            src = int(bases[r]) + roff[r, :-1][t_of] + k
+            out[off[:-1][t_of] + before[t_of] + k] = ids[src].astype(np.uint64)
+        before += c
+    return off.astype(np.uint32), out
+
+
 class EngineShard:
     """The product per-shard matcher: one HIP engine (one GPU) holding this rank's keys."""
 
@@ -74,24 +103,39 @@ class EngineShard:
         return self.eng.commit()
 
     def match_ids(self, t_bytes, t_off):
-        """Host path: (cnt u32 [n], ids u64 topic-major, status i32 [n])."""
+        """Host path: (topic-major offsets u32 [n+1], ids u64, status i32 [n])."""
         off, cnt, keys, st = self.eng.match_packed(t_bytes, t_off)
         n = len(cnt)
-        total = int(cnt.sum(dtype=np.uint64))
-        if total == 0:
-            return cnt.astype(np.uint32), np.zeros(0, np.uint64), st
-        # topic-major gather of the engine's (wave-ordered) key ranges
         starts = np.zeros(n + 1, dtype=np.int64)
         np.cumsum(cnt, out=starts[1:])
+        total = int(starts[-1])
+        if total == 0:
+            return starts.astype(np.uint32), np.zeros(0, np.uint64), st
+        # topic-major gather of the engine's (wave-ordered) key ranges
         idx = np.repeat(off.astype(np.int64) - starts[:-1], cnt.astype(np.int64)) + np.arange(total)
-        return cnt.astype(np.uint32), self.eng.key_ids(keys[idx]), st
+        return starts.astype(np.uint32), self.eng.key_ids(keys[idx]), st
 
 
 class ShardedIndex:
-    """One rank's view of a filter-sharded index over `world` ranks."""
+    """One rank's view of a filter-sharded index over `world` ranks.
 
-    def __init__(self, shard, rank: int, world: int, group=None):
+    The exchange of a step (`exchange`, SURVEY.md §8(e) mode 2):
+      padded  all-gather of every rank's header (topic-major offsets + flags) and of its ids
+              padded to a common stride fixed by prepare_device: no host sync in the step;
+      exact   all-gather of the headers, then every rank's ids at their exact size by grouped
+              send/recv (the sizes come from the gathered headers: one host read per step);
+      local   no collective: each rank copies its own shard's lists to the host, and the
+              consumer reads the G shard lists of a topic side by side.
+    Ids cross the wire as u32 while every id of every shard fits 32 bits (u64 otherwise)."""
+
+    def __init__(self, shard, rank: int, world: int, group=None, exchange: str = "padded"):
+        if exchange not in EXCHANGES:
+            raise ValueError(f"exchange must be one of {EXCHANGES}")
         self.shard, self.rank, self.world, self.group = shard, rank, world, group
+        self.exchange = exchange
+        self.id_bytes = 8
+        self.stride = None
+        self.wire_bytes = 0  # bytes this rank received in the last step's exchange
 
     # ---- writes: every rank sees the same op stream and keeps its own keys
     def apply_packed(self, op, buf, off, ids, flags=None):
@@ -102,41 +146,89 @@ class ShardedIndex:
     def commit(self):
         return self.shard.commit()
 
-    # ---- host path (gloo or nccl)
-    def match(self, t_bytes, t_off):
-        """Match the whole batch on every rank; returns the merged (off[n+1] u32, ids u64,
-        status i32[n]) on every rank."""
+    # ---- the collective part, shared by the host (gloo) and device (RCCL) paths
+    def _exchange(self, hdr, ids, n: int, exchange: str):
+        """hdr: this rank's (n+2) i32 [offsets | flags]; ids: its ids buffer (>= its total, the
+        padded stride long for `padded`).  Returns (H (G, n+2) i32, Ids flat, bases)."""
         import torch
         import torch.distributed as dist
-        cnt, ids, st = self.shard.match_ids(t_bytes, t_off)
-        n = len(cnt)
-        if self.world == 1:
-            return N.merge_shards(cnt.reshape(1, n), ids.reshape(1, -1)) + (st,)
+        G = self.world
+        if G == 1:
+            self.wire_bytes = 0
+            return hdr.view(1, n + 2), ids, [0]
+        H = torch.empty(G * (n + 2), dtype=hdr.dtype, device=hdr.device)
+        dist.all_gather_into_tensor(H, hdr, group=self.group)
+        H = H.view(G, n + 2)
+        eb = ids.element_size()
+        if exchange == "padded":
+            stride = ids.numel()
+            Ids = torch.empty(G * stride, dtype=ids.dtype, device=ids.device)
+            dist.all_gather_into_tensor(Ids, ids, group=self.group)
+            self.wire_bytes = (G - 1) * (stride * eb + (n + 2) * 4)
+            return H, Ids, [r * stride for r in range(G)]
+        # exact: the sizes are the headers' offsets[n] (one small D2H on a device path)
+        tot = [int(x) for x in H[:, n].to(torch.int64).cpu().tolist()]
+        bases = [0] * G
+        for r in range(1, G):
+            bases[r] = bases[r - 1] + tot[r - 1]
+        Ids = torch.empty(max(1, bases[-1] + tot[-1]), dtype=ids.dtype, device=ids.device)
+        me = self.rank
+        if tot[me]:
+            Ids[bases[me]:bases[me] + tot[me]].copy_(ids[:tot[me]])
+        ops = []
+        for q in range(G):
+            if q == me:
+                continue
+            peer = dist.get_global_rank(self.group, q) if self.group is not None else q
+            if tot[me]:
+                ops.append(dist.P2POp(dist.isend, ids[:tot[me]], peer, self.group))
+            if tot[q]:
+                ops.append(dist.P2POp(dist.irecv, Ids[bases[q]:bases[q] + tot[q]], peer, self.group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        self.wire_bytes = sum(tot[q] for q in range(G) if q != me) * eb + (G - 1) * (n + 2) * 4
+        return H, Ids, bases
+
+    # ---- host path (gloo or nccl)
+    def match(self, t_bytes, t_off, exchange: str | None = None):
+        """Match the whole batch on every rank.  padded / exact: the merged (off[n+1] u32,
+        ids u64, status i32[n]) on every rank; local: this rank's own shard lists in the same
+        form (the union over ranks is the result)."""
+        import torch
+        import torch.distributed as dist
+        exchange = exchange or self.exchange
+        roff, ids, st = self.shard.match_ids(t_bytes, t_off)
+        n = len(roff) - 1
+        if exchange == "local":
+            self.wire_bytes = 0
+            return roff, ids, st
         dev = torch.device("cpu")
-        if dist.get_backend(self.group) != "gloo":
+        if self.world > 1 and dist.get_backend(self.group) != "gloo":
             dev = torch.device("cuda", torch.cuda.current_device())
-        c = torch.from_numpy(cnt.view(np.int32).copy()).to(dev)
-        C = torch.empty(self.world * n, dtype=torch.int32, device=dev)  # flat: gloo and RCCL alike
-        dist.all_gather_into_tensor(C, c, group=self.group)
-        C = C.view(self.world, n)
-        totals = C.to(torch.int64).sum(1)
-        maxT = max(int(totals.max().item()), 1)
-        mine = torch.zeros(maxT, dtype=torch.int64, device=dev)
-        if len(ids):
-            mine[:len(ids)] = torch.from_numpy(ids.view(np.int64)).to(dev)
-        Ids = torch.empty(self.world * maxT, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(Ids, mine, group=self.group)
-        Ids = Ids.view(self.world, maxT)
-        off, merged = N.merge_shards(C.cpu().numpy().view(np.uint32), Ids.cpu().numpy().view(np.uint64))
+        hdr = torch.from_numpy(np.concatenate([roff, np.zeros(1, np.uint32)]).view(np.int32)).to(dev)
+        total = int(roff[-1])
+        if exchange == "padded":
+            # without prepare_device the host path pads to the largest rank's total
+            t = torch.tensor([total], dtype=torch.int64, device=dev)
+            if self.world > 1:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            buf = np.zeros(max(1, int(t.item())), np.uint64)
+        else:
+            buf = np.zeros(max(1, total), np.uint64)
+        buf[:total] = ids
+        H, Ids, bases = self._exchange(hdr, torch.from_numpy(buf.view(np.int64)).to(dev), n, exchange)
+        off, merged = merge_shard_ids_host(H.cpu().numpy(), Ids.cpu().numpy().view(np.uint64), bases, n)
         return off, merged, st
 
     # ---- device path (RCCL over xGMI)
     def prepare_device(self, eng: "N.Engine", d_bytes: int, d_off: int, n: int, total_bytes: int,
                        headroom: float = 1.25):
-        """Size this rank's output arena and the exchange stride from one synchronous run of
-        the batch (collective when world > 1).  Not part of the step: the step itself never
-        waits on the host; a later batch that outgrows these sizes is flagged on the device
-        (match_device's third result) and re-run by the caller after prepare_device."""
+        """Size this rank's buffers and the exchange stride from one synchronous run of the
+        batch (collective when world > 1), and pick the id width every rank can use.  Not part
+        of the step: the step itself never waits on the host (padded); a later batch that
+        outgrows these sizes is flagged on the device (match_device's flags) and re-run by
+        the caller after prepare_device."""
         import torch
         import torch.distributed as dist
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -144,54 +236,67 @@ class ShardedIndex:
         r = eng.match_device(d_bytes, d_off, n, total_bytes, 0)
         eng.device_sync()  # also sizes the chunk pools to this batch's demand
         total = _read_u64(r.d_total)
-        eng.reserve_matches(int(total * headroom) + 1024)
-        t = torch.tensor([total], dtype=torch.int64, device=dev)
+        idb = 4
+        probe = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        try:  # u32 ids unless this shard holds an id past 32 bits
+            eng.match_ids_device(d_bytes, d_off, n, total_bytes, 4, 0, 0, probe.data_ptr(), 0, 0)
+        except N.TMError as e:
+            if e.rc != N.TM_ESTATE:
+                raise
+            idb = 8
+        torch.cuda.synchronize()
+        t = torch.tensor([total, idb], dtype=torch.int64, device=dev)
         if self.world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        self.stride = int(int(t.item()) * headroom) + 1024
+        self.id_bytes = int(t[1].item())
+        eng.reserve_matches((int(total * headroom) + 1024) * (self.id_bytes // 4))
+        self.stride = int(int(t[0].item()) * headroom) + 1024
         return total
 
+    def id_dtype(self):
+        import torch
+        return torch.int32 if self.id_bytes == 4 else torch.int64
+
     def local_device(self, eng: "N.Engine", d_bytes: int, d_off: int, n: int, total_bytes: int, sp: int):
-        """This rank's half of the step, queued on stream `sp` with no host sync: the walk,
-        then the route ids compacted topic-major (tm_result_ids_device_ex).  Returns
-        (cnt_ext i32[n+1]: per-topic counts + the TM_RES_* overflow flags, ids i64[stride])."""
+        """This rank's half of the step, queued on stream `sp` with no host sync: the walk with
+        the route ids written by its copy-out and compacted topic-major (tm_match_ids_device).
+        Returns (hdr i32[n+2]: topic-major offsets + the TM_RES_* flags, ids[stride])."""
         import torch
         dev = torch.device("cuda", torch.cuda.current_device())
-        eng.match_device(d_bytes, d_off, n, total_bytes, sp)
-        lo = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        ids = torch.empty(self.stride, dtype=torch.int64, device=dev)
-        cnt_ext = torch.empty(n + 1, dtype=torch.int32, device=dev)
-        eng.result_ids_device_ex(ids.data_ptr(), self.stride, lo.data_ptr(), cnt_ext[n:].data_ptr(), sp)
-        torch.sub(lo[1:], lo[:-1], out=cnt_ext[:n])
-        return cnt_ext, ids
+        hdr = torch.empty(n + 2, dtype=torch.int32, device=dev)
+        ids = torch.empty(self.stride, dtype=self.id_dtype(), device=dev)
+        eng.match_ids_device(d_bytes, d_off, n, total_bytes, self.id_bytes, ids.data_ptr(), self.stride,
+                             hdr.data_ptr(), hdr[n + 1:].data_ptr(), sp)
+        return hdr, ids
 
-    def merge_device(self, eng: "N.Engine", C_ext, Ids, G: int, n: int, sp: int):
-        """Concatenate G shards' slices per topic on the device.  C_ext: (G, n+1) i32 (counts
-        + flags rows), Ids: (G * stride) i64.  Returns (off i32[n+1], ids i64 buffer whose first
+    def merge_device(self, eng: "N.Engine", H, Ids, bases, n: int, sp: int):
+        """Concatenate the G shards' slices per topic on the device.  H: (G, n+2) i32 headers,
+        rank r's ids at Ids[bases[r]:].  Returns (off i32[n+1], ids i64 buffer whose first
         off[n] entries are the result, flags i32[1]: nonzero if any shard overflowed)."""
         import torch
         dev = torch.device("cuda", torch.cuda.current_device())
-        C = C_ext[:, :n].contiguous()
-        flags = C_ext[:, n].max().reshape(1)
+        G = H.shape[0]
+        flags = H[:, n + 1].max().reshape(1)
         out_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
         cap = G * self.stride
         out_ids = torch.empty(cap, dtype=torch.int64, device=dev)
-        eng.merge_shards_device(G, n, C.data_ptr(), Ids.data_ptr(), self.stride, out_off.data_ptr(),
-                                out_ids.data_ptr(), cap, sp)
+        eng.merge_shard_ids_device(G, n, H.data_ptr(), n + 2, Ids.data_ptr(), self.id_bytes, bases,
+                                   out_off.data_ptr(), out_ids.data_ptr(), cap, sp)
         return out_off, out_ids, flags
 
-    def match_device(self, eng: "N.Engine", d_bytes: int, d_off: int, n: int, total_bytes: int):
-        """GPU step: local walk, ids compacted on device, RCCL all-gathers of the counts and of
-        the ids (padded to the stride prepare_device fixed), device merge.  Nothing in it
-        waits on the host.  The engine calls and the torch ops between them run on ONE torch
-        stream (the engine's own stream is non-blocking, so torch's legacy default stream
-        would not order after it); the caller's current stream waits for it before this
-        returns.  Returns device tensors (off i32[n+1], ids i64 buffer holding off[n] u64
-        route ids, flags i32[1]); flags != 0 means a shard outgrew its sizes: call
-        prepare_device again and re-run the batch."""
+    def match_device(self, eng: "N.Engine", d_bytes: int, d_off: int, n: int, total_bytes: int,
+                     exchange: str | None = None):
+        """GPU step: the walk writes route ids, compacted topic-major; the exchange; the device
+        merge.  The engine calls and the torch ops between them run on ONE torch stream (the
+        engine's own stream is non-blocking, so torch's legacy default stream would not order
+        after it); the caller's current stream waits for it before this returns.
+        padded / exact: device tensors (off i32[n+1], ids i64 buffer holding off[n] u64 route
+        ids, flags i32[1]); flags != 0 means a shard outgrew its sizes: call prepare_device
+        again and re-run the batch.  local: this rank's own lists on the host (pinned):
+        (offsets i32[n+1], ids, flags)."""
         import torch
-        import torch.distributed as dist
-        if getattr(self, "stride", None) is None:
+        exchange = exchange or self.exchange
+        if self.stride is None:
             self.prepare_device(eng, d_bytes, d_off, n, total_bytes)
         dev = torch.device("cuda", torch.cuda.current_device())
         caller = torch.cuda.current_stream()
@@ -201,15 +306,23 @@ class ShardedIndex:
         s.wait_stream(caller)  # the topic batch was written on the caller's stream
         sp = s.cuda_stream
         with torch.cuda.stream(s):
-            cnt_ext, ids = self.local_device(eng, d_bytes, d_off, n, total_bytes, sp)
-            if self.world > 1:
-                C = torch.empty(self.world * (n + 1), dtype=torch.int32, device=dev)
-                dist.all_gather_into_tensor(C, cnt_ext, group=self.group)
-                Ids = torch.empty(self.world * self.stride, dtype=torch.int64, device=dev)
-                dist.all_gather_into_tensor(Ids, ids, group=self.group)
-            else:  # one shard: the exchange is the identity
-                C, Ids = cnt_ext, ids
-            out = self.merge_device(eng, C.view(self.world, n + 1), Ids, self.world, n, sp)
+            hdr, ids = self.local_device(eng, d_bytes, d_off, n, total_bytes, sp)
+            if exchange == "local":
+                if getattr(self, "_h_hdr", None) is None or self._h_hdr.numel() < n + 2:
+                    self._h_hdr = torch.empty(n + 2, dtype=torch.int32, pin_memory=True)
+                if getattr(self, "_h_ids", None) is None or self._h_ids.numel() < self.stride \
+                        or self._h_ids.dtype != ids.dtype:
+                    self._h_ids = torch.empty(self.stride, dtype=ids.dtype, pin_memory=True)
+                h_hdr = self._h_hdr[:n + 2]
+                h_hdr.copy_(hdr, non_blocking=True)
+                s.synchronize()  # the shard's size, for an exact copy of its ids
+                total = min(int(h_hdr[n].item()), self.stride)
+                self._h_ids[:total].copy_(ids[:total], non_blocking=True)
+                s.synchronize()
+                self.wire_bytes = 0
+                return h_hdr[:n + 1], self._h_ids[:total], h_hdr[n + 1:]
+            H, Ids, bases = self._exchange(hdr, ids, n, exchange)
+            out = self.merge_device(eng, H, Ids, bases, n, sp)
         caller.wait_stream(s)
         for t in out:
             t.record_stream(caller)  # consumed on the caller's stream from here on

@@ -71,7 +71,7 @@
 extern "C" {
 #endif
 
-#define TM_ABI_VERSION 6u
+#define TM_ABI_VERSION 7u
 
 /* status codes */
 #define TM_OK          0
@@ -310,6 +310,29 @@ int tm_result_ids_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint
 int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off, uint32_t *d_flags,
                             void *stream);
 
+/* The walk with the route ids written by the walk itself (the key -> id gather of
+ * emqx_router:match_to_route/1, apps/emqx/src/emqx_router.erl:648-649, fused into the
+ * copy-out; get_id/1, emqx_topic_index.erl:87-89, of every key), then compacted topic-major
+ * on the device: topic i's ids are d_ids[d_off[i] .. d_off[i+1]) (d_off: n+1 entries,
+ * d_off[n] = the batch's id count), ids of id_bytes each: 8 (u64), or 4 (u32: TM_ESTATE
+ * unless every id the engine ever held is below 2^32).  d_flags (may be NULL): one u32 of
+ * TM_RES_* bits written on the device (TM_RES_KEYS_OVERFLOW: the walk's own buffer was short,
+ * call tm_reserve_matches and run again; TM_RES_IDS_OVERFLOW: d_off[n] > ids_cap).  Works on
+ * replicas.  Asynchronous on `stream`; nothing waits on the host. */
+int tm_match_ids_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                        uint64_t total_bytes, uint32_t id_bytes, void *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
+                        uint32_t *d_flags, void *stream);
+
+/* Filter-sharded merge over tm_match_ids_device results: rank r's d_off_out row (n+1 u32) at
+ * d_roff + r * roff_stride, its ids (id_bytes each) at d_ids + base[r] elements (base: G
+ * host values).  Writes the merged result as u64: topic i's ids are the concatenation of its
+ * slices from shard 0..G-1 at d_out_ids[d_out_off[i] .. d_out_off[i+1]) (n+1 offsets).  One
+ * column-sum launch and one output-parallel copy; topics past out_cap are left unwritten.
+ * G <= 64. */
+int tm_merge_shard_ids_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_t *d_roff, uint64_t roff_stride,
+                              const void *d_ids, uint32_t id_bytes, const uint64_t *base, uint32_t *d_out_off,
+                              uint64_t *d_out_ids, uint64_t out_cap, void *stream);
+
 /* Filter-sharded mode: G shards matched the same n topics against disjoint
  * key sets; shard r's compacted result (tm_result_ids_device) is counts[r*n .. r*n+n) and
  * ids[r*stride ..).  Writes the merged result: topic i's ids are the concatenation of its
@@ -397,6 +420,11 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out);
  * three phases summed over the waves holding a topic with more than 256 keys
  * (under a hot '#' filter), and the number of such waves}. */
 int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out18);
+/* diagnostics: the same counters by walk depth d (16 rows, the last = depth 15 and deeper),
+ * read WITHOUT resetting (call before tm_debug_stats' read): out64[d] edge-slot probes,
+ * out64[16 + d] summed wave cycles spent at depth d, out64[32 + d] frontier entries
+ * expanded, out64[48 + d] dependent probe round trips (per wave). */
+int tm_debug_depth_stats(tm_engine *eng, uint64_t *out64);
 /* diagnostics: time the dominant kernel of the next match with HIP events on its
  * launch stream; enable=1 arms, then (after the match) enable=0 + ms_out reads. */
 int tm_debug_timing(tm_engine *eng, int enable, float *ms_out);

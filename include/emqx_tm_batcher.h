@@ -10,8 +10,8 @@
  *
  *   window   a batch is dispatched when max_batch publishes are queued, or when the
  *            oldest queued publish has waited max_wait_us, or at tm_batcher_destroy
- *            (which drains the queue).  Four windows are in flight at once: window k+3
- *            walks on the GPU while earlier windows' ids cross PCIe and window k's
+ *            (which drains the queue).  Six windows are in flight at once: the newest
+ *            walks on the GPU while earlier windows' ids cross PCIe and the oldest's
  *            publishers are called back; under load windows grow by themselves.
  *   result   per publish: TM_TOPIC_OK with the ids of its matched keys (route dests,
  *            emqx_topic_index:get_id/1 of every key, emqx_topic_index.erl:87-89), or

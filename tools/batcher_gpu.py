@@ -1,6 +1,7 @@
 """Batcher sweep on one GPU (bench tooling): config C engine, closed-loop publishers through
-tm_batcher_submit for each (publishers, delivery threads, max_wait_us) given, one JSON line
-each.  Usage: python tools/batcher_gpu.py P:T:W [P:T:W ...]"""
+tm_batcher_submit for each (publishers, delivery threads, max_wait_us[, transport, spans callback,
+slots, max_batch]) given, one JSON line each.
+Usage: python tools/batcher_gpu.py P:T:W[:TR:SP:NSLOT:MB] ...   (TR 0 auto/runs, 1 ids; SP 1 = span callback)"""
 import ctypes as C
 import json
 import os
@@ -25,9 +26,9 @@ def main():
     tb = np.ascontiguousarray(w.t_bytes, dtype=np.uint8)
     to32 = np.ascontiguousarray(w.t_off, dtype=np.uint32)
     lg = C.CDLL(os.path.join(ROOT, "tools", "libtm_loadgen.so"))
-    lg.loadgen_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double,
-                               C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
-                               C.POINTER(C.c_double)]
+    lg.loadgen_run2.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double, C.c_int,
+                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
     if os.environ.get("HOSTPATH"):  # tm_match_batch with host buffers, 1 M publishes per call
         eng.match_packed_view(tb, to32)
         ts = []
@@ -39,14 +40,17 @@ def main():
                           "publishes_per_s": round(len(to32) / 1 / min(ts) if False else (len(to32) - 1) / float(np.median(ts)))}),
               flush=True)
     for spec in sys.argv[1:]:
-        pubs, th, wait = (int(x) for x in spec.split(":"))
-        b = N.Batcher(eng, max_batch=65536, max_wait_us=wait, delivery_threads=th)
-        got, ids, errs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
-        rc = lg.loadgen_run(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, 2.0, C.byref(got),
-                            C.byref(ids), C.byref(errs), C.byref(el))
+        v = [int(x) for x in spec.split(":")] + [0, 0, 4, 65536][len(spec.split(":")) - 3:]
+        pubs, th, wait, tr, sp, nslot, mb = v[:7]
+        os.environ["EMQX_TM_NSLOT"] = str(nslot)
+        b = N.Batcher(eng, max_batch=mb, max_wait_us=wait, delivery_threads=th, transport=tr)
+        got, ids, errs, cs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
+        rc = lg.loadgen_run2(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, 2.0, sp, C.byref(got),
+                             C.byref(ids), C.byref(errs), C.byref(cs), C.byref(el))
         st = b.stats()
         b.close()
-        print(json.dumps({"publishers": pubs, "threads": th, "max_wait_us": wait, "rc": rc, "errors": errs.value,
+        print(json.dumps({"publishers": pubs, "threads": th, "max_wait_us": wait, "transport": tr, "spans": sp,
+                          "nslot": nslot, "max_batch": mb, "rc": rc, "errors": errs.value,
                           "publishes_per_s": round(got.value / el.value), "ids_per_publish": round(ids.value / max(got.value, 1), 1),
                           "mean_batch": round(st["publishes"] / max(st["batches"], 1), 1),
                           "p50_ms": round(st["lat_p50_us"] / 1e3, 3), "p99_ms": round(st["lat_p99_us"] / 1e3, 3),

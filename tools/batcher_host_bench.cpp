@@ -57,9 +57,12 @@ int main(int argc, char **argv) {
     tm_batcher_stats st{};
     tm_batcher_stats_get(b, &st);
     tm_batcher_destroy(b);
+    // delivery cost per publish: the delivery threads' busy time (deliver_us is per thread)
+    const double del_ns = (double)st.deliver_us * 1e3 * threads / (double)(got ? got : 1);
     printf("{\"publishers\": %u, \"ids_per_publish\": %u, \"threads\": %u, \"publishes_per_s\": %.0f, "
-           "\"mean_batch\": %.1f, \"p50_ms\": %.3f, \"p99_ms\": %.3f, \"errors\": %lu}\n",
+           "\"mean_batch\": %.1f, \"p50_ms\": %.3f, \"p99_ms\": %.3f, \"errors\": %lu, \"deliver_ns_per_publish\": %.1f, "
+           "\"cut_ns_per_publish\": %.1f}\n",
            P, K, threads, got / el, st.batches ? (double)st.publishes / st.batches : 0.0, st.lat_p50_us / 1e3,
-           st.lat_p99_us / 1e3, (unsigned long)errs);
+           st.lat_p99_us / 1e3, (unsigned long)errs, del_ns, (double)st.cut_us * 1e3 / (double)(got ? got : 1));
     return 0;
 }

@@ -4,7 +4,8 @@
 // table).  Their ceiling is not the streaming HBM bandwidth but the rate at which the
 // memory system serves random 16-B requests that miss the caches.  This measures it with
 // no dependence between loads: every lane keeps U loads in flight, tables of 2 MiB (L2-
-// resident) to 4 GiB (the config-C edge table is 8 GiB), 16 waves per CU.
+// resident) to 32 GiB (round 3: the config-C edge table is 16 GiB at load 1/16), 16 waves
+// per CU.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 tools/gather_roof.hip -o tools/gather_roof
 #include <hip/hip_runtime.h>
@@ -54,12 +55,13 @@ static void run(const uint4 *tab, unsigned long long bytes, unsigned *out) {
 }
 
 int main() {
-    const unsigned long long maxb = 4ull << 30;
+    const unsigned long long maxb = 32ull << 30;
     uint4 *tab;
     unsigned *out;
     if (hipMalloc(&tab, maxb) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
     hipMemset(tab, 1, maxb);
-    for (unsigned long long b : {2ull << 20, 16ull << 20, 64ull << 20, 256ull << 20, 1ull << 30, 4ull << 30}) {
+    for (unsigned long long b : {2ull << 20, 16ull << 20, 64ull << 20, 256ull << 20, 1ull << 30, 4ull << 30, 8ull << 30,
+                                 16ull << 30, 32ull << 30}) {
         run<1>(tab, b, out);
         run<4>(tab, b, out);
         run<8>(tab, b, out);
