@@ -103,6 +103,7 @@ class tm_intersect_result(C.Structure):
 
 
 TM_INTERSECT_FALSE, TM_INTERSECT_BADHASH = -1, -2
+TM_MATCH_TOPIC_WORDS = 0x100  # OR'd into a tm_match_batch mode: '/'-joined word-list topics
 
 
 class tm_dev_result(C.Structure):
@@ -207,7 +208,8 @@ def load() -> C.CDLL:
     lib.tm_match_ids_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
                                         C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.tm_merge_shard_ids_device.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p,
-                                              C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+                                              C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64,
+                                              C.c_void_p]
     lib.tm_image_size.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.tm_image_export.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
     lib.tm_replica_create.argtypes = [P(tm_config), C.c_void_p, C.c_uint64, C.c_void_p, P(C.c_void_p)]
@@ -555,6 +557,20 @@ class Engine:
                 out.append(k[o[i]:o[i] + c[i]].tolist())
         return out
 
+    def match_words(self, word_lists, mode: int = TM_MATCH_ALL):
+        """matches/3 with pre-split topics (TM_MATCH_TOPIC_WORDS): each topic a non-empty list of
+        byte words (no '/' inside a word); list of key-handle lists.  A "+" or "#" word is a
+        plain word here, and keys given as binaries never match (match_topics/4)."""
+        topics = []
+        for ws in word_lists:
+            bs = [w.encode() if isinstance(w, str) else bytes(w) for w in ws]
+            if not bs or any(b"/" in b for b in bs):
+                raise ValueError(f"word list {ws!r} has no '/'-joined form")
+            topics.append(b"/".join(bs))
+        buf, off = pack_topics(topics)
+        o, c, k, st = self.match_packed(buf, off, mode | TM_MATCH_TOPIC_WORDS)
+        return [k[o[i]:o[i] + c[i]].tolist() for i in range(len(topics))]
+
     def key_info(self, key: int):
         ident = C.c_uint64()
         flags = C.c_uint32()
@@ -629,13 +645,15 @@ class Engine:
                                                  C.c_void_p(stream) if stream else None))
 
     def merge_shard_ids_device(self, G: int, n: int, d_roff: int, roff_stride: int, d_ids: int, id_bytes: int,
-                               bases, d_out_off: int, d_out_ids: int, out_cap: int, stream: int = 0):
+                               bases, max_rank_ids: int, d_out_off: int, d_out_ids: int, out_cap: int,
+                               stream: int = 0):
         """tm_merge_shard_ids_device: rank r's offsets row at d_roff + r*roff_stride (u32), its ids
-        at d_ids + bases[r] elements of id_bytes; merged u64 ids + n+1 offsets out."""
+        at d_ids + bases[r] elements of id_bytes (at most max_rank_ids of them); merged u64 ids +
+        n+1 offsets out."""
         b = (C.c_uint64 * G)(*[int(x) for x in bases])
         self._check(self.lib.tm_merge_shard_ids_device(self.h, G, n, C.c_void_p(d_roff), roff_stride,
-                                                       C.c_void_p(d_ids), id_bytes, b, C.c_void_p(d_out_off),
-                                                       C.c_void_p(d_out_ids), out_cap,
+                                                       C.c_void_p(d_ids), id_bytes, b, max_rank_ids,
+                                                       C.c_void_p(d_out_off), C.c_void_p(d_out_ids), out_cap,
                                                        C.c_void_p(stream) if stream else None))
 
     def merge_shards_device(self, G: int, n: int, d_counts: int, d_ids: int, stride: int, d_out_off: int,

@@ -145,9 +145,16 @@ struct HBuf {
     ~HBuf() { drop(); }
 };
 
-#define BT_HIP(E)                                 \
-    do {                                          \
-        if ((E) != hipSuccess) return TM_EDEVICE; \
+// the HIP call that failed last on this thread (reported with the window's failure)
+thread_local char bt_err[160];
+#define BT_HIP(E)                                                                                  \
+    do {                                                                                           \
+        const hipError_t bt_e_ = (E);                                                              \
+        if (bt_e_ != hipSuccess) {                                                                 \
+            std::snprintf(bt_err, sizeof bt_err, "%s at batcher.cpp:%d", hipGetErrorString(bt_e_), \
+                          __LINE__);                                                               \
+            return TM_EDEVICE;                                                                     \
+        }                                                                                          \
     } while (0)
 
 struct Pending {
@@ -244,8 +251,8 @@ struct tm_batcher {
     std::atomic<bool> reported{false};  // the first failed window is reported on stderr (once)
     void report(const char *stage, int rc) {
         if (rc >= 0 || reported.exchange(true)) return;
-        std::fprintf(stderr, "tm_batcher: a window failed in %s: rc %d (%s)\n", stage, rc,
-                     eng ? tm_last_error(eng) : "custom backend");
+        std::fprintf(stderr, "tm_batcher: a window failed in %s: rc %d (%s%s%s)\n", stage, rc,
+                     eng ? tm_last_error(eng) : "custom backend", bt_err[0] ? "; " : "", bt_err);
     }
     bool runs_ok = false;        // runs transport in use (TM_MATCH_ALL windows of a master engine)
     hipStream_t s_comp = nullptr, s_copy = nullptr;
@@ -571,7 +578,11 @@ struct tm_batcher {
                 if (S.mode == TM_MATCH_ALL) S.ids_cap = std::max(S.ids_cap, want);
                 if ((rc = enqueue(S))) return rc;
                 BT_HIP(hipEventSynchronize(S.ev));
-                if (S.h_ctl.as<uint64_t>()[0] > S.keys_cap) return TM_EDEVICE;
+                if (S.h_ctl.as<uint64_t>()[0] > S.keys_cap) {
+                    std::snprintf(bt_err, sizeof bt_err, "re-run still past its output (%llu > %llu ids)",
+                                  (unsigned long long)S.h_ctl.as<uint64_t>()[0], (unsigned long long)S.keys_cap);
+                    return TM_EDEVICE;
+                }
             }
         }
         S.v.status = S.h_status.as<int32_t>();

@@ -37,7 +37,8 @@ struct MatchArgs {
     uint32_t tpw;         // topics per wave of k_match_fast (pick_tpw)
     uint32_t first_dfs;   // MODE_FIRST: 1 = lane-per-topic DFS (index holds keys deeper than the
                           // 31-level order code), 0 = k_match_first_wave + k_first_slow
-    uint32_t _pad0;
+    uint32_t topic_words; // 1: topics are '/'-joined word lists (matches/3's [word()] form): a
+                          // "+" or "#" level is a literal word, not badarg (emqx_trie_search.erl:369-370)
     // frozen index
     const WordSlot *wtab;
     uint64_t wmask;
@@ -69,6 +70,10 @@ struct MatchArgs {
     uint32_t *slow_count;
     uint32_t *scratch_w;  // (total bytes + 2n + 2) u32: word ids, at off[t]-off[0] + 2t
     uint64_t *scratch_s;  // (total bytes + 2n + 2) u64: DFS stack, same indexing
+    // MODE_IDS*: per wave {output base, ids, 1 if a topic of the wave spilled, 0}: a wave's
+    // topics are contiguous and in order in its output range, so the topic-major compaction
+    // moves whole wave blocks (launch_compact_waves)
+    uint4 *wave_info;
     // segment chunk pool (wave LDS overflow): seg_chunks chunks of SEG_CHUNK uint4
     uint4 *seg_pool;
     uint64_t seg_chunks;
@@ -134,13 +139,22 @@ hipError_t launch_result_ids32(const uint32_t *cnt, const uint32_t *src_off, con
 hipError_t launch_compact_ids(uint32_t id_bytes, const uint32_t *src_off, const void *src, const uint32_t *dst_off,
                               uint32_t n, void *ids, uint64_t cap, uint64_t src_cap, const unsigned long long *cursor,
                               uint32_t *flags, hipStream_t stream);
+// MODE_IDS* compaction by wave blocks: wave w's ids src[info.x .. + info.y) go to
+// dst[dst_off[w * tpw] ..) whole; a wave with a spilled topic copies topic by topic
+// (src_off / cnt: the walk's per-topic arrays).  Nothing is written when the walk overflowed
+// (cursor > src_cap); ids past cap are dropped (flags report both, as launch_compact_ids).
+hipError_t launch_compact_waves(uint32_t id_bytes, const uint4 *wave_info, uint32_t nwaves, uint32_t tpw, uint32_t n,
+                                const uint32_t *src_off, const uint32_t *cnt, const void *src, const uint32_t *dst_off,
+                                void *dst, uint64_t cap, uint64_t src_cap, const unsigned long long *cursor,
+                                uint32_t *flags, hipStream_t stream);
 // Concatenate G shards' topic-major compacted ids per topic (tm_merge_shard_ids_device):
 // roff G rows (stride roff_stride) of n+1 per-rank exclusive scans, rank r's ids (id_bytes
 // each) at ids + base[r] elements; off: n+1 merged scan out; out: merged u64 ids.
 constexpr uint32_t MERGE_MAX_G = 64;
+// max_total bounds every rank's id count (its chunks are launched from it; surplus blocks exit).
 hipError_t launch_merge_shard_ids(uint32_t G, uint32_t n, const uint32_t *roff, uint64_t roff_stride, const void *ids,
                                   uint32_t id_bytes, const uint64_t *base, uint32_t *off, uint64_t *out, uint64_t cap,
-                                  hipStream_t stream);
+                                  uint32_t max_total, hipStream_t stream);
 // Concatenate G shards' topic-major results per topic.  roff: G*(n+1) u32, tot: n u32,
 // scratch: scan_scratch_words(n) u32 (work areas); off: n+1 u32 out; out: merged ids.
 hipError_t launch_merge_shards(uint32_t G, uint32_t n, const uint32_t *counts, const uint64_t *ids, uint64_t stride,

@@ -122,6 +122,8 @@ struct BatchBufs {
     DevBuf d_ukeys, d_ucnt;     // UNIQUE / AGGRE: reducer scratch at the result's offsets; reduced counts
     DevBuf d_dd_wl, d_dd_wl_n;  // k_dd_pass -> k_dedupe worklist
     DevBuf d_kcnt, d_rcur;      // runs: ids per topic; the batch's span cursor (shared by its sub-batches)
+    DevBuf d_wave_info;         // ids modes: per wave {base, ids, spilled} (MatchArgs.wave_info)
+    DevBuf d_res_scan;          // scan scratch of the set's result passes (one per set: sets run concurrently)
     // A launch's counters live in one 32-B block {cursor u64, slow_count u32 (+pad),
     // seg_cursor u64, fr_cursor u64}.  Two blocks alternate: each launch zeroes the block
     // the NEXT launch will use, so no memset launches precede a batch.
@@ -137,7 +139,7 @@ struct BatchBufs {
     void release() {
         for (DevBuf *b : {&d_bytes, &d_off, &d_outoff, &d_outcnt, &d_status, &d_keys, &d_slow_list, &d_scr_w, &d_scr_s,
                           &d_seg_pool, &d_fr_pool, &d_wave_chunks, &d_ukeys, &d_ucnt, &d_dd_wl, &d_dd_wl_n, &d_kcnt,
-                          &d_rcur, &d_ctl})
+                          &d_rcur, &d_ctl, &d_wave_info, &d_res_scan})
             b->release();
     }
 };
@@ -516,7 +518,7 @@ struct tm_engine {
     DevBuf d_key_dd;                  // key handle -> KDD_* flags (u8; which keys k_dedupe must table)
     std::vector<uint64_t> dirty_kid;  // handles (re)assigned since the last upload
     uint64_t n_deep = 0;              // live word-list keys too deep for the 64-bit order code
-    DevBuf d_res_scan, d_mrg_roff, d_mrg_tot;  // scratch of tm_result_ids_device / tm_merge_shards_device
+    DevBuf d_mrg_roff, d_mrg_tot;  // scratch of tm_merge_shards_device
     DevBuf d_stats;
     // Batch buffers: one set for the device-result calls (tm_match_device*, whose result the
     // engine keeps until the next such call) and one for the host-result calls (tm_match_batch*,
@@ -550,6 +552,7 @@ struct tm_engine {
     uint64_t dev_used[A_N] = {};  // bytes of each device array in use (image export)
     hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // around k_match_fast (tm_debug_timing)
     bool timing_on = false;
+    bool topic_words = false;  // the batch being enqueued holds word-list topics (TM_MATCH_TOPIC_WORDS)
     // pipelined tm_match_batch: a copy stream, per-half events, the counter blocks' landing
     // place, and the last such batch's keys per topic (sizes the next one's buffers)
     hipStream_t s_pipe = nullptr;
@@ -2007,7 +2010,7 @@ void tm_destroy(tm_engine *eng) {
     eng->bb_host.release();
     eng->bb_batch.release();
     eng->h_rctl.release();
-    for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_res_scan, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
+    for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
                       &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan, &eng->fx.d_pool,
                       &eng->fx.d_ctl, &eng->fx.d_jobs, &eng->fx.d_krec, &eng->d_ia, &eng->d_iaoff,
@@ -2221,6 +2224,7 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.first_dfs = eng->dv.n_deep ? 1u : 0u;
     a.key_bin = eng->d_key_bin.as<uint32_t>();
     a.key_rec = eng->d_key_rec.as<uint64_t>();
+    a.topic_words = eng->topic_words ? 1u : 0u;
     a.bytes = d_bytes;
     a.off = d_off;
     a.n = n;
@@ -2262,6 +2266,7 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.seg_chunks = eng->bb->seg_chunks;
     a.seg_cursor = (unsigned long long *)(eng->bb->p_ctl + CTL_SEG);
     a.wave_chunks = eng->bb->d_wave_chunks.as<uint32_t>();
+    a.wave_info = eng->bb->d_wave_info.as<uint4>();
     a.fr_pool = eng->bb->d_fr_pool.as<uint2>();
     a.fr_chunks = eng->bb->fr_chunks;
     a.fr_cursor = (unsigned long long *)(eng->bb->p_ctl + CTL_FR);
@@ -2437,8 +2442,8 @@ static int match_batch_pipelined(tm_engine *eng, HostOut &o, const uint8_t *byte
     return TM_OK;
 }
 
-int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
-                   tm_result *out) {
+static int match_batch_impl(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
+                            tm_result *out) {
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
     if (mode > TM_MATCH_AGGRE) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
@@ -2595,6 +2600,83 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, ui
     return TM_OK;
 }
 
+// matches/3 with a pre-split topic `[word()]` (emqx_trie_search.erl:182, topic_words/1 :369-370):
+// the words come '/'-joined.  The walk is the same as for a binary topic except that a "+" or
+// "#" level is a plain word (no badarg: topic_words/1 checks nothing for a list), and the
+// final match_topics/4 step (:380-389) compares the LIST with the keys, so a key given as a
+// binary ({Binary, {ID}}, K_EXACT_BIN) never matches: those are dropped here, on the host,
+// which knows every key's form.  FIRST needs no filtering beyond that (binary keys sort after
+// every list: a binary first key means no list key matched); COUNT and UNIQUE are taken from
+// the filtered full result.
+static int match_words_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
+                             tm_result *out) {
+    if (mode > TM_MATCH_COUNT) {
+        eng->err = "tm_match_batch: TM_MATCH_TOPIC_WORDS supports ALL, UNIQUE, FIRST and COUNT";
+        return TM_EINVAL;
+    }
+    if (eng->replica) return replica_refuses(eng, "tm_match_batch (word-list topics)");
+    std::lock_guard<std::mutex> gh(eng->mu_host);  // key kinds and term order: the host copy
+    std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+    struct Flag {
+        tm_engine *e;
+        ~Flag() { e->topic_words = false; }
+    } reset{eng};
+    eng->topic_words = true;
+    const uint32_t inner = mode == TM_MATCH_FIRST ? TM_MATCH_FIRST : TM_MATCH_ALL;
+    int rc = match_batch_impl(eng, bytes, off, n, inner, out);
+    if (rc || n == 0) return rc;
+    HostOut &o = eng->out();
+    std::vector<uint32_t> noff(n), ncnt(n), nkeys;
+    nkeys.reserve(out->total);
+    std::vector<uint32_t> tmp;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t *ks = out->keys ? out->keys + out->off[i] : nullptr;
+        const uint32_t c = out->status[i] == TM_TOPIC_OK ? out->cnt[i] : 0;
+        noff[i] = (uint32_t)nkeys.size();
+        tmp.clear();
+        for (uint32_t k = 0; k < c; k++)
+            if (eng->keys[ks[k]].kind != K_EXACT_BIN) tmp.push_back(ks[k]);
+        if (mode == TM_MATCH_UNIQUE && tmp.size() > 1) {
+            // matches/3 [unique]: per id the greatest key in term order (match_add/2 overwrites)
+            std::sort(tmp.begin(), tmp.end(), [&](uint32_t a, uint32_t b) { return eng->cmp_keys(a, b) < 0; });
+            std::vector<std::pair<uint64_t, uint32_t>> best;
+            std::unordered_map<uint64_t, size_t> at;
+            for (uint32_t k : tmp) {
+                auto ins = at.emplace(eng->keys[k].id, best.size());
+                if (ins.second) best.push_back({eng->keys[k].id, k});
+                else best[ins.first->second].second = k;
+            }
+            std::sort(best.begin(), best.end());
+            tmp.clear();
+            for (auto &p : best) tmp.push_back(p.second);
+        }
+        ncnt[i] = (uint32_t)tmp.size();
+        if (mode != TM_MATCH_COUNT) nkeys.insert(nkeys.end(), tmp.begin(), tmp.end());
+    }
+    o.pp_off.swap(noff);
+    o.pp_cnt.swap(ncnt);
+    o.pp_keys.swap(nkeys);
+    out->off = o.pp_off.data();
+    out->cnt = o.pp_cnt.data();
+    out->keys = mode == TM_MATCH_COUNT ? nullptr : o.pp_keys.data();
+    out->total = o.pp_keys.size();
+    if (mode == TM_MATCH_COUNT) {
+        std::fill(o.pp_off.begin(), o.pp_off.end(), 0u);
+        out->total = 0;
+    }
+    return TM_OK;
+}
+
+int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
+                   tm_result *out) {
+    if (!eng) return TM_EINVAL;
+    if (mode & TM_MATCH_TOPIC_WORDS) {
+        if (!out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
+        return match_words_batch(eng, bytes, off, n, mode & ~TM_MATCH_TOPIC_WORDS, out);
+    }
+    return match_batch_impl(eng, bytes, off, n, mode, out);
+}
+
 int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap) {
     if (!eng) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
@@ -2700,10 +2782,10 @@ static int result_ids_impl(tm_engine *eng, BatchBufs *set, uint64_t *d_ids, uint
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     hipStream_t s = stream ? (hipStream_t)stream : (eng->bb->last_stream ? eng->bb->last_stream : eng->stream);
     const uint32_t n = eng->bb->last_n;
-    TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_res_scan, scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
     const bool red = reduced_mode(eng->bb->last_mode);
     const uint32_t *cnt = (red ? eng->bb->d_ucnt : eng->bb->d_outcnt).as<uint32_t>();
-    TM_TRY_HIP(launch_excl_scan(cnt, 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s), TM_EDEVICE, "scan");
+    TM_TRY_HIP(launch_excl_scan(cnt, 1, n, d_off_out, eng->bb->d_res_scan.as<uint32_t>(), s), TM_EDEVICE, "scan");
     TM_TRY_HIP(launch_result_ids(cnt, eng->bb->d_outoff.as<uint32_t>(), eng->bb->d_keys.as<uint32_t>(),
                                  eng->d_key_rec.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, eng->bb->keys_cap,
                                  (const unsigned long long *)(eng->bb->p_ctl + CTL_CURSOR), d_flags, s),
@@ -2731,9 +2813,9 @@ __attribute__((visibility("hidden"))) int tmx_result_ids32_device(tm_engine *eng
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     hipStream_t s = stream ? (hipStream_t)stream : (eng->bb->last_stream ? eng->bb->last_stream : eng->stream);
     const uint32_t n = eng->bb->last_n;
-    TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_res_scan, scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
     const uint32_t *cnt = (reduced_mode(eng->bb->last_mode) ? eng->bb->d_ucnt : eng->bb->d_outcnt).as<uint32_t>();
-    TM_TRY_HIP(launch_excl_scan(cnt, 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s), TM_EDEVICE, "scan");
+    TM_TRY_HIP(launch_excl_scan(cnt, 1, n, d_off_out, eng->bb->d_res_scan.as<uint32_t>(), s), TM_EDEVICE, "scan");
     TM_TRY_HIP(launch_result_ids32(cnt, eng->bb->d_outoff.as<uint32_t>(), eng->bb->d_keys.as<uint32_t>(),
                                    eng->d_key_rec.as<uint64_t>(), d_off_out, n, d_ids, ids_cap, eng->bb->keys_cap,
                                    (const unsigned long long *)(eng->bb->p_ctl + CTL_CURSOR), s),
@@ -2764,15 +2846,20 @@ static int match_ids_impl(tm_engine *eng, BatchBufs *set, const uint8_t *d_bytes
     // id as id_bytes needs), then one pass copies them topic-major into the caller's buffer
     const uint64_t cap = eng->bb->keys_cap / (id_bytes / 4);
     const uint32_t kmode = id_bytes == 4 ? MODE_IDS32 : MODE_IDS64;
+    const uint32_t tpw = pick_tpw(n, eng->cfg.topics_per_wave);
+    const uint32_t nwaves = (uint32_t)match_grid(n, tpw);
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_wave_info, (uint64_t)nwaves * 16 + 16), TM_ENOMEM, "alloc");
     TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s, kmode, 0, eng->bb->d_keys.as<uint32_t>(), cap),
                TM_EDEVICE, "kernel launch");
     eng->bb->last_mode = TM_MATCH_ALL;
     eng->bb->dev_batch = false;  // the key buffer holds ids now: no tm_result_ids_device on it
-    TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(launch_excl_scan(eng->bb->d_outcnt.as<uint32_t>(), 1, n, d_off_out, eng->d_res_scan.as<uint32_t>(), s),
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_res_scan, scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(launch_excl_scan(eng->bb->d_outcnt.as<uint32_t>(), 1, n, d_off_out, eng->bb->d_res_scan.as<uint32_t>(), s),
                TM_EDEVICE, "scan");
-    TM_TRY_HIP(launch_compact_ids(id_bytes, eng->bb->d_outoff.as<uint32_t>(), eng->bb->d_keys.p, d_off_out, n, d_ids,
-                                  ids_cap, cap, (const unsigned long long *)(eng->bb->p_ctl + CTL_CURSOR), d_flags, s),
+    TM_TRY_HIP(launch_compact_waves(id_bytes, eng->bb->d_wave_info.as<uint4>(), nwaves, tpw, n,
+                                    eng->bb->d_outoff.as<uint32_t>(), eng->bb->d_outcnt.as<uint32_t>(), eng->bb->d_keys.p,
+                                    d_off_out, d_ids, ids_cap, cap,
+                                    (const unsigned long long *)(eng->bb->p_ctl + CTL_CURSOR), d_flags, s),
                TM_EDEVICE, "compact ids");
     TM_TRY_HIP(eng->note_use(s), TM_EDEVICE, "event");
     if (out) {  // the walk's own per-topic arrays and counter block (library-internal callers)
@@ -2804,15 +2891,16 @@ __attribute__((visibility("hidden"))) int tmx_batch_match_ids(tm_engine *eng, co
 }
 
 int tm_merge_shard_ids_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_t *d_roff, uint64_t roff_stride,
-                              const void *d_ids, uint32_t id_bytes, const uint64_t *base, uint32_t *d_out_off,
-                              uint64_t *d_out_ids, uint64_t out_cap, void *stream) {
+                              const void *d_ids, uint32_t id_bytes, const uint64_t *base, uint64_t max_rank_ids,
+                              uint32_t *d_out_off, uint64_t *d_out_ids, uint64_t out_cap, void *stream) {
     if (!eng || G == 0 || G > MERGE_MAX_G || !d_roff || !base || !d_out_off || roff_stride < (uint64_t)n + 1 ||
-        (id_bytes != 4 && id_bytes != 8) || (out_cap && (!d_out_ids || !d_ids)))
+        (id_bytes != 4 && id_bytes != 8) || (out_cap && (!d_out_ids || !d_ids)) || max_rank_ids > 0xFFFFFFFFull)
         return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
-    TM_TRY_HIP(launch_merge_shard_ids(G, n, d_roff, roff_stride, d_ids, id_bytes, base, d_out_off, d_out_ids, out_cap, s),
+    TM_TRY_HIP(launch_merge_shard_ids(G, n, d_roff, roff_stride, d_ids, id_bytes, base, d_out_off, d_out_ids, out_cap,
+                                      (uint32_t)max_rank_ids, s),
                TM_EDEVICE, "merge");
     return TM_OK;
 }
@@ -2823,11 +2911,12 @@ int tm_merge_shards_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
-    TM_TRY_HIP(eng->d_res_scan.ensure(scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_mrg_roff.ensure((uint64_t)G * (n + 1) * 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->d_mrg_tot.ensure((uint64_t)n * 4 + 4), TM_ENOMEM, "alloc");
+    eng->bb = &eng->bb_dev;  // the device path's set (the sharded step's walk ran on it)
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_res_scan, scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->d_mrg_roff, (uint64_t)G * (n + 1) * 4), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->d_mrg_tot, (uint64_t)n * 4 + 4), TM_ENOMEM, "alloc");
     TM_TRY_HIP(launch_merge_shards(G, n, d_counts, d_ids, stride, eng->d_mrg_roff.as<uint32_t>(),
-                                   eng->d_mrg_tot.as<uint32_t>(), eng->d_res_scan.as<uint32_t>(), d_off_out, d_ids_out,
+                                   eng->d_mrg_tot.as<uint32_t>(), eng->bb->d_res_scan.as<uint32_t>(), d_off_out, d_ids_out,
                                    out_cap, s),
                TM_EDEVICE, "merge");
     return TM_OK;

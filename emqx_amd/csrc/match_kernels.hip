@@ -249,7 +249,7 @@ __device__ __forceinline__ uint32_t probes_needed(uint32_t info, uint32_t bloom,
                 wst[l] = i;                                                                         \
                 key[l] = level_key(&i, e, byte_at);                                                 \
                 const uint32_t len = i - wst[l];                                                    \
-                if (len == 1 && (key[l] == '+' || key[l] == '#')) badarg = true;                    \
+                if (len == 1 && (key[l] == '+' || key[l] == '#') && !a.topic_words) badarg = true;                    \
                 tag[l] = len > 8 ? (len | W_LONG) : len;                                            \
                 sl[l] = word_slot_hash(key[l], tag[l]) & a.wmask;                                   \
                 x[l] = *reinterpret_cast<const uint4 *>(a.wtab + sl[l]);                            \
@@ -291,7 +291,7 @@ __device__ __forceinline__ uint32_t probes_needed(uint32_t info, uint32_t bloom,
                 const bool end = i2 == e;                                                           \
                 const uint8_t c = end ? (uint8_t)'/' : byte_at(i2);                                 \
                 if (c == '/') {                                                                     \
-                    if (i2 - st == 1 && (byte_at(st) == '+' || byte_at(st) == '#')) badarg = true;  \
+                    if (i2 - st == 1 && (byte_at(st) == '+' || byte_at(st) == '#') && !a.topic_words) badarg = true;  \
                     nl++;                                                                           \
                     st = i2 + 1;                                                                    \
                     if (end) break;                                                                 \
@@ -360,14 +360,24 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
         if (!is_long && g.y) {
             const uint32_t dst = L.tbase[g.w & 0xFFu] + g.z;
             if (g.w & SEG_INLINE) {
-                const uint32_t one[1] = {g.x};
-                store_group<OUT, 1>(a, dst, 1, one, 1);
+                if constexpr (OUT == O_KEYS) {
+                    put_key(&a.keys[dst], g.x);
+                } else {
+                    const uint32_t one[1] = {g.x};
+                    store_group<OUT, 1>(a, dst, 1, one, 1);
+                }
             } else {
                 uint32_t key[CP_SHORT];
 #pragma unroll
                 for (int k = 0; k < CP_SHORT; k++)
                     if ((uint32_t)k < g.y) key[k] = a.arena[g.x + k];
-                store_group<OUT, CP_SHORT>(a, dst, 1, key, g.y);
+                if constexpr (OUT == O_KEYS) {
+#pragma unroll
+                    for (int k = 0; k < CP_SHORT; k++)
+                        if ((uint32_t)k < g.y) put_key(&a.keys[dst + k], key[k]);
+                } else {
+                    store_group<OUT, CP_SHORT>(a, dst, 1, key, g.y);
+                }
             }
         }
 #if TM_QCOPY
@@ -406,8 +416,15 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
                         const uint32_t k = k0 + u * GRP;
                         if (k < g.y) key[u] = a.arena[g.x + k];
                     }
-                    // keys k0, k0 + GRP, ... are valid while below g.y
-                    store_group<OUT, CP_UNROLL>(a, (uint64_t)dst + k0, GRP, key, (g.y - k0 + GRP - 1) / GRP);
+                    if constexpr (OUT == O_KEYS) {
+#pragma unroll
+                        for (int u = 0; u < CP_UNROLL; u++) {
+                            const uint32_t k = k0 + u * GRP;
+                            if (k < g.y) put_key(&a.keys[dst + k], key[u]);
+                        }
+                    } else {  // keys k0, k0 + GRP, ... are valid while below g.y
+                        store_group<OUT, CP_UNROLL>(a, (uint64_t)dst + k0, GRP, key, (g.y - k0 + GRP - 1) / GRP);
+                    }
                 }
             }
         }
@@ -428,7 +445,15 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
                 const uint32_t k = k0 + u * WAVE;
                 if (k < g.y) key[u] = a.arena[g.x + k];
             }
-            store_group<OUT, CP_UNROLL>(a, (uint64_t)dst + k0, WAVE, key, (g.y - k0 + WAVE - 1) / WAVE);
+            if constexpr (OUT == O_KEYS) {
+#pragma unroll
+                for (int u = 0; u < CP_UNROLL; u++) {
+                    const uint32_t k = k0 + u * WAVE;
+                    if (k < g.y) put_key(&a.keys[dst + k], key[u]);
+                }
+            } else {
+                store_group<OUT, CP_UNROLL>(a, (uint64_t)dst + k0, WAVE, key, (g.y - k0 + WAVE - 1) / WAVE);
+            }
         }
     }
     __syncthreads();
@@ -506,7 +531,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
             const bool end = i == e;
             const uint8_t c = end ? (uint8_t)'/' : byte_at(i);
             if (c == '/') {
-                if (i - st == 1 && (byte_at(st) == '+' || byte_at(st) == '#')) badarg = true;
+                if (i - st == 1 && (byte_at(st) == '+' || byte_at(st) == '#') && !a.topic_words) badarg = true;
                 nl++;
                 st = i + 1;
                 if (end) break;
@@ -902,6 +927,10 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
         a.out_cnt[t] = my;
         if constexpr (RUNS) a.out_kcnt[t] = my_keys;
     }
+    if constexpr (OUT == O_IDS32 || OUT == O_IDS64) {
+        const bool any_spill = __ballot(spill) != 0;
+        if (lane == 0) a.wave_info[blockIdx.x] = make_uint4((uint32_t)gb, total, any_spill ? 1u : 0u, 0u);
+    }
     {
         uint32_t tot_sp;
         const uint32_t ps = wave_excl_scan(spill ? 1u : 0u, &tot_sp);
@@ -1171,7 +1200,7 @@ __device__ __forceinline__ bool topic_badarg(const MatchArgs &a, uint32_t t) {
     for (uint32_t i = b, st = b;; ++i) {
         const bool end = i == e;
         if (end || a.bytes[i] == '/') {
-            if (i - st == 1 && (a.bytes[st] == '+' || a.bytes[st] == '#')) badarg = true;
+            if (i - st == 1 && (a.bytes[st] == '+' || a.bytes[st] == '#') && !a.topic_words) badarg = true;
             st = i + 1;
             if (end) break;
         }
@@ -1272,7 +1301,7 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
             const bool end = i == e;
             const uint8_t c = end ? (uint8_t)'/' : byte_at(i);
             if (c == '/') {
-                if (i - st == 1 && (byte_at(st) == '+' || byte_at(st) == '#')) badarg = true;
+                if (i - st == 1 && (byte_at(st) == '+' || byte_at(st) == '#') && !a.topic_words) badarg = true;
                 nl++;
                 st = i + 1;
                 if (end) break;

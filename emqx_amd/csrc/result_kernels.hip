@@ -198,6 +198,69 @@ hipError_t launch_result_ids32(const uint32_t *cnt, const uint32_t *src_off, con
                                                s);
 }
 
+// ---------------------------------------------------------------------------
+// topic-major compaction of a MODE_IDS* walk by wave blocks (launch_compact_waves): one
+// block per wave, a straight coalesced copy of the wave's whole output range (its topics are
+// contiguous and in order there), CW_U loads in flight per thread.
+constexpr uint32_t CW_T = 256, CW_U = 4;
+
+template <class IdT>
+__global__ __launch_bounds__(CW_T) void k_compact_waves(const uint4 *wave_info, uint32_t nwaves, uint32_t tpw, uint32_t n,
+                                                        const uint32_t *src_off, const uint32_t *cnt, const IdT *src,
+                                                        const uint32_t *dst_off, IdT *dst, uint64_t cap,
+                                                        uint64_t src_cap, const unsigned long long *cursor) {
+    if (*cursor > src_cap) return;  // the walk overflowed: its waves past the cap wrote nothing
+    for (uint32_t w = blockIdx.x; w < nwaves; w += gridDim.x) {
+        const uint4 wi = wave_info[w];
+        const uint32_t t0 = w * tpw;
+        if (!wi.z) {  // no spilled topic: the wave's range moves whole
+            const uint64_t d0 = dst_off[t0];
+            const uint64_t m = (uint64_t)wi.y;
+            const uint64_t lim = d0 + m <= cap ? m : (cap > d0 ? cap - d0 : 0);
+            for (uint64_t k0 = threadIdx.x; k0 < lim; k0 += CW_T * CW_U) {
+                IdT v[CW_U];
+#pragma unroll
+                for (uint32_t u = 0; u < CW_U; u++)
+                    if (k0 + u * CW_T < lim) v[u] = src[(uint64_t)wi.x + k0 + u * CW_T];
+#pragma unroll
+                for (uint32_t u = 0; u < CW_U; u++)
+                    if (k0 + u * CW_T < lim) dst[d0 + k0 + u * CW_T] = v[u];
+            }
+        } else {  // topic by topic (a spilled topic's ids are where the spill kernel put them)
+            const uint32_t t1 = min(t0 + tpw, n);
+            for (uint32_t t = t0; t < t1; t++) {
+                const uint64_t d0 = dst_off[t], s0 = src_off[t], c = cnt[t];
+                if (d0 + c > cap) continue;
+                for (uint64_t k = threadIdx.x; k < c; k += CW_T) dst[d0 + k] = src[s0 + k];
+            }
+        }
+    }
+}
+
+hipError_t launch_compact_waves(uint32_t id_bytes, const uint4 *wave_info, uint32_t nwaves, uint32_t tpw, uint32_t n,
+                                const uint32_t *src_off, const uint32_t *cnt, const void *src, const uint32_t *dst_off,
+                                void *dst, uint64_t cap, uint64_t src_cap, const unsigned long long *cursor,
+                                uint32_t *flags, hipStream_t s) {
+    if (n && cap && nwaves) {
+        const uint32_t blocks = std::min<uint32_t>(nwaves, 8192);
+        if (id_bytes == 4)
+            k_compact_waves<uint32_t><<<blocks, CW_T, 0, s>>>(wave_info, nwaves, tpw, n, src_off, cnt,
+                                                              (const uint32_t *)src, dst_off, (uint32_t *)dst, cap,
+                                                              src_cap, cursor);
+        else
+            k_compact_waves<uint64_t><<<blocks, CW_T, 0, s>>>(wave_info, nwaves, tpw, n, src_off, cnt,
+                                                              (const uint64_t *)src, dst_off, (uint64_t *)dst, cap,
+                                                              src_cap, cursor);
+        hipError_t e = hipGetLastError();
+        if (e) return e;
+    }
+    if (flags) {
+        k_result_flags<<<1, 64, 0, s>>>(cursor, src_cap, dst_off, n, cap, flags);
+        return hipGetLastError();
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_compact_ids(uint32_t id_bytes, const uint32_t *src_off, const void *src, const uint32_t *dst_off,
                               uint32_t n, void *ids, uint64_t cap, uint64_t src_cap, const unsigned long long *cursor,
                               uint32_t *flags, hipStream_t s) {
@@ -274,56 +337,112 @@ __global__ void k_roff_colsum(const uint32_t *roff, uint64_t stride, uint32_t G,
     off[t] = s;
 }
 
+// Rank-chunk parallel: block (r, c) moves rank r's ids [c * MG_CH, (c + 1) * MG_CH) (its
+// topic-major array) to their merged positions.  The block marks in LDS where each of the
+// chunk's topics starts (its local index k, with the topic's destination shift), a max-scan
+// gives every element its topic, and each element lands at
+//   off[t] + (ids of ranks < r in topic t) + (i - roff_r[t]).
+// Reads and writes are contiguous runs (a topic's slice from one rank), no per-element search.
+constexpr uint32_t MG_T = 256, MG_PER = 16, MG_CH = MG_T * MG_PER;
+
+__device__ __forceinline__ uint32_t first_topic_ending_after(const uint32_t *ro, uint32_t n, uint64_t i) {
+    // the first t in [0, n) with ro[t + 1] > i (ro is nondecreasing, ro[n] > i)
+    uint32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if ((uint64_t)ro[mid + 1] > i) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
 template <class IdT>
-__global__ __launch_bounds__(RI_T) void k_merge_flat(const uint32_t *roff, uint64_t stride, uint32_t G, uint32_t n,
-                                                     const IdT *ids, ShardBases base, const uint32_t *off,
-                                                     uint64_t *out, uint64_t cap) {
-    const uint64_t lim = min((uint64_t)off[n], cap);  // topics past the caller's cap stay unwritten
+__global__ __launch_bounds__(MG_T) void k_merge_ranks(const uint32_t *roff, uint64_t stride, uint32_t G, uint32_t n,
+                                                      const IdT *ids, ShardBases base, const uint32_t *off,
+                                                      uint64_t *out, uint64_t cap, uint32_t chunks_per_rank) {
+    __shared__ uint32_t s_mark[MG_CH];  // 1 + the position where the topic covering it starts (0: none yet)
+    __shared__ int64_t s_shift[MG_CH];  // at a topic's first position: its destination - source index
+    __shared__ uint32_t s_part[MG_T];
     __shared__ uint32_t s_t0, s_t1;
-    for (uint64_t q0 = (uint64_t)blockIdx.x * RI_BLK; q0 < lim; q0 += (uint64_t)gridDim.x * RI_BLK) {
-        const uint64_t q1 = min(q0 + RI_BLK, lim);
+    const uint32_t tid = threadIdx.x;
+    for (uint64_t bc = blockIdx.x; bc < (uint64_t)G * chunks_per_rank; bc += gridDim.x) {
+        const uint32_t r = (uint32_t)(bc / chunks_per_rank), c = (uint32_t)(bc % chunks_per_rank);
+        const uint32_t *ro = roff + (uint64_t)r * stride;
+        const uint64_t total = ro[n];
+        const uint64_t i0 = (uint64_t)c * MG_CH;
+        if (i0 >= total) continue;  // block-uniform
+        const uint64_t i1 = min(i0 + MG_CH, total);
         __syncthreads();
-        if (threadIdx.x == 0) {
-            s_t0 = topic_of(off, 0, n, q0);
-            s_t1 = topic_of(off, s_t0, n, q1 - 1);
+        if (tid == 0) {
+            s_t0 = first_topic_ending_after(ro, n, i0);
+            s_t1 = first_topic_ending_after(ro, n, i1 - 1);
+        }
+        for (uint32_t k = tid; k < MG_CH; k += MG_T) s_mark[k] = 0;
+        __syncthreads();
+        const uint32_t t0 = s_t0, t1 = s_t1;
+        // mark each nonempty topic's first element in the chunk with its local index + 1
+        for (uint32_t t = t0 + tid; t <= t1; t += MG_T) {
+            const uint32_t a = ro[t], e = ro[t + 1];
+            if (e == a) continue;
+            uint64_t before = 0;  // ids of ranks < r in topic t
+            for (uint32_t q = 0; q < r; q++)
+                before += roff[(uint64_t)q * stride + t + 1] - roff[(uint64_t)q * stride + t];
+            const uint64_t at = a > i0 ? a : i0;  // the topic's first position in the chunk
+            s_shift[at - i0] = (int64_t)off[t] + (int64_t)before - (int64_t)a;
+            s_mark[at - i0] = (uint32_t)(at - i0) + 1;
         }
         __syncthreads();
-        uint32_t t = s_t0;
-        const uint32_t t1 = s_t1;
-#pragma unroll 4
-        for (uint32_t i = 0; i < RI_PER; i++) {
-            const uint64_t q = q0 + (uint64_t)i * RI_T + threadIdx.x;
-            if (q >= q1) break;
-            t = topic_of(off, t, t1, q);
-            uint32_t k = (uint32_t)(q - off[t]);
-            for (uint32_t r = 0; r < G; r++) {
-                const uint32_t a = roff[(uint64_t)r * stride + t], c = roff[(uint64_t)r * stride + t + 1] - a;
-                if (k < c) {
-                    out[q] = (uint64_t)ids[base.b[r] + a + k];
-                    break;
-                }
-                k -= c;
-            }
+        // inclusive max-scan of the marks: thread-local over MG_PER, then over the threads
+        uint32_t m = 0;
+        for (uint32_t u = 0; u < MG_PER; u++) {
+            const uint32_t v = s_mark[tid * MG_PER + u];
+            m = v > m ? v : m;
+            s_mark[tid * MG_PER + u] = m;
+        }
+        s_part[tid] = m;
+        __syncthreads();
+        for (uint32_t d = 1; d < MG_T; d <<= 1) {
+            const uint32_t v = tid >= d ? s_part[tid - d] : 0u;
+            __syncthreads();
+            if (v > s_part[tid]) s_part[tid] = v;
+            __syncthreads();
+        }
+        const uint32_t carry = tid ? s_part[tid - 1] : 0u;
+        for (uint32_t u = 0; u < MG_PER; u++) {
+            const uint32_t v = s_mark[tid * MG_PER + u];
+            s_mark[tid * MG_PER + u] = v > carry ? v : carry;
+        }
+        __syncthreads();
+        // every element: its topic's shift; coalesced reads of the rank's ids
+        for (uint32_t u = 0; u < MG_PER; u++) {
+            const uint32_t k = u * MG_T + tid;
+            const uint64_t i = i0 + k;
+            if (i >= i1) break;
+            const uint32_t lt = s_mark[k];  // >= 1: position 0 carries the chunk's first topic
+            const uint64_t d = (uint64_t)((int64_t)i + s_shift[lt - 1]);
+            if (d < cap) out[d] = (uint64_t)ids[base.b[r] + i];
         }
     }
 }
 
 hipError_t launch_merge_shard_ids(uint32_t G, uint32_t n, const uint32_t *roff, uint64_t roff_stride, const void *ids,
                                   uint32_t id_bytes, const uint64_t *base, uint32_t *off, uint64_t *out, uint64_t cap,
-                                  hipStream_t s) {
+                                  uint32_t max_total, hipStream_t s) {
     if (G == 0 || G > MERGE_MAX_G) return hipErrorInvalidValue;
     ShardBases b{};
     for (uint32_t r = 0; r < G; r++) b.b[r] = base[r];
     k_roff_colsum<<<(n + 1 + 255) / 256, 256, 0, s>>>(roff, roff_stride, G, n, off);
     hipError_t e = hipGetLastError();
-    if (e || !n || !cap) return e;
-    const uint64_t blocks = std::min<uint64_t>((cap + RI_BLK - 1) / RI_BLK, 2048);
+    if (e || !n || !cap || !max_total) return e;
+    // chunks per rank from the caller's bound on any rank's total (the totals are on the device)
+    const uint32_t cpr = (uint32_t)(((uint64_t)max_total + MG_CH - 1) / MG_CH);
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((uint64_t)G * cpr, 16384);
     if (id_bytes == 4)
-        k_merge_flat<uint32_t><<<(uint32_t)blocks, RI_T, 0, s>>>(roff, roff_stride, G, n, (const uint32_t *)ids, b, off,
-                                                                 out, cap);
+        k_merge_ranks<uint32_t><<<blocks, MG_T, 0, s>>>(roff, roff_stride, G, n, (const uint32_t *)ids, b, off, out, cap,
+                                                        cpr);
     else
-        k_merge_flat<uint64_t><<<(uint32_t)blocks, RI_T, 0, s>>>(roff, roff_stride, G, n, (const uint64_t *)ids, b, off,
-                                                                 out, cap);
+        k_merge_ranks<uint64_t><<<blocks, MG_T, 0, s>>>(roff, roff_stride, G, n, (const uint64_t *)ids, b, off, out, cap,
+                                                        cpr);
     return hipGetLastError();
 }
 

@@ -280,7 +280,7 @@ class ShardedIndex:
         out_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
         cap = G * self.stride
         out_ids = torch.empty(cap, dtype=torch.int64, device=dev)
-        eng.merge_shard_ids_device(G, n, H.data_ptr(), n + 2, Ids.data_ptr(), self.id_bytes, bases,
+        eng.merge_shard_ids_device(G, n, H.data_ptr(), n + 2, Ids.data_ptr(), self.id_bytes, bases, self.stride,
                                    out_off.data_ptr(), out_ids.data_ptr(), cap, sp)
         return out_off, out_ids, flags
 

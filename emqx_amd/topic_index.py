@@ -152,7 +152,16 @@ class TopicIndex:
         out = [None] * len(topics)
         if wl:
             empty = [i for i in wl if not topics[i]]
-            byw = [i for i in wl if topics[i]]
+            # lists of binary words: the engine's own walk of word-list topics
+            # (TM_MATCH_TOPIC_WORDS); lists holding the '+' / '#' / '' atoms act as filters of
+            # the walk (compare/3's filter-search clauses) and go through matches_filter
+            plain = [i for i in wl if topics[i] and not any(isinstance(w, str) and w in (PLUS, HASH, "")
+                                                           for w in topics[i])
+                     and not any(b"/" in (w.encode() if isinstance(w, str) else bytes(w)) for w in topics[i])]
+            if plain:
+                for i, hs in zip(plain, self.eng.match_words([topics[i] for i in plain], N.TM_MATCH_ALL)):
+                    out[i] = self._reduce([self._key_of(h) for h in hs], opts)
+            byw = [i for i in wl if topics[i] and out[i] is None]
             if byw:
                 for i, r in zip(byw, self.matches_filter_batch([words_topic_bytes(topics[i]) for i in byw], opts)):
                     out[i] = r

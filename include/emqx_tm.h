@@ -105,6 +105,12 @@ extern "C" {
 #define TM_MATCH_AGGRE  4u  /* emqx_broker:aggre/1 (emqx_broker.erl:361-377): keys whose id is a
                                shared-subscription dest (TM_ID_SHARED) collapse to one key per
                                {Filter, Group}; every other key is kept */
+/* OR'd into tm_match_batch's mode: the topics are pre-split word lists, '/'-joined
+ * (matches/3's `[word()]` form, emqx_trie_search.erl:182, topic_words/1 :369-370).  A "+" or "#"
+ * level is then a plain word (no TM_BADARG), and keys given as binaries ({Binary, {ID}})
+ * do not match (match_topics/4 compares the list itself, :380-389).  With ALL, UNIQUE, FIRST
+ * and COUNT; not on replicas.  Words containing '/' have no joined form. */
+#define TM_MATCH_TOPIC_WORDS 0x100u
 
 /* Route-id convention for TM_MATCH_AGGRE: a $share/$queue dest {Group, Node}
  * (emqx_shared_sub.erl:444-456) gets an id with TM_ID_SHARED set and its group index in
@@ -325,13 +331,13 @@ int tm_match_ids_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *
 
 /* Filter-sharded merge over tm_match_ids_device results: rank r's d_off_out row (n+1 u32) at
  * d_roff + r * roff_stride, its ids (id_bytes each) at d_ids + base[r] elements (base: G
- * host values).  Writes the merged result as u64: topic i's ids are the concatenation of its
- * slices from shard 0..G-1 at d_out_ids[d_out_off[i] .. d_out_off[i+1]) (n+1 offsets).  One
- * column-sum launch and one output-parallel copy; topics past out_cap are left unwritten.
- * G <= 64. */
+ * host values); max_rank_ids bounds every rank's id count (e.g. the padded stride).  Writes
+ * the merged result as u64: topic i's ids are the concatenation of its slices from shard
+ * 0..G-1 at d_out_ids[d_out_off[i] .. d_out_off[i+1]) (n+1 offsets).  One column-sum launch
+ * and one rank-chunk-parallel copy; ids past out_cap are left unwritten.  G <= 64. */
 int tm_merge_shard_ids_device(tm_engine *eng, uint32_t G, uint32_t n, const uint32_t *d_roff, uint64_t roff_stride,
-                              const void *d_ids, uint32_t id_bytes, const uint64_t *base, uint32_t *d_out_off,
-                              uint64_t *d_out_ids, uint64_t out_cap, void *stream);
+                              const void *d_ids, uint32_t id_bytes, const uint64_t *base, uint64_t max_rank_ids,
+                              uint32_t *d_out_off, uint64_t *d_out_ids, uint64_t out_cap, void *stream);
 
 /* Filter-sharded mode: G shards matched the same n topics against disjoint
  * key sets; shard r's compacted result (tm_result_ids_device) is counts[r*n .. r*n+n) and

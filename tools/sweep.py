@@ -30,6 +30,7 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 # same-process reference point.
 VARIANTS = {
     "head": ([], 0),  # match_kernels.hip as committed (git HEAD)
+    "prev": ([], 0),  # match_kernels.hip at SWEEP_PREV (default af8ba73: before the fused-id copy-out)
     "base": ([], 0),
     "base2": ([], 0),  # the same build again: run-to-run noise and the digest's self-check
     "nopre": (["-DTM_PRELOOK=0"], 0),
@@ -71,10 +72,11 @@ def build(names):
         flags = VARIANTS[name][0]
         out = os.path.join(VDIR, f"libemqx_tm_{name}.so")
         kern = os.path.join(CSRC, "match_kernels.hip")
-        if name == "head":
-            kern = os.path.join(CSRC, "_head_match_kernels.hip")
+        if name in ("head", "prev"):
+            ref = "HEAD" if name == "head" else os.environ.get("SWEEP_PREV", "af8ba73")
+            kern = os.path.join(CSRC, f"_{name}_match_kernels.hip")
             with open(kern, "w") as f:
-                f.write(subprocess.check_output(["git", "-C", ROOT, "show", "HEAD:emqx_amd/csrc/match_kernels.hip"],
+                f.write(subprocess.check_output(["git", "-C", ROOT, "show", f"{ref}:emqx_amd/csrc/match_kernels.hip"],
                                                 text=True))
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                "-Wno-unused-function", *flags, os.path.join(CSRC, "engine.cpp"),
