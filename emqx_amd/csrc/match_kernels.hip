@@ -72,6 +72,9 @@ constexpr uint32_t DO_PLUS = 0x80u, DO_LIT = 0x40u;  // frontier meta: probes th
 #ifndef TM_CP_UNROLL
 #define TM_CP_UNROLL 8
 #endif
+#ifndef TM_NT_DEPTH
+#define TM_NT_DEPTH 0  // 0: every edge probe is a normal load; d: probes at depth >= d are non-temporal
+#endif
 #ifndef TM_NT_KEYS
 #define TM_NT_KEYS 1  // key copy-out with non-temporal stores: the output is never re-read here, so it
                       // should not evict trie lines from L2 (0.9255 -> 0.9122 ms at config C)
@@ -694,8 +697,23 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                     uint4 x1[RPL], x2[RPL];
 #pragma unroll
                     for (int k = 0; k < RPL; k++) {
+#if TM_NT_DEPTH
+                        // probes past depth TM_NT_DEPTH are random lines of a 16 GiB table that are
+                        // rarely met again: non-temporal loads keep them from evicting the upper
+                        // levels and the hot lists from L2 (experiment knob)
+                        if (d >= (uint32_t)TM_NT_DEPTH) {
+                            typedef unsigned v4u __attribute__((ext_vector_type(4)));
+                            v4u y1 = {NONE, 0, 0, 0}, y2 = {NONE, 0, 0, 0};
+                            if (p1[k]) y1 = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(a.etab + s1[k]));
+                            if (p2[k]) y2 = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(a.etab + s2[k]));
+                            x1[k] = make_uint4(y1.x, y1.y, y1.z, y1.w);
+                            x2[k] = make_uint4(y2.x, y2.y, y2.z, y2.w);
+                        } else
+#endif
+                        {
                         x1[k] = p1[k] ? *reinterpret_cast<const uint4 *>(a.etab + s1[k]) : make_uint4(NONE, 0, 0, 0);
                         x2[k] = p2[k] ? *reinterpret_cast<const uint4 *>(a.etab + s2[k]) : make_uint4(NONE, 0, 0, 0);
+                        }
                         st_probe += (uint32_t)p1[k] + (uint32_t)p2[k];
                         if constexpr (STATS) dp_probe += (uint32_t)p1[k] + (uint32_t)p2[k];
                     }

@@ -30,7 +30,10 @@ CSRC = os.path.join(ROOT, "emqx_amd", "csrc")
 # same-process reference point.
 VARIANTS = {
     "head": ([], 0),  # match_kernels.hip as committed (git HEAD)
-    "prev": ([], 0),  # match_kernels.hip at SWEEP_PREV (default af8ba73: before the fused-id copy-out)
+    "prev": ([], 0),
+    "ntd2": (["-DTM_NT_DEPTH=2"], 0),
+    "ntd3": (["-DTM_NT_DEPTH=3"], 0),
+    "ntd4": (["-DTM_NT_DEPTH=4"], 0),  # match_kernels.hip at SWEEP_PREV (default af8ba73: before the fused-id copy-out)
     "base": ([], 0),
     "base2": ([], 0),  # the same build again: run-to-run noise and the digest's self-check
     "nopre": (["-DTM_PRELOOK=0"], 0),
