@@ -316,9 +316,10 @@ def main():
     ap.add_argument("--mode", choices=("replicated", "sharded"), default="replicated",
                     help="replicated trie, publishes data-parallel (default); or filters hash-sharded over "
                          "ranks with an RCCL all-gather merge (config D; DESIGN.md §6)")
-    ap.add_argument("--exchange", choices=("padded", "exact", "local"), default="padded",
+    ap.add_argument("--exchange", choices=("padded", "exact", "local", "a2a"), default="padded",
                     help="sharded mode: padded all-gather (no host sync), exact all-gather-v by grouped "
-                         "send/recv, or local (each rank D2H's its own shard lists, no collective)")
+                         "send/recv, local (each rank D2H's its own shard lists, no collective), or a2a "
+                         "(all-to-all by topic range: each rank keeps 1/G of the batch's merged results)")
     ap.add_argument("--shard-of", type=int, default=0, metavar="G",
                     help="sharded mode on one process: hold shard 0 of a G-way split (per-GPU share of G GPUs)")
     ap.add_argument("--churn", type=int, default=0, metavar="EPOCHS",
@@ -713,6 +714,7 @@ def run_sharded(args):
         wire = {"model": f"{G}-rank exchange from this shard's sizes (every shard assumed to match as many)",
                 "padded": (G - 1) * (six.stride * six.id_bytes + hdr_b),
                 "exact": (G - 1) * (own * six.id_bytes + hdr_b), "local": 0,
+                "a2a": int((G - 1) / G * own * six.id_bytes) + (G - 1) * ((n // G + 1) * 4 + (G + 2) * 4),
                 "bound_(G-1)/G*sumM*4": int((G - 1) / G * (G * own) * 4),
                 "exact_ids_only": (G - 1) * own * six.id_bytes}
     if rank == 0:

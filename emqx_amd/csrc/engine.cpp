@@ -1777,7 +1777,7 @@ struct tm_engine {
         std::vector<std::string> dict;   // sorted distinct literal words of the keys
         uint32_t K = 0;
         DevBuf d_kw, d_koff, d_kh;
-        DevBuf d_qw, d_qoff, d_qdollar, d_qstatus, d_cnt, d_off, d_out, d_scan, d_pool, d_ctl, d_jobs, d_krec;
+        DevBuf d_qw, d_qoff, d_qdollar, d_qstatus, d_cnt, d_off, d_out, d_scan, d_pool, d_ctl, d_jobs, d_krec, d_kend;
         uint64_t out_want = 1 << 16, pool_want = 1024;  // one-pass sizes (from the demand seen)
         std::vector<uint32_t> qw, qoff;
         std::vector<uint32_t> wcode;     // interned word id -> order code (NONE: not cached yet)
@@ -1887,16 +1887,37 @@ struct tm_engine {
             krec[j * 8] = L;
             for (uint32_t i = 0; i < std::min<uint32_t>(L, FW_REC_WORDS); i++) krec[j * 8 + 1 + i] = kw[b + i];
         }
+        // prefix-group ends: kend[j][d] = the first key after j whose first d+1 words differ
+        // from key j's.  A seek's probe {first np words of key ks ++ [w]} lands inside
+        // [ks, kend[ks][np-1]] (every key in between shares those np words, the key at the end
+        // is past them), so the walk searches that range instead of galloping from the cursor;
+        // a '#'-run's end IS kend[rs][p-1].  One backward pass over the common prefixes of
+        // neighbours.
+        const size_t K = lk.size();
+        std::vector<uint32_t> kend(std::max<size_t>(K, 1) * FW_END_DEPTHS, 0u);
+        for (size_t j = K; j-- > 0;) {
+            uint32_t lcp = 0;
+            if (j + 1 < K) {
+                const uint32_t *x = &kw[koff[j]], *y = &kw[koff[j + 1]];
+                const uint32_t lx = koff[j + 1] - koff[j], ly = koff[j + 2] - koff[j + 1];
+                while (lcp < lx && lcp < ly && lcp < FW_END_DEPTHS && x[lcp] == y[lcp]) lcp++;
+            }
+            for (uint32_t d = 0; d < FW_END_DEPTHS; d++)
+                kend[j * FW_END_DEPTHS + d] = (j + 1 < K && lcp >= d + 1) ? kend[(j + 1) * FW_END_DEPTHS + d]
+                                                                          : (uint32_t)(j + 1);
+        }
         fx.K = (uint32_t)lk.size();
         hipError_t e;
-        if ((e = fx.d_krec.ensure(krec.size() * 4)) != hipSuccess ||
+        if ((e = fx.d_kend.ensure(kend.size() * 4)) != hipSuccess ||
+            (e = fx.d_krec.ensure(krec.size() * 4)) != hipSuccess ||
             (e = fx.d_kw.ensure(std::max<size_t>(kw.size(), 1) * 4)) != hipSuccess ||
             (e = fx.d_koff.ensure(koff.size() * 4)) != hipSuccess ||
             (e = fx.d_kh.ensure(std::max<size_t>(kh.size(), 1) * 4)) != hipSuccess) {
             err = std::string("matches_filter index alloc: ") + hipGetErrorString(e);
             return TM_ENOMEM;
         }
-        if ((e = hipMemcpy(fx.d_krec.p, krec.data(), krec.size() * 4, hipMemcpyHostToDevice)) ||
+        if ((e = hipMemcpy(fx.d_kend.p, kend.data(), kend.size() * 4, hipMemcpyHostToDevice)) ||
+            (e = hipMemcpy(fx.d_krec.p, krec.data(), krec.size() * 4, hipMemcpyHostToDevice)) ||
             (!kw.empty() && (e = hipMemcpy(fx.d_kw.p, kw.data(), kw.size() * 4, hipMemcpyHostToDevice))) ||
             (e = hipMemcpy(fx.d_koff.p, koff.data(), koff.size() * 4, hipMemcpyHostToDevice)) ||
             (!kh.empty() && (e = hipMemcpy(fx.d_kh.p, kh.data(), kh.size() * 4, hipMemcpyHostToDevice)))) {
@@ -2013,7 +2034,7 @@ void tm_destroy(tm_engine *eng) {
     for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
                       &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan, &eng->fx.d_pool,
-                      &eng->fx.d_ctl, &eng->fx.d_jobs, &eng->fx.d_krec, &eng->d_ia, &eng->d_iaoff,
+                      &eng->fx.d_ctl, &eng->fx.d_jobs, &eng->fx.d_krec, &eng->fx.d_kend, &eng->d_ia, &eng->d_iaoff,
                       &eng->d_ib, &eng->d_iboff, &eng->d_iout, &eng->d_ilen})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
@@ -3035,6 +3056,7 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
     FilterArgs a{};
     a.kw = fx.d_kw.as<uint32_t>();
     a.krec = fx.d_krec.as<uint4>();
+    a.kend = fx.d_kend.as<uint32_t>();
     a.koff = fx.d_koff.as<uint32_t>();
     a.kh = fx.d_kh.as<uint32_t>();
     a.K = fx.K;

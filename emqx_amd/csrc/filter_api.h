@@ -14,6 +14,9 @@ struct FilterArgs {
     const uint32_t *kw;    // order codes of every key's words, keys back to back
     const uint32_t *koff;  // K+1: key j's words are kw[koff[j] .. koff[j+1])
     const uint4 *krec;     // 2 per key: {length, words 0 .. FW_REC_WORDS-1 (0-padded)}
+    const uint32_t *kend;  // FW_END_DEPTHS per key: kend[j * FW_END_DEPTHS + d] = the first key
+                           // after j whose first d+1 words differ from key j's (its prefix
+                           // group's end; key j shorter than d+1 words: j + 1)
     const uint32_t *kh;    // K: key handle of sorted key j
     uint32_t K;
     uint32_t n;            // queries
@@ -42,6 +45,7 @@ constexpr uint32_t FW_CHUNK = 256;   // u32 words per pool chunk (1 link entry +
 constexpr uint32_t FW_BULK = 4096;   // ranges longer than this are copied by k_filter_bulk
 constexpr uint32_t FW_JOB = 8192;    // keys per k_filter_bulk job (a long range is split)
 constexpr uint32_t FW_REC_WORDS = 7; // key words held in the fixed-stride record
+constexpr uint32_t FW_END_DEPTHS = 8; // prefix-group ends kept per key (prefixes of 1..8 words)
 hipError_t launch_filter_walk(const FilterArgs &a, int pass, hipStream_t stream);
 // FW_ONEPASS's bulk copies (after launch_filter_walk, same stream; reads the job count on device)
 hipError_t launch_filter_bulk(const FilterArgs &a, hipStream_t stream);

@@ -82,19 +82,24 @@ __device__ inline int cmp_key_seek(const FilterArgs &a, uint32_t j, const Probe 
     return cmp_rec_probe(a, j, kr, L, pb);
 }
 
-// next(probe) among keys [lo, K): the first key >= the probe, found by the whole
-// wave.  Gallop: lane L probes lo + 2^L - 1 (lane 32 lies past any K < 2^32), which
-// brackets the answer; then 64-ary narrowing, each round probing 64 evenly spaced keys
-// (a range of K keys takes about log64(K) rounds).  Wave-uniform result.
-__device__ uint32_t wave_seek(const FilterArgs &a, uint32_t lo, const Probe &pb, uint32_t lane) {
-    const uint64_t K = a.K;
-    if (lo >= K) return (uint32_t)K;
-    const uint64_t p = lane < 33 ? (uint64_t)lo + ((1ull << lane) - 1) : ~0ull;
-    const bool ge = p >= K || cmp_key_seek(a, (uint32_t)p, pb) >= 0;
-    const uint32_t g = (uint32_t)__ffsll((long long)__ballot(ge)) - 1;  // lane 32 is always ge
-    if (g == 0) return lo;
-    // invariant: every key below l is < the probe; key h is >= it (or h == K)
-    uint64_t l = (uint64_t)lo + (1ull << (g - 1)), h = std::min<uint64_t>((uint64_t)lo + (1ull << g) - 1, K);
+// next(probe) among keys [lo, hi): the first key >= the probe, found by the whole wave; hi
+// itself when none is (the caller knows key hi is past the probe, or hi == K).  A far bound
+// starts with a gallop (lane L probes lo + 2^L - 1; lanes past hi count as past the probe),
+// which brackets the answer; then 64-ary narrowing, each round probing 64 evenly spaced keys
+// (a range of R keys takes about log64(R) rounds).  A near bound (the probe's prefix group,
+// kend) is narrowed directly.  Wave-uniform result.
+__device__ uint32_t wave_seek(const FilterArgs &a, uint32_t lo, const Probe &pb, uint32_t lane, uint32_t hi) {
+    if (lo >= hi) return hi;
+    // invariant: every key below l is < the probe; key h is >= it (or h == hi)
+    uint64_t l = lo, h = hi;
+    if (hi - lo > 64u * 64u) {
+        const uint64_t p = lane < 33 ? (uint64_t)lo + ((1ull << lane) - 1) : ~0ull;
+        const bool ge = p >= hi || cmp_key_seek(a, (uint32_t)p, pb) >= 0;
+        const uint32_t g = (uint32_t)__ffsll((long long)__ballot(ge)) - 1;  // lane 32 is always ge
+        if (g == 0) return lo;
+        l = (uint64_t)lo + (1ull << (g - 1));
+        h = std::min<uint64_t>((uint64_t)lo + (1ull << g) - 1, hi);
+    }
     while (l < h) {
         const uint64_t step = (h - l + 63) / 64;
         const uint64_t x = l + lane * step;
@@ -111,6 +116,13 @@ __device__ uint32_t wave_seek(const FilterArgs &a, uint32_t lo, const Probe &pb,
         h = hf;
     }
     return (uint32_t)l;
+}
+
+// The end of key ks's group of keys sharing its first np words (1 <= np <= FW_END_DEPTHS), or
+// K when np is out of that range: an upper bound of next({first np words of ks ++ [w], {}}).
+__device__ __forceinline__ uint32_t prefix_end(const FilterArgs &a, uint32_t ks, uint32_t np) {
+    if (np == 0 || np > FW_END_DEPTHS) return a.K;
+    return a.kend[(uint64_t)ks * FW_END_DEPTHS + np - 1];  // wave-uniform address: one load
 }
 
 // One position of compare/3 with the filter-search clauses, in the reference's clause
@@ -261,7 +273,7 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             Probe pb{};
             pb.np = 0;
             pb.w = W[0];
-            idx = wave_seek(a, 0, pb, lane);
+            idx = wave_seek(a, 0, pb, lane, K);
         }
         uint32_t *out = pass == FW_EMIT ? a.out + a.out_off[q] : nullptr;
         const uint64_t below = (1ull << lane) - 1;
@@ -286,7 +298,12 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
                 const bool ge = lane > from && (!inr || cmp_rec_probe(a, j, fr, FL, pb) >= 0);
                 const uint64_t gm = __ballot(ge);
                 if (gm) return min(idx + (uint32_t)__ffsll((long long)gm) - 1, K);
-                return wave_seek(a, idx + 64, pb, lane);
+                // past the window: the target lies in the probe's prefix group, whose end is
+                // known per key (kend); a '#'-run's end (probe word +inf) IS that end
+                // (never below idx + 64, which the window just ruled out: the walk only moves on)
+                const uint32_t hi = min(max(prefix_end(a, pb.ks, pb.np), idx + 64), K);
+                if (pb.w == NONE_FW && pb.np >= 1 && pb.np <= FW_END_DEPTHS) return hi;
+                return wave_seek(a, idx + 64, pb, lane, hi);
             };
             // the probe of a seek or run end from lane l: key idx+l's record words, no loads
             auto probe_from = [&](uint32_t l, uint32_t np, uint32_t w) {

@@ -62,7 +62,7 @@ def select_keys(buf, off, ids, mask, flags=None):
     return nbuf, noff, ids[mask], nfl
 
 
-EXCHANGES = ("padded", "exact", "local")
+EXCHANGES = ("padded", "exact", "local", "a2a")
 
 
 def merge_shard_ids_host(H, ids, bases, n: int):
@@ -125,7 +125,12 @@ class ShardedIndex:
       exact   all-gather of the headers, then every rank's ids at their exact size by grouped
               send/recv (the sizes come from the gathered headers: one host read per step);
       local   no collective: each rank copies its own shard's lists to the host, and the
-              consumer reads the G shard lists of a topic side by side.
+              consumer reads the G shard lists of a topic side by side;
+      a2a     by topic range: rank r keeps the merged results of topics [r*n/G, (r+1)*n/G)
+              (the publishes it answers); every rank sends each other rank just that range
+              of its ids (all_to_all at exact sizes, from an all-gather of G+1 offsets per
+              rank: one host read per step), so a rank receives (G-1)/G of ONE shard's ids
+              instead of G-1 shards' worth, and merges 1/G of the batch.
     Ids cross the wire as u32 while every id of every shard fits 32 bits (u64 otherwise)."""
 
     def __init__(self, shard, rank: int, world: int, group=None, exchange: str = "padded"):
@@ -190,11 +195,49 @@ class ShardedIndex:
         self.wire_bytes = sum(tot[q] for q in range(G) if q != me) * eb + (G - 1) * (n + 2) * 4
         return H, Ids, bases
 
+    def topic_range(self, n: int, rank: int | None = None):
+        """a2a: the topics [lo, hi) whose merged results this rank keeps."""
+        r = self.rank if rank is None else rank
+        return r * n // self.world, (r + 1) * n // self.world
+
+    def _exchange_a2a(self, hdr, ids, n: int):
+        """a2a exchange: returns (H (G, m+2) i32 rows of this rank's topic range [offsets
+        rebased to 0 | flags], Ids, bases) for m = the range's topic count."""
+        import torch
+        import torch.distributed as dist
+        G, me = self.world, self.rank
+        T = [q * n // G for q in range(G + 1)]
+        dev = hdr.device
+        Tt = torch.tensor(T, dtype=torch.int64, device=dev)
+        mine = torch.cat([hdr[:n + 1][Tt], hdr[n + 1:n + 2]])  # my offsets at the range bounds + flags
+        B = torch.empty(G * (G + 2), dtype=hdr.dtype, device=dev)
+        dist.all_gather_into_tensor(B, mine.contiguous(), group=self.group)
+        Bh = (B.view(G, G + 2)[:, :G + 1].to(torch.int64) & 0xFFFFFFFF).cpu().tolist()  # sizes: one host read
+        flags = B.view(G, G + 2)[:, G + 1]
+        send = [Bh[me][q + 1] - Bh[me][q] for q in range(G)]
+        recv = [Bh[q][me + 1] - Bh[q][me] for q in range(G)]
+        lo = Bh[me][0]
+        Ids = torch.empty(max(1, sum(recv)), dtype=ids.dtype, device=ids.device)
+        dist.all_to_all_single(Ids[:sum(recv)], ids[lo:lo + sum(send)].contiguous(), recv, send, group=self.group)
+        # every rank's offsets over my topic range, rebased to its slice's start
+        m = T[me + 1] - T[me]
+        offs = torch.cat([hdr[T[q]:T[q + 1] + 1] - hdr[T[q]] for q in range(G)])
+        O = torch.empty(G * (m + 1), dtype=hdr.dtype, device=dev)
+        dist.all_to_all_single(O, offs, [m + 1] * G, [T[q + 1] - T[q] + 1 for q in range(G)], group=self.group)
+        H = torch.cat([O.view(G, m + 1), flags.view(G, 1)], dim=1).contiguous()
+        bases = [0] * G
+        for q in range(1, G):
+            bases[q] = bases[q - 1] + recv[q - 1]
+        eb = ids.element_size()
+        self.wire_bytes = sum(recv[q] for q in range(G) if q != me) * eb + (G - 1) * ((m + 1) * 4 + (G + 2) * 4)
+        return H, Ids, bases
+
     # ---- host path (gloo or nccl)
     def match(self, t_bytes, t_off, exchange: str | None = None):
         """Match the whole batch on every rank.  padded / exact: the merged (off[n+1] u32,
         ids u64, status i32[n]) on every rank; local: this rank's own shard lists in the same
-        form (the union over ranks is the result)."""
+        form (the union over ranks is the result); a2a: the merged results of this rank's
+        topic range (topic_range), as (off[m+1], ids, status[m])."""
         import torch
         import torch.distributed as dist
         exchange = exchange or self.exchange
@@ -208,6 +251,15 @@ class ShardedIndex:
             dev = torch.device("cuda", torch.cuda.current_device())
         hdr = torch.from_numpy(np.concatenate([roff, np.zeros(1, np.uint32)]).view(np.int32)).to(dev)
         total = int(roff[-1])
+        if exchange == "a2a":
+            buf = np.zeros(max(1, total), np.uint64)
+            buf[:total] = ids
+            if self.world == 1:
+                return roff, ids, st
+            H, Ids, bases = self._exchange_a2a(hdr, torch.from_numpy(buf.view(np.int64)).to(dev), n)
+            lo, hi = self.topic_range(n)
+            off, merged = merge_shard_ids_host(H.cpu().numpy(), Ids.cpu().numpy().view(np.uint64), bases, hi - lo)
+            return off, merged, st[lo:hi]
         if exchange == "padded":
             # without prepare_device the host path pads to the largest rank's total
             t = torch.tensor([total], dtype=torch.int64, device=dev)
@@ -321,8 +373,13 @@ class ShardedIndex:
                 s.synchronize()
                 self.wire_bytes = 0
                 return h_hdr[:n + 1], self._h_ids[:total], h_hdr[n + 1:]
-            H, Ids, bases = self._exchange(hdr, ids, n, exchange)
-            out = self.merge_device(eng, H, Ids, bases, n, sp)
+            if exchange == "a2a" and self.world > 1:
+                H, Ids, bases = self._exchange_a2a(hdr, ids, n)
+                lo, hi = self.topic_range(n)
+                out = self.merge_device(eng, H, Ids, bases, hi - lo, sp)
+            else:
+                H, Ids, bases = self._exchange(hdr, ids, n, exchange)
+                out = self.merge_device(eng, H, Ids, bases, n, sp)
         caller.wait_stream(s)
         for t in out:
             t.record_stream(caller)  # consumed on the caller's stream from here on

@@ -164,7 +164,8 @@ def test_host_merge_concatenates_per_topic():
 def test_sharded_gloo_world2_matches_unsharded_oracle():
     """Every exchange variant over gloo, world 2: padded and exact merge to the unsharded
     oracle's sets on every rank (two epochs); local leaves each rank its own lists, whose
-    union is the oracle's; the exact variant moves no more than the ids themselves."""
+    union is the oracle's; a2a leaves each rank the merged sets of its topic range; the exact
+    variant moves no more than the ids themselves, a2a only the other rank's ids of its range."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -193,6 +194,16 @@ def test_sharded_gloo_world2_matches_unsharded_oracle():
         got = np.sort(np.concatenate([li[r][lo[r][t]:lo[r][t + 1]] for r in range(2)]))
         assert np.array_equal(got, eids[eoff[t]:eoff[t + 1]]), t
     assert res[0][1]["local"][3] == 0
+    # a2a: each rank holds the merged results of its topic range; together, every topic
+    for rank, rr, _ in res:
+        off, ids, st, wire = rr["a2a"]
+        lo, hi = rank * n // 2, (rank + 1) * n // 2
+        assert len(off) == hi - lo + 1 and np.array_equal(np.asarray(st), est[lo:hi])
+        _same_sets(off, ids, eoff[lo:hi + 1] - eoff[lo], eids[eoff[lo]:eoff[hi]])
+        # it received only the other rank's ids for its own topics (+ offsets)
+        other = 1 - rank
+        lo_o = np.asarray(res[other][1]["local"][0], np.int64)
+        assert wire == (lo_o[hi] - lo_o[lo]) * 8 + ((hi - lo + 1) * 4 + 4 * 4)
     # exact: each rank received the other's ids at exact size (+ its header)
     for rank, rr, _ in res:
         other = 1 - rank
