@@ -1101,6 +1101,7 @@ def filter_leg(args, w, eng, q):
     import oracle
     qb, qo = filter_queries(w, q, kinds=[int(x) for x in args.filter_kinds.split(",")] if args.filter_kinds else None)
     qo = np.ascontiguousarray(qo, dtype=np.uint32)
+    q = len(qo) - 1  # --filter-kinds keeps only the chosen kinds' share of the queries
     t0 = time.perf_counter()
     eng.match_filter_view(qb, qo[:2])  # first call after the commit builds the index
     t_index = time.perf_counter() - t0

@@ -280,30 +280,60 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
         uint32_t wr[8];  // the query's first 8 words (qw is padded by 8 words on the device)
 #pragma unroll
         for (int i = 0; i < 8; i++) wr[i] = W[i];
+        // The window: lanes [0, nv) hold the records of keys wbase + lane.  A seek whose
+        // target lies inside it moves the window by shifting registers across lanes, not by
+        // reloading: a walk under a query '+' visits many small prefix groups one after the
+        // other, and most of its seeks land a few keys ahead.
+        uint32_t fr[RW] = {};
+        uint32_t FL = 0, nv = 0, wbase = 0;
         while (idx < K) {
             const uint32_t j = idx + lane;
-            int r = R_LOWER;  // past the end of the table: the walk stops there
+            const bool inr = j < K;
+            {  // keep what the previous window already holds
+                const uint32_t o = idx - wbase;
+                if (nv > o) {
+#pragma unroll
+                    for (int i = 0; i < (int)RW; i++) fr[i] = __shfl(fr[i], (int)(lane + o) & 63);
+                    FL = __shfl(FL, (int)(lane + o) & 63);
+                    nv -= o;
+                } else {
+                    nv = 0;
+                }
+                wbase = idx;
+            }
+            int r = R_LOWER;  // past the end of the table (or not loaded yet): a stop
             uint32_t spos = 0, sword = 0, qh = NONE_FW;
-            uint32_t fr[RW] = {};
-            uint32_t FL = 0;
-            const bool inr = j < K && j >= idx;
-            if (inr) {
-                FL = load_rec(a, j, fr);
-                r = cmp_filter(fr, a, j, FL, wr, W, WL, spos, sword, qh);
+            if (inr && lane < nv) r = cmp_filter(fr, a, j, FL, wr, W, WL, spos, sword, qh);
+            {
+                // the step is decided by its first event (a stop, or a '#'-run start); when
+                // that comes before the first key not held yet, nothing needs loading
+                const bool known = lane < nv || !inr;
+                const uint64_t ev = __ballot(known && (r == R_LOWER || r == R_SEEK || qh != NONE_FW));
+                const uint64_t unk = __ballot(!known);
+                const bool need = unk && (!ev || __ffsll((long long)unk) < __ffsll((long long)ev));
+                if (need) {
+                    if (inr && lane >= nv) {
+                        FL = load_rec(a, j, fr);
+                        r = cmp_filter(fr, a, j, FL, wr, W, WL, spos, sword, qh);
+                    }
+                    nv = 64;
+                }
             }
             // next(probe) from key lo = idx + from + 1: the lanes past `from` already hold
             // their records, so a target inside this window costs no memory round trip;
-            // past it, the wave searches from idx + 64 (keys past K count as the end)
+            // past it, the wave searches from the first key not held (keys past K count as
+            // the end)
             auto seek_from = [&](uint32_t from, const Probe &pb) -> uint32_t {
-                const bool ge = lane > from && (!inr || cmp_rec_probe(a, j, fr, FL, pb) >= 0);
+                const bool ge = lane > from && (!inr || (lane < nv && cmp_rec_probe(a, j, fr, FL, pb) >= 0));
                 const uint64_t gm = __ballot(ge);
-                if (gm) return min(idx + (uint32_t)__ffsll((long long)gm) - 1, K);
+                if (gm && (nv == 64 || __ffsll((long long)gm) - 1 < (int)nv)) return min(idx + (uint32_t)__ffsll((long long)gm) - 1, K);
+                const uint32_t lo = idx + nv;
                 // past the window: the target lies in the probe's prefix group, whose end is
                 // known per key (kend); a '#'-run's end (probe word +inf) IS that end
-                // (never below idx + 64, which the window just ruled out: the walk only moves on)
-                const uint32_t hi = min(max(prefix_end(a, pb.ks, pb.np), idx + 64), K);
+                // (never below lo, which the window just ruled out: the walk only moves on)
+                const uint32_t hi = min(max(prefix_end(a, pb.ks, pb.np), lo), K);
                 if (pb.w == NONE_FW && pb.np >= 1 && pb.np <= FW_END_DEPTHS) return hi;
-                return wave_seek(a, idx + 64, pb, lane, hi);
+                return wave_seek(a, lo, pb, lane, hi);
             };
             // the probe of a seek or run end from lane l: key idx+l's record words, no loads
             auto probe_from = [&](uint32_t l, uint32_t np, uint32_t w) {
