@@ -284,26 +284,36 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
         // target lies inside it moves the window by shifting registers across lanes, not by
         // reloading: a walk under a query '+' visits many small prefix groups one after the
         // other, and most of its seeks land a few keys ahead.
+        // The compare of a key depends on that key alone, so its result (r, spos, sword, qh)
+        // travels with the record.
         uint32_t fr[RW] = {};
         uint32_t FL = 0, nv = 0, wbase = 0;
+        int r = R_LOWER;  // past the end of the table (or not loaded yet): a stop
+        uint32_t spos = 0, sword = 0, qh = NONE_FW;
         while (idx < K) {
             const uint32_t j = idx + lane;
             const bool inr = j < K;
             {  // keep what the previous window already holds
                 const uint32_t o = idx - wbase;
                 if (nv > o) {
+                    const int src = (int)(lane + o) & 63;
 #pragma unroll
-                    for (int i = 0; i < (int)RW; i++) fr[i] = __shfl(fr[i], (int)(lane + o) & 63);
-                    FL = __shfl(FL, (int)(lane + o) & 63);
+                    for (int i = 0; i < (int)RW; i++) fr[i] = __shfl(fr[i], src);
+                    FL = __shfl(FL, src);
+                    r = __shfl(r, src);
+                    spos = __shfl(spos, src);
+                    sword = __shfl(sword, src);
+                    qh = __shfl(qh, src);
                     nv -= o;
                 } else {
                     nv = 0;
                 }
                 wbase = idx;
+                if (!inr || lane >= nv) {
+                    r = R_LOWER;
+                    qh = NONE_FW;
+                }
             }
-            int r = R_LOWER;  // past the end of the table (or not loaded yet): a stop
-            uint32_t spos = 0, sword = 0, qh = NONE_FW;
-            if (inr && lane < nv) r = cmp_filter(fr, a, j, FL, wr, W, WL, spos, sword, qh);
             {
                 // the step is decided by its first event (a stop, or a '#'-run start); when
                 // that comes before the first key not held yet, nothing needs loading
@@ -315,6 +325,13 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
                     if (inr && lane >= nv) {
                         FL = load_rec(a, j, fr);
                         r = cmp_filter(fr, a, j, FL, wr, W, WL, spos, sword, qh);
+                        // A seek whose probe prefix (the key's first spos words) no other key
+                        // shares lands on the next key: seek({Pos, W}) from key j returns a key
+                        // in (j, end of j's spos-word group], and that end is j + 1.  Such a
+                        // step is next(Cursor), like match_prefix.
+                        if (r == R_SEEK && spos >= 1 && spos <= FW_END_DEPTHS &&
+                            a.kend[(uint64_t)j * FW_END_DEPTHS + spos - 1] == j + 1)
+                            r = R_PREFIX;
                     }
                     nv = 64;
                 }
