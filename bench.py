@@ -308,6 +308,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: every CPU this process may use, see cpu_topology)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pin", action="store_true",
+                    help="leave the process on every CPU (default: pin to the GPU's own socket, "
+                         "emqx_amd/placement.py)")
     ap.add_argument("--batcher-seconds", type=float, default=2.0,
                     help="closed-loop load per publisher count through the batching aggregator (0: skip)")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no CPU baseline)")
@@ -355,6 +358,11 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
+    # Host placement: the engine's staging buffers, the host id arena the
+    # runs-form replies read and the aggregator's delivery threads live in host memory, so
+    # the rank runs on its GPU's socket; done before the workload and the engine allocate.
+    from emqx_amd import placement
+    placed = {"pinned": False, "reason": "--no-pin"} if args.no_pin else placement.pin_to_gpu(local)
 
     from emqx_amd import _native as N
     from emqx_amd import workloads
@@ -619,6 +627,7 @@ def main():
             "library": {"path": os.path.relpath(N.LIB_PATH, ROOT), "src_sha": lib_sha,
                         "build_info": N.load().tm_build_info().decode()},
             "build_s": round(t_build, 2),
+            "host_placement": placed,
             "host_peak_rss_gib": host_rss_gib(),
             "host_peak_rss_gib_max_over_ranks": round(float(rss.item()), 2),
             "replication": ({"mode": "one host master on rank 0, device image broadcast to replicas",

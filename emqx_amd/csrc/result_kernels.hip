@@ -18,6 +18,7 @@
 
 #include <algorithm>
 
+#include "copy_api.h"
 #include "device_api.h"
 #include "wave.h"
 
@@ -235,6 +236,36 @@ __global__ __launch_bounds__(CW_T) void k_compact_waves(const uint4 *wave_info, 
             }
         }
     }
+}
+
+// launch_copy_to_host: a grid-stride stream, 16-B loads and stores when source and
+// destination share their alignment (the head up to a 16-B boundary word by word), else
+// 4-B words; consecutive lanes write consecutive addresses, so each wave's stores leave the
+// chip as whole 256-B runs.
+__global__ __launch_bounds__(256) void k_copy_to_host(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src,
+                                                      uint64_t n) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (uint64_t)gridDim.x * blockDim.x;
+    const uintptr_t da = reinterpret_cast<uintptr_t>(dst), sa = reinterpret_cast<uintptr_t>(src);
+    if (((da ^ sa) & 15u) == 0) {
+        const uint64_t head = std::min<uint64_t>(((16u - (da & 15u)) & 15u) / 4u, n);
+        if (tid < head) dst[tid] = src[tid];
+        const uint64_t nv = (n - head) / 4;
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(src + head);
+        uint4 *d4 = reinterpret_cast<uint4 *>(dst + head);
+        for (uint64_t i = tid; i < nv; i += nt) d4[i] = s4[i];
+        const uint64_t t0 = head + nv * 4;
+        if (tid < n - t0) dst[t0 + tid] = src[t0 + tid];
+    } else {
+        for (uint64_t i = tid; i < n; i += nt) dst[i] = src[i];
+    }
+}
+
+hipError_t launch_copy_to_host(uint32_t *dst, const uint32_t *src, uint64_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint64_t want = (n / 4 + 255) / 256;
+    const uint32_t blocks = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, 2048));
+    k_copy_to_host<<<blocks, 256, 0, s>>>(dst, src, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_compact_waves(uint32_t id_bytes, const uint4 *wave_info, uint32_t nwaves, uint32_t tpw, uint32_t n,

@@ -20,7 +20,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "k_match_fast<false>"
+KERNEL = "k_match_fast<false, 0>"  # STATS off, keys output (the headline step)
 
 
 def per_kernel(path, kernel=KERNEL):
