@@ -285,3 +285,70 @@ def test_replica_matches_master_across_epochs_gpu():
     assert rep.stats()["n_keys"] == len(live_keys)
     rep.close()
     master.close()
+
+
+def _gpu_worker(rank, world, port, q):
+    """Mode 1 over gloo with REAL engines: rank 0 a master engine, rank 1 a replica built
+    from the broadcast image, both on the box's one GPU (the CPU tensors of gloo carry the
+    image and the patches)."""
+    import torch
+    import torch.distributed as dist
+    from emqx_amd.replica import EngineReplicaAdapter
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        w = workloads.generate("E", scale=0.02, n_topics=3000)
+        fl = w.filters()
+        eng = None
+        if rank == 0:
+            eng = N.Engine(0, record_patch=True)
+            eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+            eng.commit()
+        ad = EngineReplicaAdapter(0, eng)
+        rix = ReplicatedIndex(ad, rank, world)
+        rix.start()
+        out = [_sets(ad.eng, w)[1]]
+        kinds = []
+        # epoch 2: a delta epoch (patch); epoch 3: two commits before one sync (image)
+        if rank == 0:
+            eng.apply([(N.TM_OP_DEL, fl[k], int(w.f_id[k])) for k in range(0, len(fl), 25)]
+                      + [(N.TM_OP_ADD, b"#", 10**9), (N.TM_OP_ADD, b"+/+/+/+", 10**9 + 1)])
+            eng.commit()
+        kinds.append(rix.sync())
+        out.append(_sets(ad.eng, w)[1])
+        if rank == 0:
+            eng.apply([(N.TM_OP_ADD, b"b/+", 10**9 + 2)])
+            eng.commit()
+            eng.apply([(N.TM_OP_DEL, b"#", 10**9)])
+            eng.commit()
+        kinds.append(rix.sync())
+        kinds.append(rix.sync())
+        out.append(_sets(ad.eng, w)[1])
+        q.put((rank, out, kinds, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, None, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_replicated_gloo_world2_real_engines_gpu():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in ps], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+    for r in res:
+        assert r[3] is None, r[3]
+    (_, m_out, m_kinds, _), (_, r_out, r_kinds, _) = res
+    assert r_out == m_out  # the replica answers exactly as the master, every epoch
+    assert m_kinds == r_kinds == [ReplicatedIndex.SYNC_PATCH, ReplicatedIndex.SYNC_IMAGE, ReplicatedIndex.SYNC_NONE]
+    assert m_out[1] != m_out[0] and any(len(x) for x in m_out[1])
