@@ -51,7 +51,6 @@ extern "C" int tmx_batch_match_device(tm_engine *eng, const uint8_t *d_bytes, co
                                       uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out);
 extern "C" int tmx_result_ids64_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
                                        void *stream);
-extern "C" hipError_t tmx_d2h_words(void *host, void *host_dev, const void *src, uint64_t n, hipStream_t s);
 extern "C" int tmx_batch_match_ids(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                                    uint64_t total_bytes, uint32_t id_bytes, void *d_ids, uint64_t ids_cap,
                                    uint32_t *d_off_out, void *stream, tm_dev_result *out);
@@ -117,14 +116,12 @@ struct HBuf {
     void *p = nullptr;
     size_t cap = 0;
     bool pinned = true;
-    void *dev = nullptr;  // pinned: the buffer's device address (copy kernels write into it)
     void drop() {
         if (p) {
             if (pinned) (void)hipHostFree(p);
             else std::free(p);
         }
         p = nullptr;
-        dev = nullptr;
         cap = 0;
     }
     hipError_t ensure(size_t bytes) {
@@ -138,13 +135,7 @@ struct HBuf {
             return hipSuccess;
         }
         hipError_t e = hipHostMalloc(&p, c, hipHostMallocDefault);
-        if (e == hipSuccess) {
-            cap = c;
-            if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess) {
-                dev = nullptr;
-                (void)hipGetLastError();
-            }
-        }
+        if (e == hipSuccess) cap = c;
         return e;
     }
     template <class T>
@@ -625,8 +616,11 @@ struct tm_batcher {
         for (uint32_t j = 0; j < nch; j++) {
             const uint64_t a = oo[S.chunk_lo[j]], b = oo[S.chunk_lo[j + 1]];
             if (b > a)
-                BT_HIP(tmx_d2h_words(S.h_ids.as<uint8_t>() + a * w, S.h_ids.dev ? (uint8_t *)S.h_ids.dev + a * w : nullptr,
-                                     (const uint8_t *)S.d_ids.p + a * w, (b - a) * w / 4, s_copy));
+                // DMA, not launch_copy_to_host: a window's chunks are a few MB, and a copy kernel
+                // here competes with the next windows' walks (ids transport 45 -> 37 M/s at
+                // 65,536 publishers when it was tried)
+                BT_HIP(hipMemcpyAsync(S.h_ids.as<uint8_t>() + a * w, (const uint8_t *)S.d_ids.p + a * w, (b - a) * w,
+                                      hipMemcpyDeviceToHost, s_copy));
             BT_HIP(hipEventRecord(S.cev[j], s_copy));
         }
         S.cnt.resize(S.n);

@@ -136,14 +136,6 @@ static hipError_t d2h_words(const PinBuf &h, uint64_t at, const void *src, uint6
     return hipMemcpyAsync(h.as<uint32_t>() + at, src, n * 4, hipMemcpyDeviceToHost, s);
 }
 
-// the same for the batching aggregator's pinned buffers (batcher.cpp)
-extern "C" hipError_t tmx_d2h_words(void *host, void *host_dev, const void *src, uint64_t n, hipStream_t s) {
-    if (!n) return hipSuccess;
-    if (host_dev && n >= D2H_KERNEL_MIN_WORDS)
-        return launch_copy_to_host(static_cast<uint32_t *>(host_dev), static_cast<const uint32_t *>(src), n, s);
-    return hipMemcpyAsync(host, src, n * 4, hipMemcpyDeviceToHost, s);
-}
-
 // One set of per-batch device buffers and the counters sized from its batches' demand.
 struct BatchBufs {
     DevBuf d_bytes, d_off, d_outoff, d_outcnt, d_status, d_keys, d_slow_list, d_scr_w, d_scr_s, d_seg_pool, d_fr_pool,
@@ -3760,8 +3752,9 @@ int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *of
                 return TM_OK;
             }
             TM_TRY_HIP(hipStreamWaitEvent(c, eng->ev_pk[h], 0), TM_EDEVICE, "wait");
-            if (c_j > prev)
-                TM_TRY_HIP(d2h_words(o.r_runs, prev * 4, eng->bb->d_keys.as<uint8_t>() + prev * 16, (c_j - prev) * 4, c),
+            if (c_j > prev)  // DMA: a copy kernel here competes with the next sub-batch's walk
+                TM_TRY_HIP(hipMemcpyAsync(o.r_runs.as<uint8_t>() + prev * 16, eng->bb->d_keys.as<uint8_t>() + prev * 16,
+                                          (c_j - prev) * 16, hipMemcpyDeviceToHost, c),
                            TM_EDEVICE, "D2H");
             for (std::pair<PinBuf *, DevBuf *> pr :
                  {std::make_pair(&o.r_off, &eng->bb->d_outoff), std::make_pair(&o.r_cnt, &eng->bb->d_outcnt),
