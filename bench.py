@@ -491,6 +491,42 @@ def main():
     # digests must equal rank 0's (the master's own parity vs the oracle is checked at N = 1)
     replica_parity = replica_check(eng, all_b, all_o, min(20000, n), dev, backend, sp, world) if world > 1 else None
 
+    # ---------------------------------------------------------------- two batches in flight
+    # (not the metric): the same steps alternating the engine's two direct buffer sets on two
+    # streams (tm_match_device_set), so one batch's launch tail overlaps the next one's start;
+    # batch latency is then the time a batch shares the device with its neighbour
+    pipelined = None
+    if rank == 0 and not args.profile:
+        st2 = [stream, torch.cuda.Stream(dev)]
+
+        def step2(k):
+            return eng.match_device_set(k % 2, d_bytes.data_ptr(), d_off.data_ptr(), n, topic_bytes,
+                                        N.TM_MATCH_ALL, st2[k % 2].cuda_stream)
+        for k in range(4):
+            step2(k)
+        eng.device_sync(0)
+        eng.device_sync(1)  # sizes set 1's chunk pools to the batch's demand
+        r1 = step2(1)
+        eng.device_sync(1)
+        assert _read_u64(r1.d_total) <= r1.keys_cap
+        torch.cuda.synchronize()
+        ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            ev2[k][0].record(st2[k % 2])
+            step2(k)
+            ev2[k][1].record(st2[k % 2])
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t0
+        l2 = np.array([a.elapsed_time(b) for a, b in ev2])
+        pipelined = {"api": "tm_match_device_set, sets 0/1 alternating on two streams",
+                     "publishes_per_s": round(n * args.steps / el2, 1), "ms_per_step": round(el2 * 1e3 / args.steps, 4),
+                     "batch_ms_p50": round(float(np.percentile(l2, 50)), 4),
+                     "batch_ms_p99": round(float(np.percentile(l2, 99)), 4),
+                     "slow_topics": int(eng.stats()["n_slow_topics"])}
+        log(f"[rank 0] two batches in flight: {pipelined['publishes_per_s'] / 1e9:.3f} G publishes/s, "
+            f"{pipelined['ms_per_step']} ms per step, batch p50 {pipelined['batch_ms_p50']} ms")
+
     # ---------------------------------------------------------------- latency vs batch size
     # (not the metric: the batching window's trade-off); rank 0 only
     lat_sweep = []
@@ -628,6 +664,7 @@ def main():
                         "build_info": N.load().tm_build_info().decode()},
             "build_s": round(t_build, 2),
             "host_placement": placed,
+            "two_batches_in_flight": pipelined,
             "host_peak_rss_gib": host_rss_gib(),
             "host_peak_rss_gib_max_over_ranks": round(float(rss.item()), 2),
             "replication": ({"mode": "one host master on rank 0, device image broadcast to replicas",

@@ -62,7 +62,8 @@ EXPORTS = (
     "tm_match_filter_batch", "tm_intersect_batch", "tm_result_ids_device_ex", "tm_image_size", "tm_image_export",
     "tm_replica_create", "tm_replica_load", "tm_patch_size", "tm_patch_export", "tm_replica_apply_patch",
     "tm_discard_staged", "tm_result_release", "tm_match_batch_runs", "tm_runs_release", "tm_build_info",
-    "tm_match_ids_device", "tm_merge_shard_ids_device", "tm_debug_depth_stats",
+    "tm_match_ids_device", "tm_merge_shard_ids_device", "tm_debug_depth_stats", "tm_match_device_set",
+    "tm_device_sync_set",
 )
 # every symbol include/emqx_tm_batcher.h declares
 BATCHER_EXPORTS = (
@@ -193,6 +194,9 @@ def load() -> C.CDLL:
     lib.tm_match_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64,
                                     C.c_void_p, P(tm_dev_result)]
     lib.tm_device_sync.argtypes = [C.c_void_p]
+    lib.tm_device_sync_set.argtypes = [C.c_void_p, C.c_uint32]
+    lib.tm_match_device_set.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64,
+                                        C.c_uint32, C.c_void_p, P(tm_dev_result)]
     lib.tm_match_device_mode.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
                                          C.c_void_p, P(tm_dev_result)]
     lib.tm_reserve_matches.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32]
@@ -668,8 +672,17 @@ class Engine:
                                                   mode, C.c_void_p(stream) if stream else None, C.byref(r)))
         return r
 
-    def device_sync(self):
-        self._check(self.lib.tm_device_sync(self.h))
+    def match_device_set(self, dset: int, d_bytes: int, d_off: int, n: int, total_bytes: int,
+                         mode: int = TM_MATCH_ALL, stream: int = 0):
+        """tm_match_device_set: the batch on direct buffer set `dset` (0 or 1), so two
+        batches can be in flight on two streams."""
+        r = tm_dev_result()
+        self._check(self.lib.tm_match_device_set(self.h, dset, C.c_void_p(d_bytes), C.c_void_p(d_off), n, total_bytes,
+                                                 mode, C.c_void_p(stream) if stream else None, C.byref(r)))
+        return r
+
+    def device_sync(self, dset: int = 0):
+        self._check(self.lib.tm_device_sync_set(self.h, dset))
 
     def reserve_matches(self, keys_cap: int, topics: int = 0):
         self._check(self.lib.tm_reserve_matches(self.h, keys_cap, topics))

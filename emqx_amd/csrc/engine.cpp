@@ -546,6 +546,7 @@ struct tm_engine {
     // synchronous), so a host call from one thread never overwrites another thread's pending
     // device result.  `bb` is the set of the call in progress (under mu_dev).
     BatchBufs bb_dev, bb_host, bb_batch;  // bb_batch: the batching aggregator's windows (batcher.cpp)
+    BatchBufs bb_dev2;  // tm_match_device_set(.., 1, ..): a second direct batch in flight
     BatchBufs *bb = &bb_dev;
     double runs_spt = 4.0;     // spans per topic of the last runs batch (sizes the next)
     PinBuf h_rctl;             // runs: per sub-batch {span cursor, counter block}
@@ -2051,6 +2052,7 @@ void tm_destroy(tm_engine *eng) {
     eng->bb_dev.release();
     eng->bb_host.release();
     eng->bb_batch.release();
+    eng->bb_dev2.release();
     eng->h_rctl.release();
     for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
@@ -2226,6 +2228,7 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
     }
     if (eng->bb->keys_cap == 0) {
         uint64_t want = eng->cfg.reserve_matches ? eng->cfg.reserve_matches : std::max<uint64_t>(n * 8ull, 1 << 16);
+        if (eng->bb == &eng->bb_dev2) want = std::max(want, eng->bb_dev.keys_cap);  // starts at set 0's reservation
         TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, want * 4), TM_ENOMEM, "alloc");
         eng->bb->keys_cap = want;
     }
@@ -2718,11 +2721,17 @@ int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap) {
     if (!eng) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
-    eng->bb = &eng->bb_dev;  // the tm_match_device* path (host calls size their own output)
-    if (keys_cap > eng->bb->keys_cap) {
-        TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, keys_cap * 4), TM_ENOMEM, "alloc keys");
-        eng->bb->keys_cap = keys_cap;
+    // the tm_match_device* path (host calls size their own output); the second direct set
+    // once it is in use
+    for (BatchBufs *b : {&eng->bb_dev, &eng->bb_dev2}) {
+        if (b == &eng->bb_dev2 && !b->keys_cap) continue;
+        eng->bb = b;
+        if (keys_cap > eng->bb->keys_cap) {
+            TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, keys_cap * 4), TM_ENOMEM, "alloc keys");
+            eng->bb->keys_cap = keys_cap;
+        }
     }
+    eng->bb = &eng->bb_dev;
     (void)topics_cap;
     return TM_OK;
 }
@@ -2775,6 +2784,14 @@ int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t 
                          uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out) {
     return eng ? match_device_impl(eng, &eng->bb_dev, d_bytes, d_off, n, total_bytes, mode, stream, out) : TM_EINVAL;
 }
+static BatchBufs *direct_set(tm_engine *eng, uint32_t set) {
+    return !eng ? nullptr : set == 0 ? &eng->bb_dev : set == 1 ? &eng->bb_dev2 : nullptr;
+}
+int tm_match_device_set(tm_engine *eng, uint32_t set, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                        uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out) {
+    BatchBufs *b = direct_set(eng, set);
+    return b ? match_device_impl(eng, b, d_bytes, d_off, n, total_bytes, mode, stream, out) : TM_EINVAL;
+}
 // library-internal (batcher.cpp): the same on the aggregator's own buffer set, so its windows
 // never disturb a direct tm_match_device caller's pending result
 __attribute__((visibility("hidden"))) int tmx_batch_match_device(tm_engine *eng, const uint8_t *d_bytes,
@@ -2783,11 +2800,14 @@ __attribute__((visibility("hidden"))) int tmx_batch_match_device(tm_engine *eng,
     return match_device_impl(eng, &eng->bb_batch, d_bytes, d_off, n, total_bytes, mode, stream, out);
 }
 
-int tm_device_sync(tm_engine *eng) {
-    if (!eng) return TM_EINVAL;
+int tm_device_sync(tm_engine *eng) { return tm_device_sync_set(eng, 0); }
+
+int tm_device_sync_set(tm_engine *eng, uint32_t set) {
+    BatchBufs *b = direct_set(eng, set);
+    if (!b) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
-    eng->bb = &eng->bb_dev;
+    eng->bb = b;
     hipStream_t s = eng->bb->last_stream ? eng->bb->last_stream : eng->stream;
     TM_TRY_HIP(eng->h_cursor.ensure(64), TM_ENOMEM, "pinned alloc");
     uint8_t *h = (uint8_t *)eng->h_cursor.p;

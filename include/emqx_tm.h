@@ -71,7 +71,7 @@
 extern "C" {
 #endif
 
-#define TM_ABI_VERSION 7u
+#define TM_ABI_VERSION 8u
 
 /* status codes */
 #define TM_OK          0
@@ -296,6 +296,17 @@ int tm_device_sync(tm_engine *eng);
  * order code); tm_match_batch then reduces on the host. */
 int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                          uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out);
+/* Two device batches in flight (ABI 8).  tm_match_device_mode on direct buffer set `set`:
+ * 0 is tm_match_device's own set, 1 a second one with its own scratch and output, so a
+ * caller alternating sets on two streams overlaps one batch's tail with the next batch's
+ * start (a launch costs ~0.1 ms of ramp and tail at config C).  A set's
+ * result stays valid until that set's next batch.  tm_device_sync_set(eng, set) is
+ * tm_device_sync for that set; tm_reserve_matches grows both sets once set 1 is in use.
+ * No reference counterpart: the broker-side caller decides how many batches it keeps
+ * in flight (emqx_broker.erl:285-290 calls one publish at a time). */
+int tm_match_device_set(tm_engine *eng, uint32_t set, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+                        uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out);
+int tm_device_sync_set(tm_engine *eng, uint32_t set);
 int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap);
 
 /* Route ids of the last tm_match_device* batch (all keys, TM_MATCH_ALL), compacted topic-major on

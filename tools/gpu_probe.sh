@@ -1,8 +1,7 @@
 #!/bin/bash
-# round 3: FETCH/WRITE of the filter walk with window reuse
+# round 3: two direct buffer sets in flight with more hardware queues per process
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-bash tools/prof_filter_pmc.sh gpurun_out/r3w_filter_pmc > gpurun_out/r3w.log 2>&1
-rc=$?; cat gpurun_out/r3w.log; exit $rc
+GPU_MAX_HW_QUEUES=8 timeout -k 10 400 python -u bench.py --quick > gpurun_out/r3y_bench.json 2> gpurun_out/r3y_bench.err
+echo "bench rc=$?"
