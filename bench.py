@@ -26,6 +26,12 @@ import time
 
 import numpy as np
 
+# Two device batches in flight need their two streams on different hardware queues; HIP's
+# default is 4 queues per process, shared round-robin by every stream the process creates
+# (torch's, the engine's, the aggregator's), so the bench asks for 8.  Set before HIP starts.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -308,6 +314,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: every CPU this process may use, see cpu_topology)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sequential", action="store_true",
+                    help="one batch in flight (default: two, alternating the engine's two direct buffer "
+                         "sets on two streams; the sequential rate is reported beside either way)")
     ap.add_argument("--no-pin", action="store_true",
                     help="leave the process on every CPU (default: pin to the GPU's own socket, "
                          "emqx_amd/placement.py)")
@@ -431,6 +440,16 @@ def main():
     def step():
         return eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, topic_bytes, sp)
 
+    # the timed steps alternate the engine's two direct buffer sets on two streams
+    # (tm_match_device_set): step k+1's walk starts while step k's last waves finish
+    streams2 = [stream, torch.cuda.Stream(dev)]
+
+    def step2(k):
+        if args.sequential:
+            return step()
+        return eng.match_device_set(k % 2, d_bytes.data_ptr(), d_off.data_ptr(), n, topic_bytes, N.TM_MATCH_ALL,
+                                    streams2[k % 2].cuda_stream)
+
     # size the output arena from the first run (overflow -> grow -> rerun)
     r = step()
     eng.device_sync()  # also sizes the engine's chunk pools to this batch's demand
@@ -444,6 +463,14 @@ def main():
     for _ in range(max(0, args.warmup - 1)):
         step()
     eng.device_sync()
+    if not args.sequential:  # size set 1 (its chunk pools, its output) the same way
+        for k in range(max(2, args.warmup)):
+            step2(k)
+        eng.device_sync(0)
+        eng.device_sync(1)
+        r1 = step2(1)
+        eng.device_sync(1)
+        assert _read_u64(r1.d_total) <= r1.keys_cap
     torch.cuda.synchronize()
 
     # walk statistics for the algorithmic-byte count (one untimed, counted run)
@@ -462,9 +489,10 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
-        evs[k][0].record(stream)
-        step()
-        evs[k][1].record(stream)
+        sk = stream if args.sequential else streams2[k % 2]
+        evs[k][0].record(sk)
+        step2(k)
+        evs[k][1].record(sk)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     if world > 1:
@@ -491,41 +519,27 @@ def main():
     # digests must equal rank 0's (the master's own parity vs the oracle is checked at N = 1)
     replica_parity = replica_check(eng, all_b, all_o, min(20000, n), dev, backend, sp, world) if world > 1 else None
 
-    # ---------------------------------------------------------------- two batches in flight
-    # (not the metric): the same steps alternating the engine's two direct buffer sets on two
-    # streams (tm_match_device_set), so one batch's launch tail overlaps the next one's start;
-    # batch latency is then the time a batch shares the device with its neighbour
-    pipelined = None
-    if rank == 0 and not args.profile:
-        st2 = [stream, torch.cuda.Stream(dev)]
-
-        def step2(k):
-            return eng.match_device_set(k % 2, d_bytes.data_ptr(), d_off.data_ptr(), n, topic_bytes,
-                                        N.TM_MATCH_ALL, st2[k % 2].cuda_stream)
-        for k in range(4):
-            step2(k)
-        eng.device_sync(0)
-        eng.device_sync(1)  # sizes set 1's chunk pools to the batch's demand
-        r1 = step2(1)
-        eng.device_sync(1)
-        assert _read_u64(r1.d_total) <= r1.keys_cap
+    # ---------------------------------------------------------------- one batch in flight
+    # (beside the metric): the same steps on one buffer set and one stream, each batch alone on
+    # the device (its latency is the kernel's), rank 0
+    sequential = None
+    if rank == 0 and not args.profile and not args.sequential:
+        ev1 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
         torch.cuda.synchronize()
-        ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
         t0 = time.perf_counter()
         for k in range(args.steps):
-            ev2[k][0].record(st2[k % 2])
-            step2(k)
-            ev2[k][1].record(st2[k % 2])
+            ev1[k][0].record(stream)
+            step()
+            ev1[k][1].record(stream)
         torch.cuda.synchronize()
-        el2 = time.perf_counter() - t0
-        l2 = np.array([a.elapsed_time(b) for a, b in ev2])
-        pipelined = {"api": "tm_match_device_set, sets 0/1 alternating on two streams",
-                     "publishes_per_s": round(n * args.steps / el2, 1), "ms_per_step": round(el2 * 1e3 / args.steps, 4),
-                     "batch_ms_p50": round(float(np.percentile(l2, 50)), 4),
-                     "batch_ms_p99": round(float(np.percentile(l2, 99)), 4),
-                     "slow_topics": int(eng.stats()["n_slow_topics"])}
-        log(f"[rank 0] two batches in flight: {pipelined['publishes_per_s'] / 1e9:.3f} G publishes/s, "
-            f"{pipelined['ms_per_step']} ms per step, batch p50 {pipelined['batch_ms_p50']} ms")
+        el1 = time.perf_counter() - t0
+        l1 = np.array([a.elapsed_time(b) for a, b in ev1])
+        sequential = {"api": "tm_match_device, one stream", "publishes_per_s": round(n * args.steps / el1, 1),
+                      "ms_per_step": round(el1 * 1e3 / args.steps, 4),
+                      "p50_batch_ms": round(float(np.percentile(l1, 50)), 4),
+                      "p99_batch_ms": round(float(np.percentile(l1, 99)), 4)}
+        log(f"[rank 0] one batch in flight: {sequential['publishes_per_s'] / 1e9:.3f} G publishes/s, "
+            f"{sequential['ms_per_step']} ms per step, batch p99 {sequential['p99_batch_ms']} ms")
 
     # ---------------------------------------------------------------- latency vs batch size
     # (not the metric: the batching window's trade-off); rank 0 only
@@ -624,8 +638,11 @@ def main():
                 "route_keys": w.n_keys,
                 "publishes_per_step_per_gpu": n,
                 "matches_per_step_per_gpu": int(total),
-                "parallelism": f"replicated trie, dp{world}",
+                "parallelism": f"replicated trie, dp{world}"
+                               + ("" if args.sequential else ", 2 batches in flight per GPU"),
             },
+            # per-batch device time from enqueue to completion on its stream; with two batches
+            # in flight a batch shares the device with its neighbour (one_batch_in_flight: alone)
             "p50_batch_ms": round(float(np.percentile(lat_ms, 50)), 4),
             "p99_batch_ms": round(float(np.percentile(lat_ms, 99)), 4),
             "roofline": {
@@ -664,7 +681,8 @@ def main():
                         "build_info": N.load().tm_build_info().decode()},
             "build_s": round(t_build, 2),
             "host_placement": placed,
-            "two_batches_in_flight": pipelined,
+            "batches_in_flight": 1 if args.sequential else 2,
+            "one_batch_in_flight": sequential,
             "host_peak_rss_gib": host_rss_gib(),
             "host_peak_rss_gib_max_over_ranks": round(float(rss.item()), 2),
             "replication": ({"mode": "one host master on rank 0, device image broadcast to replicas",

@@ -1,7 +1,9 @@
 #!/bin/bash
-# round 3: two direct buffer sets in flight with more hardware queues per process
+# round 3: the default bench line with two batches in flight, then smoke
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
-GPU_MAX_HW_QUEUES=8 timeout -k 10 400 python -u bench.py --quick > gpurun_out/r3y_bench.json 2> gpurun_out/r3y_bench.err
-echo "bench rc=$?"
+timeout -k 10 500 python -u bench.py > gpurun_out/r3z_bench.json 2> gpurun_out/r3z_bench.err
+rc=$?; echo "bench rc=$rc"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3z_smoke.log 2>&1
+echo "smoke rc=$?"
