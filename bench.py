@@ -654,6 +654,10 @@ def main():
                 "traffic": traffic,
                 "kernel": "k_match_fast",
                 "kernel_ms": round(kernel_ms, 4),
+                # the same bytes per timed step (launch ramp and tail overlapped by the second
+                # batch in flight): what the device sustains, not one launch's rate
+                "achieved_per_step": round(alg_bytes / (elapsed / args.steps) / 1e9, 1),
+                "frac_per_step": round(alg_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": int(alg_bytes),
                 "traffic_source": (f"{os.path.relpath(prof[0], ROOT)}: FETCH_SIZE+WRITE_SIZE per launch "
                                    f"(upper bound {int(prof[1]['hbm_bytes_upper'])} if the key-arena stream "
