@@ -5,7 +5,7 @@
 set -o pipefail
 OUT=${1:-gpurun_out/prof}
 shift || true
-ARGS="--profile --steps 4 --warmup 1 $*"
+ARGS="--profile --sequential --steps 4 --warmup 1 $*"  # one launch at a time: per-kernel durations and counters
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 # which kernel source these counters belong to (bench.py only reports a matching profile)
