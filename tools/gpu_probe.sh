@@ -1,8 +1,8 @@
 #!/bin/bash
-# round 3: the N>1 path rehearsed on one GPU: 2 ranks over gloo (master + replica), two
-# batches in flight per rank
+# round 3: kernel trace + stats of the default step loop (two batches in flight)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
-EMQX_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 30 --warmup 3 > gpurun_out/r3g2_bench.json 2> gpurun_out/r3g2_bench.err
-echo "gloo2 rc=$?"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+GPU_MAX_HW_QUEUES=8 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3pp -o two -- python3 -u bench.py --quick --steps 50 > gpurun_out/r3pp_bench.json 2> gpurun_out/r3pp_bench.err
+echo "prof rc=$?"
