@@ -70,3 +70,46 @@ def test_two_direct_sets_in_flight():
     with pytest.raises(N.TMError):
         eng.match_device_set(2, halves[0][0].data_ptr(), halves[0][1].data_ptr(), halves[0][2], halves[0][3])
     eng.close()
+
+
+def test_two_direct_sets_on_a_replica():
+    """The same on a read replica made from the master's device image (mode 1's ranks > 0
+    run the bench's two-in-flight loop on replicas)."""
+    import torch
+    w = workloads.generate("E", scale=0.02, n_topics=12000)
+    master = N.Engine(0, record_patch=True)
+    master.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    master.commit()
+    size = master.image_size()
+    img = torch.empty(size, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    master.image_export(img.data_ptr(), size)
+    rep = N.Engine.replica_from_image(0, img.data_ptr(), img.numel())
+    del img
+    dev = torch.device("cuda", 0)
+    d_bytes = torch.from_numpy(w.t_bytes).to(dev)
+    d_off = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
+    n, nb = w.n_topics, int(w.t_off[-1])
+    off, cnt, hk, _ = master.match_packed(w.t_bytes, w.t_off)
+    master_ids = [np.sort(master.key_ids(hk[off[t]:off[t] + cnt[t]])) for t in range(n)]
+    rep.reserve_matches(int(cnt.sum()) + 1024)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    torch.cuda.synchronize()
+    rs = [rep.match_device_set(k, d_bytes.data_ptr(), d_off.data_ptr(), n, nb, N.TM_MATCH_ALL, streams[k].cuda_stream)
+          for k in range(2)]
+    rep.device_sync(0)
+    rep.device_sync(1)
+    assert rs[0].d_keys != rs[1].d_keys  # each set has its own output
+    for r in rs:
+        assert np.array_equal(_d2h_u32(r.d_cnt, n), cnt)
+    # route ids of set 0's batch (result_ids_device reads tm_match_device's set) equal the master's
+    ids_t = torch.zeros(int(cnt.sum()) + 1, dtype=torch.int64, device=dev)
+    ioff_t = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    rep.result_ids_device(ids_t.data_ptr(), ids_t.numel(), ioff_t.data_ptr())
+    torch.cuda.synchronize()
+    io = ioff_t.cpu().numpy().view(np.uint32)
+    v = ids_t.cpu().numpy().view(np.uint64)
+    for t in range(n):
+        assert np.array_equal(np.sort(v[io[t]:io[t + 1]]), master_ids[t]), t
+    rep.close()
+    master.close()
