@@ -41,25 +41,25 @@
 #include "../../include/emqx_tm_batcher.h"
 
 extern "C" int tmx_engine_device(const tm_engine *eng);  // engine.cpp, library-internal
-extern "C" int tmx_engine_grow_pools(tm_engine *eng, uint64_t seg_demand, uint64_t fr_demand);
-extern "C" void tmx_engine_pool_caps(const tm_engine *eng, uint64_t *seg_chunks, uint64_t *fr_chunks);
-extern "C" int tmx_result_ids32_device(tm_engine *eng, uint32_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
+extern "C" int tmx_engine_grow_pools(tm_engine *eng, uint32_t set, uint64_t seg_demand, uint64_t fr_demand);
+extern "C" void tmx_engine_pool_caps(const tm_engine *eng, uint32_t set, uint64_t *seg_chunks, uint64_t *fr_chunks);
+extern "C" int tmx_result_ids32_device(tm_engine *eng, uint32_t set, uint32_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
                                        void *stream);
 extern "C" void tmx_engine_lock(tm_engine *eng);
 extern "C" void tmx_engine_unlock(tm_engine *eng);
-extern "C" int tmx_batch_match_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+extern "C" int tmx_batch_match_device(tm_engine *eng, uint32_t set, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                                       uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out);
-extern "C" int tmx_result_ids64_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
+extern "C" int tmx_result_ids64_device(tm_engine *eng, uint32_t set, uint64_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
                                        void *stream);
-extern "C" int tmx_batch_match_ids(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+extern "C" int tmx_batch_match_ids(tm_engine *eng, uint32_t set, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                                    uint64_t total_bytes, uint32_t id_bytes, void *d_ids, uint64_t ids_cap,
                                    uint32_t *d_off_out, void *stream, tm_dev_result *out);
-extern "C" int tmx_batch_match_runs(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
+extern "C" int tmx_batch_match_runs(tm_engine *eng, uint32_t set, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                                     uint64_t total_bytes, void *stream, void *d_spans, uint64_t spans_cap,
                                     uint32_t *d_soff, uint32_t *d_scnt, uint32_t *d_kcnt, int32_t *d_status,
                                     unsigned long long *d_cursor, const void **d_ctl_out);
 extern "C" void tmx_lease_take(tm_engine *eng);
-extern "C" int tmx_batch_reserve_matches(tm_engine *eng, uint64_t keys_cap);
+extern "C" int tmx_batch_reserve_matches(tm_engine *eng, uint32_t set, uint64_t keys_cap);
 extern "C" void tmx_lease_drop(tm_engine *eng);
 extern "C" int tmx_engine_is_replica(const tm_engine *eng);
 
@@ -229,6 +229,7 @@ struct Slot {
     HBuf h_spans, h_soff, h_scnt, h_kcnt;
     uint64_t spans_cap = 0;
     const void *d_ctl = nullptr;
+    uint32_t set = 0;  // the engine buffer set and compute stream of this slot (slot index & 1)
 };
 
 }  // namespace
@@ -255,7 +256,9 @@ struct tm_batcher {
                      eng ? tm_last_error(eng) : "custom backend", bt_err[0] ? "; " : "", bt_err);
     }
     bool runs_ok = false;        // runs transport in use (TM_MATCH_ALL windows of a master engine)
-    hipStream_t s_comp = nullptr, s_copy = nullptr;
+    // two compute streams, each with its own engine buffer set: consecutive windows alternate,
+    // so one window's walk starts while the previous one's last waves finish
+    hipStream_t s_comps[2] = {}, s_copy = nullptr;
     int device = 0;
 
     Slot slot[NSLOT_MAX];
@@ -386,6 +389,7 @@ struct tm_batcher {
         const uint32_t n = S.n;
         S.host_done = false;
         if (S.runs) return enqueue_runs(S);
+        hipStream_t s_comp = s_comps[S.set];
         BT_HIP(hipSetDevice(device));
         BT_HIP(S.d_bytes.ensure(S.nbytes + 16));
         BT_HIP(S.d_off.ensure((size_t)n * 4 + 4));
@@ -404,11 +408,11 @@ struct tm_batcher {
             S.ids_cap = std::max<uint64_t>(S.ids_cap, std::max<uint64_t>((uint64_t)n * 8, 1 << 16));
             BT_HIP(S.d_ids.ensure(S.ids_cap * 8 + 8));
             S.narrow = true;
-            int rc = tmx_batch_match_ids(eng, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, 4,
+            int rc = tmx_batch_match_ids(eng, S.set, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, 4,
                                          S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp, &r);
             if (rc == TM_ESTATE) {
                 S.narrow = false;
-                rc = tmx_batch_match_ids(eng, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, 8,
+                rc = tmx_batch_match_ids(eng, S.set, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, 8,
                                          S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp, &r);
             }
             if (rc) return rc;
@@ -420,7 +424,7 @@ struct tm_batcher {
             BT_HIP(hipEventRecord(S.ev, s_comp));
             return TM_OK;
         }
-        int rc = tmx_batch_match_device(eng, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes,
+        int rc = tmx_batch_match_device(eng, S.set, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes,
                                         S.mode, s_comp, &r);
         if (rc) return rc;
         S.keys_cap = r.keys_cap;
@@ -433,10 +437,10 @@ struct tm_batcher {
             S.ids_cap = S.mode == TM_MATCH_FIRST ? n : r.keys_cap;
             BT_HIP(S.d_ids.ensure(S.ids_cap * 8 + 8));
             // u32 ids while they fit: half the PCIe bytes, the bottleneck of this path
-            rc = tmx_result_ids32_device(eng, (uint32_t *)S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp);
+            rc = tmx_result_ids32_device(eng, S.set, (uint32_t *)S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp);
             S.narrow = rc == TM_OK;
             if (rc == TM_ESTATE)
-                rc = tmx_result_ids64_device(eng, (uint64_t *)S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp);
+                rc = tmx_result_ids64_device(eng, S.set, (uint64_t *)S.d_ids.p, S.ids_cap, (uint32_t *)S.d_off_out.p, s_comp);
             if (rc) return rc;
             BT_HIP(hipMemcpyAsync(S.h_off_out.p, S.d_off_out.p, (size_t)n * 4 + 4, hipMemcpyDeviceToHost, s_comp));
         }
@@ -450,6 +454,7 @@ struct tm_batcher {
     // compute stream, the spans themselves on the copy stream once their count is known.
     int enqueue_runs(Slot &S) {
         const uint32_t n = S.n;
+        hipStream_t s_comp = s_comps[S.set];
         BT_HIP(hipSetDevice(device));
         BT_HIP(S.d_bytes.ensure(S.nbytes + 16));
         BT_HIP(S.d_off.ensure((size_t)n * 4 + 4));
@@ -465,7 +470,7 @@ struct tm_batcher {
         }
         BT_HIP(hipMemcpyAsync(S.d_bytes.p, S.h_bytes.p, S.nbytes + 1, hipMemcpyHostToDevice, s_comp));
         BT_HIP(hipMemcpyAsync(S.d_off.p, S.h_off.p, (size_t)n * 4 + 4, hipMemcpyHostToDevice, s_comp));
-        int rc = tmx_batch_match_runs(eng, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, s_comp,
+        int rc = tmx_batch_match_runs(eng, S.set, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, s_comp,
                                       S.d_spans.p, S.spans_cap, (uint32_t *)S.d_soff.p, (uint32_t *)S.d_scnt.p,
                                       (uint32_t *)S.d_kcnt.p, (int32_t *)S.d_st.p, (unsigned long long *)S.d_cur.p,
                                       &S.d_ctl);
@@ -489,12 +494,12 @@ struct tm_batcher {
         uint64_t total = ctl[0];
         const uint64_t seg = ctl[3], fr = ctl[4];
         uint64_t seg_cap = 0, fr_cap = 0;
-        tmx_engine_pool_caps(eng, &seg_cap, &fr_cap);
+        tmx_engine_pool_caps(eng, S.set, &seg_cap, &fr_cap);
         const bool over = total > S.spans_cap;
         if (over || seg > seg_cap || fr > fr_cap) {
             std::lock_guard<std::mutex> g(eng_mu);
-            BT_HIP(hipStreamSynchronize(s_comp));
-            int rc = tmx_engine_grow_pools(eng, seg, fr);
+            BT_HIP(hipStreamSynchronize(s_comps[S.set]));
+            int rc = tmx_engine_grow_pools(eng, S.set, seg, fr);
             if (rc) return rc;
             if (over) {  // more spans than the window's buffer: grow to the demand, run again
                 spans_per_pub = std::max(spans_per_pub, (double)total / std::max<uint32_t>(S.n, 1));
@@ -521,7 +526,7 @@ struct tm_batcher {
     // Synchronous; copies the result into the slot (engine memory is reused by the next call).
     int run_host(Slot &S) {
         S.narrow = false;
-        BT_HIP(hipStreamSynchronize(s_comp));  // nothing of ours in flight on the engine
+        for (hipStream_t sc : s_comps) BT_HIP(hipStreamSynchronize(sc));  // nothing of ours in flight on the engine
         tm_result res;
         int rc = tm_match_batch(eng, S.h_bytes.as<uint8_t>(), S.h_off.as<uint32_t>(), S.n, S.mode, &res);
         if (rc) return rc;
@@ -563,18 +568,18 @@ struct tm_batcher {
         const uint64_t total = ctl[0], seg = ctl[2], fr = ctl[3];
         const bool over = (S.mode != TM_MATCH_COUNT && S.mode != TM_MATCH_FIRST) && total > S.keys_cap;
         uint64_t seg_cap = 0, fr_cap = 0;
-        tmx_engine_pool_caps(eng, &seg_cap, &fr_cap);
+        tmx_engine_pool_caps(eng, S.set, &seg_cap, &fr_cap);
         if (over || seg > seg_cap || fr > fr_cap) {
             // pools sized to the demand for later windows (only when short: the engine compares)
             std::lock_guard<std::mutex> g(eng_mu);
-            BT_HIP(hipStreamSynchronize(s_comp));
-            int rc = tmx_engine_grow_pools(eng, seg, fr);
+            BT_HIP(hipStreamSynchronize(s_comps[S.set]));
+            int rc = tmx_engine_grow_pools(eng, S.set, seg, fr);
             if (rc) return rc;
             if (over) {  // output arena too small: grow to the demand, run this window again
                 const uint64_t want = total + total / 8 + 1024;
                 // a TM_MATCH_ALL window's walk writes ids: u64 ones take two words of the arena
                 const uint64_t words = S.mode == TM_MATCH_ALL && !S.narrow ? 2 * want : want;
-                if ((rc = tmx_batch_reserve_matches(eng, words))) return rc;
+                if ((rc = tmx_batch_reserve_matches(eng, S.set, words))) return rc;
                 if (S.mode == TM_MATCH_ALL) S.ids_cap = std::max(S.ids_cap, want);
                 if ((rc = enqueue(S))) return rc;
                 BT_HIP(hipEventSynchronize(S.ev));
@@ -949,12 +954,18 @@ struct tm_batcher {
             if (cfg.transport == TM_TRANSPORT_RUNS && !runs_ok) return TM_ESTATE;
             device = tmx_engine_device(eng);
             if (hipSetDevice(device) != hipSuccess ||
-                hipStreamCreateWithFlags(&s_comp, hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithFlags(&s_comps[0], hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithFlags(&s_comps[1], hipStreamNonBlocking) != hipSuccess ||
                 hipStreamCreateWithFlags(&s_copy, hipStreamNonBlocking) != hipSuccess)
                 return TM_EDEVICE;
-            for (Slot &S : slot)
-                for (hipEvent_t &e : S.cev)
+            // EMQX_TM_STREAMS=1: every window on one stream and one buffer set (A/B runs)
+            const char *es = std::getenv("EMQX_TM_STREAMS");
+            const uint32_t nstreams = es && std::atoi(es) == 1 ? 1u : 2u;
+            for (uint32_t i = 0; i < NSLOT_MAX; i++) {
+                slot[i].set = nstreams == 2 ? (i & 1u) : 0u;
+                for (hipEvent_t &e : slot[i].cev)
                     if (hipEventCreateWithFlags(&e, EV_FLAGS) != hipSuccess) return TM_EDEVICE;
+            }
         }
         try {
             for (uint32_t i = 0; i < n_delivery; i++) workers.emplace_back([this] { worker_loop(); });
@@ -994,7 +1005,8 @@ struct tm_batcher {
                 for (hipEvent_t e : S.cev)
                     if (e) (void)hipEventDestroy(e);
             }
-            if (s_comp) (void)hipStreamDestroy(s_comp);
+            for (hipStream_t sc : s_comps)
+                if (sc) (void)hipStreamDestroy(sc);
             if (s_copy) (void)hipStreamDestroy(s_copy);
         }
     }

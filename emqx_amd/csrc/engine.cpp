@@ -547,6 +547,8 @@ struct tm_engine {
     // device result.  `bb` is the set of the call in progress (under mu_dev).
     BatchBufs bb_dev, bb_host, bb_batch;  // bb_batch: the batching aggregator's windows (batcher.cpp)
     BatchBufs bb_dev2;  // tm_match_device_set(.., 1, ..): a second direct batch in flight
+    BatchBufs bb_batch2;  // the aggregator's second window set (its windows alternate sets and streams)
+    BatchBufs *batch_set(uint32_t set) { return set ? &bb_batch2 : &bb_batch; }
     BatchBufs *bb = &bb_dev;
     double runs_spt = 4.0;     // spans per topic of the last runs batch (sizes the next)
     PinBuf h_rctl;             // runs: per sub-batch {span cursor, counter block}
@@ -2052,6 +2054,7 @@ void tm_destroy(tm_engine *eng) {
     eng->bb_dev.release();
     eng->bb_host.release();
     eng->bb_batch.release();
+    eng->bb_batch2.release();
     eng->bb_dev2.release();
     eng->h_rctl.release();
     for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
@@ -2085,17 +2088,17 @@ __attribute__((visibility("hidden"))) int tmx_engine_device(const tm_engine *eng
 static int grow_pools(tm_engine *eng);
 // library-internal (batcher.cpp): size the chunk pools to a batch's demand (the counter
 // block the batcher copied back); no kernel of this engine may be in flight
-__attribute__((visibility("hidden"))) void tmx_engine_pool_caps(const tm_engine *eng, uint64_t *seg_chunks,
+__attribute__((visibility("hidden"))) void tmx_engine_pool_caps(const tm_engine *eng, uint32_t set, uint64_t *seg_chunks,
                                                                uint64_t *fr_chunks) {
     std::lock_guard<std::recursive_mutex> g(const_cast<tm_engine *>(eng)->mu_dev);
-    const_cast<tm_engine *>(eng)->bb = const_cast<BatchBufs *>(&eng->bb_batch);
+    const_cast<tm_engine *>(eng)->bb = const_cast<tm_engine *>(eng)->batch_set(set);
     *seg_chunks = eng->cfg.seg_chunks ? ~0ull : eng->bb->seg_chunks;  // fixed pools (test aid) never grow
     *fr_chunks = eng->cfg.seg_chunks ? ~0ull : eng->bb->fr_chunks;
 }
-__attribute__((visibility("hidden"))) int tmx_engine_grow_pools(tm_engine *eng, uint64_t seg_demand,
+__attribute__((visibility("hidden"))) int tmx_engine_grow_pools(tm_engine *eng, uint32_t set, uint64_t seg_demand,
                                                                 uint64_t fr_demand) {
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
-    eng->bb = &eng->bb_batch;
+    eng->bb = eng->batch_set(set);
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     eng->bb->seg_demand_last = seg_demand;
     eng->bb->fr_demand_last = fr_demand;
@@ -2794,10 +2797,10 @@ int tm_match_device_set(tm_engine *eng, uint32_t set, const uint8_t *d_bytes, co
 }
 // library-internal (batcher.cpp): the same on the aggregator's own buffer set, so its windows
 // never disturb a direct tm_match_device caller's pending result
-__attribute__((visibility("hidden"))) int tmx_batch_match_device(tm_engine *eng, const uint8_t *d_bytes,
+__attribute__((visibility("hidden"))) int tmx_batch_match_device(tm_engine *eng, uint32_t set, const uint8_t *d_bytes,
                                                                  const uint32_t *d_off, uint32_t n, uint64_t total_bytes,
                                                                  uint32_t mode, void *stream, tm_dev_result *out) {
-    return match_device_impl(eng, &eng->bb_batch, d_bytes, d_off, n, total_bytes, mode, stream, out);
+    return match_device_impl(eng, eng->batch_set(set), d_bytes, d_off, n, total_bytes, mode, stream, out);
 }
 
 int tm_device_sync(tm_engine *eng) { return tm_device_sync_set(eng, 0); }
@@ -2855,17 +2858,17 @@ int tm_result_ids_device_ex(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap, u
                             void *stream) {
     return eng ? result_ids_impl(eng, &eng->bb_dev, d_ids, ids_cap, d_off_out, d_flags, stream) : TM_EINVAL;
 }
-__attribute__((visibility("hidden"))) int tmx_result_ids64_device(tm_engine *eng, uint64_t *d_ids, uint64_t ids_cap,
-                                                                  uint32_t *d_off_out, void *stream) {
-    return result_ids_impl(eng, &eng->bb_batch, d_ids, ids_cap, d_off_out, nullptr, stream);
+__attribute__((visibility("hidden"))) int tmx_result_ids64_device(tm_engine *eng, uint32_t set, uint64_t *d_ids,
+                                                                  uint64_t ids_cap, uint32_t *d_off_out, void *stream) {
+    return result_ids_impl(eng, eng->batch_set(set), d_ids, ids_cap, d_off_out, nullptr, stream);
 }
 
 // library-internal (batcher.cpp): tm_result_ids_device with u32 ids, when every id ever
 // added is below 2^32 (TM_ESTATE otherwise)
-__attribute__((visibility("hidden"))) int tmx_result_ids32_device(tm_engine *eng, uint32_t *d_ids, uint64_t ids_cap,
-                                                                  uint32_t *d_off_out, void *stream) {
+__attribute__((visibility("hidden"))) int tmx_result_ids32_device(tm_engine *eng, uint32_t set, uint32_t *d_ids,
+                                                                  uint64_t ids_cap, uint32_t *d_off_out, void *stream) {
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
-    eng->bb = &eng->bb_batch;
+    eng->bb = eng->batch_set(set);
     if (eng->dv.max_id > 0xFFFFFFFFull || eng->replica || !eng->bb->dev_batch) return TM_ESTATE;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     hipStream_t s = stream ? (hipStream_t)stream : (eng->bb->last_stream ? eng->bb->last_stream : eng->stream);
@@ -2939,11 +2942,11 @@ int tm_match_ids_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *
                : TM_EINVAL;
 }
 // library-internal (batcher.cpp): the same on the aggregator's own buffer set
-__attribute__((visibility("hidden"))) int tmx_batch_match_ids(tm_engine *eng, const uint8_t *d_bytes,
+__attribute__((visibility("hidden"))) int tmx_batch_match_ids(tm_engine *eng, uint32_t set, const uint8_t *d_bytes,
                                                               const uint32_t *d_off, uint32_t n, uint64_t total_bytes,
                                                               uint32_t id_bytes, void *d_ids, uint64_t ids_cap,
                                                               uint32_t *d_off_out, void *stream, tm_dev_result *out) {
-    return match_ids_impl(eng, &eng->bb_batch, d_bytes, d_off, n, total_bytes, id_bytes, d_ids, ids_cap, d_off_out,
+    return match_ids_impl(eng, eng->batch_set(set), d_bytes, d_off, n, total_bytes, id_bytes, d_ids, ids_cap, d_off_out,
                           nullptr, stream, out);
 }
 
@@ -3829,7 +3832,7 @@ int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *of
 // buffers: spans (uint4 = tm_span) at d_spans, reserved from *d_cursor (zeroed here);
 // per-topic span offset / span count / id count / status.  *d_ctl_out: the launch's counter
 // block (pool demand).  The caller holds a lease (tmx_lease_take) until the spans are used.
-__attribute__((visibility("hidden"))) int tmx_batch_match_runs(tm_engine *eng, const uint8_t *d_bytes,
+__attribute__((visibility("hidden"))) int tmx_batch_match_runs(tm_engine *eng, uint32_t set, const uint8_t *d_bytes,
                                                                const uint32_t *d_off, uint32_t n, uint64_t total_bytes,
                                                                void *stream, void *d_spans, uint64_t spans_cap,
                                                                uint32_t *d_soff, uint32_t *d_scnt, uint32_t *d_kcnt,
@@ -3837,7 +3840,7 @@ __attribute__((visibility("hidden"))) int tmx_batch_match_runs(tm_engine *eng, c
                                                                const void **d_ctl_out) {
     if (eng->replica) return TM_ESTATE;
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
-    eng->bb = &eng->bb_batch;
+    eng->bb = eng->batch_set(set);
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
     TM_TRY_HIP(eng->chain_after_last(s), TM_EDEVICE, "stream order");
@@ -3855,9 +3858,9 @@ __attribute__((visibility("hidden"))) int tmx_batch_match_runs(tm_engine *eng, c
     return TM_OK;
 }
 // library-internal (batcher.cpp): tm_reserve_matches for the aggregator's buffer set
-__attribute__((visibility("hidden"))) int tmx_batch_reserve_matches(tm_engine *eng, uint64_t keys_cap) {
+__attribute__((visibility("hidden"))) int tmx_batch_reserve_matches(tm_engine *eng, uint32_t set, uint64_t keys_cap) {
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
-    eng->bb = &eng->bb_batch;
+    eng->bb = eng->batch_set(set);
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     if (keys_cap > eng->bb->keys_cap) {
         TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, keys_cap * 4), TM_ENOMEM, "alloc keys");

@@ -1,7 +1,8 @@
 """Batcher sweep on one GPU (bench tooling): config C engine, closed-loop publishers through
 tm_batcher_submit for each (publishers, delivery threads, max_wait_us[, transport, spans callback,
-slots, max_batch]) given, one JSON line each.
-Usage: python tools/batcher_gpu.py P:T:W[:TR:SP:NSLOT:MB] ...   (TR 0 auto/runs, 1 ids; SP 1 = span callback)"""
+slots, max_batch, compute streams]) given, one JSON line each.
+Usage: python tools/batcher_gpu.py P:T:W[:TR:SP:NSLOT:MB:ST] ...   (TR 0 auto/runs, 1 ids; SP 1 = span callback;
+ST 1 or 2 compute streams, EMQX_TM_STREAMS).  PIN=1 pins the process to the GPU's socket first."""
 import ctypes as C
 import json
 import os
@@ -17,6 +18,9 @@ def main():
 
     from emqx_amd import _native as N
     from emqx_amd import workloads as W
+    if os.environ.get("PIN"):
+        from emqx_amd import placement
+        print(json.dumps({"placement": placement.pin_to_gpu(0)}), flush=True)
     t0 = time.time()
     w = W.generate("C", scale=float(os.environ.get("SCALE", "1.0")), n_topics=1_000_000)
     eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
@@ -40,9 +44,10 @@ def main():
                           "publishes_per_s": round(len(to32) / 1 / min(ts) if False else (len(to32) - 1) / float(np.median(ts)))}),
               flush=True)
     for spec in sys.argv[1:]:
-        v = [int(x) for x in spec.split(":")] + [0, 0, 4, 65536][len(spec.split(":")) - 3:]
-        pubs, th, wait, tr, sp, nslot, mb = v[:7]
+        v = [int(x) for x in spec.split(":")] + [0, 0, 4, 65536, 2][len(spec.split(":")) - 3:]
+        pubs, th, wait, tr, sp, nslot, mb, nst = v[:8]
         os.environ["EMQX_TM_NSLOT"] = str(nslot)
+        os.environ["EMQX_TM_STREAMS"] = str(nst)
         b = N.Batcher(eng, max_batch=mb, max_wait_us=wait, delivery_threads=th, transport=tr)
         got, ids, errs, cs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
         rc = lg.loadgen_run2(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, 2.0, sp, C.byref(got),
@@ -50,7 +55,7 @@ def main():
         st = b.stats()
         b.close()
         print(json.dumps({"publishers": pubs, "threads": th, "max_wait_us": wait, "transport": tr, "spans": sp,
-                          "nslot": nslot, "max_batch": mb, "rc": rc, "errors": errs.value,
+                          "nslot": nslot, "max_batch": mb, "streams": nst, "rc": rc, "errors": errs.value,
                           "publishes_per_s": round(got.value / el.value), "ids_per_publish": round(ids.value / max(got.value, 1), 1),
                           "mean_batch": round(st["publishes"] / max(st["batches"], 1), 1),
                           "p50_ms": round(st["lat_p50_us"] / 1e3, 3), "p99_ms": round(st["lat_p99_us"] / 1e3, 3),

@@ -1,8 +1,13 @@
 #!/bin/bash
-# round 3: kernel trace + stats of the default step loop (two batches in flight)
+# round 3: aggregator A/B, one vs two compute streams, same process and box, pinned
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONUNBUFFERED=1
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-GPU_MAX_HW_QUEUES=8 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3pp -o two -- python3 -u bench.py --quick --steps 50 > gpurun_out/r3pp_bench.json 2> gpurun_out/r3pp_bench.err
-echo "prof rc=$?"
+S=""
+for rep in 1 2; do
+  for st in 1 2; do
+    S="$S 65536:13:200:0:0:6:65536:$st 65536:13:200:0:1:6:65536:$st 65536:13:200:1:0:6:65536:$st"
+  done
+done
+PIN=1 GPU_MAX_HW_QUEUES=8 timeout -k 10 500 python -u tools/batcher_gpu.py $S > gpurun_out/r3ab.jsonl 2> gpurun_out/r3ab.err
+echo "ab rc=$?"
