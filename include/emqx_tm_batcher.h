@@ -11,8 +11,9 @@
  *   window   a batch is dispatched when max_batch publishes are queued, or when the
  *            oldest queued publish has waited max_wait_us, or at tm_batcher_destroy
  *            (which drains the queue).  Six windows are in flight at once: the newest
- *            walks on the GPU while earlier windows' ids cross PCIe and the oldest's
- *            publishers are called back; under load windows grow by themselves.
+ *            walk on the GPU (consecutive windows on two streams, each with its own engine
+ *            buffer set, so their walks overlap) while earlier windows' ids cross PCIe and
+ *            the oldest's publishers are called back; under load windows grow by themselves.
  *   result   per publish: TM_TOPIC_OK with the ids of its matched keys (route dests,
  *            emqx_topic_index:get_id/1 of every key, emqx_topic_index.erl:87-89), or
  *            TM_BADARG with no ids (a level exactly "+" or "#": emqx_trie_search.erl:374-375),
