@@ -100,6 +100,10 @@ def _loadgen():
     lg.loadgen_run2.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double, C.c_int,
                                 C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                 C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+    from emqx_amd import _native as N
+    lg.loadgen_run3.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double, C.c_double,
+                                C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(N.tm_batcher_stats)]
     lg.spans_checksum.restype = C.c_uint64
     lg.spans_checksum.argtypes = [C.c_void_p, C.c_uint32]
     return lg
@@ -120,30 +124,46 @@ def batcher_load(eng, tb, to32, seconds):
     dt = max(2, min(14, cpu_topology()["usable_cpus"] - 3))  # leave the cutter, completer and caller a CPU
     plan = [(4096, N.TM_TRANSPORT_AUTO, 0), (65536, N.TM_TRANSPORT_AUTO, 0), (262144, N.TM_TRANSPORT_AUTO, 0),
             (65536, N.TM_TRANSPORT_AUTO, 1), (65536, N.TM_TRANSPORT_IDS, 0)]
+    warm = 0.5
     for pubs, transport, spans in plan:
         b = N.Batcher(eng, max_batch=65536, max_wait_us=200, delivery_threads=dt, transport=transport)
         got, ids, errs, cs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
-        rc = lg.loadgen_run2(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, seconds, spans,
-                             C.byref(got), C.byref(ids), C.byref(errs), C.byref(cs), C.byref(el))
+        win = N.tm_batcher_stats()
+        rc = lg.loadgen_run3(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, warm, seconds, spans,
+                             C.byref(got), C.byref(ids), C.byref(errs), C.byref(cs), C.byref(el), C.byref(win))
         st = b.stats()
         b.close()
-        if rc != 0 or errs.value:
+        if rc != 0 or errs.value or not win.lat_count:
             raise RuntimeError(f"batcher load failed: rc {rc}, {errs.value} failed publishes")
+        rate = win.lat_count / win.window_s  # publishes delivered in the steady-state window
+        little_ms = pubs / rate * 1e3        # closed loop: mean latency = publishers / throughput
+        mean_ms = win.lat_mean_us / 1e3
         runs.append({"publishers": pubs,
                      "transport": "runs" if transport != N.TM_TRANSPORT_IDS else "ids (u32 over PCIe)",
                      "callback": "spans (tm_batcher_submit_spans)" if spans else "id list (tm_batcher_submit)",
-                     "publishes_per_s": round(got.value / el.value, 1),
+                     "publishes_per_s": round(rate, 1),
+                     "publishes_per_s_whole_run": round(got.value / el.value, 1),
                      "ids_per_s": round(ids.value / el.value, 1),
                      "mean_batch": round(st["publishes"] / max(st["batches"], 1), 1),
-                     "lat_p50_ms": round(st["lat_p50_us"] / 1e3, 3), "lat_p99_ms": round(st["lat_p99_us"] / 1e3, 3),
+                     "lat_mean_ms": round(mean_ms, 3),
+                     "lat_p50_ms": round(win.lat_p50_us / 1e3, 3), "lat_p99_ms": round(win.lat_p99_us / 1e3, 3),
+                     "lat_p999_ms": round(win.lat_p999_us / 1e3, 3), "lat_max_ms": round(win.lat_max_us / 1e3, 3),
+                     "lat_sample": int(win.lat_count), "window_s": round(win.window_s, 3),
+                     "littles_law": {"publishers_over_rate_ms": round(little_ms, 3),
+                                     "mean_over_that": round(mean_ms / little_ms, 3),
+                                     "ok": bool(abs(mean_ms - little_ms) <= 0.2 * little_ms)},
                      "backend_frac": round(st["backend_us"] * 1e-6 / el.value, 3),
                      # share of the run's wall time each pipeline stage was busy (stages overlap)
                      "stage_busy": {k: round(st[k + "_us"] * 1e-6 / el.value, 3)
                                     for k in ("cut", "enqueue", "gpu_wait", "copy", "deliver")}})
+        if not runs[-1]["littles_law"]["ok"]:
+            log(f"batcher: latency mean {mean_ms:.3f} ms differs from publishers / rate {little_ms:.3f} ms by > 20%")
     return {"api": f"tm_batcher_submit (max_batch 65536, max_wait 200 us, {dt} delivery threads)", "runs": runs,
             "note": "closed loop: each publisher resubmits from its result callback, which reads every id once; "
                     "six windows in flight (GPU walk / PCIe / callbacks); runs transport: spans cross PCIe and "
                     "replies are read from the host id arena (one span: zero-copy; several: gathered); "
+                    f"rate and latency over a {seconds:g} s steady-state window after {warm:g} s of warm-up "
+                    "(every publish delivered in it, tm_batcher_stats_reset / _get), checked against Little's law; "
                     "stage_busy: share of wall time each stage worked (copy and deliver: per delivery thread)"}
 
 
@@ -202,22 +222,29 @@ def host_runs_leg(eng, tb, to32, n, w, reps=10):
     return out
 
 
-def gather_roof(walk, kernel_ms):
+def gather_roof(walk, kernel_ms, table_bytes):
     """The walk's second ceiling: independent random 16-B requests (edge + word probes).
     tools/gather_roof.hip measured what one MI355X serves with nothing dependent between
-    loads (profiles/*gather_roof.jsonl, 4 GiB table = the size of the config-C edge table)."""
+    loads, per table size (profiles/*gather_roof.jsonl); the row used is the one measured at
+    the engine's allocated edge-table size (the smallest measured table >= it, else the
+    largest): 16 GiB at config C (edge load 1/16), where random misses are served at ~39 G/s
+    against ~49 G/s from a 4 GiB table."""
     import glob
     ceil = None
+    want_mib = table_bytes / 2**20
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*gather_roof.jsonl"))):
         rows = [json.loads(x) for x in open(p) if x.strip().startswith("{")]
-        big = [r["G_loads_per_s"] for r in rows if r.get("table_MiB") == 4096]
-        if big:
-            ceil = (os.path.relpath(p, ROOT), max(big))
+        sizes = sorted({r["table_MiB"] for r in rows if "table_MiB" in r})
+        if not sizes:
+            continue
+        pick = next((m for m in sizes if m >= want_mib), sizes[-1])
+        ceil = (os.path.relpath(p, ROOT), max(r["G_loads_per_s"] for r in rows if r.get("table_MiB") == pick), pick)
     probes = walk["edge_probes"] + walk["word_probes"]
     rate = probes / (kernel_ms * 1e-3) / 1e9
-    out = {"probes_per_launch": probes, "achieved_G_probes_per_s": round(rate, 2)}
+    out = {"probes_per_launch": probes, "achieved_G_probes_per_s": round(rate, 2),
+           "edge_table_MiB": round(want_mib, 1)}
     if ceil:
-        out.update({"ceiling_G_loads_per_s": ceil[1], "source": ceil[0]})
+        out.update({"ceiling_G_loads_per_s": ceil[1], "ceiling_table_MiB": ceil[2], "source": ceil[0]})
         # request model: every L2 miss at the random-miss rate, every L2 hit at the
         # L2-resident random rate (2 MiB table), the key writes at the stream rate; the
         # L2 hit/miss request counts come from the PMC profile of this kernel source
@@ -302,6 +329,68 @@ def host_rss_gib():
     return round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2**20, 2)
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_cmd(argv, gpus, port):
+    """The command that starts `gpus` ranks of this bench, one process per GPU, with the same
+    arguments (torch.distributed.run on one node, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def world_plan(gpus, env):
+    """What this process is, before anything touches the GPU: ("launch", N) when no launcher
+    started it and N > 1 ranks are asked for (the parent starts N fresh rank processes and
+    relays rank 0's line), ("rank", world) when a launcher did (WORLD_SIZE must equal
+    --gpus), ("single", 1) otherwise."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return ("launch", gpus) if gpus > 1 else ("single", 1)
+    if int(ws) != gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} set by the launcher but --gpus {gpus}: refusing to "
+                         f"report a {ws}-rank run as {gpus} GPUs")
+    return ("rank", int(ws))
+
+
+def launch_ranks(argv, gpus):
+    """Parent of an N-rank run started without a launcher: no GPU call happens here; the ranks
+    are child processes (their stdout, where rank 0 prints the JSON line, is this process's)."""
+    import subprocess
+    cmd = launcher_cmd(argv, gpus, _free_port())
+    log(f"bench.py: starting {gpus} ranks: {' '.join(cmd)}")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check():
+    """--launch-check: each rank joins a gloo group and all-reduces its rank; rank 0 prints
+    one JSON line (CPU test of the launcher plumbing, no GPU)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "rank_sum": int(t.item()),
+                          "local_ranks": os.environ.get("LOCAL_WORLD_SIZE")}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -342,7 +431,14 @@ def main():
                          "generalised) walked on the GPU (tm_match_filter_batch), oracle beside it")
     ap.add_argument("--filter-kinds", default="", help="development: comma list of query kinds to keep "
                     "(0 stored filters, 1 one level '+', 2 prefix + '#')")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    # N ranks, one process per GPU: started here when no launcher did (before any GPU call)
+    kind, _ = world_plan(args.gpus, os.environ)
+    if kind == "launch":
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    if args.launch_check:
+        return launch_check()
     if args.filter_search:
         return run_filter(args)
     if args.mode == "sharded":
@@ -578,7 +674,9 @@ def main():
             ms = np.array([a.elapsed_time(b) for a, b in ev])
             mode_rates[mname] = {"ms_per_batch": round(float(np.mean(ms)), 4),
                                  "publishes_per_s": round(n / (float(np.mean(ms)) * 1e-3), 1)}
-        # host buffers in, host results out (H2D + kernels + D2H of every key): PCIe-inclusive
+    if rank == 0 and world == 1 and not args.profile:
+        # host buffers in, host results out (H2D + kernels + D2H of every key): PCIe-inclusive;
+        # N = 1 only (the N > 1 lines carry the metric and replica parity, the host legs once)
         to32 = np.ascontiguousarray(to, dtype=np.uint32)
         eng.match_packed_view(tb, to32)
         hl = []
@@ -602,7 +700,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile and not args.quick:
         cpu, parity = cpu_baseline(args, w, eng, tb, to, n)
     # the rest of the index API on the same engine, off the headline metric
-    legs = rank == 0 and not args.profile and not args.quick
+    legs = rank == 0 and world == 1 and not args.profile and not args.quick
     filt = filter_leg(args, w, eng, 20000) if legs else None
     inter = intersect_leg(w, tb, to) if legs else None
     # BASELINE.md's other per-config rows (E churn, B), and a forced full rebuild of the headline
@@ -666,7 +764,7 @@ def main():
                 "walk": walk,
                 "walk_by_depth": by_depth,
             },
-            "gather": gather_roof(walk, kernel_ms),
+            "gather": gather_roof(walk, kernel_ms, 16 * int(st["edge_slots"])),
             "latency_vs_batch": lat_sweep,
             "host_path": host_path,
             "host_path_runs": host_runs,
@@ -713,10 +811,19 @@ def run_sharded(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # EMQX_BENCH_BACKEND=gloo: several ranks on fewer GPUs (the exchange goes through host
+    # copies, shard.py _staged); the default is RCCL, one rank per GPU
+    backend = os.environ.get("EMQX_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    hdev = dev if backend != "gloo" else torch.device("cpu")  # where this group's host-side collectives run
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     t0 = time.time()
     # --shard-of G on one process: this rank holds shard 0 of a G-way split (the per-GPU
     # share of a G-GPU run) and the exchange is the identity
@@ -751,7 +858,7 @@ def run_sharded(args):
         el = time.perf_counter() - t_start
         if world > 1:
             dist.barrier()
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            t = torch.tensor([el], dtype=torch.float64, device=hdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
         if int(out[2].max().item()):
@@ -771,13 +878,19 @@ def run_sharded(args):
         m_own = int(o[0][-1].item()) if ex == "local" else None
         variants[ex] = {"ms_per_step": round(el / max(5, args.steps // 2) * 1e3, 4),
                         "publishes_per_s": round(n * max(5, args.steps // 2) / el, 1),
-                        "p99_batch_ms": round(float(np.percentile(lt, 99)), 4)}
+                        "p99_batch_ms": round(float(np.percentile(lt, 99)), 4),
+                        "wire_bytes": int(six.wire_bytes)}
         if ex == "local":
             variants[ex]["own_matches"] = m_own
             variants[ex]["d2h_bytes"] = hdr_b + m_own * six.id_bytes
     own = variants["local"]["own_matches"]
     if world > 1:
-        wire = {"measured_last_step": six.wire_bytes}
+        # the bytes each exchange moved into THIS rank in its last step (the sizes it sent and
+        # received: ids at the wire width + headers), max over ranks
+        mx = torch.tensor([variants[ex]["wire_bytes"] for ex in S.EXCHANGES], dtype=torch.int64, device=hdev)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        wire = {"measured_last_step_max_over_ranks": dict(zip(S.EXCHANGES, [int(x) for x in mx.tolist()])),
+                "bound_(G-1)/G*sumM*id_bytes": int((G - 1) / G * matches * six.id_bytes)}
     else:  # one rank holding 1/G: what a G-rank exchange would move into each rank
         wire = {"model": f"{G}-rank exchange from this shard's sizes (every shard assumed to match as many)",
                 "padded": (G - 1) * (six.stride * six.id_bytes + hdr_b),
@@ -785,9 +898,14 @@ def run_sharded(args):
                 "a2a": int((G - 1) / G * own * six.id_bytes) + (G - 1) * ((n // G + 1) * 4 + (G + 2) * 4),
                 "bound_(G-1)/G*sumM*4": int((G - 1) / G * (G * own) * 4),
                 "exact_ids_only": (G - 1) * own * six.id_bytes}
+    parity = sharded_parity(six, eng, w, d_bytes, d_off, n, tb, rank, world, hdev, min(n, 2000))
+    rss = torch.tensor([host_rss_gib()], dtype=torch.float64, device=hdev)
+    if world > 1:
+        dist.all_reduce(rss, op=dist.ReduceOp.MAX)
     if rank == 0:
         print(json.dumps({
-            "metric": METRIC, "value": round(n * args.steps / elapsed, 1), "unit": "publishes/s",
+            "metric": f"matched publishes/sec, filters hash-sharded over {nshards} GPU shard(s) (config {args.config})",
+            "value": round(n * args.steps / elapsed, 1), "unit": "publishes/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "u32",
@@ -799,10 +917,58 @@ def run_sharded(args):
             "p50_batch_ms": round(float(np.percentile(lat, 50)), 4),
             "p99_batch_ms": round(float(np.percentile(lat, 99)), 4),
             "id_bytes_on_wire": six.id_bytes, "stride_ids": six.stride,
-            "wire_bytes_per_rank": wire, "exchanges": variants,
+            "wire_bytes_per_rank": wire, "exchanges": variants, "parity": parity,
+            "host_peak_rss_gib_max_over_ranks": round(float(rss.item()), 2),
+            "backend": backend if world > 1 else None,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def sharded_parity(six, eng, w, d_bytes, d_off, n, tb, rank, world, hdev, ps):
+    """Parity of the sharded step on the first `ps` topics, in two parts that together pin it:
+    (1) each rank's own shard lists (the walk through the same C-ABI, host form) equal the
+    oracle over THAT shard's keys (w holds only this rank's keys); (2) the merged result of the
+    padded step equals, per topic, the union of every rank's shard lists (count and the sum of
+    a hash of the ids, all-gathered).  Shards are disjoint, so (1) + (2) = the unsharded set."""
+    import torch
+    import torch.distributed as dist
+    import oracle
+    tsub = np.ascontiguousarray(w.t_off[:ps + 1])
+    roff, rids, rst = six.shard.match_ids(w.t_bytes, tsub)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    eo, eids, est = ix.match(w.t_bytes, tsub, threads=8)
+    bad_local = int(np.sum(rst != est))
+    for t in range(ps):
+        if not np.array_equal(np.sort(rids[roff[t]:roff[t + 1]]), eids[eo[t]:eo[t + 1]]):
+            bad_local += 1
+
+    def digest(off, ids):
+        h = (ids.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(16)
+        cs = np.zeros(len(ids) + 1, np.uint64)
+        np.cumsum(h, out=cs[1:])
+        o = off.astype(np.int64)
+        return np.diff(o), (cs[o[1:]] - cs[o[:-1]]).view(np.int64)
+
+    c_loc, h_loc = digest(np.asarray(roff, np.int64), np.asarray(rids, np.uint64))
+    loc = torch.from_numpy(np.stack([c_loc, h_loc])).to(hdev)
+    if world > 1:
+        dist.all_reduce(loc)  # per topic: ids and hash sums over all shards (wrapping add)
+    off, ids, flags = six.match_device(eng, d_bytes.data_ptr(), d_off.data_ptr(), n, tb, exchange="padded")
+    torch.cuda.synchronize()
+    o = off[:ps + 1].cpu().numpy().view(np.uint32).astype(np.int64)
+    m = ids[:int(o[-1])].cpu().numpy().view(np.uint64)
+    c_m, h_m = digest(o - o[0], m[o[0]:])
+    lc = loc.cpu().numpy()
+    bad_merged = int(np.sum((c_m != lc[0]) | (h_m != lc[1]))) + (1 if int(flags.max().item()) else 0)
+    bad = torch.tensor([bad_local, bad_merged], dtype=torch.int64, device=hdev)
+    if world > 1:
+        dist.all_reduce(bad)
+    return {"sampled_topics": ps, "shard_lists_vs_oracle_mismatches": int(bad[0].item()),
+            "merged_vs_union_of_shards_mismatches": int(bad[1].item()),
+            "oracle": "oracle/trie_search.cpp over each rank's shard keys",
+            "compared": "per topic: each shard's sorted ids vs the oracle; merged (padded) step vs the union of "
+                        "shards by count + hash sum"}
 
 
 def _new_filter(f, n):

@@ -50,6 +50,7 @@ def shared_id(group: int, member: int) -> int:
 
 TM_CFG_FORCE_SLOW = 1
 TM_CFG_RECORD_PATCH = 2
+TM_CFG_FAIL_HOST_CALLS = 4
 TM_RES_KEYS_OVERFLOW = 1
 TM_RES_IDS_OVERFLOW = 2
 
@@ -69,6 +70,7 @@ EXPORTS = (
 BATCHER_EXPORTS = (
     "tm_batcher_create", "tm_batcher_create_fn", "tm_batcher_destroy", "tm_batcher_submit", "tm_batcher_match",
     "tm_batcher_apply", "tm_batcher_commit", "tm_batcher_stats_get", "tm_batcher_submit_spans",
+    "tm_batcher_stats_reset",
 )
 
 
@@ -150,7 +152,9 @@ class tm_batcher_stats(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("publishes", C.c_uint64), ("max_batch_seen", C.c_uint64),
                 ("backend_us", C.c_uint64), ("lat_p50_us", C.c_double), ("lat_p99_us", C.c_double),
                 ("lat_max_us", C.c_double), ("cut_us", C.c_uint64), ("enqueue_us", C.c_uint64),
-                ("gpu_wait_us", C.c_uint64), ("copy_us", C.c_uint64), ("deliver_us", C.c_uint64)]
+                ("gpu_wait_us", C.c_uint64), ("copy_us", C.c_uint64), ("deliver_us", C.c_uint64),
+                ("lat_mean_us", C.c_double), ("lat_count", C.c_uint64), ("lat_p999_us", C.c_double),
+                ("window_s", C.c_double)]
 
 
 tm_match_cb = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.POINTER(C.c_uint64), C.c_uint32)
@@ -239,6 +243,7 @@ def load() -> C.CDLL:
     lib.tm_batcher_apply.argtypes = [C.c_void_p, P(tm_op), C.c_size_t]
     lib.tm_batcher_commit.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.tm_batcher_stats_get.argtypes = [C.c_void_p, P(tm_batcher_stats)]
+    lib.tm_batcher_stats_reset.argtypes = [C.c_void_p]
     for name in BATCHER_EXPORTS:
         if name != "tm_batcher_destroy":
             getattr(lib, name).restype = C.c_int
@@ -306,11 +311,11 @@ class Engine:
     def __init__(self, device: int = 0, *, force_slow: bool = False, reserve_keys: int = 0,
                  reserve_nodes: int = 0, reserve_matches: int = 0, seg_chunks: int = 0, edge_load_inv: int = 0,
                  topics_per_wave: int = 0, record_patch: bool = False, max_nodes: int = 0,
-                 max_list_words: int = 0, _image=None):
+                 max_list_words: int = 0, flags: int = 0, _image=None):
         self.lib = load()
         cfg = tm_config()
         cfg.device = device
-        cfg.flags = (TM_CFG_FORCE_SLOW if force_slow else 0) | (TM_CFG_RECORD_PATCH if record_patch else 0)
+        cfg.flags = (TM_CFG_FORCE_SLOW if force_slow else 0) | (TM_CFG_RECORD_PATCH if record_patch else 0) | flags
         cfg.reserve_keys = reserve_keys
         cfg.reserve_nodes = reserve_nodes
         cfg.reserve_matches = reserve_matches
@@ -778,6 +783,12 @@ class Batcher:
         if rc != TM_OK:
             raise TMError(rc, "tm_batcher_stats_get failed")
         return {k: getattr(st, k) for k, _ in tm_batcher_stats._fields_}
+
+    def reset_stats(self):
+        """Start a new latency window (tm_batcher_stats_reset)."""
+        rc = self.lib.tm_batcher_stats_reset(self.h)
+        if rc != TM_OK:
+            raise TMError(rc, "tm_batcher_stats_reset failed")
 
     def close(self):
         if getattr(self, "h", None):

@@ -57,11 +57,7 @@ def built_sha(lib_path: str):
 
 def build(force: bool = False, verbose: bool = True):
     tm = os.path.join(HERE, "libemqx_tm.so")
-    srcs = [os.path.join(CSRC, f) for f in ("engine.cpp", "batcher.cpp", "match_kernels.hip",
-                                            "result_kernels.hip", "filter_kernels.hip", "layout.h", "device_api.h", "filter_api.h",
-                                            "wave.h")]
-    srcs += [os.path.join(os.path.dirname(HERE), "include", h) for h in ("emqx_tm.h", "emqx_tm_batcher.h")]
-    sha = src_sha()
+    sha = src_sha()  # over TM_SRCS, the one list of the library's sources
     # rebuilt whenever the library's embedded source hash differs from the sources' (not mtimes:
     # the tree travels to the GPU box with its built library)
     if force or built_sha(tm) != sha:

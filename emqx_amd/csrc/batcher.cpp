@@ -33,6 +33,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -64,6 +65,14 @@ extern "C" void tmx_lease_drop(tm_engine *eng);
 extern "C" int tmx_engine_is_replica(const tm_engine *eng);
 
 namespace {
+// set on the delivery threads: the engine refuses a commit from a callback (it would wait for
+// the read lease of the very window being delivered) and lets a callback's own runs call take
+// a lease past a waiting commit
+thread_local int tl_delivering = 0;
+}  // namespace
+extern "C" __attribute__((visibility("hidden"))) int tmx_in_delivery(void) { return tl_delivering; }
+
+namespace {
 
 // The aggregator stamps every publish (submit -> callback latency), so its clock is on the
 // per-publish path: the TSC (invariant on the hosts this runs on; Linux uses it as the
@@ -92,6 +101,49 @@ uint64_t now_ns() {
     const uint64_t t = __builtin_ia32_rdtsc();
     return t > c.tsc0 ? (uint64_t)((double)(t - c.tsc0) * c.ns_per_tick) : 0;
 }
+
+// Submit -> callback latency of EVERY delivered publish since the last reset, as a log-linear
+// histogram (64 buckets per power of two: <= 1.6 % relative error), one per delivery thread so
+// a record is two plain stores; tm_batcher_stats_get sums them.  Round 3 kept the last 65,536
+// latencies in a ring, which at 60 M publishes/s held only the final millisecond of a run.
+constexpr uint32_t LAT_SUB = 6;
+constexpr uint32_t LAT_NB = 44u << LAT_SUB;  // up to 2^43 ns (~2.4 h): the top bucket clamps
+inline uint32_t lat_bucket(uint64_t ns) {
+    if (ns < (1u << LAT_SUB)) return (uint32_t)ns;
+    const uint32_t sh = (uint32_t)(63 - __builtin_clzll(ns)) - LAT_SUB;
+    return std::min<uint32_t>(LAT_NB - 1, ((sh + 1) << LAT_SUB) + (uint32_t)((ns >> sh) & ((1u << LAT_SUB) - 1)));
+}
+inline double lat_bucket_mid(uint32_t b) {  // the bucket's midpoint, ns
+    if (b < (1u << LAT_SUB)) return (double)b;
+    const uint32_t sh = (b >> LAT_SUB) - 1, m = b & ((1u << LAT_SUB) - 1);
+    return (double)(((uint64_t)(m + (1u << LAT_SUB)) << sh)) + (double)((1ull << sh) - 1) / 2.0;
+}
+struct alignas(64) LatHist {
+    std::atomic<uint64_t> gen{0};  // the reset generation these counts belong to
+    std::atomic<uint64_t> n{0}, sum_ns{0}, max_ns{0};
+    std::atomic<uint64_t> b[LAT_NB];
+    LatHist() {
+        for (auto &x : b) x.store(0, std::memory_order_relaxed);
+    }
+    // single writer (the owning delivery thread): relaxed load + store, no locked instruction
+    static void bump(std::atomic<uint64_t> &x, uint64_t d) {
+        x.store(x.load(std::memory_order_relaxed) + d, std::memory_order_relaxed);
+    }
+    void sync_gen(uint64_t g) {  // the owner clears its counts when a reset happened
+        if (gen.load(std::memory_order_relaxed) == g) return;
+        for (auto &x : b) x.store(0, std::memory_order_relaxed);
+        n.store(0, std::memory_order_relaxed);
+        sum_ns.store(0, std::memory_order_relaxed);
+        max_ns.store(0, std::memory_order_relaxed);
+        gen.store(g, std::memory_order_release);
+    }
+    void add(uint64_t ns) {
+        bump(b[lat_bucket(ns)], 1);
+        bump(n, 1);
+        bump(sum_ns, ns);
+        if (ns > max_ns.load(std::memory_order_relaxed)) max_ns.store(ns, std::memory_order_relaxed);
+    }
+};
 
 // grow-only device / pinned buffers
 struct DBuf {
@@ -165,7 +217,6 @@ struct Pending {
     uint64_t t0;  // submit time (ns)
 };
 
-constexpr size_t LAT_RING = 65536;
 constexpr size_t QUEUE_BYTES_MAX = 1ull << 31;
 constexpr uint32_t SHARDS = 16;
 #ifndef TM_NSLOT
@@ -284,8 +335,9 @@ struct tm_batcher {
     std::mutex st_mu;  // stats
     uint64_t n_batches = 0, n_pub = 0, max_seen = 0, backend_ns = 0;
     std::atomic<uint64_t> ns_cut{0}, ns_enq{0}, ns_gpu{0}, ns_copy{0}, ns_del{0};  // stage times
-    std::vector<uint32_t> lat_ns;
-    size_t lat_pos = 0, lat_n = 0;
+    std::unique_ptr<LatHist[]> lat;        // one per delivery thread
+    std::atomic<uint64_t> lat_gen{1};      // tm_batcher_stats_reset bumps it
+    std::chrono::steady_clock::time_point t_window;  // start of the stats window (under st_mu)
 
     // ------------------------------------------------------------------ submit side
     // No state shared by all submitters on this path: one shard lock (shards by submitting
@@ -659,9 +711,8 @@ struct tm_batcher {
         p.cb(p.ctx, st, nids ? flat.data() : nullptr, (uint32_t)nids);
     }
 
-    void deliver_range(Slot &S, uint32_t lo, uint32_t hi, int rc) {
-        std::vector<uint32_t> lats;
-        lats.reserve(hi - lo);
+    void deliver_range(Slot &S, uint32_t lo, uint32_t hi, int rc, LatHist &H) {
+        H.sync_gen(lat_gen.load(std::memory_order_acquire));
         if (S.runs && rc >= 0) {
             const tm_span *spans = S.h_spans.as<tm_span>();
             const uint32_t *so = S.h_soff.as<uint32_t>(), *sc = S.h_scnt.as<uint32_t>(), *kc = S.h_kcnt.as<uint32_t>();
@@ -683,15 +734,8 @@ struct tm_batcher {
                 if (st == TM_TOPIC_OK) reply(p, st, spans + so[i], sc[i], kc[i]);
                 else reply(p, st, nullptr, 0, 0);
                 if (((i - lo) & 15) == 0) now = now_ns();
-                const uint64_t d = now > p.t0 ? now - p.t0 : 0;
-                lats.push_back(d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d);
+                H.add(now > p.t0 ? now - p.t0 : 0);
             }
-            std::lock_guard<std::mutex> g(st_mu);
-            for (uint32_t x : lats) {
-                lat_ns[lat_pos] = x;
-                lat_pos = (lat_pos + 1) % LAT_RING;
-            }
-            lat_n = std::min(LAT_RING, lat_n + lats.size());
             return;
         }
         thread_local std::vector<uint64_t> wide;  // a narrowed window's ids, one publish at a time
@@ -725,15 +769,8 @@ struct tm_batcher {
                 }
             }
             if (((i - lo) & 15) == 0) now = now_ns();  // one clock read per 16 callbacks
-            const uint64_t d = now > p.t0 ? now - p.t0 : 0;
-            lats.push_back(d > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d);
+            H.add(now > p.t0 ? now - p.t0 : 0);
         }
-        std::lock_guard<std::mutex> g(st_mu);
-        for (uint32_t x : lats) {
-            lat_ns[lat_pos] = x;
-            lat_pos = (lat_pos + 1) % LAT_RING;
-        }
-        lat_n = std::min(LAT_RING, lat_n + lats.size());
     }
 
     static constexpr int SPIN = 256;  // polls (a few microseconds) before sleeping: the CPUs are a quota
@@ -795,7 +832,9 @@ struct tm_batcher {
         return true;
     }
 
-    void worker_loop() {
+    void worker_loop(uint32_t me) {
+        LatHist &H = lat[me];
+        tl_delivering = 1;
         Work w;
         while (next_work(w)) {
             Slot &S = slot[w.slot];
@@ -808,7 +847,7 @@ struct tm_batcher {
                 ns_copy.fetch_add(now_ns() - t0, std::memory_order_relaxed);  // waited on PCIe
             }
             const uint64_t td0 = now_ns();
-            deliver_range(S, w.lo, w.hi, rc);
+            deliver_range(S, w.lo, w.hi, rc, H);
             ns_del.fetch_add(now_ns() - td0, std::memory_order_relaxed);
             if (S.parts_left.fetch_sub(1, std::memory_order_acq_rel) == 1) free_slot(S);
         }
@@ -943,7 +982,10 @@ struct tm_batcher {
         if (cfg.mode > TM_MATCH_AGGRE) return TM_EINVAL;
         n_delivery = cfg.delivery_threads ? cfg.delivery_threads : 4;
         if (n_delivery > 64) return TM_EINVAL;
-        lat_ns.assign(LAT_RING, 0);
+        lat.reset(new (std::nothrow) LatHist[n_delivery]);
+        if (!lat) return TM_ENOMEM;
+        t_window = std::chrono::steady_clock::now();
+        (void)now_ns();  // calibrate the clock before the first publish is stamped
         if (const char *e = std::getenv("EMQX_TM_NSLOT")) nslot = std::max(2u, std::min(NSLOT_MAX, (uint32_t)std::atoi(e)));
         if (!eng)
             for (Slot &S : slot)
@@ -968,7 +1010,7 @@ struct tm_batcher {
             }
         }
         try {
-            for (uint32_t i = 0; i < n_delivery; i++) workers.emplace_back([this] { worker_loop(); });
+            for (uint32_t i = 0; i < n_delivery; i++) workers.emplace_back([this, i] { worker_loop(i); });
             completer = std::thread([this] { completer_loop(); });
             cutter = std::thread([this] { cutter_loop(); });
         } catch (...) {
@@ -1111,7 +1153,6 @@ int tm_batcher_commit(tm_batcher *b, uint64_t *epoch_out) {
 
 int tm_batcher_stats_get(tm_batcher *b, tm_batcher_stats *out) {
     if (!b || !out) return TM_EINVAL;
-    std::vector<uint32_t> lat;
     {
         std::lock_guard<std::mutex> g(b->st_mu);
         out->batches = b->n_batches;
@@ -1124,19 +1165,48 @@ int tm_batcher_stats_get(tm_batcher *b, tm_batcher_stats *out) {
         const uint64_t nt = std::max<size_t>(1, b->workers.size());  // per delivery thread
         out->copy_us = b->ns_copy / 1000 / nt;
         out->deliver_us = b->ns_del / 1000 / nt;
-        lat.assign(b->lat_ns.begin(), b->lat_ns.begin() + (ptrdiff_t)b->lat_n);
+        out->window_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - b->t_window).count();
     }
-    out->lat_p50_us = out->lat_p99_us = out->lat_max_us = 0;
-    if (!lat.empty()) {
-        auto pct = [&](double q) {
-            size_t k = std::min(lat.size() - 1, (size_t)(q * (double)(lat.size() - 1) + 0.5));
-            std::nth_element(lat.begin(), lat.begin() + (ptrdiff_t)k, lat.end());
-            return lat[k] / 1000.0;
-        };
-        out->lat_p50_us = pct(0.50);
-        out->lat_p99_us = pct(0.99);
-        out->lat_max_us = *std::max_element(lat.begin(), lat.end()) / 1000.0;
+    // every publish delivered since the last reset: the delivery threads' histograms of this
+    // generation (a thread that has not delivered since the reset holds none of its publishes)
+    const uint64_t g = b->lat_gen.load(std::memory_order_acquire);
+    std::vector<uint64_t> hist(LAT_NB, 0);
+    uint64_t n = 0, mx = 0;
+    double sum = 0;
+    for (uint32_t t = 0; t < b->n_delivery; t++) {
+        const LatHist &H = b->lat[t];
+        if (H.gen.load(std::memory_order_acquire) != g) continue;
+        for (uint32_t k = 0; k < LAT_NB; k++) hist[k] += H.b[k].load(std::memory_order_relaxed);
+        n += H.n.load(std::memory_order_relaxed);
+        sum += (double)H.sum_ns.load(std::memory_order_relaxed);
+        mx = std::max<uint64_t>(mx, H.max_ns.load(std::memory_order_relaxed));
     }
+    uint64_t hn = 0;
+    for (uint64_t x : hist) hn += x;  // read after n: a record in flight may be half counted
+    out->lat_count = hn;
+    out->lat_mean_us = n ? sum / (double)n / 1000.0 : 0;
+    out->lat_max_us = mx / 1000.0;
+    auto pct = [&](double q) {
+        if (!hn) return 0.0;
+        const uint64_t want = std::min<uint64_t>(hn - 1, (uint64_t)(q * (double)(hn - 1) + 0.5));
+        uint64_t seen = 0;
+        for (uint32_t k = 0; k < LAT_NB; k++) {
+            seen += hist[k];
+            if (seen > want) return lat_bucket_mid(k) / 1000.0;
+        }
+        return mx / 1000.0;
+    };
+    out->lat_p50_us = pct(0.50);
+    out->lat_p99_us = pct(0.99);
+    out->lat_p999_us = pct(0.999);
+    return TM_OK;
+}
+
+int tm_batcher_stats_reset(tm_batcher *b) {
+    if (!b) return TM_EINVAL;
+    std::lock_guard<std::mutex> g(b->st_mu);
+    b->lat_gen.fetch_add(1, std::memory_order_acq_rel);
+    b->t_window = std::chrono::steady_clock::now();
     return TM_OK;
 }
 

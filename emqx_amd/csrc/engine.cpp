@@ -40,6 +40,9 @@
 
 using namespace tmx;
 
+// batcher.cpp, library-internal: nonzero on an aggregator delivery thread (inside a callback)
+extern "C" int tmx_in_delivery(void);
+
 namespace {
 
 // key kinds (where the key hangs in the trie)
@@ -650,7 +653,10 @@ struct tm_engine {
     // ---- read leases on the host id arena (tm_match_batch_runs)
     void lease_take_raw() {
         std::unique_lock<std::mutex> lk(lease_mu);
-        lease_cv.wait(lk, [&] { return !lease_block; });
+        // writer preference, except on an aggregator delivery thread: the window it is calling
+        // back holds a lease a waiting commit needs dropped, so waiting there would never end
+        // (the arena cannot change under it while that window's lease is held anyway)
+        if (!tmx_in_delivery()) lease_cv.wait(lk, [&] { return !lease_block; });
         n_leases++;
     }
     void lease_drop_raw() {
@@ -2161,6 +2167,12 @@ int tm_apply_packed(tm_engine *eng, uint32_t op, const uint8_t *bytes, const uin
 int tm_commit_epoch(tm_engine *eng, uint64_t *epoch_out) {
     if (!eng) return TM_EINVAL;
     if (eng->replica) return replica_refuses(eng, "tm_commit_epoch");
+    if (tmx_in_delivery()) {
+        // a commit waits for every runs window's read lease, including the one whose callback
+        // this is: it would never return.  Stage with tm_apply here, commit from another thread.
+        eng->err = "tm_commit_epoch from an aggregator delivery callback (it would wait for its own window's lease)";
+        return TM_ESTATE;
+    }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     std::lock_guard<std::mutex> g(eng->mu_commit);
     HostOut *me = nullptr;
@@ -3658,6 +3670,9 @@ static uint32_t env_u32(const char *name, uint32_t dflt) {
     return v && *v ? (uint32_t)strtoul(v, nullptr, 10) : dflt;
 }
 
+static int match_runs_impl(tm_engine *eng, HostOut &o, const uint8_t *bytes, const uint32_t *off, uint32_t n,
+                           tm_runs_result *out);
+
 int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, tm_runs_result *out) {
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
     if (eng->replica) return replica_refuses(eng, "tm_match_batch_runs (spans point into the host id arena)");
@@ -3665,6 +3680,19 @@ int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *of
     HostOut &o = eng->out();
     eng->lease_drop(o);  // the previous result of this thread ends here
     eng->lease_take(o);  // waits while a commit changes the host copy
+    const int rc = match_runs_impl(eng, o, bytes, off, n, out);
+    // a failed call hands back no spans, so its caller has no reason to release them: the
+    // lease ends here (else every commit would wait for this thread's next runs call)
+    if (rc != TM_OK) eng->lease_drop(o);
+    return rc;
+}
+
+static int match_runs_impl(tm_engine *eng, HostOut &o, const uint8_t *bytes, const uint32_t *off, uint32_t n,
+                           tm_runs_result *out) {
+    if (eng->cfg.flags & TM_CFG_FAIL_HOST_CALLS) {
+        eng->err = "tm_match_batch_runs: failure injected (TM_CFG_FAIL_HOST_CALLS)";
+        return TM_EDEVICE;
+    }
     std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
     eng->bb = &eng->bb_host;
     memset(out, 0, sizeof(*out));

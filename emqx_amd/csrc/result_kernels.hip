@@ -390,7 +390,8 @@ __device__ __forceinline__ uint32_t first_topic_ending_after(const uint32_t *ro,
 template <class IdT>
 __global__ __launch_bounds__(MG_T) void k_merge_ranks(const uint32_t *roff, uint64_t stride, uint32_t G, uint32_t n,
                                                       const IdT *ids, ShardBases base, const uint32_t *off,
-                                                      uint64_t *out, uint64_t cap, uint32_t chunks_per_rank) {
+                                                      uint64_t *out, uint64_t cap, uint32_t chunks_per_rank,
+                                                      uint64_t max_total) {
     __shared__ uint32_t s_mark[MG_CH];  // 1 + the position where the topic covering it starts (0: none yet)
     __shared__ int64_t s_shift[MG_CH];  // at a topic's first position: its destination - source index
     __shared__ uint32_t s_part[MG_T];
@@ -399,7 +400,9 @@ __global__ __launch_bounds__(MG_T) void k_merge_ranks(const uint32_t *roff, uint
     for (uint64_t bc = blockIdx.x; bc < (uint64_t)G * chunks_per_rank; bc += gridDim.x) {
         const uint32_t r = (uint32_t)(bc / chunks_per_rank), c = (uint32_t)(bc % chunks_per_rank);
         const uint32_t *ro = roff + (uint64_t)r * stride;
-        const uint64_t total = ro[n];
+        // a rank that outgrew its id buffer (TM_RES_IDS_OVERFLOW: ro[n] > what it holds) is read
+        // only as far as the buffer goes; its step is flagged and the caller re-runs it
+        const uint64_t total = min((uint64_t)ro[n], max_total);
         const uint64_t i0 = (uint64_t)c * MG_CH;
         if (i0 >= total) continue;  // block-uniform
         const uint64_t i1 = min(i0 + MG_CH, total);
@@ -470,10 +473,10 @@ hipError_t launch_merge_shard_ids(uint32_t G, uint32_t n, const uint32_t *roff, 
     const uint32_t blocks = (uint32_t)std::min<uint64_t>((uint64_t)G * cpr, 16384);
     if (id_bytes == 4)
         k_merge_ranks<uint32_t><<<blocks, MG_T, 0, s>>>(roff, roff_stride, G, n, (const uint32_t *)ids, b, off, out, cap,
-                                                        cpr);
+                                                        cpr, max_total);
     else
         k_merge_ranks<uint64_t><<<blocks, MG_T, 0, s>>>(roff, roff_stride, G, n, (const uint64_t *)ids, b, off, out, cap,
-                                                        cpr);
+                                                        cpr, max_total);
     return hipGetLastError();
 }
 

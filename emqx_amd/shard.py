@@ -152,15 +152,26 @@ class ShardedIndex:
         return self.shard.commit()
 
     # ---- the collective part, shared by the host (gloo) and device (RCCL) paths
+    def _staged(self, hdr):
+        """A device step over a gloo group (rehearsing several ranks on one GPU): gloo moves
+        host tensors, so the exchange runs on host copies and its results go back to the device.
+        Over RCCL the device tensors go on the wire as they are."""
+        import torch.distributed as dist
+        return self.world > 1 and hdr.is_cuda and dist.get_backend(self.group) == "gloo"
+
     def _exchange(self, hdr, ids, n: int, exchange: str):
         """hdr: this rank's (n+2) i32 [offsets | flags]; ids: its ids buffer (>= its total, the
-        padded stride long for `padded`).  Returns (H (G, n+2) i32, Ids flat, bases)."""
+        padded stride long for `padded`).  Returns (H (G, n+2) i32, Ids flat, bases); Ids and
+        bases are None when a rank overflowed and the ids were not exchanged (exact)."""
         import torch
         import torch.distributed as dist
         G = self.world
         if G == 1:
             self.wire_bytes = 0
             return hdr.view(1, n + 2), ids, [0]
+        if self._staged(hdr):
+            H, Ids, bases = self._exchange(hdr.cpu(), ids.cpu(), n, exchange)
+            return H.to(hdr.device), (None if Ids is None else Ids.to(hdr.device)), bases
         H = torch.empty(G * (n + 2), dtype=hdr.dtype, device=hdr.device)
         dist.all_gather_into_tensor(H, hdr, group=self.group)
         H = H.view(G, n + 2)
@@ -171,8 +182,15 @@ class ShardedIndex:
             dist.all_gather_into_tensor(Ids, ids, group=self.group)
             self.wire_bytes = (G - 1) * (stride * eb + (n + 2) * 4)
             return H, Ids, [r * stride for r in range(G)]
-        # exact: the sizes are the headers' offsets[n] (one small D2H on a device path)
-        tot = [int(x) for x in H[:, n].to(torch.int64).cpu().tolist()]
+        # exact: the sizes are the headers' offsets[n] (one small D2H on a device path), read
+        # together with every rank's flags: a rank that outgrew its id buffer holds fewer ids
+        # than its offsets say, so on overflow EVERY rank skips the id exchange (a transfer sized
+        # from those offsets would never complete) and the caller sees the flag
+        hn = (H[:, n:n + 2].to(torch.int64) & 0xFFFFFFFF).cpu().tolist()
+        tot = [r[0] for r in hn]
+        if any(r[1] for r in hn):
+            self.wire_bytes = (G - 1) * (n + 2) * 4
+            return H, None, None
         bases = [0] * G
         for r in range(1, G):
             bases[r] = bases[r - 1] + tot[r - 1]
@@ -205,6 +223,9 @@ class ShardedIndex:
         rebased to 0 | flags], Ids, bases) for m = the range's topic count."""
         import torch
         import torch.distributed as dist
+        if self._staged(hdr):
+            H, Ids, bases = self._exchange_a2a(hdr.cpu(), ids.cpu(), n)
+            return H.to(hdr.device), (None if Ids is None else Ids.to(hdr.device)), bases
         G, me = self.world, self.rank
         T = [q * n // G for q in range(G + 1)]
         dev = hdr.device
@@ -212,15 +233,20 @@ class ShardedIndex:
         mine = torch.cat([hdr[:n + 1][Tt], hdr[n + 1:n + 2]])  # my offsets at the range bounds + flags
         B = torch.empty(G * (G + 2), dtype=hdr.dtype, device=dev)
         dist.all_gather_into_tensor(B, mine.contiguous(), group=self.group)
-        Bh = (B.view(G, G + 2)[:, :G + 1].to(torch.int64) & 0xFFFFFFFF).cpu().tolist()  # sizes: one host read
+        Bh = (B.view(G, G + 2).to(torch.int64) & 0xFFFFFFFF).cpu().tolist()  # sizes + flags: one host read
         flags = B.view(G, G + 2)[:, G + 1]
+        m = T[me + 1] - T[me]
+        if any(row[G + 1] for row in Bh):  # some rank overflowed: nobody exchanges (see _exchange)
+            self.wire_bytes = (G - 1) * (G + 2) * 4
+            H = torch.zeros(G, m + 2, dtype=hdr.dtype, device=dev)
+            H[:, m + 1] = flags
+            return H, None, None
         send = [Bh[me][q + 1] - Bh[me][q] for q in range(G)]
         recv = [Bh[q][me + 1] - Bh[q][me] for q in range(G)]
         lo = Bh[me][0]
         Ids = torch.empty(max(1, sum(recv)), dtype=ids.dtype, device=ids.device)
         dist.all_to_all_single(Ids[:sum(recv)], ids[lo:lo + sum(send)].contiguous(), recv, send, group=self.group)
         # every rank's offsets over my topic range, rebased to its slice's start
-        m = T[me + 1] - T[me]
         offs = torch.cat([hdr[T[q]:T[q + 1] + 1] - hdr[T[q]] for q in range(G)])
         O = torch.empty(G * (m + 1), dtype=hdr.dtype, device=dev)
         dist.all_to_all_single(O, offs, [m + 1] * G, [T[q + 1] - T[q] + 1 for q in range(G)], group=self.group)
@@ -297,7 +323,8 @@ class ShardedIndex:
                 raise
             idb = 8
         torch.cuda.synchronize()
-        t = torch.tensor([total, idb], dtype=torch.int64, device=dev)
+        gloo = self.world > 1 and dist.get_backend(self.group) == "gloo"
+        t = torch.tensor([total, idb], dtype=torch.int64, device="cpu" if gloo else dev)
         if self.world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         self.id_bytes = int(t[1].item())
@@ -329,6 +356,8 @@ class ShardedIndex:
         dev = torch.device("cuda", torch.cuda.current_device())
         G = H.shape[0]
         flags = H[:, n + 1].max().reshape(1)
+        if Ids is None:  # the exchange was skipped: a rank overflowed (flags != 0), nothing to merge
+            return torch.zeros(n + 1, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int64, device=dev), flags
         out_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
         cap = G * self.stride
         out_ids = torch.empty(cap, dtype=torch.int64, device=dev)

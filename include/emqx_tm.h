@@ -71,7 +71,7 @@
 extern "C" {
 #endif
 
-#define TM_ABI_VERSION 8u
+#define TM_ABI_VERSION 9u
 
 /* status codes */
 #define TM_OK          0
@@ -124,6 +124,8 @@ extern "C" {
 #define TM_CFG_FORCE_SLOW   1u  /* route every topic through the spill (slow) kernel: test aid */
 #define TM_CFG_RECORD_PATCH 2u  /* master of a replicated index: every commit records the device
                                    changes it made as an epoch patch (tm_patch_export) */
+#define TM_CFG_FAIL_HOST_CALLS 4u /* test aid: tm_match_batch_runs fails (TM_EDEVICE) after taking
+                                     its read lease, to check a failed call leaves no lease held */
 
 typedef struct tm_engine tm_engine;
 
@@ -342,7 +344,8 @@ int tm_match_ids_device(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *
 
 /* Filter-sharded merge over tm_match_ids_device results: rank r's d_off_out row (n+1 u32) at
  * d_roff + r * roff_stride, its ids (id_bytes each) at d_ids + base[r] elements (base: G
- * host values); max_rank_ids bounds every rank's id count (e.g. the padded stride).  Writes
+ * host values); max_rank_ids is what every rank's id buffer holds (e.g. the padded stride): a
+ * rank whose row counts more (it raised TM_RES_IDS_OVERFLOW) is read only that far.  Writes
  * the merged result as u64: topic i's ids are the concatenation of its slices from shard
  * 0..G-1 at d_out_ids[d_out_off[i] .. d_out_off[i+1]) (n+1 offsets).  One column-sum launch
  * and one rank-chunk-parallel copy; ids past out_cap are left unwritten.  G <= 64. */

@@ -28,6 +28,9 @@
  *            the ids (u32 while every id fits).
  *   writes   any thread may write the engine directly (tm_apply / tm_commit_epoch are safe
  *            beside the aggregator); tm_batcher_apply / tm_batcher_commit are the same calls.
+ *            A delivery callback may stage (tm_apply) but not commit: tm_commit_epoch and
+ *            tm_batcher_commit return TM_ESTATE there, since a commit waits for the read lease
+ *            of the window being delivered.
  *
  * Erlang binding: a NIF calls tm_batcher_submit with a callback that
  * enif_send()s the id list to the publishing pid, which waits in `receive`; the callback
@@ -88,12 +91,19 @@ typedef struct tm_batcher_stats {
     uint64_t publishes;
     uint64_t max_batch_seen;
     uint64_t backend_us;        /* wall time inside the engine / backend, summed  */
-    /* submit -> callback latency over the last (up to) 65536 publishes, microseconds */
+    /* submit -> callback latency of EVERY publish delivered since the batcher started or the
+     * last tm_batcher_stats_reset (a whole-run histogram, <= 1.6 % bucket error), microseconds */
     double   lat_p50_us, lat_p99_us, lat_max_us;
     /* per pipeline stage, microseconds summed over windows: cutting a window from the queue,
      * queueing its GPU part, waiting for the GPU part; then, averaged over the delivery
      * threads: waiting for ids still on PCIe, calling back */
     uint64_t cut_us, enqueue_us, gpu_wait_us, copy_us, deliver_us;
+    /* (ABI 9) the same window: mean latency, publishes delivered (the percentiles' sample),
+     * p99.9, and the window's length in seconds (steady clock) */
+    double   lat_mean_us;
+    uint64_t lat_count;
+    double   lat_p999_us;
+    double   window_s;
 } tm_batcher_stats;
 
 /* Over an engine: batches go through tm_match_device_mode on the engine's device and the
@@ -119,6 +129,10 @@ int tm_batcher_apply(tm_batcher *b, const tm_op *ops, size_t n);
 int tm_batcher_commit(tm_batcher *b, uint64_t *epoch_out);
 
 int tm_batcher_stats_get(tm_batcher *b, tm_batcher_stats *out);
+/* Starts a new latency window: the percentiles, mean and count cover publishes delivered from
+ * here on (a load generator resets after its warm-up and reads the stats before its drain).
+ * Stage times and batch counts are not reset. */
+int tm_batcher_stats_reset(tm_batcher *b);
 
 #ifdef __cplusplus
 }

@@ -233,6 +233,57 @@ def test_closed_loop_loadgen_over_python_backend():
     assert ids.value <= max(per) * got.value
 
 
+def test_latency_window_covers_every_publish_and_obeys_littles_law():
+    """tm_batcher_stats_reset / _get (ABI 9): the latency histogram covers every publish
+    delivered in the window (not the last 65,536), and in a closed loop its mean equals
+    publishers / throughput (Little's law) within the bench's 20 % check."""
+    import os
+    lib = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(__file__)), "tools", "libtm_loadgen.so"))
+    U = C.POINTER(C.c_uint64)
+    lib.loadgen_run3.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double, C.c_double,
+                                 C.c_int, U, U, U, U, C.POINTER(C.c_double), C.POINTER(N.tm_batcher_stats)]
+    tb, to = N.pack_topics([b"a/b", b"x/y/z", b"a", b"$SYS/a"])
+    calls = []
+
+    def slow(topics, mode):  # a backend with a real service time: windows of ~2 ms
+        time.sleep(0.002)
+        return _oracle_backend(ROUTES, calls)(topics, mode)
+
+    pubs = 128
+    b = N.Batcher(backend=slow, max_batch=4096, max_wait_us=200)
+    got, ids, errs, cs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
+    win = N.tm_batcher_stats()
+    rc = lib.loadgen_run3(b.h, tb.ctypes.data, to.ctypes.data, 4, pubs, 0.3, 1.0, 0, C.byref(got), C.byref(ids),
+                          C.byref(errs), C.byref(cs), C.byref(el), C.byref(win))
+    whole = b.stats()
+    b.close()
+    assert rc == 0 and errs.value == 0
+    assert 0.95 <= win.window_s <= 1.5
+    # the window saw a share of the run's publishes, far more than a handful
+    assert 0 < win.lat_count < got.value and win.lat_count > 10 * pubs
+    rate = win.lat_count / win.window_s
+    little_ms = pubs / rate * 1e3
+    assert abs(win.lat_mean_us / 1e3 - little_ms) <= 0.2 * little_ms, (win.lat_mean_us, little_ms)
+    # every window's service time (2 ms) is in every latency
+    assert 2000 <= win.lat_p50_us <= win.lat_p99_us <= win.lat_p999_us <= win.lat_max_us * 1.02
+    # after the drain, the whole window (no reset since) holds at least as many publishes
+    assert whole["lat_count"] >= win.lat_count
+
+
+def test_latency_histogram_without_reset_counts_all():
+    b = N.Batcher(backend=_oracle_backend(ROUTES), max_wait_us=100)
+    for t in (b"a/b", b"a", b"x/y/z") * 30:
+        b.match(t)
+    s = b.stats()
+    assert s["lat_count"] == 90 and s["lat_mean_us"] > 0 and s["lat_p50_us"] <= s["lat_max_us"] * 1.02
+    b.reset_stats()
+    s2 = b.stats()
+    assert s2["lat_count"] == 0 and s2["lat_p50_us"] == 0
+    b.match(b"a/b")
+    assert b.stats()["lat_count"] == 1
+    b.close()
+
+
 def test_batcher_pipeline_under_thread_sanitizer():
     """tests/native/batcher_tsan: the aggregator's threads (cutter, completion, delivery
     pool) and sharded submission under ThreadSanitizer, 8,192 closed-loop publishers over

@@ -304,3 +304,59 @@ def test_last_error_is_per_thread():
     assert b"apply_patch" in got["a"], got
     assert b"tm_replica_load" in eng.lib.tm_last_error(eng.h)
     eng.close()
+
+
+def test_failed_runs_call_holds_no_lease():
+    """A tm_match_batch_runs that fails after taking its read lease (TM_CFG_FAIL_HOST_CALLS,
+    test aid) hands back no spans, so it must not keep the lease: a commit from another
+    thread completes at once (before the fix it waited for this thread's next runs call)."""
+    w = workloads.generate("A", scale=0.05, n_topics=500)
+    eng = N.Engine(0, flags=N.TM_CFG_FAIL_HOST_CALLS)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    to32 = np.ascontiguousarray(w.t_off, dtype=np.uint32)
+    with pytest.raises(N.TMError) as e:
+        eng.match_runs_view(w.t_bytes, to32)
+    assert e.value.rc == N.TM_EDEVICE
+    done = threading.Event()
+
+    def writer():
+        eng.apply([(N.TM_OP_ADD, b"x/+/z", 7)])
+        eng.commit()
+        done.set()
+
+    th = threading.Thread(target=writer)
+    th.start()
+    th.join(timeout=30)
+    assert done.is_set(), "a commit waited for the lease of a failed runs call"
+    eng.close()
+
+
+def test_commit_from_delivery_callback_is_refused_not_deadlocked():
+    """A delivery callback of a runs window may stage writes but not commit: the commit would
+    wait for that window's own read lease.  tm_commit_epoch / tm_batcher_commit return
+    TM_ESTATE there; the staged op commits from the caller's thread afterwards."""
+    eng = N.Engine(0)
+    eng.apply([(N.TM_OP_ADD, b"a/+", 1)])
+    eng.commit()
+    b = N.Batcher(eng, max_batch=64, max_wait_us=200)
+    seen = {}
+    ev = threading.Event()
+    f = b"q/#"
+    op = N.tm_op(N.TM_OP_ADD, 0, N.C.cast(N.C.c_char_p(f), N.C.c_void_p), len(f), 0, 5)
+
+    @N.tm_match_cb
+    def cb(ctx, status, ids, n):
+        seen["ids"] = sorted(ids[i] for i in range(n))
+        seen["apply"] = eng.lib.tm_apply(eng.h, N.C.byref(op), 1)
+        seen["commit"] = eng.lib.tm_commit_epoch(eng.h, None)
+        seen["bcommit"] = b.lib.tm_batcher_commit(b.h, None)
+        ev.set()
+
+    assert b.lib.tm_batcher_submit(b.h, b"a/b", 3, cb, None) == N.TM_OK
+    assert ev.wait(30), "callback never ran"
+    assert seen == {"ids": [1], "apply": N.TM_OK, "commit": N.TM_ESTATE, "bcommit": N.TM_ESTATE}
+    eng.commit()  # from this thread: the op staged in the callback becomes visible
+    assert b.match(b"q/r") == (N.TM_TOPIC_OK, [5])
+    b.close()
+    eng.close()

@@ -377,3 +377,120 @@ def test_config_d_full_size_shard_properties_gpu():
         assert np.array_equal(got, eids[eo[t]:eo[t + 1]]), t
     eng.close()
     torch.cuda.synchronize()
+
+
+def _gpu_shard_worker(rank, world, port, q):
+    """Mode 2 across two ranks with REAL engines (both processes on the box's one GPU, gloo
+    carrying the exchange through host copies): each rank's EngineShard holds its
+    splitmix64(id) % 2 keys; every exchange runs the device step (walk writing route ids,
+    exchange, device merge) over two epochs, plus the host path; then a forced overflow on
+    rank 0 under exact and a2a must come back flagged on both ranks instead of hanging."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        w = workloads.generate("A", scale=0.5, n_topics=3000)
+        n, tb = w.n_topics, int(w.t_off[-1])
+        d_bytes = torch.from_numpy(w.t_bytes).to(dev)
+        d_off = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
+        eng = N.Engine(0)
+        six = S.ShardedIndex(S.EngineShard(eng), rank, world)
+        six.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+        six.commit()
+        res = {}
+
+        def run_all(tag):
+            for ex in S.EXCHANGES:
+                off, ids, flags = six.match_device(eng, d_bytes.data_ptr(), d_off.data_ptr(), n, tb, exchange=ex)
+                torch.cuda.synchronize()
+                o = off.cpu().numpy().view(np.uint32).copy()
+                if ex == "local":
+                    a = ids.numpy()
+                    got = a.view(np.uint32 if a.dtype == np.int32 else np.uint64).astype(np.uint64)[:int(o[-1])]
+                else:
+                    got = ids[:int(o[-1])].cpu().numpy().view(np.uint64).copy()
+                res[(tag, ex)] = (o, got, int(flags.max().item()), six.wire_bytes)
+            off, ids, st = six.match(w.t_bytes, w.t_off, exchange="exact")  # host path, same engines
+            res[(tag, "host_exact")] = (off, ids, 0, six.wire_bytes)
+            res[(tag, "status")] = st
+
+        run_all(1)
+        dm = np.arange(w.n_keys) % 7 == 0
+        b, o, i, _ = S.select_keys(w.f_bytes, w.f_off, w.f_id, dm)
+        six.apply_packed(N.TM_OP_DEL, b, o, i)
+        xb, xo = N.pack_topics([b"#", b"+/+/+/+"])
+        six.apply_packed(N.TM_OP_ADD, xb, xo.astype(np.uint64), np.array([10**9, 10**9 + 1], np.uint64))
+        six.commit()
+        six.stride = None  # sizes for the new epoch (collective, inside the next step)
+        run_all(2)
+        # rank 0's id buffer far too small: it raises TM_RES_IDS_OVERFLOW; exact and a2a must
+        # skip their exchange on BOTH ranks (sized from its offsets it would never complete)
+        keep = six.stride
+        for ex in ("exact", "a2a", "padded"):
+            if ex == "padded":
+                six.stride = 16  # both ranks: the padded all-gather needs one stride
+            elif rank == 0:
+                six.stride = 16
+            _, _, flags = six.match_device(eng, d_bytes.data_ptr(), d_off.data_ptr(), n, tb, exchange=ex)
+            torch.cuda.synchronize()
+            res[("overflow", ex)] = int(flags.max().item())
+            six.stride = keep
+        q.put((rank, res, None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_sharded_gloo_world2_real_engines_gpu():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gpu_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in ps], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+    for r in res:
+        assert r[2] is None, r[2]
+    w = workloads.generate("A", scale=0.5, n_topics=3000)
+    n = w.n_topics
+    eoff, eids, est, eoff2, eids2 = _reference(w)
+    ref = {1: (eoff, eids), 2: (eoff2, eids2)}
+    for rank, rr, _ in res:
+        for tag in (1, 2):
+            for ex in ("padded", "exact", "host_exact"):
+                off, ids, flags, _ = rr[(tag, ex)]
+                assert flags == 0
+                _same_sets(off, ids, *ref[tag])
+            assert np.array_equal(np.asarray(rr[(1, "status")]), est)
+            lo, hi = rank * n // 2, (rank + 1) * n // 2
+            off, ids, flags, _ = rr[(tag, "a2a")]
+            ro, ri = ref[tag]
+            assert flags == 0 and len(off) == hi - lo + 1
+            _same_sets(off, ids, ro[lo:hi + 1] - ro[lo], ri[ro[lo]:ro[hi]])
+        for ex in ("exact", "a2a", "padded"):
+            assert rr[("overflow", ex)] & N.TM_RES_IDS_OVERFLOW, (rank, ex)
+    for tag in (1, 2):
+        # local: each rank's own lists; their union per topic is the full result
+        lo = [np.asarray(rr[(tag, "local")][0], np.int64) for _, rr, _ in res]
+        li = [rr[(tag, "local")][1] for _, rr, _ in res]
+        ro, ri = ref[tag]
+        for t in range(n):
+            got = np.sort(np.concatenate([li[r][lo[r][t]:lo[r][t + 1]] for r in range(2)]))
+            assert np.array_equal(got, ri[ro[t]:ro[t + 1]]), (tag, t)
+        # exact moved the other rank's ids (u32 on the wire) + one header; a2a only its range
+        for rank, rr, _ in res:
+            other = lo[1 - rank]
+            assert rr[(tag, "exact")][3] == int(other[-1]) * 4 + (n + 2) * 4
+            a, b = rank * n // 2, (rank + 1) * n // 2
+            assert rr[(tag, "a2a")][3] == int(other[b] - other[a]) * 4 + ((b - a + 1) * 4 + 4 * 4)

@@ -8,8 +8,10 @@
 // (tm_batcher_submit_spans) and reads the ids straight from the engine's id arena.
 #include <atomic>
 #include <chrono>
+#include <climits>
 #include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../include/emqx_tm_batcher.h"
@@ -30,7 +32,7 @@ struct Load {
     const uint8_t *bytes;
     const uint32_t *off;
     uint32_t n_topics;
-    std::chrono::steady_clock::time_point deadline;
+    std::atomic<int64_t> deadline{INT64_MAX};  // steady_clock ticks; the main thread may move it
     std::atomic<uint32_t> live{0};
     std::mutex m;
     std::condition_variable cv;
@@ -80,14 +82,22 @@ void on_spans(void *ctx, int32_t status, const tm_span *sp, uint32_t ns, uint64_
 
 void next_or_retire(Pub *p) {
     // the deadline is looked at every 8th publish of a publisher (a clock read is not free)
-    if (((p->done & 7) == 0 && std::chrono::steady_clock::now() >= p->L->deadline) || !submit_next(p)) retire(p->L);
+    if (((p->done & 7) == 0 &&
+         std::chrono::steady_clock::now().time_since_epoch().count() >= p->L->deadline.load(std::memory_order_relaxed)) ||
+        !submit_next(p))
+        retire(p->L);
 }
 
 }  // namespace
 
-extern "C" int loadgen_run2(tm_batcher *b, const uint8_t *bytes, const uint32_t *off, uint32_t n_topics,
-                            uint32_t publishers, double seconds, int spans, uint64_t *published, uint64_t *ids_out,
-                            uint64_t *errors, uint64_t *checksum, double *elapsed_s) {
+// Closed loop for warmup_s + seconds.  With `window` non-null: after warmup_s the batcher's
+// latency window is reset (tm_batcher_stats_reset), and at the end of the measured `seconds`,
+// BEFORE the publishers stop and the queue drains, its stats are read into *window: the
+// latency of every publish delivered in the steady state, and how many there were.
+extern "C" int loadgen_run3(tm_batcher *b, const uint8_t *bytes, const uint32_t *off, uint32_t n_topics,
+                            uint32_t publishers, double warmup_s, double seconds, int spans, uint64_t *published,
+                            uint64_t *ids_out, uint64_t *errors, uint64_t *checksum, double *elapsed_s,
+                            tm_batcher_stats *window) {
     if (!b || !bytes || !off || !n_topics || !publishers) return TM_EINVAL;
     Load L;
     L.spans = spans != 0;
@@ -96,13 +106,22 @@ extern "C" int loadgen_run2(tm_batcher *b, const uint8_t *bytes, const uint32_t 
     L.off = off;
     L.n_topics = n_topics;
     std::vector<Pub> pubs(publishers);
-    const auto t0 = std::chrono::steady_clock::now();
-    L.deadline = t0 + std::chrono::duration_cast<std::chrono::steady_clock::duration>(
-                          std::chrono::duration<double>(seconds));
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const auto dur = [](double s) { return std::chrono::duration_cast<clk::duration>(std::chrono::duration<double>(s)); };
+    if (!window) L.deadline = (t0 + dur(warmup_s + seconds)).time_since_epoch().count();
     L.live = publishers;
     for (uint32_t p = 0; p < publishers; p++) {
         pubs[p] = Pub{&L, (uint64_t)p * 7919u, 0, 0, 0, 0};
         if (!submit_next(&pubs[p])) retire(&L);
+    }
+    if (window) {
+        std::this_thread::sleep_until(t0 + dur(warmup_s));
+        int rc = tm_batcher_stats_reset(b);
+        std::this_thread::sleep_until(t0 + dur(warmup_s + seconds));
+        if (!rc) rc = tm_batcher_stats_get(b, window);
+        L.deadline = clk::now().time_since_epoch().count();  // now the publishers stop
+        if (rc) window->lat_count = 0;
     }
     {
         std::unique_lock<std::mutex> lk(L.m);
@@ -123,6 +142,13 @@ extern "C" int loadgen_run2(tm_batcher *b, const uint8_t *bytes, const uint32_t 
     return TM_OK;
 }
 
+extern "C" int loadgen_run2(tm_batcher *b, const uint8_t *bytes, const uint32_t *off, uint32_t n_topics,
+                            uint32_t publishers, double seconds, int spans, uint64_t *published, uint64_t *ids_out,
+                            uint64_t *errors, uint64_t *checksum, double *elapsed_s) {
+    return loadgen_run3(b, bytes, off, n_topics, publishers, 0.0, seconds, spans, published, ids_out, errors, checksum,
+                        elapsed_s, nullptr);
+}
+
 extern "C" int loadgen_run(tm_batcher *b, const uint8_t *bytes, const uint32_t *off, uint32_t n_topics,
                            uint32_t publishers, double seconds, uint64_t *published, uint64_t *ids_out,
                            uint64_t *errors, double *elapsed_s) {
@@ -132,7 +158,6 @@ extern "C" int loadgen_run(tm_batcher *b, const uint8_t *bytes, const uint32_t *
 
 // Read every id a tm_match_batch_runs result covers (a checksum), on `threads` threads by
 // topic range: what a consumer building replies from the spans does at least once per id.
-#include <thread>
 extern "C" uint64_t spans_checksum(const tm_runs_result *r, uint32_t threads) {
     if (!r || !r->n) return 0;
     threads = threads ? threads : 1;
