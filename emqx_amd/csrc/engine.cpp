@@ -342,7 +342,43 @@ struct HostOut {
     std::vector<uint32_t> span_off;
     uint64_t lease_epoch = 0;
     bool lease = false;  // holds a read lease on the host id arena (tm_match_batch_runs)
+    // The device side of this thread's host-form calls (tm_match_batch ALL / FIRST / COUNT,
+    // tm_match_batch_runs): its own batch buffers, streams, events and pinned staging, so the
+    // calls of several threads overlap on the device.  A call holds the engine's device lock
+    // only while it queues work that reads the index (and records that work, note_use, so a
+    // commit orders its in-place writes and buffer swaps after it), not across the H2D, the
+    // sync and the D2H of its own buffers (round 4; the reference index is read_concurrency,
+    // emqx_topic_index.erl:41-42).
+    BatchBufs bb;
+    hipStream_t s_walk = nullptr, s_copy = nullptr, s_h2d = nullptr;
+    hipEvent_t ev_pk[2] = {}, ev_pd[2] = {}, ev_h2d[16] = {};
+    PinBuf h_bytes, h_off, h_ctl, h_rctl;
+    double pipe_kpt = 0, runs_spt = 4.0;  // keys / spans per topic of this thread's last batch
+    hipError_t lanes() {  // streams and events, once per thread (the device is already set)
+        if (s_walk) return hipSuccess;
+        hipError_t e;
+        for (hipStream_t *st : {&s_walk, &s_copy, &s_h2d})
+            if ((e = hipStreamCreateWithFlags(st, hipStreamNonBlocking))) return e;
+        for (hipEvent_t *ev : {&ev_pk[0], &ev_pk[1], &ev_pd[0], &ev_pd[1]})
+            if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming))) return e;
+        for (hipEvent_t &ev : ev_h2d)
+            if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming))) return e;
+        return hipSuccess;
+    }
     void release() {
+        for (hipStream_t st : {s_walk, s_copy, s_h2d})
+            if (st) (void)hipStreamSynchronize(st);
+        for (hipEvent_t ev : {ev_pk[0], ev_pk[1], ev_pd[0], ev_pd[1]})
+            if (ev) (void)hipEventDestroy(ev);
+        for (hipEvent_t &ev : ev_h2d)
+            if (ev) (void)hipEventDestroy(ev);
+        for (hipStream_t st : {s_walk, s_copy, s_h2d})
+            if (st) (void)hipStreamDestroy(st);
+        s_walk = s_copy = s_h2d = nullptr;
+        ev_pk[0] = ev_pk[1] = ev_pd[0] = ev_pd[1] = nullptr;
+        for (hipEvent_t &ev : ev_h2d) ev = nullptr;
+        bb.release();
+        for (PinBuf *b : {&h_bytes, &h_off, &h_ctl, &h_rctl}) b->release();
         for (PinBuf *b : {&h_outoff, &h_outcnt, &h_status, &h_keys, &f_keys, &r_off, &r_cnt, &r_kcnt, &r_status, &r_runs})
             b->release();
         std::vector<uint32_t>().swap(pp_off);
@@ -548,19 +584,16 @@ struct tm_engine {
     // engine keeps until the next such call) and one for the host-result calls (tm_match_batch*,
     // synchronous), so a host call from one thread never overwrites another thread's pending
     // device result.  `bb` is the set of the call in progress (under mu_dev).
-    BatchBufs bb_dev, bb_host, bb_batch;  // bb_batch: the batching aggregator's windows (batcher.cpp)
+    BatchBufs bb_dev, bb_batch;  // bb_batch: the batching aggregator's windows (batcher.cpp); host-form calls: HostOut::bb
     BatchBufs bb_dev2;  // tm_match_device_set(.., 1, ..): a second direct batch in flight
     BatchBufs bb_batch2;  // the aggregator's second window set (its windows alternate sets and streams)
     BatchBufs *batch_set(uint32_t set) { return set ? &bb_batch2 : &bb_batch; }
     BatchBufs *bb = &bb_dev;
-    double runs_spt = 4.0;     // spans per topic of the last runs batch (sizes the next)
-    PinBuf h_rctl;             // runs: per sub-batch {span cursor, counter block}
-    PinBuf h_bytes, h_off, h_cursor;
+    PinBuf h_cursor;           // tm_device_sync_set: the counter block of a direct batch
     hipStream_t stream = nullptr;
     hipStream_t s_build = nullptr;  // a full rebuild's standby upload (beside the matches)
-    hipStream_t s_h2d = nullptr;    // tm_match_batch_runs: topic H2D beside the walks
-    hipEvent_t ev_h2d[16] = {};
-    CopyPool copier;
+    CopyPool copier;  // tm_match_batch_runs: staging a pageable batch into pinned memory
+    std::once_flag copier_once;
     hipEvent_t ev_chain = nullptr;  // orders a device match after the previous one's stream
     uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0;
     uint64_t commit_us[3] = {0, 0, 0};  // last commit: apply / lists / upload (tm_stats)
@@ -580,12 +613,6 @@ struct tm_engine {
     hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // around k_match_fast (tm_debug_timing)
     bool timing_on = false;
     bool topic_words = false;  // the batch being enqueued holds word-list topics (TM_MATCH_TOPIC_WORDS)
-    // pipelined tm_match_batch: a copy stream, per-half events, the counter blocks' landing
-    // place, and the last such batch's keys per topic (sizes the next one's buffers)
-    hipStream_t s_pipe = nullptr;
-    hipEvent_t ev_pk[2] = {}, ev_pd[2] = {};
-    PinBuf h_pctl;
-    double pipe_kpt = 0;
 
     uint64_t edge_load_inv() const { return cfg.edge_load_inv ? cfg.edge_load_inv : EDGE_LOAD_INV; }
     uint64_t node_budget() const {  // trie nodes below the root
@@ -2058,11 +2085,9 @@ void tm_destroy(tm_engine *eng) {
     eng->outs.clear();
     eng->release_ids();
     eng->bb_dev.release();
-    eng->bb_host.release();
     eng->bb_batch.release();
     eng->bb_batch2.release();
     eng->bb_dev2.release();
-    eng->h_rctl.release();
     for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
                       &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan, &eng->fx.d_pool,
@@ -2072,19 +2097,10 @@ void tm_destroy(tm_engine *eng) {
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
                       &eng->d_arena, &eng->d_scatter_idx, &eng->d_scatter_src, &eng->d_stats})
         b->release();
-    for (PinBuf *b : {&eng->h_bytes, &eng->h_off, &eng->h_cursor}) b->release();
+    eng->h_cursor.release();
     if (eng->ev_fast0) (void)hipEventDestroy(eng->ev_fast0);
     if (eng->ev_fast1) (void)hipEventDestroy(eng->ev_fast1);
-    if (eng->s_pipe) (void)hipStreamSynchronize(eng->s_pipe);
-    for (hipEvent_t e : {eng->ev_pk[0], eng->ev_pk[1], eng->ev_pd[0], eng->ev_pd[1]})
-        if (e) (void)hipEventDestroy(e);
-    eng->h_pctl.release();
-    if (eng->s_pipe) (void)hipStreamDestroy(eng->s_pipe);
     if (eng->s_build) (void)hipStreamDestroy(eng->s_build);
-    if (eng->s_h2d) (void)hipStreamSynchronize(eng->s_h2d);
-    for (hipEvent_t e : eng->ev_h2d)
-        if (e) (void)hipEventDestroy(e);
-    if (eng->s_h2d) (void)hipStreamDestroy(eng->s_h2d);
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
     delete eng;
 }
@@ -2206,6 +2222,19 @@ int tm_result_release(tm_engine *eng) {
         eng->outs.erase(it);
     }
     eng->lease_drop(*mine);
+    {  // its streams leave the set a commit orders its writes after
+        std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+        for (size_t i = 0; i < eng->uses.size();) {
+            hipStream_t us = eng->uses[i].first;
+            if (us && (us == mine->s_walk || us == mine->s_copy || us == mine->s_h2d)) {
+                (void)hipEventSynchronize(eng->uses[i].second);
+                (void)hipEventDestroy(eng->uses[i].second);
+                eng->uses.erase(eng->uses.begin() + (ptrdiff_t)i);
+            } else {
+                i++;
+            }
+        }
+    }
     mine->release();
     return TM_OK;
 }
@@ -2367,37 +2396,38 @@ constexpr uint32_t PIPE_MAXSUB = 8;
 
 static int match_batch_pipelined(tm_engine *eng, HostOut &o, const uint8_t *bytes, const uint32_t *off, uint32_t n,
                                  tm_result *out) {
+    // called without the device lock: it is taken only around the walks and the buffer sizing
     const uint32_t base = off[0];
     const uint64_t nbytes = (uint64_t)off[n] - base;
     const uint32_t S = std::max<uint32_t>(2, std::min<uint32_t>(PIPE_MAXSUB, n / PIPE_SUB));
     uint32_t b[PIPE_MAXSUB + 1];
     for (uint32_t j = 0; j <= S; j++) b[j] = (uint32_t)((uint64_t)n * j / S);
-    int rc = ensure_batch(eng, n, nbytes);
-    if (rc) return rc;
-    TM_TRY_HIP(eng->h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->h_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->grow_buf(eng->bb->d_bytes, nbytes + 16), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->grow_buf(eng->bb->d_off, ((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+    BatchBufs &B = o.bb;
+    // each half of the key arena holds one sub-batch; sized from this thread's last pipelined batch
+    const uint64_t est_sub = (uint64_t)(o.pipe_kpt * (double)(n / S + 1) * 1.15) + 4096;
+    {
+        std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+        eng->bb = &B;
+        int rc = ensure_batch(eng, n, nbytes);
+        if (rc) return rc;
+        TM_TRY_HIP(eng->grow_buf(B.d_bytes, nbytes + 16), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(eng->grow_buf(B.d_off, ((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+        if (B.keys_cap < 2 * est_sub) {
+            TM_TRY_HIP(eng->grow_buf(B.d_keys, 2 * est_sub * 4), TM_ENOMEM, "alloc keys");
+            B.keys_cap = 2 * est_sub;
+        }
+    }
+    TM_TRY_HIP(o.h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(o.h_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(o.h_outoff.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(o.h_outcnt.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(o.h_status.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->h_pctl.ensure(2 * CTL_BYTES), TM_ENOMEM, "pinned alloc");
-    if (!eng->s_pipe) {
-        TM_TRY_HIP(hipStreamCreateWithFlags(&eng->s_pipe, hipStreamNonBlocking), TM_EDEVICE, "stream");
-        for (hipEvent_t *e : {&eng->ev_pk[0], &eng->ev_pk[1], &eng->ev_pd[0], &eng->ev_pd[1]})
-            TM_TRY_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming), TM_EDEVICE, "event");
-    }
-    // each half of the key arena holds one sub-batch; sized from the last pipelined batch
-    const uint64_t est_sub = (uint64_t)(eng->pipe_kpt * (double)(n / S + 1) * 1.15) + 4096;
-    if (eng->bb->keys_cap < 2 * est_sub) {
-        TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, 2 * est_sub * 4), TM_ENOMEM, "alloc keys");
-        eng->bb->keys_cap = 2 * est_sub;
-    }
-    uint64_t hc = eng->bb->keys_cap / 2;
-    TM_TRY_HIP(o.h_keys.ensure((size_t)(eng->pipe_kpt * (double)n * 1.1) * 4 + 4), TM_ENOMEM, "pinned alloc");
-    hipStream_t s = eng->stream, c = eng->s_pipe;
-    uint8_t *hb8 = eng->h_bytes.as<uint8_t>(), *hctl = eng->h_pctl.as<uint8_t>();
-    uint32_t *ho = eng->h_off.as<uint32_t>();
+    TM_TRY_HIP(o.h_ctl.ensure(2 * CTL_BYTES), TM_ENOMEM, "pinned alloc");
+    uint64_t hc = B.keys_cap / 2;
+    TM_TRY_HIP(o.h_keys.ensure((size_t)(o.pipe_kpt * (double)n * 1.1) * 4 + 4), TM_ENOMEM, "pinned alloc");
+    hipStream_t s = o.s_walk, c = o.s_copy;
+    uint8_t *hb8 = o.h_bytes.as<uint8_t>(), *hctl = o.h_ctl.as<uint8_t>();
+    uint32_t *ho = o.h_off.as<uint32_t>();
     uint64_t hb[PIPE_MAXSUB] = {}, hbase = 0, seg_d = 0, fr_d = 0, slow = 0;
 
     auto stage = [&](uint32_t j) -> int {  // sub-batch j's topics into pinned memory, then H2D
@@ -2406,30 +2436,35 @@ static int match_batch_pipelined(tm_engine *eng, HostOut &o, const uint8_t *byte
         if (bhi > blo) memcpy(hb8 + blo, bytes + base + blo, bhi - blo);
         for (uint32_t i = lo; i <= hi; i++) ho[i] = off[i] - base;
         if (bhi > blo)
-            TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_bytes.as<uint8_t>() + blo, hb8 + blo, bhi - blo, hipMemcpyHostToDevice, s),
+            TM_TRY_HIP(hipMemcpyAsync(B.d_bytes.as<uint8_t>() + blo, hb8 + blo, bhi - blo, hipMemcpyHostToDevice, s),
                        TM_EDEVICE, "H2D");
-        TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_off.as<uint32_t>() + lo, ho + lo, ((size_t)hi - lo + 1) * 4,
-                                  hipMemcpyHostToDevice, s),
+        TM_TRY_HIP(hipMemcpyAsync(B.d_off.as<uint32_t>() + lo, ho + lo, ((size_t)hi - lo + 1) * 4, hipMemcpyHostToDevice, s),
                    TM_EDEVICE, "H2D");
         return TM_OK;
     };
     auto walk = [&](uint32_t j) -> int {  // sub-batch j walks into key half j % 2
         const uint32_t lo = b[j], hi = b[j + 1], h = j & 1;
-        if (j >= 2) TM_TRY_HIP(hipStreamWaitEvent(s, eng->ev_pd[h], 0), TM_EDEVICE, "wait");  // half's last D2H
-        eng->bb->last_n = hi - lo;
-        TM_TRY_HIP(enqueue_match(eng, eng->bb->d_bytes.as<uint8_t>(), eng->bb->d_off.as<uint32_t>() + lo, hi - lo, s, MODE_ALL,
-                                 lo, eng->bb->d_keys.as<uint32_t>() + h * hc, hc),
-                   TM_EDEVICE, "kernel launch");
-        TM_TRY_HIP(hipMemcpyAsync(hctl + h * CTL_BYTES, eng->bb->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-                   "D2H");
-        TM_TRY_HIP(hipEventRecord(eng->ev_pk[h], s), TM_EDEVICE, "event");
+        if (j >= 2) TM_TRY_HIP(hipStreamWaitEvent(s, o.ev_pd[h], 0), TM_EDEVICE, "wait");  // half's last D2H
+        const uint8_t *pctl;
+        {
+            std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+            eng->bb = &B;
+            B.last_n = hi - lo;
+            TM_TRY_HIP(enqueue_match(eng, B.d_bytes.as<uint8_t>(), B.d_off.as<uint32_t>() + lo, hi - lo, s, MODE_ALL, lo,
+                                     B.d_keys.as<uint32_t>() + h * hc, hc),
+                       TM_EDEVICE, "kernel launch");
+            TM_TRY_HIP(eng->note_use(s), TM_EDEVICE, "event");
+            pctl = B.p_ctl;
+        }
+        TM_TRY_HIP(hipMemcpyAsync(hctl + h * CTL_BYTES, pctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipEventRecord(o.ev_pk[h], s), TM_EDEVICE, "event");
         return TM_OK;
     };
     // sub-batch j's walk is done: its keys and per-topic results D2H on the copy stream
     // (1: its key half was too small)
     auto finish = [&](uint32_t j) -> int {
         const uint32_t lo = b[j], hi = b[j + 1], h = j & 1;
-        TM_TRY_HIP(hipEventSynchronize(eng->ev_pk[h]), TM_EDEVICE, "match kernels");
+        TM_TRY_HIP(hipEventSynchronize(o.ev_pk[h]), TM_EDEVICE, "match kernels");
         const uint8_t *ctl = hctl + h * CTL_BYTES;
         const uint64_t total = *(const uint64_t *)ctl;
         if (total > hc) return 1;
@@ -2446,20 +2481,20 @@ static int match_batch_pipelined(tm_engine *eng, HostOut &o, const uint8_t *byte
             std::swap(nb.dev, o.h_keys.dev);
             nb.release();
         }
-        TM_TRY_HIP(hipStreamWaitEvent(c, eng->ev_pk[h], 0), TM_EDEVICE, "wait");
-        TM_TRY_HIP(d2h_words(o.h_keys, hbase, eng->bb->d_keys.as<uint32_t>() + h * hc, total, c), TM_EDEVICE, "D2H");
-        for (std::pair<PinBuf *, DevBuf *> pr : {std::make_pair(&o.h_outoff, &eng->bb->d_outoff),
-                                                 std::make_pair(&o.h_outcnt, &eng->bb->d_outcnt),
-                                                 std::make_pair(&o.h_status, &eng->bb->d_status)})
-            TM_TRY_HIP(hipMemcpyAsync(pr.first->as<uint32_t>() + lo, pr.second->as<uint32_t>() + lo,
-                                      ((size_t)hi - lo) * 4, hipMemcpyDeviceToHost, c),
+        TM_TRY_HIP(hipStreamWaitEvent(c, o.ev_pk[h], 0), TM_EDEVICE, "wait");
+        TM_TRY_HIP(d2h_words(o.h_keys, hbase, B.d_keys.as<uint32_t>() + h * hc, total, c), TM_EDEVICE, "D2H");
+        for (std::pair<PinBuf *, DevBuf *> pr : {std::make_pair(&o.h_outoff, &B.d_outoff), std::make_pair(&o.h_outcnt, &B.d_outcnt),
+                                                 std::make_pair(&o.h_status, &B.d_status)})
+            TM_TRY_HIP(hipMemcpyAsync(pr.first->as<uint32_t>() + lo, pr.second->as<uint32_t>() + lo, ((size_t)hi - lo) * 4,
+                                      hipMemcpyDeviceToHost, c),
                        TM_EDEVICE, "D2H");
-        TM_TRY_HIP(hipEventRecord(eng->ev_pd[h], c), TM_EDEVICE, "event");
+        TM_TRY_HIP(hipEventRecord(o.ev_pd[h], c), TM_EDEVICE, "event");
         hb[j] = hbase;
         hbase += total;
         return TM_OK;
     };
 
+    int rc;
     if ((rc = stage(0)) || (rc = walk(0))) return rc;
     for (uint32_t j = 0; j < S; j++) {
         if (j + 1 < S && ((rc = stage(j + 1)) || (rc = walk(j + 1)))) return rc;
@@ -2471,8 +2506,11 @@ static int match_batch_pipelined(tm_engine *eng, HostOut &o, const uint8_t *byte
             TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "sync");
             TM_TRY_HIP(hipStreamSynchronize(c), TM_EDEVICE, "sync");
             const uint64_t want = 2 * (need + need / 8 + 1024);
-            TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, want * 4), TM_ENOMEM, "alloc keys");
-            eng->bb->keys_cap = want;
+            {
+                std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+                TM_TRY_HIP(eng->grow_buf(B.d_keys, want * 4), TM_ENOMEM, "alloc keys");
+                B.keys_cap = want;
+            }
             hc = want / 2;
             if ((rc = walk(j)) || (j + 1 < S && (rc = walk(j + 1)))) return rc;
             rc = finish(j);
@@ -2485,13 +2523,17 @@ static int match_batch_pipelined(tm_engine *eng, HostOut &o, const uint8_t *byte
     uint32_t *oo = o.h_outoff.as<uint32_t>();
     for (uint32_t j = 1; j < S; j++)
         for (uint32_t i = b[j]; i < b[j + 1]; i++) oo[i] += (uint32_t)hb[j];
-    eng->n_slow_last = slow;
-    eng->bb->seg_demand_last = seg_d;
-    eng->bb->fr_demand_last = fr_d;
-    if ((rc = grow_pools(eng))) return rc;
-    eng->pipe_kpt = (double)hbase / n;
-    eng->bb->dev_batch = false;  // the device holds sub-batches, not this batch
-    eng->bb->last_n = 0;
+    {
+        std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+        eng->bb = &B;
+        eng->n_slow_last = slow;
+        B.seg_demand_last = seg_d;
+        B.fr_demand_last = fr_d;
+        if ((rc = grow_pools(eng))) return rc;
+    }
+    o.pipe_kpt = (double)hbase / n;
+    B.dev_batch = false;  // the device holds sub-batches, not this batch
+    B.last_n = 0;
     out->total = hbase;
     out->off = oo;
     out->cnt = o.h_outcnt.as<uint32_t>();
@@ -2500,6 +2542,10 @@ static int match_batch_pipelined(tm_engine *eng, HostOut &o, const uint8_t *byte
     return TM_OK;
 }
 
+// Host-form batch (tm_match_batch).  ALL / FIRST / COUNT run concurrently across threads: each
+// thread has its own buffers and streams (HostOut::bb), and the device lock is held only while
+// the walk is queued.  UNIQUE / AGGRE keep the lock across the call: their reducer reads key
+// records the walk's result must match, so walk and reducer see one epoch.
 static int match_batch_impl(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
                             tm_result *out) {
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
@@ -2509,77 +2555,95 @@ static int match_batch_impl(tm_engine *eng, const uint8_t *bytes, const uint32_t
     // keys needs the host copy, so that mode also holds mu_host (taken before mu_dev)
     std::unique_lock<std::mutex> gh(eng->mu_host, std::defer_lock);
     if (mode == TM_MATCH_UNIQUE && !eng->replica) gh.lock();
-    std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
-    eng->bb = &eng->bb_host;
     HostOut &o = eng->out();
     memset(out, 0, sizeof(*out));
     out->n = n;
+    TM_TRY_HIP(o.lanes(), TM_EDEVICE, "stream");
+    BatchBufs &B = o.bb;
+    std::unique_lock<std::recursive_mutex> gd(eng->mu_dev);
+    eng->bb = &B;
     // UNIQUE is reduced on the GPU unless a key is too deep for the device order code
     const bool dev_reduce = reduced_mode(mode) && (mode == TM_MATCH_AGGRE || eng->dv.n_deep == 0);
     if (reduced_mode(mode) && !dev_reduce && eng->replica) return replica_refuses(eng, "tm_match_batch (host UNIQUE)");
-    eng->bb->last_mode = (reduced_mode(mode) && !dev_reduce) ? TM_MATCH_ALL : mode;  // what the device holds
+    B.last_mode = (reduced_mode(mode) && !dev_reduce) ? TM_MATCH_ALL : mode;  // what the device holds
     if (n == 0) return TM_OK;
-    if (mode == TM_MATCH_ALL && n >= 2 * PIPE_SUB)
+    if (mode == TM_MATCH_ALL && n >= 2 * PIPE_SUB) {
+        gd.unlock();
         return match_batch_pipelined(eng, o, bytes, off, n, out);
-    eng->bb->dev_batch = true;
+    }
+    const bool hold = reduced_mode(mode);  // keep the device lock across the whole call
+    B.dev_batch = true;
     // rebase offsets to 0
     uint32_t base = off[0];
     uint64_t nbytes = (uint64_t)off[n] - base;
     int rc = ensure_batch(eng, n, nbytes);
     if (rc) return rc;
-    TM_TRY_HIP(eng->h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->h_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->grow_buf(eng->bb->d_bytes, nbytes + 16), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->grow_buf(eng->bb->d_off, ((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
-    if (nbytes) memcpy(eng->h_bytes.p, bytes + base, nbytes);
-    uint32_t *ho = eng->h_off.as<uint32_t>();
-    for (uint32_t i = 0; i <= n; i++) ho[i] = off[i] - base;
-    hipStream_t s = eng->stream;
-    TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_bytes.p, eng->h_bytes.p, nbytes + 1, hipMemcpyHostToDevice, s), TM_EDEVICE,
-               "H2D");
-    TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_off.p, ho, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
-    TM_TRY_HIP(eng->h_cursor.ensure(64), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(eng->grow_buf(B.d_bytes, nbytes + 16), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(B.d_off, ((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
     // FIRST runs k_match_first (<= 1 key per topic); COUNT skips the key copy-out
     const uint32_t kmode = mode == TM_MATCH_FIRST ? MODE_FIRST : (mode == TM_MATCH_COUNT ? MODE_COUNT : MODE_ALL);
-    if (kmode == MODE_FIRST && eng->bb->keys_cap < n) {
-        TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, (uint64_t)n * 4), TM_ENOMEM, "alloc keys");
-        eng->bb->keys_cap = n;
+    if (kmode == MODE_FIRST && B.keys_cap < n) {
+        TM_TRY_HIP(eng->grow_buf(B.d_keys, (uint64_t)n * 4), TM_ENOMEM, "alloc keys");
+        B.keys_cap = n;
     }
+    if (!hold) gd.unlock();
+    TM_TRY_HIP(o.h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(o.h_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(o.h_ctl.ensure(64), TM_ENOMEM, "pinned alloc");
+    if (nbytes) memcpy(o.h_bytes.p, bytes + base, nbytes);
+    uint32_t *ho = o.h_off.as<uint32_t>();
+    for (uint32_t i = 0; i <= n; i++) ho[i] = off[i] - base;
+    hipStream_t s = o.s_walk;
+    TM_TRY_HIP(hipMemcpyAsync(B.d_bytes.p, o.h_bytes.p, nbytes + 1, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
+    TM_TRY_HIP(hipMemcpyAsync(B.d_off.p, ho, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
+    const uint64_t *ctl = o.h_ctl.as<uint64_t>();
+    uint64_t total = 0;
     for (int attempt = 0; attempt < 2; attempt++) {
-        eng->bb->last_n = n;
-        TM_TRY_HIP(enqueue_match(eng, eng->bb->d_bytes.as<uint8_t>(), eng->bb->d_off.as<uint32_t>(), n, s, kmode), TM_EDEVICE,
-                   "kernel launch");
-        // the counter block has the host layout: cursor @0, slow_count @8, seg @16, fr @24
-        TM_TRY_HIP(hipMemcpyAsync(eng->h_cursor.p, eng->bb->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-                   "D2H");
+        {
+            std::unique_lock<std::recursive_mutex> ga(eng->mu_dev, std::defer_lock);
+            if (!hold) ga.lock();
+            eng->bb = &B;
+            if (attempt) {
+                // output arena too small: grow to the demand and run again (once suffices:
+                // the cursor counts every key the batch asked for)
+                const uint64_t want = total + total / 8 + 1024;
+                TM_TRY_HIP(eng->grow_buf(B.d_keys, want * 4), TM_ENOMEM, "alloc keys");
+                B.keys_cap = want;
+            }
+            B.last_n = n;
+            TM_TRY_HIP(enqueue_match(eng, B.d_bytes.as<uint8_t>(), B.d_off.as<uint32_t>(), n, s, kmode), TM_EDEVICE,
+                       "kernel launch");
+            TM_TRY_HIP(eng->note_use(s), TM_EDEVICE, "event");
+            // the counter block has the host layout: cursor @0, slow_count @8, seg @16, fr @24
+            TM_TRY_HIP(hipMemcpyAsync(o.h_ctl.p, B.p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+        }
         TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "match kernels");
-        uint64_t total = *eng->h_cursor.as<uint64_t>();
-        eng->n_slow_last = *(uint32_t *)((uint8_t *)eng->h_cursor.p + 8);
-        eng->bb->seg_demand_last = *(uint64_t *)((uint8_t *)eng->h_cursor.p + 16);
-        eng->bb->fr_demand_last = *(uint64_t *)((uint8_t *)eng->h_cursor.p + 24);
-        if (kmode != MODE_ALL || total <= eng->bb->keys_cap) break;
-        // output arena too small: grow to the demand and run again (once suffices:
-        // the cursor counts every key the batch asked for)
-        uint64_t want = total + total / 8 + 1024;
-        TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, want * 4), TM_ENOMEM, "alloc keys");
-        eng->bb->keys_cap = want;
+        total = ctl[0];
+        B.seg_demand_last = ctl[2];
+        B.fr_demand_last = ctl[3];
+        if (kmode != MODE_ALL || total <= B.keys_cap) break;
     }
-    uint64_t total = kmode == MODE_ALL ? *eng->h_cursor.as<uint64_t>() : (kmode == MODE_FIRST ? n : 0);
-    if (dev_reduce && (rc = enqueue_reduce(eng, mode, n, s))) return rc;
+    const uint32_t n_slow = (uint32_t)ctl[1];
+    total = kmode == MODE_ALL ? total : (kmode == MODE_FIRST ? n : 0);
+    if (dev_reduce && (rc = enqueue_reduce(eng, mode, n, s))) return rc;  // (hold: under the lock)
     TM_TRY_HIP(o.h_outoff.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(o.h_outcnt.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(o.h_status.ensure((size_t)n * 4), TM_ENOMEM, "pinned alloc");
     TM_TRY_HIP(o.h_keys.ensure(total * 4 + 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(hipMemcpyAsync(o.h_outoff.p, eng->bb->d_outoff.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-               "D2H");
-    TM_TRY_HIP(hipMemcpyAsync(o.h_outcnt.p, (dev_reduce ? eng->bb->d_ucnt : eng->bb->d_outcnt).p, (size_t)n * 4,
-                              hipMemcpyDeviceToHost, s),
+    TM_TRY_HIP(hipMemcpyAsync(o.h_outoff.p, B.d_outoff.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+    TM_TRY_HIP(hipMemcpyAsync(o.h_outcnt.p, (dev_reduce ? B.d_ucnt : B.d_outcnt).p, (size_t)n * 4, hipMemcpyDeviceToHost, s),
                TM_EDEVICE, "D2H");
-    TM_TRY_HIP(hipMemcpyAsync(o.h_status.p, eng->bb->d_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-               "D2H");
-    TM_TRY_HIP(d2h_words(o.h_keys, 0, eng->bb->d_keys.p, total, s), TM_EDEVICE, "D2H");
+    TM_TRY_HIP(hipMemcpyAsync(o.h_status.p, B.d_status.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+    TM_TRY_HIP(d2h_words(o.h_keys, 0, B.d_keys.p, total, s), TM_EDEVICE, "D2H");
     TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "D2H");
-    if ((rc = grow_pools(eng))) return rc;
+    {
+        std::unique_lock<std::recursive_mutex> ga(eng->mu_dev, std::defer_lock);
+        if (!hold) ga.lock();
+        eng->bb = &B;
+        eng->n_slow_last = n_slow;
+        if ((rc = grow_pools(eng))) return rc;
+    }
+    if (gd.owns_lock()) gd.unlock();
     out->total = total;
     out->off = o.h_outoff.as<uint32_t>();
     out->cnt = o.h_outcnt.as<uint32_t>();
@@ -2628,25 +2692,20 @@ static int match_batch_impl(tm_engine *eng, const uint8_t *bytes, const uint32_t
         }
         tmp.assign(ks, ks + c);
         std::sort(tmp.begin(), tmp.end(), [&](uint32_t a, uint32_t b) { return eng->cmp_keys(a, b) < 0; });
-        if (mode == TM_MATCH_FIRST) {
-            o.pp_keys.push_back(tmp[0]);
-            o.pp_cnt[i] = 1;
-        } else {
-            // maps:put in ascending walk order: the last (greatest) key per id wins,
-            // maps:values/1 returns them ordered by id (small maps are sorted).
-            std::vector<std::pair<uint64_t, uint32_t>> best;
-            std::unordered_map<uint64_t, size_t> at;  // id -> index in best
-            at.reserve(tmp.size() * 2);
-            for (uint32_t k : tmp) {
-                const uint64_t id = eng->keys[k].id;
-                auto ins = at.emplace(id, best.size());
-                if (ins.second) best.push_back({id, k});
-                else best[ins.first->second].second = k;
-            }
-            std::sort(best.begin(), best.end());
-            for (auto &p : best) o.pp_keys.push_back(p.second);
-            o.pp_cnt[i] = (uint32_t)best.size();
+        // maps:put in ascending walk order: the last (greatest) key per id wins,
+        // maps:values/1 returns them ordered by id (small maps are sorted).
+        std::vector<std::pair<uint64_t, uint32_t>> best;
+        std::unordered_map<uint64_t, size_t> at;  // id -> index in best
+        at.reserve(tmp.size() * 2);
+        for (uint32_t k : tmp) {
+            const uint64_t id = eng->keys[k].id;
+            auto ins = at.emplace(id, best.size());
+            if (ins.second) best.push_back({id, k});
+            else best[ins.first->second].second = k;
         }
+        std::sort(best.begin(), best.end());
+        for (auto &p : best) o.pp_keys.push_back(p.second);
+        o.pp_cnt[i] = (uint32_t)best.size();
     }
     out->off = o.pp_off.data();
     out->cnt = o.pp_cnt.data();
@@ -3693,11 +3752,16 @@ static int match_runs_impl(tm_engine *eng, HostOut &o, const uint8_t *bytes, con
         eng->err = "tm_match_batch_runs: failure injected (TM_CFG_FAIL_HOST_CALLS)";
         return TM_EDEVICE;
     }
-    std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
-    eng->bb = &eng->bb_host;
+    // this thread's own buffers and streams (HostOut::bb); the device lock is held only while
+    // the buffers are sized and while each sub-batch's walk is queued
+    TM_TRY_HIP(o.lanes(), TM_EDEVICE, "stream");
+    BatchBufs &B = o.bb;
     memset(out, 0, sizeof(*out));
     out->n = n;
-    out->epoch = eng->dv.epoch;
+    {
+        std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+        out->epoch = eng->dv.epoch;
+    }
     if (n == 0) return TM_OK;
     const uint32_t base = off[0];
     const uint64_t nbytes = (uint64_t)off[n] - base;
@@ -3708,54 +3772,49 @@ static int match_runs_impl(tm_engine *eng, HostOut &o, const uint8_t *bytes, con
     const uint32_t S = std::max<uint32_t>(1, std::min<uint32_t>(RUNS_MAXSUB, n / runs_sub));
     uint32_t b[RUNS_MAXSUB + 1];
     for (uint32_t j = 0; j <= S; j++) b[j] = (uint32_t)((uint64_t)n * j / S);
-    int rc = ensure_batch(eng, n, nbytes);
-    if (rc) return rc;
-    {  // every sub-batch's grid must fit the per-wave chunk lists (sized for the whole batch above)
+    {
+        std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+        eng->bb = &B;
+        int rc = ensure_batch(eng, n, nbytes);
+        if (rc) return rc;
+        // every sub-batch's grid must fit the per-wave chunk lists (sized for the whole batch above)
         uint64_t g = 0;
-        for (uint32_t j = 0; j < S; j++)
-        {
+        for (uint32_t j = 0; j < S; j++) {
             const uint32_t sub = b[j + 1] - b[j], t = runs_tpw_of(sub);
             g = std::max<uint64_t>(g, match_grid(sub, pick_tpw(sub, t ? t : eng->cfg.topics_per_wave)));
         }
-        TM_TRY_HIP(eng->grow_buf(eng->bb->d_wave_chunks, g * SEG_MAXCHUNK * 4 + 4), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(eng->grow_buf(B.d_wave_chunks, g * SEG_MAXCHUNK * 4 + 4), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(eng->grow_buf(B.d_bytes, nbytes + 16), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(eng->grow_buf(B.d_off, ((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(eng->grow_buf(B.d_kcnt, (size_t)n * 4 + 4), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(eng->grow_buf(B.d_rcur, 64), TM_ENOMEM, "alloc");
     }
-    TM_TRY_HIP(eng->grow_buf(eng->bb->d_bytes, nbytes + 16), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->grow_buf(eng->bb->d_off, ((size_t)n + 1) * 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->grow_buf(eng->bb->d_kcnt, (size_t)n * 4 + 4), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->grow_buf(eng->bb->d_rcur, 64), TM_ENOMEM, "alloc");
-    TM_TRY_HIP(eng->h_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "pinned alloc");
-    TM_TRY_HIP(eng->h_rctl.ensure((size_t)RUNS_MAXSUB * 64), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(o.h_off.ensure(((size_t)n + 1) * 4), TM_ENOMEM, "pinned alloc");
+    TM_TRY_HIP(o.h_rctl.ensure((size_t)RUNS_MAXSUB * 64), TM_ENOMEM, "pinned alloc");
     for (PinBuf *pb : {&o.r_off, &o.r_cnt, &o.r_kcnt, &o.r_status})
         TM_TRY_HIP(pb->ensure((size_t)n * 4 + 4), TM_ENOMEM, "pinned alloc");
     const bool direct = host_pinned(bytes + base);  // DMA straight from the caller's batch
-    if (!direct) TM_TRY_HIP(eng->h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
-    if (!eng->s_pipe) {
-        TM_TRY_HIP(hipStreamCreateWithFlags(&eng->s_pipe, hipStreamNonBlocking), TM_EDEVICE, "stream");
-        for (hipEvent_t *e : {&eng->ev_pk[0], &eng->ev_pk[1], &eng->ev_pd[0], &eng->ev_pd[1]})
-            TM_TRY_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming), TM_EDEVICE, "event");
-    }
-    if (!eng->s_h2d) {
-        TM_TRY_HIP(hipStreamCreateWithFlags(&eng->s_h2d, hipStreamNonBlocking), TM_EDEVICE, "stream");
-        for (hipEvent_t &e : eng->ev_h2d) TM_TRY_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming), TM_EDEVICE, "event");
-    }
-    if (!direct && eng->copier.th.empty()) eng->copier.start(3);
-    hipStream_t s = eng->stream, c = eng->s_pipe, hq = eng->s_h2d;
-    eng->bb->last_n = 0;
-    eng->bb->dev_batch = false;  // the device result is in span form, not keys
-    uint32_t *ho = eng->h_off.as<uint32_t>();
-    uint8_t *hb = direct ? nullptr : eng->h_bytes.as<uint8_t>();
-    uint64_t *rctl = eng->h_rctl.as<uint64_t>();  // per sub-batch: [0] span cursor, [1..4] counter block
+    if (!direct) TM_TRY_HIP(o.h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
+    if (!direct) std::call_once(eng->copier_once, [eng] { eng->copier.start(3); });
+    hipStream_t s = o.s_walk, c = o.s_copy, hq = o.s_h2d;
+    B.last_n = 0;
+    B.dev_batch = false;  // the device result is in span form, not keys
+    uint32_t *ho = o.h_off.as<uint32_t>();
+    uint8_t *hb = direct ? nullptr : o.h_bytes.as<uint8_t>();
+    uint64_t *rctl = o.h_rctl.as<uint64_t>();  // per sub-batch: [0] span cursor, [1..4] counter block
+    int rc;
 
     for (int attempt = 0; attempt < 2; attempt++) {
-        const uint64_t cap = std::max<uint64_t>(65536, (uint64_t)(eng->runs_spt * 1.3 * n) + 4096);
-        if (eng->bb->d_keys.cap < cap * 16) {
-            TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, cap * 16), TM_ENOMEM, "alloc spans");
-            eng->bb->keys_cap = eng->bb->d_keys.cap / 4;
+        const uint64_t cap = std::max<uint64_t>(65536, (uint64_t)(o.runs_spt * 1.3 * n) + 4096);
+        if (B.d_keys.cap < cap * 16) {
+            std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+            TM_TRY_HIP(eng->grow_buf(B.d_keys, cap * 16), TM_ENOMEM, "alloc spans");
+            B.keys_cap = B.d_keys.cap / 4;
         }
-        const uint64_t span_cap = eng->bb->d_keys.cap / 16;
+        const uint64_t span_cap = B.d_keys.cap / 16;
         TM_TRY_HIP(o.r_runs.ensure(span_cap * 16), TM_ENOMEM, "pinned alloc");
-        TM_TRY_HIP(hipMemsetAsync(eng->bb->d_rcur.p, 0, 8, s), TM_EDEVICE, "memset");
-        unsigned long long *cur = eng->bb->d_rcur.as<unsigned long long>();
+        TM_TRY_HIP(hipMemsetAsync(B.d_rcur.p, 0, 8, s), TM_EDEVICE, "memset");
+        unsigned long long *cur = B.d_rcur.as<unsigned long long>();
         auto stage = [&](uint32_t j) -> int {
             const uint32_t lo = b[j], hi = b[j + 1];
             const uint64_t blo = off[lo] - base, bhi = off[hi] - base;
@@ -3767,32 +3826,37 @@ static int match_runs_impl(tm_engine *eng, HostOut &o, const uint8_t *bytes, con
             }
             // on their own stream: sub-batch j+1's topics cross PCIe while sub-batch j walks
             if (bhi > blo)
-                TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_bytes.as<uint8_t>() + blo, src, bhi - blo, hipMemcpyHostToDevice, hq),
+                TM_TRY_HIP(hipMemcpyAsync(B.d_bytes.as<uint8_t>() + blo, src, bhi - blo, hipMemcpyHostToDevice, hq),
                            TM_EDEVICE, "H2D");
-            TM_TRY_HIP(hipMemcpyAsync(eng->bb->d_off.as<uint32_t>() + lo, ho + lo, ((size_t)hi - lo + 1) * 4,
+            TM_TRY_HIP(hipMemcpyAsync(B.d_off.as<uint32_t>() + lo, ho + lo, ((size_t)hi - lo + 1) * 4,
                                       hipMemcpyHostToDevice, hq),
                        TM_EDEVICE, "H2D");
-            TM_TRY_HIP(hipEventRecord(eng->ev_h2d[j], hq), TM_EDEVICE, "event");
+            TM_TRY_HIP(hipEventRecord(o.ev_h2d[j], hq), TM_EDEVICE, "event");
             return TM_OK;
         };
         auto walk = [&](uint32_t j) -> int {
             const uint32_t lo = b[j], hi = b[j + 1], h = j & 1;
-            TM_TRY_HIP(hipStreamWaitEvent(s, eng->ev_h2d[j], 0), TM_EDEVICE, "wait");
-            TM_TRY_HIP(enqueue_match(eng, eng->bb->d_bytes.as<uint8_t>(), eng->bb->d_off.as<uint32_t>() + lo, hi - lo, s,
-                                     MODE_RUNS, lo, eng->bb->d_keys.as<uint32_t>(), span_cap, cur, nullptr,
-                                     runs_tpw_of(hi - lo)),
-                       TM_EDEVICE, "kernel launch");
+            TM_TRY_HIP(hipStreamWaitEvent(s, o.ev_h2d[j], 0), TM_EDEVICE, "wait");
+            const uint8_t *pctl;
+            {
+                std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+                eng->bb = &B;
+                TM_TRY_HIP(enqueue_match(eng, B.d_bytes.as<uint8_t>(), B.d_off.as<uint32_t>() + lo, hi - lo, s, MODE_RUNS,
+                                         lo, B.d_keys.as<uint32_t>(), span_cap, cur, nullptr, runs_tpw_of(hi - lo)),
+                           TM_EDEVICE, "kernel launch");
+                TM_TRY_HIP(eng->note_use(s), TM_EDEVICE, "event");
+                pctl = B.p_ctl;
+            }
             TM_TRY_HIP(hipMemcpyAsync(rctl + 8 * j, cur, 8, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
-            TM_TRY_HIP(hipMemcpyAsync(rctl + 8 * j + 1, eng->bb->p_ctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-                       "D2H");
-            TM_TRY_HIP(hipEventRecord(eng->ev_pk[h], s), TM_EDEVICE, "event");
+            TM_TRY_HIP(hipMemcpyAsync(rctl + 8 * j + 1, pctl, CTL_BYTES, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+            TM_TRY_HIP(hipEventRecord(o.ev_pk[h], s), TM_EDEVICE, "event");
             return TM_OK;
         };
         uint64_t prev = 0, slow = 0, seg_d = 0, fr_d = 0;
         bool over = false;
         auto finish = [&](uint32_t j) -> int {  // sub-batch j walked: its results cross PCIe
             const uint32_t lo = b[j], hi = b[j + 1], h = j & 1;
-            TM_TRY_HIP(hipEventSynchronize(eng->ev_pk[h]), TM_EDEVICE, "match kernels");
+            TM_TRY_HIP(hipEventSynchronize(o.ev_pk[h]), TM_EDEVICE, "match kernels");
             const uint64_t c_j = rctl[8 * j];
             slow += (uint32_t)rctl[8 * j + 2];
             seg_d = std::max(seg_d, rctl[8 * j + 3]);
@@ -3802,14 +3866,14 @@ static int match_runs_impl(tm_engine *eng, HostOut &o, const uint8_t *bytes, con
                 prev = c_j;
                 return TM_OK;
             }
-            TM_TRY_HIP(hipStreamWaitEvent(c, eng->ev_pk[h], 0), TM_EDEVICE, "wait");
+            TM_TRY_HIP(hipStreamWaitEvent(c, o.ev_pk[h], 0), TM_EDEVICE, "wait");
             if (c_j > prev)  // DMA: a copy kernel here competes with the next sub-batch's walk
-                TM_TRY_HIP(hipMemcpyAsync(o.r_runs.as<uint8_t>() + prev * 16, eng->bb->d_keys.as<uint8_t>() + prev * 16,
+                TM_TRY_HIP(hipMemcpyAsync(o.r_runs.as<uint8_t>() + prev * 16, B.d_keys.as<uint8_t>() + prev * 16,
                                           (c_j - prev) * 16, hipMemcpyDeviceToHost, c),
                            TM_EDEVICE, "D2H");
             for (std::pair<PinBuf *, DevBuf *> pr :
-                 {std::make_pair(&o.r_off, &eng->bb->d_outoff), std::make_pair(&o.r_cnt, &eng->bb->d_outcnt),
-                  std::make_pair(&o.r_kcnt, &eng->bb->d_kcnt), std::make_pair(&o.r_status, &eng->bb->d_status)})
+                 {std::make_pair(&o.r_off, &B.d_outoff), std::make_pair(&o.r_cnt, &B.d_outcnt),
+                  std::make_pair(&o.r_kcnt, &B.d_kcnt), std::make_pair(&o.r_status, &B.d_status)})
                 TM_TRY_HIP(hipMemcpyAsync(pr.first->as<uint32_t>() + lo, pr.second->as<uint32_t>() + lo,
                                           ((size_t)hi - lo) * 4, hipMemcpyDeviceToHost, c),
                            TM_EDEVICE, "D2H");
@@ -3825,10 +3889,14 @@ static int match_runs_impl(tm_engine *eng, HostOut &o, const uint8_t *bytes, con
         TM_TRY_HIP(hipStreamSynchronize(hq), TM_EDEVICE, "sync");
         TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "sync");
         TM_TRY_HIP(hipStreamSynchronize(c), TM_EDEVICE, "D2H");
-        eng->n_slow_last = slow;
-        eng->bb->seg_demand_last = seg_d;
-        eng->bb->fr_demand_last = fr_d;
-        if ((rc = grow_pools(eng))) return rc;
+        {
+            std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+            eng->bb = &B;
+            eng->n_slow_last = slow;
+            B.seg_demand_last = seg_d;
+            B.fr_demand_last = fr_d;
+            if ((rc = grow_pools(eng))) return rc;
+        }
         if (over) {  // more spans than estimated: size from the demand seen so far, run again
             uint32_t done = 0;
             for (uint32_t j = 0; j < S; j++)
@@ -3836,10 +3904,10 @@ static int match_runs_impl(tm_engine *eng, HostOut &o, const uint8_t *bytes, con
                     done = b[j + 1];
                     break;
                 }
-            eng->runs_spt = std::max(eng->runs_spt * 2, (double)prev / std::max<uint32_t>(done, 1));
+            o.runs_spt = std::max(o.runs_spt * 2, (double)prev / std::max<uint32_t>(done, 1));
             continue;
         }
-        eng->runs_spt = (double)prev / n;
+        o.runs_spt = (double)prev / n;
         uint64_t tot = 0;
         const uint32_t *kc = o.r_kcnt.as<uint32_t>();
         for (uint32_t i = 0; i < n; i++) tot += kc[i];
