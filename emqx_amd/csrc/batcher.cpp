@@ -307,6 +307,10 @@ struct tm_batcher {
                      eng ? tm_last_error(eng) : "custom backend", bt_err[0] ? "; " : "", bt_err);
     }
     bool runs_ok = false;        // runs transport in use (TM_MATCH_ALL windows of a master engine)
+    // delivery prefetch (runs transport): replies this many publishes ahead have their spans'
+    // first line prefetched, or (pf_lines > 0) up to pf_lines lines of them (development knobs
+    // EMQX_TM_PF_PUBS / EMQX_TM_PF_LINES)
+    uint32_t pf_pubs = 6, pf_lines = 0;
     // two compute streams, each with its own engine buffer set: consecutive windows alternate,
     // so one window's walk starts while the previous one's last waves finish
     hipStream_t s_comps[2] = {}, s_copy = nullptr;
@@ -720,10 +724,21 @@ struct tm_batcher {
             uint64_t now = 0;
             // the id arena is read at random places (a span's start, an inline key's id): start
             // the loads of a few publishes ahead so the replies do not wait on each miss in turn
-            constexpr uint32_t PF = 6;
+            const uint32_t PF = pf_pubs;
             auto prefetch = [&](uint32_t i) {
                 const uint32_t b = so[i], e = b + std::min<uint32_t>(sc[i], 4);
-                for (uint32_t j = b; j < e; j++) __builtin_prefetch(spans[j].ids);
+                if (!pf_lines) {
+                    for (uint32_t j = b; j < e; j++) __builtin_prefetch(spans[j].ids);
+                    return;
+                }
+                // every line of the reply's first spans, up to pf_lines lines
+                uint32_t left = pf_lines;
+                for (uint32_t j = b; j < e && left; j++) {
+                    const char *p = (const char *)spans[j].ids;
+                    const char *end = p + spans[j].n * 8;
+                    for (p = (const char *)((uintptr_t)p & ~(uintptr_t)63); p < end && left; p += 64, left--)
+                        __builtin_prefetch(p);
+                }
             };
             for (uint32_t i = lo; i < std::min(hi, lo + PF); i++) prefetch(i);
             for (uint32_t i = lo; i < hi; i++) {
@@ -987,6 +1002,8 @@ struct tm_batcher {
         t_window = std::chrono::steady_clock::now();
         (void)now_ns();  // calibrate the clock before the first publish is stamped
         if (const char *e = std::getenv("EMQX_TM_NSLOT")) nslot = std::max(2u, std::min(NSLOT_MAX, (uint32_t)std::atoi(e)));
+        if (const char *e = std::getenv("EMQX_TM_PF_PUBS")) pf_pubs = std::max(1u, std::min(64u, (uint32_t)std::atoi(e)));
+        if (const char *e = std::getenv("EMQX_TM_PF_LINES")) pf_lines = std::min(256u, (uint32_t)std::atoi(e));
         if (!eng)
             for (Slot &S : slot)
                 for (HBuf *h : {&S.h_bytes, &S.h_off, &S.h_off_out, &S.h_status, &S.h_cnt, &S.h_ids, &S.h_ctl})

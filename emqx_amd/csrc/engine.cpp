@@ -293,8 +293,10 @@ struct CopyPool {
             });
     }
     void copy(void *dst, const void *src, size_t n) {
-        const size_t per = 2u << 20;
-        const size_t parts = std::min<size_t>(th.size() + 1, (n + per - 1) / per);
+        // the pool only for large batches: several threads' calls may share it, and a small copy
+        // is cheaper on the calling thread than a hand-off
+        const size_t per = 4u << 20;
+        const size_t parts = n < (8u << 20) ? 1 : std::min<size_t>(th.size() + 1, (n + per - 1) / per);
         if (parts <= 1 || th.empty()) {
             if (n) memcpy(dst, src, n);
             return;
@@ -1087,19 +1089,31 @@ struct tm_engine {
     // A prefix stays valid while ops apply (nodes are only ever added), and an op whose
     // path appears only during this epoch resumes from where resolution stopped.
     // nwalk[i]: levels of the trie path an ADD creates or reuses (0: no path).
+    // pkind[i]: the key kind when the op's whole path already exists (its key would hang at
+    // hnode[i]), else PK_NONE: the apply loop prefetches the key-set slot of such ops ahead.
+    static constexpr uint8_t PK_NONE = 0xFF;
     void resolve_all(const std::vector<StagedOp> &ops, const uint8_t *ob, std::vector<uint32_t> &hnode,
-                     std::vector<uint32_t> &hdepth, std::vector<uint32_t> &nwalk) const {
+                     std::vector<uint32_t> &hdepth, std::vector<uint32_t> &nwalk, std::vector<uint8_t> &pkind) const {
         const size_t n = ops.size();
         auto one = [&](size_t i, std::vector<std::pair<uint32_t, uint32_t>> &lv) {
             const uint8_t *f = ob + ops[i].off;
             resolve_prefix(f, ops[i].len, lv, &hnode[i], &hdepth[i]);
-            if (ops[i].op != TM_OP_ADD) return;
             // a '#' before the last level: a dead key, no path; a final '#': the path stops above it
             int hash_pos = -1;
-            for (size_t k = 0; k < lv.size() && hash_pos < 0; k++)
-                if (lv[k].second == 1 && f[lv[k].first] == '#') hash_pos = (int)k;
-            if (hash_pos >= 0 && hash_pos != (int)lv.size() - 1) nwalk[i] = 0;
-            else nwalk[i] = (uint32_t)(hash_pos >= 0 ? lv.size() - 1 : lv.size());
+            bool wild = false;
+            for (size_t k = 0; k < lv.size(); k++)
+                if (lv[k].second == 1 && (f[lv[k].first] == '#' || f[lv[k].first] == '+')) {
+                    wild = true;
+                    if (f[lv[k].first] == '#' && hash_pos < 0) hash_pos = (int)k;
+                }
+            const bool dead = hash_pos >= 0 && hash_pos != (int)lv.size() - 1;
+            const uint32_t levels = (uint32_t)(hash_pos >= 0 ? lv.size() - 1 : lv.size());
+            pkind[i] = PK_NONE;
+            if (!dead && hdepth[i] == levels)
+                pkind[i] = !wild ? ((ops[i].flags & TM_KEY_WORDS) ? K_EXACT_WORDS : K_EXACT_BIN)
+                                 : (hash_pos >= 0 ? K_HASH : K_WILD);
+            if (ops[i].op != TM_OP_ADD) return;
+            nwalk[i] = dead ? 0 : levels;
         };
         const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         const unsigned nt = n < 4096 ? 1u : (unsigned)std::min<size_t>(hw, n / 2048);
@@ -1224,38 +1238,93 @@ struct tm_engine {
         need_full = true;
     }
 
-    // Fold this epoch's deltas into the arena by appending new lists for dirty nodes.
+    // Fold this epoch's deltas into the arena.  Per dirty node, in parallel (read-only on the
+    // host copy): its new key list, the list header's minima and the ids of its keys, i.e.
+    // every random read of the key records a list needs.  Then in node order, sequentially:
+    // the list is rewritten in place when it fits its room, else appended (the arena grows).
+    struct NewList {
+        std::vector<uint32_t> keys;  // term keys, then '#' keys
+        std::vector<uint64_t> ids;   // their ids (the host id arena's words)
+        uint32_t tc = 0, hc = 0, mb = NONE, mw = NONE, mh = NONE;
+    };
+    void build_list(size_t i, size_t j, NewList &L) const {
+        const uint32_t node = deltas[i].node;
+        const NodeList r = node_list[node];
+        std::vector<uint32_t> terms(arena.begin() + r.list_off, arena.begin() + r.list_off + r.term_cnt);
+        std::vector<uint32_t> hashes(arena.begin() + r.list_off + r.term_cnt,
+                                     arena.begin() + r.list_off + r.term_cnt + r.hash_cnt);
+        for (size_t k = i; k < j; k++) {
+            std::vector<uint32_t> &Lst = deltas[k].hash ? hashes : terms;
+            if (deltas[k].add) {
+                Lst.push_back(deltas[k].key);
+            } else {
+                auto it = std::find(Lst.begin(), Lst.end(), deltas[k].key);
+                if (it != Lst.end()) Lst.erase(it);
+            }
+        }
+        L.tc = (uint32_t)terms.size();
+        L.hc = (uint32_t)hashes.size();
+        L.keys = std::move(terms);
+        L.keys.insert(L.keys.end(), hashes.begin(), hashes.end());
+        L.ids.resize(L.keys.size());
+        auto take = [&](uint32_t &m, uint32_t h) {
+            if (m == NONE || keys[h].id < keys[m].id) m = h;
+        };
+        for (uint32_t q = 0; q < L.tc + L.hc; q++) {
+            const uint32_t h = L.keys[q];
+            L.ids[q] = keys[h].id;
+            if (q < L.tc) take(keys[h].kind == K_EXACT_BIN ? L.mb : L.mw, h);
+            else take(L.mh, h);
+        }
+    }
+    void place_header(uint32_t pos, const NewList &L) {
+        arena[pos - 5] = L.mb;
+        arena[pos - 4] = L.mw;
+        arena[pos - 3] = L.mh;
+        arena[pos - 2] = L.tc;
+        arena[pos - 1] = L.hc;
+    }
+    void place_ids(uint64_t pos, const NewList &L) {
+        if (!arena_id) return;
+        uint64_t n = L.ids.size();
+        if (pos + n > arena_id_res) {  // past the reservation: only until the compaction this forces
+            ids_stale = true;
+            n = pos < arena_id_res ? arena_id_res - pos : 0;
+        }
+        if (n) memcpy(arena_id + pos, L.ids.data(), n * 8);
+    }
     void apply_deltas() {
         std::stable_sort(deltas.begin(), deltas.end(),
                          [](const Delta &a, const Delta &b) { return a.node < b.node; });
-        std::vector<uint32_t> terms, hashes;
-        size_t i = 0;
-        while (i < deltas.size()) {
-            size_t j = i;
-            uint32_t node = deltas[i].node;
-            while (j < deltas.size() && deltas[j].node == node) j++;
+        std::vector<size_t> gs;  // group g: deltas [gs[g], gs[g + 1]) of one node
+        for (size_t i = 0; i < deltas.size(); i++)
+            if (i == 0 || deltas[i].node != deltas[i - 1].node) gs.push_back(i);
+        gs.push_back(deltas.size());
+        const size_t G = gs.size() - 1;
+        std::vector<NewList> nl(G);
+        const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        const unsigned nt = G < 512 ? 1u : (unsigned)std::min<size_t>(hw, G / 256);
+        if (nt <= 1) {
+            for (size_t g = 0; g < G; g++) build_list(gs[g], gs[g + 1], nl[g]);
+        } else {
+            std::vector<std::thread> th;
+            for (unsigned k = 0; k < nt; k++)
+                th.emplace_back([&, k] {
+                    for (size_t g = k; g < G; g += nt) build_list(gs[g], gs[g + 1], nl[g]);
+                });
+            for (auto &t : th) t.join();
+        }
+        for (size_t g = 0; g < G; g++) {
+            const uint32_t node = deltas[gs[g]].node;
             const NodeList r = node_list[node];
-            terms.assign(arena.begin() + r.list_off, arena.begin() + r.list_off + r.term_cnt);
-            hashes.assign(arena.begin() + r.list_off + r.term_cnt,
-                          arena.begin() + r.list_off + r.term_cnt + r.hash_cnt);
-            for (size_t k = i; k < j; k++) {
-                std::vector<uint32_t> &Lst = deltas[k].hash ? hashes : terms;
-                if (deltas[k].add) {
-                    Lst.push_back(deltas[k].key);
-                } else {
-                    auto it = std::find(Lst.begin(), Lst.end(), deltas[k].key);
-                    if (it != Lst.end()) Lst.erase(it);
-                }
-            }
-            const uint32_t tc = (uint32_t)terms.size(), hc = (uint32_t)hashes.size(), cap = node_cap[node];
+            NewList &L = nl[g];
+            const uint32_t tc = L.tc, hc = L.hc, cap = node_cap[node];
             if (r.list_off && tc + hc && tc + hc <= cap) {
                 // fits the list's room: rewrite it in place (header + keys), so the churn of a
                 // long list (a hot '#' prefix's subscribers) leaves no garbage behind
-                uint32_t *dst = &arena[r.list_off];
-                std::copy(terms.begin(), terms.end(), dst);
-                std::copy(hashes.begin(), hashes.end(), dst + tc);
-                write_header(r.list_off, terms.data(), tc, hashes.data(), hc);
-                ids_of(r.list_off, (uint64_t)r.list_off + tc + hc);
+                std::copy(L.keys.begin(), L.keys.end(), arena.begin() + r.list_off);
+                place_header(r.list_off, L);
+                place_ids(r.list_off, L);
                 for (uint64_t w = r.list_off - LIST_HDR; w < (uint64_t)r.list_off + tc + hc; w++)
                     if (w < arena_dev) dirty_arena.push_back(w);
                 node_list[node] = NodeList{r.list_off, tc, hc};
@@ -1263,11 +1332,20 @@ struct tm_engine {
                 arena_garbage += cap + (r.list_off ? LIST_HDR : 0);
                 // lists of 16 keys or more get a quarter more room when they move
                 const uint32_t room = tc + hc >= 16 ? tc + hc + (tc + hc) / 4 : tc + hc;
-                node_list[node] = append_list(terms.data(), tc, hashes.data(), hc, room);
+                if (tc + hc == 0) {
+                    node_list[node] = NodeList{0, 0, 0};
+                } else {
+                    arena.resize(arena.size() + LIST_HDR);
+                    const uint32_t off = (uint32_t)arena.size();
+                    arena.insert(arena.end(), L.keys.begin(), L.keys.end());
+                    if (room > tc + hc) arena.resize(arena.size() + (room - tc - hc), 0u);
+                    place_header(off, L);
+                    place_ids(off, L);
+                    node_list[node] = NodeList{off, tc, hc};
+                }
                 node_cap[node] = tc + hc ? room : 0;
             }
             refresh_info(node);
-            i = j;
         }
     }
 
@@ -1663,7 +1741,8 @@ struct tm_engine {
         const uint64_t t0 = now_us();
         const size_t n = ops.size();
         std::vector<uint32_t> hnode(n, ROOT), hdepth(n, 0), nwalk(n, 0);
-        resolve_all(ops, ob.data(), hnode, hdepth, nwalk);
+        std::vector<uint8_t> pkind(n, PK_NONE);
+        resolve_all(ops, ob.data(), hnode, hdepth, nwalk, pkind);
         int rc = capacity_check(ops, ob.data(), hdepth, nwalk);
         if (rc) {
             restage(ops, ob);
@@ -1678,7 +1757,24 @@ struct tm_engine {
             ~Unblock() { e->leases_unblock(); }
         } unblock{this};
         std::lock_guard<std::mutex> gh(mu_host);
-        for (size_t i = 0; i < n; i++) apply_one(ops[i], ob.data(), hnode[i], hdepth[i]);
+        // Ops apply in order (last op per key wins), each a few dependent random reads of host
+        // tables far larger than the caches (key set, key records, ids).  Their addresses are
+        // known ahead for ops whose path exists: a two-stage prefetch (the key-set slot 16 ops
+        // ahead, then the key record and id slot it leads to 8 ops ahead) overlaps those misses.
+        auto pf_slot = [&](size_t i) {
+            if (pkind[i] != PK_NONE) __builtin_prefetch(&kset[key_hash(hnode[i], pkind[i], ops[i].id) & kmask]);
+        };
+        auto pf_key = [&](size_t i) {
+            if (!idtab.empty()) __builtin_prefetch(&idtab[mix64(ops[i].id) & (idtab.size() - 1)]);
+            if (pkind[i] == PK_NONE) return;
+            const uint32_t h = kset[key_hash(hnode[i], pkind[i], ops[i].id) & kmask];
+            if (h != NONE) __builtin_prefetch(&keys[h]);
+        };
+        for (size_t i = 0; i < n; i++) {
+            if (i + 16 < n) pf_slot(i + 16);
+            if (i + 8 < n) pf_key(i + 8);
+            apply_one(ops[i], ob.data(), hnode[i], hdepth[i]);
+        }
         if (edge_full) {  // cannot happen after capacity_check; never serve a half-applied trie
             err = "internal: edge table overflow past the capacity check";
             return TM_EDEVICE;
@@ -3796,7 +3892,9 @@ static int match_runs_impl(tm_engine *eng, HostOut &o, const uint8_t *bytes, con
     const bool direct = host_pinned(bytes + base);  // DMA straight from the caller's batch
     if (!direct) TM_TRY_HIP(o.h_bytes.ensure(nbytes + 16), TM_ENOMEM, "pinned alloc");
     if (!direct) std::call_once(eng->copier_once, [eng] { eng->copier.start(3); });
-    hipStream_t s = o.s_walk, c = o.s_copy, hq = o.s_h2d;
+    // one sub-batch: everything in order on the thread's walk stream (no cross-stream waits, and
+    // one hardware queue per calling thread); several: H2D, walks and D2H on three streams
+    hipStream_t s = o.s_walk, c = S > 1 ? o.s_copy : o.s_walk, hq = S > 1 ? o.s_h2d : o.s_walk;
     B.last_n = 0;
     B.dev_batch = false;  // the device result is in span form, not keys
     uint32_t *ho = o.h_off.as<uint32_t>();

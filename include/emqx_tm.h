@@ -59,7 +59,12 @@
  *     until that thread's next call of the same kind.  Device results (tm_dev_result) belong
  *     to the engine: valid until the next tm_match_device* call from ANY thread, which the
  *     engine orders after everything already queued on the previous call's stream (keep
- *     that stream alive until then).  tm_last_error() is per thread.
+ *     that stream alive until then).  tm_last_error() is per thread.  Host-form calls
+ *     (tm_match_batch, tm_match_batch_runs) of different threads run concurrently: each
+ *     thread has its own device lane (batch buffers, streams, pinned staging), and a call
+ *     holds the engine's device lock only while it queues work that reads the index
+ *     (UNIQUE / AGGRE and word-list topics keep it for the whole call).  Give the process
+ *     one HIP hardware queue per concurrent caller or more (GPU_MAX_HW_QUEUES).
  */
 #ifndef EMQX_TM_H
 #define EMQX_TM_H
@@ -229,8 +234,10 @@ int tm_apply_packed(tm_engine *eng, uint32_t op, const uint8_t *bytes, const uin
 int tm_commit_epoch(tm_engine *eng, uint64_t *epoch_out);
 /* Drop every staged op (e.g. a batch a capacity error refused); *n_out = ops dropped. */
 int tm_discard_staged(tm_engine *eng, uint64_t *n_out);
-/* Free the calling thread's host result buffers (tm_result / tm_intersect_result / runs) and
- * end its runs lease; results it still points to become invalid. */
+/* Free the calling thread's host result buffers (tm_result / tm_intersect_result / runs), its
+ * device lane (the batch buffers and streams its host-form calls use) and end its runs lease;
+ * results it still points to become invalid.  A thread that stops calling the engine calls it
+ * (a NIF's dirty scheduler threads live as long as the VM and need not). */
 int tm_result_release(tm_engine *eng);
 
 /* reads ------------------------------------------------------------------- */

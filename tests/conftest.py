@@ -7,6 +7,12 @@ import pytest
 # first serves the whole process.  Load torch's before libemqx_tm.so so that GPU tests
 # that mix torch device tensors with the engine run on one HIP runtime (bench.py and
 # __graft_entry__ already import in that order or do not use torch at all).
+# Several host-form callers at once (tests/test_gpu_concurrency.py) each use their own streams;
+# HIP's default of 4 hardware queues per process would put streams of different threads on one
+# in-order queue.  bench.py asks for 8 as well.  Set before HIP starts.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 import torch  # noqa: E402,F401
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

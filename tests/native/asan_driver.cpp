@@ -13,6 +13,7 @@
 #include <atomic>
 #include <thread>
 #include <cstdio>
+#include <unistd.h>
 #include <cstdlib>
 #include <cstring>
 #include <random>
@@ -290,5 +291,9 @@ int main() {
     CHECK(tm_match_batch(eng, nullptr, nullptr, 0, 7, nullptr) == TM_EINVAL);
     tm_destroy(eng);
     printf("asan driver ok\n");
-    return 0;
+    fflush(stdout);
+    // every engine and batcher is destroyed above (their frees ran under ASan); skip the HIP
+    // runtime's own static teardown, where ASan's device-allocator quarantine can recycle a
+    // chunk after the device runtime unloaded (a CHECK inside ASan, not a finding in this code)
+    _exit(0);
 }

@@ -1,4 +1,6 @@
-"""The headline configuration at full size (BASELINE.json configs[2], "10M filters, deep
+"""Full-size configurations in the GPU suite: config B (1 M filters, configs[1]), config E
+(1 M keys + 5 churn epochs, configs[4]) and the headline configuration (BASELINE.json
+configs[2], "10M filters, deep
 10-level topics, '#'-heavy fan-out"): 10.65 M route keys, one 1 M-publish batch, through the
 C-ABI, against the oracle's emqx_trie_search restatement over the SAME keys and topics.
 
@@ -49,6 +51,113 @@ def _digests(vals, starts, cnt):
             s[nz] = np.add.reduceat(m, starts[:-1][nz])
         x[nz] = np.bitwise_xor.reduceat(m, starts[:-1][nz])
     return s, x
+
+
+def _check_full_batch(eng, w, ix, sample, seed=0xC0FFEE, t_bytes=None, t_off=None):
+    """ALL over the whole batch vs the oracle index `ix`: statuses, counts, per-topic digests of
+    the id multisets, and `sample` topics id for id.  Returns (cnt, st) of ALL."""
+    t_bytes = w.t_bytes if t_bytes is None else t_bytes
+    t_off = w.t_off if t_off is None else t_off
+    n = len(t_off) - 1
+    off, cnt, keys, st = eng.match_packed(t_bytes, t_off)
+    ids = eng.key_ids(keys)
+    del keys
+    cnt64 = cnt.astype(np.int64)
+    starts = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(cnt64, out=starts[1:])
+    total = int(starts[-1])
+    idx = np.repeat(off.astype(np.int64) - starts[:-1], cnt64) + np.arange(total, dtype=np.int64)
+    v = ids[idx]
+    del idx, ids
+    eo, eids, est = ix.match(t_bytes, t_off, threads=16)
+    assert np.array_equal(st, est)
+    assert np.array_equal(cnt64, np.diff(eo).astype(np.int64))
+    es, ex = _digests(eids, eo.astype(np.int64), np.diff(eo).astype(np.int64))
+    gs, gx = _digests(v, starts, cnt64)
+    bad = np.nonzero((es != gs) | (ex != gx))[0]
+    assert len(bad) == 0, f"{len(bad)} topics differ, first {bad[:8]}"
+    rng = np.random.default_rng(seed)
+    for i in rng.choice(n, min(sample, n), replace=False):
+        got = np.sort(v[starts[i]:starts[i + 1]])
+        assert np.array_equal(got, eids[eo[i]:eo[i + 1]]), f"topic {i}"
+    return cnt, st, total
+
+
+@pytest.mark.timeout(300)
+def test_config_b_full_batch_vs_oracle():
+    """BASELINE configs[1] at full size: 1 M filters over 6-level topics (10 % '+', 5 % '#'),
+    one 1 M-publish batch: every topic by digest, 20,000 id for id, COUNT and FIRST."""
+    w = workloads.generate("B", scale=1.0, n_topics=1_000_000)
+    assert w.n_keys >= 1_000_000
+    eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
+    try:
+        eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+        eng.commit()
+        ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+        cnt, st, total = _check_full_batch(eng, w, ix, 20_000)
+        assert total > w.n_topics // 4  # about half of the publishes hit existing filters
+        _, ccnt, _, cst = eng.match_packed(w.t_bytes, w.t_off, N.TM_MATCH_COUNT)
+        assert np.array_equal(ccnt, cnt) and np.array_equal(cst, st)
+        foff, fcnt, fkeys, fst = eng.match_packed(w.t_bytes, w.t_off, N.TM_MATCH_FIRST)
+        assert np.array_equal(fst, st)
+        assert np.array_equal(fcnt.astype(np.int64), (cnt.astype(np.int64) > 0).astype(np.int64))
+        feo, feids, _ = ix.match(w.t_bytes, w.t_off, mode=oracle.MODE_FIRST, threads=16)
+        assert np.array_equal(eng.key_ids(fkeys[foff[fcnt > 0].astype(np.int64)]), feids)
+    finally:
+        eng.close()
+
+
+def _new_filter(f, n):
+    """A new valid filter near f: one more level, before a trailing '#' (bench.py _new_filter)."""
+    if f == b"#":
+        return b"n%d/#" % n
+    if f.endswith(b"/#"):
+        return f[:-2] + b"/n%d/#" % n
+    return f + b"/n%d" % n
+
+
+@pytest.mark.timeout(400)
+def test_config_e_full_size_churn_vs_oracle():
+    """BASELINE configs[4] at full size: 1 M route keys with $SYS topics, root '#', '+/...' and
+    $share duplicates, then 5 delta epochs of 1 % adds + 1 % deletes (half new dests on live
+    filters, half new filters), each committed between batches.  After EVERY epoch the whole
+    1 M-publish batch is checked by digest against an oracle over that epoch's keys; the last
+    epoch also 20,000 topics id for id."""
+    w = workloads.generate("E", scale=1.0, n_topics=1_000_000)
+    assert w.n_keys >= 1_000_000
+    eng = N.Engine(0, reserve_keys=w.n_keys * 2, reserve_nodes=w.n_keys * 8)
+    try:
+        eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+        eng.commit()
+        live_f = w.filters()
+        live_id = w.f_id.astype(np.uint64).copy()
+        next_id = int(live_id.max()) + 1
+        rng = np.random.default_rng(0xE11A0005)
+        kinds = []
+        for ep in range(5):
+            k = max(1, len(live_id) // 100)
+            dsel = rng.choice(len(live_id), size=k, replace=False)
+            keep = np.ones(len(live_id), dtype=bool)
+            keep[dsel] = False
+            src = rng.integers(0, len(live_f), size=k)
+            add_f = [live_f[j] if (i & 1) else _new_filter(live_f[j], next_id + i) for i, j in enumerate(src)]
+            add_id = np.arange(next_id, next_id + k, dtype=np.uint64)
+            next_id += k
+            db, do = N.pack_topics([live_f[i] for i in dsel])
+            ab, ao = N.pack_topics(add_f)
+            n_full = eng.stats()["n_full_rebuilds"]
+            eng.apply_packed(N.TM_OP_DEL, db, do.astype(np.uint64), live_id[dsel])
+            eng.apply_packed(N.TM_OP_ADD, ab, ao.astype(np.uint64), add_id)
+            eng.commit()
+            kinds.append("full" if eng.stats()["n_full_rebuilds"] > n_full else "delta")
+            live_f = [f for f, kk in zip(live_f, keep) if kk] + add_f
+            live_id = np.concatenate([live_id[keep], add_id])
+            ix = oracle.OrderedIndex.from_filters(live_f, live_id.tolist())
+            _check_full_batch(eng, w, ix, 20_000 if ep == 4 else 2_000, seed=ep)
+        assert eng.stats()["n_keys"] == len(live_id)
+        assert "delta" in kinds  # the churn really went through delta epochs
+    finally:
+        eng.close()
 
 
 def test_config_c_full_batch_vs_oracle():

@@ -1,8 +1,9 @@
 """Batcher sweep on one GPU (bench tooling): config C engine, closed-loop publishers through
 tm_batcher_submit for each (publishers, delivery threads, max_wait_us[, transport, spans callback,
 slots, max_batch, compute streams]) given, one JSON line each.
-Usage: python tools/batcher_gpu.py P:T:W[:TR:SP:NSLOT:MB:ST] ...   (TR 0 auto/runs, 1 ids; SP 1 = span callback;
-ST 1 or 2 compute streams, EMQX_TM_STREAMS).  PIN=1 pins the process to the GPU's socket first."""
+Usage: python tools/batcher_gpu.py P:T:W[:TR:SP:NSLOT:MB:ST:PFP:PFL] ...   (TR 0 auto/runs, 1 ids; SP 1 = span
+callback, 2 = span callback reading no id; ST 1 or 2 compute streams, EMQX_TM_STREAMS; PFP/PFL delivery prefetch:
+publishes ahead / lines per reply, 0 lines = first line of each span).  PIN=1 pins the process to the GPU's socket first."""
 import ctypes as C
 import json
 import os
@@ -30,9 +31,9 @@ def main():
     tb = np.ascontiguousarray(w.t_bytes, dtype=np.uint8)
     to32 = np.ascontiguousarray(w.t_off, dtype=np.uint32)
     lg = C.CDLL(os.path.join(ROOT, "tools", "libtm_loadgen.so"))
-    lg.loadgen_run2.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double, C.c_int,
-                                C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
-                                C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
+    U = C.POINTER(C.c_uint64)
+    lg.loadgen_run3.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double, C.c_double,
+                                C.c_int, U, U, U, U, C.POINTER(C.c_double), C.POINTER(N.tm_batcher_stats)]
     if os.environ.get("HOSTPATH"):  # tm_match_batch with host buffers, 1 M publishes per call
         eng.match_packed_view(tb, to32)
         ts = []
@@ -44,21 +45,30 @@ def main():
                           "publishes_per_s": round(len(to32) / 1 / min(ts) if False else (len(to32) - 1) / float(np.median(ts)))}),
               flush=True)
     for spec in sys.argv[1:]:
-        v = [int(x) for x in spec.split(":")] + [0, 0, 4, 65536, 2][len(spec.split(":")) - 3:]
+        v = [int(x) for x in spec.split(":")]
+        v = v + [0, 0, 6, 65536, 2, 6, 0][len(v) - 3:]
         pubs, th, wait, tr, sp, nslot, mb, nst = v[:8]
         os.environ["EMQX_TM_NSLOT"] = str(nslot)
         os.environ["EMQX_TM_STREAMS"] = str(nst)
+        pfp, pfl = (v[8], v[9]) if len(v) > 9 else (6, 0)  # delivery prefetch knobs
+        os.environ["EMQX_TM_PF_PUBS"] = str(pfp)
+        os.environ["EMQX_TM_PF_LINES"] = str(pfl)
         b = N.Batcher(eng, max_batch=mb, max_wait_us=wait, delivery_threads=th, transport=tr)
         got, ids, errs, cs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
-        rc = lg.loadgen_run2(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, 2.0, sp, C.byref(got),
-                             C.byref(ids), C.byref(errs), C.byref(cs), C.byref(el))
+        win = N.tm_batcher_stats()
+        rc = lg.loadgen_run3(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, 0.5, 2.0, sp, C.byref(got),
+                             C.byref(ids), C.byref(errs), C.byref(cs), C.byref(el), C.byref(win))
         st = b.stats()
         b.close()
         print(json.dumps({"publishers": pubs, "threads": th, "max_wait_us": wait, "transport": tr, "spans": sp,
                           "nslot": nslot, "max_batch": mb, "streams": nst, "rc": rc, "errors": errs.value,
-                          "publishes_per_s": round(got.value / el.value), "ids_per_publish": round(ids.value / max(got.value, 1), 1),
+                          "pf_pubs": pfp, "pf_lines": pfl,
+                          "publishes_per_s": round(win.lat_count / win.window_s),
+                          "publishes_per_s_whole_run": round(got.value / el.value),
+                          "ids_per_publish": round(ids.value / max(got.value, 1), 1),
                           "mean_batch": round(st["publishes"] / max(st["batches"], 1), 1),
-                          "p50_ms": round(st["lat_p50_us"] / 1e3, 3), "p99_ms": round(st["lat_p99_us"] / 1e3, 3),
+                          "mean_ms": round(win.lat_mean_us / 1e3, 3),
+                          "p50_ms": round(win.lat_p50_us / 1e3, 3), "p99_ms": round(win.lat_p99_us / 1e3, 3),
                           "busy": {k: round(st[k + "_us"] * 1e-6 / el.value, 3)
                                    for k in ("cut", "enqueue", "gpu_wait", "copy", "deliver")}}), flush=True)
 

@@ -37,6 +37,7 @@ struct Load {
     std::mutex m;
     std::condition_variable cv;
     bool spans = false;
+    bool no_read = false;  // spans == 2 (development): the callback reads no id (the pipeline's floor)
 };
 
 void on_result(void *ctx, int32_t status, const uint64_t *ids, uint32_t n);
@@ -73,8 +74,9 @@ void on_spans(void *ctx, int32_t status, const tm_span *sp, uint32_t ns, uint64_
     p->done++;
     p->ids += nids;
     uint64_t s = 0;
-    for (uint32_t j = 0; j < ns; j++)
-        for (uint64_t i = 0; i < sp[j].n; i++) s += sp[j].ids[i];
+    if (!p->L->no_read)
+        for (uint32_t j = 0; j < ns; j++)
+            for (uint64_t i = 0; i < sp[j].n; i++) s += sp[j].ids[i];
     p->sum += s;
     if (status < 0) p->errors++;
     next_or_retire(p);
@@ -101,6 +103,7 @@ extern "C" int loadgen_run3(tm_batcher *b, const uint8_t *bytes, const uint32_t 
     if (!b || !bytes || !off || !n_topics || !publishers) return TM_EINVAL;
     Load L;
     L.spans = spans != 0;
+    L.no_read = spans == 2;
     L.b = b;
     L.bytes = bytes;
     L.off = off;
@@ -178,4 +181,99 @@ extern "C" uint64_t spans_checksum(const tm_runs_result *r, uint32_t threads) {
         s += part[t];
     }
     return s;
+}
+
+// Host-form callers on `threads` native threads at once (tests/test_gpu_concurrency.py): thread k
+// makes `reps` calls on its own batch (bytes[k], offs[k], ns[k] topics) per round, `rounds`
+// rounds between barriers (the first ones warm each thread's engine lane, as a NIF's dirty
+// schedulers keep theirs); *wall_s_out = the LAST round's wall time.  form 0: tm_match_batch_runs,
+// 1: tm_match_batch (keys) + tm_key_ids.  digest_out[k]: over thread k's last result,
+// sum over topics t of sum over its ids of mix(id + t * golden), and every status folded in:
+// order-independent within a topic, tied to the topic.
+#include <cstring>
+namespace {
+struct Gate {
+    std::mutex m;
+    std::condition_variable cv;
+    uint32_t n, waiting = 0;
+    uint64_t gen = 0;
+    explicit Gate(uint32_t n_) : n(n_) {}
+    void wait() {
+        std::unique_lock<std::mutex> lk(m);
+        const uint64_t g = gen;
+        if (++waiting == n) {
+            waiting = 0;
+            gen++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g; });
+        }
+    }
+};
+inline uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+}  // namespace
+
+extern "C" int conc_calls(tm_engine *eng, int form, const uint8_t *const *bytes, const uint32_t *const *offs,
+                          const uint32_t *ns, uint32_t threads, uint32_t reps, uint32_t rounds, double *wall_s_out,
+                          uint64_t *digest_out) {
+    if (!eng || !threads || !reps || !rounds) return TM_EINVAL;
+    Gate start(threads + 1), done(threads + 1);
+    std::vector<int> rcs(threads, TM_OK);
+    std::vector<std::thread> th;
+    for (uint32_t k = 0; k < threads; k++)
+        th.emplace_back([&, k] {
+            std::vector<uint64_t> ids;
+            for (uint32_t r = 0; r < rounds; r++) {
+                start.wait();
+                for (uint32_t q = 0; q < reps && rcs[k] == TM_OK; q++) {
+                    const bool last = r + 1 == rounds && q + 1 == reps;
+                    uint64_t dg = 0;
+                    if (form == 0) {
+                        tm_runs_result res;
+                        rcs[k] = tm_match_batch_runs(eng, bytes[k], offs[k], ns[k], &res);
+                        if (rcs[k] == TM_OK && last)
+                            for (uint32_t t = 0; t < res.n; t++) {
+                                dg += mix64((uint64_t)(uint32_t)res.status[t] + 0x51ull * t);
+                                for (uint32_t j = res.span_off[t]; j < res.span_off[t] + res.span_cnt[t]; j++)
+                                    for (uint64_t i = 0; i < res.spans[j].n; i++)
+                                        dg += mix64(res.spans[j].ids[i] + 0x9E3779B97F4A7C15ull * t);
+                            }
+                    } else {
+                        tm_result res;
+                        rcs[k] = tm_match_batch(eng, bytes[k], offs[k], ns[k], TM_MATCH_ALL, &res);
+                        if (rcs[k] == TM_OK && last) {
+                            ids.resize(res.total + 1);
+                            if (res.total) rcs[k] = tm_key_ids(eng, res.keys, res.total, ids.data());
+                            for (uint32_t t = 0; t < res.n && rcs[k] == TM_OK; t++) {
+                                dg += mix64((uint64_t)(uint32_t)res.status[t] + 0x51ull * t);
+                                for (uint32_t i = 0; i < res.cnt[t]; i++)
+                                    dg += mix64(ids[res.off[t] + i] + 0x9E3779B97F4A7C15ull * t);
+                            }
+                        }
+                    }
+                    if (last) digest_out[k] = dg;
+                }
+                if (form == 0) tm_runs_release(eng);
+                done.wait();
+            }
+            tm_result_release(eng);  // this thread's lane
+        });
+    double wall = 0;
+    for (uint32_t r = 0; r < rounds; r++) {
+        start.wait();
+        const auto t0 = std::chrono::steady_clock::now();
+        done.wait();
+        wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    for (auto &t : th) t.join();
+    *wall_s_out = wall;
+    for (int rc : rcs)
+        if (rc != TM_OK) return rc;
+    return TM_OK;
 }
