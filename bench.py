@@ -399,6 +399,9 @@ def main():
     ap.add_argument("--config", default="C")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--batch", type=int, default=1_000_000)
+    ap.add_argument("--distinct-batches", type=int, default=4,
+                    help="N = 1: the timed steps cycle through this many distinct batches of --batch publishes "
+                         "(N > 1: through the ranks' slices)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work (s)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: every CPU this process may use, see cpu_topology)")
@@ -478,10 +481,14 @@ def main():
     # builds the ONE host master copy; every other rank gets a read replica of its device
     # index (tm_image_export -> RCCL broadcast -> tm_replica_create) and its topic slice
     # over the same group, so host memory and build work are one copy per node.
+    # The timed steps walk DISTINCT batches: rank r's step k walks slice (r + k) % n_slices of
+    # the generated publishes (N = 1: --distinct-batches slices; N > 1: the ranks' slices), so
+    # no step re-walks the batch the step before it walked.
+    n_slices = world if world > 1 else max(1, args.distinct_batches)
     t0 = time.time()
     w = None
     if rank == 0:
-        w = workloads.generate(args.config, scale=args.scale, n_topics=args.batch * world)
+        w = workloads.generate(args.config, scale=args.scale, n_topics=args.batch * n_slices)
     t_gen = time.time() - t0
     t0 = time.time()
     eng = None
@@ -499,7 +506,7 @@ def main():
         rix.start()
         eng = rix.ad.eng
         image_s = time.time() - t0
-        # topics: rank 0's whole batch to every rank, each keeps its slice (untimed)
+        # topics: rank 0's whole batch to every rank (untimed)
         tdev = dev if backend != "gloo" else torch.device("cpu")
         sz = torch.tensor([len(w.t_bytes), len(w.t_off)] if rank == 0 else [0, 0], dtype=torch.int64, device=tdev)
         dist.broadcast(sz, 0)
@@ -510,73 +517,87 @@ def main():
         dist.broadcast(all_b, 0)
         dist.broadcast(all_o, 0)
         all_b, all_o = all_b.to(dev), all_o.to(dev)
+    else:
+        all_b = torch.from_numpy(w.t_bytes).to(dev)
+        all_o = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
     st = eng.stats()
     log(f"[rank {rank}] {'generated ' + str(w.n_keys) + ' keys in ' + format(t_gen, '.1f') + 's, ' if w else ''}"
         f"engine build {t_build:.1f}s{', replica image ' + format(image_s, '.1f') + 's' if image_s else ''}, "
         f"keys {st['n_keys']}, nodes {st['n_nodes']}, words {st['n_words']}, "
         f"index {st['device_bytes'] / 2**30:.2f} GiB, host RSS {host_rss_gib()} GiB")
 
-    lo, hi = rank * args.batch, (rank + 1) * args.batch
-    n = hi - lo
-    if world > 1:
-        base = int(all_o[lo].item())
-        topic_bytes = int(all_o[hi].item()) - base
-        d_bytes = all_b[base:]
-        d_off = (all_o[lo:hi + 1] - base).contiguous()
-        tb, to = (w.topic_slice(lo, hi) if rank == 0 else (None, None))
-    else:
-        tb, to = w.topic_slice(lo, hi)
-        topic_bytes = int(to[-1])
-        d_bytes = torch.from_numpy(tb).to(dev)
-        d_off = torch.from_numpy(to.view(np.int32)).to(dev)
+    n = args.batch
+    slices = []  # per slice: (bytes view, rebased offsets, topic bytes), all in HBM
+    for j in range(n_slices):
+        a, b = j * n, (j + 1) * n
+        base = int(all_o[a].item())
+        slices.append((all_b[base:], (all_o[a:b + 1] - base).contiguous(), int(all_o[b].item()) - base))
+    own = rank % n_slices
+    d_bytes, d_off, topic_bytes = slices[own]
+    lo, hi = own * n, (own + 1) * n
+    tb, to = (w.topic_slice(lo, hi) if rank == 0 else (None, None))
     torch.cuda.synchronize()
     stream = torch.cuda.Stream(dev)  # kernels and timing events share this stream
     sp = stream.cuda_stream
 
-    def step():
-        return eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, topic_bytes, sp)
+    def step(j=own):
+        sb, so, stb = slices[j]
+        return eng.match_device(sb.data_ptr(), so.data_ptr(), n, stb, sp)
 
     # the timed steps alternate the engine's two direct buffer sets on two streams
     # (tm_match_device_set): step k+1's walk starts while step k's last waves finish
     streams2 = [stream, torch.cuda.Stream(dev)]
 
     def step2(k):
+        j = (own + k) % n_slices
         if args.sequential:
-            return step()
-        return eng.match_device_set(k % 2, d_bytes.data_ptr(), d_off.data_ptr(), n, topic_bytes, N.TM_MATCH_ALL,
+            return step(j)
+        sb, so, stb = slices[j]
+        return eng.match_device_set(k % 2, sb.data_ptr(), so.data_ptr(), n, stb, N.TM_MATCH_ALL,
                                     streams2[k % 2].cuda_stream)
 
-    # size the output arena from the first run (overflow -> grow -> rerun)
-    r = step()
-    eng.device_sync()  # also sizes the engine's chunk pools to this batch's demand
-    total = _read_u64(r.d_total)
+    # size the output arena from one run of every slice (overflow -> grow -> rerun)
+    total = 0
+    for j in range(n_slices):
+        r = step(j)
+        eng.device_sync()  # also sizes the engine's chunk pools to this batch's demand
+        total = max(total, _read_u64(r.d_total))
     if total > r.keys_cap:
         eng.reserve_matches(int(total * 1.1) + 1024)
         r = step()
         torch.cuda.synchronize()
-        total = _read_u64(r.d_total)
     assert total <= r.keys_cap
     for _ in range(max(0, args.warmup - 1)):
         step()
     eng.device_sync()
     if not args.sequential:  # size set 1 (its chunk pools, its output) the same way
-        for k in range(max(2, args.warmup)):
+        for k in range(max(2 * n_slices, args.warmup)):
             step2(k)
         eng.device_sync(0)
         eng.device_sync(1)
-        r1 = step2(1)
-        eng.device_sync(1)
-        assert _read_u64(r1.d_total) <= r1.keys_cap
+        for k in range(1, 2 * n_slices, 2):
+            r1 = step2(k)
+            eng.device_sync(1)
+            assert _read_u64(r1.d_total) <= r1.keys_cap
     torch.cuda.synchronize()
 
-    # walk statistics for the algorithmic-byte count (one untimed, counted run)
-    eng.debug_stats(True, read=False)
-    step()
-    torch.cuda.synchronize()
-    by_depth = eng.depth_stats()  # per walk depth: probes, wave cycles, frontier, round trips
-    walk = dict(zip(N.Engine.STAT_NAMES, [int(x) for x in eng.debug_stats(False)]))
-    alg_bytes = algorithmic_bytes(walk, topic_bytes, n)
+    # walk statistics for the algorithmic-byte count: one untimed, counted run per slice (the
+    # per-launch figure is their mean); per-depth counters from this rank's own slice
+    walks, algs = [], []
+    by_depth = None
+    for j in [own] + [x for x in range(n_slices) if x != own]:
+        eng.debug_stats(True, read=False)
+        step(j)
+        torch.cuda.synchronize()
+        if by_depth is None:
+            by_depth = eng.depth_stats()  # per walk depth: probes, wave cycles, frontier, round trips
+        wj = dict(zip(N.Engine.STAT_NAMES, [int(x) for x in eng.debug_stats(False)]))
+        walks.append(wj)
+        algs.append(algorithmic_bytes(wj, slices[j][2], n))
     eng.debug_stats(False, read=False)
+    walk = {k: int(round(np.mean([x[k] for x in walks]))) for k in walks[0]}
+    alg_bytes = float(np.mean(algs))
+    total = walk["keys"]
 
     # ---------------------------------------------------------------- timed region
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -736,6 +757,7 @@ def main():
                 "route_keys": w.n_keys,
                 "publishes_per_step_per_gpu": n,
                 "matches_per_step_per_gpu": int(total),
+                "distinct_batches": n_slices,
                 "parallelism": f"replicated trie, dp{world}"
                                + ("" if args.sequential else ", 2 batches in flight per GPU"),
             },

@@ -1739,11 +1739,23 @@ struct tm_engine {
             ob.swap(stage_bytes);
         }
         const uint64_t t0 = now_us();
+        // EMQX_TM_COMMIT_TRACE=1 (development): each commit's sub-phases on stderr
+        static const bool trace = getenv("EMQX_TM_COMMIT_TRACE") != nullptr;
+        uint64_t tr_last = t0;
+        std::string tr;
+        auto tick = [&](const char *what) {
+            if (!trace) return;
+            const uint64_t t = now_us();
+            tr += std::string(" ") + what + "=" + std::to_string(t - tr_last);
+            tr_last = t;
+        };
         const size_t n = ops.size();
         std::vector<uint32_t> hnode(n, ROOT), hdepth(n, 0), nwalk(n, 0);
         std::vector<uint8_t> pkind(n, PK_NONE);
         resolve_all(ops, ob.data(), hnode, hdepth, nwalk, pkind);
+        tick("resolve");
         int rc = capacity_check(ops, ob.data(), hdepth, nwalk);
+        tick("capacity");
         if (rc) {
             restage(ops, ob);
             n_commits_refused++;
@@ -1757,6 +1769,7 @@ struct tm_engine {
             ~Unblock() { e->leases_unblock(); }
         } unblock{this};
         std::lock_guard<std::mutex> gh(mu_host);
+        tick("leases+host_lock");
         // Ops apply in order (last op per key wins), each a few dependent random reads of host
         // tables far larger than the caches (key set, key records, ids).  Their addresses are
         // known ahead for ops whose path exists: a two-stage prefetch (the key-set slot 16 ops
@@ -1775,6 +1788,7 @@ struct tm_engine {
             if (i + 8 < n) pf_key(i + 8);
             apply_one(ops[i], ob.data(), hnode[i], hdepth[i]);
         }
+        tick("apply_ops");
         if (edge_full) {  // cannot happen after capacity_check; never serve a half-applied trie
             err = "internal: edge table overflow past the capacity check";
             return TM_EDEVICE;
@@ -1789,6 +1803,7 @@ struct tm_engine {
                 ids_stale)
                 rebuild_arena();
         }
+        tick(full ? "rebuild_arena" : "apply_deltas");
         deltas.clear();
         const uint64_t t2 = now_us();
         patch.reset();
@@ -1807,6 +1822,10 @@ struct tm_engine {
                               "uploads the index again): ") + hipGetErrorString(e);
             return e == hipErrorOutOfMemory ? TM_ENOMEM : TM_EDEVICE;
         }
+        tick(was_full ? "publish_full" : "publish_delta");
+        if (trace)
+            fprintf(stderr, "tm commit epoch %llu: %zu ops, %s:%s\n", (unsigned long long)epoch, n,
+                    was_full ? "full" : "delta", tr.c_str());
         commit_us[0] = t1 - t0;
         commit_us[1] = t2 - t1;
         commit_us[2] = now_us() - t2;

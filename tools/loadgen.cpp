@@ -219,9 +219,18 @@ inline uint64_t mix64(uint64_t x) {
 }
 }  // namespace
 
+extern "C" int conc_calls2(tm_engine *eng, int form, const uint8_t *const *bytes, const uint32_t *const *offs,
+                           const uint32_t *ns, uint32_t threads, uint32_t reps, uint32_t rounds, double *wall_s_out,
+                           uint64_t *digest_out, double *call_s_out);
 extern "C" int conc_calls(tm_engine *eng, int form, const uint8_t *const *bytes, const uint32_t *const *offs,
                           const uint32_t *ns, uint32_t threads, uint32_t reps, uint32_t rounds, double *wall_s_out,
                           uint64_t *digest_out) {
+    return conc_calls2(eng, form, bytes, offs, ns, threads, reps, rounds, wall_s_out, digest_out, nullptr);
+}
+// call_s_out (optional): threads x reps, each call's duration in the last round
+extern "C" int conc_calls2(tm_engine *eng, int form, const uint8_t *const *bytes, const uint32_t *const *offs,
+                           const uint32_t *ns, uint32_t threads, uint32_t reps, uint32_t rounds, double *wall_s_out,
+                           uint64_t *digest_out, double *call_s_out) {
     if (!eng || !threads || !reps || !rounds) return TM_EINVAL;
     Gate start(threads + 1), done(threads + 1);
     std::vector<int> rcs(threads, TM_OK);
@@ -234,6 +243,7 @@ extern "C" int conc_calls(tm_engine *eng, int form, const uint8_t *const *bytes,
                 for (uint32_t q = 0; q < reps && rcs[k] == TM_OK; q++) {
                     const bool last = r + 1 == rounds && q + 1 == reps;
                     uint64_t dg = 0;
+                    const auto c0 = std::chrono::steady_clock::now();
                     if (form == 0) {
                         tm_runs_result res;
                         rcs[k] = tm_match_batch_runs(eng, bytes[k], offs[k], ns[k], &res);
@@ -258,6 +268,9 @@ extern "C" int conc_calls(tm_engine *eng, int form, const uint8_t *const *bytes,
                         }
                     }
                     if (last) digest_out[k] = dg;
+                    if (call_s_out && r + 1 == rounds)
+                        call_s_out[(size_t)k * reps + q] =
+                            std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
                 }
                 if (form == 0) tm_runs_release(eng);
                 done.wait();

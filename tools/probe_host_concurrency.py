@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--form", default="runs")
     ap.add_argument("--threads", default="1,2,4")
     ap.add_argument("--pinned", action="store_true", help="topic slices in pinned memory")
+    ap.add_argument("--native", action="store_true", help="also from native threads (conc_calls2), first")
     args = ap.parse_args()
     tmax = max(int(x) for x in args.threads.split(","))
     w = workloads.generate("C", scale=args.scale, n_topics=tmax * args.per)
@@ -68,6 +69,26 @@ def main():
             done.wait()
         eng.result_release()  # this thread's lane
 
+    if args.native:  # the same calls from native threads (tools/loadgen.cpp conc_calls2)
+        import ctypes as C
+        lg = C.CDLL(os.path.join(ROOT, "tools", "libtm_loadgen.so"))
+        P = C.POINTER
+        lg.conc_calls2.argtypes = [C.c_void_p, C.c_int, P(C.c_void_p), P(C.c_void_p), P(C.c_uint32), C.c_uint32,
+                                   C.c_uint32, C.c_uint32, P(C.c_double), P(C.c_uint64), P(C.c_double)]
+        bp = (C.c_void_p * tmax)(*[s[1].ctypes.data for s in slices])
+        op = (C.c_void_p * tmax)(*[s[2].ctypes.data for s in slices])
+        nn = (C.c_uint32 * tmax)(*[args.per] * tmax)
+        for T in [int(x) for x in args.threads.split(",")]:
+            wall = C.c_double()
+            dg = (C.c_uint64 * tmax)()
+            cs = (C.c_double * (T * args.reps))()
+            rc = lg.conc_calls2(eng.h, 0 if args.form == "runs" else 1, bp, op, nn, T, args.reps, 3, C.byref(wall), dg, cs)
+            allt = np.array(list(cs)) * 1e3
+            print(json.dumps({"form": args.form, "native": True, "threads": T, "per": args.per, "reps": args.reps,
+                              "rc": rc, "pinned": args.pinned, "wall_ms": round(wall.value * 1e3, 2),
+                              "calls_per_s": round(T * args.reps / wall.value, 1),
+                              "call_ms": [round(x, 3) for x in allt[:args.reps]],
+                              "call_ms_p50": round(float(np.median(allt)), 3)}), flush=True)
     for T in [int(x) for x in args.threads.split(",")]:
         rounds = 3  # persistent threads (a NIF's dirty schedulers): the first rounds warm their lanes
         start, done = threading.Barrier(T + 1), threading.Barrier(T + 1)
