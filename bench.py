@@ -121,9 +121,10 @@ def batcher_load(eng, tb, to32, seconds):
     from emqx_amd import _native as N
     lg = _loadgen()
     runs = []
-    dt = max(2, min(14, cpu_topology()["usable_cpus"] - 3))  # leave the cutter, completer and caller a CPU
+    # the cutter keeps a CPU; the completion thread and the caller block (driver waits, a sleep)
+    dt = max(2, min(14, cpu_topology()["usable_cpus"] - 2))
     plan = [(4096, N.TM_TRANSPORT_AUTO, 0), (65536, N.TM_TRANSPORT_AUTO, 0), (262144, N.TM_TRANSPORT_AUTO, 0),
-            (65536, N.TM_TRANSPORT_AUTO, 1), (65536, N.TM_TRANSPORT_IDS, 0)]
+            (65536, N.TM_TRANSPORT_AUTO, 1), (65536, N.TM_TRANSPORT_AUTO, 3), (65536, N.TM_TRANSPORT_IDS, 0)]
     warm = 0.5
     for pubs, transport, spans in plan:
         b = N.Batcher(eng, max_batch=65536, max_wait_us=200, delivery_threads=dt, transport=transport)
@@ -140,7 +141,8 @@ def batcher_load(eng, tb, to32, seconds):
         mean_ms = win.lat_mean_us / 1e3
         runs.append({"publishers": pubs,
                      "transport": "runs" if transport != N.TM_TRANSPORT_IDS else "ids (u32 over PCIe)",
-                     "callback": "spans (tm_batcher_submit_spans)" if spans else "id list (tm_batcher_submit)",
+                     "callback": {0: "id list (tm_batcher_submit)", 1: "spans (tm_batcher_submit_spans)",
+                                  3: "u32 spans (tm_batcher_submit_spans32)"}[spans],
                      "publishes_per_s": round(rate, 1),
                      "publishes_per_s_whole_run": round(got.value / el.value, 1),
                      "ids_per_s": round(ids.value / el.value, 1),

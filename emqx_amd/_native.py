@@ -70,7 +70,7 @@ EXPORTS = (
 BATCHER_EXPORTS = (
     "tm_batcher_create", "tm_batcher_create_fn", "tm_batcher_destroy", "tm_batcher_submit", "tm_batcher_match",
     "tm_batcher_apply", "tm_batcher_commit", "tm_batcher_stats_get", "tm_batcher_submit_spans",
-    "tm_batcher_stats_reset",
+    "tm_batcher_stats_reset", "tm_batcher_submit_spans32",
 )
 
 
@@ -159,6 +159,7 @@ class tm_batcher_stats(C.Structure):
 
 tm_match_cb = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.POINTER(C.c_uint64), C.c_uint32)
 tm_spans_cb = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_void_p, C.c_uint32, C.c_uint64)
+tm_spans32_cb = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_void_p, C.c_uint32, C.c_uint64)
 tm_batch_fn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32), C.c_uint32, C.c_uint32,
                           C.POINTER(tm_batch_view))
 
@@ -238,6 +239,7 @@ def load() -> C.CDLL:
     lib.tm_batcher_destroy.restype = None
     lib.tm_batcher_submit.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, tm_match_cb, C.c_void_p]
     lib.tm_batcher_submit_spans.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, tm_spans_cb, C.c_void_p]
+    lib.tm_batcher_submit_spans32.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, tm_spans32_cb, C.c_void_p]
     lib.tm_batcher_match.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, P(C.c_uint32),
                                      P(C.c_int32)]
     lib.tm_batcher_apply.argtypes = [C.c_void_p, P(tm_op), C.c_size_t]

@@ -58,7 +58,7 @@ extern "C" int tmx_batch_match_ids(tm_engine *eng, uint32_t set, const uint8_t *
 extern "C" int tmx_batch_match_runs(tm_engine *eng, uint32_t set, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                                     uint64_t total_bytes, void *stream, void *d_spans, uint64_t spans_cap,
                                     uint32_t *d_soff, uint32_t *d_scnt, uint32_t *d_kcnt, int32_t *d_status,
-                                    unsigned long long *d_cursor, const void **d_ctl_out);
+                                    unsigned long long *d_cursor, const void **d_ctl_out, uint32_t id_w);
 extern "C" void tmx_lease_take(tm_engine *eng);
 extern "C" int tmx_batch_reserve_matches(tm_engine *eng, uint32_t set, uint64_t keys_cap);
 extern "C" void tmx_lease_drop(tm_engine *eng);
@@ -211,11 +211,12 @@ thread_local char bt_err[160];
 
 struct Pending {
     uint32_t len;
-    tm_match_cb cb;    // id-list callback, or
-    tm_spans_cb scb;   // span callback (tm_batcher_submit_spans)
+    uint32_t kind;     // CB_IDS: id list, CB_SPANS: u64 spans, CB_SPANS32: u32 spans
+    void (*fn)();      // the callback, of the type `kind` names
     void *ctx;
     uint64_t t0;  // submit time (ns)
 };
+enum : uint32_t { CB_IDS = 0, CB_SPANS = 1, CB_SPANS32 = 2 };
 
 constexpr size_t QUEUE_BYTES_MAX = 1ull << 31;
 constexpr uint32_t SHARDS = 16;
@@ -276,6 +277,7 @@ struct Slot {
     // runs transport (TM_MATCH_ALL on a master engine): the walk's spans of the engine's host
     // id arena cross PCIe instead of the ids; the window holds a read lease until delivered
     bool runs = false, leased = false;
+    uint32_t runs_w = 8;  // runs: id width of the window's spans (4: the engine's u32 id arena)
     DBuf d_spans, d_soff, d_scnt, d_kcnt, d_st, d_cur;
     HBuf h_spans, h_soff, h_scnt, h_kcnt;
     uint64_t spans_cap = 0;
@@ -311,6 +313,12 @@ struct tm_batcher {
     // first line prefetched, or (pf_lines > 0) up to pf_lines lines of them (development knobs
     // EMQX_TM_PF_PUBS / EMQX_TM_PF_LINES)
     uint32_t pf_pubs = 6, pf_lines = 0;
+    // runs windows: spans of the u64 id arena (zero-copy for id-list and u64-span callbacks), or
+    // (EMQX_TM_RUNS_IDW=4) of the u32 one while every id fits.  Measured on the box at 65,536
+    // closed-loop publishers: u32 windows made the id-list and u64-span callbacks
+    // pay a widening copy per reply (64 -> 42 / 72 -> 37 M/s) and gave the u32-span callback
+    // no gain over u64 spans, so u64 is the default.
+    uint32_t runs_w = 8;
     // two compute streams, each with its own engine buffer set: consecutive windows alternate,
     // so one window's walk starts while the previous one's last waves finish
     hipStream_t s_comps[2] = {}, s_copy = nullptr;
@@ -346,7 +354,7 @@ struct tm_batcher {
     // ------------------------------------------------------------------ submit side
     // No state shared by all submitters on this path: one shard lock (shards by submitting
     // thread) and a read of the cutter's idle flag.
-    int submit(const uint8_t *topic, uint32_t len, tm_match_cb cb, tm_spans_cb scb, void *ctx) {
+    int submit(const uint8_t *topic, uint32_t len, uint32_t kind, void (*fn)(), void *ctx) {
         const uint64_t t0 = now_ns();
         Shard &sh = shards[shard_of_thread()];
         {
@@ -355,7 +363,7 @@ struct tm_batcher {
             // `stopping` is set, so a publish either lands before that pass or is refused here
             if (stopping.load()) return TM_ESTATE;
             if (sh.bytes.size() + len > QUEUE_BYTES_MAX / SHARDS) return TM_ENOMEM;  // back-pressure
-            sh.q.push_back(Pending{len, cb, scb, ctx, t0});
+            sh.q.push_back(Pending{len, kind, fn, ctx, t0});
             sh.bytes.insert(sh.bytes.end(), topic, topic + len);
             sh.n.store((uint32_t)sh.q.size(), std::memory_order_relaxed);
         }
@@ -526,10 +534,17 @@ struct tm_batcher {
         }
         BT_HIP(hipMemcpyAsync(S.d_bytes.p, S.h_bytes.p, S.nbytes + 1, hipMemcpyHostToDevice, s_comp));
         BT_HIP(hipMemcpyAsync(S.d_off.p, S.h_off.p, (size_t)n * 4 + 4, hipMemcpyHostToDevice, s_comp));
-        int rc = tmx_batch_match_runs(eng, S.set, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, s_comp,
-                                      S.d_spans.p, S.spans_cap, (uint32_t *)S.d_soff.p, (uint32_t *)S.d_scnt.p,
+        // spans of the u32 id arena while every id fits (half the lines a reply reads), else u64
+        S.runs_w = runs_w;
+        int rc = TM_ESTATE;
+        for (int k = 0; k < 2 && rc == TM_ESTATE; k++) {
+            rc = tmx_batch_match_runs(eng, S.set, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes,
+                                      s_comp, S.d_spans.p, S.spans_cap, (uint32_t *)S.d_soff.p, (uint32_t *)S.d_scnt.p,
                                       (uint32_t *)S.d_kcnt.p, (int32_t *)S.d_st.p, (unsigned long long *)S.d_cur.p,
-                                      &S.d_ctl);
+                                      &S.d_ctl, S.runs_w);
+            if (rc == TM_ESTATE && S.runs_w == 4) S.runs_w = 8;
+            else break;
+        }
         if (rc) return rc;
         // h_ctl: [0] spans reserved, [1..4] the launch's counter block {-, slow, seg, fr}
         BT_HIP(hipMemcpyAsync(S.h_ctl.p, S.d_cur.p, 8, hipMemcpyDeviceToHost, s_comp));
@@ -696,14 +711,35 @@ struct tm_batcher {
     // ------------------------------------------------------------------ delivery
     // one publish's reply: its own id list (gathered from its spans when it has several), or
     // the spans themselves for a span callback
+    // one publish's reply from spans of u64 ids: its own id list (gathered when it has
+    // several), the spans themselves for a span callback; a u32-span callback gets them only
+    // narrowed from a window whose ids fit (else TM_ESTATE)
     static void reply(const Pending &p, int32_t st, const tm_span *sp, uint32_t ns, uint64_t nids) {
         thread_local std::vector<uint64_t> flat;
-        if (p.scb) {
-            p.scb(p.ctx, st, sp, ns, nids);
+        if (p.kind == CB_SPANS) {
+            reinterpret_cast<tm_spans_cb>(p.fn)(p.ctx, st, sp, ns, nids);
             return;
         }
+        if (p.kind == CB_SPANS32) {  // a window of u64 ids: narrowed into one span while they fit
+            thread_local std::vector<uint32_t> narrow;
+            if (narrow.size() < nids) narrow.resize(nids);
+            uint64_t at = 0, wide = 0;
+            for (uint32_t j = 0; j < ns; j++) {
+                const uint64_t *src = sp[j].ids;
+                for (uint64_t k = 0; k < sp[j].n; k++) {
+                    wide |= src[k];
+                    narrow[at + k] = (uint32_t)src[k];
+                }
+                at += sp[j].n;
+            }
+            const tm_span32 one{narrow.data(), nids};
+            if (wide >> 32) reinterpret_cast<tm_spans32_cb>(p.fn)(p.ctx, TM_ESTATE, nullptr, 0, 0);
+            else reinterpret_cast<tm_spans32_cb>(p.fn)(p.ctx, st, nids ? &one : nullptr, nids ? 1u : 0u, nids);
+            return;
+        }
+        const tm_match_cb cb = reinterpret_cast<tm_match_cb>(p.fn);
         if (ns == 1) {  // zero-copy: one run of the id arena
-            p.cb(p.ctx, st, sp[0].ids, (uint32_t)nids);
+            cb(p.ctx, st, sp[0].ids, (uint32_t)nids);
             return;
         }
         if (flat.size() < nids) flat.resize(nids);
@@ -712,7 +748,37 @@ struct tm_batcher {
             std::memcpy(flat.data() + at, sp[j].ids, sp[j].n * 8);
             at += sp[j].n;
         }
-        p.cb(p.ctx, st, nids ? flat.data() : nullptr, (uint32_t)nids);
+        cb(p.ctx, st, nids ? flat.data() : nullptr, (uint32_t)nids);
+    }
+    // the same from spans of u32 ids (the engine's u32 id arena): a u32-span callback reads
+    // them in place; the others get them widened into one list (one span)
+    static void reply32(const Pending &p, int32_t st, const tm_span32 *sp, uint32_t ns, uint64_t nids) {
+        thread_local std::vector<uint64_t> flat;
+        if (p.kind == CB_SPANS32) {
+            reinterpret_cast<tm_spans32_cb>(p.fn)(p.ctx, st, sp, ns, nids);
+            return;
+        }
+        if (flat.size() < nids) flat.resize(nids);
+        uint64_t at = 0;
+        for (uint32_t j = 0; j < ns; j++) {
+            const uint32_t *src = sp[j].ids;
+            uint64_t *dst = flat.data() + at;
+            for (uint64_t k = 0; k < sp[j].n; k++) dst[k] = src[k];
+            at += sp[j].n;
+        }
+        const uint64_t *ids = nids ? flat.data() : nullptr;
+        if (p.kind == CB_SPANS) {
+            const tm_span one{ids, nids};
+            reinterpret_cast<tm_spans_cb>(p.fn)(p.ctx, st, nids ? &one : nullptr, nids ? 1u : 0u, nids);
+        } else {
+            reinterpret_cast<tm_match_cb>(p.fn)(p.ctx, st, ids, (uint32_t)nids);
+        }
+    }
+    // a failed window, or a publish with no ids
+    static void reply_none(const Pending &p, int32_t st) {
+        if (p.kind == CB_SPANS) reinterpret_cast<tm_spans_cb>(p.fn)(p.ctx, st, nullptr, 0, 0);
+        else if (p.kind == CB_SPANS32) reinterpret_cast<tm_spans32_cb>(p.fn)(p.ctx, st, nullptr, 0, 0);
+        else reinterpret_cast<tm_match_cb>(p.fn)(p.ctx, st, nullptr, 0);
     }
 
     void deliver_range(Slot &S, uint32_t lo, uint32_t hi, int rc, LatHist &H) {
@@ -735,7 +801,7 @@ struct tm_batcher {
                 uint32_t left = pf_lines;
                 for (uint32_t j = b; j < e && left; j++) {
                     const char *p = (const char *)spans[j].ids;
-                    const char *end = p + spans[j].n * 8;
+                    const char *end = p + spans[j].n * S.runs_w;
                     for (p = (const char *)((uintptr_t)p & ~(uintptr_t)63); p < end && left; p += 64, left--)
                         __builtin_prefetch(p);
                 }
@@ -746,8 +812,9 @@ struct tm_batcher {
                 if (i + 8 < hi) __builtin_prefetch(S.pubs[i + 8].ctx);
                 if (i + PF < hi) prefetch(i + PF);
                 const int32_t st = stv[i];
-                if (st == TM_TOPIC_OK) reply(p, st, spans + so[i], sc[i], kc[i]);
-                else reply(p, st, nullptr, 0, 0);
+                if (st != TM_TOPIC_OK) reply_none(p, st);
+                else if (S.runs_w == 4) reply32(p, st, reinterpret_cast<const tm_span32 *>(spans) + so[i], sc[i], kc[i]);
+                else reply(p, st, spans + so[i], sc[i], kc[i]);
                 if (((i - lo) & 15) == 0) now = now_ns();
                 H.add(now > p.t0 ? now - p.t0 : 0);
             }
@@ -760,8 +827,19 @@ struct tm_batcher {
             const Pending &p = S.pubs[i];
             if (i + 8 < hi) __builtin_prefetch(S.pubs[i + 8].ctx);  // the caller's per-publish state
             if (rc < 0) {
-                if (p.scb) p.scb(p.ctx, rc, nullptr, 0, 0);
-                else p.cb(p.ctx, rc, nullptr, 0);
+                reply_none(p, rc);
+            } else if (p.kind == CB_SPANS32) {  // u32 ids: in place when they crossed as u32
+                const int32_t st = S.v.status[i];
+                const uint32_t c = st == TM_TOPIC_OK ? S.v.cnt[i] : 0;
+                const tm_spans32_cb cb = reinterpret_cast<tm_spans32_cb>(p.fn);
+                if (!c) {
+                    cb(p.ctx, st, nullptr, 0, 0);
+                } else if (ids32) {
+                    const tm_span32 one{ids32 + S.v.off[i], c};
+                    cb(p.ctx, st, &one, 1, c);
+                } else {
+                    cb(p.ctx, TM_ESTATE, nullptr, 0, 0);  // u64 ids (some id needs 64 bits)
+                }
             } else {
                 const int32_t st = S.v.status[i];
                 const uint32_t c = st == TM_TOPIC_OK ? S.v.cnt[i] : 0;
@@ -776,11 +854,11 @@ struct tm_batcher {
                         ids = S.v.ids + S.v.off[i];
                     }
                 }
-                if (p.scb) {
+                if (p.kind == CB_SPANS) {
                     const tm_span one{ids, c};
-                    p.scb(p.ctx, st, c ? &one : nullptr, c ? 1u : 0u, c);
+                    reinterpret_cast<tm_spans_cb>(p.fn)(p.ctx, st, c ? &one : nullptr, c ? 1u : 0u, c);
                 } else {
-                    p.cb(p.ctx, st, ids, c);
+                    reinterpret_cast<tm_match_cb>(p.fn)(p.ctx, st, ids, c);
                 }
             }
             if (((i - lo) & 15) == 0) now = now_ns();  // one clock read per 16 callbacks
@@ -1004,6 +1082,7 @@ struct tm_batcher {
         if (const char *e = std::getenv("EMQX_TM_NSLOT")) nslot = std::max(2u, std::min(NSLOT_MAX, (uint32_t)std::atoi(e)));
         if (const char *e = std::getenv("EMQX_TM_PF_PUBS")) pf_pubs = std::max(1u, std::min(64u, (uint32_t)std::atoi(e)));
         if (const char *e = std::getenv("EMQX_TM_PF_LINES")) pf_lines = std::min(256u, (uint32_t)std::atoi(e));
+        if (const char *e = std::getenv("EMQX_TM_RUNS_IDW")) runs_w = std::atoi(e) == 4 ? 4u : 8u;
         if (!eng)
             for (Slot &S : slot)
                 for (HBuf *h : {&S.h_bytes, &S.h_off, &S.h_off_out, &S.h_status, &S.h_cnt, &S.h_ids, &S.h_ctl})
@@ -1109,12 +1188,17 @@ void tm_batcher_destroy(tm_batcher *b) {
 
 int tm_batcher_submit(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_match_cb cb, void *ctx) {
     if (!b || !cb || (len && !topic) || len > 65535) return TM_EINVAL;
-    return b->submit(topic, len, cb, nullptr, ctx);
+    return b->submit(topic, len, CB_IDS, reinterpret_cast<void (*)()>(cb), ctx);
 }
 
 int tm_batcher_submit_spans(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_spans_cb cb, void *ctx) {
     if (!b || !cb || (len && !topic) || len > 65535) return TM_EINVAL;
-    return b->submit(topic, len, nullptr, cb, ctx);
+    return b->submit(topic, len, CB_SPANS, reinterpret_cast<void (*)()>(cb), ctx);
+}
+
+int tm_batcher_submit_spans32(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_spans32_cb cb, void *ctx) {
+    if (!b || !cb || (len && !topic) || len > 65535) return TM_EINVAL;
+    return b->submit(topic, len, CB_SPANS32, reinterpret_cast<void (*)()>(cb), ctx);
 }
 
 namespace {

@@ -59,8 +59,10 @@ struct MatchArgs {
     uint64_t keys_cap;
     // MODE_RUNS
     uint32_t *out_kcnt;
-    uint64_t span_arena;  // host address of the id arena: an arena run at src spans span_arena + 8 * src
-    uint64_t span_keys;   // host address of key handle 0's id: key h's id is at span_keys + 16 * h
+    uint64_t span_arena;  // host address of the id arena: an arena run at src spans span_arena + span_w * src
+    uint64_t span_keys;   // host address of key handle 0's id: key h's id is at span_keys + span_kstride * h
+    uint32_t span_w;       // 8: the u64 id arena; 4: the u32 one
+    uint32_t span_kstride; // bytes between consecutive keys' ids (16: KeyRec.id; 4: key_id32)
     unsigned long long *cursor;  // keys requested so far (may exceed keys_cap)
     // the counters (cursor, slow_count, seg_cursor, fr_cursor) share one CTL_BYTES block;
     // the launch zeroes the block the next launch will use (no memsets before a batch)

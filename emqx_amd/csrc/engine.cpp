@@ -77,6 +77,43 @@ struct StagedOp {
     uint32_t len;
 };
 
+// The host master copy's big tables (edge slots, node arrays, key records, key set, ids,
+// arena) are read at random places by every commit: on 4-KiB pages nearly each such read also
+// misses the TLB.  Allocations of 4 MiB or more are mapped 2-MiB aligned and advised as
+// transparent huge pages (the hosts here run THP in "madvise" mode).
+template <class T>
+struct HugeAlloc {
+    using value_type = T;
+    static constexpr size_t HUGE = 2u << 20, MIN = 4u << 20;
+    HugeAlloc() = default;
+    template <class U>
+    HugeAlloc(const HugeAlloc<U> &) {}
+    static size_t span(size_t bytes) { return (bytes + HUGE - 1) & ~(HUGE - 1); }
+    T *allocate(size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < MIN) return static_cast<T *>(::operator new(bytes));
+        const size_t len = span(bytes);
+        void *p = mmap(nullptr, len + HUGE, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) throw std::bad_alloc();
+        const uintptr_t a = ((uintptr_t)p + HUGE - 1) & ~(uintptr_t)(HUGE - 1);
+        if (a > (uintptr_t)p) munmap(p, a - (uintptr_t)p);                 // unaligned head
+        munmap((void *)(a + len), (uintptr_t)p + len + HUGE - (a + len));  // the rest of the tail
+        (void)madvise((void *)a, len, MADV_HUGEPAGE);
+        return reinterpret_cast<T *>(a);
+    }
+    void deallocate(T *p, size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < MIN) ::operator delete(p);
+        else munmap(p, span(bytes));
+    }
+    template <class U>
+    bool operator==(const HugeAlloc<U> &) const { return true; }
+    template <class U>
+    bool operator!=(const HugeAlloc<U> &) const { return false; }
+};
+template <class T>
+using hvec = std::vector<T, HugeAlloc<T>>;
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
@@ -447,18 +484,18 @@ struct tm_engine {
     size_t warena_dev = 0;                      // bytes of warena already on device
 
     // ---- edges / nodes
-    std::vector<EdgeSlot> etab;
+    hvec<EdgeSlot> etab;
     uint64_t emask = 0;
     uint64_t n_edges = 0;
-    std::vector<uint32_t> node_parent, node_word, node_slot;
-    std::vector<NodeList> node_list;  // terminal list of every node (host numbering)
-    std::vector<uint32_t> node_cap;   // keys the node's arena list has room for (>= its count)
-    std::vector<uint32_t> slot_node;  // slot -> host node (NONE for empty slots)
-    std::vector<uint32_t> slot_list;  // slot -> first key of the node's list (device copy)
+    hvec<uint32_t> node_parent, node_word, node_slot;
+    hvec<NodeList> node_list;  // terminal list of every node (host numbering)
+    hvec<uint32_t> node_cap;   // keys the node's arena list has room for (>= its count)
+    hvec<uint32_t> slot_node;  // slot -> host node (NONE for empty slots)
+    hvec<uint32_t> slot_list;  // slot -> first key of the node's list (device copy)
     RootRec root{0, 0, 0, 0};
 
     // ---- terminal-list arena
-    std::vector<uint32_t> arena;
+    hvec<uint32_t> arena;
     uint64_t arena_garbage = 0;
     size_t arena_dev = 0;  // words already on device
     // Host id arena: arena_id[i] = id of the key handle arena[i] (key positions only), so a run
@@ -466,6 +503,12 @@ struct tm_engine {
     // (MAP_NORESERVE, touched as it fills), so spans stay valid while the arena grows.
     uint64_t *arena_id = nullptr;
     uint64_t arena_id_res = 0;  // entries reserved
+    // The same as u32 (round 4), kept while every id ever added fits 32 bits (max_id < 2^32):
+    // a span of it is half the cache lines for the consumer that reads it (the aggregator's
+    // delivery threads: DESIGN.md §9).  Inline (single-key) spans point into key_id32.
+    uint32_t *arena_id32 = nullptr;
+    hvec<uint32_t> key_id32;  // by key handle
+    bool ids32() const { return arena_id32 && max_id <= 0xFFFFFFFFull; }
     void ids_of(uint64_t lo, uint64_t hi) {  // refresh arena_id over key positions [lo, hi)
         if (!arena_id) return;
         if (hi > arena_id_res) {  // past the reservation: only until the compaction this forces
@@ -473,6 +516,8 @@ struct tm_engine {
             hi = arena_id_res;
         }
         for (uint64_t i = lo; i < hi; i++) arena_id[i] = keys[arena[i]].id;
+        if (arena_id32)
+            for (uint64_t i = lo; i < hi; i++) arena_id32[i] = (uint32_t)arena_id[i];
     }
     bool ids_stale = false;
     bool reserve_ids() {  // a virtual reservation of the budget (halved until the OS grants it)
@@ -480,7 +525,11 @@ struct tm_engine {
         while (want >= (1ull << 12)) {
             void *p = mmap(nullptr, want * 8, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
             if (p != MAP_FAILED) {
+                void *q = mmap(nullptr, want * 4, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+                (void)madvise(p, want * 8, MADV_HUGEPAGE);  // read at random places by every reply
+                if (q != MAP_FAILED) (void)madvise(q, want * 4, MADV_HUGEPAGE);
                 arena_id = (uint64_t *)p;
+                arena_id32 = q != MAP_FAILED ? (uint32_t *)q : nullptr;  // without it: u64 runs only
                 arena_id_res = want;
                 return true;
             }
@@ -490,15 +539,17 @@ struct tm_engine {
     }
     void release_ids() {
         if (arena_id) munmap(arena_id, arena_id_res * 8);
+        if (arena_id32) munmap(arena_id32, arena_id_res * 4);
         arena_id = nullptr;
+        arena_id32 = nullptr;
         arena_id_res = 0;
     }
 
     // ---- keys
-    std::vector<KeyRec> keys;
+    hvec<KeyRec> keys;
     std::vector<uint32_t> free_keys, free_pending;
     uint64_t n_live = 0;
-    std::vector<uint32_t> kset;  // open addressing over key handles
+    hvec<uint32_t> kset;  // open addressing over key handles
     uint64_t kmask = 0, kset_used = 0;
     std::map<std::pair<std::string, uint64_t>, uint32_t> dead_keys;
 
@@ -512,10 +563,10 @@ struct tm_engine {
     };
     static constexpr uint32_t ID_EMPTY = 0xFFFFFFFFu;
     static constexpr uint8_t KR_MULTI = 1;
-    std::vector<IdUse> idtab;
+    hvec<IdUse> idtab;
     uint64_t idtab_used = 0;
     void id_rehash() {  // drops ids with no live key
-        std::vector<IdUse> old;
+        hvec<IdUse> old;
         old.swap(idtab);
         uint64_t live = 0;
         for (const IdUse &e : old) live += e.cnt != ID_EMPTY && e.cnt;
@@ -615,6 +666,7 @@ struct tm_engine {
     hipEvent_t ev_fast0 = nullptr, ev_fast1 = nullptr;  // around k_match_fast (tm_debug_timing)
     bool timing_on = false;
     bool topic_words = false;  // the batch being enqueued holds word-list topics (TM_MATCH_TOPIC_WORDS)
+    uint32_t runs_w = 8;       // the MODE_RUNS batch being enqueued: id width of its spans (4: arena_id32)
 
     uint64_t edge_load_inv() const { return cfg.edge_load_inv ? cfg.edge_load_inv : EDGE_LOAD_INV; }
     uint64_t node_budget() const {  // trie nodes below the root
@@ -806,12 +858,12 @@ struct tm_engine {
     // creation order (parents first).  Node ids on the device change: full upload.
     bool edge_full = false;  // the edge table hit MAX_EDGE_SLOTS at load 1/2: commit fails
     void edge_rehash(uint64_t cap) {
-        std::vector<EdgeSlot> old;
+        hvec<EdgeSlot> old;
         old.swap(etab);
         EdgeSlot empty{NONE, 0, 0, 0};
         etab.assign(cap, empty);
         emask = cap - 1;
-        std::vector<uint32_t> old_list;
+        hvec<uint32_t> old_list;
         old_list.swap(slot_list);
         slot_list.assign(cap, 0);
         slot_node.assign(cap, NONE);
@@ -877,7 +929,7 @@ struct tm_engine {
         return mix64(mix64(((uint64_t)node << 8) | kind) ^ id);
     }
     void kset_rehash(uint64_t cap) {
-        std::vector<uint32_t> old;
+        hvec<uint32_t> old;
         old.swap(kset);
         kset.assign(cap, NONE);
         kmask = cap - 1;
@@ -931,6 +983,7 @@ struct tm_engine {
             return h;
         }
         keys.push_back(KeyRec{NONE, K_FREE, {0, 0, 0}, 0});
+        key_id32.push_back(0);
         dead_filter.emplace_back();
         return (uint32_t)(keys.size() - 1);
     }
@@ -1048,6 +1101,7 @@ struct tm_engine {
             if (kset_find(node, kind, op.id, &slot) != NONE) return;  // set semantics
             uint32_t h = alloc_key();
             keys[h] = KeyRec{node, kind, {0, 0, 0}, op.id};
+            key_id32[h] = (uint32_t)op.id;
             if (deep_shape(kind, depth)) n_deep++;
             id_add(h);
             max_id = std::max(max_id, op.id);
@@ -1115,8 +1169,9 @@ struct tm_engine {
             if (ops[i].op != TM_OP_ADD) return;
             nwalk[i] = dead ? 0 : levels;
         };
+        // memory-latency bound (a few dependent misses per level): 16 threads from 4 K ops on
         const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-        const unsigned nt = n < 4096 ? 1u : (unsigned)std::min<size_t>(hw, n / 2048);
+        const unsigned nt = n < 2048 ? 1u : (unsigned)std::min<size_t>(hw, n / 256);
         if (nt <= 1) {
             std::vector<std::pair<uint32_t, uint32_t>> lv;
             for (size_t i = 0; i < n; i++) one(i, lv);
@@ -1292,6 +1347,8 @@ struct tm_engine {
             n = pos < arena_id_res ? arena_id_res - pos : 0;
         }
         if (n) memcpy(arena_id + pos, L.ids.data(), n * 8);
+        if (arena_id32)
+            for (uint64_t i = 0; i < n; i++) arena_id32[pos + i] = (uint32_t)L.ids[i];
     }
     void apply_deltas() {
         std::stable_sort(deltas.begin(), deltas.end(),
@@ -1354,8 +1411,8 @@ struct tm_engine {
     // fails (out of HBM) leaves the device holding the previous epoch intact.
 
     // Replace array a's device buffer with one holding h (headroom num/den), allocated first.
-    template <class T>
-    hipError_t replace_whole(DevBuf &d, uint32_t a, const std::vector<T> &h, size_t num = 3, size_t den = 2) {
+    template <class V, class T = typename V::value_type>
+    hipError_t replace_whole(DevBuf &d, uint32_t a, const V &h, size_t num = 3, size_t den = 2) {
         const size_t bytes = h.size() * sizeof(T);
         DevBuf nb;
         hipError_t e = nb.ensure(std::max<size_t>(bytes * num / den, 4096));
@@ -1375,8 +1432,8 @@ struct tm_engine {
         patch.add(P_WHOLE, a, bytes / ARR_ELEM[a], d.cap, h.data(), bytes);
         return hipSuccess;
     }
-    template <class T>
-    hipError_t put_tail(DevBuf &d, const std::vector<T> &h, size_t &dev_n) {
+    template <class V, class T = typename V::value_type>
+    hipError_t put_tail(DevBuf &d, const V &h, size_t &dev_n) {
         if (h.size() <= dev_n) return hipSuccess;
         hipError_t e = hipMemcpyAsync(d.as<T>() + dev_n, h.data() + dev_n, (h.size() - dev_n) * sizeof(T),
                                       hipMemcpyHostToDevice, stream);
@@ -1418,8 +1475,8 @@ struct tm_engine {
     // while matches keep running on the current image (mu_dev is not held); then, under
     // mu_dev, the in-flight matches drain and the buffers swap.  At config C that is ~20 GiB
     // uploaded beside the match path; the match path stalls only for the swap.
-    template <class T>
-    static hipError_t stage_to(DevBuf &d, const std::vector<T> &h, hipStream_t s, uint64_t *used, size_t num = 3,
+    template <class V, class T = typename V::value_type>
+    static hipError_t stage_to(DevBuf &d, const V &h, hipStream_t s, uint64_t *used, size_t num = 3,
                                size_t den = 2) {
         const size_t bytes = h.size() * sizeof(T);
         hipError_t e = d.ensure(std::max<size_t>(bytes * num / den, 4096));
@@ -1497,34 +1554,56 @@ struct tm_engine {
         const uint64_t top = idx[n - 1] + 1;
         for (uint32_t a : {A_KEY_REC, A_KEY_BIN, A_KEY_NODE, A_KEY_DD})
             dev_used[a] = std::max<uint64_t>(dev_used[a], top * ARR_ELEM[a]);
-        hipError_t e;
-        if ((e = hipMemcpyAsync(d_scatter_idx.p, idx.data(), n * 8, hipMemcpyHostToDevice, stream))) return e;
-        if ((e = hipMemcpyAsync(d_scatter_src.p, rec.data(), n * 16, hipMemcpyHostToDevice, stream))) return e;
-        if ((e = launch_scatter16(d_key_rec.as<uint4>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint4>(), n,
-                                  stream)))
-            return e;
-        if ((e = hipStreamSynchronize(stream))) return e;  // d_scatter_src is reused below
-        if ((e = hipMemcpyAsync(d_scatter_src.p, bin.data(), n * 4, hipMemcpyHostToDevice, stream))) return e;
-        if ((e = launch_scatter4(d_key_bin.as<uint32_t>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint32_t>(), n,
-                                 stream)))
-            return e;
-        if ((e = hipStreamSynchronize(stream))) return e;
-        if ((e = hipMemcpyAsync(d_scatter_src.p, node.data(), n * 4, hipMemcpyHostToDevice, stream))) return e;
-        if ((e = launch_scatter4(d_key_node.as<uint32_t>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint32_t>(),
-                                 n, stream)))
-            return e;
-        if ((e = hipStreamSynchronize(stream))) return e;
-        if ((e = hipMemcpyAsync(d_scatter_src.p, dd.data(), n, hipMemcpyHostToDevice, stream))) return e;
-        if ((e = launch_scatter1(d_key_dd.as<uint8_t>(), d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint8_t>(), n,
-                                 stream)))
-            return e;
-        return hipStreamSynchronize(stream);
+        const size_t io = stage_bytes_add(idx.data(), n * 8);
+        sjobs.push_back(SJob{16, d_key_rec.p, n, io, stage_bytes_add(rec.data(), n * 16)});
+        sjobs.push_back(SJob{4, d_key_bin.p, n, io, stage_bytes_add(bin.data(), n * 4)});
+        sjobs.push_back(SJob{4, d_key_node.p, n, io, stage_bytes_add(node.data(), n * 4)});
+        sjobs.push_back(SJob{1, d_key_dd.p, n, io, stage_bytes_add(dd.data(), n)});
+        return hipSuccess;
     }
 
-    // dst[idx[i]] = src[i] for 16-byte records (edge slots, word slots, node records)
-    template <class Rec16>
-    hipError_t scatter16(std::vector<uint64_t> &dirty, const std::vector<Rec16> &tab, DevBuf &dbuf) {
-        void *dtab = dbuf.p;
+    // A delta commit's scatters are staged into one blob (indices and values of every array),
+    // which crosses PCIe as ONE pinned copy; then one scatter kernel per array and one sync
+    // (round 3 made two pageable copies, a kernel and a sync per array: ~3.6 ms at config E).
+    struct SJob {
+        uint32_t width;  // bytes per element: 16, 4 or 1
+        void *dst;
+        size_t n, idx_off, src_off;  // offsets into the staged blob
+    };
+    std::vector<SJob> sjobs;
+    std::vector<uint8_t> sblob;
+    PinBuf h_sblob;
+    DevBuf d_sblob;
+    size_t stage_bytes_add(const void *p, size_t bytes) {
+        const size_t at = (sblob.size() + 15) & ~size_t(15);
+        sblob.resize(at + bytes);
+        if (bytes) memcpy(sblob.data() + at, p, bytes);
+        return at;
+    }
+    hipError_t flush_scatters() {
+        if (sjobs.empty()) return hipSuccess;
+        hipError_t e;
+        const size_t bytes = sblob.size();
+        if ((e = h_sblob.ensure(bytes))) return e;
+        if (bytes > d_sblob.cap && (e = d_sblob.ensure(bytes + bytes / 2))) return e;
+        memcpy(h_sblob.p, sblob.data(), bytes);
+        if ((e = hipMemcpyAsync(d_sblob.p, h_sblob.p, bytes, hipMemcpyHostToDevice, stream))) return e;
+        const uint8_t *base = d_sblob.as<uint8_t>();
+        for (const SJob &j : sjobs) {
+            const uint64_t *idx = reinterpret_cast<const uint64_t *>(base + j.idx_off);
+            if (j.width == 16) e = launch_scatter16((uint4 *)j.dst, idx, reinterpret_cast<const uint4 *>(base + j.src_off), j.n, stream);
+            else if (j.width == 4) e = launch_scatter4((uint32_t *)j.dst, idx, reinterpret_cast<const uint32_t *>(base + j.src_off), j.n, stream);
+            else e = launch_scatter1((uint8_t *)j.dst, idx, base + j.src_off, j.n, stream);
+            if (e) return e;
+        }
+        sjobs.clear();
+        sblob.clear();
+        return hipStreamSynchronize(stream);  // the pinned blob is reused by the next commit
+    }
+
+    // dst[idx[i]] = src[i] for 16-byte records (edge slots, word slots, node records): staged
+    template <class V, class Rec16 = typename V::value_type>
+    hipError_t scatter16(std::vector<uint64_t> &dirty, const V &tab, DevBuf &dbuf) {
         static_assert(sizeof(Rec16) == 16, "16-byte records");
         if (dirty.empty()) return hipSuccess;
         std::sort(dirty.begin(), dirty.end());
@@ -1533,19 +1612,14 @@ struct tm_engine {
         std::vector<Rec16> src(n);
         for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
         patch.add(P_SCATTER, arr_of(&dbuf), n, 0, dirty.data(), n * 8, src.data(), n * 16);
-        hipError_t e;
-        if ((e = hipMemcpyAsync(d_scatter_idx.p, dirty.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, stream)))
-            return e;
-        if ((e = hipMemcpyAsync(d_scatter_src.p, src.data(), n * 16, hipMemcpyHostToDevice, stream))) return e;
-        if ((e = launch_scatter16((uint4 *)dtab, d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint4>(), n,
-                                  stream)))
-            return e;
-        return hipStreamSynchronize(stream);  // src dies at scope exit
+        const size_t io = stage_bytes_add(dirty.data(), n * 8);
+        sjobs.push_back(SJob{16, dbuf.p, n, io, stage_bytes_add(src.data(), n * 16)});
+        return hipSuccess;
     }
 
-    // dst[idx[i]] = src[i] for u32 entries (slot_list)
-    hipError_t scatter4(std::vector<uint64_t> &dirty, const std::vector<uint32_t> &tab, DevBuf &dbuf) {
-        void *dtab = dbuf.p;
+    // dst[idx[i]] = src[i] for u32 entries (slot_list, arena words): staged
+    template <class V>
+    hipError_t scatter4(std::vector<uint64_t> &dirty, const V &tab, DevBuf &dbuf) {
         if (dirty.empty()) return hipSuccess;
         std::sort(dirty.begin(), dirty.end());
         dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
@@ -1553,22 +1627,17 @@ struct tm_engine {
         std::vector<uint32_t> src(n);
         for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
         patch.add(P_SCATTER, arr_of(&dbuf), n, 0, dirty.data(), n * 8, src.data(), n * 4);
-        hipError_t e;
-        if ((e = hipMemcpyAsync(d_scatter_idx.p, dirty.data(), n * sizeof(uint64_t), hipMemcpyHostToDevice, stream)))
-            return e;
-        if ((e = hipMemcpyAsync(d_scatter_src.p, src.data(), n * 4, hipMemcpyHostToDevice, stream))) return e;
-        if ((e = launch_scatter4((uint32_t *)dtab, d_scatter_idx.as<uint64_t>(), d_scatter_src.as<uint32_t>(), n,
-                                 stream)))
-            return e;
-        return hipStreamSynchronize(stream);
+        const size_t io = stage_bytes_add(dirty.data(), n * 8);
+        sjobs.push_back(SJob{4, dbuf.p, n, io, stage_bytes_add(src.data(), n * 4)});
+        return hipSuccess;
     }
 
     // A grow-only array that outgrew its device buffer moves to one 1.5x its size: its device
     // contents are copied on the device and only the tail then crosses PCIe (round 1
     // re-uploaded the whole index, edge table included: a 70 ms commit at config E).  Replicas
     // get the array whole (P_WHOLE with the new capacity) ahead of the tail.
-    template <class T>
-    hipError_t grow(DevBuf &d, const std::vector<T> &h, size_t dev_n) {
+    template <class V, class T = typename V::value_type>
+    hipError_t grow(DevBuf &d, const V &h, size_t dev_n) {
         if (h.size() * sizeof(T) <= d.cap) return hipSuccess;
         DevBuf nb;
         hipError_t e = nb.ensure(std::max<size_t>(h.size() * sizeof(T) * 3 / 2, 4096));
@@ -1627,6 +1696,7 @@ struct tm_engine {
         if ((e = scatter16(dirty_eslots, etab, d_etab))) return e;
         if ((e = scatter4(dirty_lists, slot_list, d_slot_list))) return e;
         if ((e = upload_key_ids_delta())) return e;
+        if ((e = flush_scatters())) return e;
         if (root_dirty) {
             if ((e = hipMemcpyAsync(d_root.p, &root, sizeof(RootRec), hipMemcpyHostToDevice, stream))) return e;
             patch.add(P_WHOLE, A_ROOT, 1, d_root.cap, &root, sizeof(RootRec));
@@ -2210,9 +2280,10 @@ void tm_destroy(tm_engine *eng) {
                       &eng->d_ib, &eng->d_iboff, &eng->d_iout, &eng->d_ilen})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
-                      &eng->d_arena, &eng->d_scatter_idx, &eng->d_scatter_src, &eng->d_stats})
+                      &eng->d_arena, &eng->d_scatter_idx, &eng->d_scatter_src, &eng->d_stats, &eng->d_sblob})
         b->release();
     eng->h_cursor.release();
+    eng->h_sblob.release();
     if (eng->ev_fast0) (void)hipEventDestroy(eng->ev_fast0);
     if (eng->ev_fast1) (void)hipEventDestroy(eng->ev_fast1);
     if (eng->s_build) (void)hipStreamDestroy(eng->s_build);
@@ -2452,8 +2523,17 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.cursor = cursor ? cursor : (unsigned long long *)(eng->bb->p_ctl + CTL_CURSOR);
     if (mode == MODE_RUNS) {
         a.out_kcnt = eng->bb->d_kcnt.as<uint32_t>() + obase;
-        a.span_arena = (uint64_t)(uintptr_t)eng->arena_id;
-        a.span_keys = eng->keys.empty() ? 0 : (uint64_t)(uintptr_t)&eng->keys[0].id;
+        if (eng->runs_w == 4) {  // spans of the u32 id arena (the caller checked ids32())
+            a.span_arena = (uint64_t)(uintptr_t)eng->arena_id32;
+            a.span_keys = eng->key_id32.empty() ? 0 : (uint64_t)(uintptr_t)&eng->key_id32[0];
+            a.span_w = 4;
+            a.span_kstride = 4;
+        } else {
+            a.span_arena = (uint64_t)(uintptr_t)eng->arena_id;
+            a.span_keys = eng->keys.empty() ? 0 : (uint64_t)(uintptr_t)&eng->keys[0].id;
+            a.span_w = 8;
+            a.span_kstride = sizeof(KeyRec);
+        }
     }
     if (to) {
         a.out_off = to->off;
@@ -3654,10 +3734,10 @@ int tm_replica_create(const tm_config *cfg, const void *d_image, uint64_t bytes,
     eng->replica = true;
     // the replica keeps no host master copy
     std::vector<WordSlot>().swap(eng->wtab);
-    std::vector<EdgeSlot>().swap(eng->etab);
-    std::vector<uint32_t>().swap(eng->slot_list);
-    std::vector<uint32_t>().swap(eng->slot_node);
-    std::vector<uint32_t>().swap(eng->kset);
+    hvec<EdgeSlot>().swap(eng->etab);
+    hvec<uint32_t>().swap(eng->slot_list);
+    hvec<uint32_t>().swap(eng->slot_node);
+    hvec<uint32_t>().swap(eng->kset);
     eng->release_ids();
     if ((rc = tm_replica_load(eng, d_image, bytes, stream)) != TM_OK) {
         tm_destroy(eng);
@@ -4050,9 +4130,18 @@ __attribute__((visibility("hidden"))) int tmx_batch_match_runs(tm_engine *eng, u
                                                                void *stream, void *d_spans, uint64_t spans_cap,
                                                                uint32_t *d_soff, uint32_t *d_scnt, uint32_t *d_kcnt,
                                                                int32_t *d_status, unsigned long long *d_cursor,
-                                                               const void **d_ctl_out) {
+                                                               const void **d_ctl_out, uint32_t id_w) {
     if (eng->replica) return TM_ESTATE;
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    // id_w 4: spans of the u32 id arena, while every id fits (the caller holds a lease: no
+    // commit can add a wider id before the spans are used)
+    if (id_w != 4 && id_w != 8) return TM_EINVAL;
+    if (id_w == 4 && !eng->ids32()) return TM_ESTATE;
+    struct W {
+        tm_engine *e;
+        ~W() { e->runs_w = 8; }
+    } reset_w{eng};
+    eng->runs_w = id_w;
     eng->bb = eng->batch_set(set);
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;

@@ -471,10 +471,10 @@ __device__ __forceinline__ void emit_spans(const MatchArgs &a, const WaveLds &L,
         if (!g.y || ((L.spill >> (g.w & 0x3Fu)) & 1ull)) continue;  // spilled: the slow kernel owns it
         uint64_t p;
         if (g.w & SEG_INLINE) {
-            p = a.span_keys + 16ull * g.x;
+            p = a.span_keys + (uint64_t)a.span_kstride * g.x;
         } else {
             const uint32_t src = (g.w & SEG_NODE) ? a.slot_list[g.x] + (g.w >> SEG_SKIP_SHIFT) : g.x;
-            p = a.span_arena + 8ull * src;
+            p = a.span_arena + (uint64_t)a.span_w * src;
         }
         spans[L.tbase[g.w & 0x3Fu] + g.z] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), g.y, 0u);
     }
@@ -1018,7 +1018,7 @@ constexpr uint64_t ROOT_MARK = (1ull << 40) - 1;
 // one-key span, or (MODE_IDS*) its route id
 __device__ __forceinline__ void out_key(const MatchArgs &a, uint64_t i, uint32_t key) {
     if (a.mode == MODE_RUNS) {
-        const uint64_t p = a.span_keys + 16ull * key;
+        const uint64_t p = a.span_keys + (uint64_t)a.span_kstride * key;
         reinterpret_cast<uint4 *>(a.keys)[i] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), 1u, 0u);
     } else if (a.mode == MODE_IDS32) {
         a.keys[i] = (uint32_t)a.key_rec[2ull * key];

@@ -24,8 +24,10 @@
  *            publish's reply is read straight from the arena (one span: zero-copy; several:
  *            gathered by the delivery thread).  A window holds a read lease on the arena from
  *            its enqueue until its last callback returns; a commit waits for those leases, so
- *            every window sees exactly one committed epoch.  Other modes, and replicas, ship
- *            the ids (u32 while every id fits).
+ *            every window sees exactly one committed epoch.  With EMQX_TM_RUNS_IDW=4 the spans
+ *            are of the engine's u32 id arena while every id fits (a u32-span callback reads
+ *            them in place, the others get them widened).  Other modes, and replicas, ship the
+ *            ids (u32 while every id fits).
  *   writes   any thread may write the engine directly (tm_apply / tm_commit_epoch are safe
  *            beside the aggregator); tm_batcher_apply / tm_batcher_commit are the same calls.
  *            A delivery callback may stage (tm_apply) but not commit: tm_commit_epoch and
@@ -72,6 +74,15 @@ typedef void (*tm_match_cb)(void *ctx, int32_t status, const uint64_t *ids, uint
 /* The same as spans (ids = the concatenation of spans[0 .. nspans), nids in all), valid only
  * during the call: a NIF builds its reply list straight from the engine's id arena. */
 typedef void (*tm_spans_cb)(void *ctx, int32_t status, const tm_span *spans, uint32_t nspans, uint64_t nids);
+/* (ABI 9) The same with u32 ids, for a consumer that builds small integers: spans of the
+ * engine's u32 id arena when the aggregator runs its windows on it (EMQX_TM_RUNS_IDW=4), else
+ * the reply narrowed into one span.  A reply with an id past 32 bits gets status TM_ESTATE
+ * and no spans. */
+typedef struct tm_span32 {
+    const uint32_t *ids;
+    uint64_t        n;
+} tm_span32;
+typedef void (*tm_spans32_cb)(void *ctx, int32_t status, const tm_span32 *spans, uint32_t nspans, uint64_t nids);
 
 /* A batch matcher other than an engine (e.g. a filter-sharded index): match topics
  * bytes[off[i] .. off[i+1]) for i < n and fill `out` with memory the backend owns until
@@ -119,6 +130,8 @@ void tm_batcher_destroy(tm_batcher *b);
 int tm_batcher_submit(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_match_cb cb, void *ctx);
 /* tm_batcher_submit with a span callback (no copy of the ids on the host at all). */
 int tm_batcher_submit_spans(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_spans_cb cb, void *ctx);
+/* tm_batcher_submit with a u32-span callback (ABI 9; see tm_spans32_cb). */
+int tm_batcher_submit_spans32(tm_batcher *b, const uint8_t *topic, uint32_t len, tm_spans32_cb cb, void *ctx);
 /* Blocking form: waits for the publish's batch.  Copies up to `cap` ids, *n_out = the
  * full count (> cap means truncated), *status = the publish's status. */
 int tm_batcher_match(tm_batcher *b, const uint8_t *topic, uint32_t len, uint64_t *ids, uint32_t cap,

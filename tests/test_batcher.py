@@ -413,3 +413,81 @@ def test_gpu_batcher_beside_direct_writers_and_device_callers():
     b.close()
     eng.close()
     assert not bad, bad[:5]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("idw", [8, 4], ids=["u64-arena", "u32-arena"])
+@pytest.mark.parametrize("wide_ids", [False, True], ids=["u32-ids", "ids-past-32-bits"])
+def test_gpu_batcher_span_kinds_vs_oracle(wide_ids, idw, monkeypatch):
+    """Every reply kind vs the oracle: on windows of the engine's u32 id arena the u32-span
+    callback (tm_batcher_submit_spans32) reads in place and the id-list and u64-span callbacks
+    get the ids widened; on u64 windows the reverse.  Once an id needs 64 bits the windows fall
+    back to the u64 arena: id lists and u64 spans stay exact, u32 spans get TM_ESTATE.  The
+    default windows read the u64 arena (u32-span replies are narrowed); EMQX_TM_RUNS_IDW=4
+    runs them on the u32 one."""
+    import oracle
+    from emqx_amd import workloads
+    monkeypatch.setenv("EMQX_TM_RUNS_IDW", str(idw))
+    w = workloads.generate("A", scale=0.3, n_topics=3000)
+    ids = w.f_id.astype(np.uint64) + (np.uint64(1 << 40) if wide_ids else np.uint64(0))
+    eng = N.Engine(0)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, ids)
+    eng.commit()
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, ids)
+    eoff, eids, est = ix.match(w.t_bytes, w.t_off)
+    topics = w.topics()
+    got = {}
+    lock = threading.Lock()
+    done = threading.Event()
+    want = 3 * len(topics)
+
+    def put(key, st, vals):
+        with lock:
+            got[key] = (st, sorted(vals))
+            if len(got) == want:
+                done.set()
+
+    @N.tm_match_cb
+    def cb_ids(ctx, st, p, n):
+        put(("ids", ctx), st, [p[i] for i in range(n)])
+
+    def span_vals(sp, ns, width):
+        out = []
+        T = N.C.c_uint32 if width == 4 else N.C.c_uint64
+        for j in range(ns):
+            base = sp + 16 * j
+            ptr = N.C.c_void_p.from_address(base).value
+            n = N.C.c_uint64.from_address(base + 8).value
+            arr = (T * n).from_address(ptr) if n else []
+            out.extend(int(x) for x in arr)
+        return out
+
+    @N.tm_spans_cb
+    def cb_spans(ctx, st, sp, ns, nids):
+        put(("spans", ctx), st, span_vals(sp, ns, 8) if sp else [])
+
+    @N.tm_spans32_cb
+    def cb_spans32(ctx, st, sp, ns, nids):
+        put(("spans32", ctx), st, span_vals(sp, ns, 4) if sp else [])
+
+    b = N.Batcher(eng, max_batch=512, max_wait_us=300)
+    for i, t in enumerate(topics):
+        ctx = N.C.c_void_p(i + 1)
+        assert b.lib.tm_batcher_submit(b.h, t, len(t), cb_ids, ctx) == N.TM_OK
+        assert b.lib.tm_batcher_submit_spans(b.h, t, len(t), cb_spans, ctx) == N.TM_OK
+        assert b.lib.tm_batcher_submit_spans32(b.h, t, len(t), cb_spans32, ctx) == N.TM_OK
+    assert done.wait(120)
+    b.close()
+    for i in range(len(topics)):
+        exp = [int(x) for x in eids[eoff[i]:eoff[i + 1]]]
+        for kind in ("ids", "spans"):
+            st, vals = got[(kind, i + 1)]
+            assert st == est[i] and vals == (exp if st == N.TM_TOPIC_OK else []), (kind, i)
+        st, vals = got[("spans32", i + 1)]
+        if wide_ids and est[i] == N.TM_TOPIC_OK and exp:
+            assert st == N.TM_ESTATE and vals == [], i
+        elif st == N.TM_TOPIC_OK:
+            assert vals == exp, i
+        else:
+            assert st == est[i] or (wide_ids and st == N.TM_ESTATE), i
+    eng.close()

@@ -1,9 +1,10 @@
 """Batcher sweep on one GPU (bench tooling): config C engine, closed-loop publishers through
 tm_batcher_submit for each (publishers, delivery threads, max_wait_us[, transport, spans callback,
 slots, max_batch, compute streams]) given, one JSON line each.
-Usage: python tools/batcher_gpu.py P:T:W[:TR:SP:NSLOT:MB:ST:PFP:PFL] ...   (TR 0 auto/runs, 1 ids; SP 1 = span
-callback, 2 = span callback reading no id; ST 1 or 2 compute streams, EMQX_TM_STREAMS; PFP/PFL delivery prefetch:
-publishes ahead / lines per reply, 0 lines = first line of each span).  PIN=1 pins the process to the GPU's socket first."""
+Usage: python tools/batcher_gpu.py P:T:W[:TR:SP:NSLOT:MB:ST:PFP:PFL:IDW] ...   (TR 0 auto/runs, 1 ids; SP 1 = span
+callback, 2 = span callback reading no id, 3 = u32-span callback, 4 = u32-span callback reading no id; ST 1 or 2 compute streams, EMQX_TM_STREAMS; PFP/PFL delivery prefetch:
+publishes ahead / lines per reply, 0 lines = first line of each span; IDW 4 / 8: runs windows read
+the engine's u32 / u64 id arena).  PIN=1 pins the process to the GPU's socket first."""
 import ctypes as C
 import json
 import os
@@ -51,8 +52,10 @@ def main():
         os.environ["EMQX_TM_NSLOT"] = str(nslot)
         os.environ["EMQX_TM_STREAMS"] = str(nst)
         pfp, pfl = (v[8], v[9]) if len(v) > 9 else (6, 0)  # delivery prefetch knobs
+        idw = v[10] if len(v) > 10 else 4  # runs windows: u32 (4) or u64 (8) id arena
         os.environ["EMQX_TM_PF_PUBS"] = str(pfp)
         os.environ["EMQX_TM_PF_LINES"] = str(pfl)
+        os.environ["EMQX_TM_RUNS_IDW"] = str(idw)
         b = N.Batcher(eng, max_batch=mb, max_wait_us=wait, delivery_threads=th, transport=tr)
         got, ids, errs, cs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
         win = N.tm_batcher_stats()
@@ -62,7 +65,7 @@ def main():
         b.close()
         print(json.dumps({"publishers": pubs, "threads": th, "max_wait_us": wait, "transport": tr, "spans": sp,
                           "nslot": nslot, "max_batch": mb, "streams": nst, "rc": rc, "errors": errs.value,
-                          "pf_pubs": pfp, "pf_lines": pfl,
+                          "pf_pubs": pfp, "pf_lines": pfl, "runs_idw": idw,
                           "publishes_per_s": round(win.lat_count / win.window_s),
                           "publishes_per_s_whole_run": round(got.value / el.value),
                           "ids_per_publish": round(ids.value / max(got.value, 1), 1),

@@ -3,6 +3,12 @@
 set -o pipefail
 T=${1:-f}
 mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -v --timeout 240 --timeout-method thread tests/test_batcher.py -m gpu > gpurun_out/pytest_batcher_$T.log 2>&1
+rc=$?; tail -n 2 gpurun_out/pytest_batcher_$T.log; grep -E "FAILED" gpurun_out/pytest_batcher_$T.log | head -5; [ $rc -eq 0 ] || exit $rc
+PIN=1 timeout -k 10 300 python -u tools/batcher_gpu.py 65536:14:200:0:0:6:65536:2:6:0:8 65536:14:200:0:0:6:65536:2:6:0:4 \
+    65536:14:200:0:1:6:65536:2:6:0:8 65536:14:200:0:1:6:65536:2:6:0:4 65536:14:200:0:3:6:65536:2:6:0:4 \
+    65536:14:200:0:4:6:65536:2:6:0:4 > gpurun_out/batcher_idw_$T.jsonl 2> gpurun_out/batcher_idw_$T.err
+rc=$?; cat gpurun_out/batcher_idw_$T.jsonl; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python -u tools/probe_host_concurrency.py --form runs --threads 1,4 --native > gpurun_out/probe_conc_$T.jsonl 2> gpurun_out/probe_conc_$T.err
 rc=$?; cat gpurun_out/probe_conc_$T.jsonl; [ $rc -eq 0 ] || { tail -5 gpurun_out/probe_conc_$T.err; exit $rc; }
 timeout -k 10 200 python -u tools/probe_host_concurrency.py --form keys --threads 1,4 --native >> gpurun_out/probe_conc_$T.jsonl 2>> gpurun_out/probe_conc_$T.err

@@ -4,8 +4,9 @@
 // (apps/emqx/src/emqx_broker.erl:285-290): a publisher's next topic is submitted from the
 // callback that delivers its previous result.  Runs until `seconds` have passed, then waits
 // for the publishes in flight.  Every callback reads each id it is given once (a checksum),
-// as a NIF building its reply list would; with `spans` it takes the span callback
-// (tm_batcher_submit_spans) and reads the ids straight from the engine's id arena.
+// as a NIF building its reply list would; with `spans` 1 it takes the span callback
+// (tm_batcher_submit_spans), 3 the u32-span one (tm_batcher_submit_spans32), and reads the ids
+// straight from the engine's id arena.
 #include <atomic>
 #include <chrono>
 #include <climits>
@@ -37,15 +38,19 @@ struct Load {
     std::mutex m;
     std::condition_variable cv;
     bool spans = false;
-    bool no_read = false;  // spans == 2 (development): the callback reads no id (the pipeline's floor)
+    bool spans32 = false;  // spans == 3 (u32-span callback, tm_batcher_submit_spans32)
+    bool no_read = false;  // spans == 2 / 4 (development): span / u32-span callbacks reading no id
 };
 
 void on_result(void *ctx, int32_t status, const uint64_t *ids, uint32_t n);
 void on_spans(void *ctx, int32_t status, const tm_span *sp, uint32_t ns, uint64_t nids);
+void on_spans32(void *ctx, int32_t status, const tm_span32 *sp, uint32_t ns, uint64_t nids);
 
 bool submit_next(Pub *p) {
     Load *L = p->L;
     const uint64_t k = p->k++ % L->n_topics;
+    if (L->spans32)
+        return tm_batcher_submit_spans32(L->b, L->bytes + L->off[k], L->off[k + 1] - L->off[k], on_spans32, p) == TM_OK;
     if (L->spans)
         return tm_batcher_submit_spans(L->b, L->bytes + L->off[k], L->off[k + 1] - L->off[k], on_spans, p) == TM_OK;
     return tm_batcher_submit(L->b, L->bytes + L->off[k], L->off[k + 1] - L->off[k], on_result, p) == TM_OK;
@@ -82,6 +87,19 @@ void on_spans(void *ctx, int32_t status, const tm_span *sp, uint32_t ns, uint64_
     next_or_retire(p);
 }
 
+void on_spans32(void *ctx, int32_t status, const tm_span32 *sp, uint32_t ns, uint64_t nids) {
+    Pub *p = static_cast<Pub *>(ctx);
+    p->done++;
+    p->ids += nids;
+    uint64_t s = 0;
+    if (!p->L->no_read)
+        for (uint32_t j = 0; j < ns; j++)
+            for (uint64_t i = 0; i < sp[j].n; i++) s += sp[j].ids[i];
+    p->sum += s;
+    if (status < 0) p->errors++;
+    next_or_retire(p);
+}
+
 void next_or_retire(Pub *p) {
     // the deadline is looked at every 8th publish of a publisher (a clock read is not free)
     if (((p->done & 7) == 0 &&
@@ -103,7 +121,8 @@ extern "C" int loadgen_run3(tm_batcher *b, const uint8_t *bytes, const uint32_t 
     if (!b || !bytes || !off || !n_topics || !publishers) return TM_EINVAL;
     Load L;
     L.spans = spans != 0;
-    L.no_read = spans == 2;
+    L.spans32 = spans == 3 || spans == 4;
+    L.no_read = spans == 2 || spans == 4;
     L.b = b;
     L.bytes = bytes;
     L.off = off;
@@ -186,7 +205,8 @@ extern "C" uint64_t spans_checksum(const tm_runs_result *r, uint32_t threads) {
 // Host-form callers on `threads` native threads at once (tests/test_gpu_concurrency.py): thread k
 // makes `reps` calls on its own batch (bytes[k], offs[k], ns[k] topics) per round, `rounds`
 // rounds between barriers (the first ones warm each thread's engine lane, as a NIF's dirty
-// schedulers keep theirs); *wall_s_out = the LAST round's wall time.  form 0: tm_match_batch_runs,
+// schedulers keep theirs); *wall_s_out = the LAST round's wall time; then one untimed call per
+// thread whose result is digested.  form 0: tm_match_batch_runs,
 // 1: tm_match_batch (keys) + tm_key_ids.  digest_out[k]: over thread k's last result,
 // sum over topics t of sum over its ids of mix(id + t * golden), and every status folded in:
 // order-independent within a topic, tied to the topic.
@@ -238,10 +258,12 @@ extern "C" int conc_calls2(tm_engine *eng, int form, const uint8_t *const *bytes
     for (uint32_t k = 0; k < threads; k++)
         th.emplace_back([&, k] {
             std::vector<uint64_t> ids;
-            for (uint32_t r = 0; r < rounds; r++) {
+            // the timed rounds make plain calls; one more, untimed, computes the digests
+            for (uint32_t r = 0; r <= rounds; r++) {
                 start.wait();
-                for (uint32_t q = 0; q < reps && rcs[k] == TM_OK; q++) {
-                    const bool last = r + 1 == rounds && q + 1 == reps;
+                const uint32_t nrep = r == rounds ? 1 : reps;
+                for (uint32_t q = 0; q < nrep && rcs[k] == TM_OK; q++) {
+                    const bool last = r == rounds;
                     uint64_t dg = 0;
                     const auto c0 = std::chrono::steady_clock::now();
                     if (form == 0) {
@@ -268,7 +290,7 @@ extern "C" int conc_calls2(tm_engine *eng, int form, const uint8_t *const *bytes
                         }
                     }
                     if (last) digest_out[k] = dg;
-                    if (call_s_out && r + 1 == rounds)
+                    if (call_s_out && r + 1 == rounds)  // the last timed round
                         call_s_out[(size_t)k * reps + q] =
                             std::chrono::duration<double>(std::chrono::steady_clock::now() - c0).count();
                 }
@@ -278,11 +300,11 @@ extern "C" int conc_calls2(tm_engine *eng, int form, const uint8_t *const *bytes
             tm_result_release(eng);  // this thread's lane
         });
     double wall = 0;
-    for (uint32_t r = 0; r < rounds; r++) {
+    for (uint32_t r = 0; r <= rounds; r++) {
         start.wait();
         const auto t0 = std::chrono::steady_clock::now();
         done.wait();
-        wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (r < rounds) wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
     for (auto &t : th) t.join();
     *wall_s_out = wall;
