@@ -1190,7 +1190,10 @@ struct tm_engine {
     // a single key goes inline into the slot; otherwise the counts go inline and the
     // list offset stays in slot_list (M_CNT), or, for huge lists, the walk reads the
     // counts from the list header (M_REC).
-    void refresh_info(uint32_t node) {
+    void refresh_info(uint32_t node) { refresh_info_to(node, dirty_eslots, dirty_lists); }
+    // the same, recording the slots it changes in the given vectors (several threads at once
+    // on different nodes below the root: apply_deltas)
+    void refresh_info_to(uint32_t node, std::vector<uint64_t> &d_eslots, std::vector<uint64_t> &d_lists) {
         const NodeList &r = node_list[node];
         if (node == ROOT) {
             root.list_off = r.list_off;
@@ -1210,11 +1213,11 @@ struct tm_engine {
             info |= M_REC << I_MODE_SHIFT;
         if (info != e.info) {
             e.info = info;
-            if (!need_full) dirty_eslots.push_back(sl);
+            if (!need_full) d_eslots.push_back(sl);
         }
         if (slot_list[sl] != r.list_off) {
             slot_list[sl] = r.list_off;
-            if (!need_full) dirty_lists.push_back(sl);
+            if (!need_full) d_lists.push_back(sl);
         }
     }
 
@@ -1339,16 +1342,20 @@ struct tm_engine {
         arena[pos - 2] = L.tc;
         arena[pos - 1] = L.hc;
     }
-    void place_ids(uint64_t pos, const NewList &L) {
-        if (!arena_id) return;
+    // returns false when the list ran past the id arena's reservation (ids_stale: the commit
+    // compacts); several threads may place different lists at once
+    bool place_ids(uint64_t pos, const NewList &L) {
+        if (!arena_id) return true;
         uint64_t n = L.ids.size();
+        bool ok = true;
         if (pos + n > arena_id_res) {  // past the reservation: only until the compaction this forces
-            ids_stale = true;
+            ok = false;
             n = pos < arena_id_res ? arena_id_res - pos : 0;
         }
         if (n) memcpy(arena_id + pos, L.ids.data(), n * 8);
         if (arena_id32)
             for (uint64_t i = 0; i < n; i++) arena_id32[pos + i] = (uint32_t)L.ids[i];
+        return ok;
     }
     void apply_deltas() {
         std::stable_sort(deltas.begin(), deltas.end(),
@@ -1371,17 +1378,66 @@ struct tm_engine {
                 });
             for (auto &t : th) t.join();
         }
+        // Lists that fit their room are rewritten in place: disjoint arena ranges, nodes and
+        // slots, so in parallel (the dirty records per thread, merged after); the rest move to
+        // the arena's tail in node order on this thread.
+        std::vector<uint8_t> inplace(G, 0);
+        size_t n_in = 0;
         for (size_t g = 0; g < G; g++) {
+            const uint32_t node = deltas[gs[g]].node;
+            const NodeList &r = node_list[node];
+            const uint32_t k = nl[g].tc + nl[g].hc;
+            inplace[g] = node != ROOT && r.list_off && k && k <= node_cap[node];
+            n_in += inplace[g];
+        }
+        auto place_inplace = [&](size_t g, std::vector<uint64_t> &da, std::vector<uint64_t> &de,
+                                 std::vector<uint64_t> &dl) -> bool {
+            const uint32_t node = deltas[gs[g]].node;
+            const uint32_t off = node_list[node].list_off;
+            NewList &L = nl[g];
+            const uint32_t tc = L.tc, hc = L.hc;
+            // fits the list's room: rewrite it in place (header + keys), so the churn of a long
+            // list (a hot '#' prefix's subscribers) leaves no garbage behind
+            std::copy(L.keys.begin(), L.keys.end(), arena.begin() + off);
+            place_header(off, L);
+            const bool ok = place_ids(off, L);
+            for (uint64_t w = off - LIST_HDR; w < (uint64_t)off + tc + hc; w++)
+                if (w < arena_dev) da.push_back(w);
+            node_list[node] = NodeList{off, tc, hc};
+            refresh_info_to(node, de, dl);
+            return ok;
+        };
+        const unsigned nt2 = n_in < 1024 ? 1u : (unsigned)std::min<size_t>(hw, n_in / 512);
+        if (nt2 <= 1) {
+            for (size_t g = 0; g < G; g++)
+                if (inplace[g] && !place_inplace(g, dirty_arena, dirty_eslots, dirty_lists)) ids_stale = true;
+        } else {
+            std::vector<std::vector<uint64_t>> da(nt2), de(nt2), dl(nt2);
+            std::vector<uint8_t> stale(nt2, 0);
+            std::vector<std::thread> th;
+            for (unsigned k = 0; k < nt2; k++)
+                th.emplace_back([&, k] {
+                    for (size_t g = k; g < G; g += nt2)
+                        if (inplace[g] && !place_inplace(g, da[k], de[k], dl[k])) stale[k] = 1;
+                });
+            for (auto &t : th) t.join();
+            for (unsigned k = 0; k < nt2; k++) {
+                dirty_arena.insert(dirty_arena.end(), da[k].begin(), da[k].end());
+                dirty_eslots.insert(dirty_eslots.end(), de[k].begin(), de[k].end());
+                dirty_lists.insert(dirty_lists.end(), dl[k].begin(), dl[k].end());
+                if (stale[k]) ids_stale = true;
+            }
+        }
+        for (size_t g = 0; g < G; g++) {
+            if (inplace[g]) continue;
             const uint32_t node = deltas[gs[g]].node;
             const NodeList r = node_list[node];
             NewList &L = nl[g];
             const uint32_t tc = L.tc, hc = L.hc, cap = node_cap[node];
-            if (r.list_off && tc + hc && tc + hc <= cap) {
-                // fits the list's room: rewrite it in place (header + keys), so the churn of a
-                // long list (a hot '#' prefix's subscribers) leaves no garbage behind
+            if (r.list_off && tc + hc && tc + hc <= cap) {  // the root's list (never in parallel)
                 std::copy(L.keys.begin(), L.keys.end(), arena.begin() + r.list_off);
                 place_header(r.list_off, L);
-                place_ids(r.list_off, L);
+                if (!place_ids(r.list_off, L)) ids_stale = true;
                 for (uint64_t w = r.list_off - LIST_HDR; w < (uint64_t)r.list_off + tc + hc; w++)
                     if (w < arena_dev) dirty_arena.push_back(w);
                 node_list[node] = NodeList{r.list_off, tc, hc};
@@ -1397,7 +1453,7 @@ struct tm_engine {
                     arena.insert(arena.end(), L.keys.begin(), L.keys.end());
                     if (room > tc + hc) arena.resize(arena.size() + (room - tc - hc), 0u);
                     place_header(off, L);
-                    place_ids(off, L);
+                    if (!place_ids(off, L)) ids_stale = true;
                     node_list[node] = NodeList{off, tc, hc};
                 }
                 node_cap[node] = tc + hc ? room : 0;
