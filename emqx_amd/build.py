@@ -21,7 +21,7 @@ def _newer(out, srcs):
 
 TM_SRCS = ("emqx_amd/csrc/engine.cpp", "emqx_amd/csrc/batcher.cpp", "emqx_amd/csrc/match_kernels.hip",
            "emqx_amd/csrc/result_kernels.hip", "emqx_amd/csrc/filter_kernels.hip", "emqx_amd/csrc/layout.h",
-           "emqx_amd/csrc/device_api.h", "emqx_amd/csrc/copy_api.h", "emqx_amd/csrc/filter_api.h", "emqx_amd/csrc/wave.h", "include/emqx_tm.h",
+           "emqx_amd/csrc/device_api.h", "emqx_amd/csrc/copy_api.h", "emqx_amd/csrc/image_api.h", "emqx_amd/csrc/filter_api.h", "emqx_amd/csrc/wave.h", "include/emqx_tm.h",
            "include/emqx_tm_batcher.h")
 
 

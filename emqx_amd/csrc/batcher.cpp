@@ -69,6 +69,11 @@ namespace {
 // the read lease of the very window being delivered) and lets a callback's own runs call take
 // a lease past a waiting commit
 thread_local int tl_delivering = 0;
+// On a delivery thread: the clock as deliver_range last read it (it reads it once per 16
+// callbacks), the submit time of a publish re-submitted from a callback.  A clock read costs
+// about as much as the rest of a submit; this stamp is at most 16 callbacks (a few
+// microseconds) early, so such a publish's latency is overstated by that much, never hidden.
+thread_local uint64_t tl_clock_ns = 0;
 }  // namespace
 extern "C" __attribute__((visibility("hidden"))) int tmx_in_delivery(void) { return tl_delivering; }
 
@@ -355,7 +360,7 @@ struct tm_batcher {
     // No state shared by all submitters on this path: one shard lock (shards by submitting
     // thread) and a read of the cutter's idle flag.
     int submit(const uint8_t *topic, uint32_t len, uint32_t kind, void (*fn)(), void *ctx) {
-        const uint64_t t0 = now_ns();
+        const uint64_t t0 = tl_clock_ns ? tl_clock_ns : now_ns();
         Shard &sh = shards[shard_of_thread()];
         {
             std::lock_guard<std::mutex> g(sh.m);
@@ -811,13 +816,14 @@ struct tm_batcher {
                 const Pending &p = S.pubs[i];
                 if (i + 8 < hi) __builtin_prefetch(S.pubs[i + 8].ctx);
                 if (i + PF < hi) prefetch(i + PF);
+                if (((i - lo) & 15) == 0) tl_clock_ns = now = now_ns();
+                H.add(now > p.t0 ? now - p.t0 : 0);
                 const int32_t st = stv[i];
                 if (st != TM_TOPIC_OK) reply_none(p, st);
                 else if (S.runs_w == 4) reply32(p, st, reinterpret_cast<const tm_span32 *>(spans) + so[i], sc[i], kc[i]);
                 else reply(p, st, spans + so[i], sc[i], kc[i]);
-                if (((i - lo) & 15) == 0) now = now_ns();
-                H.add(now > p.t0 ? now - p.t0 : 0);
             }
+            tl_clock_ns = 0;
             return;
         }
         thread_local std::vector<uint64_t> wide;  // a narrowed window's ids, one publish at a time
@@ -826,6 +832,8 @@ struct tm_batcher {
         for (uint32_t i = lo; i < hi; i++) {
             const Pending &p = S.pubs[i];
             if (i + 8 < hi) __builtin_prefetch(S.pubs[i + 8].ctx);  // the caller's per-publish state
+            if (((i - lo) & 15) == 0) tl_clock_ns = now = now_ns();  // one clock read per 16 callbacks
+            H.add(now > p.t0 ? now - p.t0 : 0);
             if (rc < 0) {
                 reply_none(p, rc);
             } else if (p.kind == CB_SPANS32) {  // u32 ids: in place when they crossed as u32
@@ -861,9 +869,8 @@ struct tm_batcher {
                     reinterpret_cast<tm_match_cb>(p.fn)(p.ctx, st, ids, c);
                 }
             }
-            if (((i - lo) & 15) == 0) now = now_ns();  // one clock read per 16 callbacks
-            H.add(now > p.t0 ? now - p.t0 : 0);
         }
+        tl_clock_ns = 0;
     }
 
     static constexpr int SPIN = 256;  // polls (a few microseconds) before sleeping: the CPUs are a quota

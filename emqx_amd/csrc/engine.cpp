@@ -36,6 +36,7 @@
 #include "copy_api.h"
 #include "device_api.h"
 #include "filter_api.h"
+#include "image_api.h"
 #include "layout.h"
 
 using namespace tmx;
@@ -484,14 +485,23 @@ struct tm_engine {
     size_t warena_dev = 0;                      // bytes of warena already on device
 
     // ---- edges / nodes
-    hvec<EdgeSlot> etab;
-    uint64_t emask = 0;
+    // The device edge table is slot-indexed (a node is its slot, at load <= 1/16: 16 GiB at
+    // config C).  The host keeps no copy of it: per node its slot, bloom, info and device
+    // list entry, a bitmap of the taken slots (where a new edge goes: the same linear probe
+    // the device runs), and a node-sized map (parent node, word) -> child for its own walks.
+    uint64_t emask = 0;  // device slots - 1
     uint64_t n_edges = 0;
     hvec<uint32_t> node_parent, node_word, node_slot;
     hvec<NodeList> node_list;  // terminal list of every node (host numbering)
     hvec<uint32_t> node_cap;   // keys the node's arena list has room for (>= its count)
-    hvec<uint32_t> slot_node;  // slot -> host node (NONE for empty slots)
-    hvec<uint32_t> slot_list;  // slot -> first key of the node's list (device copy)
+    hvec<uint32_t> node_bloom, node_info;  // the node's EdgeSlot.bloom / .info on the device
+    hvec<uint32_t> node_slist;             // the node's slot_list entry on the device
+    hvec<uint64_t> eocc;                   // taken device slots, one bit each
+    struct EMapEnt {
+        uint32_t parent, word, child, pad;  // parent == NONE: empty
+    };
+    hvec<EMapEnt> emap;
+    uint64_t emap_mask = 0;
     RootRec root{0, 0, 0, 0};
 
     // ---- terminal-list arena
@@ -614,7 +624,8 @@ struct tm_engine {
     std::vector<uint8_t> stage_bytes;
     std::vector<std::pair<uint32_t, uint32_t>> lv_scratch;  // classify(): (start, len) per level
     std::vector<Delta> deltas;
-    std::vector<uint64_t> dirty_eslots, dirty_wslots, dirty_lists;
+    std::vector<uint64_t> dirty_wslots;
+    std::vector<uint64_t> dirty_enodes, dirty_lnodes;  // nodes whose edge slot / slot_list entry changed
     std::vector<uint64_t> dirty_arena;  // arena words already on the device, rewritten in place
     uint64_t n_grows = 0;               // device arrays moved to a larger buffer by a delta commit
     bool root_dirty = true;
@@ -840,44 +851,48 @@ struct tm_engine {
     // edges.  Host nodes are numbered in creation order (a parent before its
     // children); on the device a node is the index of its edge slot.
     uint32_t dev_id(uint32_t node) const { return node == ROOT ? ROOT_ID : node_slot[node]; }
-    uint64_t edge_find(uint32_t parent_dev, uint32_t word) const {
-        uint64_t s = edge_hash(parent_dev, word) & emask;
-        for (;;) {
-            const EdgeSlot &e = etab[s];
-            if (e.parent == NONE) return ~0ull;
-            if (e.parent == parent_dev && e.word == word) return s;
-            s = (s + 1) & emask;
+    uint64_t edge_slots() const { return emask + 1; }
+    static uint64_t emap_hash(uint32_t parent, uint32_t word) { return mix64(((uint64_t)parent << 32) | word); }
+    // the child of host node `parent` by `word`, or NONE
+    uint32_t child_of(uint32_t parent, uint32_t word) const {
+        for (uint64_t i = emap_hash(parent, word) & emap_mask;; i = (i + 1) & emap_mask) {
+            const EMapEnt &e = emap[i];
+            if (e.parent == NONE) return NONE;
+            if (e.parent == parent && e.word == word) return e.child;
         }
     }
+    void emap_put(uint32_t parent, uint32_t word, uint32_t child) {
+        uint64_t i = emap_hash(parent, word) & emap_mask;
+        while (emap[i].parent != NONE) i = (i + 1) & emap_mask;
+        emap[i] = EMapEnt{parent, word, child, 0};
+    }
+    void emap_rehash(uint64_t cap) {  // load <= 1/2
+        emap.assign(cap, EMapEnt{NONE, 0, 0, 0});
+        emap_mask = cap - 1;
+        for (size_t v = 1; v < node_parent.size(); v++) emap_put(node_parent[v], node_word[v], (uint32_t)v);
+    }
+    bool slot_taken(uint64_t s) const { return (eocc[s >> 6] >> (s & 63)) & 1u; }
+    // where the device's linear probe for (parent slot, word) ends: the first free slot
     uint64_t edge_place(uint32_t parent_dev, uint32_t word) const {
         uint64_t s = edge_hash(parent_dev, word) & emask;
-        while (etab[s].parent != NONE) s = (s + 1) & emask;
+        while (slot_taken(s)) s = (s + 1) & emask;
         return s;
     }
     // Re-place every node: slot positions hash the parent's slot, so nodes go in in
     // creation order (parents first).  Node ids on the device change: full upload.
     bool edge_full = false;  // the edge table hit MAX_EDGE_SLOTS at load 1/2: commit fails
     void edge_rehash(uint64_t cap) {
-        hvec<EdgeSlot> old;
-        old.swap(etab);
-        EdgeSlot empty{NONE, 0, 0, 0};
-        etab.assign(cap, empty);
+        eocc.assign(std::max<uint64_t>(cap / 64, 1), 0);
         emask = cap - 1;
-        hvec<uint32_t> old_list;
-        old_list.swap(slot_list);
-        slot_list.assign(cap, 0);
-        slot_node.assign(cap, NONE);
         for (size_t v = 1; v < node_parent.size(); v++) {
-            const uint32_t os = node_slot[v];
-            const uint32_t pd = dev_id(node_parent[v]);
-            const uint64_t ns = edge_place(pd, node_word[v]);
-            etab[ns] = EdgeSlot{pd, node_word[v], old[os].bloom, old[os].info};
-            slot_list[ns] = old_list[os];
-            slot_node[ns] = (uint32_t)v;
+            const uint64_t ns = edge_place(dev_id(node_parent[v]), node_word[v]);
+            eocc[ns >> 6] |= 1ull << (ns & 63);
             node_slot[v] = (uint32_t)ns;
         }
         need_full = true;
     }
+    // the device EdgeSlot of node v
+    EdgeSlot edge_rec(uint32_t v) const { return EdgeSlot{dev_id(node_parent[v]), node_word[v], node_bloom[v], node_info[v]}; }
     void node_set_flag(uint32_t node, uint32_t f, uint32_t bloom) {
         if (node == ROOT) {
             if ((root.info & f) != f || (root.bloom & bloom) != bloom) {
@@ -887,21 +902,20 @@ struct tm_engine {
             }
             return;
         }
-        EdgeSlot &e = etab[node_slot[node]];
-        if ((e.info & f) != f || (e.bloom & bloom) != bloom) {
-            e.info |= f;
-            e.bloom |= bloom;
-            dirty_eslots.push_back(node_slot[node]);
+        if ((node_info[node] & f) != f || (node_bloom[node] & bloom) != bloom) {
+            node_info[node] |= f;
+            node_bloom[node] |= bloom;
+            dirty_enodes.push_back(node);
         }
     }
     uint32_t edge_child(uint32_t parent, uint32_t word) {
-        uint64_t s = edge_find(dev_id(parent), word);
-        if (s != ~0ull) return slot_node[s];
-        if ((n_edges + 1) * edge_load_inv() > etab.size()) {
+        const uint32_t c = child_of(parent, word);
+        if (c != NONE) return c;
+        if ((n_edges + 1) * edge_load_inv() > edge_slots()) {
             // a node is its slot index (u32, below the NONE/ROOT_ID sentinels): at the
             // size cap the table fills up to half instead of growing
-            if (etab.size() < MAX_EDGE_SLOTS) edge_rehash(etab.size() * 2);
-            else if ((n_edges + 1) * 2 > etab.size()) {
+            if (edge_slots() < MAX_EDGE_SLOTS) edge_rehash(edge_slots() * 2);
+            else if ((n_edges + 1) * 2 > edge_slots()) {
                 edge_full = true;
                 return ROOT;  // dropped; commit() reports TM_ENOMEM
             }
@@ -912,13 +926,16 @@ struct tm_engine {
         node_slot.push_back(NONE);
         node_list.push_back(NodeList{0, 0, 0});
         node_cap.push_back(0);
-        const uint32_t pd = dev_id(parent);
-        s = edge_place(pd, word);
-        etab[s] = EdgeSlot{pd, word, 0, 0};
-        slot_node[s] = child;
+        node_bloom.push_back(0);
+        node_info.push_back(0);
+        node_slist.push_back(0);
+        const uint64_t s = edge_place(dev_id(parent), word);
+        eocc[s >> 6] |= 1ull << (s & 63);
         node_slot[child] = (uint32_t)s;
+        if ((n_edges + 2) * 2 > emap.size()) emap_rehash(std::max<uint64_t>(emap.size() * 2, 1024));
+        else emap_put(parent, word, child);
         n_edges++;
-        dirty_eslots.push_back(s);
+        dirty_enodes.push_back(child);
         node_set_flag(parent, word == W_PLUS ? I_PLUS : I_LIT, word == W_PLUS ? 0u : bloom_bit(word));
         return child;
     }
@@ -993,7 +1010,7 @@ struct tm_engine {
     // Returns kind and the terminal node (creating the path when `create`).
     // Returns kind and the terminal node (creating the path when `create`); *depth_out =
     // the node's level count.  The walk may start below the root at a node known to lie
-    // on the filter's path (hint_node at level hint_depth: resolve_prefix()).
+    // on the filter's path (hint_node at level hint_depth: resolve_all()).
     bool classify(const uint8_t *f, uint32_t flen, uint32_t flags, bool create, uint8_t *kind_out,
                   uint32_t *node_out, uint32_t *depth_out = nullptr, uint32_t hint_node = ROOT,
                   uint32_t hint_depth = 0) {
@@ -1039,9 +1056,8 @@ struct tm_engine {
             if (create) {
                 node = edge_child(node, w);
             } else {
-                uint64_t s = edge_find(dev_id(node), w);
-                if (s == ~0ull) return false;
-                node = slot_node[s];
+                node = child_of(node, w);
+                if (node == NONE) return false;
             }
         }
         *kind_out = kind;
@@ -1049,10 +1065,12 @@ struct tm_engine {
         return true;
     }
 
-    // Deepest existing node on a filter's path, read-only (safe to run in parallel
-    // before an epoch's ops are applied: nodes are never removed while ops apply).
-    void resolve_prefix(const uint8_t *f, uint32_t flen, std::vector<std::pair<uint32_t, uint32_t>> &lv,
-                        uint32_t *node_out, uint32_t *depth_out) const {
+    // Deepest existing node on a filter's path (resolve_all), read-only (safe to run in
+    // parallel before an epoch's ops are applied: nodes are never removed while ops apply).
+    // The walk runs in slot space: a node's device id IS its edge slot (node_slot[v] == the
+    // slot edge_find returns for v), so each level costs one edge-table probe, and the host
+    // node id is looked up once, at the end.
+    static void split_levels(const uint8_t *f, uint32_t flen, std::vector<std::pair<uint32_t, uint32_t>> &lv) {
         lv.clear();
         uint32_t st = 0;
         for (uint32_t i = 0; i <= flen; i++)
@@ -1060,19 +1078,12 @@ struct tm_engine {
                 lv.push_back({st, i - st});
                 st = i + 1;
             }
-        uint32_t node = ROOT, d = 0;
-        for (; d < lv.size(); d++) {
-            const uint8_t *p = f + lv[d].first;
-            const uint32_t len = lv[d].second;
-            if (len == 1 && *p == '#') break;
-            const uint32_t w = (len == 1 && *p == '+') ? W_PLUS : word_lookup(p, len);
-            if (w == NONE) break;
-            const uint64_t s = edge_find(dev_id(node), w);
-            if (s == ~0ull) break;
-            node = slot_node[s];
-        }
-        *node_out = node;
-        *depth_out = d;
+    }
+    // level d's word id for the prefix walk, or NONE to stop there ('#', unknown word)
+    uint32_t prefix_word(const uint8_t *f, const std::pair<uint32_t, uint32_t> &l) const {
+        const uint8_t *p = f + l.first;
+        if (l.second == 1 && *p == '#') return NONE;
+        return (l.second == 1 && *p == '+') ? W_PLUS : word_lookup(p, l.second);
     }
     // the shape test of key_ord() from the level count alone (no parent-chain walk)
     static bool deep_shape(uint8_t kind, uint32_t depth) {
@@ -1100,6 +1111,11 @@ struct tm_engine {
             uint64_t slot;
             if (kset_find(node, kind, op.id, &slot) != NONE) return;  // set semantics
             uint32_t h = alloc_key();
+            if (free_keys.size() > 8) {  // the handle the 8th ADD from now reuses (random, cold)
+                const uint32_t nx = free_keys[free_keys.size() - 8];
+                __builtin_prefetch(&keys[nx]);
+                __builtin_prefetch(&key_id32[nx]);
+            }
             keys[h] = KeyRec{node, kind, {0, 0, 0}, op.id};
             key_id32[h] = (uint32_t)op.id;
             if (deep_shape(kind, depth)) n_deep++;
@@ -1146,12 +1162,68 @@ struct tm_engine {
     // pkind[i]: the key kind when the op's whole path already exists (its key would hang at
     // hnode[i]), else PK_NONE: the apply loop prefetches the key-set slot of such ops ahead.
     static constexpr uint8_t PK_NONE = 0xFF;
+    // mslot[i]: for an op whose walk stopped at a missing edge, the emap slot the walk probed
+    // first (where an ADD's new edge is entered), else ~0.
     void resolve_all(const std::vector<StagedOp> &ops, const uint8_t *ob, std::vector<uint32_t> &hnode,
-                     std::vector<uint32_t> &hdepth, std::vector<uint32_t> &nwalk, std::vector<uint8_t> &pkind) const {
+                     std::vector<uint32_t> &hdepth, std::vector<uint32_t> &nwalk, std::vector<uint8_t> &pkind,
+                     std::vector<uint64_t> &mslot) const {
         const size_t n = ops.size();
+        // ops in groups of GRP, their walks advanced one level at a time, so the map probes of
+        // the group are in flight together (one dependent miss per level each)
+        constexpr size_t GRP = 8;
+        auto walk_group = [&](size_t i0, size_t i1, std::vector<std::pair<uint32_t, uint32_t>> (&lvs)[GRP]) {
+            uint32_t cur[GRP], d[GRP], wnext[GRP];
+            uint64_t nxt[GRP];
+            bool live[GRP];
+            const size_t m = i1 - i0;
+            for (size_t k = 0; k < m; k++) {
+                split_levels(ob + ops[i0 + k].off, ops[i0 + k].len, lvs[k]);
+                cur[k] = ROOT;
+                d[k] = 0;
+                live[k] = true;
+            }
+            for (;;) {
+                bool any = false;
+                for (size_t k = 0; k < m; k++) {  // this level's word and first probe slot
+                    if (!live[k]) continue;
+                    const uint8_t *f = ob + ops[i0 + k].off;
+                    if (d[k] >= lvs[k].size() || (wnext[k] = prefix_word(f, lvs[k][d[k]])) == NONE) {
+                        live[k] = false;
+                        continue;
+                    }
+                    nxt[k] = emap_hash(cur[k], wnext[k]) & emap_mask;
+                    __builtin_prefetch(&emap[nxt[k]]);
+                    any = true;
+                }
+                if (!any) break;
+                for (size_t k = 0; k < m; k++) {  // the probes (their lines requested above)
+                    if (!live[k]) continue;
+                    uint32_t c = NONE;
+                    for (uint64_t i = nxt[k];; i = (i + 1) & emap_mask) {
+                        const EMapEnt &e = emap[i];
+                        if (e.parent == NONE) break;
+                        if (e.parent == cur[k] && e.word == wnext[k]) {
+                            c = e.child;
+                            break;
+                        }
+                    }
+                    if (c == NONE) {
+                        live[k] = false;
+                        mslot[i0 + k] = nxt[k];
+                        continue;
+                    }
+                    cur[k] = c;
+                    d[k]++;
+                }
+            }
+            for (size_t k = 0; k < m; k++) {
+                hnode[i0 + k] = cur[k];
+                hdepth[i0 + k] = d[k];
+            }
+        };
         auto one = [&](size_t i, std::vector<std::pair<uint32_t, uint32_t>> &lv) {
             const uint8_t *f = ob + ops[i].off;
-            resolve_prefix(f, ops[i].len, lv, &hnode[i], &hdepth[i]);
+            split_levels(f, ops[i].len, lv);  // (hnode / hdepth come from walk_group)
             // a '#' before the last level: a dead key, no path; a final '#': the path stops above it
             int hash_pos = -1;
             bool wild = false;
@@ -1172,17 +1244,21 @@ struct tm_engine {
         // memory-latency bound (a few dependent misses per level): 16 threads from 4 K ops on
         const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         const unsigned nt = n < 2048 ? 1u : (unsigned)std::min<size_t>(hw, n / 256);
+        // thread k takes groups k, k + nt, ... of GRP consecutive ops
+        auto range = [&](unsigned k, unsigned nthreads) {
+            std::vector<std::pair<uint32_t, uint32_t>> lvs[GRP];
+            for (size_t g = (size_t)k * GRP; g < n; g += (size_t)nthreads * GRP) {
+                const size_t e = std::min(n, g + GRP);
+                walk_group(g, e, lvs);
+                for (size_t i = g; i < e; i++) one(i, lvs[0]);
+            }
+        };
         if (nt <= 1) {
-            std::vector<std::pair<uint32_t, uint32_t>> lv;
-            for (size_t i = 0; i < n; i++) one(i, lv);
+            range(0, 1);
             return;
         }
         std::vector<std::thread> th;
-        for (unsigned k = 0; k < nt; k++)
-            th.emplace_back([&, k] {
-                std::vector<std::pair<uint32_t, uint32_t>> lv;
-                for (size_t i = k; i < n; i += nt) one(i, lv);
-            });
+        for (unsigned k = 0; k < nt; k++) th.emplace_back([&, k] { range(k, nt); });
         for (auto &t : th) t.join();
     }
 
@@ -1190,10 +1266,10 @@ struct tm_engine {
     // a single key goes inline into the slot; otherwise the counts go inline and the
     // list offset stays in slot_list (M_CNT), or, for huge lists, the walk reads the
     // counts from the list header (M_REC).
-    void refresh_info(uint32_t node) { refresh_info_to(node, dirty_eslots, dirty_lists); }
-    // the same, recording the slots it changes in the given vectors (several threads at once
-    // on different nodes below the root: apply_deltas)
-    void refresh_info_to(uint32_t node, std::vector<uint64_t> &d_eslots, std::vector<uint64_t> &d_lists) {
+    void refresh_info(uint32_t node) { refresh_info_to(node, dirty_enodes, dirty_lnodes); }
+    // the same, recording the nodes whose device records change in the given vectors (several
+    // threads at once on different nodes below the root: apply_deltas)
+    void refresh_info_to(uint32_t node, std::vector<uint64_t> &d_enodes, std::vector<uint64_t> &d_lnodes) {
         const NodeList &r = node_list[node];
         if (node == ROOT) {
             root.list_off = r.list_off;
@@ -1201,9 +1277,7 @@ struct tm_engine {
             root_dirty = true;
             return;
         }
-        const uint32_t sl = node_slot[node];
-        EdgeSlot &e = etab[sl];
-        uint32_t info = e.info & I_KIDS;
+        uint32_t info = node_info[node] & I_KIDS;
         const uint32_t n = r.term_cnt + r.hash_cnt;
         if (n == 1 && arena[r.list_off] < INLINE_KEY_LIMIT)
             info |= (M_INLINE << I_MODE_SHIFT) | (r.hash_cnt ? I_INL_HASH : 0u) | arena[r.list_off];
@@ -1211,13 +1285,13 @@ struct tm_engine {
             info |= (M_CNT << I_MODE_SHIFT) | (r.term_cnt << CNT_BITS) | r.hash_cnt;
         else if (n)
             info |= M_REC << I_MODE_SHIFT;
-        if (info != e.info) {
-            e.info = info;
-            if (!need_full) d_eslots.push_back(sl);
+        if (info != node_info[node]) {
+            node_info[node] = info;
+            if (!need_full) d_enodes.push_back(node);
         }
-        if (slot_list[sl] != r.list_off) {
-            slot_list[sl] = r.list_off;
-            if (!need_full) d_lists.push_back(sl);
+        if (node_slist[node] != r.list_off) {
+            node_slist[node] = r.list_off;
+            if (!need_full) d_lnodes.push_back(node);
         }
     }
 
@@ -1410,7 +1484,7 @@ struct tm_engine {
         const unsigned nt2 = n_in < 1024 ? 1u : (unsigned)std::min<size_t>(hw, n_in / 512);
         if (nt2 <= 1) {
             for (size_t g = 0; g < G; g++)
-                if (inplace[g] && !place_inplace(g, dirty_arena, dirty_eslots, dirty_lists)) ids_stale = true;
+                if (inplace[g] && !place_inplace(g, dirty_arena, dirty_enodes, dirty_lnodes)) ids_stale = true;
         } else {
             std::vector<std::vector<uint64_t>> da(nt2), de(nt2), dl(nt2);
             std::vector<uint8_t> stale(nt2, 0);
@@ -1423,8 +1497,8 @@ struct tm_engine {
             for (auto &t : th) t.join();
             for (unsigned k = 0; k < nt2; k++) {
                 dirty_arena.insert(dirty_arena.end(), da[k].begin(), da[k].end());
-                dirty_eslots.insert(dirty_eslots.end(), de[k].begin(), de[k].end());
-                dirty_lists.insert(dirty_lists.end(), dl[k].begin(), dl[k].end());
+                dirty_enodes.insert(dirty_enodes.end(), de[k].begin(), de[k].end());
+                dirty_lnodes.insert(dirty_lnodes.end(), dl[k].begin(), dl[k].end());
                 if (stale[k]) ids_stale = true;
             }
         }
@@ -1556,10 +1630,28 @@ struct tm_engine {
             for (DevBuf &b : sb) b.release();
             return err;
         };
+        // the edge table: built on the device from one record per node
+        hvec<NodeImage> nim(node_parent.size() - 1);
+        for (size_t v = 1; v < node_parent.size(); v++) {
+            const EdgeSlot r = edge_rec((uint32_t)v);
+            nim[v - 1] = NodeImage{node_slot[v], r.parent, r.word, r.bloom, r.info, node_slist[v]};
+        }
+        DevBuf d_nim;
+        const uint64_t slots = edge_slots();
+        if ((e = sb[A_ETAB].ensure(slots * sizeof(EdgeSlot))) || (e = sb[A_SLOT_LIST].ensure(slots * 4)) ||
+            (e = d_nim.ensure(std::max<size_t>(nim.size() * sizeof(NodeImage), 4096))) ||
+            (nim.size() && (e = hipMemcpyAsync(d_nim.p, nim.data(), nim.size() * sizeof(NodeImage), hipMemcpyHostToDevice, s))) ||
+            (e = launch_edge_image(sb[A_ETAB].as<uint4>(), sb[A_SLOT_LIST].as<uint32_t>(), slots, d_nim.as<NodeImage>(), nim.size(), s)) ||
+            (e = hipStreamSynchronize(s))) {
+            d_nim.release();
+            return fail(e);
+        }
+        d_nim.release();
+        hvec<NodeImage>().swap(nim);
+        used[A_ETAB] = slots * sizeof(EdgeSlot);
+        used[A_SLOT_LIST] = slots * 4;
         if ((e = stage_to(sb[A_WTAB], wtab, s, &used[A_WTAB], 1, 1)) || (e = stage_to(sb[A_WARENA], warena, s, &used[A_WARENA])) ||
             (e = stage_to(sb[A_WORD_OFF], word_off, s, &used[A_WORD_OFF])) ||
-            (e = stage_to(sb[A_ETAB], etab, s, &used[A_ETAB], 1, 1)) ||
-            (e = stage_to(sb[A_SLOT_LIST], slot_list, s, &used[A_SLOT_LIST], 1, 1)) ||
             (e = stage_to(sb[A_ARENA], arena, s, &used[A_ARENA])) || (e = stage_to(sb[A_KEY_REC], ka.rec, s, &used[A_KEY_REC])) ||
             (e = stage_to(sb[A_KEY_NODE], ka.node, s, &used[A_KEY_NODE])) ||
             (e = stage_to(sb[A_KEY_BIN], ka.bin, s, &used[A_KEY_BIN])) ||
@@ -1673,7 +1765,34 @@ struct tm_engine {
         return hipSuccess;
     }
 
-    // dst[idx[i]] = src[i] for u32 entries (slot_list, arena words): staged
+    // the device records of nodes (host ids): their edge slots (width 16) or slot_list
+    // entries (width 4), each at the node's slot: staged
+    hipError_t scatter_nodes(std::vector<uint64_t> &dirty, uint32_t width) {
+        if (dirty.empty()) return hipSuccess;
+        std::sort(dirty.begin(), dirty.end());
+        dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+        const size_t n = dirty.size();
+        std::vector<uint64_t> idx(n);
+        for (size_t i = 0; i < n; i++) idx[i] = node_slot[dirty[i]];
+        DevBuf &dbuf = width == 16 ? d_etab : d_slot_list;
+        size_t so;
+        if (width == 16) {
+            std::vector<EdgeSlot> src(n);
+            for (size_t i = 0; i < n; i++) src[i] = edge_rec((uint32_t)dirty[i]);
+            patch.add(P_SCATTER, A_ETAB, n, 0, idx.data(), n * 8, src.data(), n * 16);
+            so = stage_bytes_add(src.data(), n * 16);
+        } else {
+            std::vector<uint32_t> src(n);
+            for (size_t i = 0; i < n; i++) src[i] = node_slist[dirty[i]];
+            patch.add(P_SCATTER, A_SLOT_LIST, n, 0, idx.data(), n * 8, src.data(), n * 4);
+            so = stage_bytes_add(src.data(), n * 4);
+        }
+        const size_t io = stage_bytes_add(idx.data(), n * 8);
+        sjobs.push_back(SJob{width, dbuf.p, n, io, so});
+        return hipSuccess;
+    }
+
+    // dst[idx[i]] = src[i] for u32 entries (arena words): staged
     template <class V>
     hipError_t scatter4(std::vector<uint64_t> &dirty, const V &tab, DevBuf &dbuf) {
         if (dirty.empty()) return hipSuccess;
@@ -1739,7 +1858,7 @@ struct tm_engine {
             dirty_wslots.clear();
         }
         size_t mx = 0;
-        for (const std::vector<uint64_t> *v : {&dirty_arena, &dirty_wslots, &dirty_eslots, &dirty_lists, &dirty_kid})
+        for (const std::vector<uint64_t> *v : {&dirty_arena, &dirty_wslots, &dirty_enodes, &dirty_lnodes, &dirty_kid})
             mx = std::max(mx, v->size());
         if ((e = d_scatter_idx.ensure(std::max<size_t>(mx, 1) * sizeof(uint64_t)))) return e;
         if ((e = d_scatter_src.ensure(std::max<size_t>(mx, 1) * 16))) return e;
@@ -1749,8 +1868,8 @@ struct tm_engine {
         if ((e = put_tail(d_arena, arena, arena_dev))) return e;
         if ((e = scatter4(dirty_arena, arena, d_arena))) return e;  // lists rewritten in place
         if ((e = scatter16(dirty_wslots, wtab, d_wtab))) return e;
-        if ((e = scatter16(dirty_eslots, etab, d_etab))) return e;
-        if ((e = scatter4(dirty_lists, slot_list, d_slot_list))) return e;
+        if ((e = scatter_nodes(dirty_enodes, 16))) return e;
+        if ((e = scatter_nodes(dirty_lnodes, 4))) return e;
         if ((e = upload_key_ids_delta())) return e;
         if ((e = flush_scatters())) return e;
         if (root_dirty) {
@@ -1878,7 +1997,8 @@ struct tm_engine {
         const size_t n = ops.size();
         std::vector<uint32_t> hnode(n, ROOT), hdepth(n, 0), nwalk(n, 0);
         std::vector<uint8_t> pkind(n, PK_NONE);
-        resolve_all(ops, ob.data(), hnode, hdepth, nwalk, pkind);
+        std::vector<uint64_t> mslot(n, ~0ull);
+        resolve_all(ops, ob.data(), hnode, hdepth, nwalk, pkind, mslot);
         tick("resolve");
         int rc = capacity_check(ops, ob.data(), hdepth, nwalk);
         tick("capacity");
@@ -1900,8 +2020,19 @@ struct tm_engine {
         // tables far larger than the caches (key set, key records, ids).  Their addresses are
         // known ahead for ops whose path exists: a two-stage prefetch (the key-set slot 16 ops
         // ahead, then the key record and id slot it leads to 8 ops ahead) overlaps those misses.
+        // An ADD whose path is new touches its deepest existing node (the child flags, its slot)
+        // and the map slot of its first new edge: known from the resolve, prefetched 16 ahead.
         auto pf_slot = [&](size_t i) {
-            if (pkind[i] != PK_NONE) __builtin_prefetch(&kset[key_hash(hnode[i], pkind[i], ops[i].id) & kmask]);
+            if (pkind[i] != PK_NONE) {
+                __builtin_prefetch(&kset[key_hash(hnode[i], pkind[i], ops[i].id) & kmask]);
+            } else if (ops[i].op == TM_OP_ADD) {
+                if (hnode[i] != ROOT) {
+                    __builtin_prefetch(&node_info[hnode[i]]);
+                    __builtin_prefetch(&node_bloom[hnode[i]]);
+                    __builtin_prefetch(&node_slot[hnode[i]]);
+                }
+                if (mslot[i] != ~0ull) __builtin_prefetch(&emap[mslot[i]]);
+            }
         };
         auto pf_key = [&](size_t i) {
             if (!idtab.empty()) __builtin_prefetch(&idtab[mix64(ops[i].id) & (idtab.size() - 1)]);
@@ -1960,9 +2091,9 @@ struct tm_engine {
         need_full = false;
         words_full = false;
         root_dirty = false;
-        dirty_eslots.clear();
+        dirty_enodes.clear();
         dirty_wslots.clear();
-        dirty_lists.clear();
+        dirty_lnodes.clear();
         dirty_arena.clear();
         for (uint32_t h : free_pending) free_keys.push_back(h);
         free_pending.clear();
@@ -2297,6 +2428,11 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     eng->node_list.reserve(rn);
     eng->node_list.push_back(NodeList{0, 0, 0});
     eng->node_cap.push_back(0);
+    for (hvec<uint32_t> *v : {&eng->node_bloom, &eng->node_info, &eng->node_slist}) {
+        v->reserve(rn);
+        v->push_back(0);
+    }
+    eng->emap_rehash(next_pow2(std::max<uint64_t>(rn * 2, 1024)));
     eng->edge_rehash(std::min<uint64_t>(next_pow2(std::max<uint64_t>(rn * eng->edge_load_inv(), 1024)), MAX_EDGE_SLOTS));
     eng->kset_rehash(next_pow2(std::max<uint64_t>(rk * 2, 1024)));
     eng->keys.reserve(rk);
@@ -3594,7 +3730,7 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
     out->n_keys = eng->replica ? eng->dv.n_live : eng->n_live;
     out->n_nodes = eng->replica ? eng->dv.n_nodes : eng->node_parent.size();
     out->n_words = eng->replica ? eng->dv.n_words : eng->word_off.size();
-    out->edge_slots = eng->replica ? eng->emask + 1 : eng->etab.size();
+    out->edge_slots = eng->emask + 1;
     out->word_slots = eng->replica ? eng->wmask + 1 : eng->wtab.size();
     out->list_words = eng->replica ? eng->dev_used[A_ARENA] / 4 : eng->arena.size();
     out->device_bytes = eng->d_wtab.cap + eng->d_warena.cap + eng->d_word_off.cap + eng->d_etab.cap +
@@ -3790,9 +3926,8 @@ int tm_replica_create(const tm_config *cfg, const void *d_image, uint64_t bytes,
     eng->replica = true;
     // the replica keeps no host master copy
     std::vector<WordSlot>().swap(eng->wtab);
-    hvec<EdgeSlot>().swap(eng->etab);
-    hvec<uint32_t>().swap(eng->slot_list);
-    hvec<uint32_t>().swap(eng->slot_node);
+    hvec<uint64_t>().swap(eng->eocc);
+    decltype(eng->emap)().swap(eng->emap);
     hvec<uint32_t>().swap(eng->kset);
     eng->release_ids();
     if ((rc = tm_replica_load(eng, d_image, bytes, stream)) != TM_OK) {

@@ -20,6 +20,7 @@
 
 #include "copy_api.h"
 #include "device_api.h"
+#include "image_api.h"
 #include "wave.h"
 
 namespace tmx {
@@ -740,6 +741,36 @@ __global__ void k_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *s
 hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, hipStream_t s) {
     if (!n) return hipSuccess;
     k_scatter8<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// The edge table image of a full publish: every slot empty, then each node's record in its
+// slot.  HBM-bound writes (20 B per slot, then 20 B per node at random slots).
+__global__ void k_edge_clear(uint4 *etab, uint32_t *slot_list, uint64_t cap) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
+        etab[i] = make_uint4(NONE, 0u, 0u, 0u);
+        slot_list[i] = 0u;
+    }
+}
+
+__global__ void k_edge_place(uint4 *etab, uint32_t *slot_list, const NodeImage *nodes, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const NodeImage r = nodes[i];
+    etab[r.slot] = make_uint4(r.parent, r.word, r.bloom, r.info);
+    slot_list[r.slot] = r.list;
+}
+
+hipError_t launch_edge_image(uint4 *etab, uint32_t *slot_list, uint64_t cap, const NodeImage *nodes, uint64_t n,
+                             hipStream_t s) {
+    if (!cap) return hipSuccess;
+    const uint64_t want = (cap + 255) / 256;
+    k_edge_clear<<<(unsigned)std::min<uint64_t>(want, 16384), 256, 0, s>>>(etab, slot_list, cap);
+    hipError_t e = hipGetLastError();
+    if (e || !n) return e;
+    k_edge_place<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(etab, slot_list, nodes, n);
     return hipGetLastError();
 }
 

@@ -312,3 +312,32 @@ extern "C" int conc_calls2(tm_engine *eng, int form, const uint8_t *const *bytes
         if (rc != TM_OK) return rc;
     return TM_OK;
 }
+
+// A backend with no matching at all (development: the aggregator's own per-publish cost on a
+// CPU-only host).  Every publish of a window gets the same `fake_ids` ids (one shared list,
+// like a hot '#' list every topic matches).
+namespace {
+struct FakeBackend {
+    std::vector<uint32_t> off, cnt;
+    std::vector<int32_t> status;
+    std::vector<uint64_t> ids;
+};
+}  // namespace
+
+extern "C" void *fake_backend_new(uint32_t ids_per_publish) {
+    FakeBackend *f = new FakeBackend();
+    f->ids.resize(ids_per_publish ? ids_per_publish : 1);
+    for (size_t i = 0; i < f->ids.size(); i++) f->ids[i] = i * 7 + 1;
+    return f;
+}
+extern "C" void fake_backend_free(void *p) { delete static_cast<FakeBackend *>(p); }
+extern "C" int fake_backend_fn(void *p, const uint8_t *, const uint32_t *, uint32_t n, uint32_t, tm_batch_view *out) {
+    FakeBackend *f = static_cast<FakeBackend *>(p);
+    if (f->off.size() < n + 1) {
+        f->off.assign(n + 1, 0);
+        f->cnt.assign(n, (uint32_t)f->ids.size());
+        f->status.assign(n, TM_TOPIC_OK);
+    }
+    *out = tm_batch_view{f->off.data(), f->cnt.data(), f->ids.data(), f->status.data()};
+    return TM_OK;
+}
