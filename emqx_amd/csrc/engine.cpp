@@ -1431,7 +1431,10 @@ struct tm_engine {
             for (uint64_t i = 0; i < n; i++) arena_id32[pos + i] = (uint32_t)L.ids[i];
         return ok;
     }
+    uint64_t ad_us[3] = {};  // the last apply_deltas: sort + list builds, in-place rewrites, moves
+    size_t ad_groups = 0, ad_inplace = 0;
     void apply_deltas() {
+        uint64_t ta = now_us();
         std::stable_sort(deltas.begin(), deltas.end(),
                          [](const Delta &a, const Delta &b) { return a.node < b.node; });
         std::vector<size_t> gs;  // group g: deltas [gs[g], gs[g + 1]) of one node
@@ -1455,6 +1458,8 @@ struct tm_engine {
         // Lists that fit their room are rewritten in place: disjoint arena ranges, nodes and
         // slots, so in parallel (the dirty records per thread, merged after); the rest move to
         // the arena's tail in node order on this thread.
+        ad_us[0] = now_us() - ta;
+        ta = now_us();
         std::vector<uint8_t> inplace(G, 0);
         size_t n_in = 0;
         for (size_t g = 0; g < G; g++) {
@@ -1502,6 +1507,8 @@ struct tm_engine {
                 if (stale[k]) ids_stale = true;
             }
         }
+        ad_us[1] = now_us() - ta;
+        ta = now_us();
         for (size_t g = 0; g < G; g++) {
             if (inplace[g]) continue;
             const uint32_t node = deltas[gs[g]].node;
@@ -1534,6 +1541,9 @@ struct tm_engine {
             }
             refresh_info(node);
         }
+        ad_us[2] = now_us() - ta;
+        ad_groups = G;
+        ad_inplace = n_in;
     }
 
     // ---- device upload.  Every allocation of a publish comes before its first in-place
@@ -1838,8 +1848,11 @@ struct tm_engine {
     // Delta publish, under mu_dev after quiesce().  Phase 1 allocates (moves of grown arrays,
     // key arrays that outgrew their buffers, the word table after a rehash, the scatter
     // staging); phase 2 writes in place.  A failure in phase 1 leaves the previous epoch whole.
+    uint64_t pub_us[4] = {};
+    size_t n_dirty_arena = 0;  // the last delta publish: quiesce, allocations, staging, H2D + scatter kernels
     hipError_t upload_delta() {
         hipError_t e;
+        uint64_t tp = now_us();
         // phase 1
         if ((e = grow(d_warena, warena, warena_dev))) return e;
         if ((e = grow(d_word_off, word_off, word_off_dev))) return e;
@@ -1862,21 +1875,28 @@ struct tm_engine {
             mx = std::max(mx, v->size());
         if ((e = d_scatter_idx.ensure(std::max<size_t>(mx, 1) * sizeof(uint64_t)))) return e;
         if ((e = d_scatter_src.ensure(std::max<size_t>(mx, 1) * 16))) return e;
+        pub_us[1] = now_us() - tp;
+        tp = now_us();
         // phase 2
         if ((e = put_tail(d_warena, warena, warena_dev))) return e;
         if ((e = put_tail(d_word_off, word_off, word_off_dev))) return e;
         if ((e = put_tail(d_arena, arena, arena_dev))) return e;
+        n_dirty_arena = dirty_arena.size();
         if ((e = scatter4(dirty_arena, arena, d_arena))) return e;  // lists rewritten in place
         if ((e = scatter16(dirty_wslots, wtab, d_wtab))) return e;
         if ((e = scatter_nodes(dirty_enodes, 16))) return e;
         if ((e = scatter_nodes(dirty_lnodes, 4))) return e;
         if ((e = upload_key_ids_delta())) return e;
+        pub_us[2] = now_us() - tp;
+        tp = now_us();
         if ((e = flush_scatters())) return e;
         if (root_dirty) {
             if ((e = hipMemcpyAsync(d_root.p, &root, sizeof(RootRec), hipMemcpyHostToDevice, stream))) return e;
             patch.add(P_WHOLE, A_ROOT, 1, d_root.cap, &root, sizeof(RootRec));
         }
-        return hipStreamSynchronize(stream);
+        e = hipStreamSynchronize(stream);
+        pub_us[3] = now_us() - tp;
+        return e;
     }
 
     static uint64_t now_us() {
@@ -1959,6 +1979,7 @@ struct tm_engine {
         std::lock_guard<std::recursive_mutex> g(mu_dev);
         const uint64_t t0 = now_us();
         hipError_t e = quiesce();  // in-flight matches read what this writes in place
+        pub_us[0] = now_us() - t0;
         if (!e) e = upload_delta();
         if (!e) set_view();
         commit_stall_us = now_us() - t0;
@@ -2061,6 +2082,10 @@ struct tm_engine {
                 rebuild_arena();
         }
         tick(full ? "rebuild_arena" : "apply_deltas");
+        if (trace && !full)
+            tr += " [lists=" + std::to_string(ad_us[0]) + " inplace=" + std::to_string(ad_us[1]) + " moved=" +
+                  std::to_string(ad_us[2]) + " nodes=" + std::to_string(ad_groups) + " inplace_nodes=" +
+                  std::to_string(ad_inplace) + " deltas=" + std::to_string(deltas.size()) + "]";
         deltas.clear();
         const uint64_t t2 = now_us();
         patch.reset();
@@ -2080,6 +2105,10 @@ struct tm_engine {
             return e == hipErrorOutOfMemory ? TM_ENOMEM : TM_EDEVICE;
         }
         tick(was_full ? "publish_full" : "publish_delta");
+        if (trace && !was_full)
+            tr += " [quiesce=" + std::to_string(pub_us[0]) + " alloc=" + std::to_string(pub_us[1]) +
+                  " stage=" + std::to_string(pub_us[2]) + " h2d+scatter=" + std::to_string(pub_us[3]) +
+                  " arena_words=" + std::to_string(n_dirty_arena) + "]";
         if (trace)
             fprintf(stderr, "tm commit epoch %llu: %zu ops, %s:%s\n", (unsigned long long)epoch, n,
                     was_full ? "full" : "delta", tr.c_str());
