@@ -23,6 +23,7 @@
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -299,6 +300,96 @@ struct ErrSlot {
     }
     const char *c_str() const { return tl_err().c_str(); }
 };
+
+// Resident helpers for a commit's parallel phases (resolve, list builds, list placement, the
+// delta upload's gathers): starting 15 threads costs ~0.3-0.5 ms, several times per commit,
+// against phases of 1-2 ms.  run(nt, f) calls f(0..nt-1), f(0) on the caller, and returns when
+// all are done.  One caller at a time (commits are serialised by mu_commit).
+struct WorkPool {
+    std::mutex m;
+    std::condition_variable cv_go, cv_done;
+    std::vector<std::thread> th;
+    const std::function<void(unsigned)> *job = nullptr;
+    unsigned want = 0, left = 0;
+    uint64_t gen = 0;
+    bool quit = false;
+    void loop(unsigned id) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(unsigned)> *j;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv_go.wait(lk, [&] { return quit || gen != seen; });
+                if (quit) return;
+                seen = gen;
+                if (id >= want) continue;
+                j = job;
+            }
+            (*j)(id);
+            std::lock_guard<std::mutex> g(m);
+            if (--left == 0) cv_done.notify_one();
+        }
+    }
+    void run(unsigned nt, const std::function<void(unsigned)> &f) {
+        try {
+            while (nt > 1 && th.size() < nt - 1) {
+                const unsigned id = (unsigned)th.size() + 1;
+                th.emplace_back([this, id] { loop(id); });
+            }
+        } catch (...) {  // fewer helpers than parts: the caller runs the parts left over
+        }
+        const unsigned helpers = std::min<unsigned>(nt ? nt - 1 : 0, (unsigned)th.size());
+        if (helpers) {
+            std::lock_guard<std::mutex> g(m);
+            job = &f;
+            want = helpers + 1;
+            left = helpers;
+            gen++;
+        }
+        if (helpers) cv_go.notify_all();
+        f(0);
+        for (unsigned k = helpers + 1; k < nt; k++) f(k);
+        if (!helpers) return;
+        std::unique_lock<std::mutex> lk(m);
+        cv_done.wait(lk, [&] { return left == 0; });
+    }
+    ~WorkPool() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            quit = true;
+        }
+        cv_go.notify_all();
+        for (std::thread &t : th) t.join();
+    }
+};
+// Sort and deduplicate a commit's dirty list (node ids, key handles, arena words: all below
+// 2^32): three 11-bit LSD radix passes for long lists (std::sort of 20 K random ids took ~2-3
+// ms of a config-E commit).
+static void sort_unique(std::vector<uint64_t> &v) {
+    const size_t n = v.size();
+    bool by_compare = n < 2048;
+    for (size_t i = 0; !by_compare && i < n; i++) by_compare = v[i] >> 32;
+    if (by_compare) {
+        std::sort(v.begin(), v.end());
+    } else {
+        std::vector<uint64_t> t(n);
+        uint32_t cnt[2048];
+        for (int sh = 0; sh < 33; sh += 11) {
+            std::fill(cnt, cnt + 2048, 0u);
+            for (uint64_t x : v) cnt[(x >> sh) & 2047]++;
+            uint32_t acc = 0;
+            for (uint32_t &c : cnt) {
+                const uint32_t k = c;
+                c = acc;
+                acc += k;
+            }
+            for (uint64_t x : v) t[cnt[(x >> sh) & 2047]++] = x;
+            v.swap(t);
+        }
+    }
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+}
+static unsigned commit_threads() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }
 
 // A few resident threads that split large host copies (staging a pageable batch into pinned
 // memory): thread start-up per copy would cost more than the copy of one sub-batch.
@@ -657,6 +748,15 @@ struct tm_engine {
     hipStream_t stream = nullptr;
     hipStream_t s_build = nullptr;  // a full rebuild's standby upload (beside the matches)
     CopyPool copier;  // tm_match_batch_runs: staging a pageable batch into pinned memory
+    mutable WorkPool pool;  // a commit's parallel phases (under mu_commit)
+    // f(0..n-1) in contiguous chunks on the pool's threads (random reads: one helper per 1 K)
+    template <class F>
+    void par_for(size_t n, const F &f) const {
+        const unsigned nt = n < 4096 ? 1u : (unsigned)std::min<size_t>(commit_threads(), n / 1024);
+        pool.run(nt, [&](unsigned k) {
+            for (size_t i = n * k / nt, e = n * (k + 1) / nt; i < e; i++) f(i);
+        });
+    }
     std::once_flag copier_once;
     hipEvent_t ev_chain = nullptr;  // orders a device match after the previous one's stream
     uint64_t n_full_rebuilds = 0, n_delta_commits = 0, n_slow_last = 0;
@@ -1222,8 +1322,7 @@ struct tm_engine {
             }
         };
         auto one = [&](size_t i, std::vector<std::pair<uint32_t, uint32_t>> &lv) {
-            const uint8_t *f = ob + ops[i].off;
-            split_levels(f, ops[i].len, lv);  // (hnode / hdepth come from walk_group)
+            const uint8_t *f = ob + ops[i].off;  // lv: its levels, hnode / hdepth: its walk (walk_group)
             // a '#' before the last level: a dead key, no path; a final '#': the path stops above it
             int hash_pos = -1;
             bool wild = false;
@@ -1241,25 +1340,18 @@ struct tm_engine {
             if (ops[i].op != TM_OP_ADD) return;
             nwalk[i] = dead ? 0 : levels;
         };
-        // memory-latency bound (a few dependent misses per level): 16 threads from 4 K ops on
-        const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-        const unsigned nt = n < 2048 ? 1u : (unsigned)std::min<size_t>(hw, n / 256);
+        // memory-latency bound (a dependent miss per level): up to 16 threads from 2 K ops on
+        const unsigned nt = n < 2048 ? 1u : (unsigned)std::min<size_t>(commit_threads(), n / 128);
         // thread k takes groups k, k + nt, ... of GRP consecutive ops
         auto range = [&](unsigned k, unsigned nthreads) {
             std::vector<std::pair<uint32_t, uint32_t>> lvs[GRP];
             for (size_t g = (size_t)k * GRP; g < n; g += (size_t)nthreads * GRP) {
                 const size_t e = std::min(n, g + GRP);
                 walk_group(g, e, lvs);
-                for (size_t i = g; i < e; i++) one(i, lvs[0]);
+                for (size_t i = g; i < e; i++) one(i, lvs[i - g]);
             }
         };
-        if (nt <= 1) {
-            range(0, 1);
-            return;
-        }
-        std::vector<std::thread> th;
-        for (unsigned k = 0; k < nt; k++) th.emplace_back([&, k] { range(k, nt); });
-        for (auto &t : th) t.join();
+        pool.run(nt, [&](unsigned k) { range(k, nt); });
     }
 
     // Recompute a node's emission bits from its list (and keep its I_PLUS/I_LIT):
@@ -1443,79 +1535,85 @@ struct tm_engine {
         gs.push_back(deltas.size());
         const size_t G = gs.size() - 1;
         std::vector<NewList> nl(G);
-        const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-        const unsigned nt = G < 512 ? 1u : (unsigned)std::min<size_t>(hw, G / 256);
-        if (nt <= 1) {
-            for (size_t g = 0; g < G; g++) build_list(gs[g], gs[g + 1], nl[g]);
-        } else {
-            std::vector<std::thread> th;
-            for (unsigned k = 0; k < nt; k++)
-                th.emplace_back([&, k] {
-                    for (size_t g = k; g < G; g += nt) build_list(gs[g], gs[g + 1], nl[g]);
-                });
-            for (auto &t : th) t.join();
-        }
-        // Lists that fit their room are rewritten in place: disjoint arena ranges, nodes and
-        // slots, so in parallel (the dirty records per thread, merged after); the rest move to
-        // the arena's tail in node order on this thread.
+        // several dependent misses per node (its list, the key records): helpers from 512 nodes
+        const unsigned nt = G < 512 ? 1u : (unsigned)std::min<size_t>(commit_threads(), G / 128);
+        pool.run(nt, [&](unsigned k) {
+            for (size_t g = k; g < G; g += nt) build_list(gs[g], gs[g + 1], nl[g]);
+        });
         ad_us[0] = now_us() - ta;
         ta = now_us();
+        // Where each list goes: lists that fit their room are rewritten in place; the others
+        // move to the arena's tail, their offsets handed out here in node order (the root's
+        // list always stays on this thread).  Then every list is written in parallel: disjoint
+        // arena ranges, nodes and slots (the dirty records per thread, merged after).
         std::vector<uint8_t> inplace(G, 0);
+        std::vector<uint32_t> dst(G, 0), room(G, 0);
         size_t n_in = 0;
+        uint64_t tail = arena.size();
         for (size_t g = 0; g < G; g++) {
             const uint32_t node = deltas[gs[g]].node;
             const NodeList &r = node_list[node];
-            const uint32_t k = nl[g].tc + nl[g].hc;
-            inplace[g] = node != ROOT && r.list_off && k && k <= node_cap[node];
-            n_in += inplace[g];
+            const uint32_t k = nl[g].tc + nl[g].hc, cap = node_cap[node];
+            if (node == ROOT) continue;
+            if (r.list_off && k && k <= cap) {
+                inplace[g] = 1;
+                n_in++;
+                dst[g] = r.list_off;
+                room[g] = cap;
+                continue;
+            }
+            arena_garbage += cap + (r.list_off ? LIST_HDR : 0);
+            // lists of 16 keys or more get a quarter more room when they move
+            room[g] = k >= 16 ? k + k / 4 : k;
+            if (k) {
+                dst[g] = (uint32_t)(tail + LIST_HDR);
+                tail += LIST_HDR + room[g];
+            }
         }
-        auto place_inplace = [&](size_t g, std::vector<uint64_t> &da, std::vector<uint64_t> &de,
-                                 std::vector<uint64_t> &dl) -> bool {
+        arena.resize(tail, 0u);  // the moved lists' room (zero past their keys)
+        auto place = [&](size_t g, std::vector<uint64_t> &da, std::vector<uint64_t> &de,
+                         std::vector<uint64_t> &dl) -> bool {
             const uint32_t node = deltas[gs[g]].node;
-            const uint32_t off = node_list[node].list_off;
             NewList &L = nl[g];
-            const uint32_t tc = L.tc, hc = L.hc;
-            // fits the list's room: rewrite it in place (header + keys), so the churn of a long
-            // list (a hot '#' prefix's subscribers) leaves no garbage behind
-            std::copy(L.keys.begin(), L.keys.end(), arena.begin() + off);
-            place_header(off, L);
-            const bool ok = place_ids(off, L);
-            for (uint64_t w = off - LIST_HDR; w < (uint64_t)off + tc + hc; w++)
-                if (w < arena_dev) da.push_back(w);
-            node_list[node] = NodeList{off, tc, hc};
+            const uint32_t tc = L.tc, hc = L.hc, off = dst[g];
+            bool ok = true;
+            if (tc + hc) {
+                std::copy(L.keys.begin(), L.keys.end(), arena.begin() + off);
+                place_header(off, L);
+                ok = place_ids(off, L);
+                if (inplace[g])  // words already on the device, rewritten in place
+                    for (uint64_t w = off - LIST_HDR; w < (uint64_t)off + tc + hc; w++)
+                        if (w < arena_dev) da.push_back(w);
+                node_list[node] = NodeList{off, tc, hc};
+            } else {
+                node_list[node] = NodeList{0, 0, 0};
+            }
+            node_cap[node] = tc + hc ? room[g] : 0;
             refresh_info_to(node, de, dl);
             return ok;
         };
-        const unsigned nt2 = n_in < 1024 ? 1u : (unsigned)std::min<size_t>(hw, n_in / 512);
-        if (nt2 <= 1) {
-            for (size_t g = 0; g < G; g++)
-                if (inplace[g] && !place_inplace(g, dirty_arena, dirty_enodes, dirty_lnodes)) ids_stale = true;
-        } else {
-            std::vector<std::vector<uint64_t>> da(nt2), de(nt2), dl(nt2);
-            std::vector<uint8_t> stale(nt2, 0);
-            std::vector<std::thread> th;
-            for (unsigned k = 0; k < nt2; k++)
-                th.emplace_back([&, k] {
-                    for (size_t g = k; g < G; g += nt2)
-                        if (inplace[g] && !place_inplace(g, da[k], de[k], dl[k])) stale[k] = 1;
-                });
-            for (auto &t : th) t.join();
-            for (unsigned k = 0; k < nt2; k++) {
-                dirty_arena.insert(dirty_arena.end(), da[k].begin(), da[k].end());
-                dirty_enodes.insert(dirty_enodes.end(), de[k].begin(), de[k].end());
-                dirty_lnodes.insert(dirty_lnodes.end(), dl[k].begin(), dl[k].end());
-                if (stale[k]) ids_stale = true;
-            }
+        const unsigned nt2 = G < 1024 ? 1u : (unsigned)std::min<size_t>(commit_threads(), G / 256);
+        std::vector<std::vector<uint64_t>> da(nt2), de(nt2), dl(nt2);
+        std::vector<uint8_t> stale(nt2, 0);
+        pool.run(nt2, [&](unsigned k) {
+            for (size_t g = k; g < G; g += nt2)
+                if (deltas[gs[g]].node != ROOT && !place(g, da[k], de[k], dl[k])) stale[k] = 1;
+        });
+        for (unsigned k = 0; k < nt2; k++) {
+            dirty_arena.insert(dirty_arena.end(), da[k].begin(), da[k].end());
+            dirty_enodes.insert(dirty_enodes.end(), de[k].begin(), de[k].end());
+            dirty_lnodes.insert(dirty_lnodes.end(), dl[k].begin(), dl[k].end());
+            if (stale[k]) ids_stale = true;
         }
         ad_us[1] = now_us() - ta;
         ta = now_us();
-        for (size_t g = 0; g < G; g++) {
-            if (inplace[g]) continue;
+        for (size_t g = 0; g < G; g++) {  // the root's list (its record lives apart from the slots)
             const uint32_t node = deltas[gs[g]].node;
+            if (node != ROOT) continue;
             const NodeList r = node_list[node];
             NewList &L = nl[g];
             const uint32_t tc = L.tc, hc = L.hc, cap = node_cap[node];
-            if (r.list_off && tc + hc && tc + hc <= cap) {  // the root's list (never in parallel)
+            if (r.list_off && tc + hc && tc + hc <= cap) {
                 std::copy(L.keys.begin(), L.keys.end(), arena.begin() + r.list_off);
                 place_header(r.list_off, L);
                 if (!place_ids(r.list_off, L)) ids_stale = true;
@@ -1524,20 +1622,19 @@ struct tm_engine {
                 node_list[node] = NodeList{r.list_off, tc, hc};
             } else {
                 arena_garbage += cap + (r.list_off ? LIST_HDR : 0);
-                // lists of 16 keys or more get a quarter more room when they move
-                const uint32_t room = tc + hc >= 16 ? tc + hc + (tc + hc) / 4 : tc + hc;
+                const uint32_t rm = tc + hc >= 16 ? tc + hc + (tc + hc) / 4 : tc + hc;
                 if (tc + hc == 0) {
                     node_list[node] = NodeList{0, 0, 0};
                 } else {
                     arena.resize(arena.size() + LIST_HDR);
                     const uint32_t off = (uint32_t)arena.size();
                     arena.insert(arena.end(), L.keys.begin(), L.keys.end());
-                    if (room > tc + hc) arena.resize(arena.size() + (room - tc - hc), 0u);
+                    if (rm > tc + hc) arena.resize(arena.size() + (rm - tc - hc), 0u);
                     place_header(off, L);
                     if (!place_ids(off, L)) ids_stale = true;
                     node_list[node] = NodeList{off, tc, hc};
                 }
-                node_cap[node] = tc + hc ? room : 0;
+                node_cap[node] = tc + hc ? rm : 0;
             }
             refresh_info(node);
         }
@@ -1693,16 +1790,15 @@ struct tm_engine {
 
     hipError_t upload_key_ids_delta() {
         if (dirty_kid.empty()) return hipSuccess;
-        std::sort(dirty_kid.begin(), dirty_kid.end());
-        dirty_kid.erase(std::unique(dirty_kid.begin(), dirty_kid.end()), dirty_kid.end());
+        sort_unique(dirty_kid);
         const size_t n = dirty_kid.size();
         std::vector<uint64_t> idx(n), rec(2 * n);
         std::vector<uint32_t> node(n), bin(n);
         std::vector<uint8_t> dd(n);
-        for (size_t i = 0; i < n; i++) {
+        par_for(n, [&](size_t i) {
             idx[i] = dirty_kid[i];
             key_dev_rec((uint32_t)dirty_kid[i], &rec[2 * i], &node[i], &bin[i], &dd[i]);
-        }
+        });
         dirty_kid.clear();
         patch.add(P_SCATTER, A_KEY_REC, n, 0, idx.data(), n * 8, rec.data(), n * 16);
         patch.add(P_SCATTER, A_KEY_BIN, n, 0, idx.data(), n * 8, bin.data(), n * 4);
@@ -1764,8 +1860,7 @@ struct tm_engine {
     hipError_t scatter16(std::vector<uint64_t> &dirty, const V &tab, DevBuf &dbuf) {
         static_assert(sizeof(Rec16) == 16, "16-byte records");
         if (dirty.empty()) return hipSuccess;
-        std::sort(dirty.begin(), dirty.end());
-        dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+        sort_unique(dirty);
         size_t n = dirty.size();
         std::vector<Rec16> src(n);
         for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
@@ -1779,21 +1874,25 @@ struct tm_engine {
     // entries (width 4), each at the node's slot: staged
     hipError_t scatter_nodes(std::vector<uint64_t> &dirty, uint32_t width) {
         if (dirty.empty()) return hipSuccess;
-        std::sort(dirty.begin(), dirty.end());
-        dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+        sort_unique(dirty);
         const size_t n = dirty.size();
         std::vector<uint64_t> idx(n);
-        for (size_t i = 0; i < n; i++) idx[i] = node_slot[dirty[i]];
         DevBuf &dbuf = width == 16 ? d_etab : d_slot_list;
         size_t so;
         if (width == 16) {
             std::vector<EdgeSlot> src(n);
-            for (size_t i = 0; i < n; i++) src[i] = edge_rec((uint32_t)dirty[i]);
+            par_for(n, [&](size_t i) {
+                idx[i] = node_slot[dirty[i]];
+                src[i] = edge_rec((uint32_t)dirty[i]);
+            });
             patch.add(P_SCATTER, A_ETAB, n, 0, idx.data(), n * 8, src.data(), n * 16);
             so = stage_bytes_add(src.data(), n * 16);
         } else {
             std::vector<uint32_t> src(n);
-            for (size_t i = 0; i < n; i++) src[i] = node_slist[dirty[i]];
+            par_for(n, [&](size_t i) {
+                idx[i] = node_slot[dirty[i]];
+                src[i] = node_slist[dirty[i]];
+            });
             patch.add(P_SCATTER, A_SLOT_LIST, n, 0, idx.data(), n * 8, src.data(), n * 4);
             so = stage_bytes_add(src.data(), n * 4);
         }
@@ -1806,8 +1905,7 @@ struct tm_engine {
     template <class V>
     hipError_t scatter4(std::vector<uint64_t> &dirty, const V &tab, DevBuf &dbuf) {
         if (dirty.empty()) return hipSuccess;
-        std::sort(dirty.begin(), dirty.end());
-        dirty.erase(std::unique(dirty.begin(), dirty.end()), dirty.end());
+        sort_unique(dirty);
         size_t n = dirty.size();
         std::vector<uint32_t> src(n);
         for (size_t i = 0; i < n; i++) src[i] = tab[dirty[i]];
@@ -2061,12 +2159,28 @@ struct tm_engine {
             const uint32_t h = kset[key_hash(hnode[i], pkind[i], ops[i].id) & kmask];
             if (h != NONE) __builtin_prefetch(&keys[h]);
         };
+        uint64_t tsc_kind[3] = {}, n_kind[3] = {};  // trace: ADD with the path present, ADD with a new path, DEL
         for (size_t i = 0; i < n; i++) {
             if (i + 16 < n) pf_slot(i + 16);
             if (i + 8 < n) pf_key(i + 8);
-            apply_one(ops[i], ob.data(), hnode[i], hdepth[i]);
+            if (trace) {
+                const int k = ops[i].op != TM_OP_ADD ? 2 : pkind[i] != PK_NONE ? 0 : 1;
+                const uint64_t c0 = __builtin_ia32_rdtsc();
+                apply_one(ops[i], ob.data(), hnode[i], hdepth[i]);
+                tsc_kind[k] += __builtin_ia32_rdtsc() - c0;
+                n_kind[k]++;
+            } else {
+                apply_one(ops[i], ob.data(), hnode[i], hdepth[i]);
+            }
         }
         tick("apply_ops");
+        if (trace) {
+            const uint64_t tot = std::max<uint64_t>(1, tsc_kind[0] + tsc_kind[1] + tsc_kind[2]);
+            tr += " [add_path=" + std::to_string(n_kind[0]) + ":" + std::to_string(100 * tsc_kind[0] / tot) + "% add_new=" +
+                  std::to_string(n_kind[1]) + ":" + std::to_string(100 * tsc_kind[1] / tot) + "% del=" +
+                  std::to_string(n_kind[2]) + ":" + std::to_string(100 * tsc_kind[2] / tot) + "% nodes=" +
+                  std::to_string(node_parent.size()) + "]";
+        }
         if (edge_full) {  // cannot happen after capacity_check; never serve a half-applied trie
             err = "internal: edge table overflow past the capacity check";
             return TM_EDEVICE;
