@@ -1685,12 +1685,14 @@ struct tm_engine {
         patch.add(P_WHOLE, a, bytes / ARR_ELEM[a], d.cap, h.data(), bytes);
         return hipSuccess;
     }
+    // the host array's new tail, staged with the epoch's scatters (one pinned H2D, then a
+    // device-side copy into place): a pageable H2D per array cost ~0.2-0.5 ms of a delta commit
     template <class V, class T = typename V::value_type>
     hipError_t put_tail(DevBuf &d, const V &h, size_t &dev_n) {
         if (h.size() <= dev_n) return hipSuccess;
-        hipError_t e = hipMemcpyAsync(d.as<T>() + dev_n, h.data() + dev_n, (h.size() - dev_n) * sizeof(T),
-                                      hipMemcpyHostToDevice, stream);
-        if (e != hipSuccess) return e;
+        const size_t bytes = (h.size() - dev_n) * sizeof(T);
+        sjobs.push_back(SJob{0, d.as<T>() + dev_n, bytes, 0, stage_bytes_add(h.data() + dev_n, bytes)});
+        const hipError_t e = hipSuccess;
         const uint32_t a = arr_of(&d);
         if (a < A_N) {
             patch.add(P_TAIL, a, (h.size() - dev_n) * sizeof(T) / ARR_ELEM[a], dev_n * sizeof(T) / ARR_ELEM[a],
@@ -1836,7 +1838,7 @@ struct tm_engine {
     // which crosses PCIe as ONE pinned copy; then one scatter kernel per array and one sync
     // (round 3 made two pageable copies, a kernel and a sync per array: ~3.6 ms at config E).
     struct SJob {
-        uint32_t width;  // bytes per element: 16, 4 or 1
+        uint32_t width;  // bytes per element: 16, 4 or 1; 0: a contiguous copy of n bytes to dst
         void *dst;
         size_t n, idx_off, src_off;  // offsets into the staged blob
     };
@@ -1861,7 +1863,8 @@ struct tm_engine {
         const uint8_t *base = d_sblob.as<uint8_t>();
         for (const SJob &j : sjobs) {
             const uint64_t *idx = reinterpret_cast<const uint64_t *>(base + j.idx_off);
-            if (j.width == 16) e = launch_scatter16((uint4 *)j.dst, idx, reinterpret_cast<const uint4 *>(base + j.src_off), j.n, stream);
+            if (j.width == 0) e = hipMemcpyAsync(j.dst, base + j.src_off, j.n, hipMemcpyDeviceToDevice, stream);
+            else if (j.width == 16) e = launch_scatter16((uint4 *)j.dst, idx, reinterpret_cast<const uint4 *>(base + j.src_off), j.n, stream);
             else if (j.width == 4) e = launch_scatter4((uint32_t *)j.dst, idx, reinterpret_cast<const uint32_t *>(base + j.src_off), j.n, stream);
             else e = launch_scatter1((uint8_t *)j.dst, idx, base + j.src_off, j.n, stream);
             if (e) return e;
