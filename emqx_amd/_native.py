@@ -64,6 +64,7 @@ EXPORTS = (
     "tm_replica_create", "tm_replica_load", "tm_patch_size", "tm_patch_export", "tm_replica_apply_patch",
     "tm_discard_staged", "tm_result_release", "tm_match_batch_runs", "tm_runs_release", "tm_build_info",
     "tm_match_ids_device", "tm_merge_shard_ids_device", "tm_debug_depth_stats", "tm_match_device_set",
+    "tm_debug_image_check",
     "tm_device_sync_set",
 )
 # every symbol include/emqx_tm_batcher.h declares
@@ -212,6 +213,7 @@ def load() -> C.CDLL:
     lib.tm_debug_timing.argtypes = [C.c_void_p, C.c_int, P(C.c_float)]
     lib.tm_debug_stats.argtypes = [C.c_void_p, C.c_int, P(C.c_uint64)]
     lib.tm_debug_depth_stats.argtypes = [C.c_void_p, P(C.c_uint64)]
+    lib.tm_debug_image_check.argtypes = [C.c_void_p, P(C.c_uint32)]
     lib.tm_result_ids_device.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     lib.tm_result_ids_device_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.tm_match_ids_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
@@ -614,6 +616,15 @@ class Engine:
                   "segments", "chunk_flushes", "frontier_chunks", "node_records", "inline_keys",
                   "cyc_prescan", "cyc_walk", "cyc_copyout", "hot_cyc_prescan", "hot_cyc_walk", "hot_cyc_copyout",
                   "hot_waves")
+
+    IMAGE_ARRAYS = ("word table", "word arena", "word offsets", "edge table", "slot lists", "list arena", "root")
+
+    def image_check(self):
+        """tm_debug_image_check: the names of the device arrays a full publish of the current
+        host state would change (empty: the delta-published index is byte-identical)."""
+        m = C.c_uint32()
+        self._check(self.lib.tm_debug_image_check(self.h, C.byref(m)))
+        return [n for a, n in enumerate(self.IMAGE_ARRAYS) if m.value >> a & 1]
 
     def depth_stats(self):
         """Per walk depth (tm_debug_depth_stats): list of dicts {depth, edge_probes, cycles,

@@ -3970,6 +3970,42 @@ int tm_debug_depth_stats(tm_engine *eng, uint64_t *out64) {
     return TM_OK;
 }
 
+// The device index as delta commits left it, array by array, against a full publish of the
+// same host state (the edge table then built on the device from one record per node, every
+// other array uploaded whole): bit a of *diff_mask set for each array whose bytes differ.
+// Words, edges, slot lists, the list arena and the root are compared; the key arrays are not
+// (a freed handle's device record stays as it was after a delta, by design: nothing refers to
+// it).  The full publish stays in place.  Test aid: commits wait meanwhile.
+int tm_debug_image_check(tm_engine *eng, uint32_t *diff_mask) {
+    if (!eng || !diff_mask || eng->replica) return TM_EINVAL;
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    std::lock_guard<std::mutex> gc(eng->mu_commit);
+    static const uint32_t arrs[] = {A_WTAB, A_WARENA, A_WORD_OFF, A_ETAB, A_SLOT_LIST, A_ARENA, A_ROOT};
+    std::vector<uint8_t> before[A_N];
+    auto grab = [&](uint32_t a, std::vector<uint8_t> &v) -> hipError_t {
+        v.resize(eng->dev_used[a]);
+        return v.empty() ? hipSuccess : hipMemcpy(v.data(), eng->arr_buf(a)->p, v.size(), hipMemcpyDeviceToHost);
+    };
+    {
+        std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+        TM_TRY_HIP(eng->quiesce(), TM_EDEVICE, "sync");
+        for (uint32_t a : arrs) TM_TRY_HIP(grab(a, before[a]), TM_EDEVICE, "D2H");
+    }
+    {
+        std::lock_guard<std::mutex> gh(eng->mu_host);
+        TM_TRY_HIP(eng->publish_full(), TM_EDEVICE, "full publish");
+    }
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    uint32_t mask = 0;
+    for (uint32_t a : arrs) {
+        std::vector<uint8_t> after;
+        TM_TRY_HIP(grab(a, after), TM_EDEVICE, "D2H");
+        if (after != before[a]) mask |= 1u << a;
+    }
+    *diff_mask = mask;
+    return TM_OK;
+}
+
 // Time the dominant kernel (k_match_fast) of the NEXT match call with HIP events
 // recorded on the stream it is launched on.  tm_debug_timing(eng, 1, NULL) arms;
 // after the match and a sync, tm_debug_timing(eng, 0, &ms) returns its duration.

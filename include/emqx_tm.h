@@ -455,6 +455,11 @@ int tm_debug_depth_stats(tm_engine *eng, uint64_t *out64);
 /* diagnostics: time the dominant kernel of the next match with HIP events on its
  * launch stream; enable=1 arms, then (after the match) enable=0 + ms_out reads. */
 int tm_debug_timing(tm_engine *eng, int enable, float *ms_out);
+/* test aid (ABI 9): the device index as delta commits left it vs a full publish of the same
+ * host state, array by array; *diff_mask gets bit a for each differing array (0: identical;
+ * the word table, word arena, word offsets, edge table, slot lists, list arena and root are
+ * compared).  The full publish stays in place. */
+int tm_debug_image_check(tm_engine *eng, uint32_t *diff_mask);
 
 #ifdef __cplusplus
 }
