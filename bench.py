@@ -121,8 +121,10 @@ def batcher_load(eng, tb, to32, seconds):
     from emqx_amd import _native as N
     lg = _loadgen()
     runs = []
-    # the cutter keeps a CPU; the completion thread and the caller block (driver waits, a sleep)
-    dt = max(2, min(14, cpu_topology()["usable_cpus"] - 2))
+    # the cutter is about half busy; the completion thread and the caller block (driver waits,
+    # a sleep): 15 delivery threads on the 16-CPU share (14: 73.8 / 15: 77.7 / 16: 77.2 M/s id
+    # lists in one box run, profiles/r04_batcher_threads_m.jsonl)
+    dt = max(2, min(15, cpu_topology()["usable_cpus"] - 1))
     plan = [(4096, N.TM_TRANSPORT_AUTO, 0), (65536, N.TM_TRANSPORT_AUTO, 0), (262144, N.TM_TRANSPORT_AUTO, 0),
             (65536, N.TM_TRANSPORT_AUTO, 1), (65536, N.TM_TRANSPORT_AUTO, 3), (65536, N.TM_TRANSPORT_IDS, 0)]
     warm = 0.5

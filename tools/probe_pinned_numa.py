@@ -44,6 +44,9 @@ def numa_nodes(addr, nbytes, samples=16):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-c", action="store_true")
+    ap.add_argument("--order", default="torch_pin_memory,hipHostMalloc,pageable")
+    ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     print(json.dumps({"placement": placement.pin_to_gpu(0)}), flush=True)
     keep = None
@@ -73,8 +76,10 @@ def main():
     tpin = torch.empty(len(tb), dtype=torch.uint8, pin_memory=True)
     tpin.numpy()[:] = tb
     dev = torch.empty(len(tb), dtype=torch.uint8, device="cuda")
-    for name, arr, t in (("torch_pin_memory", tpin.numpy(), tpin), ("hipHostMalloc", hbuf, torch.from_numpy(hbuf)),
-                         ("pageable", tb, torch.from_numpy(tb))):
+    bufs = {"torch_pin_memory": (tpin.numpy(), tpin), "hipHostMalloc": (hbuf, torch.from_numpy(hbuf)),
+            "pageable": (tb, torch.from_numpy(tb))}
+    for name in args.order.split(",") * args.rounds:
+        arr, t = bufs[name]
         torch.cuda.synchronize()
         h2d = []
         for _ in range(5):
@@ -85,7 +90,7 @@ def main():
         eng.match_runs_view(arr, to32)
         eng.lib.tm_runs_release(eng.h)
         ts = []
-        for _ in range(5):
+        for _ in range(args.reps):
             t0 = time.perf_counter()
             eng.match_runs_view(arr, to32)
             ts.append(time.perf_counter() - t0)
@@ -93,7 +98,8 @@ def main():
         print(json.dumps({"buffer": name, "bytes": len(tb), "numa_pages": numa_nodes(arr.ctypes.data, len(tb)),
                           "h2d_ms": round(float(np.median(h2d)) * 1e3, 3),
                           "h2d_GBps": round(len(tb) / float(np.median(h2d)) / 1e9, 1),
-                          "runs_ms": round(float(np.median(ts)) * 1e3, 3), "c_alive": keep is not None}), flush=True)
+                          "runs_ms": round(float(np.median(ts)) * 1e3, 3), "runs_ms_each": [round(x * 1e3, 2) for x in ts],
+                          "c_alive": keep is not None}), flush=True)
     hip.hipHostFree(hp)
     eng.close()
 
