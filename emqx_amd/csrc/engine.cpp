@@ -1191,12 +1191,22 @@ struct tm_engine {
         return (kind == K_EXACT_WORDS || kind == K_WILD) && depth > 31;
     }
 
-    void apply_one(const StagedOp &op, const uint8_t *ob, uint32_t hint_node = ROOT, uint32_t hint_depth = 0) {
+    // known_kind: the op's key kind when its whole path existed before the epoch (resolve_all's
+    // pkind): the key then hangs at hint_node, hint_depth levels down, and the filter need not
+    // be parsed again (nodes are never removed while an epoch applies)
+    void apply_one(const StagedOp &op, const uint8_t *ob, uint32_t hint_node = ROOT, uint32_t hint_depth = 0,
+                   uint8_t known_kind = PK_NONE) {
         uint8_t kind;
         uint32_t node, depth = 0;
         const uint8_t *fp = ob + op.off;
+        const bool known = known_kind != PK_NONE;
+        if (known) {
+            kind = known_kind;
+            node = hint_node;
+            depth = hint_depth;
+        }
         if (op.op == TM_OP_ADD) {
-            classify(fp, op.len, op.flags, true, &kind, &node, &depth, hint_node, hint_depth);
+            if (!known) classify(fp, op.len, op.flags, true, &kind, &node, &depth, hint_node, hint_depth);
             if (kind == K_DEAD) {
                 auto key = std::make_pair(std::string((const char *)fp, op.len), op.id);
                 if (dead_keys.count(key)) return;
@@ -1227,7 +1237,7 @@ struct tm_engine {
             n_live++;
             deltas.push_back(Delta{node, h, (uint8_t)(kind == K_HASH), 1});
         } else if (op.op == TM_OP_DEL) {
-            if (!classify(fp, op.len, op.flags, false, &kind, &node, &depth, hint_node, hint_depth))
+            if (!known && !classify(fp, op.len, op.flags, false, &kind, &node, &depth, hint_node, hint_depth))
                 return;  // idempotent
             if (kind == K_DEAD) {
                 auto it = dead_keys.find(std::make_pair(std::string((const char *)fp, op.len), op.id));
@@ -2214,11 +2224,11 @@ struct tm_engine {
             if (trace) {
                 const int k = ops[i].op != TM_OP_ADD ? 2 : pkind[i] != PK_NONE ? 0 : 1;
                 const uint64_t c0 = __builtin_ia32_rdtsc();
-                apply_one(ops[i], ob.data(), hnode[i], hdepth[i]);
+                apply_one(ops[i], ob.data(), hnode[i], hdepth[i], pkind[i]);
                 tsc_kind[k] += __builtin_ia32_rdtsc() - c0;
                 n_kind[k]++;
             } else {
-                apply_one(ops[i], ob.data(), hnode[i], hdepth[i]);
+                apply_one(ops[i], ob.data(), hnode[i], hdepth[i], pkind[i]);
             }
         }
         tick("apply_ops");

@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--order", default="torch_pin_memory,hipHostMalloc,pageable")
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--release-c-lane", action="store_true", help="free this thread's device lane on C's engine first")
     args = ap.parse_args()
     print(json.dumps({"placement": placement.pin_to_gpu(0)}), flush=True)
     keep = None
@@ -62,6 +63,8 @@ def main():
             keep.match_runs_view(pc.numpy(), to)
             keep.lib.tm_runs_release(keep.h)
         del pc
+        if args.release_c_lane:
+            keep.result_release()  # its three streams
     w = workloads.generate("B", n_topics=1_000_000)
     eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
     eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
