@@ -28,9 +28,13 @@ import numpy as np
 
 # Two device batches in flight need their two streams on different hardware queues; HIP's
 # default is 4 queues per process, shared round-robin by every stream the process creates
-# (torch's, the engine's, the aggregator's), so the bench asks for 8.  Set before HIP starts.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# (torch's, each engine's two, three per calling thread per engine for the host-form calls,
+# the aggregator's three).  With 8, the config-B engine built beside config C's ran its first
+# ~6 runs-form calls at 3.1 ms instead of 1.2 ms (its H2D, walk and D2H streams landed on
+# queues other streams held; profiles/r04_probe_hwq*_o.jsonl), so the bench asks for 16.
+# Set before HIP starts.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
