@@ -19,6 +19,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -620,7 +621,7 @@ struct tm_engine {
         if (arena_id32)
             for (uint64_t i = lo; i < hi; i++) arena_id32[i] = (uint32_t)arena_id[i];
     }
-    bool ids_stale = false;
+    std::atomic<bool> ids_stale{false};  // set by list placements running in parallel
     bool reserve_ids() {  // a virtual reservation of the budget (halved until the OS grants it)
         uint64_t want = std::min<uint64_t>(std::max<uint64_t>(arena_budget() + 16, 1ull << 16), 1ull << 32);
         while (want >= (1ull << 12)) {
@@ -1457,15 +1458,19 @@ struct tm_engine {
             else arena[tfill[k.node]++] = (uint32_t)h;
         }
         node_cap.assign(nn, 0);
-        for (size_t v = 0; v < nn; v++) {
+        // per node: disjoint arena ranges and node records, so in parallel (random reads of the
+        // key records for the headers and ids); the root's record apart
+        std::vector<uint64_t> none_e, none_l;  // need_full: refresh_info_to records nothing
+        par_for(nn, [&](size_t v) {
             node_list[v] = NodeList{pos[v], tcnt[v], hcnt[v]};
             node_cap[v] = tcnt[v] + hcnt[v];
             if (pos[v]) {
                 write_header(pos[v], &arena[pos[v]], tcnt[v], &arena[pos[v] + tcnt[v]], hcnt[v]);
                 ids_of(pos[v], (uint64_t)pos[v] + tcnt[v] + hcnt[v]);
             }
-            refresh_info((uint32_t)v);
-        }
+            if (v != ROOT) refresh_info_to((uint32_t)v, none_e, none_l);
+        });
+        refresh_info(ROOT);
         arena_garbage = 0;
         need_full = true;
     }
@@ -1733,7 +1738,7 @@ struct tm_engine {
         k.node.resize(keys.size());
         k.bin.resize(keys.size());
         k.dd.resize(keys.size());
-        for (size_t h = 0; h < keys.size(); h++) key_dev_rec((uint32_t)h, &k.rec[2 * h], &k.node[h], &k.bin[h], &k.dd[h]);
+        par_for(keys.size(), [&](size_t h) { key_dev_rec((uint32_t)h, &k.rec[2 * h], &k.node[h], &k.bin[h], &k.dd[h]); });
     }
 
     // Full publish into a STANDBY image: every array is uploaded into fresh buffers on s_build
@@ -1767,10 +1772,11 @@ struct tm_engine {
         };
         // the edge table: built on the device from one record per node
         hvec<NodeImage> nim(node_parent.size() - 1);
-        for (size_t v = 1; v < node_parent.size(); v++) {
-            const EdgeSlot r = edge_rec((uint32_t)v);
-            nim[v - 1] = NodeImage{node_slot[v], r.parent, r.word, r.bloom, r.info, node_slist[v]};
-        }
+        par_for(nim.size(), [&](size_t i) {
+            const uint32_t v = (uint32_t)i + 1;
+            const EdgeSlot r = edge_rec(v);
+            nim[i] = NodeImage{node_slot[v], r.parent, r.word, r.bloom, r.info, node_slist[v]};
+        });
         DevBuf d_nim;
         const uint64_t slots = edge_slots();
         if ((e = sb[A_ETAB].ensure(slots * sizeof(EdgeSlot))) || (e = sb[A_SLOT_LIST].ensure(slots * 4)) ||
