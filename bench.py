@@ -1393,10 +1393,37 @@ def filter_leg(args, w, eng, q):
             bad += 1
     if bad:
         log(f"PARITY FAILURE (matches_filter): {bad}/{ps} queries differ")
+    # the runs form: the walk's ranges cross PCIe and become spans of the sorted key ids
+    import ctypes as C
+    lg = _loadgen()
+    for _ in range(args.warmup):
+        eng.match_filter_runs_view(qb, qo)
+    tr, trr = [], []
+    for _ in range(max(1, min(args.steps, 20))):
+        t0 = time.perf_counter()
+        res = eng.match_filter_runs_view(qb, qo)
+        tr.append(time.perf_counter() - t0)
+        lg.spans_checksum(C.byref(res), 8)
+        trr.append(time.perf_counter() - t0)
+    dtr, dtrr = float(np.mean(tr)), float(np.mean(trr))
+    spans = int(res.total_spans)
+    ro, rids, rk, rst = eng.match_filter_runs(qb, qo[:ps + 1])
+    bad_r = int(np.sum(rst != st[:ps]))
+    for i in range(ps):
+        if not np.array_equal(rids[ro[i]:ro[i + 1]], eng_ids[o[i]:o[i] + c[i]]):
+            bad_r += 1
+    if bad_r:
+        log(f"PARITY FAILURE (matches_filter runs): {bad_r}/{ps} queries differ")
     return {
         "api": "tm_match_filter_batch (matches_filter/3)", "queries": q,
         "query_mix": "stored filters / one level '+' / deep prefix + '#', a third each",
         "queries_per_s": round(q / dt, 1), "ms_per_batch": round(dt * 1e3, 3), "keys_returned": total,
+        "runs_form": {"api": "tm_match_filter_batch_runs", "queries_per_s": round(q / dtr, 1),
+                      "ms_per_batch": round(dtr * 1e3, 3), "spans": spans, "d2h_bytes": spans * 8 + 12 * q,
+                      "read_every_id": {"ms_per_batch": round(dtrr * 1e3, 3), "queries_per_s": round(q / dtrr, 1),
+                                        "threads": 8},
+                      "parity": {"sampled_queries": ps, "mismatches": bad_r,
+                                 "compared": "ids in walk order vs the keys form's"}},
         "index_build_ms": round(t_index * 1e3, 1),
         "cpu_baseline": {"value": round(q / dt_cpu, 1), "unit": "queries/s", "cores": threads, "kind": "port",
                          "sample": f"all {q} queries, oracle/trie_search.cpp ALGO_FILTER, counts only"},

@@ -64,7 +64,7 @@ EXPORTS = (
     "tm_replica_create", "tm_replica_load", "tm_patch_size", "tm_patch_export", "tm_replica_apply_patch",
     "tm_discard_staged", "tm_result_release", "tm_match_batch_runs", "tm_runs_release", "tm_build_info",
     "tm_match_ids_device", "tm_merge_shard_ids_device", "tm_debug_depth_stats", "tm_match_device_set",
-    "tm_debug_image_check",
+    "tm_debug_image_check", "tm_match_filter_batch_runs",
     "tm_device_sync_set",
 )
 # every symbol include/emqx_tm_batcher.h declares
@@ -197,6 +197,8 @@ def load() -> C.CDLL:
     lib.tm_intersect_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                        P(tm_intersect_result)]
     lib.tm_match_filter_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, P(tm_result)]
+    lib.tm_match_filter_batch_runs.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                               P(tm_runs_result)]
     lib.tm_match_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64,
                                     C.c_void_p, P(tm_dev_result)]
     lib.tm_device_sync.argtypes = [C.c_void_p]
@@ -528,35 +530,54 @@ class Engine:
                                                  C.byref(res)))
         return res
 
+    @staticmethod
+    def _expand_runs(res, n):
+        """A tm_runs_result, expanded: (off u32[n+1], ids u64, kcnt u32[n], status i32[n]);
+        item i's ids are ids[off[i]:off[i+1]], its spans in order."""
+        if n == 0:
+            return np.zeros(1, np.uint32), np.zeros(0, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.int32)
+        kcnt = np.ctypeslib.as_array(res.kcnt, shape=(n,)).copy()
+        st = np.ctypeslib.as_array(res.status, shape=(n,)).copy()
+        soff = np.ctypeslib.as_array(res.span_off, shape=(n,)).copy()
+        scnt = np.ctypeslib.as_array(res.span_cnt, shape=(n,)).copy()
+        ids = np.zeros(int(res.total_ids), dtype=np.uint64)
+        o = np.zeros(n + 1, dtype=np.uint32)
+        np.cumsum(kcnt, out=o[1:])
+        for i in range(n):
+            at = int(o[i])
+            for j in range(int(soff[i]), int(soff[i]) + int(scnt[i])):
+                sp = res.spans[j]
+                k = int(sp.n)
+                if k:
+                    ids[at:at + k] = np.ctypeslib.as_array(C.cast(sp.ids, C.POINTER(C.c_uint64)), shape=(k,))
+                at += k
+            assert at == int(o[i + 1]), "spans of an item disagree with its id count"
+        return o, ids, kcnt, st
+
     def match_runs(self, buf: np.ndarray, off: np.ndarray):
         """tm_match_batch_runs, expanded: (off u32[n+1], ids u64, kcnt u32[n], status i32[n]).
         Topic i's ids are ids[off[i]:off[i+1]] (the multiset tm_match_batch + key ids gives)."""
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         off = np.ascontiguousarray(off, dtype=np.uint32)
-        n = len(off) - 1
         res = self.match_runs_view(buf, off)
         try:
-            if n == 0:
-                return np.zeros(1, np.uint32), np.zeros(0, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.int32)
-            kcnt = np.ctypeslib.as_array(res.kcnt, shape=(n,)).copy()
-            st = np.ctypeslib.as_array(res.status, shape=(n,)).copy()
-            soff = np.ctypeslib.as_array(res.span_off, shape=(n,)).copy()
-            scnt = np.ctypeslib.as_array(res.span_cnt, shape=(n,)).copy()
-            ids = np.zeros(int(res.total_ids), dtype=np.uint64)
-            o = np.zeros(n + 1, dtype=np.uint32)
-            np.cumsum(kcnt, out=o[1:])
-            for i in range(n):
-                at = int(o[i])
-                for j in range(int(soff[i]), int(soff[i]) + int(scnt[i])):
-                    sp = res.spans[j]
-                    k = int(sp.n)
-                    if k:
-                        ids[at:at + k] = np.ctypeslib.as_array(C.cast(sp.ids, C.POINTER(C.c_uint64)), shape=(k,))
-                    at += k
-                assert at == int(o[i + 1]), "spans of a topic disagree with its id count"
-            return o, ids, kcnt, st
+            return self._expand_runs(res, len(off) - 1)
         finally:
             self._check(self.lib.tm_runs_release(self.h))
+
+    def match_filter_runs_view(self, buf: np.ndarray, off: np.ndarray, mode: int = TM_MATCH_ALL) -> tm_runs_result:
+        """tm_match_filter_batch_runs without copying: spans of the sorted key ids, valid until
+        this thread's next such call or result_release()."""
+        res = tm_runs_result()
+        self._check(self.lib.tm_match_filter_batch_runs(self.h, buf.ctypes.data, off.ctypes.data, len(off) - 1, mode,
+                                                        C.byref(res)))
+        return res
+
+    def match_filter_runs(self, buf: np.ndarray, off: np.ndarray, mode: int = TM_MATCH_ALL):
+        """tm_match_filter_batch_runs, expanded: (off, ids u64 in walk order, kcnt, status)."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        return self._expand_runs(self.match_filter_runs_view(buf, off, mode), len(off) - 1)
 
     def match(self, topics, mode: int = TM_MATCH_ALL):
         """List of topics -> list of key-handle lists (None for badarg topics)."""

@@ -464,6 +464,13 @@ struct HostOut {
     std::vector<uint32_t> f_off, f_cnt, f_ukeys;
     std::vector<int32_t> f_status;
     PinBuf f_keys;
+    // tm_match_filter_batch_runs: per-query span counts, the walk's ranges, their spans, and the
+    // sorted ids the spans point into (kept alive here across index rebuilds)
+    std::vector<uint32_t> f_rcnt, fr_off, fr_cnt;  // fr_*: the runs result's (the keys form reuses f_*)
+    std::vector<int32_t> fr_status;
+    PinBuf f_rng;
+    std::vector<tm_span> f_spans;
+    std::shared_ptr<const std::vector<uint64_t>> f_ids;
     // intersection/2
     std::vector<uint64_t> ix_off;
     std::vector<int32_t> ix_len;
@@ -2414,7 +2421,10 @@ struct tm_engine {
         uint32_t K = 0;
         DevBuf d_kw, d_koff, d_kh;
         DevBuf d_qw, d_qoff, d_qdollar, d_qstatus, d_cnt, d_off, d_out, d_scan, d_pool, d_ctl, d_jobs, d_krec, d_kend;
+        DevBuf d_rcnt;                                  // FW_RUNS: ranges per query
         uint64_t out_want = 1 << 16, pool_want = 1024;  // one-pass sizes (from the demand seen)
+        uint64_t rng_want = 1 << 16;                    // FW_RUNS output (ranges)
+        std::shared_ptr<const std::vector<uint64_t>> ids;  // id of sorted key j (the runs form's spans)
         std::vector<uint32_t> qw, qoff;
         std::vector<uint32_t> wcode;     // interned word id -> order code (NONE: not cached yet)
         std::vector<uint8_t> qdollar;
@@ -2515,6 +2525,11 @@ struct tm_engine {
             kh[j] = lk[i];
         }
         kw.insert(kw.end(), 8, 0u);  // k_filter_walk preloads 8 words of a key unconditionally
+        {
+            auto ids = std::make_shared<std::vector<uint64_t>>(kh.size());
+            for (size_t j = 0; j < kh.size(); j++) (*ids)[j] = keys[kh[j]].id;
+            fx.ids = std::move(ids);
+        }
         // fixed-stride records {length, first FW_REC_WORDS codes}: a compare reads one 32-B
         // record instead of koff and then the words (one round trip instead of two)
         std::vector<uint32_t> krec(std::max<size_t>(lk.size(), 1) * 8, 0u);
@@ -3696,19 +3711,10 @@ int tm_key_ids(const tm_engine *eng, const uint32_t *keys, size_t n, uint64_t *i
     return TM_OK;
 }
 
-int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
-                          tm_result *out) {
-    if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
-    if (mode != TM_MATCH_ALL && mode != TM_MATCH_UNIQUE && mode != TM_MATCH_FIRST) return TM_EINVAL;
-    if (eng->replica) return replica_refuses(eng, "tm_match_filter_batch");
-    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
-    // the walk's key index is built from the host copy (mu_host); it runs on the engine stream
-    std::lock_guard<std::mutex> gh(eng->mu_host);
-    std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
-    HostOut &o = eng->out();
-    memset(out, 0, sizeof(*out));
-    out->n = n;
-    if (n == 0) return TM_OK;
+// The queries of a matches_filter batch on the device and the walk's arguments (both forms):
+// filter_words/1 as order codes, base_init/1's flag, per-query status.  Under mu_host + mu_dev.
+static int filter_prepare(tm_engine *eng, HostOut &o, const uint8_t *bytes, const uint32_t *off, uint32_t n,
+                          uint32_t mode, FilterArgs &a) {
     auto &fx = eng->fx;
     int rc;
     if (fx.epoch != eng->epoch && (rc = eng->build_filter_index())) return rc;
@@ -3757,7 +3763,6 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
     TM_TRY_HIP(hipMemcpyAsync(fx.d_qdollar.p, fx.qdollar.data(), n, hipMemcpyHostToDevice, s), TM_EDEVICE, "H2D");
     TM_TRY_HIP(hipMemcpyAsync(fx.d_qstatus.p, o.f_status.data(), (size_t)n * 4, hipMemcpyHostToDevice, s), TM_EDEVICE,
                "H2D");
-    FilterArgs a{};
     a.kw = fx.d_kw.as<uint32_t>();
     a.krec = fx.d_krec.as<uint4>();
     a.kend = fx.d_kend.as<uint32_t>();
@@ -3774,6 +3779,27 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
     a.out_off = fx.d_off.as<uint32_t>();
     o.f_off.resize((size_t)n + 1);
     o.f_cnt.resize(n);
+    return TM_OK;
+}
+
+int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
+                          tm_result *out) {
+    if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
+    if (mode != TM_MATCH_ALL && mode != TM_MATCH_UNIQUE && mode != TM_MATCH_FIRST) return TM_EINVAL;
+    if (eng->replica) return replica_refuses(eng, "tm_match_filter_batch");
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    // the walk's key index is built from the host copy (mu_host); it runs on the engine stream
+    std::lock_guard<std::mutex> gh(eng->mu_host);
+    std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+    HostOut &o = eng->out();
+    memset(out, 0, sizeof(*out));
+    out->n = n;
+    if (n == 0) return TM_OK;
+    auto &fx = eng->fx;
+    FilterArgs a{};
+    int rc = filter_prepare(eng, o, bytes, off, n, mode, a);
+    if (rc) return rc;
+    hipStream_t s = eng->stream;
     uint64_t total = 0;
     // One pass: the walk streams its keys into pooled chunks and copies them to a contiguous
     // range reserved at its end.  Sized from the demand of earlier batches; a batch that does
@@ -3880,6 +3906,92 @@ int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *
         out->total = o.f_ukeys.size();
         out->keys = o.f_ukeys.data();
     }
+    return TM_OK;
+}
+
+int tm_match_filter_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
+                               tm_runs_result *out) {
+    if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
+    if (mode != TM_MATCH_ALL && mode != TM_MATCH_FIRST) return TM_EINVAL;
+    if (eng->replica) return replica_refuses(eng, "tm_match_filter_batch_runs");
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    std::lock_guard<std::mutex> gh(eng->mu_host);
+    std::lock_guard<std::recursive_mutex> gd(eng->mu_dev);
+    HostOut &o = eng->out();
+    memset(out, 0, sizeof(*out));
+    out->n = n;
+    out->epoch = eng->epoch;
+    if (n == 0) return TM_OK;
+    auto &fx = eng->fx;
+    FilterArgs a{};
+    int rc = filter_prepare(eng, o, bytes, off, n, mode, a);
+    if (rc) return rc;
+    hipStream_t s = eng->stream;
+    TM_TRY_HIP(fx.d_rcnt.ensure((size_t)n * 4), TM_ENOMEM, "alloc");
+    a.rcnt = fx.d_rcnt.as<uint32_t>();
+    o.f_rcnt.resize(n);
+    uint64_t ranges = 0;
+    bool done = false;
+    for (int attempt = 0; attempt < 3 && !done; attempt++) {
+        // sized from the demand of earlier batches; a batch past them grows and runs again
+        const uint64_t pool = std::max<uint64_t>(fx.pool_want, (uint64_t)n + 1024);
+        const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(fx.rng_want, 1 << 16), 0xFFFFFFF0ull);
+        TM_TRY_HIP(fx.d_pool.ensure(pool * FW_CHUNK * 4), TM_ENOMEM, "alloc filter pool");
+        TM_TRY_HIP(fx.d_out.ensure(cap * 8), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(fx.d_ctl.ensure(24), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(hipMemsetAsync(fx.d_ctl.p, 0, 24, s), TM_EDEVICE, "memset");
+        a.pool = fx.d_pool.as<uint32_t>();
+        a.pool_chunks = fx.d_pool.cap / (FW_CHUNK * 4);
+        a.out = fx.d_out.as<uint32_t>();
+        a.out_cap = fx.d_out.cap / 8;
+        a.ctl = fx.d_ctl.as<unsigned long long>();
+        a.jobs = nullptr;
+        a.jobs_cap = 0;
+        uint64_t ctl[3] = {0, 0, 0};
+        TM_TRY_HIP(launch_filter_walk(a, FW_RUNS, s), TM_EDEVICE, "k_filter_walk runs");
+        TM_TRY_HIP(hipMemcpyAsync(ctl, fx.d_ctl.p, 24, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(o.f_off.data(), fx.d_off.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                   "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(o.f_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                   "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(o.f_rcnt.data(), fx.d_rcnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
+                   "D2H");
+        TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk runs");
+        ranges = ctl[0];
+        if (ranges <= a.out_cap && ctl[1] <= a.pool_chunks) {
+            TM_TRY_HIP(o.f_rng.ensure(std::max<uint64_t>(ranges, 1) * 8), TM_ENOMEM, "pinned alloc");
+            if (ranges) {
+                TM_TRY_HIP(d2h_words(o.f_rng, 0, fx.d_out.p, ranges * 2, s), TM_EDEVICE, "D2H");
+                TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk runs");
+            }
+            done = true;
+        } else {
+            fx.rng_want = std::max(fx.rng_want, ranges + ranges / 4 + 1024);
+            fx.pool_want = std::max(fx.pool_want, ctl[1] + ctl[1] / 4 + 64);
+        }
+    }
+    if (!done) {
+        eng->err = "tm_match_filter_batch_runs: output still short after resizing";
+        return TM_EDEVICE;
+    }
+    // ranges of the sorted keys -> spans of their ids (this lane keeps the ids alive)
+    o.f_ids = fx.ids;
+    const uint64_t *ids = o.f_ids->data();
+    const uint2 *rg = o.f_rng.as<uint2>();
+    o.f_spans.resize(ranges);
+    uint64_t tot = 0;
+    for (uint64_t r = 0; r < ranges; r++) o.f_spans[r] = tm_span{ids + rg[r].x, rg[r].y};
+    for (uint32_t i = 0; i < n; i++) tot += o.f_cnt[i];
+    o.fr_off.swap(o.f_off);  // the runs result's own arrays: a keys-form call does not touch them
+    o.fr_cnt.swap(o.f_cnt);
+    o.fr_status.swap(o.f_status);
+    out->total_ids = tot;
+    out->total_spans = ranges;
+    out->span_off = o.fr_off.data();
+    out->span_cnt = o.f_rcnt.data();
+    out->spans = o.f_spans.data();
+    out->kcnt = o.fr_cnt.data();
+    out->status = o.fr_status.data();
     return TM_OK;
 }
 

@@ -39,8 +39,12 @@ struct FilterArgs {
                               // [2] bulk jobs
     uint4 *jobs;              // FW_ONEPASS: {src sorted key, dst, count (<= FW_JOB), 0}
     uint64_t jobs_cap;
+    // FW_RUNS: the walk's ranges themselves are the result: query q's rcnt[q] ranges {first
+    // sorted key, count} at ((uint2 *)out)[out_off[q] ..], cnt[q] keys; ctl[0] counts ranges and
+    // out_cap is in ranges
+    uint32_t *rcnt;
 };
-constexpr int FW_COUNT = 0, FW_EMIT = 1, FW_ONEPASS = 2;
+constexpr int FW_COUNT = 0, FW_EMIT = 1, FW_ONEPASS = 2, FW_RUNS = 3;
 constexpr uint32_t FW_CHUNK = 256;   // u32 words per pool chunk (1 link entry + 127 ranges of 2 words)
 constexpr uint32_t FW_BULK = 4096;   // ranges longer than this are copied by k_filter_bulk
 constexpr uint32_t FW_JOB = 8192;    // keys per k_filter_bulk job (a long range is split)

@@ -374,7 +374,7 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             uint64_t fm = __ballot(full);
             if (a.first && fm) fm &= 0 - fm;  // return_first: the first key met only
             const uint32_t nf = __popcll(fm);
-            if (pass == FW_ONEPASS) {
+            if (pass == FW_ONEPASS || pass == FW_RUNS) {
                 // consecutive FULL lanes form one range: {first key, run length}
                 const bool st0 = ((fm >> lane) & 1ull) && (lane == 0 || !((fm >> (lane - 1)) & 1ull));
                 const uint64_t sm = __ballot(st0);
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
                 const uint32_t m = E - rs;
                 if (pass == FW_EMIT) {
                     copy_keys(a.kh + rs, out + c, m, lane);
-                } else if (pass == FW_ONEPASS) {
+                } else if (pass == FW_ONEPASS || pass == FW_RUNS) {
                     chain_put(1ull, rs, m);
                 }
                 c += m;
@@ -414,6 +414,28 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
         }
     }
     if (pass == FW_COUNT && lane == 0) a.cnt[q] = c;
+    if (pass == FW_RUNS) {
+        // the chain's ranges, in walk order, to a contiguous range of the output: no key is
+        // copied (tm_match_filter_batch_runs turns them into spans of the host's sorted ids)
+        unsigned long long base = 0;
+        if (lane == 0 && nent) base = atomicAdd(&a.ctl[0], (unsigned long long)nent);
+        base = __shfl(base, 0);
+        if (lane == 0) {
+            a.cnt[q] = c;
+            a.rcnt[q] = nent;
+            a.out_off[q] = (uint32_t)base;
+        }
+        if (short_pool || base + nent > a.out_cap) return;  // the host grows and re-runs
+        __threadfence_block();
+        uint2 *out2 = reinterpret_cast<uint2 *>(a.out);
+        uint32_t ch = head;
+        for (uint32_t cb = 0; cb < nent; cb += CE) {
+            const uint32_t m = min(CE, nent - cb);
+            const uint2 *ent = pool2 + (uint64_t)ch * (FW_CHUNK / 2) + 1;
+            for (uint32_t e = lane; e < m; e += 64) out2[base + cb + e] = ent[e];
+            if (cb + CE < nent) ch = pool2[(uint64_t)ch * (FW_CHUNK / 2)].x;  // next chunk
+        }
+    }
     if (pass == FW_ONEPASS) {
         unsigned long long base = 0;
         if (lane == 0 && c) base = atomicAdd(&a.ctl[0], (unsigned long long)c);

@@ -19,7 +19,7 @@
  *                               emqx_router:match_routes/1 (v2)   apps/emqx/src/emqx_router.erl:205-212,511-516
  *   tm_match_batch (UNIQUE)     emqx_topic_index:matches/3 ([unique])  apps/emqx/src/emqx_trie_search.erl:350-352
  *   tm_match_batch (FIRST)      emqx_topic_index:match/2 (return_first) apps/emqx/src/emqx_trie_search.erl:171-178
- *   tm_match_filter_batch       emqx_topic_index:matches_filter/3 apps/emqx/src/emqx_topic_index.erl:82-84,
+ *   tm_match_filter_batch(_runs) emqx_topic_index:matches_filter/3 apps/emqx/src/emqx_topic_index.erl:82-84,
  *                               emqx_trie_search:matches_filter/3 apps/emqx/src/emqx_trie_search.erl:186-189
  *   tm_intersect_batch          emqx_topic:intersection/2         apps/emqx/src/emqx_topic.erl:111-151
  *   tm_key_info                 emqx_topic_index:get_id/1, get_topic/1 apps/emqx/src/emqx_topic_index.erl:87-94
@@ -409,6 +409,15 @@ int tm_replica_apply_patch(tm_engine *replica, const void *patch, uint64_t bytes
  * (filter_kernels.hip) over a term-ordered copy of the word-list keys that the first call
  * after each commit builds.  Result memory as for tm_match_batch, valid until the next
  * tm_match_filter_batch / tm_commit_epoch / tm_destroy. */
+/* matches_filter/3 in runs form (ABI 9): the same walk, each query's keys as spans of the ids
+ * of the term-ordered word-list keys, in walk order.  The walk's own output is ranges of that
+ * order, so only the ranges cross PCIe (8 B each instead of 4 B per key).  mode: TM_MATCH_ALL or
+ * TM_MATCH_FIRST.  Query i: spans[span_off[i] .. + span_cnt[i]), kcnt[i] ids, status[i].  The
+ * spans point into a host copy of the ids made with the term-ordered index; it and the result
+ * stay valid, across commits too, until this thread's next tm_match_filter_batch_runs on this
+ * engine, its tm_result_release, or tm_destroy. */
+int tm_match_filter_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
+                               tm_runs_result *out);
 int tm_match_filter_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, uint32_t mode,
                           tm_result *out);
 
