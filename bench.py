@@ -33,7 +33,9 @@ import numpy as np
 # ~6 runs-form calls at 3.1 ms instead of 1.2 ms (its H2D, walk and D2H streams landed on
 # queues other streams held; profiles/r04_probe_hwq*_o.jsonl), so the bench asks for 16.
 # Set before HIP starts.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
+if os.environ.get("EMQX_BENCH_HWQ"):  # development: A/B of the queue count
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["EMQX_BENCH_HWQ"]
+elif int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 16:
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
