@@ -132,7 +132,8 @@ def batcher_load(eng, tb, to32, seconds):
     # lists in one box run, profiles/r04_batcher_threads_m.jsonl)
     dt = max(2, min(15, cpu_topology()["usable_cpus"] - 1))
     plan = [(4096, N.TM_TRANSPORT_AUTO, 0), (65536, N.TM_TRANSPORT_AUTO, 0), (262144, N.TM_TRANSPORT_AUTO, 0),
-            (65536, N.TM_TRANSPORT_AUTO, 1), (65536, N.TM_TRANSPORT_AUTO, 3), (65536, N.TM_TRANSPORT_IDS, 0)]
+            (65536, N.TM_TRANSPORT_AUTO, 1), (65536, N.TM_TRANSPORT_AUTO, 3), (65536, N.TM_TRANSPORT_IDS, 0),
+            (65536, N.TM_TRANSPORT_IDS, 3)]  # a replica's transport (no host id arena), u32 ids read in place
     warm = 0.5
     for pubs, transport, spans in plan:
         b = N.Batcher(eng, max_batch=65536, max_wait_us=200, delivery_threads=dt, transport=transport)
