@@ -1052,6 +1052,7 @@ def churn_leg(cfg, scale, batch, epochs, warmup):
     live_id = w.f_id.astype(np.uint64).copy()
     next_id = int(live_id.max()) + 1
     commit_ms, match_ms, nops, phases, full_eps = [], [], [], [], []
+    reruns = 0
 
     def pack(fs, ids):
         off = np.zeros(len(fs) + 1, dtype=np.uint64)
@@ -1088,8 +1089,18 @@ def churn_leg(cfg, scale, batch, epochs, warmup):
         e1.record(stream)
         eng.device_sync()
         torch.cuda.synchronize()
-        if _read_u64(r.d_total) > r.keys_cap:
-            raise RuntimeError("output arena overflow during churn bench")
+        got = _read_u64(r.d_total)
+        if got > r.keys_cap:
+            # the walk counts what it could not store: size the arena to it and run the batch
+            # again (the timed match is the first run; the rerun is counted in the line)
+            log(f"churn epoch {ep}: {got} matched keys > output arena {r.keys_cap} (first batch: {tot}); re-run")
+            reruns += 1
+            eng.reserve_matches(int(got * 1.25) + 1024)
+            r = eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), n, int(w.t_off[-1]), sp)
+            eng.device_sync()
+            torch.cuda.synchronize()
+            if _read_u64(r.d_total) > r.keys_cap:
+                raise RuntimeError("output arena overflow during churn bench")
         live_f = [f for f, kk in zip(live_f, keep) if kk] + add_f
         live_id = np.concatenate([live_id[keep], add_id])
         if ep >= warmup:
@@ -1127,6 +1138,7 @@ def churn_leg(cfg, scale, batch, epochs, warmup):
         "commit_ms_per_epoch": [round(x, 2) for x in commit_ms],
         "commit_phase_ms_per_epoch": [[round(x / 1e3, 2) for x in ph[:3]] for ph in phases],
         "full_rebuild_epochs": [i for i, f in enumerate(full_eps) if f],
+        "match_reruns": reruns,
         "build_s": round(t_build, 2),
         "host_peak_rss_gib": host_rss_gib(),
         "parity": {"sampled_topics": ps, "mismatches": int(bad), "oracle": "oracle/trie_search.cpp"},
