@@ -15,8 +15,13 @@ from emqx_amd import workloads  # noqa: E402
 
 
 def u64(ptr):
+    """One u64 from device memory (the batch's requested-keys counter is a device address)."""
     import ctypes as C
-    return C.c_uint64.from_address(ptr).value
+    h = (C.c_uint64 * 1)()
+    lib = C.CDLL("libamdhip64.so")
+    lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert lib.hipMemcpy(C.cast(h, C.c_void_p), C.c_void_p(ptr), 8, 2) == 0  # hipMemcpyDeviceToHost
+    return h[0]
 
 
 def run(cfg, scale):
