@@ -154,6 +154,8 @@ def test_config_e_full_size_churn_vs_oracle():
             live_id = np.concatenate([live_id[keep], add_id])
             ix = oracle.OrderedIndex.from_filters(live_f, live_id.tolist())
             _check_full_batch(eng, w, ix, 20_000 if ep == 4 else 2_000, seed=ep)
+            if ep in (0, 4):  # the index the delta left on the device == a full publish of it
+                assert eng.image_check() == [], f"epoch {ep}"
         assert eng.stats()["n_keys"] == len(live_id)
         assert "delta" in kinds  # the churn really went through delta epochs
     finally:

@@ -58,8 +58,9 @@ def _churn(eng, w, epochs, frac, seed, sample):
 
 @pytest.mark.timeout(300)
 def test_delta_index_equals_full_publish():
-    """Config E at scale 0.05 (≈ 50 K keys), 4 epochs of 3 % deletes + 3 % adds."""
-    w = workloads.generate("E", scale=0.05, n_topics=50_000)
+    """Config E at scale 0.2 (≈ 200 K keys), 4 epochs of 3 % deletes + 3 % adds: large enough
+    for every parallel phase of a commit (resolve, list builds, placement, upload gathers)."""
+    w = workloads.generate("E", scale=0.2, n_topics=50_000)
     eng = N.Engine(0, reserve_keys=w.n_keys * 2, reserve_nodes=w.n_keys * 8)
     try:
         eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
