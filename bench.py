@@ -417,6 +417,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="CPU-baseline threads (0: every CPU this process may use, see cpu_topology)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--in-flight", type=int, default=2, help="device batches in flight (1-3; --sequential: 1)")
     ap.add_argument("--sequential", action="store_true",
                     help="one batch in flight (default: two, alternating the engine's two direct buffer "
                          "sets on two streams; the sequential rate is reported beside either way)")
@@ -555,17 +556,18 @@ def main():
         sb, so, stb = slices[j]
         return eng.match_device(sb.data_ptr(), so.data_ptr(), n, stb, sp)
 
-    # the timed steps alternate the engine's two direct buffer sets on two streams
+    # the timed steps rotate over the engine's direct buffer sets, one stream each
     # (tm_match_device_set): step k+1's walk starts while step k's last waves finish
-    streams2 = [stream, torch.cuda.Stream(dev)]
+    K = max(1, min(3, args.in_flight))
+    streams2 = [stream] + [torch.cuda.Stream(dev) for _ in range(K - 1)]
 
     def step2(k):
         j = (own + k) % n_slices
         if args.sequential:
             return step(j)
         sb, so, stb = slices[j]
-        return eng.match_device_set(k % 2, sb.data_ptr(), so.data_ptr(), n, stb, N.TM_MATCH_ALL,
-                                    streams2[k % 2].cuda_stream)
+        return eng.match_device_set(k % K, sb.data_ptr(), so.data_ptr(), n, stb, N.TM_MATCH_ALL,
+                                    streams2[k % K].cuda_stream)
 
     # size the output arena from one run of every slice (overflow -> grow -> rerun)
     total = 0
@@ -581,15 +583,16 @@ def main():
     for _ in range(max(0, args.warmup - 1)):
         step()
     eng.device_sync()
-    if not args.sequential:  # size set 1 (its chunk pools, its output) the same way
-        for k in range(max(2 * n_slices, args.warmup)):
+    if not args.sequential:  # size sets 1.. (their chunk pools, their output) the same way
+        for k in range(max(K * n_slices, args.warmup)):
             step2(k)
-        eng.device_sync(0)
-        eng.device_sync(1)
-        for k in range(1, 2 * n_slices, 2):
-            r1 = step2(k)
-            eng.device_sync(1)
-            assert _read_u64(r1.d_total) <= r1.keys_cap
+        for x in range(K):
+            eng.device_sync(x)
+        for k in range(K * n_slices):
+            if k % K:
+                r1 = step2(k)
+                eng.device_sync(k % K)
+                assert _read_u64(r1.d_total) <= r1.keys_cap
     torch.cuda.synchronize()
 
     # walk statistics for the algorithmic-byte count: one untimed, counted run per slice (the
@@ -617,7 +620,7 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for k in range(args.steps):
-        sk = stream if args.sequential else streams2[k % 2]
+        sk = stream if args.sequential else streams2[k % K]
         evs[k][0].record(sk)
         step2(k)
         evs[k][1].record(sk)
@@ -816,7 +819,7 @@ def main():
                         "build_info": N.load().tm_build_info().decode()},
             "build_s": round(t_build, 2),
             "host_placement": placed,
-            "batches_in_flight": 1 if args.sequential else 2,
+            "batches_in_flight": 1 if args.sequential else K,
             "one_batch_in_flight": sequential,
             "host_peak_rss_gib": host_rss_gib(),
             "host_peak_rss_gib_max_over_ranks": round(float(rss.item()), 2),

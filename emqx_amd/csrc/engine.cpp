@@ -749,6 +749,7 @@ struct tm_engine {
     // device result.  `bb` is the set of the call in progress (under mu_dev).
     BatchBufs bb_dev, bb_batch;  // bb_batch: the batching aggregator's windows (batcher.cpp); host-form calls: HostOut::bb
     BatchBufs bb_dev2;  // tm_match_device_set(.., 1, ..): a second direct batch in flight
+    BatchBufs bb_dev3;  // tm_match_device_set(.., 2, ..): a third
     BatchBufs bb_batch2;  // the aggregator's second window set (its windows alternate sets and streams)
     BatchBufs *batch_set(uint32_t set) { return set ? &bb_batch2 : &bb_batch; }
     BatchBufs *bb = &bb_dev;
@@ -2687,6 +2688,7 @@ void tm_destroy(tm_engine *eng) {
     eng->bb_batch.release();
     eng->bb_batch2.release();
     eng->bb_dev2.release();
+    eng->bb_dev3.release();
     for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
                       &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan, &eng->fx.d_pool,
@@ -2872,7 +2874,8 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
     }
     if (eng->bb->keys_cap == 0) {
         uint64_t want = eng->cfg.reserve_matches ? eng->cfg.reserve_matches : std::max<uint64_t>(n * 8ull, 1 << 16);
-        if (eng->bb == &eng->bb_dev2) want = std::max(want, eng->bb_dev.keys_cap);  // starts at set 0's reservation
+        if (eng->bb == &eng->bb_dev2 || eng->bb == &eng->bb_dev3)
+            want = std::max(want, eng->bb_dev.keys_cap);  // starts at set 0's reservation
         TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, want * 4), TM_ENOMEM, "alloc");
         eng->bb->keys_cap = want;
     }
@@ -3406,8 +3409,8 @@ int tm_reserve_matches(tm_engine *eng, uint64_t keys_cap, uint32_t topics_cap) {
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     // the tm_match_device* path (host calls size their own output); the second direct set
     // once it is in use
-    for (BatchBufs *b : {&eng->bb_dev, &eng->bb_dev2}) {
-        if (b == &eng->bb_dev2 && !b->keys_cap) continue;
+    for (BatchBufs *b : {&eng->bb_dev, &eng->bb_dev2, &eng->bb_dev3}) {
+        if (b != &eng->bb_dev && !b->keys_cap) continue;
         eng->bb = b;
         if (keys_cap > eng->bb->keys_cap) {
             TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, keys_cap * 4), TM_ENOMEM, "alloc keys");
@@ -3468,7 +3471,7 @@ int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t 
     return eng ? match_device_impl(eng, &eng->bb_dev, d_bytes, d_off, n, total_bytes, mode, stream, out) : TM_EINVAL;
 }
 static BatchBufs *direct_set(tm_engine *eng, uint32_t set) {
-    return !eng ? nullptr : set == 0 ? &eng->bb_dev : set == 1 ? &eng->bb_dev2 : nullptr;
+    return !eng ? nullptr : set == 0 ? &eng->bb_dev : set == 1 ? &eng->bb_dev2 : set == 2 ? &eng->bb_dev3 : nullptr;
 }
 int tm_match_device_set(tm_engine *eng, uint32_t set, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                         uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out) {
