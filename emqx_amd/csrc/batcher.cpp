@@ -63,6 +63,7 @@ extern "C" void tmx_lease_take(tm_engine *eng);
 extern "C" int tmx_batch_reserve_matches(tm_engine *eng, uint32_t set, uint64_t keys_cap);
 extern "C" void tmx_lease_drop(tm_engine *eng);
 extern "C" int tmx_engine_is_replica(const tm_engine *eng);
+extern "C" int tmx_engine_runs_ok(const tm_engine *eng);
 
 namespace {
 // set on the delivery threads: the engine refuses a commit from a callback (it would wait for
@@ -1095,7 +1096,7 @@ struct tm_batcher {
                 for (HBuf *h : {&S.h_bytes, &S.h_off, &S.h_off_out, &S.h_status, &S.h_cnt, &S.h_ids, &S.h_ctl})
                     h->pinned = false;
         if (eng) {
-            runs_ok = cfg.transport != TM_TRANSPORT_IDS && !tmx_engine_is_replica(eng);
+            runs_ok = cfg.transport != TM_TRANSPORT_IDS && tmx_engine_runs_ok(eng);
             if (cfg.transport == TM_TRANSPORT_RUNS && !runs_ok) return TM_ESTATE;
             device = tmx_engine_device(eng);
             if (hipSetDevice(device) != hipSuccess ||

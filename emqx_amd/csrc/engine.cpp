@@ -617,7 +617,63 @@ struct tm_engine {
     // delivery threads: DESIGN.md §9).  Inline (single-key) spans point into key_id32.
     uint32_t *arena_id32 = nullptr;
     hvec<uint32_t> key_id32;  // by key handle
-    bool ids32() const { return arena_id32 && max_id <= 0xFFFFFFFFull; }
+    bool ids32() const { return !replica && arena_id32 && max_id <= 0xFFFFFFFFull; }
+    // A replica keeps the same host id arena (from its device copy: image loads and patches)
+    // and the id of every key handle, so its windows and host calls can answer in runs form too.
+    hvec<uint64_t> r_key_id;
+    bool r_ids = false;  // arena_id / r_key_id follow the replica's device copy
+    int replica_ids_full() {  // whole, from the device arrays (an image load, an array replaced)
+        r_ids = false;
+        if (!arena_id) return TM_OK;
+        const uint64_t nk = dev_used[A_KEY_REC] / 16, nw = dev_used[A_ARENA] / 4;
+        if (nw > arena_id_res) return TM_OK;  // past the reservation: runs stay off
+        std::vector<uint64_t> rec(2 * nk + 2);
+        std::vector<uint32_t> ar(nw + 1);
+        if (nk && hipMemcpy(rec.data(), d_key_rec.p, nk * 16, hipMemcpyDeviceToHost) != hipSuccess) return TM_EDEVICE;
+        if (nw && hipMemcpy(ar.data(), d_arena.p, nw * 4, hipMemcpyDeviceToHost) != hipSuccess) return TM_EDEVICE;
+        r_key_id.resize(nk);
+        for (uint64_t h = 0; h < nk; h++) r_key_id[h] = rec[2 * h];
+        // list headers (counts, minima) get an id too: harmless, no span covers them
+        par_for(nw, [&](size_t i) { arena_id[i] = ar[i] < nk ? r_key_id[ar[i]] : 0; });
+        r_ids = true;
+        return TM_OK;
+    }
+    // after a patch: the key records it wrote first, then the arena words it wrote
+    int replica_ids_patch(const uint8_t *p0, uint64_t n_records) {
+        if (!arena_id || !r_ids) return replica_ids_full();
+        for (int pass = 0; pass < 2; pass++) {
+            const uint8_t *p = p0;
+            for (uint64_t i = 0; i < n_records; i++) {
+                PatchRec r;
+                memcpy(&r, p, sizeof r);
+                const uint8_t *pay = p + sizeof r;
+                p += sizeof r + r.bytes;
+                if (r.arr != (pass ? A_ARENA : A_KEY_REC)) continue;
+                if (r.kind == P_WHOLE) return replica_ids_full();
+                const uint64_t el = ARR_ELEM[r.arr];
+                const uint8_t *vals = r.kind == P_SCATTER ? pay + r.count * 8 : pay;
+                for (uint64_t k = 0; k < r.count; k++) {
+                    uint64_t at = r.a + k;
+                    if (r.kind == P_SCATTER) memcpy(&at, pay + k * 8, 8);
+                    if (pass == 0) {
+                        uint64_t id;
+                        memcpy(&id, vals + k * el, 8);
+                        if (at >= r_key_id.size()) r_key_id.resize(at + 1, 0);
+                        r_key_id[at] = id;
+                    } else {
+                        if (at >= arena_id_res) {
+                            r_ids = false;  // past the reservation: runs stay off
+                            return TM_OK;
+                        }
+                        uint32_t h;
+                        memcpy(&h, vals + k * el, 4);
+                        arena_id[at] = h < r_key_id.size() ? r_key_id[h] : 0;
+                    }
+                }
+            }
+        }
+        return TM_OK;
+    }
     void ids_of(uint64_t lo, uint64_t hi) {  // refresh arena_id over key positions [lo, hi)
         if (!arena_id) return;
         if (hi > arena_id_res) {  // past the reservation: only until the compaction this forces
@@ -2945,6 +3001,11 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
             a.span_keys = eng->key_id32.empty() ? 0 : (uint64_t)(uintptr_t)&eng->key_id32[0];
             a.span_w = 4;
             a.span_kstride = 4;
+        } else if (eng->replica) {  // the replica's host copies (replica_ids_*)
+            a.span_arena = (uint64_t)(uintptr_t)eng->arena_id;
+            a.span_keys = eng->r_key_id.empty() ? 0 : (uint64_t)(uintptr_t)&eng->r_key_id[0];
+            a.span_w = 8;
+            a.span_kstride = 8;
         } else {
             a.span_arena = (uint64_t)(uintptr_t)eng->arena_id;
             a.span_keys = eng->keys.empty() ? 0 : (uint64_t)(uintptr_t)&eng->keys[0].id;
@@ -4222,6 +4283,13 @@ int tm_replica_load(tm_engine *eng, const void *d_image, uint64_t bytes, void *s
         return TM_ESTATE;
     }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    // runs results read the host id arena: no lease may be held while it is rewritten (leases
+    // come before any engine lock)
+    eng->leases_block();
+    struct Unblock {
+        tm_engine *e;
+        ~Unblock() { e->leases_unblock(); }
+    } unblock{eng};
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
     ImageHdr h;
@@ -4268,7 +4336,7 @@ int tm_replica_load(tm_engine *eng, const void *d_image, uint64_t bytes, void *s
     eng->dv.n_live = h.n_live;
     eng->dv.n_nodes = h.n_nodes;
     eng->dv.n_words = h.n_words;
-    return TM_OK;
+    return eng->replica_ids_full();
 }
 
 int tm_replica_create(const tm_config *cfg, const void *d_image, uint64_t bytes, void *stream, tm_engine **out) {
@@ -4287,7 +4355,7 @@ int tm_replica_create(const tm_config *cfg, const void *d_image, uint64_t bytes,
     hvec<uint64_t>().swap(eng->eocc);
     decltype(eng->emap)().swap(eng->emap);
     hvec<uint32_t>().swap(eng->kset);
-    eng->release_ids();
+    // the host id arena stays: the replica fills it from its device copy (runs form)
     if ((rc = tm_replica_load(eng, d_image, bytes, stream)) != TM_OK) {
         tm_destroy(eng);
         return rc;
@@ -4324,6 +4392,11 @@ int tm_replica_apply_patch(tm_engine *eng, const void *patch, uint64_t bytes) {
         eng->err = "tm_replica_apply_patch: not a replica";
         return TM_ESTATE;
     }
+    eng->leases_block();  // as tm_replica_load
+    struct Unblock {
+        tm_engine *e;
+        ~Unblock() { e->leases_unblock(); }
+    } unblock{eng};
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     PatchHdr h;
     memcpy(&h, patch, sizeof h);
@@ -4431,7 +4504,7 @@ int tm_replica_apply_patch(tm_engine *eng, const void *patch, uint64_t bytes) {
     eng->dv.n_deep = h.n_deep;
     eng->dv.max_id = h.max_id;
     eng->dv.n_live = h.n_live;
-    return TM_OK;
+    return eng->replica_ids_patch((const uint8_t *)patch + sizeof h, h.n_records);
 }
 
 // Is p host memory the device can DMA from directly (pinned / registered)?
@@ -4478,7 +4551,8 @@ static int match_runs_impl(tm_engine *eng, HostOut &o, const uint8_t *bytes, con
 
 int tm_match_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint32_t *off, uint32_t n, tm_runs_result *out) {
     if (!eng || !out || (n && (!off || (!bytes && off[n] > off[0])))) return TM_EINVAL;
-    if (eng->replica) return replica_refuses(eng, "tm_match_batch_runs (spans point into the host id arena)");
+    if (eng->replica && !eng->r_ids)
+        return replica_refuses(eng, "tm_match_batch_runs (the replica's host id arena is off)");
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
     HostOut &o = eng->out();
     eng->lease_drop(o);  // the previous result of this thread ends here
@@ -4680,7 +4754,7 @@ __attribute__((visibility("hidden"))) int tmx_batch_match_runs(tm_engine *eng, u
                                                                uint32_t *d_soff, uint32_t *d_scnt, uint32_t *d_kcnt,
                                                                int32_t *d_status, unsigned long long *d_cursor,
                                                                const void **d_ctl_out, uint32_t id_w) {
-    if (eng->replica) return TM_ESTATE;
+    if (eng->replica && !eng->r_ids) return TM_ESTATE;
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     // id_w 4: spans of the u32 id arena, while every id fits (the caller holds a lease: no
     // commit can add a wider id before the spans are used)
@@ -4722,6 +4796,10 @@ __attribute__((visibility("hidden"))) int tmx_batch_reserve_matches(tm_engine *e
 __attribute__((visibility("hidden"))) void tmx_lease_take(tm_engine *eng) { eng->lease_take_raw(); }
 __attribute__((visibility("hidden"))) void tmx_lease_drop(tm_engine *eng) { eng->lease_drop_raw(); }
 __attribute__((visibility("hidden"))) int tmx_engine_is_replica(const tm_engine *eng) { return eng->replica ? 1 : 0; }
+// the runs form on this engine: a master, or a replica that keeps its host id arena
+__attribute__((visibility("hidden"))) int tmx_engine_runs_ok(const tm_engine *eng) {
+    return !eng->replica || eng->r_ids ? 1 : 0;
+}
 
 int tm_runs_release(tm_engine *eng) {
     if (!eng) return TM_EINVAL;

@@ -261,8 +261,10 @@ int tm_match_batch(tm_engine *eng, const uint8_t *bytes, const uint32_t *off,
  * consumer reads each id once, where it builds its reply.  Zero-copy: the spans point
  * into engine memory that the calling thread holds a READ LEASE on until its next
  * tm_match_batch_runs, tm_runs_release or tm_result_release; a commit's host phase waits for
- * every lease (release promptly; a thread's own commit first ends its own lease).  Master
- * engines only (a replica keeps no host copy: TM_ESTATE). */
+ * every lease (release promptly; a thread's own commit first ends its own lease).  On a
+ * replica (round 4) the spans point into the host id arena it keeps from its device copy,
+ * rebuilt at tm_replica_load and updated by tm_replica_apply_patch, which wait for the
+ * leases the same way; so the aggregator's runs transport works on replicas too. */
 typedef struct tm_span {
     const uint64_t *ids;
     uint64_t        n;

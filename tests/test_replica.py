@@ -197,6 +197,13 @@ def _image_tensor(eng):
     return t
 
 
+def _runs_sets(eng, w):
+    """(statuses, sorted id list per topic) through the runs form (tm_match_batch_runs): spans
+    of the engine's host id arena -- on a replica, the copy it keeps from its device arrays."""
+    o, ids, kcnt, st = eng.match_runs(w.t_bytes, w.t_off)
+    return st, [sorted(ids[o[t]:o[t + 1]].tolist()) for t in range(w.n_topics)]
+
+
 def _oracle_sets(f_list, ids, w):
     ix = oracle.OrderedIndex.from_filters(f_list, ids)
     o, e, st = ix.match(w.t_bytes, w.t_off, threads=8)
@@ -250,6 +257,9 @@ def test_replica_matches_master_across_epochs_gpu():
         assert np.array_equal(ms, rs) and mids == rids, f"epoch {ep}"
         os_, oids = _oracle_sets([k[0] for k in keys], [k[1] for k in keys], w)
         assert mids == oids, f"epoch {ep}"
+        # the runs form on the replica (its host id arena follows image loads and patches)
+        rrs, rrids = _runs_sets(rep, w)
+        assert np.array_equal(rrs, ms) and [sorted(x) for x in rrids] == [sorted(x) for x in mids], f"epoch {ep}"
         assert rep.stats()["n_keys"] == len(live_keys)
     assert patches >= 2
     # a patch made from another epoch is refused; so are writes on a replica
@@ -283,6 +293,16 @@ def test_replica_matches_master_across_epochs_gpu():
     rs, rids = _sets(rep, w)
     assert mids == rids
     assert rep.stats()["n_keys"] == len(live_keys)
+    assert [sorted(x) for x in _runs_sets(rep, w)[1]] == [sorted(x) for x in mids]
+    # the aggregator on the replica answers in runs form (spans of the replica's id arena)
+    b = N.Batcher(rep, max_wait_us=200, transport=N.TM_TRANSPORT_RUNS)
+    try:
+        for t in range(0, w.n_topics, 97):
+            topic = bytes(w.t_bytes[w.t_off[t]:w.t_off[t + 1]])
+            st, ids = b.match(topic)
+            assert sorted(int(i) for i in ids) == sorted(mids[t]), t
+    finally:
+        b.close()
     rep.close()
     master.close()
 
