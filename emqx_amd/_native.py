@@ -713,8 +713,8 @@ class Engine:
 
     def match_device_set(self, dset: int, d_bytes: int, d_off: int, n: int, total_bytes: int,
                          mode: int = TM_MATCH_ALL, stream: int = 0):
-        """tm_match_device_set: the batch on direct buffer set `dset` (0 or 1), so two
-        batches can be in flight on two streams."""
+        """tm_match_device_set: the batch on direct buffer set `dset` (0, 1 or 2), so several
+        batches can be in flight on their own streams."""
         r = tm_dev_result()
         self._check(self.lib.tm_match_device_set(self.h, dset, C.c_void_p(d_bytes), C.c_void_p(d_off), n, total_bytes,
                                                  mode, C.c_void_p(stream) if stream else None, C.byref(r)))

@@ -308,7 +308,8 @@ int tm_device_sync(tm_engine *eng);
 int tm_match_device_mode(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                          uint64_t total_bytes, uint32_t mode, void *stream, tm_dev_result *out);
 /* Two device batches in flight (ABI 8).  tm_match_device_mode on direct buffer set `set`:
- * 0 is tm_match_device's own set, 1 a second one with its own scratch and output, so a
+ * 0 is tm_match_device's own set, 1 a second one (2 a third, round 4) with its own scratch
+ * and output, so a
  * caller alternating sets on two streams overlaps one batch's tail with the next batch's
  * start (a launch costs ~0.1 ms of ramp and tail at config C).  A set's
  * result stays valid until that set's next batch.  tm_device_sync_set(eng, set) is

@@ -67,8 +67,13 @@ def test_two_direct_sets_in_flight():
     eng.match_device_set(1, halves[1][0].data_ptr(), halves[1][1].data_ptr(), halves[1][2], halves[1][3])
     eng.device_sync(1)
     _check(eng, r0, *[halves[0][i] for i in (2, 4, 5, 6)])
+    # a third set (round 4): its own result, set 0's still intact
+    r2 = eng.match_device_set(2, halves[1][0].data_ptr(), halves[1][1].data_ptr(), halves[1][2], halves[1][3])
+    eng.device_sync(2)
+    _check(eng, r2, *[halves[1][i] for i in (2, 4, 5, 6)])
+    _check(eng, r0, *[halves[0][i] for i in (2, 4, 5, 6)])
     with pytest.raises(N.TMError):
-        eng.match_device_set(2, halves[0][0].data_ptr(), halves[0][1].data_ptr(), halves[0][2], halves[0][3])
+        eng.match_device_set(3, halves[0][0].data_ptr(), halves[0][1].data_ptr(), halves[0][2], halves[0][3])
     eng.close()
 
 
