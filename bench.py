@@ -115,7 +115,7 @@ def _loadgen():
     return lg
 
 
-def batcher_load(eng, tb, to32, seconds):
+def batcher_load(eng, tb, to32, seconds, plan=None):
     """End to end through the batching aggregator (include/emqx_tm_batcher.h): P concurrent
     publishers, each with one publish in flight (tools/loadgen.cpp), each publish answered
     with its own route ids on the host, every id read once by the callback (a checksum, as a
@@ -131,7 +131,7 @@ def batcher_load(eng, tb, to32, seconds):
     # a sleep): 15 delivery threads on the 16-CPU share (14: 73.8 / 15: 77.7 / 16: 77.2 M/s id
     # lists in one box run, profiles/r04_batcher_threads_m.jsonl)
     dt = max(2, min(15, cpu_topology()["usable_cpus"] - 1))
-    plan = [(4096, N.TM_TRANSPORT_AUTO, 0), (65536, N.TM_TRANSPORT_AUTO, 0), (262144, N.TM_TRANSPORT_AUTO, 0),
+    plan = plan or [(4096, N.TM_TRANSPORT_AUTO, 0), (65536, N.TM_TRANSPORT_AUTO, 0), (262144, N.TM_TRANSPORT_AUTO, 0),
             (65536, N.TM_TRANSPORT_AUTO, 1), (65536, N.TM_TRANSPORT_AUTO, 3), (65536, N.TM_TRANSPORT_IDS, 0),
             (65536, N.TM_TRANSPORT_IDS, 3)]  # a replica's transport (no host id arena), u32 ids read in place
     warm = 0.5
@@ -176,6 +176,33 @@ def batcher_load(eng, tb, to32, seconds):
                     f"rate and latency over a {seconds:g} s steady-state window after {warm:g} s of warm-up "
                     "(every publish delivered in it, tm_batcher_stats_reset / _get), checked against Little's law; "
                     "stage_busy: share of wall time each stage worked (copy and deliver: per delivery thread)"}
+
+
+def replica_batcher_leg(eng, tb, to32, seconds):
+    """The aggregator on a READ REPLICA of the index (mode 1's other ranks, §6): the master's
+    image copied into a replica on the same GPU, which keeps its own host id arena from its
+    device copy, then the 65,536-publisher rows with both transports."""
+    import torch
+
+    from emqx_amd import _native as N
+    nb = eng.image_size()
+    img = torch.empty(nb, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    eng.image_export(img.data_ptr(), nb)
+    t0 = time.perf_counter()
+    rep = N.Engine.replica_from_image(0, img.data_ptr(), nb)
+    t_load = time.perf_counter() - t0
+    del img
+    torch.cuda.empty_cache()
+    try:
+        r = batcher_load(rep, tb, to32, seconds,
+                         plan=[(65536, N.TM_TRANSPORT_AUTO, 0), (65536, N.TM_TRANSPORT_AUTO, 1),
+                               (65536, N.TM_TRANSPORT_IDS, 0)])
+    finally:
+        rep.close()
+    r["replica_load_s"] = round(t_load, 3)
+    r["image_bytes"] = nb
+    return r
 
 
 def host_runs_leg(eng, tb, to32, n, w, reps=10):
@@ -728,6 +755,8 @@ def main():
                              "bounded by PCIe D2H of the keys"}
         host_runs = host_runs_leg(eng, tb, to32, n, w)
         batcher = batcher_load(eng, tb, to32, args.batcher_seconds) if args.batcher_seconds > 0 else None
+        if batcher is not None:
+            batcher["on_replica"] = replica_batcher_leg(eng, tb, to32, args.batcher_seconds)
 
     # ---------------------------------------------------------------- CPU baseline + parity sample
     cpu = None
