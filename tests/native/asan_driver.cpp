@@ -286,6 +286,56 @@ int main() {
         ids_of(after);
         for (size_t i = 0; i < topics.size(); i++) CHECK(after[i].size() >= before[i].size());
     }
+    // big epochs (round 4): thousands of ops over thousands of distinct nodes, so every
+    // parallel phase of a commit runs on the engine's helper threads under the sanitizer
+    // (resolve, list builds, list placement, the upload's gathers; a full rebuild's too).
+    // Each exact filter's own topic must match its key (exactly once while it is live).
+    {
+        std::vector<std::string> bigf;
+        std::vector<uint64_t> bigid;
+        std::vector<char> alive;
+        uint64_t nid = 1ull << 41;
+        for (int ep = 0; ep < 5; ep++) {
+            std::vector<tm_op> ops;
+            const size_t base = bigf.size();
+            for (int i = 0; i < 6000; i++) {
+                char fb[64];
+                snprintf(fb, sizeof fb, "big/%d/n%zu/%s", i % 700, base + i, (i % 5 == 0) ? "+" : "x");
+                bigf.push_back(fb);
+                bigid.push_back(nid++);
+                alive.push_back(1);
+            }
+            for (size_t k = 0; k < bigf.size(); k++) {  // adds of this epoch, and deletes of earlier ones
+                if (k >= base) {
+                    ops.push_back(tm_op{TM_OP_ADD, 0, (const uint8_t *)bigf[k].data(), (uint32_t)bigf[k].size(), 0, bigid[k]});
+                } else if (alive[k] && (k * 2654435761u + ep) % 3 == 0) {
+                    ops.push_back(tm_op{TM_OP_DEL, 0, (const uint8_t *)bigf[k].data(), (uint32_t)bigf[k].size(), 0, bigid[k]});
+                    alive[k] = 0;
+                }
+            }
+            CHECK(tm_apply(eng, ops.data(), ops.size()) == TM_OK);
+            uint64_t ep3 = 0;
+            CHECK(tm_commit_epoch(eng, &ep3) == TM_OK);
+            std::string tb;
+            std::vector<uint32_t> to{0};
+            std::vector<size_t> which;
+            for (size_t k = 0; k < bigf.size(); k += 7) {
+                if (bigf[k].back() == '+') continue;
+                tb += bigf[k];
+                to.push_back((uint32_t)tb.size());
+                which.push_back(k);
+            }
+            tm_result res;
+            CHECK(tm_match_batch(eng, (const uint8_t *)tb.data(), to.data(), (uint32_t)which.size(), TM_MATCH_ALL, &res) ==
+                  TM_OK);
+            for (size_t i = 0; i < which.size(); i++) {
+                std::vector<uint64_t> v(res.cnt[i] + 1);
+                CHECK(tm_key_ids(eng, res.keys + res.off[i], res.cnt[i], v.data()) == TM_OK);
+                const size_t own = std::count(v.begin(), v.begin() + res.cnt[i], bigid[which[i]]);
+                CHECK(own == (alive[which[i]] ? 1u : 0u));
+            }
+        }
+    }
     // bad arguments
     CHECK(tm_apply(eng, nullptr, 1) == TM_EINVAL);
     CHECK(tm_match_batch(eng, nullptr, nullptr, 0, 7, nullptr) == TM_EINVAL);
