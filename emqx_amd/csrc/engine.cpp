@@ -1039,7 +1039,7 @@ struct tm_engine {
     bool slot_taken(uint64_t s) const { return (eocc[s >> 6] >> (s & 63)) & 1u; }
     // where the device's linear probe for (parent slot, word) ends: the first free slot
     uint64_t edge_place(uint32_t parent_dev, uint32_t word) const {
-        uint64_t s = edge_hash(parent_dev, word) & emask;
+        uint64_t s = edge_home(parent_dev, word, emask);
         while (slot_taken(s)) s = (s + 1) & emask;
         return s;
     }
@@ -2282,7 +2282,7 @@ struct tm_engine {
                 const uint32_t h = kset[key_hash(hnode[i], pkind[i], ops[i].id) & kmask];
                 if (h != NONE) __builtin_prefetch(&keys[h]);
             } else if (mword[i] != NONE) {
-                const uint64_t es = edge_hash(dev_id(hnode[i]), mword[i]) & emask;
+                const uint64_t es = edge_home(dev_id(hnode[i]), mword[i], emask);
                 __builtin_prefetch(&eocc[es >> 6]);
                 __builtin_prefetch(&kset[key_hash(pnode[i], okind[i], ops[i].id) & kmask]);
             }

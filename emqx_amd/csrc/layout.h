@@ -116,5 +116,12 @@ TM_HD uint64_t word_slot_hash(uint64_t key, uint32_t len) { return mix64(key ^ (
 TM_HD uint64_t edge_hash(uint32_t parent, uint32_t word) {
     return mix64(((uint64_t)parent << 32) | word);
 }
+// Home slot of edge (parent, word), where its linear probe starts.  A '+' edge starts right
+// after its parent's own slot: the walk reaches a node by reading that slot, so the '+' probe
+// that follows usually hits the same line in L2 instead of missing into a random one of the
+// 16 GiB table (round 4).  Every other edge, and the root's '+' edge, starts at its hash.
+TM_HD uint64_t edge_home(uint32_t parent, uint32_t word, uint64_t emask) {
+    return (word == W_PLUS && parent != ROOT_ID) ? ((uint64_t)parent + 1) & emask : edge_hash(parent, word) & emask;
+}
 
 }  // namespace tmx

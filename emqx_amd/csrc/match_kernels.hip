@@ -209,7 +209,7 @@ struct Rec {
 };
 __device__ __forceinline__ bool edge_probe(const MatchArgs &a, uint32_t parent, uint32_t word, Rec *r,
                                            uint32_t *probes) {
-    uint64_t s = edge_hash(parent, word) & a.emask;
+    uint64_t s = edge_home(parent, word, a.emask);
     for (;;) {
         const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + s);
         (*probes)++;
@@ -684,8 +684,8 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                     last[k] = has && (d + 1 == L.nlev[tl[k]]);
                     p1[k] = has && (meta & DO_LIT);
                     p2[k] = has && (meta & DO_PLUS);
-                    s1[k] = edge_hash(node[k], w[k]) & a.emask;
-                    s2[k] = edge_hash(node[k], W_PLUS) & a.emask;
+                    s1[k] = edge_home(node[k], w[k], a.emask);
+                    s2[k] = edge_home(node[k], W_PLUS, a.emask);
                     f1[k] = f2[k] = false;
                 }
                 // all 2*RPL probe chains advance together
@@ -1457,8 +1457,8 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
                     last[k] = has && (d + 1 == L.nlev[tl[k]]);
                     p1[k] = has && (meta & DO_LIT);
                     p2[k] = has && !deep && (meta & DO_PLUS);
-                    s1[k] = edge_hash(node[k], w[k]) & a.emask;
-                    s2[k] = edge_hash(node[k], W_PLUS) & a.emask;
+                    s1[k] = edge_home(node[k], w[k], a.emask);
+                    s2[k] = edge_home(node[k], W_PLUS, a.emask);
                     f1[k] = f2[k] = false;
                 }
                 for (;;) {
