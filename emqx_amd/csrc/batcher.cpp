@@ -307,7 +307,9 @@ struct tm_batcher {
     std::atomic<uint32_t> cutter_idle{0};  // 1 while the cutter sleeps on an empty queue
 
     std::mutex eng_mu;  // the cutter's enqueue vs a re-run from the completion thread
-    double spans_per_pub = 4.0;  // runs transport: spans per publish of recent windows (sizes the next)
+    // runs transport: spans per publish of recent windows (sizes the next); written by the
+    // completion thread, read by the cutter (found by ThreadSanitizer, round 4)
+    std::atomic<double> spans_per_pub{4.0};
     std::atomic<bool> reported{false};  // the first failed window is reported on stderr (once)
     void report(const char *stage, int rc) {
         if (rc >= 0 || reported.exchange(true)) return;
@@ -533,7 +535,8 @@ struct tm_batcher {
         for (HBuf *h : {&S.h_soff, &S.h_scnt, &S.h_kcnt, &S.h_status}) BT_HIP(h->ensure((size_t)n * 4 + 4));
         BT_HIP(S.h_ctl.ensure(64));
         if (!S.ev) BT_HIP(hipEventCreateWithFlags(&S.ev, EV_FLAGS));
-        const uint64_t want = std::max<uint64_t>(4096, (uint64_t)(spans_per_pub * 1.5 * n) + 1024);
+        const uint64_t want =
+            std::max<uint64_t>(4096, (uint64_t)(spans_per_pub.load(std::memory_order_relaxed) * 1.5 * n) + 1024);
         if (S.spans_cap < want) {
             BT_HIP(S.d_spans.ensure(want * 16));
             S.spans_cap = S.d_spans.cap / 16;
@@ -579,14 +582,18 @@ struct tm_batcher {
             int rc = tmx_engine_grow_pools(eng, S.set, seg, fr);
             if (rc) return rc;
             if (over) {  // more spans than the window's buffer: grow to the demand, run again
-                spans_per_pub = std::max(spans_per_pub, (double)total / std::max<uint32_t>(S.n, 1));
+                spans_per_pub.store(std::max(spans_per_pub.load(std::memory_order_relaxed),
+                                             (double)total / std::max<uint32_t>(S.n, 1)),
+                                    std::memory_order_relaxed);
                 if ((rc = enqueue(S))) return rc;
                 BT_HIP(hipEventSynchronize(S.ev));
                 total = S.h_ctl.as<uint64_t>()[0];
                 if (total > S.spans_cap) return TM_EDEVICE;
             }
         }
-        spans_per_pub = 0.9 * spans_per_pub + 0.1 * ((double)total / std::max<uint32_t>(S.n, 1));
+        spans_per_pub.store(0.9 * spans_per_pub.load(std::memory_order_relaxed) +
+                                0.1 * ((double)total / std::max<uint32_t>(S.n, 1)),
+                            std::memory_order_relaxed);
         BT_HIP(S.h_spans.ensure(total * 16 + 16));
         S.nchunk = 1;
         S.chunk_lo[0] = 0;
