@@ -120,8 +120,13 @@ TM_HD uint64_t edge_hash(uint32_t parent, uint32_t word) {
 // after its parent's own slot: the walk reaches a node by reading that slot, so the '+' probe
 // that follows usually hits the same line in L2 instead of missing into a random one of the
 // 16 GiB table (round 4).  Every other edge, and the root's '+' edge, starts at its hash.
+// TM_PLUS_NEAR=0 (a sweep variant, tools/sweep.py) hashes '+' edges like the others.
+#ifndef TM_PLUS_NEAR
+#define TM_PLUS_NEAR 1
+#endif
 TM_HD uint64_t edge_home(uint32_t parent, uint32_t word, uint64_t emask) {
-    return (word == W_PLUS && parent != ROOT_ID) ? ((uint64_t)parent + 1) & emask : edge_hash(parent, word) & emask;
+    return (TM_PLUS_NEAR && word == W_PLUS && parent != ROOT_ID) ? ((uint64_t)parent + 1) & emask
+                                                                 : edge_hash(parent, word) & emask;
 }
 
 }  // namespace tmx
