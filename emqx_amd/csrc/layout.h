@@ -116,13 +116,14 @@ TM_HD uint64_t word_slot_hash(uint64_t key, uint32_t len) { return mix64(key ^ (
 TM_HD uint64_t edge_hash(uint32_t parent, uint32_t word) {
     return mix64(((uint64_t)parent << 32) | word);
 }
-// Home slot of edge (parent, word), where its linear probe starts.  A '+' edge starts right
-// after its parent's own slot: the walk reaches a node by reading that slot, so the '+' probe
-// that follows usually hits the same line in L2 instead of missing into a random one of the
-// 16 GiB table (round 4).  Every other edge, and the root's '+' edge, starts at its hash.
-// TM_PLUS_NEAR=0 (a sweep variant, tools/sweep.py) hashes '+' edges like the others.
+// Home slot of edge (parent, word), where its linear probe starts.  TM_PLUS_NEAR=1 starts a
+// '+' edge right after its parent's own slot, so the '+' probe that follows the walk's read
+// of that slot usually hits the same L2 line: it cuts the walk's L2 misses by 8 % and its
+// HBM fetch by 11 %, yet a same-process A/B (tools/sweep.py plusnear/plushash, profiles/
+// r04_sweep_plus_aa.jsonl) times it 1 % slower -- the walk waits on round trips, not on
+// misses, and the clustering adds probes.  So every edge starts at its hash.
 #ifndef TM_PLUS_NEAR
-#define TM_PLUS_NEAR 1
+#define TM_PLUS_NEAR 0
 #endif
 TM_HD uint64_t edge_home(uint32_t parent, uint32_t word, uint64_t emask) {
     return (TM_PLUS_NEAR && word == W_PLUS && parent != ROOT_ID) ? ((uint64_t)parent + 1) & emask

@@ -65,9 +65,9 @@ VARIANTS = {
     "tb2304_f480": (["-DTM_TBCAP=2304", "-DTM_FCAP=480"], 0),
     "tb2048_f576": (["-DTM_TBCAP=2048", "-DTM_FCAP=576"], 0),
     "tb1792_f544": (["-DTM_TBCAP=1792", "-DTM_FCAP=544"], 0),
-    "plusnear": ([], 0),  # '+' edges probe from their parent's slot + 1 (the product)
-    "plushash": (["-DTM_PLUS_NEAR=0"], 0),  # '+' edges hashed like every other edge
-    "plusnear2": ([], 0),
+    "plusnear": (["-DTM_PLUS_NEAR=1"], 0),  # '+' edges probe from their parent's slot + 1
+    "plushash": (["-DTM_PLUS_NEAR=0"], 0),  # '+' edges hashed like every other edge (the product)
+    "plusnear2": (["-DTM_PLUS_NEAR=1"], 0),
     "plushash2": (["-DTM_PLUS_NEAR=0"], 0),
 }
 
