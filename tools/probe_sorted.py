@@ -9,6 +9,11 @@ Variants of the same 1 M config-C publishes:
   sortall   by the whole topic;
   sort3x    sort3, then the 64-topic wave chunks interleaved so that blocks b, b+8, b+16, ...
             (one XCD under round-robin dispatch) walk CONSECUTIVE sorted chunks.
+  xcd1/xcd2/xcd3  XCD-aware: the topics' first 1 / 2 / 3 levels are dealt to 8 groups
+            (largest prefix first, to the group with the most room), and block b takes its 64
+            topics from group b % 8 in the generator's (random) order.  Each XCD's L2 then sees
+            only its groups' subtries below that level, while every wave still walks
+            unrelated topics (no clustering, unlike the sorts).
 Prints per variant: k_match_fast ms (HIP events on its stream, mean of 10), matched keys, and
 that per-topic counts equal the original order's (permuted).
 
@@ -49,10 +54,39 @@ def level_keys(w, levels):
     return np.array(ks, dtype=object)
 
 
+def xcd_perm(keys, n, nx=8):
+    """Topic permutation for the xcdK variants (see the module doc); None if n % 64 != 0."""
+    if n % 64:
+        return None
+    _, inv, cnt = np.unique(keys, return_inverse=True, return_counts=True)
+    nw = n // 64
+    blocks = [np.arange(x, nw, nx) for x in range(nx)]
+    cap = np.array([len(b) * 64 for b in blocks], np.int64)
+    load = np.zeros(nx, np.int64)
+    assign = np.empty(len(cnt), np.int64)
+    for g in np.argsort(-cnt, kind="stable"):
+        x = int(np.argmax(cap - load))
+        assign[g] = x
+        load[x] += cnt[g]
+    xt = assign[inv.reshape(-1)]
+    lists = [np.nonzero(xt == x)[0] for x in range(nx)]
+    spill = np.concatenate([lst[cap[x]:] for x, lst in enumerate(lists)])
+    lists = [lst[:cap[x]] for x, lst in enumerate(lists)]
+    for x in range(nx):  # overflowing prefixes' tails go to the groups with room
+        need = int(cap[x] - len(lists[x]))
+        if need:
+            lists[x], spill = np.concatenate([lists[x], spill[:need]]), spill[need:]
+    perm = np.empty(n, np.int64)
+    for x in range(nx):
+        perm[(blocks[x][:, None] * 64 + np.arange(64)).reshape(-1)] = lists[x]
+    return perm, int(sum(max(0, int(l) - int(c)) for l, c in zip(load, cap)))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--variants", nargs="*", default=["orig", "sort2", "sort3", "sortall", "sort3x"])
     args = ap.parse_args()
     placement.pin_to_gpu(0)
     w = workloads.generate("C", scale=args.scale, n_topics=args.n)
@@ -63,15 +97,23 @@ def main():
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(dev)
     n = w.n_topics
+    want = set(args.variants)
     variants = {"orig": np.arange(n)}
     for name, lv in (("sort2", 2), ("sort3", 3), ("sortall", None)):
-        variants[name] = np.argsort(level_keys(w, lv), kind="stable")
-    p3 = variants["sort3"]
+        if name in want or (name == "sort3" and "sort3x" in want):
+            variants[name] = np.argsort(level_keys(w, lv), kind="stable")
     nw = (n + 63) // 64
-    if n % 64 == 0 and nw % 8 == 0:  # block b walks sorted chunk (b % 8) * (nw / 8) + b / 8
+    if "sort3x" in want and n % 64 == 0 and nw % 8 == 0:  # block b walks sorted chunk (b % 8) * (nw / 8) + b / 8
         b = np.arange(nw)
         chunk = (b % 8) * (nw // 8) + b // 8
-        variants["sort3x"] = p3.reshape(nw, 64)[chunk].reshape(-1)
+        variants["sort3x"] = variants["sort3"].reshape(nw, 64)[chunk].reshape(-1)
+    for lv in (1, 2, 3):
+        if f"xcd{lv}" in want:
+            r = xcd_perm(level_keys(w, lv), n)
+            if r is not None:
+                variants[f"xcd{lv}"] = r[0]
+                print(json.dumps({"variant": f"xcd{lv}", "spilled_topics": r[1]}), flush=True)
+    variants = {k: v for k, v in variants.items() if k in want or k == "orig"}
     base_cnt = None
     for name, perm in variants.items():
         nb, no = reorder(w, perm)
