@@ -7,10 +7,19 @@
 // resident) to 32 GiB (round 3: the config-C edge table is 16 GiB at load 1/16), 16 waves
 // per CU.
 //
+// `gather_roof contig [GiB]` allocates the table with hipExtMallocWithFlags(..,
+// hipDeviceMallocContiguous) instead of hipMalloc (round 4: does physically contiguous VRAM,
+// which lets the page tables use large fragments, relieve the address translation that the
+// walk's PMC passes show busy?).  Every line then carries "alloc": "contig".
+//
 // Build: hipcc --offload-arch=gfx950 -O3 tools/gather_roof.hip -o tools/gather_roof
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+static const char *g_alloc = "default";
 
 __device__ __forceinline__ unsigned long long mix(unsigned long long x) {
     x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
@@ -49,19 +58,28 @@ static void run(const uint4 *tab, unsigned long long bytes, unsigned *out) {
     hipEventSynchronize(e1);
     float ms;
     hipEventElapsedTime(&ms, e0, e1);
-    printf("{\"table_MiB\": %llu, \"inflight_per_lane\": %d, \"loads\": %llu, \"ms\": %.4f, \"G_loads_per_s\": %.2f, "
-           "\"GBps_at_64B\": %.0f}\n",
-           bytes >> 20, U, loads, ms, loads / (ms * 1e6), loads * 64.0 / (ms * 1e6));
+    printf("{\"alloc\": \"%s\", \"table_MiB\": %llu, \"inflight_per_lane\": %d, \"loads\": %llu, \"ms\": %.4f, "
+           "\"G_loads_per_s\": %.2f, \"GBps_at_64B\": %.0f}\n",
+           g_alloc, bytes >> 20, U, loads, ms, loads / (ms * 1e6), loads * 64.0 / (ms * 1e6));
+    fflush(stdout);
 }
 
-int main() {
-    const unsigned long long maxb = 32ull << 30;
+int main(int argc, char **argv) {
+    const bool contig = argc > 1 && !strcmp(argv[1], "contig");
+    const unsigned long long maxb = (argc > 2 ? strtoull(argv[2], nullptr, 10) : 32ull) << 30;
     uint4 *tab;
     unsigned *out;
-    if (hipMalloc(&tab, maxb) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) return 1;
+    if (contig) {
+        g_alloc = "contig";
+        if (hipExtMallocWithFlags((void **)&tab, maxb, hipDeviceMallocContiguous) != hipSuccess) return 2;
+    } else if (hipMalloc(&tab, maxb) != hipSuccess) {
+        return 1;
+    }
+    if (hipMalloc(&out, 64) != hipSuccess) return 1;
     hipMemset(tab, 1, maxb);
     for (unsigned long long b : {2ull << 20, 16ull << 20, 64ull << 20, 256ull << 20, 1ull << 30, 4ull << 30, 8ull << 30,
                                  16ull << 30, 32ull << 30}) {
+        if (b > maxb) break;
         run<1>(tab, b, out);
         run<4>(tab, b, out);
         run<8>(tab, b, out);
