@@ -117,24 +117,6 @@ struct HugeAlloc {
 template <class T>
 using hvec = std::vector<T, HugeAlloc<T>>;
 
-// EMQX_TM_DEV_CONTIG=1: device buffers of 64 MiB and more come from physically contiguous
-// VRAM (hipDeviceMallocContiguous), falling back to hipMalloc when that fails (an experiment
-// on the walk's address translation).
-static bool dev_contig() {
-    static const bool on = [] {
-        const char *e = getenv("EMQX_TM_DEV_CONTIG");
-        return e && *e == '1';
-    }();
-    return on;
-}
-static hipError_t dev_malloc(void **p, size_t bytes) {
-    if (dev_contig() && bytes >= (64ull << 20)) {
-        if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
-        (void)hipGetLastError();
-    }
-    return hipMalloc(p, bytes);
-}
-
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
@@ -144,7 +126,7 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
         size_t want = bytes ? bytes : 64;
-        hipError_t e = dev_malloc(&p, want);
+        hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
         return e;
     }
