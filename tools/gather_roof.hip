@@ -42,6 +42,52 @@ __global__ __launch_bounds__(256) void k_gather(const uint4 *tab, unsigned long 
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// The same loads, but the 64 lanes of a wave's load instruction fall into 64 / G distinct
+// 2 MiB regions (G lanes per region, random 16-B slots inside it): how much of the ceiling is
+// address translation, which lanes sharing a region share.
+template <int U>
+__global__ __launch_bounds__(256) void k_gather_grp(const uint4 *tab, unsigned long long nreg, unsigned g_shift,
+                                                    unsigned iters, unsigned seed, unsigned *out) {
+    const unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long wv = g >> 6, lane = g & 63;
+    unsigned acc = 0;
+    for (unsigned it = 0; it < iters; it++) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const unsigned long long k = (wv * iters + it) * U + u + seed;
+            const unsigned long long reg = mix(k * 64 + (lane >> g_shift)) % nreg;
+            const unsigned long long off = mix(k * 64 + lane + (1ull << 40)) & ((2ull << 20) / 16 - 1);
+            v[u] = tab[reg * ((2ull << 20) / 16) + off];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) acc += v[u].x ^ v[u].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int U>
+static void run_grp(const uint4 *tab, unsigned long long bytes, unsigned g_shift, unsigned *out) {
+    const unsigned blocks = 256 * 4, threads = 256;
+    const unsigned iters = 64 / U * 4;
+    const unsigned long long loads = (unsigned long long)blocks * threads * iters * U, nreg = bytes >> 21;
+    k_gather_grp<U><<<blocks, threads>>>(tab, nreg, g_shift, iters, 1, out);
+    (void)hipDeviceSynchronize();
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0);
+    k_gather_grp<U><<<blocks, threads>>>(tab, nreg, g_shift, iters, 7, out);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    printf("{\"alloc\": \"%s\", \"table_MiB\": %llu, \"lanes_per_2MiB_region\": %u, \"inflight_per_lane\": %d, "
+           "\"loads\": %llu, \"ms\": %.4f, \"G_loads_per_s\": %.2f}\n",
+           g_alloc, bytes >> 20, 1u << g_shift, U, loads, ms, loads / (ms * 1e6));
+    fflush(stdout);
+}
+
 template <int U>
 static void run(const uint4 *tab, unsigned long long bytes, unsigned *out) {
     const unsigned blocks = 256 * 4, threads = 256;  // 16 waves per CU
@@ -65,6 +111,8 @@ static void run(const uint4 *tab, unsigned long long bytes, unsigned *out) {
 }
 
 int main(int argc, char **argv) {
+    // `gather_roof regions [GiB]`: only the region-grouped loads, at the given table size
+    const bool regions = argc > 1 && !strcmp(argv[1], "regions");
     const bool contig = argc > 1 && !strcmp(argv[1], "contig");
     const unsigned long long maxb = (argc > 2 ? strtoull(argv[2], nullptr, 10) : 32ull) << 30;
     uint4 *tab;
@@ -76,7 +124,16 @@ int main(int argc, char **argv) {
         return 1;
     }
     if (hipMalloc(&out, 64) != hipSuccess) return 1;
-    hipMemset(tab, 1, maxb);
+    (void)hipMemset(tab, 1, maxb);
+    if (regions) {
+        for (unsigned gs = 0; gs <= 6; gs++) {
+            run_grp<1>(tab, maxb, gs, out);
+            run_grp<4>(tab, maxb, gs, out);
+        }
+        (void)hipFree(tab);
+        (void)hipFree(out);
+        return 0;
+    }
     for (unsigned long long b : {2ull << 20, 16ull << 20, 64ull << 20, 256ull << 20, 1ull << 30, 4ull << 30, 8ull << 30,
                                  16ull << 30, 32ull << 30}) {
         if (b > maxb) break;
