@@ -51,6 +51,7 @@ def shared_id(group: int, member: int) -> int:
 TM_CFG_FORCE_SLOW = 1
 TM_CFG_RECORD_PATCH = 2
 TM_CFG_FAIL_HOST_CALLS = 4
+TM_CFG_FAIL_FLUSH_ONCE = 8
 TM_RES_KEYS_OVERFLOW = 1
 TM_RES_IDS_OVERFLOW = 2
 
@@ -65,7 +66,7 @@ EXPORTS = (
     "tm_discard_staged", "tm_result_release", "tm_match_batch_runs", "tm_runs_release", "tm_build_info",
     "tm_match_ids_device", "tm_merge_shard_ids_device", "tm_debug_depth_stats", "tm_match_device_set",
     "tm_debug_image_check", "tm_match_filter_batch_runs",
-    "tm_device_sync_set",
+    "tm_device_sync_set", "tm_debug_bounds",
 )
 # every symbol include/emqx_tm_batcher.h declares
 BATCHER_EXPORTS = (
@@ -123,7 +124,7 @@ class tm_stats_t(C.Structure):
         "epoch", "n_keys", "n_nodes", "n_words", "edge_slots", "word_slots", "list_words",
         "device_bytes", "n_full_rebuilds", "n_delta_commits", "n_slow_topics",
         "commit_apply_us", "commit_lists_us", "commit_upload_us", "n_deep_keys", "n_filter_onepass",
-        "n_filter_twopass", "commit_stall_us", "n_commits_refused", "n_staged")]
+        "n_filter_twopass", "commit_stall_us", "n_commits_refused", "n_staged", "standby_bytes")]
 
 
 class tm_span(C.Structure):
@@ -216,6 +217,7 @@ def load() -> C.CDLL:
     lib.tm_debug_stats.argtypes = [C.c_void_p, C.c_int, P(C.c_uint64)]
     lib.tm_debug_depth_stats.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.tm_debug_image_check.argtypes = [C.c_void_p, P(C.c_uint32)]
+    lib.tm_debug_bounds.argtypes = [C.c_void_p, P(C.c_uint64), C.c_char_p, C.c_uint32]
     lib.tm_result_ids_device.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     lib.tm_result_ids_device_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.tm_match_ids_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
@@ -255,6 +257,20 @@ def load() -> C.CDLL:
             getattr(lib, name).restype = C.c_int
     _lib = lib
     return lib
+
+
+def debug_bounds(engine=None):
+    """tm_debug_bounds: (hits, first findings) of the bounds-checked debug build
+    (libemqx_tm_bounds.so) over the whole process -- out-of-bounds device indices, overwritten
+    canary tails, host copies past a buffer's end -- or None with the product build."""
+    lib = load()
+    hits, msg = C.c_uint64(), C.create_string_buffer(2048)
+    rc = lib.tm_debug_bounds(engine.h if engine is not None else None, C.byref(hits), msg, len(msg))
+    if rc == TM_ENOTFOUND:
+        return None
+    if rc != TM_OK:
+        raise TMError(rc, "tm_debug_bounds failed")
+    return hits.value, msg.value.decode(errors="replace")
 
 
 def build_sha() -> str:
@@ -646,6 +662,11 @@ class Engine:
         m = C.c_uint32()
         self._check(self.lib.tm_debug_image_check(self.h, C.byref(m)))
         return [n for a, n in enumerate(self.IMAGE_ARRAYS) if m.value >> a & 1]
+
+    def bounds(self):
+        """tm_debug_bounds: (hits, first findings) of the bounds-checked debug build over the
+        whole process, or None when the loaded library is the product build."""
+        return debug_bounds(self)
 
     def depth_stats(self):
         """Per walk depth (tm_debug_depth_stats): list of dicts {depth, edge_probes, cycles,

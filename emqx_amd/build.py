@@ -69,6 +69,18 @@ def build(force: bool = False, verbose: bool = True):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
+    # the bounds-checked debug build of the same sources (TM_BOUNDS=1): tests that
+    # load it set EMQX_TM_LIB to it; never the product path
+    tmb = os.path.join(HERE, "libemqx_tm_bounds.so")
+    if force or built_sha(tmb) != sha:
+        cmd = [HIPCC, "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-DTM_BOUNDS=1",
+               f'-DTM_SRC_SHA="{sha}"',
+               "-Wno-unused-function", os.path.join(CSRC, "engine.cpp"), os.path.join(CSRC, "batcher.cpp"),
+               os.path.join(CSRC, "match_kernels.hip"),
+               os.path.join(CSRC, "result_kernels.hip"), os.path.join(CSRC, "filter_kernels.hip"), "-o", tmb]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
     syn = os.path.join(HERE, "libemqx_synth.so")
     ssrc = [os.path.join(CSRC, "synth.cpp")]
     if force or not _newer(syn, ssrc):

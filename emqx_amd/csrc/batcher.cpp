@@ -70,6 +70,12 @@ namespace {
 // the read lease of the very window being delivered) and lets a callback's own runs call take
 // a lease past a waiting commit
 thread_local int tl_delivering = 0;
+// set while a delivery thread calls back a window that holds a read lease on the engine's host
+// id arena (a runs window): only then may the callback's own runs call take a lease past a
+// waiting commit -- the arena cannot change while that window's lease is held.  A window without
+// one (ids transport, other modes) gives its callbacks no such guarantee, so their runs calls
+// wait for a commit in progress like any other caller's (advisor, round 4).
+thread_local int tl_window_leased = 0;
 // On a delivery thread: the clock as deliver_range last read it (it reads it once per 16
 // callbacks), the submit time of a publish re-submitted from a callback.  A clock read costs
 // about as much as the rest of a submit; this stamp is at most 16 callbacks (a few
@@ -77,6 +83,7 @@ thread_local int tl_delivering = 0;
 thread_local uint64_t tl_clock_ns = 0;
 }  // namespace
 extern "C" __attribute__((visibility("hidden"))) int tmx_in_delivery(void) { return tl_delivering; }
+extern "C" __attribute__((visibility("hidden"))) int tmx_in_leased_delivery(void) { return tl_window_leased; }
 
 namespace {
 
@@ -794,13 +801,36 @@ struct tm_batcher {
         else reinterpret_cast<tm_match_cb>(p.fn)(p.ctx, st, nullptr, 0);
     }
 
+    // Submit -> callback-return latency, with the clock read once per 16 callbacks, AFTER them:
+    // each of the 16 is overstated by at most the callbacks that follow it in its group, never
+    // understated (round 4 read the clock before the group and left the callbacks out: advisor).
+    // The stamp taken as a group starts serves publishes its callbacks re-submit (tl_clock_ns):
+    // early, so their latency is overstated too.
+    struct LatGroup {
+        uint64_t t0[16];
+        uint32_t n = 0;
+        template <class Clock>
+        void start(const Clock &clock) {
+            if (!n) tl_clock_ns = clock();
+        }
+        template <class Clock>
+        void done(uint64_t t, bool last, LatHist &H, const Clock &clock) {
+            t0[n++] = t;
+            if (n < 16 && !last) return;
+            const uint64_t now = clock();
+            for (uint32_t k = 0; k < n; k++) H.add(now > t0[k] ? now - t0[k] : 0);
+            n = 0;
+        }
+    };
+
     void deliver_range(Slot &S, uint32_t lo, uint32_t hi, int rc, LatHist &H) {
         H.sync_gen(lat_gen.load(std::memory_order_acquire));
+        LatGroup G;
+        auto clock = [] { return now_ns(); };
         if (S.runs && rc >= 0) {
             const tm_span *spans = S.h_spans.as<tm_span>();
             const uint32_t *so = S.h_soff.as<uint32_t>(), *sc = S.h_scnt.as<uint32_t>(), *kc = S.h_kcnt.as<uint32_t>();
             const int32_t *stv = S.h_status.as<int32_t>();
-            uint64_t now = 0;
             // the id arena is read at random places (a span's start, an inline key's id): start
             // the loads of a few publishes ahead so the replies do not wait on each miss in turn
             const uint32_t PF = pf_pubs;
@@ -824,24 +854,24 @@ struct tm_batcher {
                 const Pending &p = S.pubs[i];
                 if (i + 8 < hi) __builtin_prefetch(S.pubs[i + 8].ctx);
                 if (i + PF < hi) prefetch(i + PF);
-                if (((i - lo) & 15) == 0) tl_clock_ns = now = now_ns();
-                H.add(now > p.t0 ? now - p.t0 : 0);
+                G.start(clock);
+                const uint64_t t0 = p.t0;
                 const int32_t st = stv[i];
                 if (st != TM_TOPIC_OK) reply_none(p, st);
                 else if (S.runs_w == 4) reply32(p, st, reinterpret_cast<const tm_span32 *>(spans) + so[i], sc[i], kc[i]);
                 else reply(p, st, spans + so[i], sc[i], kc[i]);
+                G.done(t0, i + 1 == hi, H, clock);
             }
             tl_clock_ns = 0;
             return;
         }
         thread_local std::vector<uint64_t> wide;  // a narrowed window's ids, one publish at a time
         const uint32_t *ids32 = S.narrow ? reinterpret_cast<const uint32_t *>(S.v.ids) : nullptr;
-        uint64_t now = 0;
         for (uint32_t i = lo; i < hi; i++) {
             const Pending &p = S.pubs[i];
             if (i + 8 < hi) __builtin_prefetch(S.pubs[i + 8].ctx);  // the caller's per-publish state
-            if (((i - lo) & 15) == 0) tl_clock_ns = now = now_ns();  // one clock read per 16 callbacks
-            H.add(now > p.t0 ? now - p.t0 : 0);
+            G.start(clock);
+            const uint64_t t0 = p.t0;
             if (rc < 0) {
                 reply_none(p, rc);
             } else if (p.kind == CB_SPANS32) {  // u32 ids: in place when they crossed as u32
@@ -877,6 +907,7 @@ struct tm_batcher {
                     reinterpret_cast<tm_match_cb>(p.fn)(p.ctx, st, ids, c);
                 }
             }
+            G.done(t0, i + 1 == hi, H, clock);
         }
         tl_clock_ns = 0;
     }
@@ -955,7 +986,9 @@ struct tm_batcher {
                 ns_copy.fetch_add(now_ns() - t0, std::memory_order_relaxed);  // waited on PCIe
             }
             const uint64_t td0 = now_ns();
+            tl_window_leased = S.leased ? 1 : 0;
             deliver_range(S, w.lo, w.hi, rc, H);
+            tl_window_leased = 0;
             ns_del.fetch_add(now_ns() - td0, std::memory_order_relaxed);
             if (S.parts_left.fetch_sub(1, std::memory_order_acq_rel) == 1) free_slot(S);
         }

@@ -26,6 +26,51 @@ constexpr int FR_CHUNK = 256;   // frontier entries per global overflow chunk (8
 // Counter block of one launch (byte offsets); the engine alternates two of them.
 constexpr uint32_t CTL_BYTES = 32, CTL_CURSOR = 0, CTL_SLOW = 8, CTL_SEG = 16, CTL_FR = 24;
 
+// ---------------------------------------------------------------------------
+// TM_BOUNDS=1: the debug build (libemqx_tm_bounds.so).  Every index the match,
+// upload and scatter kernels compute into an engine buffer goes through BI(i, cap): in the
+// debug build an index at or past the buffer's real capacity is recorded in the engine's bounds
+// record {count, source line, index, capacity} and replaced by 0, so the launch cannot fault and
+// the host reports the first offending access (tm_debug_bounds).  In the product build BI(i, cap)
+// is i.
+#ifndef TM_BOUNDS
+#define TM_BOUNDS 0
+#endif
+// the recorded source line's file: 1 match_kernels.hip, 2 result_kernels.hip, 3 filter_kernels.hip
+#ifndef TM_BND_FILE
+#define TM_BND_FILE 0
+#endif
+struct BndCaps {
+    uint64_t bytes, off, wtab, warena, word_off, etab, slot_list, arena, key_bin, key_rec;  // inputs, index
+    uint64_t out, keys, slow_list, scratch, seg_pool, wave_chunks, fr_pool, wave_info;     // outputs, scratch
+};
+#if TM_BOUNDS && defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint64_t tm_bchk(uint64_t i, uint64_t cap, uint32_t line, unsigned long long *rec) {
+    if (i < cap) return i;
+    if (rec && atomicAdd(&rec[0], 1ull) == 0) {
+        atomicExch(&rec[1], (unsigned long long)line);
+        atomicExch(&rec[2], (unsigned long long)i);
+        atomicExch(&rec[3], (unsigned long long)cap);
+    }
+    return 0;
+}
+// n elements from i (a 16-B load of bytes, a chunk of a pool): i if they all fit, else 0
+__device__ __forceinline__ uint64_t tm_bchk_n(uint64_t i, uint64_t n, uint64_t cap, uint32_t line,
+                                              unsigned long long *rec) {
+    if (i + n <= cap) return i;
+    tm_bchk(i + n - 1, cap, line, rec);  // records the last element's index
+    return 0;
+}
+#define TM_BND_WHERE ((uint32_t)(TM_BND_FILE << 24) | (uint32_t)__LINE__)
+#define BIR(i, cap, rec) ::tmx::tm_bchk((uint64_t)(i), (cap), TM_BND_WHERE, (rec))
+#define BIRN(i, n, cap, rec) ::tmx::tm_bchk_n((uint64_t)(i), (uint64_t)(n), (cap), TM_BND_WHERE, (rec))
+#else
+#define BIR(i, cap, rec) (i)
+#define BIRN(i, n, cap, rec) (i)
+#endif
+#define BI(i, capfield) BIR(i, a.cap.capfield, a.bnd)
+#define BIN(i, n, capfield) BIRN(i, n, a.cap.capfield, a.bnd)
+
 // Everything one match launch needs.  Device pointers only.
 struct MatchArgs {
     // topic batch: topic i is bytes[off[i] .. off[i+1])
@@ -94,6 +139,10 @@ struct MatchArgs {
     unsigned long long *stats;
     // optional: events recorded around k_match_fast on the launch stream
     hipEvent_t ev_fast0, ev_fast1;
+    // Real capacities (elements) of the buffers above, and the bounds record: read only by the
+    // TM_BOUNDS debug build, whose kernels check every index against them (BI() above).
+    BndCaps cap;
+    unsigned long long *bnd;
 };
 
 // Topics per wave of k_match_fast.  A wave's walk is a chain of dependent round trips
@@ -113,8 +162,11 @@ inline uint64_t match_grid(uint32_t n, uint32_t tpw) { return ((uint64_t)n + tpw
 hipError_t launch_match(const MatchArgs &a, hipStream_t stream);
 
 // Delta-epoch patches: dst[idx[i]] = src[i] (16-byte records / u32 entries).
-hipError_t launch_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n, hipStream_t stream);
-hipError_t launch_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *src, uint64_t n, hipStream_t stream);
+// dst_cap: dst's real capacity in elements, bnd: the bounds record (both read by the TM_BOUNDS build only)
+hipError_t launch_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n, hipStream_t stream,
+                            uint64_t dst_cap = ~0ull, unsigned long long *bnd = nullptr);
+hipError_t launch_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *src, uint64_t n, hipStream_t stream,
+                           uint64_t dst_cap = ~0ull, unsigned long long *bnd = nullptr);
 
 // result_kernels.hip --------------------------------------------------------
 // Exclusive scan of n u32 values (in[i * in_stride]) into out[0..n]; out[n] = total.
@@ -173,7 +225,9 @@ constexpr uint8_t KDD_SHARED = 2;  // AGGRE: the key's dest is a shared-subscrip
 hipError_t launch_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off, uint32_t *keys, uint64_t keys_cap,
                          const uint64_t *key_rec, const uint32_t *key_node, const uint8_t *key_dd, uint32_t n,
                          uint32_t *ucnt, uint32_t *scratch, uint2 *wl, uint32_t *wl_n, hipStream_t stream);
-hipError_t launch_scatter1(uint8_t *dst, const uint64_t *idx, const uint8_t *src, uint64_t n, hipStream_t stream);
-hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, hipStream_t stream);
+hipError_t launch_scatter1(uint8_t *dst, const uint64_t *idx, const uint8_t *src, uint64_t n, hipStream_t stream,
+                           uint64_t dst_cap = ~0ull, unsigned long long *bnd = nullptr);
+hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, hipStream_t stream,
+                           uint64_t dst_cap = ~0ull, unsigned long long *bnd = nullptr);
 
 }  // namespace tmx

@@ -43,8 +43,10 @@
 
 using namespace tmx;
 
-// batcher.cpp, library-internal: nonzero on an aggregator delivery thread (inside a callback)
+// batcher.cpp, library-internal: nonzero on an aggregator delivery thread (inside a callback),
+// and while that callback's window holds a read lease on the host id arena
 extern "C" int tmx_in_delivery(void);
+extern "C" int tmx_in_leased_delivery(void);
 
 namespace {
 
@@ -117,20 +119,60 @@ struct HugeAlloc {
 template <class T>
 using hvec = std::vector<T, HugeAlloc<T>>;
 
+// TM_BOUNDS=1 (debug build, libemqx_tm_bounds.so): every device buffer carries
+// a canary tail of BND_CANARY bytes past its capacity, and a registry of the live ones lets
+// tm_engine::bounds_check() find any launch that wrote past a buffer's end; the kernels check
+// their indices against the buffers' real capacities (device_api.h BI()).
+#ifndef TM_BOUNDS
+#define TM_BOUNDS 0
+#endif
+constexpr size_t BND_CANARY = TM_BOUNDS ? 4096 : 0;
+[[maybe_unused]] constexpr uint8_t BND_FILL = 0xA5;
+#if TM_BOUNDS
+// One per process (every engine's buffers, every device's bounds record, what was found): a
+// test runner checks the whole process after each test (tm_debug_bounds with a null engine).
+struct BndRegistry {
+    std::mutex m;
+    std::unordered_map<void *, size_t> live;  // pointer -> capacity (the canary follows it)
+    unsigned long long *rec[64] = {};         // per device: {count, file << 24 | line, index, capacity}
+    uint64_t hits = 0;
+    std::string msg;  // the first findings
+};
+static BndRegistry &bnd_registry() {
+    static BndRegistry *r = new BndRegistry();  // never destroyed: buffers outlive static teardown
+    return *r;
+}
+#endif
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap && p) return hipSuccess;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
+        release();
         size_t want = bytes ? bytes : 64;
-        hipError_t e = hipMalloc(&p, want);
-        if (e == hipSuccess) cap = want;
+        hipError_t e = hipMalloc(&p, want + BND_CANARY);
+        if (e == hipSuccess) {
+            cap = want;
+#if TM_BOUNDS
+            e = hipMemset(static_cast<uint8_t *>(p) + want, BND_FILL, BND_CANARY);
+            std::lock_guard<std::mutex> g(bnd_registry().m);
+            bnd_registry().live[p] = want;
+#endif
+        } else {
+            p = nullptr;
+        }
         return e;
     }
     void release() {
+#if TM_BOUNDS
+        if (p) {  // freed under the lock: a canary scan never reads a buffer being freed
+            std::lock_guard<std::mutex> g(bnd_registry().m);
+            bnd_registry().live.erase(p);
+            (void)hipFree(p);
+            p = nullptr;
+        }
+#endif
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
@@ -518,8 +560,15 @@ struct HostOut {
         for (hipEvent_t &ev : ev_h2d) ev = nullptr;
         bb.release();
         for (PinBuf *b : {&h_bytes, &h_off, &h_ctl, &h_rctl}) b->release();
-        for (PinBuf *b : {&h_outoff, &h_outcnt, &h_status, &h_keys, &f_keys, &r_off, &r_cnt, &r_kcnt, &r_status, &r_runs})
+        for (PinBuf *b : {&h_outoff, &h_outcnt, &h_status, &h_keys, &f_keys, &f_rng, &r_off, &r_cnt, &r_kcnt, &r_status,
+                          &r_runs})
             b->release();
+        std::vector<uint32_t>().swap(f_rcnt);
+        std::vector<uint32_t>().swap(fr_off);
+        std::vector<uint32_t>().swap(fr_cnt);
+        std::vector<int32_t>().swap(fr_status);
+        std::vector<tm_span>().swap(f_spans);
+        f_ids.reset();
         std::vector<uint32_t>().swap(pp_off);
         std::vector<uint32_t>().swap(pp_cnt);
         std::vector<uint32_t>().swap(pp_keys);
@@ -799,6 +848,7 @@ struct tm_engine {
     uint64_t n_deep = 0;              // live word-list keys too deep for the 64-bit order code
     DevBuf d_mrg_roff, d_mrg_tot;  // scratch of tm_merge_shards_device
     DevBuf d_stats;
+
     // Batch buffers: one set for the device-result calls (tm_match_device*, whose result the
     // engine keeps until the next such call) and one for the host-result calls (tm_match_batch*,
     // synchronous), so a host call from one thread never overwrites another thread's pending
@@ -900,6 +950,182 @@ struct tm_engine {
         return hipStreamWaitEvent(s, ev_chain, 0);
     }
 
+    // ---- TM_BOUNDS debug build
+    // elements of `elem` bytes from p to the end of the live engine buffer holding p (~0: p is
+    // not in one, e.g. a caller's tensor)
+    static uint64_t bnd_cap_of(const void *p, size_t elem) {
+#if TM_BOUNDS
+        if (!p) return 0;
+        std::lock_guard<std::mutex> g(bnd_registry().m);
+        const uint8_t *q = static_cast<const uint8_t *>(p);
+        for (const auto &kv : bnd_registry().live) {
+            const uint8_t *b = static_cast<const uint8_t *>(kv.first);
+            if (q >= b && q < b + kv.second) return (uint64_t)(b + kv.second - q) / elem;
+        }
+#else
+        (void)p;
+        (void)elem;
+#endif
+        return ~0ull;
+    }
+    // the real capacities behind a match launch's pointers (read by the bounds build's kernels)
+    void fill_caps(MatchArgs &a) const {
+        BndCaps &c = a.cap;
+        if (!TM_BOUNDS) {
+            memset(&c, 0xFF, sizeof c);
+            a.bnd = nullptr;
+            return;
+        }
+        const size_t kel = a.mode == MODE_RUNS ? 16 : a.mode == MODE_IDS64 ? 8 : 4;
+        c.bytes = bnd_cap_of(a.bytes, 1);
+        c.off = bnd_cap_of(a.off, 4);
+        c.wtab = d_wtab.cap / 16;
+        c.warena = d_warena.cap;
+        c.word_off = d_word_off.cap / 4;
+        c.etab = d_etab.cap / 16;
+        c.slot_list = d_slot_list.cap / 4;
+        c.arena = d_arena.cap / 4;
+        c.key_bin = d_key_bin.cap / 4;
+        c.key_rec = d_key_rec.cap / 8;
+        c.out = std::min(std::min(bnd_cap_of(a.out_off, 4), bnd_cap_of(a.out_cnt, 4)), bnd_cap_of(a.status, 4));
+        if (a.mode == MODE_RUNS) c.out = std::min(c.out, bnd_cap_of(a.out_kcnt, 4));
+        c.keys = bnd_cap_of(a.keys, kel);
+        c.slow_list = bnd_cap_of(a.slow_list, 4);
+        c.scratch = std::min(bnd_cap_of(a.scratch_w, 4), bnd_cap_of(a.scratch_s, 8));
+        c.seg_pool = bnd_cap_of(a.seg_pool, 16);
+        c.wave_chunks = bnd_cap_of(a.wave_chunks, 4);
+        c.fr_pool = bnd_cap_of(a.fr_pool, 8);
+        c.wave_info = a.wave_info ? bnd_cap_of(a.wave_info, 16) : 0;
+        // self-test of the bounds build (tests/test_gpu_bounds.py): pretend the edge table has
+        // one slot, so every probe past slot 0 must be recorded (and redirected to slot 0)
+        static const bool selftest = getenv("EMQX_TM_BOUNDS_SELFTEST") != nullptr;
+        if (selftest) c.etab = 1;
+        a.bnd = bnd_rec();
+    }
+    unsigned long long *bnd_rec() const {
+#if TM_BOUNDS
+        return cfg.device >= 0 && cfg.device < 64 ? bnd_registry().rec[cfg.device] : nullptr;
+#else
+        return nullptr;
+#endif
+    }
+    // the bounds build: this device's record (once per process; never freed)
+    static bool bnd_init(int device) {
+#if TM_BOUNDS
+        std::lock_guard<std::mutex> g(bnd_registry().m);
+        if (device < 0 || device >= 64) return false;
+        unsigned long long *&r = bnd_registry().rec[device];
+        if (r) return true;
+        if (hipMalloc(&r, 64) != hipSuccess || hipMemset(r, 0, 64) != hipSuccess) {
+            r = nullptr;
+            return false;
+        }
+#else
+        (void)device;
+#endif
+        return true;
+    }
+    const char *buf_name(const void *p) {
+        struct N {
+            const char *n;
+            const DevBuf *b;
+        };
+        const N main[] = {{"wtab", &d_wtab},         {"warena", &d_warena},     {"word_off", &d_word_off},
+                          {"etab", &d_etab},         {"slot_list", &d_slot_list}, {"root", &d_root},
+                          {"arena", &d_arena},       {"key_rec", &d_key_rec},   {"key_node", &d_key_node},
+                          {"key_bin", &d_key_bin},   {"key_dd", &d_key_dd},     {"sblob", &d_sblob},
+                          {"scatter_idx", &d_scatter_idx}, {"scatter_src", &d_scatter_src}, {"stats", &d_stats}};
+        for (const N &x : main)
+            if (x.b->p == p) return x.n;
+        const BatchBufs *sets[] = {&bb_dev, &bb_dev2, &bb_dev3, &bb_batch, &bb_batch2};
+        for (const BatchBufs *B : sets) {
+            const N bn[] = {{"batch.bytes", &B->d_bytes},     {"batch.off", &B->d_off},       {"batch.outoff", &B->d_outoff},
+                            {"batch.outcnt", &B->d_outcnt},   {"batch.status", &B->d_status}, {"batch.keys", &B->d_keys},
+                            {"batch.slow_list", &B->d_slow_list}, {"batch.scr_w", &B->d_scr_w}, {"batch.scr_s", &B->d_scr_s},
+                            {"batch.seg_pool", &B->d_seg_pool}, {"batch.fr_pool", &B->d_fr_pool},
+                            {"batch.wave_chunks", &B->d_wave_chunks}, {"batch.ctl", &B->d_ctl}};
+            for (const N &x : bn)
+                if (x.b->p == p) return x.n;
+        }
+        return "(other)";
+    }
+    // a host-side check of the bounds build that failed (a copy past a buffer's end)
+    void bnd_host(const char *what, const void *p, uint64_t n, uint64_t cap) {
+        char b[256];
+        snprintf(b, sizeof b, "%s: %llu bytes into buffer %s with %llu left; ", what, (unsigned long long)n, buf_name(p),
+                 (unsigned long long)cap);
+        bnd_note(b, 1);
+    }
+    static void bnd_note(const std::string &m, uint64_t hits) {
+#if TM_BOUNDS
+        fprintf(stderr, "tm bounds: %s\n", m.c_str());
+        std::lock_guard<std::mutex> g(bnd_registry().m);
+        if (bnd_registry().msg.size() < 1500) bnd_registry().msg += m;
+        bnd_registry().hits += hits;
+#else
+        (void)m;
+        (void)hits;
+#endif
+    }
+    // After work queued on s (a match, an upload, a scatter): in the bounds build, wait for it,
+    // read the kernels' bounds record and every live buffer's canary tail; what they show is
+    // kept for tm_debug_bounds and the record and canaries are reset.  No-op in the product.
+    hipError_t bnd_after(hipStream_t s, const char *what) {
+#if TM_BOUNDS
+        const hipError_t e = s ? hipStreamSynchronize(s) : hipDeviceSynchronize();
+        return e ? e : bnd_scan(cfg.device, what, this);
+#else
+        (void)s;
+        (void)what;
+        return hipSuccess;
+#endif
+    }
+    // the bounds build: device `dev`'s record and every live buffer's canary (names from `eng`)
+    static hipError_t bnd_scan(int dev, const char *what, tm_engine *eng) {
+#if TM_BOUNDS
+        hipError_t e;
+        std::string msg;
+        uint64_t hits = 0;
+        unsigned long long rec[4] = {0, 0, 0, 0};
+        unsigned long long *d_rec = dev >= 0 && dev < 64 ? bnd_registry().rec[dev] : nullptr;
+        if (d_rec && (e = hipMemcpy(rec, d_rec, sizeof rec, hipMemcpyDeviceToHost))) return e;
+        if (rec[0]) {
+            static const char *files[] = {"?", "match_kernels.hip", "result_kernels.hip", "filter_kernels.hip"};
+            char b[256];
+            snprintf(b, sizeof b, "%s: %llu out-of-bounds indices, first at %s:%llu index %llu >= capacity %llu; ", what,
+                     rec[0], files[(rec[1] >> 24) & 3], rec[1] & 0xFFFFFF, rec[2], rec[3]);
+            msg += b;
+            hits += rec[0];
+            if ((e = hipMemset(d_rec, 0, sizeof rec))) return e;
+        }
+        {
+            // under the registry lock: no buffer is freed while its canary is read
+            std::lock_guard<std::mutex> g(bnd_registry().m);
+            std::vector<uint8_t> tail(BND_CANARY);
+            for (const auto &kv : bnd_registry().live) {
+                uint8_t *t = static_cast<uint8_t *>(kv.first) + kv.second;
+                if ((e = hipMemcpy(tail.data(), t, BND_CANARY, hipMemcpyDeviceToHost))) return e;
+                for (size_t k = 0; k < BND_CANARY; k++)
+                    if (tail[k] != BND_FILL) {
+                        char b[256];
+                        snprintf(b, sizeof b, "%s: canary of buffer %s (%zu bytes) overwritten at +%zu; ", what,
+                                 eng ? eng->buf_name(kv.first) : "(buffer)", kv.second, k);
+                        msg += b;
+                        hits++;
+                        if ((e = hipMemset(t, BND_FILL, BND_CANARY))) return e;
+                        break;
+                    }
+            }
+        }
+        if (hits) bnd_note(msg, hits);
+#else
+        (void)dev;
+        (void)what;
+        (void)eng;
+#endif
+        return hipSuccess;
+    }
+
     // a batch buffer that must grow: in-flight work may still use it, so drain first
     hipError_t grow_buf(DevBuf &b, size_t bytes) {
         if (bytes <= b.cap && b.p) return hipSuccess;
@@ -910,10 +1136,11 @@ struct tm_engine {
     // ---- read leases on the host id arena (tm_match_batch_runs)
     void lease_take_raw() {
         std::unique_lock<std::mutex> lk(lease_mu);
-        // writer preference, except on an aggregator delivery thread: the window it is calling
-        // back holds a lease a waiting commit needs dropped, so waiting there would never end
-        // (the arena cannot change under it while that window's lease is held anyway)
-        if (!tmx_in_delivery()) lease_cv.wait(lk, [&] { return !lease_block; });
+        // writer preference, except on an aggregator delivery thread whose window holds a lease:
+        // a waiting commit needs that lease dropped, so waiting there would never end (and the
+        // arena cannot change under it while the lease is held).  A callback of a window without
+        // a lease waits like any caller: a commit may be changing the arena (advisor, round 4).
+        if (!tmx_in_leased_delivery()) lease_cv.wait(lk, [&] { return !lease_block; });
         n_leases++;
     }
     void lease_drop_raw() {
@@ -1813,17 +2040,83 @@ struct tm_engine {
     static hipError_t stage_to(DevBuf &d, const V &h, hipStream_t s, uint64_t *used, size_t num = 3,
                                size_t den = 2) {
         const size_t bytes = h.size() * sizeof(T);
-        hipError_t e = d.ensure(std::max<size_t>(bytes * num / den, 4096));
+        // a standby buffer that holds the array is reused as it is (no allocation beside the
+        // matches); a new one gets headroom for the delta commits that follow
+        hipError_t e = (d.p && bytes <= d.cap) ? hipSuccess : d.ensure(std::max<size_t>(bytes * num / den, 4096));
         if (e) return e;
         if (bytes && (e = hipMemcpyAsync(d.p, h.data(), bytes, hipMemcpyHostToDevice, s))) return e;
         *used = bytes;
         return hipSuccess;
     }
     uint64_t last_swap_us = 0;  // mu_dev held by the last full publish's swap (tm_stats)
+    // The standby image (round 5).  A full publish used to allocate ~20 GiB of fresh buffers
+    // (config C) beside the matches and hipFree the previous image after the swap; both stall
+    // the match path (hipFree synchronises the device: a 25 ms match on the driver's box).  Now
+    // the previous image's buffers are kept and the next full publish uploads into them; the
+    // first full publish of a sizable index also sets up a standby of the same capacities (at
+    // build time, not during a later rebuild).  Kept only while the device has room for it.
+    DevBuf standby[A_N];
+    uint64_t standby_bytes() const {
+        uint64_t b = 0;
+        for (const DevBuf &d : standby) b += d.cap;
+        return b;
+    }
+    static bool standby_wanted() {
+        static const bool on = [] {
+            const char *e = getenv("EMQX_TM_STANDBY");
+            return !(e && *e == '0');
+        }();
+        return on;
+    }
+    // room for `extra` more bytes of standby while leaving a quarter of the device free
+    static bool standby_room(uint64_t extra) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
+        return extra + tot / 4 <= fr;
+    }
+    void standby_release() {
+        for (DevBuf &d : standby) d.release();
+    }
+    // after a swap: the previous image (sb) becomes the standby, grown to the live image's
+    // capacities when the device has room (else dropped: the next full publish allocates)
+    void standby_keep(DevBuf (&sb)[A_N]) {
+        for (uint32_t a = 0; a < A_N; a++) {
+            std::swap(standby[a].p, sb[a].p);
+            std::swap(standby[a].cap, sb[a].cap);
+        }
+        for (DevBuf &d : sb) d.release();  // only non-empty if standby was not empty (never)
+        if (!standby_wanted()) {
+            standby_release();
+            return;
+        }
+        uint64_t grow = 0;
+        for (uint32_t a = 0; a < A_N; a++) {
+            const DevBuf *live = arr_buf(a);
+            if (standby[a].cap < live->cap) grow += live->cap;
+        }
+        if (!grow) return;
+        if (!standby_room(grow)) {
+            standby_release();
+            return;
+        }
+        for (uint32_t a = 0; a < A_N; a++) {
+            const DevBuf *live = arr_buf(a);
+            if (standby[a].cap < live->cap && standby[a].ensure(live->cap) != hipSuccess) {
+                (void)hipGetLastError();
+                standby_release();
+                return;
+            }
+        }
+    }
     hipError_t publish_full() {
+        drop_scatters();  // nothing a failed delta staged may replay into the buffers this frees
         patch.reset();
         patch.full = true;  // replicas reload from an image
         DevBuf sb[A_N];
+        for (uint32_t a = 0; a < A_N; a++) {  // upload into the standby image's buffers
+            std::swap(sb[a].p, standby[a].p);
+            std::swap(sb[a].cap, standby[a].cap);
+        }
         uint64_t used[A_N] = {};
         KeyArrays ka;
         key_arrays(ka);
@@ -1834,6 +2127,8 @@ struct tm_engine {
             for (DevBuf &b : sb) b.release();
             return err;
         };
+        // the edge table and slot lists: reused when the standby holds them (ensure keeps a
+        // buffer at least as large)
         // the edge table: built on the device from one record per node
         hvec<NodeImage> nim(node_parent.size() - 1);
         par_for(nim.size(), [&](size_t i) {
@@ -1846,8 +2141,9 @@ struct tm_engine {
         if ((e = sb[A_ETAB].ensure(slots * sizeof(EdgeSlot))) || (e = sb[A_SLOT_LIST].ensure(slots * 4)) ||
             (e = d_nim.ensure(std::max<size_t>(nim.size() * sizeof(NodeImage), 4096))) ||
             (nim.size() && (e = hipMemcpyAsync(d_nim.p, nim.data(), nim.size() * sizeof(NodeImage), hipMemcpyHostToDevice, s))) ||
-            (e = launch_edge_image(sb[A_ETAB].as<uint4>(), sb[A_SLOT_LIST].as<uint32_t>(), slots, d_nim.as<NodeImage>(), nim.size(), s)) ||
-            (e = hipStreamSynchronize(s))) {
+            (e = launch_edge_image(sb[A_ETAB].as<uint4>(), sb[A_SLOT_LIST].as<uint32_t>(), slots, d_nim.as<NodeImage>(), nim.size(), s,
+                                   std::min(sb[A_ETAB].cap / 16, sb[A_SLOT_LIST].cap / 4), bnd_rec())) ||
+            (e = bnd_after(s, "edge image")) || (e = hipStreamSynchronize(s))) {
             d_nim.release();
             return fail(e);
         }
@@ -1882,7 +2178,7 @@ struct tm_engine {
             set_view();
             last_swap_us = now_us() - t0;
         }
-        for (DevBuf &b : sb) b.release();  // the previous image: nothing in flight reads it
+        standby_keep(sb);  // the previous image (nothing in flight reads it) is the next standby
         return hipSuccess;
     }
 
@@ -1924,6 +2220,7 @@ struct tm_engine {
     };
     std::vector<SJob> sjobs;
     std::vector<uint8_t> sblob;
+    bool fail_flush_done = false;  // TM_CFG_FAIL_FLUSH_ONCE (test aid)
     PinBuf h_sblob;
     DevBuf d_sblob;
     size_t stage_bytes_add(const void *p, size_t bytes) {
@@ -1932,8 +2229,20 @@ struct tm_engine {
         if (bytes) memcpy(sblob.data() + at, p, bytes);
         return at;
     }
+    void drop_scatters() {
+        sjobs.clear();
+        sblob.clear();
+    }
     hipError_t flush_scatters() {
         if (sjobs.empty()) return hipSuccess;
+        struct Drop {  // whatever happens below, no job outlives this flush
+            tm_engine *e;
+            ~Drop() { e->drop_scatters(); }
+        } drop{this};
+        if ((cfg.flags & TM_CFG_FAIL_FLUSH_ONCE) && !fail_flush_done) {
+            fail_flush_done = true;
+            return hipErrorOutOfMemory;
+        }
         hipError_t e;
         const size_t bytes = sblob.size();
         if ((e = h_sblob.ensure(bytes))) return e;
@@ -1943,14 +2252,23 @@ struct tm_engine {
         const uint8_t *base = d_sblob.as<uint8_t>();
         for (const SJob &j : sjobs) {
             const uint64_t *idx = reinterpret_cast<const uint64_t *>(base + j.idx_off);
-            if (j.width == 0) e = hipMemcpyAsync(j.dst, base + j.src_off, j.n, hipMemcpyDeviceToDevice, stream);
-            else if (j.width == 16) e = launch_scatter16((uint4 *)j.dst, idx, reinterpret_cast<const uint4 *>(base + j.src_off), j.n, stream);
-            else if (j.width == 4) e = launch_scatter4((uint32_t *)j.dst, idx, reinterpret_cast<const uint32_t *>(base + j.src_off), j.n, stream);
-            else e = launch_scatter1((uint8_t *)j.dst, idx, base + j.src_off, j.n, stream);
-            if (e) return e;
+            const uint64_t cap = bnd_cap_of(j.dst, j.width ? j.width : 1);  // ~0 in the product build
+            if (j.width == 0) {
+                if (TM_BOUNDS && j.n > cap) bnd_host("delta tail copy", j.dst, j.n, cap);
+                e = hipMemcpyAsync(j.dst, base + j.src_off, j.n, hipMemcpyDeviceToDevice, stream);
+            } else if (j.width == 16) {
+                e = launch_scatter16((uint4 *)j.dst, idx, reinterpret_cast<const uint4 *>(base + j.src_off), j.n, stream, cap, bnd_rec());
+            } else if (j.width == 4) {
+                e = launch_scatter4((uint32_t *)j.dst, idx, reinterpret_cast<const uint32_t *>(base + j.src_off), j.n, stream, cap, bnd_rec());
+            } else {
+                e = launch_scatter1((uint8_t *)j.dst, idx, base + j.src_off, j.n, stream, cap, bnd_rec());
+            }
+            if (e) {
+                (void)hipStreamSynchronize(stream);  // the pinned blob may still be read by the copy
+                return e;
+            }
         }
-        sjobs.clear();
-        sblob.clear();
+        if ((e = bnd_after(stream, "delta scatters"))) return e;
         return hipStreamSynchronize(stream);  // the pinned blob is reused by the next commit
     }
 
@@ -2050,6 +2368,9 @@ struct tm_engine {
     hipError_t upload_delta() {
         hipError_t e;
         uint64_t tp = now_us();
+        // jobs a failed publish left queued point into buffers a full publish may since have
+        // freed: a delta starts from an empty queue (advisor, round 4)
+        drop_scatters();
         // phase 1
         if ((e = grow(d_warena, warena, warena_dev))) return e;
         if ((e = grow(d_word_off, word_off, word_off_dev))) return e;
@@ -2338,6 +2659,7 @@ struct tm_engine {
         if (e != hipSuccess) {
             // the device still holds the previous epoch, intact (allocations come before any
             // in-place write); the host copy has advanced: the next commit re-uploads it whole
+            drop_scatters();
             epoch--;
             need_full = true;
             patch.reset();
@@ -2695,6 +3017,10 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
         tm_destroy(eng);
         return TM_ENOMEM;
     }
+    if (!tm_engine::bnd_init(eng->cfg.device)) {
+        tm_destroy(eng);
+        return TM_EDEVICE;
+    }
     uint64_t rk = eng->cfg.reserve_keys ? eng->cfg.reserve_keys : 1024;
     uint64_t rn = eng->cfg.reserve_nodes ? eng->cfg.reserve_nodes : rk * 4;
     eng->word_rehash(1024);  // grows with the vocabulary (load <= 1/4), not with nodes
@@ -2748,12 +3074,13 @@ void tm_destroy(tm_engine *eng) {
     for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
                       &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan, &eng->fx.d_pool,
-                      &eng->fx.d_ctl, &eng->fx.d_jobs, &eng->fx.d_krec, &eng->fx.d_kend, &eng->d_ia, &eng->d_iaoff,
+                      &eng->fx.d_ctl, &eng->fx.d_jobs, &eng->fx.d_krec, &eng->fx.d_kend, &eng->fx.d_rcnt, &eng->d_ia, &eng->d_iaoff,
                       &eng->d_ib, &eng->d_iboff, &eng->d_iout, &eng->d_ilen})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,
                       &eng->d_arena, &eng->d_scatter_idx, &eng->d_scatter_src, &eng->d_stats, &eng->d_sblob})
         b->release();
+    eng->standby_release();
     eng->h_cursor.release();
     eng->h_sblob.release();
     if (eng->ev_fast0) (void)hipEventDestroy(eng->ev_fast0);
@@ -2842,9 +3169,11 @@ int tm_commit_epoch(tm_engine *eng, uint64_t *epoch_out) {
     if (!eng) return TM_EINVAL;
     if (eng->replica) return replica_refuses(eng, "tm_commit_epoch");
     if (tmx_in_delivery()) {
-        // a commit waits for every runs window's read lease, including the one whose callback
-        // this is: it would never return.  Stage with tm_apply here, commit from another thread.
-        eng->err = "tm_commit_epoch from an aggregator delivery callback (it would wait for its own window's lease)";
+        // a commit waits for every runs window's read lease: the one whose callback this is, or
+        // one queued behind it that only the delivery threads can finish -- it might never
+        // return, whatever this window's transport (include/emqx_tm_batcher.h "writes").  Stage
+        // with tm_apply here, commit from another thread.
+        eng->err = "tm_commit_epoch from an aggregator delivery callback (it could wait for a lease only a delivery thread drops)";
         return TM_ESTATE;
     }
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
@@ -3035,7 +3364,9 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.stats = eng->stats_on ? eng->d_stats.as<unsigned long long>() : nullptr;
     a.ev_fast0 = eng->timing_on ? eng->ev_fast0 : nullptr;
     a.ev_fast1 = eng->timing_on ? eng->ev_fast1 : nullptr;
-    return launch_match(a, s);
+    eng->fill_caps(a);
+    const hipError_t e = launch_match(a, s);
+    return e ? e : eng->bnd_after(s, "match");
 }
 
 // UNIQUE / AGGRE on the GPU: k_dedupe reduces the full result of the batch just enqueued
@@ -4130,6 +4461,7 @@ int tm_stats(const tm_engine *eng, tm_stats_t *out) {
     out->commit_stall_us = eng->commit_stall_us;
     out->n_commits_refused = eng->n_commits_refused;
     out->n_staged = const_cast<tm_engine *>(eng)->staged_count();
+    out->standby_bytes = eng->standby_bytes();
     return TM_OK;
 }
 
@@ -4168,6 +4500,27 @@ int tm_debug_depth_stats(tm_engine *eng, uint64_t *out64) {
 // Words, edges, slot lists, the list arena and the root are compared; the key arrays are not
 // (a freed handle's device record stays as it was after a delta, by design: nothing refers to
 // it).  The full publish stays in place.  Test aid: commits wait meanwhile.
+int tm_debug_bounds(tm_engine *eng, uint64_t *hits, char *msg, uint32_t cap) {
+    if (!hits) return TM_EINVAL;
+#if TM_BOUNDS
+    {  // the engine's device (null: device 0): wait for it, then its record and every canary
+        const int dev = eng ? eng->cfg.device : 0;
+        if (hipSetDevice(dev) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+            tm_engine::bnd_scan(dev, "tm_debug_bounds", eng) != hipSuccess)
+            return TM_EDEVICE;
+    }
+    std::lock_guard<std::mutex> g(bnd_registry().m);
+    *hits = bnd_registry().hits;
+    if (msg && cap) snprintf(msg, cap, "%s", bnd_registry().msg.c_str());
+    return TM_OK;
+#else
+    (void)eng;
+    (void)msg;
+    (void)cap;
+    return TM_ENOTFOUND;
+#endif
+}
+
 int tm_debug_image_check(tm_engine *eng, uint32_t *diff_mask) {
     if (!eng || !diff_mask || eng->replica) return TM_EINVAL;
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
@@ -4469,6 +4822,12 @@ int tm_replica_apply_patch(tm_engine *eng, const void *patch, uint64_t bytes) {
                 TM_TRY_HIP(hipMemcpyAsync(b->p, pay, r.count * el, hipMemcpyHostToDevice, s), TM_EDEVICE, "patch H2D");
             eng->dev_used[r.arr] = r.count * el;
         } else if (r.count) {
+            uint64_t top = 0;
+            for (uint64_t k = 0; k < r.count; k++) {
+                uint64_t idx;
+                memcpy(&idx, pay + k * 8, 8);
+                top = std::max(top, idx + 1);
+            }
             TM_TRY_HIP(eng->d_scatter_idx.ensure(r.count * 8), TM_ENOMEM, "alloc");
             TM_TRY_HIP(eng->d_scatter_src.ensure(r.count * el), TM_ENOMEM, "alloc");
             TM_TRY_HIP(hipMemcpyAsync(eng->d_scatter_idx.p, pay, r.count * 8, hipMemcpyHostToDevice, s), TM_EDEVICE,
@@ -4476,16 +4835,12 @@ int tm_replica_apply_patch(tm_engine *eng, const void *patch, uint64_t bytes) {
             TM_TRY_HIP(hipMemcpyAsync(eng->d_scatter_src.p, pay + r.count * 8, r.count * el, hipMemcpyHostToDevice, s),
                        TM_EDEVICE, "patch H2D");
             const uint64_t *ix = eng->d_scatter_idx.as<uint64_t>();
-            hipError_t e = el == 16  ? launch_scatter16(b->as<uint4>(), ix, eng->d_scatter_src.as<uint4>(), r.count, s)
-                           : el == 4 ? launch_scatter4(b->as<uint32_t>(), ix, eng->d_scatter_src.as<uint32_t>(), r.count, s)
-                                     : launch_scatter1(b->as<uint8_t>(), ix, eng->d_scatter_src.as<uint8_t>(), r.count, s);
+            const uint64_t cap = b->cap / el;
+            hipError_t e = el == 16  ? launch_scatter16(b->as<uint4>(), ix, eng->d_scatter_src.as<uint4>(), r.count, s, cap, eng->bnd_rec())
+                           : el == 4 ? launch_scatter4(b->as<uint32_t>(), ix, eng->d_scatter_src.as<uint32_t>(), r.count, s, cap, eng->bnd_rec())
+                                     : launch_scatter1(b->as<uint8_t>(), ix, eng->d_scatter_src.as<uint8_t>(), r.count, s, cap, eng->bnd_rec());
             TM_TRY_HIP(e, TM_EDEVICE, "patch scatter");
-            uint64_t top = 0;
-            for (uint64_t k = 0; k < r.count; k++) {
-                uint64_t idx;
-                memcpy(&idx, pay + k * 8, 8);
-                top = std::max(top, idx + 1);
-            }
+            TM_TRY_HIP(eng->bnd_after(s, "patch scatter"), TM_EDEVICE, "patch scatter");
             // a scatter past the used part (new key handles inside the capacity) extends it, so
             // an image exported from this replica carries them
             eng->dev_used[r.arr] = std::max<uint64_t>(eng->dev_used[r.arr], top * el);

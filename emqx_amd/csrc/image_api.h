@@ -20,8 +20,9 @@ struct NodeImage {
 static_assert(sizeof(NodeImage) == 24, "node image record is 24 B");
 
 // etab[0..cap) = empty slots and slot_list[0..cap) = 0, then each record written to its
-// slot (records name distinct slots).
+// slot (records name distinct slots).  buf_slots: the two buffers' real capacity in slots and
+// bnd the bounds record (read by the TM_BOUNDS build only).
 hipError_t launch_edge_image(uint4 *etab, uint32_t *slot_list, uint64_t cap, const NodeImage *nodes, uint64_t n,
-                             hipStream_t s);
+                             hipStream_t s, uint64_t buf_slots = ~0ull, unsigned long long *bnd = nullptr);
 
 }  // namespace tmx

@@ -27,6 +27,8 @@
 // No MFMA: this is a latency/gather-bound walk.
 #include <hip/hip_runtime.h>
 
+#define TM_BND_FILE 1  // device_api.h TM_BOUNDS records
+
 #include "device_api.h"
 #include "wave.h"
 
@@ -111,17 +113,17 @@ __device__ __forceinline__ void store_group(const MatchArgs &a, uint64_t dst0, u
     if constexpr (OUT == O_KEYS) {
 #pragma unroll
         for (int u = 0; u < U; u++)
-            if ((uint32_t)u < nvalid) put_key(&a.keys[dst0 + (uint64_t)u * stride], key[u]);
+            if ((uint32_t)u < nvalid) put_key(&a.keys[BI(dst0 + (uint64_t)u * stride, keys)], key[u]);
     } else {
         uint64_t id[U];
 #pragma unroll
         for (int u = 0; u < U; u++)
-            if ((uint32_t)u < nvalid) id[u] = a.key_rec[2ull * key[u]];
+            if ((uint32_t)u < nvalid) id[u] = a.key_rec[BI(2ull * key[u], key_rec)];
 #pragma unroll
         for (int u = 0; u < U; u++)
             if ((uint32_t)u < nvalid) {
-                if constexpr (OUT == O_IDS32) put_id32(&a.keys[dst0 + (uint64_t)u * stride], (uint32_t)id[u]);
-                else put_id64(reinterpret_cast<uint64_t *>(a.keys) + dst0 + (uint64_t)u * stride, id[u]);
+                if constexpr (OUT == O_IDS32) put_id32(&a.keys[BI(dst0 + (uint64_t)u * stride, keys)], (uint32_t)id[u]);
+                else put_id64(reinterpret_cast<uint64_t *>(a.keys) + BI(dst0 + (uint64_t)u * stride, keys), id[u]);
             }
     }
 }
@@ -172,12 +174,12 @@ __device__ __forceinline__ uint32_t word_lookup(const MatchArgs &a, uint64_t key
     const uint32_t tag = len > 8 ? (len | W_LONG) : len;
     uint64_t s = word_slot_hash(key, tag) & a.wmask;
     for (;;) {
-        const uint4 x = *reinterpret_cast<const uint4 *>(a.wtab + s);
+        const uint4 x = *reinterpret_cast<const uint4 *>(a.wtab + BI(s, wtab));
         (*probes)++;
         if (x.w == NONE) return NONE;
         if (x.z == tag && x.x == (uint32_t)key && x.y == (uint32_t)(key >> 32)) {
             if (len <= 8) return x.w;
-            const uint8_t *w = a.warena + a.word_off[x.w];
+            const uint8_t *w = a.warena + BIN(a.word_off[BI(x.w, word_off)], len, warena);
             bool eq = true;
             for (uint32_t i = 0; i < len && eq; i++) eq = byte_at(st + i) == w[i];
             if (eq) return x.w;
@@ -211,7 +213,7 @@ __device__ __forceinline__ bool edge_probe(const MatchArgs &a, uint32_t parent, 
                                            uint32_t *probes) {
     uint64_t s = edge_home(parent, word, a.emask);
     for (;;) {
-        const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + s);
+        const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + BI(s, etab));
         (*probes)++;
         if (x.x == NONE) return false;
         if (x.x == parent && x.y == word) {
@@ -255,7 +257,7 @@ __device__ __forceinline__ uint32_t probes_needed(uint32_t info, uint32_t bloom,
                 if (len == 1 && (key[l] == '+' || key[l] == '#') && !a.topic_words) badarg = true;                    \
                 tag[l] = len > 8 ? (len | W_LONG) : len;                                            \
                 sl[l] = word_slot_hash(key[l], tag[l]) & a.wmask;                                   \
-                x[l] = *reinterpret_cast<const uint4 *>(a.wtab + sl[l]);                            \
+                x[l] = *reinterpret_cast<const uint4 *>(a.wtab + BI(sl[l], wtab));                  \
                 (PROBES)++;                                                                         \
                 nl++;                                                                               \
                 i++;                                                                                \
@@ -275,7 +277,7 @@ __device__ __forceinline__ uint32_t probes_needed(uint32_t info, uint32_t bloom,
                         widr[l] = y.w;                                                              \
                         break;                                                                      \
                     }                                                                               \
-                    const uint8_t *w = a.warena + a.word_off[y.w];                                  \
+                    const uint8_t *w = a.warena + BIN(a.word_off[BI(y.w, word_off)], len, warena);  \
                     bool eq = true;                                                                 \
                     for (uint32_t k = 0; k < len && eq; k++) eq = byte_at(wst[l] + k) == w[k];      \
                     if (eq) {                                                                       \
@@ -284,7 +286,7 @@ __device__ __forceinline__ uint32_t probes_needed(uint32_t info, uint32_t bloom,
                     }                                                                               \
                 }                                                                                   \
                 sl[l] = (sl[l] + 1) & a.wmask;                                                      \
-                y = *reinterpret_cast<const uint4 *>(a.wtab + sl[l]);                               \
+                y = *reinterpret_cast<const uint4 *>(a.wtab + BI(sl[l], wtab));                     \
                 (PROBES)++;                                                                         \
             }                                                                                       \
         }                                                                                           \
@@ -353,7 +355,7 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
         if (j < ns) {
             g = L.seg[j];
             if (g.w & SEG_NODE) {  // M_CNT list: its offset is read now, off the walk
-                g.x = a.slot_list[g.x] + (g.w >> SEG_SKIP_SHIFT);
+                g.x = a.slot_list[BI(g.x, slot_list)] + (g.w >> SEG_SKIP_SHIFT);
                 g.w &= 0xFFu | SEG_INLINE;
                 L.seg[j] = g;
             }
@@ -364,7 +366,7 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
             const uint32_t dst = L.tbase[g.w & 0xFFu] + g.z;
             if (g.w & SEG_INLINE) {
                 if constexpr (OUT == O_KEYS) {
-                    put_key(&a.keys[dst], g.x);
+                    put_key(&a.keys[BI(dst, keys)], g.x);
                 } else {
                     const uint32_t one[1] = {g.x};
                     store_group<OUT, 1>(a, dst, 1, one, 1);
@@ -373,11 +375,11 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
                 uint32_t key[CP_SHORT];
 #pragma unroll
                 for (int k = 0; k < CP_SHORT; k++)
-                    if ((uint32_t)k < g.y) key[k] = a.arena[g.x + k];
+                    if ((uint32_t)k < g.y) key[k] = a.arena[BI(g.x + k, arena)];
                 if constexpr (OUT == O_KEYS) {
 #pragma unroll
                     for (int k = 0; k < CP_SHORT; k++)
-                        if ((uint32_t)k < g.y) put_key(&a.keys[dst + k], key[k]);
+                        if ((uint32_t)k < g.y) put_key(&a.keys[BI(dst + k, keys)], key[k]);
                 } else {
                     store_group<OUT, CP_SHORT>(a, dst, 1, key, g.y);
                 }
@@ -417,13 +419,13 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
 #pragma unroll
                     for (int u = 0; u < CP_UNROLL; u++) {
                         const uint32_t k = k0 + u * GRP;
-                        if (k < g.y) key[u] = a.arena[g.x + k];
+                        if (k < g.y) key[u] = a.arena[BI(g.x + k, arena)];
                     }
                     if constexpr (OUT == O_KEYS) {
 #pragma unroll
                         for (int u = 0; u < CP_UNROLL; u++) {
                             const uint32_t k = k0 + u * GRP;
-                            if (k < g.y) put_key(&a.keys[dst + k], key[u]);
+                            if (k < g.y) put_key(&a.keys[BI(dst + k, keys)], key[u]);
                         }
                     } else {  // keys k0, k0 + GRP, ... are valid while below g.y
                         store_group<OUT, CP_UNROLL>(a, (uint64_t)dst + k0, GRP, key, (g.y - k0 + GRP - 1) / GRP);
@@ -446,13 +448,13 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
 #pragma unroll
             for (int u = 0; u < CP_UNROLL; u++) {
                 const uint32_t k = k0 + u * WAVE;
-                if (k < g.y) key[u] = a.arena[g.x + k];
+                if (k < g.y) key[u] = a.arena[BI(g.x + k, arena)];
             }
             if constexpr (OUT == O_KEYS) {
 #pragma unroll
                 for (int u = 0; u < CP_UNROLL; u++) {
                     const uint32_t k = k0 + u * WAVE;
-                    if (k < g.y) put_key(&a.keys[dst + k], key[u]);
+                    if (k < g.y) put_key(&a.keys[BI(dst + k, keys)], key[u]);
                 }
             } else {
                 store_group<OUT, CP_UNROLL>(a, (uint64_t)dst + k0, WAVE, key, (g.y - k0 + WAVE - 1) / WAVE);
@@ -473,10 +475,10 @@ __device__ __forceinline__ void emit_spans(const MatchArgs &a, const WaveLds &L,
         if (g.w & SEG_INLINE) {
             p = a.span_keys + (uint64_t)a.span_kstride * g.x;
         } else {
-            const uint32_t src = (g.w & SEG_NODE) ? a.slot_list[g.x] + (g.w >> SEG_SKIP_SHIFT) : g.x;
+            const uint32_t src = (g.w & SEG_NODE) ? a.slot_list[BI(g.x, slot_list)] + (g.w >> SEG_SKIP_SHIFT) : g.x;
             p = a.span_arena + (uint64_t)a.span_w * src;
         }
-        spans[L.tbase[g.w & 0x3Fu] + g.z] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), g.y, 0u);
+        spans[BI(L.tbase[g.w & 0x3Fu] + g.z, keys)] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), g.y, 0u);
     }
 }
 
@@ -484,7 +486,7 @@ template <bool STATS, int OUT>
 __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) {
     constexpr bool RUNS = OUT == O_RUNS;
     __shared__ WaveLds L;
-    uint32_t *const wchunks = a.wave_chunks + (uint64_t)blockIdx.x * MAXCHUNK;  // this wave's flushed chunks
+    uint32_t *const wchunks = a.wave_chunks + BIN((uint64_t)blockIdx.x * MAXCHUNK, MAXCHUNK, wave_chunks);  // this wave's flushed chunks
     const uint32_t lane = lane_id();
     const uint32_t t = blockIdx.x * a.tpw + lane;
     const bool active = lane < a.tpw && t < a.n;
@@ -497,20 +499,20 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
 
     // ---- 0. stage the wave's topic bytes in LDS with 16-B coalesced loads
     const uint32_t t0 = blockIdx.x * a.tpw;
-    const uint32_t wb0 = a.off[t0], wb1 = a.off[min(t0 + a.tpw, a.n)];
+    const uint32_t wb0 = a.off[BI(t0, off)], wb1 = a.off[BI(min(t0 + a.tpw, a.n), off)];
     const uint32_t tbase = wb0 & ~15u;
     const bool staged = ((reinterpret_cast<uintptr_t>(a.bytes) & 15u) == 0) && (wb1 - tbase <= (uint32_t)TBCAP);
     if (staged) {
         for (uint32_t j = lane * 16; tbase + j < wb1; j += WAVE * 16) {
             if (tbase + j + 16 <= wb1) {
-                *reinterpret_cast<uint4 *>(&L.tb[j]) = *reinterpret_cast<const uint4 *>(a.bytes + tbase + j);
+                *reinterpret_cast<uint4 *>(&L.tb[j]) = *reinterpret_cast<const uint4 *>(a.bytes + BIN(tbase + j, 16, bytes));
             } else {
-                for (uint32_t k = 0; tbase + j + k < wb1; k++) L.tb[j + k] = a.bytes[tbase + j + k];
+                for (uint32_t k = 0; tbase + j + k < wb1; k++) L.tb[j + k] = a.bytes[BI(tbase + j + k, bytes)];
             }
         }
         __syncthreads();
     }
-    auto byte_at = [&](uint32_t i) -> uint8_t { return staged ? L.tb[i - tbase] : a.bytes[i]; };
+    auto byte_at = [&](uint32_t i) -> uint8_t { return staged ? L.tb[i - tbase] : a.bytes[BI(i, bytes)]; };
 
     // ---- 1. pre-scan (lane = topic): levels, badarg, '$'
     bool badarg = false, dollar = false;
@@ -519,15 +521,15 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     uint32_t widr[TM_PRELOOK];  // word ids of the first TM_PRELOOK levels
     uint32_t pre_b = 0;         // byte where level TM_PRELOOK starts
     if (active) {
-        b = a.off[t];
-        e = a.off[t + 1];
+        b = a.off[BI(t, off)];
+        e = a.off[BI(t + 1, off)];
         dollar = (e > b) && byte_at(b) == '$';
         TM_PRESCAN_PRELOOK(st_wprobe);
     }
 #else
     if (active) {
-        b = a.off[t];
-        e = a.off[t + 1];
+        b = a.off[BI(t, off)];
+        e = a.off[BI(t + 1, off)];
         dollar = (e > b) && byte_at(b) == '$';
         uint32_t st = b;
         for (uint32_t i = b;; ++i) {
@@ -627,7 +629,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
             meta = L.fr_meta[lvl][i];
         } else {
             const uint32_t k = i - FCAP;
-            const uint2 v = a.fr_pool[(uint64_t)L.fch[lvl][k / FCH] * FCH + k % FCH];
+            const uint2 v = a.fr_pool[BI((uint64_t)L.fch[lvl][k / FCH] * FCH + k % FCH, fr_pool)];
             node = v.x;
             meta = v.y;
         }
@@ -638,7 +640,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
             L.fr_meta[lvl][i] = (uint8_t)meta;
         } else {
             const uint32_t k = i - FCAP;
-            a.fr_pool[(uint64_t)L.fch[lvl][k / FCH] * FCH + k % FCH] = make_uint2(node, meta);
+            a.fr_pool[BI((uint64_t)L.fch[lvl][k / FCH] * FCH + k % FCH, fr_pool)] = make_uint2(node, meta);
         }
     };
 
@@ -711,8 +713,8 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                         } else
 #endif
                         {
-                        x1[k] = p1[k] ? *reinterpret_cast<const uint4 *>(a.etab + s1[k]) : make_uint4(NONE, 0, 0, 0);
-                        x2[k] = p2[k] ? *reinterpret_cast<const uint4 *>(a.etab + s2[k]) : make_uint4(NONE, 0, 0, 0);
+                        x1[k] = p1[k] ? *reinterpret_cast<const uint4 *>(a.etab + BI(s1[k], etab)) : make_uint4(NONE, 0, 0, 0);
+                        x2[k] = p2[k] ? *reinterpret_cast<const uint4 *>(a.etab + BI(s2[k], etab)) : make_uint4(NONE, 0, 0, 0);
                         }
                         st_probe += (uint32_t)p1[k] + (uint32_t)p2[k];
                         if constexpr (STATS) dp_probe += (uint32_t)p1[k] + (uint32_t)p2[k];
@@ -765,7 +767,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                 if (lane == 0) c = (uint32_t)atomicAdd(a.seg_cursor, 1ull);
                 c = __shfl(c, 0, WAVE);
                 if (c < a.seg_chunks && nchunk < (uint32_t)MAXCHUNK) {
-                    uint4 *dst = a.seg_pool + (uint64_t)c * SCAP;
+                    uint4 *dst = a.seg_pool + BIN((uint64_t)c * SCAP, SCAP, seg_pool);
                     for (uint32_t j = lane; j < (uint32_t)SCAP; j += WAVE)
                         dst[j] = j < nseg ? L.seg[j] : make_uint4(0u, 0u, 0u, 0u);
                     if (lane == 0) wchunks[nchunk] = c;
@@ -793,7 +795,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                 if (dok) {
                     for (uint32_t j = lane; j < ndc; j += WAVE) wchunks[nchunk + j] = dc0 + j;
                     for (uint32_t j = tot_s + lane; j < ndc * SCAP; j += WAVE)  // pad the last chunk
-                        a.seg_pool[(uint64_t)dc0 * SCAP + j] = make_uint4(0u, 0u, 0u, 0u);
+                        a.seg_pool[BI((uint64_t)dc0 * SCAP + j, seg_pool)] = make_uint4(0u, 0u, 0u, 0u);
                     nchunk += ndc;
                     st_flush += ndc;
                 }
@@ -815,7 +817,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                         }
                         const uint4 g = make_uint4(src, cnt, rel, tl[k] | fl2);
                         if (!direct) L.seg[ps] = g;
-                        else if (dok) a.seg_pool[(uint64_t)dc0 * SCAP + ps] = g;
+                        else if (dok) a.seg_pool[BI((uint64_t)dc0 * SCAP + ps, seg_pool)] = g;
                         else atomicOr(&L.spill, 1ull << tl[k]);  // pool exhausted: topic spills
                         ps++;
                     };
@@ -835,8 +837,8 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                             if (last[k] && tc) put(r.child, tc, SEG_NODE);
                             if (hc) put(r.child, hc, SEG_NODE | (tc << SEG_SKIP_SHIFT));
                         } else if (m == M_REC) {
-                            const uint32_t lo = a.slot_list[r.child];
-                            const uint32_t tc = a.arena[lo - 2], hc = a.arena[lo - 1];
+                            const uint32_t lo = a.slot_list[BI(r.child, slot_list)];
+                            const uint32_t tc = a.arena[BI(lo - 2, arena)], hc = a.arena[BI(lo - 1, arena)];
                             st_rec++;
                             put(lo, last[k] ? tc : 0u, 0u);
                             put(lo + tc, hc, 0u);
@@ -940,14 +942,14 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     const bool overflow = gb + total > a.keys_cap;
     L.tbase[lane] = (uint32_t)(gb + excl);
     if (active) {
-        a.status[t] = badarg ? 1 : 0;
-        a.out_off[t] = spill ? 0u : (uint32_t)(gb + excl);
-        a.out_cnt[t] = my;
-        if constexpr (RUNS) a.out_kcnt[t] = my_keys;
+        a.status[BI(t, out)] = badarg ? 1 : 0;
+        a.out_off[BI(t, out)] = spill ? 0u : (uint32_t)(gb + excl);
+        a.out_cnt[BI(t, out)] = my;
+        if constexpr (RUNS) a.out_kcnt[BI(t, out)] = my_keys;
     }
     if constexpr (OUT == O_IDS32 || OUT == O_IDS64) {
         const bool any_spill = __ballot(spill) != 0;
-        if (lane == 0) a.wave_info[blockIdx.x] = make_uint4((uint32_t)gb, total, any_spill ? 1u : 0u, 0u);
+        if (lane == 0) a.wave_info[BI(blockIdx.x, wave_info)] = make_uint4((uint32_t)gb, total, any_spill ? 1u : 0u, 0u);
     }
     {
         uint32_t tot_sp;
@@ -955,7 +957,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
         uint32_t sb = 0;
         if (lane == 0 && tot_sp) sb = atomicAdd(a.slow_count, tot_sp);
         sb = __shfl(sb, 0, WAVE);
-        if (spill) a.slow_list[sb + ps] = t;
+        if (spill) a.slow_list[BI(sb + ps, slow_list)] = t;
     }
     __syncthreads();
 
@@ -963,12 +965,13 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     if constexpr (RUNS) {
         if (!overflow && total) {
             emit_spans(a, L, L.seg, nseg);
-            for (uint32_t c = 0; c < nchunk; ++c) emit_spans(a, L, a.seg_pool + (uint64_t)wchunks[c] * SCAP, SCAP);
+            for (uint32_t c = 0; c < nchunk; ++c)
+                emit_spans(a, L, a.seg_pool + BIN((uint64_t)wchunks[c] * SCAP, SCAP, seg_pool), SCAP);
         }
     } else if (!overflow && total && (OUT != O_KEYS || a.mode == MODE_ALL)) {
         expand_segments<OUT>(a, L, nseg);
         for (uint32_t c = 0; c < nchunk; ++c) {
-            const uint4 *src = a.seg_pool + (uint64_t)wchunks[c] * SCAP;
+            const uint4 *src = a.seg_pool + BIN((uint64_t)wchunks[c] * SCAP, SCAP, seg_pool);
             for (uint32_t j = lane; j < (uint32_t)SCAP; j += WAVE) L.seg[j] = src[j];
             __syncthreads();
             expand_segments<OUT>(a, L, SCAP);
@@ -1019,19 +1022,20 @@ constexpr uint64_t ROOT_MARK = (1ull << 40) - 1;
 __device__ __forceinline__ void out_key(const MatchArgs &a, uint64_t i, uint32_t key) {
     if (a.mode == MODE_RUNS) {
         const uint64_t p = a.span_keys + (uint64_t)a.span_kstride * key;
-        reinterpret_cast<uint4 *>(a.keys)[i] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), 1u, 0u);
+        reinterpret_cast<uint4 *>(a.keys)[BI(i, keys)] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), 1u, 0u);
     } else if (a.mode == MODE_IDS32) {
-        a.keys[i] = (uint32_t)a.key_rec[2ull * key];
+        a.keys[BI(i, keys)] = (uint32_t)a.key_rec[BI(2ull * key, key_rec)];
     } else if (a.mode == MODE_IDS64) {
-        reinterpret_cast<uint64_t *>(a.keys)[i] = a.key_rec[2ull * key];
+        reinterpret_cast<uint64_t *>(a.keys)[BI(i, keys)] = a.key_rec[BI(2ull * key, key_rec)];
     } else {
-        a.keys[i] = key;
+        a.keys[BI(i, keys)] = key;
     }
 }
 
 template <bool WRITE>
 __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_t *wid, uint64_t *stk, uint32_t nl,
-                             bool dollar, uint64_t out, uint32_t *probes, uint32_t *visits) {
+                             bool dollar, uint64_t out, uint32_t *probes, uint32_t *visits, uint32_t stk_cap) {
+    (void)stk_cap;  // the stack's entries (len + 2), checked by the TM_BOUNDS build
     uint32_t sp = 0, count = 0;
     stk[sp++] = ROOT_MARK << 24;
     while (sp) {
@@ -1046,15 +1050,15 @@ __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_
             lo = R.list_off;
             hc = dollar ? 0 : R.hash_cnt;
         } else {
-            const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + slot);
+            const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + BI(slot, etab));
             node = (uint32_t)slot;
             bloom = x.z;
             info = x.w;
             const uint32_t m = info_mode(info);
             if (m == M_REC || m == M_CNT) {
-                lo = a.slot_list[node];
-                tc = a.arena[lo - 2];
-                hc = a.arena[lo - 1];
+                lo = a.slot_list[BI(node, slot_list)];
+                tc = a.arena[BI(lo - 2, arena)];
+                hc = a.arena[BI(lo - 1, arena)];
             } else if (m == M_INLINE && ((info & I_INL_HASH) || d == nl)) {
                 // the node's only key, inline in the slot
                 if (WRITE) out_key(a, out + count, info & I_KEY_MASK);
@@ -1064,18 +1068,20 @@ __device__ uint32_t dfs_walk(const MatchArgs &a, const RootRec &R, const uint32_
         (*visits)++;
         // "P/#" keys match at P and below
         if (WRITE)
-            for (uint32_t k = 0; k < hc; k++) out_key(a, out + count + k, a.arena[lo + tc + k]);
+            for (uint32_t k = 0; k < hc; k++) out_key(a, out + count + k, a.arena[BI(lo + tc + k, arena)]);
         count += hc;
         if (d == nl) {
             if (WRITE)
-                for (uint32_t k = 0; k < tc; k++) out_key(a, out + count + k, a.arena[lo + k]);
+                for (uint32_t k = 0; k < tc; k++) out_key(a, out + count + k, a.arena[BI(lo + k, arena)]);
             count += tc;
             continue;
         }
         const uint32_t need = probes_needed(info, bloom, wid[d]);
         Rec r;
-        if ((need & DO_PLUS) && edge_probe(a, node, W_PLUS, &r, probes)) stk[sp++] = ((uint64_t)r.child << 24) | (d + 1);
-        if ((need & DO_LIT) && edge_probe(a, node, wid[d], &r, probes)) stk[sp++] = ((uint64_t)r.child << 24) | (d + 1);
+        if ((need & DO_PLUS) && edge_probe(a, node, W_PLUS, &r, probes))
+            stk[BIR(sp++, stk_cap, a.bnd)] = ((uint64_t)r.child << 24) | (d + 1);
+        if ((need & DO_LIT) && edge_probe(a, node, wid[d], &r, probes))
+            stk[BIR(sp++, stk_cap, a.bnd)] = ((uint64_t)r.child << 24) | (d + 1);
     }
     return count;
 }
@@ -1086,31 +1092,32 @@ __global__ __launch_bounds__(WAVE) void k_match_slow(MatchArgs a) {
     const RootRec R = *a.root;
     uint32_t st_visit = 0, st_probe = 0, st_wprobe = 0;
     uint64_t st_keys = 0;
-    auto byte_at = [&](uint32_t i) -> uint8_t { return a.bytes[i]; };
+    auto byte_at = [&](uint32_t i) -> uint8_t { return a.bytes[BI(i, bytes)]; };
     for (uint32_t idx = blockIdx.x * WAVE + lane_id(); idx < nslow; idx += gridDim.x * WAVE) {
-        const uint32_t t = a.slow_list[idx];
-        const uint64_t sbase = (uint64_t)(a.off[t] - a.off[0]) + 2ull * t;  // len+2 entries per topic
+        const uint32_t t = a.slow_list[BI(idx, slow_list)];
+        const uint32_t b = a.off[BI(t, off)], e = a.off[BI(t + 1, off)];
+        const uint32_t ns = e - b + 2;  // len+2 entries per topic
+        const uint64_t sbase = BIN((uint64_t)(b - a.off[0]) + 2ull * t, ns, scratch);
         uint32_t *wid = a.scratch_w + sbase;
         uint64_t *stk = a.scratch_s + sbase;
-        const uint32_t b = a.off[t], e = a.off[t + 1];
-        const bool dollar = (e > b) && a.bytes[b] == '$';
+        const bool dollar = (e > b) && byte_at(b) == '$';
         uint32_t nl = 0;
         for (uint32_t i = b;; ++i) {  // tokenise every level (the topic is not badarg)
             const uint32_t st = i;
             const uint64_t key = level_key(&i, e, byte_at);
-            wid[nl++] = word_lookup(a, key, i - st, st, byte_at, &st_wprobe);
+            wid[BIR(nl++, ns, a.bnd)] = word_lookup(a, key, i - st, st, byte_at, &st_wprobe);
             if (i >= e) break;
         }
         uint32_t dummy_v = 0, dummy_p = 0;
-        const uint32_t c = dfs_walk<false>(a, R, wid, stk, nl, dollar, 0, &dummy_p, &dummy_v);
+        const uint32_t c = dfs_walk<false>(a, R, wid, stk, nl, dollar, 0, &dummy_p, &dummy_v, ns);
         const unsigned long long pos = atomicAdd(a.cursor, (unsigned long long)c);
-        a.out_off[t] = (uint32_t)pos;
-        a.out_cnt[t] = c;
-        a.status[t] = 0;
+        a.out_off[BI(t, out)] = (uint32_t)pos;
+        a.out_cnt[BI(t, out)] = c;
+        a.status[BI(t, out)] = 0;
         st_keys += c;
-        if (a.mode == MODE_RUNS) a.out_kcnt[t] = c;
+        if (a.mode == MODE_RUNS) a.out_kcnt[BI(t, out)] = c;
         if (a.mode != MODE_COUNT && pos + c <= a.keys_cap)  // output slots: keys, spans or ids
-            dfs_walk<true>(a, R, wid, stk, nl, dollar, pos, &st_probe, &st_visit);
+            dfs_walk<true>(a, R, wid, stk, nl, dollar, pos, &st_probe, &st_visit, ns);
     }
     if constexpr (STATS) {
         // levels were already counted by the fast kernel's pre-scan
@@ -1176,7 +1183,7 @@ __device__ __forceinline__ uint32_t first_dfs_topic(const MatchArgs &a, const Ro
             bloom = R.bloom;
             if (!dollar && R.hash_cnt) th = a.arena[R.list_off - 3];
         } else {
-            const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + slot);
+            const uint4 x = *reinterpret_cast<const uint4 *>(a.etab + BI(slot, etab));
             node = (uint32_t)slot;
             bloom = x.z;
             info = x.w;
@@ -1281,20 +1288,20 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
 
     // ---- stage the wave's topic bytes (as k_match_fast)
     const uint32_t t0 = blockIdx.x * a.tpw;
-    const uint32_t wb0 = a.off[t0], wb1 = a.off[min(t0 + a.tpw, a.n)];
+    const uint32_t wb0 = a.off[BI(t0, off)], wb1 = a.off[BI(min(t0 + a.tpw, a.n), off)];
     const uint32_t tbase = wb0 & ~15u;
     const bool staged = ((reinterpret_cast<uintptr_t>(a.bytes) & 15u) == 0) && (wb1 - tbase <= (uint32_t)TBCAP);
     if (staged) {
         for (uint32_t j = lane * 16; tbase + j < wb1; j += WAVE * 16) {
             if (tbase + j + 16 <= wb1) {
-                *reinterpret_cast<uint4 *>(&L.tb[j]) = *reinterpret_cast<const uint4 *>(a.bytes + tbase + j);
+                *reinterpret_cast<uint4 *>(&L.tb[j]) = *reinterpret_cast<const uint4 *>(a.bytes + BIN(tbase + j, 16, bytes));
             } else {
-                for (uint32_t k = 0; tbase + j + k < wb1; k++) L.tb[j + k] = a.bytes[tbase + j + k];
+                for (uint32_t k = 0; tbase + j + k < wb1; k++) L.tb[j + k] = a.bytes[BI(tbase + j + k, bytes)];
             }
         }
         __syncthreads();
     }
-    auto byte_at = [&](uint32_t i) -> uint8_t { return staged ? L.tb[i - tbase] : a.bytes[i]; };
+    auto byte_at = [&](uint32_t i) -> uint8_t { return staged ? L.tb[i - tbase] : a.bytes[BI(i, bytes)]; };
 
     bool badarg = false, dollar = false;
     uint32_t nl = 0, b = 0, e = 0;
@@ -1303,16 +1310,16 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
     uint32_t widr[TM_PRELOOK];
     uint32_t pre_b = 0;
     if (active) {
-        b = a.off[t];
-        e = a.off[t + 1];
+        b = a.off[BI(t, off)];
+        e = a.off[BI(t + 1, off)];
         dollar = (e > b) && byte_at(b) == '$';
         TM_PRESCAN_PRELOOK(dummy);
     }
     uint32_t cur_b = pre_b;
 #else
     if (active) {
-        b = a.off[t];
-        e = a.off[t + 1];
+        b = a.off[BI(t, off)];
+        e = a.off[BI(t + 1, off)];
         dollar = (e > b) && byte_at(b) == '$';
         uint32_t st = b;
         for (uint32_t i = b;; ++i) {
@@ -1469,8 +1476,8 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
                     uint4 x1[RPL], x2[RPL];
 #pragma unroll
                     for (int k = 0; k < RPL; k++) {
-                        x1[k] = p1[k] ? *reinterpret_cast<const uint4 *>(a.etab + s1[k]) : make_uint4(NONE, 0, 0, 0);
-                        x2[k] = p2[k] ? *reinterpret_cast<const uint4 *>(a.etab + s2[k]) : make_uint4(NONE, 0, 0, 0);
+                        x1[k] = p1[k] ? *reinterpret_cast<const uint4 *>(a.etab + BI(s1[k], etab)) : make_uint4(NONE, 0, 0, 0);
+                        x2[k] = p2[k] ? *reinterpret_cast<const uint4 *>(a.etab + BI(s2[k], etab)) : make_uint4(NONE, 0, 0, 0);
                     }
 #pragma unroll
                     for (int k = 0; k < RPL; k++) {
@@ -1650,30 +1657,34 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
         uint32_t sb = 0;
         if (lane == 0 && tot_sp) sb = atomicAdd(a.slow_count, tot_sp);
         sb = __shfl(sb, 0, WAVE);
-        if (spill) a.slow_list[sb + ps] = t;
+        if (spill) a.slow_list[BI(sb + ps, slow_list)] = t;
     }
 }
 
 // ---------------------------------------------------------------------------
-__global__ void k_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n) {
+__global__ void k_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n, uint64_t cap,
+                            unsigned long long *bnd) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dst[idx[i]] = src[i];
+    if (i < n) dst[BIR(idx[i], cap, bnd)] = src[i];
 }
 
-__global__ void k_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *src, uint64_t n) {
+__global__ void k_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *src, uint64_t n, uint64_t cap,
+                           unsigned long long *bnd) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dst[idx[i]] = src[i];
+    if (i < n) dst[BIR(idx[i], cap, bnd)] = src[i];
 }
 
-hipError_t launch_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n, hipStream_t s) {
+hipError_t launch_scatter16(uint4 *dst, const uint64_t *idx, const uint4 *src, uint64_t n, hipStream_t s,
+                            uint64_t cap, unsigned long long *bnd) {
     if (!n) return hipSuccess;
-    k_scatter16<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
+    k_scatter16<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n, cap, bnd);
     return hipGetLastError();
 }
 
-hipError_t launch_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *src, uint64_t n, hipStream_t s) {
+hipError_t launch_scatter4(uint32_t *dst, const uint64_t *idx, const uint32_t *src, uint64_t n, hipStream_t s,
+                           uint64_t cap, unsigned long long *bnd) {
     if (!n) return hipSuccess;
-    k_scatter4<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
+    k_scatter4<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n, cap, bnd);
     return hipGetLastError();
 }
 

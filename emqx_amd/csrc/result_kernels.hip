@@ -16,6 +16,8 @@
 // All of it is byte movement: coalesced where the layout allows, HBM-bound.
 #include <hip/hip_runtime.h>
 
+#define TM_BND_FILE 2  // device_api.h TM_BOUNDS records
+
 #include <algorithm>
 
 #include "copy_api.h"
@@ -722,55 +724,65 @@ hipError_t launch_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off
 }
 
 // ---------------------------------------------------------------------------
-__global__ void k_scatter1(uint8_t *dst, const uint64_t *idx, const uint8_t *src, uint64_t n) {
+__global__ void k_scatter1(uint8_t *dst, const uint64_t *idx, const uint8_t *src, uint64_t n, uint64_t cap,
+                           unsigned long long *bnd) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dst[idx[i]] = src[i];
+    if (i < n) dst[BIR(idx[i], cap, bnd)] = src[i];
 }
 
-hipError_t launch_scatter1(uint8_t *dst, const uint64_t *idx, const uint8_t *src, uint64_t n, hipStream_t s) {
+hipError_t launch_scatter1(uint8_t *dst, const uint64_t *idx, const uint8_t *src, uint64_t n, hipStream_t s,
+                           uint64_t cap, unsigned long long *bnd) {
     if (!n) return hipSuccess;
-    k_scatter1<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
+    k_scatter1<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n, cap, bnd);
     return hipGetLastError();
 }
 
-__global__ void k_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n) {
+__global__ void k_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, uint64_t cap,
+                           unsigned long long *bnd) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dst[idx[i]] = src[i];
+    if (i < n) dst[BIR(idx[i], cap, bnd)] = src[i];
 }
 
-hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, hipStream_t s) {
+hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, hipStream_t s,
+                           uint64_t cap, unsigned long long *bnd) {
     if (!n) return hipSuccess;
-    k_scatter8<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n);
+    k_scatter8<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(dst, idx, src, n, cap, bnd);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
 // The edge table image of a full publish: every slot empty, then each node's record in its
 // slot.  HBM-bound writes (20 B per slot, then 20 B per node at random slots).
-__global__ void k_edge_clear(uint4 *etab, uint32_t *slot_list, uint64_t cap) {
+__global__ void k_edge_clear(uint4 *etab, uint32_t *slot_list, uint64_t cap, uint64_t buf_slots,
+                             unsigned long long *bnd) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
-        etab[i] = make_uint4(NONE, 0u, 0u, 0u);
-        slot_list[i] = 0u;
+        const uint64_t j = BIR(i, buf_slots, bnd);
+        etab[j] = make_uint4(NONE, 0u, 0u, 0u);
+        slot_list[j] = 0u;
     }
 }
 
-__global__ void k_edge_place(uint4 *etab, uint32_t *slot_list, const NodeImage *nodes, uint64_t n) {
+__global__ void k_edge_place(uint4 *etab, uint32_t *slot_list, const NodeImage *nodes, uint64_t n, uint64_t cap,
+                             uint64_t buf_slots, unsigned long long *bnd) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const NodeImage r = nodes[i];
-    etab[r.slot] = make_uint4(r.parent, r.word, r.bloom, r.info);
-    slot_list[r.slot] = r.list;
+    // a record past the table the publish sized (cap) would be a host bug: the bounds build
+    // reports it against the table's size, not the buffer's
+    const uint64_t j = BIR(BIR(r.slot, cap, bnd), buf_slots, bnd);
+    etab[j] = make_uint4(r.parent, r.word, r.bloom, r.info);
+    slot_list[j] = r.list;
 }
 
 hipError_t launch_edge_image(uint4 *etab, uint32_t *slot_list, uint64_t cap, const NodeImage *nodes, uint64_t n,
-                             hipStream_t s) {
+                             hipStream_t s, uint64_t buf_slots, unsigned long long *bnd) {
     if (!cap) return hipSuccess;
     const uint64_t want = (cap + 255) / 256;
-    k_edge_clear<<<(unsigned)std::min<uint64_t>(want, 16384), 256, 0, s>>>(etab, slot_list, cap);
+    k_edge_clear<<<(unsigned)std::min<uint64_t>(want, 16384), 256, 0, s>>>(etab, slot_list, cap, buf_slots, bnd);
     hipError_t e = hipGetLastError();
     if (e || !n) return e;
-    k_edge_place<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(etab, slot_list, nodes, n);
+    k_edge_place<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(etab, slot_list, nodes, n, cap, buf_slots, bnd);
     return hipGetLastError();
 }
 

@@ -76,7 +76,7 @@
 extern "C" {
 #endif
 
-#define TM_ABI_VERSION 9u
+#define TM_ABI_VERSION 10u
 
 /* status codes */
 #define TM_OK          0
@@ -131,6 +131,8 @@ extern "C" {
                                    changes it made as an epoch patch (tm_patch_export) */
 #define TM_CFG_FAIL_HOST_CALLS 4u /* test aid: tm_match_batch_runs fails (TM_EDEVICE) after taking
                                      its read lease, to check a failed call leaves no lease held */
+#define TM_CFG_FAIL_FLUSH_ONCE 8u /* test aid (ABI 10): the first delta commit that scatters fails
+                                     in its upload, as an out-of-HBM staging buffer would */
 
 typedef struct tm_engine tm_engine;
 
@@ -214,6 +216,8 @@ typedef struct tm_stats_t {
                                    (a delta's in-place scatters; a full rebuild's standby swap) */
     uint64_t n_commits_refused; /* commits refused for capacity, ops kept staged               */
     uint64_t n_staged;          /* ops staged now (not yet committed)                          */
+    uint64_t standby_bytes;     /* (ABI 10) device bytes of the standby image a full publish
+                                   uploads into (0: none kept; the next one allocates)         */
 } tm_stats_t;
 
 /* lifecycle --------------------------------------------------------------- */
@@ -472,6 +476,12 @@ int tm_debug_timing(tm_engine *eng, int enable, float *ms_out);
  * the word table, word arena, word offsets, edge table, slot lists, list arena and root are
  * compared).  The full publish stays in place. */
 int tm_debug_image_check(tm_engine *eng, uint32_t *diff_mask);
+/* diagnostics (ABI 10): what the bounds-checked debug build (libemqx_tm_bounds.so, built with
+ * TM_BOUNDS=1) found since the engine was created: *hits = device indices at or past a buffer's
+ * real capacity (recorded and redirected by the kernels, so nothing faults) plus overwritten
+ * canary tails plus host copies past a buffer's end; msg (cap bytes) the first findings.  The
+ * product build returns TM_ENOTFOUND (it checks nothing). */
+int tm_debug_bounds(tm_engine *eng, uint64_t *hits, char *msg, uint32_t cap);
 
 #ifdef __cplusplus
 }

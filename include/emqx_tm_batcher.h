@@ -31,8 +31,13 @@
  *   writes   any thread may write the engine directly (tm_apply / tm_commit_epoch are safe
  *            beside the aggregator); tm_batcher_apply / tm_batcher_commit are the same calls.
  *            A delivery callback may stage (tm_apply) but not commit: tm_commit_epoch and
- *            tm_batcher_commit return TM_ESTATE there, since a commit waits for the read lease
- *            of the window being delivered.
+ *            tm_batcher_commit return TM_ESTATE on every delivery thread, whatever the
+ *            transport.  A commit waits for the read leases of every runs window in flight,
+ *            and only the delivery threads can finish those windows: a commit made from one of
+ *            them could wait on a window queued behind its own (with one delivery thread it
+ *            always would).  A callback's own tm_match_batch_runs call passes a waiting commit
+ *            only when its window holds a lease (the arena cannot change meanwhile); a callback
+ *            of a window without one (ids transport, other modes) waits for the commit.
  *
  * Erlang binding: a NIF calls tm_batcher_submit with a callback that
  * enif_send()s the id list to the publishing pid, which waits in `receive`; the callback

@@ -36,3 +36,23 @@ def load_golden(name):
 @pytest.fixture(scope="session")
 def golden():
     return load_golden
+
+
+# Under the bounds-checked debug build (EMQX_TM_LIB=.../libemqx_tm_bounds.so)
+# every GPU test also fails if it made the library record an out-of-bounds device index, a
+# written canary tail or a host copy past a buffer's end.
+_BOUNDS_SEEN = [0]
+
+
+@pytest.fixture(autouse=True)
+def _bounds_guard():
+    yield
+    if "bounds" not in os.path.basename(os.environ.get("EMQX_TM_LIB", "")):
+        return
+    from emqx_amd import _native as N
+    if N._lib is None:
+        return
+    r = N.debug_bounds()
+    if r is not None and r[0] > _BOUNDS_SEEN[0]:
+        _BOUNDS_SEEN[0] = r[0]
+        pytest.fail(f"bounds build: {r[0]} findings: {r[1]}")

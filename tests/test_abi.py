@@ -31,8 +31,8 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert name in exported, name
         assert getattr(lib, name) is not None
-    assert lib.tm_abi_version() == 9
-    assert C.sizeof(N.tm_stats_t) == 20 * 8  # mirrors tm_stats_t in include/emqx_tm.h
+    assert lib.tm_abi_version() == 10
+    assert C.sizeof(N.tm_stats_t) == 21 * 8  # mirrors tm_stats_t in include/emqx_tm.h
     assert C.sizeof(N.tm_config) == 11 * 4
     assert C.sizeof(N.tm_runs_result) == 9 * 8 and C.sizeof(N.tm_span) == 16
 

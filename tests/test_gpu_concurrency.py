@@ -362,6 +362,56 @@ def test_commit_from_delivery_callback_is_refused_not_deadlocked():
     eng.close()
 
 
+def test_runs_call_from_an_unleased_window_waits_for_a_commit():
+    """Advisor (round 4, medium): a delivery callback used to take a runs lease past a waiting
+    commit whatever its window; only a runs window holds a lease that keeps the host id arena
+    still.  Here an ids-transport window (no lease) calls tm_match_batch_runs from its callback
+    while a commit waits for another reader's lease: the call must wait for the commit and then
+    read the NEW epoch (before the fix it read the arena the commit was about to change)."""
+    import time
+    w = workloads.generate("A", scale=0.05, n_topics=500)
+    eng = N.Engine(0)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    e0 = eng.stats()["epoch"]
+    to32 = np.ascontiguousarray(w.t_off, dtype=np.uint32)
+    eng.match_runs_view(w.t_bytes, to32)  # this thread now holds a read lease
+    b = N.Batcher(eng, max_batch=64, max_wait_us=200, transport=N.TM_TRANSPORT_IDS)
+    committed = threading.Event()
+
+    def writer():
+        eng.apply([(N.TM_OP_ADD, b"lease/+/x", 77)])
+        eng.commit()  # waits for this thread's lease
+        committed.set()
+
+    wt = threading.Thread(target=writer)
+    wt.start()
+    time.sleep(0.5)
+    assert not committed.is_set()  # blocked on the lease, with the lease gate down
+    seen = {}
+    cb_done = threading.Event()
+
+    @N.tm_match_cb
+    def cb(ctx, status, ids, n):
+        res = N.tm_runs_result()
+        seen["rc"] = eng.lib.tm_match_batch_runs(eng.h, w.t_bytes.ctypes.data, to32.ctypes.data, 8, N.C.byref(res))
+        seen["epoch"] = res.epoch
+        seen["after_commit"] = committed.is_set()
+        eng.lib.tm_runs_release(eng.h)
+        cb_done.set()
+
+    assert b.lib.tm_batcher_submit(b.h, b"a/b", 3, cb, None) == N.TM_OK
+    time.sleep(0.5)
+    assert not cb_done.is_set(), "a callback of a window without a lease passed a waiting commit"
+    eng.lib.tm_runs_release(eng.h)  # the commit proceeds, then the callback's call
+    wt.join(timeout=30)
+    assert committed.is_set()
+    assert cb_done.wait(30)
+    assert seen["rc"] == N.TM_OK and seen["epoch"] == e0 + 1, seen
+    b.close()
+    eng.close()
+
+
 def _conc_lib():
     import os
     C = N.C
