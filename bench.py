@@ -110,6 +110,8 @@ def _loadgen():
     lg.loadgen_run3.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double, C.c_double,
                                 C.c_int, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                 C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.POINTER(N.tm_batcher_stats)]
+    lg.loadgen_run4.argtypes = lg.loadgen_run3.argtypes + [C.POINTER(N.tm_batcher_window), C.c_uint32,
+                                                           C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]
     lg.spans_checksum.restype = C.c_uint64
     lg.spans_checksum.argtypes = [C.c_void_p, C.c_uint32]
     return lg
@@ -139,8 +141,12 @@ def batcher_load(eng, tb, to32, seconds, plan=None):
         b = N.Batcher(eng, max_batch=65536, max_wait_us=200, delivery_threads=dt, transport=transport)
         got, ids, errs, cs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
         win = N.tm_batcher_stats()
-        rc = lg.loadgen_run3(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, warm, seconds, spans,
-                             C.byref(got), C.byref(ids), C.byref(errs), C.byref(cs), C.byref(el), C.byref(win))
+        wbuf = (N.tm_batcher_window * N.TM_BATCHER_WINDOWS)()
+        wn = C.c_uint32()
+        cg = (C.c_uint64 * 4)()
+        rc = lg.loadgen_run4(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, warm, seconds, spans,
+                             C.byref(got), C.byref(ids), C.byref(errs), C.byref(cs), C.byref(el), C.byref(win),
+                             wbuf, N.TM_BATCHER_WINDOWS, C.byref(wn), cg)
         st = b.stats()
         b.close()
         if rc != 0 or errs.value or not win.lat_count:
@@ -166,7 +172,11 @@ def batcher_load(eng, tb, to32, seconds, plan=None):
                      "backend_frac": round(st["backend_us"] * 1e-6 / el.value, 3),
                      # share of the run's wall time each pipeline stage was busy (stages overlap)
                      "stage_busy": {k: round(st[k + "_us"] * 1e-6 / el.value, 3)
-                                    for k in ("cut", "enqueue", "gpu_wait", "copy", "deliver")}})
+                                    for k in ("cut", "enqueue", "gpu_wait", "copy", "deliver")},
+                     "windows": window_stages(wbuf, wn.value),
+                     "cgroup_cpu": {"usage_cpus": round(cg[0] * 1e-6 / max(win.window_s, 1e-9), 2),
+                                    "periods": int(cg[1]), "throttled_periods": int(cg[2]),
+                                    "throttled_ms": round(cg[3] / 1e3, 3)}})
         if not runs[-1]["littles_law"]["ok"]:
             log(f"batcher: latency mean {mean_ms:.3f} ms differs from publishers / rate {little_ms:.3f} ms by > 20%")
     return {"api": f"tm_batcher_submit (max_batch 65536, max_wait 200 us, {dt} delivery threads)", "runs": runs,
@@ -176,6 +186,43 @@ def batcher_load(eng, tb, to32, seconds, plan=None):
                     f"rate and latency over a {seconds:g} s steady-state window after {warm:g} s of warm-up "
                     "(every publish delivered in it, tm_batcher_stats_reset / _get), checked against Little's law; "
                     "stage_busy: share of wall time each stage worked (copy and deliver: per delivery thread)"}
+
+
+def window_stages(wbuf, n):
+    """Where the aggregator's windows spent their time (tm_batcher_window stamps of the windows
+    completed in the measured steady state), to attribute the latency tail to a stage.  Per
+    window: wait (its oldest publish's submit -> the cutter takes it: the window filling, or
+    the cutter busy / off-CPU), cut (queue -> pinned staging -> GPU part queued), gpu (queued ->
+    observed done, behind the windows ahead of it), ready (counters read, any re-run, D2H queued),
+    queue (handed over -> a delivery thread starts on it), deliver (first -> last callback).  The
+    window's span (oldest submit -> last callback) bounds the latency of every publish in it."""
+    import numpy as np
+    if not n:
+        return None
+    f = {k: np.array([getattr(wbuf[i], k) for i in range(n)], dtype=np.float64)
+         for k in ("n", "flags", "t_oldest", "t_cut", "t_queued", "t_gpu", "t_ready", "t_deliver", "t_done", "epoch")}
+    t_del = np.where(f["t_deliver"] > 0, f["t_deliver"], f["t_ready"])
+    st = {"wait": f["t_cut"] - f["t_oldest"], "cut": f["t_queued"] - f["t_cut"], "gpu": f["t_gpu"] - f["t_queued"],
+          "ready": f["t_ready"] - f["t_gpu"], "queue": t_del - f["t_ready"], "deliver": f["t_done"] - t_del}
+    span = f["t_done"] - f["t_oldest"]
+    order = np.argsort(span)
+    k1 = max(1, n // 100)
+
+    def ms(idx):
+        return {k: round(float(np.mean(v[idx])) / 1e6, 3) for k, v in st.items()}
+    worst = int(order[-1])
+    gaps = np.diff(np.sort(f["t_cut"])) if n > 1 else np.zeros(1)
+    return {"windows": int(n), "mean_publishes": round(float(np.mean(f["n"])), 1),
+            "span_ms": {"p50": round(float(np.percentile(span, 50)) / 1e6, 3),
+                        "p99": round(float(np.percentile(span, 99)) / 1e6, 3),
+                        "max": round(float(span[worst]) / 1e6, 3)},
+            "stage_ms_median_window": ms(order[n // 2:n // 2 + 1]),
+            "stage_ms_slowest_1pct": ms(order[-k1:]),
+            "stage_ms_slowest": ms(np.array([worst])),
+            "slowest_publishes": int(f["n"][worst]),
+            "reruns": int(np.sum((f["flags"].astype(np.int64) & 1) != 0)),
+            "epochs_seen": int(len(np.unique(f["epoch"]))),
+            "max_gap_between_cuts_ms": round(float(np.max(gaps)) / 1e6, 3)}
 
 
 def replica_batcher_leg(eng, tb, to32, seconds):
@@ -240,7 +287,8 @@ def host_runs_leg(eng, tb, to32, n, w, reps=10):
         eng.lib.tm_runs_release(eng.h)
     dt = float(np.mean(ts))
     out["pinned_read_every_id"] = {"ms_per_batch": round(dt * 1e3, 3), "publishes_per_s": round(n / dt, 1),
-                                   "threads": 8}
+                                   "p50_ms": round(float(np.percentile(ts, 50)) * 1e3, 3),
+                                   "p99_ms": round(float(np.percentile(ts, 99)) * 1e3, 3), "threads": 8}
     res = eng.match_runs_view(pinned, to32)
     out["spans_per_batch"] = int(res.total_spans)
     out["ids_per_batch"] = int(res.total_ids)
@@ -258,6 +306,34 @@ def host_runs_leg(eng, tb, to32, n, w, reps=10):
     if bad:
         log(f"PARITY FAILURE (runs): {bad}/{ps} topics differ")
     return out
+
+
+def end_to_end(runs, keys):
+    """SURVEY §8(d)'s timing protocol: publishes/s = B / mean(H2D of the topics + kernels + D2H
+    + host result view), over the timed batches of the runs leg (tm_match_batch_runs: the
+    host view is the spans of route ids in the engine's host id arena), and the same with
+    every id then read by 8 host threads (what a consumer pays at least once); the keys form
+    (every key handle copied to the host) beside it."""
+    if not runs:
+        return None
+    pin, rd = runs["pinned"], runs["pinned_read_every_id"]
+    return {
+        "protocol": "SURVEY.md §8(d): B / mean(H2D + kernel + D2H + host result view), topics from host "
+                    "memory, results as host spans of route ids; batches timed one after another",
+        "api": "tm_match_batch_runs",
+        "batch": runs["batch"],
+        "publishes_per_s": pin["publishes_per_s"],
+        "ms_per_batch": pin["ms_per_batch"],
+        "p50_batch_ms": pin["p50_ms"],
+        "p99_batch_ms": pin["p99_ms"],
+        "read_every_id": {"publishes_per_s": rd["publishes_per_s"], "ms_per_batch": rd["ms_per_batch"],
+                          "p50_batch_ms": rd["p50_ms"], "p99_batch_ms": rd["p99_ms"], "threads": rd["threads"],
+                          "ids_per_batch": runs["ids_per_batch"]},
+        "pageable_topics": runs["pageable"]["publishes_per_s"],
+        "keys_form": ({"api": keys["api"], "publishes_per_s": keys["publishes_per_s"],
+                       "ms_per_batch": keys["ms_per_batch"]} if keys else None),
+        "parity": runs["parity"],
+    }
 
 
 def gather_roof(walk, kernel_ms, table_bytes):
@@ -753,7 +829,7 @@ def main():
                      "publishes_per_s": round(n / dt, 1),
                      "note": "H2D of the topics + kernels + D2H of every key + host result view; "
                              "bounded by PCIe D2H of the keys"}
-        host_runs = host_runs_leg(eng, tb, to32, n, w)
+        host_runs = host_runs_leg(eng, tb, to32, n, w, reps=max(10, args.steps))
         batcher = batcher_load(eng, tb, to32, args.batcher_seconds) if args.batcher_seconds > 0 else None
         if batcher is not None:
             batcher["on_replica"] = replica_batcher_leg(eng, tb, to32, args.batcher_seconds)
@@ -831,6 +907,9 @@ def main():
             },
             "gather": gather_roof(walk, kernel_ms, 16 * int(st["edge_slots"])),
             "latency_vs_batch": lat_sweep,
+            # SURVEY §8(d)'s own protocol beside the device-resident value: host topics in, spans
+            # of route ids on the host out, per batch of `publishes_per_step_per_gpu`
+            "end_to_end": end_to_end(host_runs, host_path),
             "host_path": host_path,
             "host_path_runs": host_runs,
             "batcher": batcher,

@@ -72,7 +72,7 @@ EXPORTS = (
 BATCHER_EXPORTS = (
     "tm_batcher_create", "tm_batcher_create_fn", "tm_batcher_destroy", "tm_batcher_submit", "tm_batcher_match",
     "tm_batcher_apply", "tm_batcher_commit", "tm_batcher_stats_get", "tm_batcher_submit_spans",
-    "tm_batcher_stats_reset", "tm_batcher_submit_spans32",
+    "tm_batcher_stats_reset", "tm_batcher_submit_spans32", "tm_batcher_windows",
 )
 
 
@@ -158,6 +158,14 @@ class tm_batcher_stats(C.Structure):
                 ("lat_mean_us", C.c_double), ("lat_count", C.c_uint64), ("lat_p999_us", C.c_double),
                 ("window_s", C.c_double)]
 
+
+class tm_batcher_window(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("flags", C.c_uint32)] + [(k, C.c_uint64) for k in (
+        "t_oldest", "t_cut", "t_queued", "t_gpu", "t_ready", "t_deliver", "t_done", "epoch")]
+
+
+TM_BATCHER_WINDOWS = 16384
+TM_WIN_RERUN, TM_WIN_RUNS, TM_WIN_FAILED = 1, 2, 4
 
 tm_match_cb = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.POINTER(C.c_uint64), C.c_uint32)
 tm_spans_cb = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_void_p, C.c_uint32, C.c_uint64)
@@ -252,6 +260,7 @@ def load() -> C.CDLL:
     lib.tm_batcher_commit.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.tm_batcher_stats_get.argtypes = [C.c_void_p, P(tm_batcher_stats)]
     lib.tm_batcher_stats_reset.argtypes = [C.c_void_p]
+    lib.tm_batcher_windows.argtypes = [C.c_void_p, P(tm_batcher_window), C.c_uint32, P(C.c_uint32)]
     for name in BATCHER_EXPORTS:
         if name != "tm_batcher_destroy":
             getattr(lib, name).restype = C.c_int
@@ -844,6 +853,18 @@ class Batcher:
         rc = self.lib.tm_batcher_stats_reset(self.h)
         if rc != TM_OK:
             raise TMError(rc, "tm_batcher_stats_reset failed")
+
+    def windows(self) -> np.ndarray:
+        """Stage stamps of the windows completed since the last reset (tm_batcher_windows), as a
+        structured array with tm_batcher_window's fields, oldest first."""
+        buf = (tm_batcher_window * TM_BATCHER_WINDOWS)()
+        n = C.c_uint32()
+        rc = self.lib.tm_batcher_windows(self.h, buf, TM_BATCHER_WINDOWS, C.byref(n))
+        if rc != TM_OK:
+            raise TMError(rc, "tm_batcher_windows failed")
+        dt = np.dtype([("n", np.uint32), ("flags", np.uint32)] + [(k, np.uint64) for k in (
+            "t_oldest", "t_cut", "t_queued", "t_gpu", "t_ready", "t_deliver", "t_done", "epoch")])
+        return np.frombuffer(bytes(buf), dtype=dt, count=n.value).copy()
 
     def close(self):
         if getattr(self, "h", None):

@@ -64,6 +64,7 @@ extern "C" int tmx_batch_reserve_matches(tm_engine *eng, uint32_t set, uint64_t 
 extern "C" void tmx_lease_drop(tm_engine *eng);
 extern "C" int tmx_engine_is_replica(const tm_engine *eng);
 extern "C" int tmx_engine_runs_ok(const tm_engine *eng);
+extern "C" uint64_t tmx_engine_epoch(const tm_engine *eng);
 
 namespace {
 // set on the delivery threads: the engine refuses a commit from a callback (it would wait for
@@ -268,6 +269,11 @@ struct Slot {
     uint32_t mode = 0;
     int rc = 0;
     uint64_t t_enq = 0, t_done = 0;
+    // stage stamps of this window (tm_batcher_window)
+    uint64_t t_old = 0, t_cut = 0, t_queued = 0, t_gpu = 0;
+    std::atomic<uint64_t> t_deliver{0};
+    uint32_t wflags = 0;
+    uint64_t epoch = 0;
     // engine backend
     HBuf h_bytes, h_off, h_off_out, h_status, h_cnt, h_ids, h_ctl;
     DBuf d_bytes, d_off, d_ids, d_off_out;
@@ -443,6 +449,9 @@ struct tm_batcher {
         }
         (void)taken_bytes;
         S.n = (uint32_t)S.pubs.size();
+        // each shard is FIFO, so the window's oldest publish is the oldest of the shards' heads
+        S.t_old = ~0ull;
+        for (const Pending &p : S.pubs) S.t_old = std::min(S.t_old, p.t0);
         S.nbytes = at;
         uint32_t *o = S.h_off.as<uint32_t>();
         uint32_t pos = 0;
@@ -576,7 +585,8 @@ struct tm_batcher {
     int complete_runs(Slot &S) {
         const uint64_t tw0 = now_ns();
         BT_HIP(hipEventSynchronize(S.ev));
-        ns_gpu.fetch_add(now_ns() - tw0, std::memory_order_relaxed);
+        S.t_gpu = now_ns();
+        ns_gpu.fetch_add(S.t_gpu - tw0, std::memory_order_relaxed);
         const uint64_t *ctl = S.h_ctl.as<uint64_t>();
         uint64_t total = ctl[0];
         const uint64_t seg = ctl[3], fr = ctl[4];
@@ -592,8 +602,10 @@ struct tm_batcher {
                 spans_per_pub.store(std::max(spans_per_pub.load(std::memory_order_relaxed),
                                              (double)total / std::max<uint32_t>(S.n, 1)),
                                     std::memory_order_relaxed);
+                S.wflags |= TM_WIN_RERUN;
                 if ((rc = enqueue(S))) return rc;
                 BT_HIP(hipEventSynchronize(S.ev));
+                S.t_gpu = now_ns();
                 total = S.h_ctl.as<uint64_t>()[0];
                 if (total > S.spans_cap) return TM_EDEVICE;
             }
@@ -654,6 +666,7 @@ struct tm_batcher {
         const uint64_t tw0 = now_ns();
         BT_HIP(hipEventSynchronize(S.ev));
         const uint64_t tw1 = now_ns();
+        S.t_gpu = tw1;
         ns_gpu.fetch_add(tw1 - tw0, std::memory_order_relaxed);
         const uint64_t *ctl = S.h_ctl.as<uint64_t>();
         const uint64_t total = ctl[0], seg = ctl[2], fr = ctl[3];
@@ -672,8 +685,10 @@ struct tm_batcher {
                 const uint64_t words = S.mode == TM_MATCH_ALL && !S.narrow ? 2 * want : want;
                 if ((rc = tmx_batch_reserve_matches(eng, S.set, words))) return rc;
                 if (S.mode == TM_MATCH_ALL) S.ids_cap = std::max(S.ids_cap, want);
+                S.wflags |= TM_WIN_RERUN;
                 if ((rc = enqueue(S))) return rc;
                 BT_HIP(hipEventSynchronize(S.ev));
+                S.t_gpu = now_ns();
                 if (S.h_ctl.as<uint64_t>()[0] > S.keys_cap) {
                     std::snprintf(bt_err, sizeof bt_err, "re-run still past its output (%llu > %llu ids)",
                                   (unsigned long long)S.h_ctl.as<uint64_t>()[0], (unsigned long long)S.keys_cap);
@@ -942,7 +957,26 @@ struct tm_batcher {
         if (sleepers.load()) work_cv.notify_all();
     }
 
+    // the last TM_BATCHER_WINDOWS windows' stage stamps (tm_batcher_windows)
+    std::unique_ptr<tm_batcher_window[]> wins{new tm_batcher_window[TM_BATCHER_WINDOWS]};
+    std::atomic<uint64_t> win_next{0}, win_first{0};  // ring positions; win_first: the reset's
+    void trace_window(Slot &S) {
+        if (!S.n) return;
+        const uint64_t i = win_next.fetch_add(1, std::memory_order_relaxed);
+        tm_batcher_window &w = wins[i % TM_BATCHER_WINDOWS];
+        w.n = S.n;
+        w.flags = S.wflags | (S.runs ? TM_WIN_RUNS : 0u) | (S.rc < 0 ? TM_WIN_FAILED : 0u);
+        w.t_oldest = S.t_old;
+        w.t_cut = S.t_cut;
+        w.t_queued = S.t_queued;
+        w.t_gpu = S.t_gpu ? S.t_gpu : S.t_queued;
+        w.t_ready = S.t_done;
+        w.t_deliver = S.t_deliver.load(std::memory_order_relaxed);
+        w.t_done = now_ns();
+        w.epoch = S.epoch;
+    }
     void free_slot(Slot &S) {
+        trace_window(S);
         if (S.leased) {  // the window's spans are delivered: a commit may change the id arena now
             S.leased = false;
             tmx_lease_drop(eng);
@@ -986,6 +1020,8 @@ struct tm_batcher {
                 ns_copy.fetch_add(now_ns() - t0, std::memory_order_relaxed);  // waited on PCIe
             }
             const uint64_t td0 = now_ns();
+            uint64_t z = 0;
+            S.t_deliver.compare_exchange_strong(z, td0, std::memory_order_relaxed);
             tl_window_leased = S.leased ? 1 : 0;
             deliver_range(S, w.lo, w.hi, rc, H);
             tl_window_leased = 0;
@@ -1039,6 +1075,10 @@ struct tm_batcher {
             }
             const uint64_t tc0 = now_ns();
             S.runs = false;
+            S.wflags = 0;
+            S.t_gpu = 0;
+            S.t_deliver.store(0, std::memory_order_relaxed);
+            S.t_cut = tc0;
             S.rc = take_window(S);
             S.mode = cfg.mode;
             S.t_enq = now_ns();
@@ -1063,7 +1103,9 @@ struct tm_batcher {
                     S.narrow = false;
                 }
             }
-            ns_enq.fetch_add(now_ns() - S.t_enq, std::memory_order_relaxed);
+            S.t_queued = now_ns();
+            S.epoch = eng ? tmx_engine_epoch(eng) : 0;
+            ns_enq.fetch_add(S.t_queued - S.t_enq, std::memory_order_relaxed);
             {
                 std::lock_guard<std::mutex> g(slot_mu);
                 fifo.push_back(next);
@@ -1356,6 +1398,18 @@ int tm_batcher_stats_reset(tm_batcher *b) {
     std::lock_guard<std::mutex> g(b->st_mu);
     b->lat_gen.fetch_add(1, std::memory_order_acq_rel);
     b->t_window = std::chrono::steady_clock::now();
+    b->win_first.store(b->win_next.load(std::memory_order_relaxed), std::memory_order_relaxed);
+    return TM_OK;
+}
+
+int tm_batcher_windows(tm_batcher *b, tm_batcher_window *out, uint32_t cap, uint32_t *n_out) {
+    if (!b || !n_out || (cap && !out)) return TM_EINVAL;
+    const uint64_t hi = b->win_next.load(std::memory_order_acquire);
+    uint64_t lo = std::max(b->win_first.load(std::memory_order_relaxed),
+                           hi > TM_BATCHER_WINDOWS ? hi - TM_BATCHER_WINDOWS : 0);
+    if (hi - lo > cap) lo = hi - cap;
+    for (uint64_t i = lo; i < hi; i++) out[i - lo] = b->wins[i % TM_BATCHER_WINDOWS];
+    *n_out = (uint32_t)(hi - lo);
     return TM_OK;
 }
 

@@ -588,7 +588,7 @@ struct HostOut {
 // PUBLISHES (under mu_dev), so a match never sees a table mask of a host table that a commit
 // running on another thread has already rehashed but not yet uploaded.
 struct DevView {
-    uint64_t epoch = 0;
+    std::atomic<uint64_t> epoch{0};  // also read without the lock (the aggregator's window trace)
     uint64_t wmask = 0, emask = 0;
     uint64_t n_deep = 0;
     uint64_t max_id = 0;
@@ -5151,6 +5151,10 @@ __attribute__((visibility("hidden"))) int tmx_batch_reserve_matches(tm_engine *e
 __attribute__((visibility("hidden"))) void tmx_lease_take(tm_engine *eng) { eng->lease_take_raw(); }
 __attribute__((visibility("hidden"))) void tmx_lease_drop(tm_engine *eng) { eng->lease_drop_raw(); }
 __attribute__((visibility("hidden"))) int tmx_engine_is_replica(const tm_engine *eng) { return eng->replica ? 1 : 0; }
+// the epoch the device serves (a stamp for the aggregator's window trace: read without the lock)
+__attribute__((visibility("hidden"))) uint64_t tmx_engine_epoch(const tm_engine *eng) {
+    return eng->dv.epoch.load(std::memory_order_relaxed);
+}
 // the runs form on this engine: a master, or a replica that keeps its host id arena
 __attribute__((visibility("hidden"))) int tmx_engine_runs_ok(const tm_engine *eng) {
     return !eng->replica || eng->r_ids ? 1 : 0;

@@ -152,6 +152,28 @@ int tm_batcher_stats_get(tm_batcher *b, tm_batcher_stats *out);
  * Stage times and batch counts are not reset. */
 int tm_batcher_stats_reset(tm_batcher *b);
 
+/* (ABI 10) Per-window stage stamps: where a window's time went, to attribute the latency tail to
+ * a stage.  Nanoseconds on the aggregator's clock (the TSC scaled to ns).  The aggregator keeps
+ * the last TM_BATCHER_WINDOWS windows completed since tm_batcher_stats_reset. */
+#define TM_BATCHER_WINDOWS 16384
+#define TM_WIN_RERUN 1u    /* the window's output was too small: grown and walked again */
+#define TM_WIN_RUNS  2u    /* runs transport (spans of the host id arena) */
+#define TM_WIN_FAILED 4u   /* the window failed as a whole (every publish got the status) */
+typedef struct tm_batcher_window {
+    uint32_t n;            /* publishes */
+    uint32_t flags;        /* TM_WIN_* */
+    uint64_t t_oldest;     /* submit stamp of the window's oldest publish */
+    uint64_t t_cut;        /* the cutter starts taking the window from the queue */
+    uint64_t t_queued;     /* its GPU part queued (bytes H2D, walk, result copies on the stream) */
+    uint64_t t_gpu;        /* the GPU part observed done (including any re-run) */
+    uint64_t t_ready;      /* results copied / D2H queued: handed to the delivery threads */
+    uint64_t t_deliver;    /* the first delivery thread starts on it */
+    uint64_t t_done;       /* its last callback returned */
+    uint64_t epoch;        /* engine epoch when the window was queued (commits between windows) */
+} tm_batcher_window;
+/* Copies up to `cap` of the kept windows, oldest first; *n_out = how many. */
+int tm_batcher_windows(tm_batcher *b, tm_batcher_window *out, uint32_t cap, uint32_t *n_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,6 +7,8 @@
 // as a NIF building its reply list would; with `spans` 1 it takes the span callback
 // (tm_batcher_submit_spans), 3 the u32-span one (tm_batcher_submit_spans32), and reads the ids
 // straight from the engine's id arena.
+#include <cstring>
+#include <cstdio>
 #include <atomic>
 #include <chrono>
 #include <climits>
@@ -114,10 +116,46 @@ void next_or_retire(Pub *p) {
 // latency window is reset (tm_batcher_stats_reset), and at the end of the measured `seconds`,
 // BEFORE the publishers stop and the queue drains, its stats are read into *window: the
 // latency of every publish delivered in the steady state, and how many there were.
+// The cgroup's CPU accounting (cgroup v2 cpu.stat): usage, and how often / how long the CPU
+// quota throttled this job -- a throttled period stops every thread of the process at once.
+// out4: usage_usec, nr_periods, nr_throttled, throttled_usec (all 0 when there is no such file).
+static void cpu_stat(uint64_t *out4) {
+    out4[0] = out4[1] = out4[2] = out4[3] = 0;
+    FILE *f = std::fopen("/sys/fs/cgroup/cpu.stat", "r");
+    if (!f) return;
+    char k[64];
+    unsigned long long v;
+    while (std::fscanf(f, "%63s %llu", k, &v) == 2) {
+        if (!std::strcmp(k, "usage_usec")) out4[0] = v;
+        else if (!std::strcmp(k, "nr_periods")) out4[1] = v;
+        else if (!std::strcmp(k, "nr_throttled")) out4[2] = v;
+        else if (!std::strcmp(k, "throttled_usec")) out4[3] = v;
+    }
+    std::fclose(f);
+}
+
+// loadgen_run3 + what the measured window saw besides latency: the aggregator's per-window stage
+// stamps of the windows completed in it (tm_batcher_windows, read with the stats, before the
+// drain) and the cgroup CPU accounting over it (cpu_stat deltas).
+extern "C" int loadgen_run4(tm_batcher *b, const uint8_t *bytes, const uint32_t *off, uint32_t n_topics,
+                            uint32_t publishers, double warmup_s, double seconds, int spans, uint64_t *published,
+                            uint64_t *ids_out, uint64_t *errors, uint64_t *checksum, double *elapsed_s,
+                            tm_batcher_stats *window, tm_batcher_window *wins, uint32_t wcap, uint32_t *wn,
+                            uint64_t *cg4);
+
 extern "C" int loadgen_run3(tm_batcher *b, const uint8_t *bytes, const uint32_t *off, uint32_t n_topics,
                             uint32_t publishers, double warmup_s, double seconds, int spans, uint64_t *published,
                             uint64_t *ids_out, uint64_t *errors, uint64_t *checksum, double *elapsed_s,
                             tm_batcher_stats *window) {
+    return loadgen_run4(b, bytes, off, n_topics, publishers, warmup_s, seconds, spans, published, ids_out, errors,
+                        checksum, elapsed_s, window, nullptr, 0, nullptr, nullptr);
+}
+
+extern "C" int loadgen_run4(tm_batcher *b, const uint8_t *bytes, const uint32_t *off, uint32_t n_topics,
+                            uint32_t publishers, double warmup_s, double seconds, int spans, uint64_t *published,
+                            uint64_t *ids_out, uint64_t *errors, uint64_t *checksum, double *elapsed_s,
+                            tm_batcher_stats *window, tm_batcher_window *wins, uint32_t wcap, uint32_t *wn,
+                            uint64_t *cg4) {
     if (!b || !bytes || !off || !n_topics || !publishers) return TM_EINVAL;
     Load L;
     L.spans = spans != 0;
@@ -139,11 +177,17 @@ extern "C" int loadgen_run3(tm_batcher *b, const uint8_t *bytes, const uint32_t 
     }
     if (window) {
         std::this_thread::sleep_until(t0 + dur(warmup_s));
+        uint64_t c0[4], c1[4];
+        cpu_stat(c0);
         int rc = tm_batcher_stats_reset(b);
         std::this_thread::sleep_until(t0 + dur(warmup_s + seconds));
         if (!rc) rc = tm_batcher_stats_get(b, window);
+        cpu_stat(c1);
+        if (!rc && wins && wn) rc = tm_batcher_windows(b, wins, wcap, wn);
         L.deadline = clk::now().time_since_epoch().count();  // now the publishers stop
         if (rc) window->lat_count = 0;
+        if (cg4)
+            for (int k = 0; k < 4; k++) cg4[k] = c1[k] - c0[k];
     }
     {
         std::unique_lock<std::mutex> lk(L.m);
