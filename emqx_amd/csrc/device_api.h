@@ -41,7 +41,7 @@ constexpr uint32_t CTL_BYTES = 32, CTL_CURSOR = 0, CTL_SLOW = 8, CTL_SEG = 16, C
 #define TM_BND_FILE 0
 #endif
 struct BndCaps {
-    uint64_t bytes, off, wtab, warena, word_off, etab, slot_list, arena, key_bin, key_rec;  // inputs, index
+    uint64_t bytes, off, wtab, warena, word_off, etab, slot_list, arena, key_bin, key_rec, key_dd;  // inputs, index
     uint64_t out, keys, slow_list, scratch, seg_pool, wave_chunks, fr_pool, wave_info;     // outputs, scratch
 };
 #if TM_BOUNDS && defined(__HIP_DEVICE_COMPILE__)
@@ -139,6 +139,15 @@ struct MatchArgs {
     unsigned long long *stats;
     // optional: events recorded around k_match_fast on the launch stream
     hipEvent_t ev_fast0, ev_fast1;
+    // [unique] / aggre/1 (round 5): dd_bit = KDD_MULTI or KDD_SHARED, else 0.  The walk also
+    // counts, per topic, the keys of its lists whose header collapse bit (layout.h HDR_DD) has
+    // dd_bit, inline keys by their own key_dd flag; a topic with fewer than two is final
+    // (ucnt[t] = its count), the others go to the reducer's worklist wl {topic, that count}.
+    uint32_t dd_bit;
+    const uint8_t *key_dd;
+    uint32_t *ucnt;
+    uint2 *wl;
+    uint32_t *wl_n;
     // Real capacities (elements) of the buffers above, and the bounds record: read only by the
     // TM_BOUNDS debug build, whose kernels check every index against them (BI() above).
     BndCaps cap;
@@ -225,6 +234,10 @@ constexpr uint8_t KDD_SHARED = 2;  // AGGRE: the key's dest is a shared-subscrip
 hipError_t launch_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off, uint32_t *keys, uint64_t keys_cap,
                          const uint64_t *key_rec, const uint32_t *key_node, const uint8_t *key_dd, uint32_t n,
                          uint32_t *ucnt, uint32_t *scratch, uint2 *wl, uint32_t *wl_n, hipStream_t stream);
+// k_dedupe alone, over the worklist a walk with MatchArgs.dd_bit left (round 5: no k_dd_pass)
+hipError_t launch_dedupe_wl(uint32_t mode, const uint32_t *cnt, const uint32_t *off, uint32_t *keys,
+                            const uint64_t *key_rec, const uint32_t *key_node, const uint8_t *key_dd, uint32_t n,
+                            uint32_t *ucnt, uint32_t *scratch, const uint2 *wl, const uint32_t *wl_n, hipStream_t stream);
 hipError_t launch_scatter1(uint8_t *dst, const uint64_t *idx, const uint8_t *src, uint64_t n, hipStream_t stream,
                            uint64_t dst_cap = ~0ull, unsigned long long *bnd = nullptr);
 hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *src, uint64_t n, hipStream_t stream,

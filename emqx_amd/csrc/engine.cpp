@@ -16,6 +16,7 @@
 // from it (SURVEY.md §5 checkpoint/resume).
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
 #include <sys/mman.h>
 
 #include <algorithm>
@@ -432,7 +433,27 @@ static void sort_unique(std::vector<uint64_t> &v) {
     }
     v.erase(std::unique(v.begin(), v.end()), v.end());
 }
-static unsigned commit_threads() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }
+// CPUs this process may keep busy at once: its affinity set, cut to the cgroup's CPU quota
+// (cpu.max).  Past the quota a job's threads all stop until the period ends (the GPU boxes
+// here grant 16 CPUs per 100 ms period while every CPU of the machine is in the affinity set),
+// so parallel phases never use more helpers than this.
+static unsigned usable_cpus() {
+    static const unsigned n = [] {
+        unsigned c = std::max(1u, std::thread::hardware_concurrency());
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof set, &set) == 0) c = std::min<unsigned>(c, (unsigned)CPU_COUNT(&set));
+        if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {0};
+            unsigned long long per = 0;
+            if (fscanf(f, "%31s %llu", q, &per) == 2 && strcmp(q, "max") != 0 && per)
+                c = std::min<unsigned>(c, (unsigned)std::max(1ull, strtoull(q, nullptr, 10) / per));
+            fclose(f);
+        }
+        return std::max(1u, c);
+    }();
+    return n;
+}
+static unsigned commit_threads() { return std::max(1u, std::min(16u, usable_cpus())); }
 
 // A few resident threads that split large host copies (staging a pageable batch into pinned
 // memory): thread start-up per copy would cost more than the copy of one sub-batch.
@@ -810,6 +831,7 @@ struct tm_engine {
             if (e.solo != NONE) {  // the id's first key meets a second one: flag it too
                 keys[e.solo]._p[0] |= KR_MULTI;
                 dirty_kid.push_back(e.solo);
+                dd_touch.push_back(e.solo);  // its list's header bit (lists_dd_touch)
                 e.solo = NONE;
             }
             keys[h]._p[0] |= KR_MULTI;
@@ -822,6 +844,20 @@ struct tm_engine {
         e.solo = NONE;  // a key left behind was flagged when the count reached 2
     }
     std::vector<std::string> dead_filter;  // by key handle (only K_DEAD entries non-empty)
+    // keys flagged KR_MULTI this epoch whose list may not be rewritten by it: their lists' header
+    // collapse bits are OR'd in after the lists are placed (lists_dd_touch)
+    std::vector<uint32_t> dd_touch;
+    void lists_dd_touch() {
+        for (uint32_t h : dd_touch) {
+            const KeyRec &k = keys[h];
+            if (k.kind == K_FREE || k.kind == K_DEAD) continue;
+            const uint32_t lo = node_list[k.node].list_off;
+            if (!lo || (arena[lo - HDR_DD] & KDD_MULTI)) continue;
+            arena[lo - HDR_DD] |= KDD_MULTI;
+            if (!need_full && lo - HDR_DD < arena_dev) dirty_arena.push_back(lo - HDR_DD);
+        }
+        dd_touch.clear();
+    }
 
     // ---- staged ops and epoch deltas
     std::vector<StagedOp> staged;
@@ -893,6 +929,7 @@ struct tm_engine {
     bool timing_on = false;
     bool topic_words = false;  // the batch being enqueued holds word-list topics (TM_MATCH_TOPIC_WORDS)
     uint32_t runs_w = 8;       // the MODE_RUNS batch being enqueued: id width of its spans (4: arena_id32)
+    uint32_t dd_next = 0;      // the next enqueue_match counts collapsible keys for this KDD_* bit (under mu_dev)
 
     uint64_t edge_load_inv() const { return cfg.edge_load_inv ? cfg.edge_load_inv : EDGE_LOAD_INV; }
     uint64_t node_budget() const {  // trie nodes below the root
@@ -987,6 +1024,7 @@ struct tm_engine {
         c.arena = d_arena.cap / 4;
         c.key_bin = d_key_bin.cap / 4;
         c.key_rec = d_key_rec.cap / 8;
+        c.key_dd = d_key_dd.cap;
         c.out = std::min(std::min(bnd_cap_of(a.out_off, 4), bnd_cap_of(a.out_cnt, 4)), bnd_cap_of(a.status, 4));
         if (a.mode == MODE_RUNS) c.out = std::min(c.out, bnd_cap_of(a.out_kcnt, 4));
         c.keys = bnd_cap_of(a.keys, kel);
@@ -1692,13 +1730,20 @@ struct tm_engine {
     // where "min" = the key with the smallest id of that kind (NONE if none).  A node's keys
     // all spell the same filter per kind, so these are the return_first candidates
     // (k_match_first) without scanning the list.
+    // the KDD_* flags a key carries on the device (key_dev_rec), OR'd into its list's header
+    uint32_t key_dd_bits(uint32_t h) const {
+        const KeyRec &k = keys[h];
+        return ((k._p[0] & KR_MULTI) ? KDD_MULTI : 0u) | ((k.id & TM_ID_SHARED) ? KDD_SHARED : 0u);
+    }
     void write_header(uint32_t pos, const uint32_t *terms, uint32_t tc, const uint32_t *hashes, uint32_t hc) {
-        uint32_t mb = NONE, mw = NONE, mh = NONE;
+        uint32_t mb = NONE, mw = NONE, mh = NONE, dd = 0;
         auto take = [&](uint32_t &m, uint32_t h) {
             if (m == NONE || keys[h].id < keys[m].id) m = h;
+            dd |= key_dd_bits(h);
         };
         for (uint32_t i = 0; i < tc; i++) take(keys[terms[i]].kind == K_EXACT_BIN ? mb : mw, terms[i]);
         for (uint32_t i = 0; i < hc; i++) take(mh, hashes[i]);
+        arena[pos - HDR_DD] = dd;
         arena[pos - 5] = mb;
         arena[pos - 4] = mw;
         arena[pos - 3] = mh;
@@ -1773,7 +1818,7 @@ struct tm_engine {
     struct NewList {
         std::vector<uint32_t> keys;  // term keys, then '#' keys
         std::vector<uint64_t> ids;   // their ids (the host id arena's words)
-        uint32_t tc = 0, hc = 0, mb = NONE, mw = NONE, mh = NONE;
+        uint32_t tc = 0, hc = 0, mb = NONE, mw = NONE, mh = NONE, dd = 0;
     };
     void build_list(size_t i, size_t j, NewList &L) const {
         const uint32_t node = deltas[i].node;
@@ -1801,11 +1846,13 @@ struct tm_engine {
         for (uint32_t q = 0; q < L.tc + L.hc; q++) {
             const uint32_t h = L.keys[q];
             L.ids[q] = keys[h].id;
+            L.dd |= key_dd_bits(h);
             if (q < L.tc) take(keys[h].kind == K_EXACT_BIN ? L.mb : L.mw, h);
             else take(L.mh, h);
         }
     }
     void place_header(uint32_t pos, const NewList &L) {
+        arena[pos - HDR_DD] = L.dd;
         arena[pos - 5] = L.mb;
         arena[pos - 4] = L.mw;
         arena[pos - 3] = L.mh;
@@ -2644,6 +2691,7 @@ struct tm_engine {
                 ids_stale)
                 rebuild_arena();
         }
+        lists_dd_touch();  // (a full rebuild wrote every header from the key flags already)
         tick(full ? "rebuild_arena" : "apply_deltas");
         if (trace && !full)
             tr += " [lists=" + std::to_string(ad_us[0]) + " inplace=" + std::to_string(ad_us[1]) + " moved=" +
@@ -3297,6 +3345,22 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
                                 const TopicOut *to = nullptr, uint32_t tpw = 0) {
     MatchArgs a{};
     a.mode = mode;
+    // [unique] / aggre/1 (set by the caller for this launch only): the walk counts each topic's
+    // collapsible keys and leaves k_dedupe its worklist
+    const uint32_t dd = eng->dd_next;
+    eng->dd_next = 0;
+    if (dd && mode == MODE_ALL && !to) {
+        hipError_t e;
+        if ((e = eng->grow_buf(eng->bb->d_ucnt, (uint64_t)(obase + n) * 4 + 4)) ||
+            (e = eng->grow_buf(eng->bb->d_dd_wl, (uint64_t)n * 8 + 8)) || (e = eng->grow_buf(eng->bb->d_dd_wl_n, 4)) ||
+            (e = hipMemsetAsync(eng->bb->d_dd_wl_n.p, 0, 4, s)))
+            return e;
+        a.dd_bit = dd;
+        a.key_dd = eng->d_key_dd.as<uint8_t>();
+        a.ucnt = eng->bb->d_ucnt.as<uint32_t>() + obase;
+        a.wl = eng->bb->d_dd_wl.as<uint2>();
+        a.wl_n = eng->bb->d_dd_wl_n.as<uint32_t>();
+    }
     a.tpw = pick_tpw(n, tpw ? tpw : eng->cfg.topics_per_wave);
     a.first_dfs = eng->dv.n_deep ? 1u : 0u;
     a.key_bin = eng->d_key_bin.as<uint32_t>();
@@ -3372,20 +3436,21 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
 // UNIQUE / AGGRE on the GPU: k_dedupe reduces the full result of the batch just enqueued
 // in place in d_keys, the reduced counts in d_ucnt.
 static bool reduced_mode(uint32_t mode) { return mode == TM_MATCH_UNIQUE || mode == TM_MATCH_AGGRE; }
+static uint32_t dd_bit_of(uint32_t mode) { return mode == TM_MATCH_UNIQUE ? KDD_MULTI : KDD_SHARED; }
 
+// The walk just enqueued (with dd_next set) wrote the final count of every topic that cannot
+// collapse and listed the others; k_dedupe reduces those in place (round 5: k_dd_pass, a second
+// read of every key and a gather of every key's flag, is gone).
 static int enqueue_reduce(tm_engine *eng, uint32_t mode, uint32_t n, hipStream_t s) {
     if (eng->bb->ukeys_cap < eng->bb->keys_cap) {
         TM_TRY_HIP(eng->grow_buf(eng->bb->d_ukeys, eng->bb->keys_cap * 4), TM_ENOMEM, "alloc reduced keys");
         eng->bb->ukeys_cap = eng->bb->keys_cap;
     }
-    TM_TRY_HIP(eng->grow_buf(eng->bb->d_ucnt, (uint64_t)n * 4 + 4), TM_ENOMEM, "alloc reduced counts");
-    TM_TRY_HIP(eng->grow_buf(eng->bb->d_dd_wl, (uint64_t)n * 8), TM_ENOMEM, "alloc reducer worklist");
-    TM_TRY_HIP(eng->grow_buf(eng->bb->d_dd_wl_n, 4), TM_ENOMEM, "alloc reducer worklist");
-    TM_TRY_HIP(launch_dedupe(mode == TM_MATCH_UNIQUE ? DD_UNIQUE : DD_AGGRE, eng->bb->d_outcnt.as<uint32_t>(),
-                             eng->bb->d_outoff.as<uint32_t>(), eng->bb->d_keys.as<uint32_t>(), eng->bb->keys_cap,
-                             eng->d_key_rec.as<uint64_t>(), eng->d_key_node.as<uint32_t>(),
-                             eng->d_key_dd.as<uint8_t>(), n, eng->bb->d_ucnt.as<uint32_t>(), eng->bb->d_ukeys.as<uint32_t>(),
-                             eng->bb->d_dd_wl.as<uint2>(), eng->bb->d_dd_wl_n.as<uint32_t>(), s),
+    TM_TRY_HIP(launch_dedupe_wl(mode == TM_MATCH_UNIQUE ? DD_UNIQUE : DD_AGGRE, eng->bb->d_outcnt.as<uint32_t>(),
+                                eng->bb->d_outoff.as<uint32_t>(), eng->bb->d_keys.as<uint32_t>(),
+                                eng->d_key_rec.as<uint64_t>(), eng->d_key_node.as<uint32_t>(), eng->d_key_dd.as<uint8_t>(),
+                                n, eng->bb->d_ucnt.as<uint32_t>(), eng->bb->d_ukeys.as<uint32_t>(),
+                                eng->bb->d_dd_wl.as<uint2>(), eng->bb->d_dd_wl_n.as<uint32_t>(), s),
                TM_EDEVICE, "dedupe");
     return TM_OK;
 }
@@ -3615,6 +3680,7 @@ static int match_batch_impl(tm_engine *eng, const uint8_t *bytes, const uint32_t
                 B.keys_cap = want;
             }
             B.last_n = n;
+            if (dev_reduce) eng->dd_next = dd_bit_of(mode);  // the walk counts collapsible keys
             TM_TRY_HIP(enqueue_match(eng, B.d_bytes.as<uint8_t>(), B.d_off.as<uint32_t>(), n, s, kmode), TM_EDEVICE,
                        "kernel launch");
             TM_TRY_HIP(eng->note_use(s), TM_EDEVICE, "event");
@@ -3843,6 +3909,7 @@ static int match_device_impl(tm_engine *eng, BatchBufs *set, const uint8_t *d_by
         TM_TRY_HIP(eng->grow_buf(eng->bb->d_keys, (uint64_t)n * 4), TM_ENOMEM, "alloc keys");
         eng->bb->keys_cap = n;
     }
+    if (reduced_mode(mode)) eng->dd_next = dd_bit_of(mode);  // the walk counts collapsible keys
     TM_TRY_HIP(enqueue_match(eng, d_bytes, d_off, n, s, kmode), TM_EDEVICE, "kernel launch");
     eng->bb->last_mode = mode;
     eng->bb->dev_batch = true;

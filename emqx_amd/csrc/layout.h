@@ -54,10 +54,16 @@ constexpr uint32_t I_INL_HASH = 1u << 27;   // M_INLINE: the key is a '#' key (e
 constexpr uint32_t I_KEY_MASK = (1u << 27) - 1;  // M_INLINE: the key handle
 constexpr uint32_t INLINE_KEY_LIMIT = 1u << 27;  // handles >= this never go inline
 constexpr uint32_t CNT_BITS = 14, CNT_MAX = (1u << CNT_BITS) - 1;
-// List header words before a list's first key (lo): lo-5 smallest-id {Binary,{ID}} term key,
-// lo-4 smallest-id word-list term key, lo-3 smallest-id '#' key (NONE if none), lo-2
-// term_cnt, lo-1 hash_cnt.
-constexpr uint32_t LIST_HDR = 5;
+// List header words before a list's first key (lo): lo-6 the list's collapse bits (below),
+// lo-5 smallest-id {Binary,{ID}} term key, lo-4 smallest-id word-list term key, lo-3
+// smallest-id '#' key (NONE if none), lo-2 term_cnt, lo-1 hash_cnt.
+constexpr uint32_t LIST_HDR = 6;
+// lo-6: the OR over the list's keys of their device_api.h KDD_* flags (bit 0: the key's id is
+// carried by another live key, so [unique] may collapse it; bit 1: a shared-subscription dest,
+// which aggre/1 may collapse).  Kept as a superset (a bit is never cleared before the list is
+// rewritten): the [unique] / aggre walks count a list's keys as collapsible only when its bit is
+// set, so a topic none of whose lists carries one is final without reading its keys again.
+constexpr uint32_t HDR_DD = 6;
 
 TM_HD uint32_t info_mode(uint32_t info) { return (info >> I_MODE_SHIFT) & 3u; }
 TM_HD uint32_t info_term_cnt(uint32_t info) { return (info >> CNT_BITS) & CNT_MAX; }

@@ -58,6 +58,8 @@ constexpr uint32_t SEG_NODE = 1u << 9;      // segment.w flag: .x is a node (slo
                                             // offset is read from slot_list at copy-out
 constexpr uint32_t SEG_SKIP_SHIFT = 11;     // with SEG_NODE: keys to skip (term_cnt for the
                                             // '#' part) in .w bits 11-31
+constexpr uint32_t SEG_DD = 1u << 10;       // list segment (not SEG_NODE): its list's header has
+                                            // the batch's collapse bit (MatchArgs.dd_bit)
 constexpr uint32_t DO_PLUS = 0x80u, DO_LIT = 0x40u;  // frontier meta: probes this entry needs
 #ifndef TM_RPL
 #define TM_RPL 2
@@ -354,12 +356,25 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
         uint4 g = make_uint4(0u, 0u, 0u, 0u);
         if (j < ns) {
             g = L.seg[j];
+            bool dd_list = (g.w & SEG_DD) != 0;
             if (g.w & SEG_NODE) {  // M_CNT list: its offset is read now, off the walk
-                g.x = a.slot_list[BI(g.x, slot_list)] + (g.w >> SEG_SKIP_SHIFT);
+                const uint32_t lo = a.slot_list[BI(g.x, slot_list)];
+                if constexpr (OUT == O_KEYS)
+                    if (a.dd_bit) dd_list = (a.arena[BI(lo - HDR_DD, arena)] & a.dd_bit) != 0;
+                g.x = lo + (g.w >> SEG_SKIP_SHIFT);
                 g.w &= 0xFFu | SEG_INLINE;
                 L.seg[j] = g;
             }
             if ((L.spill >> (g.w & 0x3Fu)) & 1ull) g.y = 0;  // spilled topic: the slow kernel owns it
+            if constexpr (OUT == O_KEYS) {
+                // [unique] / aggre/1: the topic's keys that may collapse (a list's whole count
+                // when its header bit is set; an inline key by its own flag), L.nlev reused
+                if (a.dd_bit && g.y) {
+                    const uint32_t c = (g.w & SEG_INLINE) ? ((a.key_dd[BI(g.x, key_dd)] & a.dd_bit) ? 1u : 0u)
+                                                          : (dd_list ? g.y : 0u);
+                    if (c) atomicAdd(&L.nlev[g.w & 0x3Fu], c);
+                }
+            }
         }
         const bool is_long = g.y > (uint32_t)CP_SHORT;
         if (!is_long && g.y) {
@@ -593,7 +608,9 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
         uint32_t tot;
         const uint32_t pos = wave_excl_scan(em ? 1u : 0u, &tot);
         if (em) {
-            L.seg[pos] = make_uint4(R.list_off, R.hash_cnt, 0u, lane);
+            const uint32_t fl = (OUT == O_KEYS && a.dd_bit && (a.arena[BI(R.list_off - HDR_DD, arena)] & a.dd_bit))
+                                    ? SEG_DD : 0u;
+            L.seg[pos] = make_uint4(R.list_off, R.hash_cnt, 0u, lane | fl);
             if constexpr (RUNS) {
                 L.cnt[lane] = 1;
                 L.tbase[lane] = R.hash_cnt;
@@ -839,9 +856,11 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                         } else if (m == M_REC) {
                             const uint32_t lo = a.slot_list[BI(r.child, slot_list)];
                             const uint32_t tc = a.arena[BI(lo - 2, arena)], hc = a.arena[BI(lo - 1, arena)];
+                            const uint32_t ddf =
+                                (OUT == O_KEYS && a.dd_bit && (a.arena[BI(lo - HDR_DD, arena)] & a.dd_bit)) ? SEG_DD : 0u;
                             st_rec++;
-                            put(lo, last[k] ? tc : 0u, 0u);
-                            put(lo + tc, hc, 0u);
+                            put(lo, last[k] ? tc : 0u, ddf);
+                            put(lo + tc, hc, ddf);
                         }
                     }
                 }
@@ -959,6 +978,8 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
         sb = __shfl(sb, 0, WAVE);
         if (spill) a.slow_list[BI(sb + ps, slow_list)] = t;
     }
+    if constexpr (OUT == O_KEYS)
+        if (a.dd_bit) L.nlev[lane] = 0;  // the walk is done with it: collapsible keys per topic
     __syncthreads();
 
     // ---- 5. load-balanced expansion: staged segments, then flushed chunks
@@ -975,6 +996,15 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
             for (uint32_t j = lane; j < (uint32_t)SCAP; j += WAVE) L.seg[j] = src[j];
             __syncthreads();
             expand_segments<OUT>(a, L, SCAP);
+        }
+    }
+    if constexpr (OUT == O_KEYS) {
+        // [unique] / aggre/1: a topic with fewer than two keys that may collapse is final as it
+        // stands; the others go to k_dedupe's worklist (the walk's reads replace k_dd_pass's)
+        if (a.dd_bit && !overflow && active && !spill) {
+            const uint32_t pf = L.nlev[lane];
+            if (walk && pf >= 2) a.wl[BI(atomicAdd(a.wl_n, 1u), out)] = make_uint2(t, pf);
+            else a.ucnt[BI(t, out)] = my;
         }
     }
 
@@ -1116,8 +1146,13 @@ __global__ __launch_bounds__(WAVE) void k_match_slow(MatchArgs a) {
         a.status[BI(t, out)] = 0;
         st_keys += c;
         if (a.mode == MODE_RUNS) a.out_kcnt[BI(t, out)] = c;
-        if (a.mode != MODE_COUNT && pos + c <= a.keys_cap)  // output slots: keys, spans or ids
+        if (a.mode != MODE_COUNT && pos + c <= a.keys_cap) {  // output slots: keys, spans or ids
             dfs_walk<true>(a, R, wid, stk, nl, dollar, pos, &st_probe, &st_visit, ns);
+            if (a.dd_bit) {  // [unique] / aggre/1: the reducer decides (no per-list bits here)
+                if (c >= 2) a.wl[BI(atomicAdd(a.wl_n, 1u), out)] = make_uint2(t, c);
+                else a.ucnt[BI(t, out)] = c;
+            }
+        }
     }
     if constexpr (STATS) {
         // levels were already counted by the fast kernel's pre-scan

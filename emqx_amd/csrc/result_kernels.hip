@@ -710,6 +710,15 @@ __global__ __launch_bounds__(64) void k_dedupe(uint32_t mode, const uint32_t *cn
     }
 }
 
+hipError_t launch_dedupe_wl(uint32_t mode, const uint32_t *cnt, const uint32_t *off, uint32_t *keys,
+                            const uint64_t *key_rec, const uint32_t *key_node, const uint8_t *key_dd, uint32_t n,
+                            uint32_t *ucnt, uint32_t *scratch, const uint2 *wl, const uint32_t *wl_n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint32_t grid = n < 4096u ? n : 4096u;
+    k_dedupe<<<grid, 64, 0, s>>>(mode, cnt, off, keys, key_rec, key_node, key_dd, wl, wl_n, ucnt, scratch);
+    return hipGetLastError();
+}
+
 hipError_t launch_dedupe(uint32_t mode, const uint32_t *cnt, const uint32_t *off, uint32_t *keys, uint64_t keys_cap,
                          const uint64_t *key_rec, const uint32_t *key_node, const uint8_t *key_dd, uint32_t n,
                          uint32_t *ucnt, uint32_t *scratch, uint2 *wl, uint32_t *wl_n, hipStream_t s) {

@@ -31,9 +31,39 @@ def gpu_local_cpus(device: int = 0):
     return sorted(cpus) or None
 
 
+def cgroup_quota_cpus():
+    """The cgroup v2 CPU quota (cpu.max) in whole CPUs, or None when unlimited / unknown."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        return None
+
+
+def one_per_core(cpus, k):
+    """k of `cpus`, one per physical core first (SMT siblings only when the cores run out)."""
+    seen, first, rest = set(), [], []
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            core = (open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip())
+        except OSError:
+            core = ("?", str(c))
+        (rest if core in seen else first).append(c)
+        seen.add(core)
+    return sorted((first + rest)[:k])
+
+
 def pin_to_gpu(device: int = 0) -> dict:
     """Restrict this process (and the threads it creates later) to the GPU-local CPUs that
-    it may use.  Returns what was done, for the bench line."""
+    it may use.  Returns what was done, for the bench line.
+
+    Under a cgroup CPU quota (the GPU boxes here: cpu.max 16 CPUs per 100 ms period, while the
+    process may run on every CPU of the machine) the set is cut to as many CPUs as the quota
+    grants, one per physical core: with more runnable threads than that on more CPUs, the job
+    spends its quota before the period ends and EVERY thread stops for the rest of it (tens of
+    milliseconds: round 4's aggregator tail).  On exactly `quota` CPUs it can
+    never run ahead of its quota; extra threads time-slice instead."""
     local = gpu_local_cpus(device)
     before = sorted(os.sched_getaffinity(0))
     if not local:
@@ -41,5 +71,9 @@ def pin_to_gpu(device: int = 0) -> dict:
     use = sorted(set(local) & set(before))
     if not use:
         return {"pinned": False, "reason": "no GPU-local CPU in this process's affinity"}
+    quota = cgroup_quota_cpus()
+    if quota and quota < len(use):
+        use = one_per_core(use, quota)
     os.sched_setaffinity(0, use)
-    return {"pinned": True, "cpus": len(use), "of": len(before)}
+    return {"pinned": True, "cpus": len(use), "of": len(before), "quota_cpus": quota,
+            "gpu_local_cpus": len(local)}
