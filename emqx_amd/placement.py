@@ -54,7 +54,7 @@ def one_per_core(cpus, k):
     return sorted((first + rest)[:k])
 
 
-def pin_to_gpu(device: int = 0) -> dict:
+def pin_to_gpu(device: int = 0, quota_cut: bool = True) -> dict:
     """Restrict this process (and the threads it creates later) to the GPU-local CPUs that
     it may use.  Returns what was done, for the bench line.
 
@@ -72,7 +72,7 @@ def pin_to_gpu(device: int = 0) -> dict:
     if not use:
         return {"pinned": False, "reason": "no GPU-local CPU in this process's affinity"}
     quota = cgroup_quota_cpus()
-    if quota and quota < len(use):
+    if quota_cut and quota and quota < len(use):
         use = one_per_core(use, quota)
     os.sched_setaffinity(0, use)
     return {"pinned": True, "cpus": len(use), "of": len(before), "quota_cpus": quota,

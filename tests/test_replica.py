@@ -372,3 +372,63 @@ def test_replicated_gloo_world2_real_engines_gpu():
     assert r_out == m_out  # the replica answers exactly as the master, every epoch
     assert m_kinds == r_kinds == [ReplicatedIndex.SYNC_PATCH, ReplicatedIndex.SYNC_IMAGE, ReplicatedIndex.SYNC_NONE]
     assert m_out[1] != m_out[0] and any(len(x) for x in m_out[1])
+
+
+def _gpu_worker_d(rank, world, port, q):
+    """Config D in mode 1 (100 M filters fit one MI355X, so D is replicated, not
+    sharded): rank 0 builds the master over ALL of D's keys (scale 0.002 here: 200 K keys,
+    8-level topics), rank 1 gets a replica from the broadcast image; each rank matches ITS half
+    of the publishes (the data-parallel split of the bench's step) and returns its sets."""
+    import torch
+    import torch.distributed as dist
+    from emqx_amd.replica import EngineReplicaAdapter
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        w = workloads.generate("D", scale=0.002, n_topics=4000)
+        eng = None
+        if rank == 0:
+            eng = N.Engine(0, record_patch=True)
+            eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+            eng.commit()
+        ad = EngineReplicaAdapter(0, eng)
+        ReplicatedIndex(ad, rank, world).start()
+        lo, hi = rank * w.n_topics // world, (rank + 1) * w.n_topics // world
+        tb, to = w.topic_slice(lo, hi)
+        part = workloads.Workload("D", w.f_bytes, w.f_off, w.f_id, tb, np.ascontiguousarray(to, dtype=np.uint32))
+        st, sets = _sets(ad.eng, part)
+        q.put((rank, (lo, hi, st.tolist(), sets), None))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_replicated_config_d_gloo_world2_vs_oracle_gpu():
+    """Config D replicated over two ranks (a master and an image-fed replica on the box's GPU):
+    the publishes split between the ranks, every topic's route-id set equal to the oracle's
+    over ALL of D's keys (the unsharded index), on both ranks."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gpu_worker_d, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in ps], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=60)
+    for r in res:
+        assert r[2] is None, r[2]
+    w = workloads.generate("D", scale=0.002, n_topics=4000)
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    eo, eids, est = ix.match(w.t_bytes, w.t_off)
+    for _, (lo, hi, st, sets), _ in res:
+        assert st == est[lo:hi].tolist()
+        for k, t in enumerate(range(lo, hi)):
+            assert sets[k] == sorted(eids[eo[t]:eo[t + 1]].tolist()), t
+    assert sum(len(s) for r in res for s in r[1][3]) > 0

@@ -20,9 +20,9 @@ def main():
 
     from emqx_amd import _native as N
     from emqx_amd import workloads as W
-    if os.environ.get("PIN"):
+    if os.environ.get("PIN"):  # PIN=1: the GPU's socket cut to the cgroup quota; PIN=socket: the whole socket
         from emqx_amd import placement
-        print(json.dumps({"placement": placement.pin_to_gpu(0)}), flush=True)
+        print(json.dumps({"placement": placement.pin_to_gpu(0, quota_cut=os.environ["PIN"] != "socket")}), flush=True)
     t0 = time.time()
     w = W.generate("C", scale=float(os.environ.get("SCALE", "1.0")), n_topics=1_000_000)
     eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
@@ -35,6 +35,9 @@ def main():
     U = C.POINTER(C.c_uint64)
     lg.loadgen_run3.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_double, C.c_double,
                                 C.c_int, U, U, U, U, C.POINTER(C.c_double), C.POINTER(N.tm_batcher_stats)]
+    lg.loadgen_run4.argtypes = lg.loadgen_run3.argtypes + [C.POINTER(N.tm_batcher_window), C.c_uint32,
+                                                           C.POINTER(C.c_uint32), U]
+    import bench
     if os.environ.get("HOSTPATH"):  # tm_match_batch with host buffers, 1 M publishes per call
         eng.match_packed_view(tb, to32)
         ts = []
@@ -59,8 +62,11 @@ def main():
         b = N.Batcher(eng, max_batch=mb, max_wait_us=wait, delivery_threads=th, transport=tr)
         got, ids, errs, cs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
         win = N.tm_batcher_stats()
-        rc = lg.loadgen_run3(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, 0.5, 2.0, sp, C.byref(got),
-                             C.byref(ids), C.byref(errs), C.byref(cs), C.byref(el), C.byref(win))
+        wbuf = (N.tm_batcher_window * N.TM_BATCHER_WINDOWS)()
+        wn, cg = C.c_uint32(), (C.c_uint64 * 4)()
+        rc = lg.loadgen_run4(b.h, tb.ctypes.data, to32.ctypes.data, len(to32) - 1, pubs, 0.5, 2.0, sp, C.byref(got),
+                             C.byref(ids), C.byref(errs), C.byref(cs), C.byref(el), C.byref(win), wbuf,
+                             N.TM_BATCHER_WINDOWS, C.byref(wn), cg)
         st = b.stats()
         b.close()
         print(json.dumps({"publishers": pubs, "threads": th, "max_wait_us": wait, "transport": tr, "spans": sp,
@@ -72,6 +78,9 @@ def main():
                           "mean_batch": round(st["publishes"] / max(st["batches"], 1), 1),
                           "mean_ms": round(win.lat_mean_us / 1e3, 3),
                           "p50_ms": round(win.lat_p50_us / 1e3, 3), "p99_ms": round(win.lat_p99_us / 1e3, 3),
+                          "p999_ms": round(win.lat_p999_us / 1e3, 3), "max_ms": round(win.lat_max_us / 1e3, 3),
+                          "throttled_ms": round(cg[3] / 1e3, 3), "usage_cpus": round(cg[0] * 1e-6 / win.window_s, 2),
+                          "windows": bench.window_stages(wbuf, wn.value),
                           "busy": {k: round(st[k + "_us"] * 1e-6 / el.value, 3)
                                    for k in ("cut", "enqueue", "gpu_wait", "copy", "deliver")}}), flush=True)
 

@@ -69,6 +69,10 @@ VARIANTS = {
     "plushash": (["-DTM_PLUS_NEAR=0"], 0),  # '+' edges hashed like every other edge (the product)
     "plusnear2": (["-DTM_PLUS_NEAR=1"], 0),
     "plushash2": (["-DTM_PLUS_NEAR=0"], 0),
+    # round 5: edge-table load (translation pressure vs probe-chain length), 2 / 4 / 8 GiB
+    "el2": ([], 2),
+    "el4": ([], 4),
+    "el8": ([], 8),
 }
 
 
