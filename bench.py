@@ -200,16 +200,25 @@ def window_stages(wbuf, n):
     if not n:
         return None
     f = {k: np.array([getattr(wbuf[i], k) for i in range(n)], dtype=np.float64)
-         for k in ("n", "flags", "t_oldest", "t_cut", "t_queued", "t_gpu", "t_ready", "t_deliver", "t_done", "epoch")}
+         for k in ("n", "flags", "t_oldest", "t_cut", "t_queued", "t_gpu", "t_ready", "t_deliver", "t_done", "epoch",
+                   "t_slot", "cut_cpu_us", "cut_ivcsw", "wait_ivcsw", "del_cpu_us", "del_wall_us", "del_ivcsw")}
     t_del = np.where(f["t_deliver"] > 0, f["t_deliver"], f["t_ready"])
+    t_slot = np.clip(f["t_slot"], f["t_oldest"], f["t_cut"])
     st = {"wait": f["t_cut"] - f["t_oldest"], "cut": f["t_queued"] - f["t_cut"], "gpu": f["t_gpu"] - f["t_queued"],
-          "ready": f["t_ready"] - f["t_gpu"], "queue": t_del - f["t_ready"], "deliver": f["t_done"] - t_del}
+          "ready": f["t_ready"] - f["t_gpu"], "queue": t_del - f["t_ready"], "deliver": f["t_done"] - t_del,
+          # wait = fill (the window filling / max_wait polling) + slot (no free slot: pipeline full)
+          "wait_fill": t_slot - f["t_oldest"], "wait_slot": f["t_cut"] - t_slot,
+          # CPU the cutter spent in its cut stage, and the delivery threads' CPU over their wall
+          "cut_cpu": f["cut_cpu_us"] * 1e3, "del_cpu": f["del_cpu_us"] * 1e3, "del_wall": f["del_wall_us"] * 1e3}
+    cnt = {"cut_ivcsw": f["cut_ivcsw"], "wait_ivcsw": f["wait_ivcsw"], "del_ivcsw": f["del_ivcsw"]}
     span = f["t_done"] - f["t_oldest"]
     order = np.argsort(span)
     k1 = max(1, n // 100)
 
     def ms(idx):
-        return {k: round(float(np.mean(v[idx])) / 1e6, 3) for k, v in st.items()}
+        out = {k: round(float(np.mean(v[idx])) / 1e6, 3) for k, v in st.items()}
+        out.update({k: round(float(np.mean(v[idx])), 2) for k, v in cnt.items()})  # counts, not ms
+        return out
     worst = int(order[-1])
     gaps = np.diff(np.sort(f["t_cut"])) if n > 1 else np.zeros(1)
     return {"windows": int(n), "mean_publishes": round(float(np.mean(f["n"])), 1),
@@ -222,6 +231,10 @@ def window_stages(wbuf, n):
             "slowest_publishes": int(f["n"][worst]),
             "reruns": int(np.sum((f["flags"].astype(np.int64) & 1) != 0)),
             "epochs_seen": int(len(np.unique(f["epoch"]))),
+            # preemption: involuntary context switches of the cutter (over its cut stage) and the
+            # delivery threads, in the slowest 1 % of windows against all windows
+            "ivcsw_per_window": {k: {"all": round(float(np.mean(v)), 3), "slowest_1pct": round(float(np.mean(v[order[-k1:]])), 3)}
+                                 for k, v in cnt.items()},
             "max_gap_between_cuts_ms": round(float(np.max(gaps)) / 1e6, 3)}
 
 

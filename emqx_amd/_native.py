@@ -161,7 +161,9 @@ class tm_batcher_stats(C.Structure):
 
 class tm_batcher_window(C.Structure):
     _fields_ = [("n", C.c_uint32), ("flags", C.c_uint32)] + [(k, C.c_uint64) for k in (
-        "t_oldest", "t_cut", "t_queued", "t_gpu", "t_ready", "t_deliver", "t_done", "epoch")]
+        "t_oldest", "t_cut", "t_queued", "t_gpu", "t_ready", "t_deliver", "t_done", "epoch", "t_slot")] + [
+        ("cut_cpu_us", C.c_uint32), ("cut_ivcsw", C.c_uint16), ("wait_ivcsw", C.c_uint16),
+        ("del_cpu_us", C.c_uint32), ("del_wall_us", C.c_uint32), ("del_ivcsw", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 TM_BATCHER_WINDOWS = 16384
@@ -862,8 +864,8 @@ class Batcher:
         rc = self.lib.tm_batcher_windows(self.h, buf, TM_BATCHER_WINDOWS, C.byref(n))
         if rc != TM_OK:
             raise TMError(rc, "tm_batcher_windows failed")
-        dt = np.dtype([("n", np.uint32), ("flags", np.uint32)] + [(k, np.uint64) for k in (
-            "t_oldest", "t_cut", "t_queued", "t_gpu", "t_ready", "t_deliver", "t_done", "epoch")])
+        dt = np.dtype([(name, np.dtype(ct)) for name, ct in tm_batcher_window._fields_])
+        assert dt.itemsize == C.sizeof(tm_batcher_window)
         return np.frombuffer(bytes(buf), dtype=dt, count=n.value).copy()
 
     def close(self):

@@ -24,6 +24,10 @@
 // Submissions go to one of SHARDS queue shards (by submitting thread), so publishers that
 // resubmit from their callbacks do not all contend on one lock.
 #include <hip/hip_runtime.h>
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -87,6 +91,21 @@ extern "C" __attribute__((visibility("hidden"))) int tmx_in_delivery(void) { ret
 extern "C" __attribute__((visibility("hidden"))) int tmx_in_leased_delivery(void) { return tl_window_leased; }
 
 namespace {
+
+// A thread's own CPU time (CLOCK_THREAD_CPUTIME_ID: the scheduler's runtime, ns; rusage's
+// times are tick-granular) and involuntary context switches (getrusage RUSAGE_THREAD): read a
+// few times per window, to tell a stage that worked from one whose thread was preempted.
+struct ThreadUse {
+    uint64_t cpu_ns = 0, ivcsw = 0;
+};
+ThreadUse thread_use() {
+    ThreadUse u;
+    struct timespec ts;
+    if (clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts) == 0) u.cpu_ns = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+    struct rusage r;
+    if (getrusage(RUSAGE_THREAD, &r) == 0) u.ivcsw = (uint64_t)r.ru_nivcsw;
+    return u;
+}
 
 // The aggregator stamps every publish (submit -> callback latency), so its clock is on the
 // per-publish path: the TSC (invariant on the hosts this runs on; Linux uses it as the
@@ -272,6 +291,10 @@ struct Slot {
     // stage stamps of this window (tm_batcher_window)
     uint64_t t_old = 0, t_cut = 0, t_queued = 0, t_gpu = 0;
     std::atomic<uint64_t> t_deliver{0};
+    uint64_t t_slot = 0;
+    uint32_t cut_cpu_us = 0, cut_ivcsw = 0, wait_ivcsw = 0;
+    std::atomic<uint64_t> del_cpu_ns{0}, del_wall_ns{0};
+    std::atomic<uint32_t> del_ivcsw{0};
     uint32_t wflags = 0;
     uint64_t epoch = 0;
     // engine backend
@@ -334,6 +357,8 @@ struct tm_batcher {
     // first line prefetched, or (pf_lines > 0) up to pf_lines lines of them (development knobs
     // EMQX_TM_PF_PUBS / EMQX_TM_PF_LINES)
     uint32_t pf_pubs = 6, pf_lines = 0;
+    // delivery threads' nice value (EMQX_TM_DELIVERY_NICE; unprivileged processes may raise it)
+    int deliver_nice = 0;
     // runs windows: spans of the u64 id arena (zero-copy for id-list and u64-span callbacks), or
     // (EMQX_TM_RUNS_IDW=4) of the u32 one while every id fits.  Measured on the box at 65,536
     // closed-loop publishers: u32 windows made the id-list and u64-span callbacks
@@ -974,6 +999,14 @@ struct tm_batcher {
         w.t_deliver = S.t_deliver.load(std::memory_order_relaxed);
         w.t_done = now_ns();
         w.epoch = S.epoch;
+        w.t_slot = S.t_slot;
+        w.cut_cpu_us = S.cut_cpu_us;
+        w.cut_ivcsw = (uint16_t)std::min<uint32_t>(S.cut_ivcsw, 0xFFFF);
+        w.wait_ivcsw = (uint16_t)std::min<uint32_t>(S.wait_ivcsw, 0xFFFF);
+        w.del_cpu_us = (uint32_t)(S.del_cpu_ns.load(std::memory_order_relaxed) / 1000);
+        w.del_wall_us = (uint32_t)(S.del_wall_ns.load(std::memory_order_relaxed) / 1000);
+        w.del_ivcsw = S.del_ivcsw.load(std::memory_order_relaxed);
+        w.reserved = 0;
     }
     void free_slot(Slot &S) {
         trace_window(S);
@@ -1008,6 +1041,9 @@ struct tm_batcher {
     void worker_loop(uint32_t me) {
         LatHist &H = lat[me];
         tl_delivering = 1;
+        // below the cutter and the completer: on a full CPU share a woken cutter/completer
+        // preempts a delivery thread instead of waiting out its time slice (the latency tail)
+        if (deliver_nice > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), deliver_nice);
         Work w;
         while (next_work(w)) {
             Slot &S = slot[w.slot];
@@ -1019,13 +1055,19 @@ struct tm_batcher {
                 else S.chunk_ready[w.chunk].store(1, std::memory_order_release);
                 ns_copy.fetch_add(now_ns() - t0, std::memory_order_relaxed);  // waited on PCIe
             }
+            const ThreadUse u0 = thread_use();
             const uint64_t td0 = now_ns();
             uint64_t z = 0;
             S.t_deliver.compare_exchange_strong(z, td0, std::memory_order_relaxed);
             tl_window_leased = S.leased ? 1 : 0;
             deliver_range(S, w.lo, w.hi, rc, H);
             tl_window_leased = 0;
-            ns_del.fetch_add(now_ns() - td0, std::memory_order_relaxed);
+            const uint64_t td1 = now_ns();
+            ns_del.fetch_add(td1 - td0, std::memory_order_relaxed);
+            const ThreadUse u1 = thread_use();
+            S.del_cpu_ns.fetch_add(u1.cpu_ns - u0.cpu_ns, std::memory_order_relaxed);
+            S.del_wall_ns.fetch_add(td1 - td0, std::memory_order_relaxed);
+            S.del_ivcsw.fetch_add((uint32_t)(u1.ivcsw - u0.ivcsw), std::memory_order_relaxed);
             if (S.parts_left.fetch_sub(1, std::memory_order_acq_rel) == 1) free_slot(S);
         }
     }
@@ -1033,6 +1075,7 @@ struct tm_batcher {
     // ------------------------------------------------------------------ threads
     void cutter_loop() {
         uint32_t next = 0;
+        ThreadUse u_prev = thread_use();
         for (;;) {
             // a window: something queued, and (max_batch queued, or the oldest waited
             // max_wait_us, or stopping)
@@ -1068,12 +1111,19 @@ struct tm_batcher {
             }
             // a free slot (slots complete in order, so the next one in turn)
             Slot &S = slot[next];
+            const uint64_t t_slot = now_ns();
             {
                 std::unique_lock<std::mutex> lk(slot_mu);
                 slot_cv.wait(lk, [&] { return S.state == Slot::FREE; });
                 S.state = Slot::BUSY;
             }
+            const ThreadUse u0 = thread_use();
             const uint64_t tc0 = now_ns();
+            S.t_slot = t_slot;
+            S.wait_ivcsw = (uint32_t)(u0.ivcsw - u_prev.ivcsw);
+            S.del_cpu_ns.store(0, std::memory_order_relaxed);
+            S.del_wall_ns.store(0, std::memory_order_relaxed);
+            S.del_ivcsw.store(0, std::memory_order_relaxed);
             S.runs = false;
             S.wflags = 0;
             S.t_gpu = 0;
@@ -1104,6 +1154,9 @@ struct tm_batcher {
                 }
             }
             S.t_queued = now_ns();
+            u_prev = thread_use();
+            S.cut_cpu_us = (uint32_t)((u_prev.cpu_ns - u0.cpu_ns) / 1000);
+            S.cut_ivcsw = (uint32_t)(u_prev.ivcsw - u0.ivcsw);
             S.epoch = eng ? tmx_engine_epoch(eng) : 0;
             ns_enq.fetch_add(S.t_queued - S.t_enq, std::memory_order_relaxed);
             {
@@ -1173,6 +1226,7 @@ struct tm_batcher {
         if (const char *e = std::getenv("EMQX_TM_PF_PUBS")) pf_pubs = std::max(1u, std::min(64u, (uint32_t)std::atoi(e)));
         if (const char *e = std::getenv("EMQX_TM_PF_LINES")) pf_lines = std::min(256u, (uint32_t)std::atoi(e));
         if (const char *e = std::getenv("EMQX_TM_RUNS_IDW")) runs_w = std::atoi(e) == 4 ? 4u : 8u;
+        if (const char *e = std::getenv("EMQX_TM_DELIVERY_NICE")) deliver_nice = std::max(0, std::min(19, std::atoi(e)));
         if (!eng)
             for (Slot &S : slot)
                 for (HBuf *h : {&S.h_bytes, &S.h_off, &S.h_off_out, &S.h_status, &S.h_cnt, &S.h_ids, &S.h_ctl})

@@ -2854,6 +2854,10 @@ struct tm_engine {
         std::shared_ptr<const std::vector<uint64_t>> ids;  // id of sorted key j (the runs form's spans)
         std::vector<uint32_t> qw, qoff;
         std::vector<uint32_t> wcode;     // interned word id -> order code (NONE: not cached yet)
+        std::vector<uint32_t> h_kw, h_koff, h_kend;  // host copies of the order (plan_filter_parts)
+        DevBuf d_items, d_stop;          // FW_RUNS parts: {query, start, end, first}; per part: stopped
+        std::vector<uint4> items;
+        std::vector<uint32_t> i_cnt, i_rcnt, i_off, i_stop;
         std::vector<uint8_t> qdollar;
         uint64_t n_onepass = 0, n_twopass = 0;  // batches by path (tests / bench)
     } fx;
@@ -3004,8 +3008,84 @@ struct tm_engine {
         }
         fx.wcode.swap(wcode);
         fx.wcode.resize(word_off.size(), NONE);
+        // the runs form splits long '+' queries at child-group boundaries (plan_filter_parts):
+        // it reads the order on the host
+        fx.h_kw.swap(kw);
+        fx.h_koff.swap(koff);
+        fx.h_kend.swap(kend);
         fx.epoch = epoch;
         return TM_OK;
+    }
+
+    // matches_filter/3's walk over a query with '+' at level p (its levels before p literal)
+    // spends its time inside G, the keys whose first p words are the query's: it enters every
+    // child group of level p (a distinct word there) at its first key, since a seek inside G
+    // lands in the child group it came from or at the next one's first key (its probe holds
+    // the level-p word); and the keys before G cannot seek past G's first key.  So the walk
+    // can be cut at child-group starts c_1 < c_2 < ... inside G: part k walks [c_k, c_{k+1})
+    // from c_k as if it had arrived there (part 0 from the query's own start), and the query's
+    // result is its parts' results in order up to the first part that stopped.
+    // Items {query, start, end (NONE: none), first part?}, queries in order, parts in order.
+    // EMQX_TM_FILTER_SPLIT=min_keys:part_keys (0 disables; default 16384:4096).
+    void plan_filter_parts(uint32_t n, std::vector<uint4> &items) {
+        items.clear();
+        uint32_t min_keys = 16384, part_keys = 4096;  // read per call: tests change it
+        if (const char *e = getenv("EMQX_TM_FILTER_SPLIT")) {
+            min_keys = (uint32_t)strtoul(e, nullptr, 10);
+            if (const char *c = strchr(e, ':')) part_keys = std::max(1u, (uint32_t)strtoul(c + 1, nullptr, 10));
+        }
+        const uint32_t K = fx.K;
+        bool any = false;
+        std::vector<uint32_t> cuts;
+        for (uint32_t q = 0; q < n; q++) {
+            cuts.clear();
+            const uint32_t *W = fx.qw.data() + fx.qoff[q];
+            const uint32_t WL = fx.qoff[q + 1] - fx.qoff[q];
+            uint32_t p = 0;
+            while (p < WL && W[p] >= 2 && (W[p] & 1u)) p++;  // literal dictionary words
+            if (min_keys && K && !fx.qdollar[q] && p >= 1 && p < WL && W[p] == 1u && p + 1 <= FW_END_DEPTHS) {
+                // G = [g0, g1): the first key whose first p words are >= W's, if it has them
+                auto less_prefix = [&](uint32_t j) {  // key j's words < W[0..p) (a shorter prefix is less)
+                    const uint32_t *k = fx.h_kw.data() + fx.h_koff[j], L = fx.h_koff[j + 1] - fx.h_koff[j];
+                    for (uint32_t i = 0; i < p; i++) {
+                        if (i == L) return true;
+                        if (k[i] != W[i]) return k[i] < W[i];
+                    }
+                    return false;
+                };
+                uint32_t lo = 0, hi = K;
+                while (lo < hi) {
+                    const uint32_t mid = lo + (hi - lo) / 2;
+                    if (less_prefix(mid)) lo = mid + 1;
+                    else hi = mid;
+                }
+                const uint32_t g0 = lo;
+                bool has = g0 < K && fx.h_koff[g0 + 1] - fx.h_koff[g0] >= p;
+                for (uint32_t i = 0; has && i < p; i++) has = fx.h_kw[fx.h_koff[g0] + i] == W[i];
+                if (has) {
+                    const uint32_t g1 = fx.h_kend[(uint64_t)g0 * FW_END_DEPTHS + p - 1];
+                    if (g1 - g0 >= min_keys)
+                        for (uint64_t x = (uint64_t)g0 + part_keys; x < g1; x += part_keys) {
+                            // the next child-group start at or after x (x's group's end, unless
+                            // x starts one itself)
+                            const uint32_t xs = (uint32_t)x;
+                            const bool starts = xs == g0 || fx.h_kend[(uint64_t)(xs - 1) * FW_END_DEPTHS + p] == xs;
+                            const uint32_t c = starts ? xs : fx.h_kend[(uint64_t)xs * FW_END_DEPTHS + p];
+                            // (a key of p words, the group of G's own prefix, never starts a part)
+                            if (c < g1 && (cuts.empty() || c > cuts.back()) && fx.h_koff[c + 1] - fx.h_koff[c] > p)
+                                cuts.push_back(c);
+                        }
+                }
+            }
+            any = any || !cuts.empty();
+            uint32_t st = 0;
+            for (size_t k = 0; k <= cuts.size(); k++) {
+                const uint32_t en = k < cuts.size() ? cuts[k] : NONE;
+                items.push_back(make_uint4(q, st, en, k == 0 ? 1u : 0u));
+                st = en;
+            }
+        }
+        if (!any) items.clear();  // nothing to split: one wave per query, as before
     }
 };
 
@@ -4389,9 +4469,32 @@ int tm_match_filter_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint3
     int rc = filter_prepare(eng, o, bytes, off, n, mode, a);
     if (rc) return rc;
     hipStream_t s = eng->stream;
-    TM_TRY_HIP(fx.d_rcnt.ensure((size_t)n * 4), TM_ENOMEM, "alloc");
+    // long '+' queries walked as several parts, one wave each (plan_filter_parts)
+    eng->plan_filter_parts(n, fx.items);
+    const bool parts = !fx.items.empty();
+    const uint32_t ni = parts ? (uint32_t)fx.items.size() : n;  // per-item outputs
+    TM_TRY_HIP(fx.d_rcnt.ensure((size_t)ni * 4), TM_ENOMEM, "alloc");
     a.rcnt = fx.d_rcnt.as<uint32_t>();
     o.f_rcnt.resize(n);
+    if (parts) {
+        TM_TRY_HIP(fx.d_items.ensure((size_t)ni * sizeof(uint4)), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(fx.d_stop.ensure((size_t)ni * 4), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(fx.d_cnt.ensure((size_t)ni * 4), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(fx.d_off.ensure(((size_t)ni + 1) * 4), TM_ENOMEM, "alloc");
+        TM_TRY_HIP(hipMemcpyAsync(fx.d_items.p, fx.items.data(), (size_t)ni * sizeof(uint4), hipMemcpyHostToDevice, s),
+                   TM_EDEVICE, "H2D");
+        a.items = fx.d_items.as<uint4>();
+        a.n_items = ni;
+        a.stop = fx.d_stop.as<uint32_t>();
+        a.cnt = fx.d_cnt.as<uint32_t>();
+        a.out_off = fx.d_off.as<uint32_t>();
+        fx.i_off.resize(ni);
+        fx.i_cnt.resize(ni);
+        fx.i_rcnt.resize(ni);
+        fx.i_stop.resize(ni);
+    }
+    uint32_t *h_off = parts ? fx.i_off.data() : o.f_off.data(), *h_cnt = parts ? fx.i_cnt.data() : o.f_cnt.data(),
+             *h_rcnt = parts ? fx.i_rcnt.data() : o.f_rcnt.data();
     uint64_t ranges = 0;
     bool done = false;
     for (int attempt = 0; attempt < 3 && !done; attempt++) {
@@ -4412,12 +4515,12 @@ int tm_match_filter_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint3
         uint64_t ctl[3] = {0, 0, 0};
         TM_TRY_HIP(launch_filter_walk(a, FW_RUNS, s), TM_EDEVICE, "k_filter_walk runs");
         TM_TRY_HIP(hipMemcpyAsync(ctl, fx.d_ctl.p, 24, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
-        TM_TRY_HIP(hipMemcpyAsync(o.f_off.data(), fx.d_off.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-                   "D2H");
-        TM_TRY_HIP(hipMemcpyAsync(o.f_cnt.data(), fx.d_cnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-                   "D2H");
-        TM_TRY_HIP(hipMemcpyAsync(o.f_rcnt.data(), fx.d_rcnt.p, (size_t)n * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE,
-                   "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(h_off, fx.d_off.p, (size_t)ni * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(h_cnt, fx.d_cnt.p, (size_t)ni * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+        TM_TRY_HIP(hipMemcpyAsync(h_rcnt, fx.d_rcnt.p, (size_t)ni * 4, hipMemcpyDeviceToHost, s), TM_EDEVICE, "D2H");
+        if (parts)
+            TM_TRY_HIP(hipMemcpyAsync(fx.i_stop.data(), fx.d_stop.p, (size_t)ni * 4, hipMemcpyDeviceToHost, s),
+                       TM_EDEVICE, "D2H");
         TM_TRY_HIP(hipStreamSynchronize(s), TM_EDEVICE, "k_filter_walk runs");
         ranges = ctl[0];
         if (ranges <= a.out_cap && ctl[1] <= a.pool_chunks) {
@@ -4440,9 +4543,32 @@ int tm_match_filter_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint3
     o.f_ids = fx.ids;
     const uint64_t *ids = o.f_ids->data();
     const uint2 *rg = o.f_rng.as<uint2>();
-    o.f_spans.resize(ranges);
     uint64_t tot = 0;
-    for (uint64_t r = 0; r < ranges; r++) o.f_spans[r] = tm_span{ids + rg[r].x, rg[r].y};
+    if (!parts) {
+        o.f_spans.resize(ranges);
+        for (uint64_t r = 0; r < ranges; r++) o.f_spans[r] = tm_span{ids + rg[r].x, rg[r].y};
+    } else {
+        // a query's parts in order, up to the first one that stopped (its walk ends there)
+        o.f_spans.clear();
+        size_t i = 0;
+        for (uint32_t q = 0; q < n; q++) {
+            o.f_off[q] = (uint32_t)o.f_spans.size();
+            uint32_t kc = 0;
+            bool on = true;
+            for (; i < ni && fx.items[i].x == q; i++) {
+                if (!on) continue;
+                for (uint32_t r = 0; r < fx.i_rcnt[i]; r++) {
+                    const uint2 g = rg[(uint64_t)fx.i_off[i] + r];
+                    o.f_spans.push_back(tm_span{ids + g.x, g.y});
+                }
+                kc += fx.i_cnt[i];
+                on = !fx.i_stop[i];
+            }
+            o.f_cnt[q] = kc;
+            o.f_rcnt[q] = (uint32_t)(o.f_spans.size() - o.f_off[q]);
+        }
+        ranges = o.f_spans.size();
+    }
     for (uint32_t i = 0; i < n; i++) tot += o.f_cnt[i];
     o.fr_off.swap(o.f_off);  // the runs result's own arrays: a keys-form call does not touch them
     o.fr_cnt.swap(o.f_cnt);

@@ -43,6 +43,13 @@ struct FilterArgs {
     // sorted key, count} at ((uint2 *)out)[out_off[q] ..], cnt[q] keys; ctl[0] counts ranges and
     // out_cap is in ranges
     uint32_t *rcnt;
+    // FW_RUNS parts (round 5, engine.cpp plan_filter_parts): when items is set, wave i walks
+    // item i = {query, start key, end key (NONE: none), 1 for the query's first part} from its
+    // start until it stops or reaches its end, and cnt / rcnt / out_off / stop are per item
+    // (stop[i] = 1 unless the part reached its end); null: item i is query i, whole
+    const uint4 *items;
+    uint32_t n_items;
+    uint32_t *stop;
 };
 constexpr int FW_COUNT = 0, FW_EMIT = 1, FW_ONEPASS = 2, FW_RUNS = 3;
 constexpr uint32_t FW_CHUNK = 256;   // u32 words per pool chunk (1 link entry + 127 ranges of 2 words)

@@ -217,12 +217,18 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t *total, 
 // range do not fit the pool / out_cap leaves its query unwritten; the host sees the demand
 // in ctl and re-runs the batch (two-pass) after growing.
 __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
-    const uint32_t q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t it = blockIdx.x * 4 + (threadIdx.x >> 6);  // the item: a query, or a part of one
     const uint32_t lane = threadIdx.x & 63;
-    if (q >= a.n) return;  // wave-uniform
+    if (it >= (a.items ? a.n_items : a.n)) return;  // wave-uniform
+    const uint4 item = a.items ? a.items[it] : make_uint4(it, 0u, NONE_FW, 1u);
+    const uint32_t q = item.x;
     const uint32_t qb = a.qoff[q], WL = a.qoff[q + 1] - qb;
     const uint32_t *W = a.qw + qb;
     const uint32_t K = a.K;
+    // a part ends where the next one starts: keys at or past pend are not its own (they count
+    // as a stop in a step), and reaching pend is not a stop of the query's walk
+    const uint32_t pend = min(item.z, K);
+    bool reached = false;  // wave-uniform
     uint32_t c = 0;  // wave-uniform
     // FW_ONEPASS chain of ranges (wave-uniform): head, current chunk, ranges in the current chunk
     constexpr uint32_t CE = FW_CHUNK / 2 - 1;  // ranges per chunk (entry 0 is the link)
@@ -268,8 +274,8 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
     };
     if (WL && a.qstatus[q] == 0) {
         // base_init/1 (:160-163): a first word <<"$", _/bytes>> starts at next({[W0], {}})
-        uint32_t idx = 0;
-        if (a.qdollar[q]) {
+        uint32_t idx = item.y;  // a later part starts at its child-group start
+        if (item.w && a.qdollar[q]) {
             Probe pb{};
             pb.np = 0;
             pb.w = W[0];
@@ -290,9 +296,9 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
         uint32_t FL = 0, nv = 0, wbase = 0;
         int r = R_LOWER;  // past the end of the table (or not loaded yet): a stop
         uint32_t spos = 0, sword = 0, qh = NONE_FW;
-        while (idx < K) {
+        while (idx < pend) {
             const uint32_t j = idx + lane;
-            const bool inr = j < K;
+            const bool inr = j < pend;
             {  // keep what the previous window already holds
                 const uint32_t o = idx - wbase;
                 if (nv > o) {
@@ -389,7 +395,8 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             if (rl < fs) {
                 // the run [rs, E): E = next({first p words of key rs ++ [+inf], {}})
                 const uint32_t rs = idx + rl, p = lane_value(qh, rl);
-                const uint32_t E = a.first ? rs + 1 : seek_from(rl, probe_from(rl, p, NONE_FW));
+                // (a run ends inside its child group: never past a part's end)
+                const uint32_t E = a.first ? rs + 1 : min(seek_from(rl, probe_from(rl, p, NONE_FW)), pend);
                 const uint32_t m = E - rs;
                 if (pass == FW_EMIT) {
                     copy_keys(a.kh + rs, out + c, m, lane);
@@ -407,11 +414,18 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             }
             const int rs = (int)lane_value((uint32_t)r, fs);
             const uint32_t ks = idx + fs;
-            if (rs == R_LOWER || ks >= K) break;  // lower, or '$end_of_table'
+            if (ks >= pend) {  // the part's end (or '$end_of_table')
+                idx = pend;
+                break;
+            }
+            if (rs == R_LOWER) break;  // lower
             // seek/3: next({first spos words of key ks ++ [sword], {}})
             const uint32_t sp = lane_value(spos, fs), sw = lane_value(sword, fs);
             idx = seek_from(fs, probe_from(fs, sp, sw));
         }
+        // a part that reached its end hands the walk to the next part (return_first: unless it
+        // found its key); anything else is the walk's own stop
+        reached = idx >= pend && pend < K && !(a.first && c);
     }
     if (pass == FW_COUNT && lane == 0) a.cnt[q] = c;
     if (pass == FW_RUNS) {
@@ -421,9 +435,10 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
         if (lane == 0 && nent) base = atomicAdd(&a.ctl[0], (unsigned long long)nent);
         base = __shfl(base, 0);
         if (lane == 0) {
-            a.cnt[q] = c;
-            a.rcnt[q] = nent;
-            a.out_off[q] = (uint32_t)base;
+            a.cnt[it] = c;
+            a.rcnt[it] = nent;
+            a.out_off[it] = (uint32_t)base;
+            if (a.stop) a.stop[it] = reached ? 0u : 1u;
         }
         if (short_pool || base + nent > a.out_cap) return;  // the host grows and re-runs
         __threadfence_block();
@@ -514,7 +529,8 @@ hipError_t launch_filter_bulk(const FilterArgs &a, hipStream_t stream) {
 
 hipError_t launch_filter_walk(const FilterArgs &a, int pass, hipStream_t stream) {
     if (!a.n) return hipSuccess;
-    const uint32_t blocks = (a.n + 3) / 4;  // 4 waves of 64 per block, one query per wave
+    const uint32_t waves = a.items ? a.n_items : a.n;  // one query, or one part of one, per wave
+    const uint32_t blocks = (waves + 3) / 4;           // 4 waves of 64 per block
     hipLaunchKernelGGL(k_filter_walk, dim3(blocks), dim3(256), 0, stream, a, pass);
     return hipGetLastError();
 }

@@ -170,6 +170,17 @@ typedef struct tm_batcher_window {
     uint64_t t_deliver;    /* the first delivery thread starts on it */
     uint64_t t_done;       /* its last callback returned */
     uint64_t epoch;        /* engine epoch when the window was queued (commits between windows) */
+    /* CPU accounting (CPU time: CLOCK_THREAD_CPUTIME_ID; context switches: getrusage
+     * RUSAGE_THREAD), to tell a stage that worked from one whose thread was off its CPU: */
+    uint64_t t_slot;       /* the cutter starts waiting for a free slot (<= t_cut; the rest of
+                              t_oldest..t_cut is the window filling / max_wait polling) */
+    uint32_t cut_cpu_us;   /* the cutter's CPU time over t_cut..t_queued */
+    uint16_t cut_ivcsw;    /* its involuntary context switches over t_cut..t_queued */
+    uint16_t wait_ivcsw;   /* ... since it queued the previous window (over this one's wait) */
+    uint32_t del_cpu_us;   /* the delivery threads' CPU time on this window's ranges, summed */
+    uint32_t del_wall_us;  /* their wall time on those ranges, summed */
+    uint32_t del_ivcsw;    /* their involuntary context switches inside those ranges */
+    uint32_t reserved;
 } tm_batcher_window;
 /* Copies up to `cap` of the kept windows, oldest first; *n_out = how many. */
 int tm_batcher_windows(tm_batcher *b, tm_batcher_window *out, uint32_t cap, uint32_t *n_out);

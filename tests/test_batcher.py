@@ -68,6 +68,29 @@ def test_blocking_match_one_publish():
     b.close()
 
 
+def test_window_trace_stamps_and_cpu_accounting():
+    """tm_batcher_windows: per window the stage stamps in order, and the cutter's / delivery
+    threads' CPU time and involuntary context switches (getrusage per thread), which tell a
+    slow stage that worked from one whose thread was preempted."""
+    b = N.Batcher(backend=_oracle_backend(ROUTES), max_batch=8, max_wait_us=500, delivery_threads=2)
+    b.reset_stats()
+    th = [threading.Thread(target=lambda k=k: [b.match(b"a/b") for _ in range(20)]) for k in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    w = b.windows()
+    b.close()
+    assert len(w) >= 20 and int(w["n"].sum()) == 160
+    assert np.all(w["t_oldest"] <= w["t_cut"]) and np.all(w["t_slot"] <= w["t_cut"])
+    assert np.all(w["t_cut"] <= w["t_queued"]) and np.all(w["t_queued"] <= w["t_done"])
+    # a thread's CPU time inside an interval never exceeds the interval (plus rusage's tick)
+    cut_wall_us = (w["t_queued"] - w["t_cut"]) / 1e3
+    assert np.all(w["cut_cpu_us"] <= cut_wall_us + 5000)
+    assert np.all(w["del_cpu_us"] <= w["del_wall_us"] + 5000)
+    assert np.all(w["del_wall_us"] > 0)
+
+
 def test_concurrent_publishers_share_windows():
     calls = []
     b = N.Batcher(backend=_oracle_backend(ROUTES, calls), max_batch=16, max_wait_us=20000)

@@ -101,3 +101,27 @@ def test_filter_runs_outlive_a_commit():
     got = eng._expand_runs(res, len(queries))
     for a, b in zip(got, exp):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("split", ["1:1", "64:16", "16384:4096"])
+def test_filter_runs_split_parts(monkeypatch, split):
+    """Long one-'+' queries walked as parts, one wave each, cut at child-group starts of the
+    '+' level (plan_filter_parts): the query's ids are its parts' in order up to the first part
+    that stopped, id for id the oracle's walk (ALL and FIRST)."""
+    monkeypatch.setenv("EMQX_TM_FILTER_SPLIT", split)
+    rng = random.Random(0x5917)
+    filters = []
+    for i in range(20000):
+        g = rng.randrange(3000)
+        tail = rng.choice([b"x", b"y", b"x/z", b"#", b"+", b"x/#", b""])
+        filters.append(b"a/b/g%d" % g + (b"/" + tail if tail else b""))
+    filters += [b"a/b", b"a/b", b"a", b"a/c/g1/x", b"a/b/#", b"a/+/g7/x", b"$SYS/a/b/x"] * 3
+    ids = list(range(1, len(filters) + 1))
+    wf = [i % 2 for i in range(len(filters))]
+    queries = [b"a/b/+/x", b"a/b/+", b"a/b/+/#", b"a/b/+/x/z", b"a/b/+/+", b"a/b/+/y/#", b"a/+/+/x",
+               b"+/b/+/x", b"a/b/+/nope", b"a/b/+/x/+", b"$SYS/a/+/x", b"a/b/g7/x", b"a/b/+/+/z"]
+    queries += [b"a/b/+/" + rng.choice([b"x", b"y", b"#", b"+", b"x/z", b"q"]) for _ in range(40)]
+    eng = N.Engine(0)
+    _load(eng, filters, ids, wf)
+    _check(eng, filters, ids, wf, queries)
+    _check(eng, filters, ids, wf, queries, N.TM_MATCH_FIRST)
