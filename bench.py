@@ -129,10 +129,11 @@ def batcher_load(eng, tb, to32, seconds, plan=None):
     from emqx_amd import _native as N
     lg = _loadgen()
     runs = []
-    # the cutter is about half busy; the completion thread and the caller block (driver waits,
-    # a sleep): 15 delivery threads on the 16-CPU share (14: 73.8 / 15: 77.7 / 16: 77.2 M/s id
-    # lists in one box run, profiles/r04_batcher_threads_m.jsonl)
-    dt = max(2, min(15, cpu_topology()["usable_cpus"] - 1))
+    # the cutter and the completion thread each keep a CPU of the 16-CPU share: 14 delivery
+    # threads.  With the process pinned to 16 CPUs (placement.pin_to_gpu), 15 threads left the
+    # cutter waiting for a CPU: 60.2 / 59.7 M/s id lists against 80.4-86.1 M/s at 14 in the
+    # same box runs (profiles/r05_batcher_acct_quota.jsonl, r05_batcher_grow_quota.jsonl)
+    dt = max(2, min(14, cpu_topology()["usable_cpus"] - 2))
     plan = plan or [(4096, N.TM_TRANSPORT_AUTO, 0), (65536, N.TM_TRANSPORT_AUTO, 0), (262144, N.TM_TRANSPORT_AUTO, 0),
             (65536, N.TM_TRANSPORT_AUTO, 1), (65536, N.TM_TRANSPORT_AUTO, 3), (65536, N.TM_TRANSPORT_IDS, 0),
             (65536, N.TM_TRANSPORT_IDS, 3)]  # a replica's transport (no host id arena), u32 ids read in place
@@ -231,6 +232,10 @@ def window_stages(wbuf, n):
             "slowest_publishes": int(f["n"][worst]),
             "reruns": int(np.sum((f["flags"].astype(np.int64) & 1) != 0)),
             "epochs_seen": int(len(np.unique(f["epoch"]))),
+            # delivery CPU per publish (all windows): the callbacks' own cost, which outside
+            # contention for caches / DRAM raises without any preemption
+            "deliver_cpu_ns_per_publish": round(float(np.sum(f["del_cpu_us"]) * 1e3 / max(np.sum(f["n"]), 1)), 1),
+            "cut_cpu_ns_per_publish": round(float(np.sum(f["cut_cpu_us"]) * 1e3 / max(np.sum(f["n"]), 1)), 1),
             # preemption: involuntary context switches of the cutter (over its cut stage) and the
             # delivery threads, in the slowest 1 % of windows against all windows
             "ivcsw_per_window": {k: {"all": round(float(np.mean(v)), 3), "slowest_1pct": round(float(np.mean(v[order[-k1:]])), 3)}
@@ -882,7 +887,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (seeded generator, emqx_amd/workloads.py config C)",
+            "data": f"synthetic (seeded generator, emqx_amd/workloads.py config {args.config})",
             "config": {
                 "workload": f"{args.config}: {w.n_keys} route keys, 10-level topics, '#'-heavy fan-out"
                 if args.config == "C" else f"{args.config} (scale {args.scale}): {w.n_keys} route keys",
@@ -904,7 +909,10 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_match_fast",
+                # the step's kernels between the two timing events (engine.cpp prepass_on: the
+                # product build launches k_prescan ahead of the walk only with EMQX_TM_PREPASS=1)
+                "kernel": ("k_prescan + k_match_fast" if os.environ.get("EMQX_TM_PREPASS", "0") != "0"
+                           else "k_match_fast"),
                 "kernel_ms": round(kernel_ms, 4),
                 # the same bytes per timed step (launch ramp and tail overlapped by the second
                 # batch in flight): what the device sustains, not one launch's rate

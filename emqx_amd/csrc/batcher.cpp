@@ -179,15 +179,19 @@ struct alignas(64) LatHist {
 };
 
 // grow-only device / pinned buffers
+// Growth is a stall: hipFree waits for the whole device and hipHostMalloc takes milliseconds
+// (the slowest windows of a steady run were exactly the ones that grew a buffer, their
+// cutter busy 3-6 ms, round 5).  So a buffer grows once to its size for a max_batch window
+// (`hint`, from the per-publish high-water marks), not to the demand of the window at hand.
 struct DBuf {
     void *p = nullptr;
     size_t cap = 0;
-    hipError_t ensure(size_t bytes) {
+    hipError_t ensure(size_t bytes, size_t hint = 0) {
         if (bytes <= cap) return hipSuccess;
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        size_t c = std::max<size_t>(bytes + bytes / 4, 4096);
+        size_t c = std::max<size_t>(std::max<size_t>(bytes + bytes / 4, hint), 4096);
         hipError_t e = hipMalloc(&p, c);
         if (e == hipSuccess) cap = c;
         return e;
@@ -209,10 +213,10 @@ struct HBuf {
         p = nullptr;
         cap = 0;
     }
-    hipError_t ensure(size_t bytes) {
+    hipError_t ensure(size_t bytes, size_t hint = 0) {
         if (bytes <= cap) return hipSuccess;
         drop();
-        size_t c = std::max<size_t>(bytes + bytes / 4, 4096);
+        size_t c = std::max<size_t>(std::max<size_t>(bytes + bytes / 4, hint), 4096);
         if (!pinned) {
             p = std::malloc(c);
             if (!p) return hipErrorOutOfMemory;
@@ -346,6 +350,17 @@ struct tm_batcher {
     // runs transport: spans per publish of recent windows (sizes the next); written by the
     // completion thread, read by the cutter (found by ThreadSanitizer, round 4)
     std::atomic<double> spans_per_pub{4.0};
+    // per-publish high-water marks: buffer sizes for a max_batch window (DBuf/HBuf::ensure)
+    std::atomic<double> hw_bytes{64.0}, hw_spans{4.0}, hw_ids{16.0};
+    static void raise_hw(std::atomic<double> &hw, double v) {
+        double c = hw.load(std::memory_order_relaxed);
+        while (v > c && !hw.compare_exchange_weak(c, v, std::memory_order_relaxed)) {
+        }
+    }
+    size_t hint_of(const std::atomic<double> &hw, size_t width) const {
+        return (size_t)(hw.load(std::memory_order_relaxed) * 1.25 * cfg.max_batch) * width + 64;
+    }
+    size_t hint_pub4() const { return ((size_t)cfg.max_batch + 1) * 4; }
     std::atomic<bool> reported{false};  // the first failed window is reported on stderr (once)
     void report(const char *stage, int rc) {
         if (rc >= 0 || reported.exchange(true)) return;
@@ -445,7 +460,7 @@ struct tm_batcher {
             nb += sh.bytes.size();
         }
         S.n = 0;
-        BT_HIP(S.h_bytes.ensure(nb + 64));
+        BT_HIP(S.h_bytes.ensure(nb + 64, hint_of(hw_bytes, 1)));
         BT_HIP(S.h_off.ensure(((size_t)cfg.max_batch + 1) * 4));
         uint8_t *dst = S.h_bytes.as<uint8_t>();
         uint64_t at = 0, taken_bytes = 0;
@@ -478,6 +493,7 @@ struct tm_batcher {
         S.t_old = ~0ull;
         for (const Pending &p : S.pubs) S.t_old = std::min(S.t_old, p.t0);
         S.nbytes = at;
+        if (S.n) raise_hw(hw_bytes, (double)at / S.n);
         uint32_t *o = S.h_off.as<uint32_t>();
         uint32_t pos = 0;
         for (uint32_t i = 0; i < S.n; i++) {
@@ -504,12 +520,12 @@ struct tm_batcher {
         if (S.runs) return enqueue_runs(S);
         hipStream_t s_comp = s_comps[S.set];
         BT_HIP(hipSetDevice(device));
-        BT_HIP(S.d_bytes.ensure(S.nbytes + 16));
-        BT_HIP(S.d_off.ensure((size_t)n * 4 + 4));
-        BT_HIP(S.d_off_out.ensure((size_t)n * 4 + 4));
-        BT_HIP(S.h_off_out.ensure((size_t)n * 4 + 4));
-        BT_HIP(S.h_status.ensure((size_t)n * 4 + 4));
-        BT_HIP(S.h_cnt.ensure((size_t)n * 4 + 4));
+        BT_HIP(S.d_bytes.ensure(S.nbytes + 16, hint_of(hw_bytes, 1)));
+        BT_HIP(S.d_off.ensure((size_t)n * 4 + 4, hint_pub4()));
+        BT_HIP(S.d_off_out.ensure((size_t)n * 4 + 4, hint_pub4()));
+        BT_HIP(S.h_off_out.ensure((size_t)n * 4 + 4, hint_pub4()));
+        BT_HIP(S.h_status.ensure((size_t)n * 4 + 4, hint_pub4()));
+        BT_HIP(S.h_cnt.ensure((size_t)n * 4 + 4, hint_pub4()));
         BT_HIP(S.h_ctl.ensure(CTL_BYTES));
         if (!S.ev) BT_HIP(hipEventCreateWithFlags(&S.ev, EV_FLAGS));
         BT_HIP(hipMemcpyAsync(S.d_bytes.p, S.h_bytes.p, S.nbytes + 1, hipMemcpyHostToDevice, s_comp));
@@ -518,7 +534,7 @@ struct tm_batcher {
         if (S.mode == TM_MATCH_ALL) {
             // the walk writes the route ids itself (u32 while every id fits), compacted
             // topic-major: no key handles, no separate id pass (tm_match_ids_device)
-            S.ids_cap = std::max<uint64_t>(S.ids_cap, std::max<uint64_t>((uint64_t)n * 8, 1 << 16));
+            S.ids_cap = std::max<uint64_t>(S.ids_cap, std::max<uint64_t>(hint_of(hw_ids, 1), 1 << 16));
             BT_HIP(S.d_ids.ensure(S.ids_cap * 8 + 8));
             S.narrow = true;
             int rc = tmx_batch_match_ids(eng, S.set, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, 4,
@@ -569,17 +585,17 @@ struct tm_batcher {
         const uint32_t n = S.n;
         hipStream_t s_comp = s_comps[S.set];
         BT_HIP(hipSetDevice(device));
-        BT_HIP(S.d_bytes.ensure(S.nbytes + 16));
-        BT_HIP(S.d_off.ensure((size_t)n * 4 + 4));
-        for (DBuf *d : {&S.d_soff, &S.d_scnt, &S.d_kcnt, &S.d_st}) BT_HIP(d->ensure((size_t)n * 4 + 4));
+        BT_HIP(S.d_bytes.ensure(S.nbytes + 16, hint_of(hw_bytes, 1)));
+        BT_HIP(S.d_off.ensure((size_t)n * 4 + 4, hint_pub4()));
+        for (DBuf *d : {&S.d_soff, &S.d_scnt, &S.d_kcnt, &S.d_st}) BT_HIP(d->ensure((size_t)n * 4 + 4, hint_pub4()));
         BT_HIP(S.d_cur.ensure(64));
-        for (HBuf *h : {&S.h_soff, &S.h_scnt, &S.h_kcnt, &S.h_status}) BT_HIP(h->ensure((size_t)n * 4 + 4));
+        for (HBuf *h : {&S.h_soff, &S.h_scnt, &S.h_kcnt, &S.h_status}) BT_HIP(h->ensure((size_t)n * 4 + 4, hint_pub4()));
         BT_HIP(S.h_ctl.ensure(64));
         if (!S.ev) BT_HIP(hipEventCreateWithFlags(&S.ev, EV_FLAGS));
         const uint64_t want =
             std::max<uint64_t>(4096, (uint64_t)(spans_per_pub.load(std::memory_order_relaxed) * 1.5 * n) + 1024);
         if (S.spans_cap < want) {
-            BT_HIP(S.d_spans.ensure(want * 16));
+            BT_HIP(S.d_spans.ensure(want * 16, hint_of(hw_spans, 16)));
             S.spans_cap = S.d_spans.cap / 16;
         }
         BT_HIP(hipMemcpyAsync(S.d_bytes.p, S.h_bytes.p, S.nbytes + 1, hipMemcpyHostToDevice, s_comp));
@@ -621,9 +637,12 @@ struct tm_batcher {
         if (over || seg > seg_cap || fr > fr_cap) {
             std::lock_guard<std::mutex> g(eng_mu);
             BT_HIP(hipStreamSynchronize(s_comps[S.set]));
-            int rc = tmx_engine_grow_pools(eng, S.set, seg, fr);
+            // to a max_batch window's demand at this window's rate (growth stalls the device)
+            const double sc = std::max(1.0, (double)cfg.max_batch / std::max<uint32_t>(S.n, 1));
+            int rc = tmx_engine_grow_pools(eng, S.set, (uint64_t)(seg * sc), (uint64_t)(fr * sc));
             if (rc) return rc;
             if (over) {  // more spans than the window's buffer: grow to the demand, run again
+                raise_hw(hw_spans, (double)total / std::max<uint32_t>(S.n, 1));
                 spans_per_pub.store(std::max(spans_per_pub.load(std::memory_order_relaxed),
                                              (double)total / std::max<uint32_t>(S.n, 1)),
                                     std::memory_order_relaxed);
@@ -638,7 +657,8 @@ struct tm_batcher {
         spans_per_pub.store(0.9 * spans_per_pub.load(std::memory_order_relaxed) +
                                 0.1 * ((double)total / std::max<uint32_t>(S.n, 1)),
                             std::memory_order_relaxed);
-        BT_HIP(S.h_spans.ensure(total * 16 + 16));
+        raise_hw(hw_spans, (double)total / std::max<uint32_t>(S.n, 1));
+        BT_HIP(S.h_spans.ensure(total * 16 + 16, hint_of(hw_spans, 16)));
         S.nchunk = 1;
         S.chunk_lo[0] = 0;
         S.chunk_lo[1] = S.n;
@@ -702,10 +722,13 @@ struct tm_batcher {
             // pools sized to the demand for later windows (only when short: the engine compares)
             std::lock_guard<std::mutex> g(eng_mu);
             BT_HIP(hipStreamSynchronize(s_comps[S.set]));
-            int rc = tmx_engine_grow_pools(eng, S.set, seg, fr);
+            // to a max_batch window's demand at this window's rate (growth stalls the device)
+            const double sc = std::max(1.0, (double)cfg.max_batch / std::max<uint32_t>(S.n, 1));
+            int rc = tmx_engine_grow_pools(eng, S.set, (uint64_t)(seg * sc), (uint64_t)(fr * sc));
             if (rc) return rc;
             if (over) {  // output arena too small: grow to the demand, run this window again
-                const uint64_t want = total + total / 8 + 1024;
+                raise_hw(hw_ids, (double)total / std::max<uint32_t>(S.n, 1));
+                const uint64_t want = std::max<uint64_t>(total + total / 8 + 1024, hint_of(hw_ids, 1));
                 // a TM_MATCH_ALL window's walk writes ids: u64 ones take two words of the arena
                 const uint64_t words = S.mode == TM_MATCH_ALL && !S.narrow ? 2 * want : want;
                 if ((rc = tmx_batch_reserve_matches(eng, S.set, words))) return rc;
@@ -737,7 +760,8 @@ struct tm_batcher {
         const uint32_t *oo = S.h_off_out.as<uint32_t>();
         const uint64_t got = oo[S.n];
         const uint64_t w = S.narrow ? 4 : 8;
-        BT_HIP(S.h_ids.ensure(got * w + 8));
+        raise_hw(hw_ids, (double)got / std::max<uint32_t>(S.n, 1));
+        BT_HIP(S.h_ids.ensure(got * w + 8, hint_of(hw_ids, w)));
         // chunks of >= 2 MiB of ids, at most MAXCH, cut at publish boundaries
         uint32_t nch = (uint32_t)std::min<uint64_t>(Slot::MAXCH, std::max<uint64_t>(1, got * w >> 21));
         nch = std::max<uint32_t>(1, std::min<uint32_t>(nch, S.n));

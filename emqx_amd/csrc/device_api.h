@@ -43,6 +43,7 @@ constexpr uint32_t CTL_BYTES = 32, CTL_CURSOR = 0, CTL_SLOW = 8, CTL_SEG = 16, C
 struct BndCaps {
     uint64_t bytes, off, wtab, warena, word_off, etab, slot_list, arena, key_bin, key_rec, key_dd;  // inputs, index
     uint64_t out, keys, slow_list, scratch, seg_pool, wave_chunks, fr_pool, wave_info;     // outputs, scratch
+    uint64_t pre_wid, pre_meta;                                                              // k_prescan
 };
 #if TM_BOUNDS && defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ uint64_t tm_bchk(uint64_t i, uint64_t cap, uint32_t line, unsigned long long *rec) {
@@ -148,11 +149,25 @@ struct MatchArgs {
     uint32_t *ucnt;
     uint2 *wl;
     uint32_t *wl_n;
+    // Pre-pass (round 5): k_prescan tokenises every topic and looks up the word ids of its
+    // first TM_PRELOOK levels in a launch of its own (pre_wid[l * pre_stride + t]; pre_meta[t]
+    // = {levels | badarg << 30 | '$' << 31, byte where level TM_PRELOOK starts}), and
+    // k_match_fast reads them instead of staging the topic bytes and scanning them itself.
+    // Null pre_wid: k_match_fast does its own pre-scan.
+    uint32_t *pre_wid;
+    uint2 *pre_meta;
+    uint32_t pre_stride;
     // Real capacities (elements) of the buffers above, and the bounds record: read only by the
     // TM_BOUNDS debug build, whose kernels check every index against them (BI() above).
     BndCaps cap;
     unsigned long long *bnd;
 };
+
+// Levels whose word ids the pre-scan looks up, all in flight together (k_match_fast's own
+// pre-scan, or k_prescan)
+#ifndef TM_PRELOOK
+#define TM_PRELOOK 10
+#endif
 
 // Topics per wave of k_match_fast.  A wave's walk is a chain of dependent round trips
 // whose length grows with its frontier, so a small batch is spread thin (down to 4

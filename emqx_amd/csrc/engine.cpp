@@ -230,6 +230,7 @@ struct BatchBufs {
     DevBuf d_dd_wl, d_dd_wl_n;  // k_dd_pass -> k_dedupe worklist
     DevBuf d_kcnt, d_rcur;      // runs: ids per topic; the batch's span cursor (shared by its sub-batches)
     DevBuf d_wave_info;         // ids modes: per wave {base, ids, spilled} (MatchArgs.wave_info)
+    DevBuf d_pre;               // k_prescan's output: TM_PRELOOK word ids + {levels, byte} per topic
     DevBuf d_res_scan;          // scan scratch of the set's result passes (one per set: sets run concurrently)
     // A launch's counters live in one 32-B block {cursor u64, slow_count u32 (+pad),
     // seg_cursor u64, fr_cursor u64}.  Two blocks alternate: each launch zeroes the block
@@ -246,7 +247,7 @@ struct BatchBufs {
     void release() {
         for (DevBuf *b : {&d_bytes, &d_off, &d_outoff, &d_outcnt, &d_status, &d_keys, &d_slow_list, &d_scr_w, &d_scr_s,
                           &d_seg_pool, &d_fr_pool, &d_wave_chunks, &d_ukeys, &d_ucnt, &d_dd_wl, &d_dd_wl_n, &d_kcnt,
-                          &d_rcur, &d_ctl, &d_wave_info, &d_res_scan})
+                          &d_rcur, &d_ctl, &d_wave_info, &d_pre, &d_res_scan})
             b->release();
     }
 };
@@ -1034,6 +1035,8 @@ struct tm_engine {
         c.wave_chunks = bnd_cap_of(a.wave_chunks, 4);
         c.fr_pool = bnd_cap_of(a.fr_pool, 8);
         c.wave_info = a.wave_info ? bnd_cap_of(a.wave_info, 16) : 0;
+        c.pre_wid = a.pre_wid ? bnd_cap_of(a.pre_wid, 4) : 0;
+        c.pre_meta = a.pre_meta ? bnd_cap_of(a.pre_meta, 8) : 0;
         // self-test of the bounds build (tests/test_gpu_bounds.py): pretend the edge table has
         // one slot, so every probe past slot 0 must be recorded (and redirected to slot 0)
         static const bool selftest = getenv("EMQX_TM_BOUNDS_SELFTEST") != nullptr;
@@ -2856,6 +2859,7 @@ struct tm_engine {
         std::vector<uint32_t> wcode;     // interned word id -> order code (NONE: not cached yet)
         std::vector<uint32_t> h_kw, h_koff, h_kend;  // host copies of the order (plan_filter_parts)
         DevBuf d_items, d_stop;          // FW_RUNS parts: {query, start, end, first}; per part: stopped
+        DevBuf d_wtime;                  // development: per wave duration (EMQX_TM_FILTER_WTIME)
         std::vector<uint4> items;
         std::vector<uint32_t> i_cnt, i_rcnt, i_off, i_stop;
         std::vector<uint8_t> qdollar;
@@ -3026,10 +3030,11 @@ struct tm_engine {
     // from c_k as if it had arrived there (part 0 from the query's own start), and the query's
     // result is its parts' results in order up to the first part that stopped.
     // Items {query, start, end (NONE: none), first part?}, queries in order, parts in order.
-    // EMQX_TM_FILTER_SPLIT=min_keys:part_keys (0 disables; default 16384:4096).
+    // EMQX_TM_FILTER_SPLIT=min_keys:part_keys (0 or unset: no split, the default).
     void plan_filter_parts(uint32_t n, std::vector<uint4> &items) {
         items.clear();
-        uint32_t min_keys = 16384, part_keys = 4096;  // read per call: tests change it
+        // off by default: every setting measured made the batches slower
+        uint32_t min_keys = 0, part_keys = 4096;  // read per call: tests change it
         if (const char *e = getenv("EMQX_TM_FILTER_SPLIT")) {
             min_keys = (uint32_t)strtoul(e, nullptr, 10);
             if (const char *c = strchr(e, ':')) part_keys = std::max(1u, (uint32_t)strtoul(c + 1, nullptr, 10));
@@ -3419,6 +3424,17 @@ struct TopicOut {
     uint32_t *off, *cnt, *kcnt;
     int32_t *status;
 };
+#ifndef TM_PREPASS
+#define TM_PREPASS 0
+#endif
+// k_prescan ahead of k_match_fast<PRE>: off by default, measured 4 % slower
+// (0.7185 vs 0.6923 ms per batch, profiles/r05_sweep_pre.jsonl) although it lifts the walk
+// to 20 waves per CU; EMQX_TM_PREPASS=0 / 1 overrides the build's default per launch
+static bool prepass_on() {
+    const char *e = getenv("EMQX_TM_PREPASS");
+    return e ? atoi(e) != 0 : TM_PREPASS != 0;
+}
+
 static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const uint32_t *d_off, uint32_t n,
                                 hipStream_t s, uint32_t mode = MODE_ALL, uint32_t obase = 0, uint32_t *keys = nullptr,
                                 uint64_t keys_cap = 0, unsigned long long *cursor = nullptr,
@@ -3505,6 +3521,18 @@ static hipError_t enqueue_match(tm_engine *eng, const uint8_t *d_bytes, const ui
     a.fr_pool = eng->bb->d_fr_pool.as<uint2>();
     a.fr_chunks = eng->bb->fr_chunks;
     a.fr_cursor = (unsigned long long *)(eng->bb->p_ctl + CTL_FR);
+    if (mode != MODE_FIRST && prepass_on() && TM_PRELOOK > 0) {
+        // k_prescan's output, SoA: level l's word ids at [l * stride, ..), then the topics' meta
+        const uint64_t stride = ((uint64_t)n + 63) & ~63ull;
+        const uint64_t want = stride * TM_PRELOOK * 4 + stride * 8;
+        if (eng->bb->d_pre.cap < want) {
+            const hipError_t e = eng->grow_buf(eng->bb->d_pre, want + want / 4);
+            if (e) return e;
+        }
+        a.pre_wid = eng->bb->d_pre.as<uint32_t>();
+        a.pre_meta = reinterpret_cast<uint2 *>(eng->bb->d_pre.as<uint8_t>() + stride * TM_PRELOOK * 4);
+        a.pre_stride = (uint32_t)stride;
+    }
     a.stats = eng->stats_on ? eng->d_stats.as<unsigned long long>() : nullptr;
     a.ev_fast0 = eng->timing_on ? eng->ev_fast0 : nullptr;
     a.ev_fast1 = eng->timing_on ? eng->ev_fast1 : nullptr;
@@ -4493,6 +4521,12 @@ int tm_match_filter_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint3
         fx.i_rcnt.resize(ni);
         fx.i_stop.resize(ni);
     }
+    // development: per-wave durations, the slowest reported on stderr (what sets a batch's time)
+    static const bool wtime = getenv("EMQX_TM_FILTER_WTIME") != nullptr;
+    if (wtime) {
+        TM_TRY_HIP(fx.d_wtime.ensure((size_t)ni * 8), TM_ENOMEM, "alloc");
+        a.wtime = fx.d_wtime.as<unsigned long long>();
+    }
     uint32_t *h_off = parts ? fx.i_off.data() : o.f_off.data(), *h_cnt = parts ? fx.i_cnt.data() : o.f_cnt.data(),
              *h_rcnt = parts ? fx.i_rcnt.data() : o.f_rcnt.data();
     uint64_t ranges = 0;
@@ -4538,6 +4572,26 @@ int tm_match_filter_batch_runs(tm_engine *eng, const uint8_t *bytes, const uint3
     if (!done) {
         eng->err = "tm_match_filter_batch_runs: output still short after resizing";
         return TM_EDEVICE;
+    }
+    if (wtime) {
+        std::vector<unsigned long long> wt(ni);
+        TM_TRY_HIP(hipMemcpy(wt.data(), fx.d_wtime.p, (size_t)ni * 8, hipMemcpyDeviceToHost), TM_EDEVICE, "D2H");
+        std::vector<uint32_t> ord(ni);
+        for (uint32_t i = 0; i < ni; i++) ord[i] = i;
+        std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return wt[x] > wt[y]; });
+        unsigned long long sum = 0;
+        for (auto v : wt) sum += v;
+        fprintf(stderr, "[filter wtime] waves %u, sum %.1f us, max %.1f us, p50 %.1f us; slowest:", ni, sum / 100.0,
+                wt[ord[0]] / 100.0, wt[ord[ni / 2]] / 100.0);
+        for (uint32_t k = 0; k < std::min<uint32_t>(ni, 8); k++) {
+            const uint32_t i = ord[k];
+            const uint32_t q = parts ? fx.items[i].x : i;
+            std::string qs;
+            for (uint32_t j = fx.qoff[q]; j < fx.qoff[q + 1]; j++) qs += (fx.qw[j] == 1 ? "+" : fx.qw[j] == 0 ? "#" : "w") + std::string(j + 1 < fx.qoff[q + 1] ? "/" : "");
+            fprintf(stderr, " [q %u %s part %u..%u keys %u %.1f us]", q, qs.c_str(), parts ? fx.items[i].y : 0u,
+                    parts ? fx.items[i].z : NONE, h_cnt[i], wt[i] / 100.0);
+        }
+        fprintf(stderr, "\n");
     }
     // ranges of the sorted keys -> spans of their ids (this lane keeps the ids alive)
     o.f_ids = fx.ids;

@@ -50,6 +50,9 @@ struct FilterArgs {
     const uint4 *items;
     uint32_t n_items;
     uint32_t *stop;
+    // development (EMQX_TM_FILTER_WTIME=1, FW_RUNS): per wave, its duration in wall-clock ticks
+    // (100 MHz); null in the product
+    unsigned long long *wtime;
 };
 constexpr int FW_COUNT = 0, FW_EMIT = 1, FW_ONEPASS = 2, FW_RUNS = 3;
 constexpr uint32_t FW_CHUNK = 256;   // u32 words per pool chunk (1 link entry + 127 ranges of 2 words)

@@ -220,6 +220,7 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
     const uint32_t it = blockIdx.x * 4 + (threadIdx.x >> 6);  // the item: a query, or a part of one
     const uint32_t lane = threadIdx.x & 63;
     if (it >= (a.items ? a.n_items : a.n)) return;  // wave-uniform
+    const unsigned long long t_begin = a.wtime ? wall_clock64() : 0ull;
     const uint4 item = a.items ? a.items[it] : make_uint4(it, 0u, NONE_FW, 1u);
     const uint32_t q = item.x;
     const uint32_t qb = a.qoff[q], WL = a.qoff[q + 1] - qb;
@@ -440,6 +441,7 @@ __global__ __launch_bounds__(256) void k_filter_walk(FilterArgs a, int pass) {
             a.out_off[it] = (uint32_t)base;
             if (a.stop) a.stop[it] = reached ? 0u : 1u;
         }
+        if (a.wtime && lane == 0) a.wtime[it] = wall_clock64() - t_begin;  // before the range copy
         if (short_pool || base + nent > a.out_cap) return;  // the host grows and re-runs
         __threadfence_block();
         uint2 *out2 = reinterpret_cast<uint2 *>(a.out);

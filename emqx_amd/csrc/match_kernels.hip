@@ -70,9 +70,6 @@ constexpr uint32_t DO_PLUS = 0x80u, DO_LIT = 0x40u;  // frontier meta: probes th
 #ifndef TM_QMED
 #define TM_QMED 2  // a "medium" list is at most TM_QMED group-iterations long
 #endif
-#ifndef TM_PRELOOK
-#define TM_PRELOOK 10  // levels whose word ids are looked up in the pre-scan, all in flight together
-#endif
 #ifndef TM_CP_UNROLL
 #define TM_CP_UNROLL 8
 #endif
@@ -326,8 +323,9 @@ __device__ __forceinline__ uint32_t prelook_word(const uint32_t (&widr)[TM_PRELO
 // is flushed to a global chunk pool when full, and per-topic cursors.  Levels are
 // tokenised lazily (one level per depth) so there is no level cap; a topic only
 // spills to k_match_slow when a pool is exhausted.
-struct WaveLds {
-    uint8_t tb[TBCAP];            // the wave's topic bytes (16-B aligned window)
+template <int TB>
+struct WaveLdsT {
+    uint8_t tb[TB];               // the wave's topic bytes (16-B aligned window; a stub with k_prescan)
     uint32_t fr_node[2][FCAP];
     uint8_t fr_meta[2][FCAP];     // topic lane | DO_PLUS / DO_LIT
     uint32_t fch[2][MAXF];        // global overflow chunks of each frontier buffer
@@ -340,13 +338,14 @@ struct WaveLds {
     unsigned long long spill;     // bit per topic lane: spill to k_match_slow
     unsigned long long alive[2];  // bit per topic lane: has frontier entries at this / the next depth
 };
+using WaveLds = WaveLdsT<TBCAP>;
 
 // Expand L.seg[0..ns) into the output.  Short segments (<= CP_SHORT keys, most of them
 // single inline keys) are copied by the lane that holds them; long ones (hot '#'
 // filters with thousands of subscribers) are queued and copied by the whole wave, 64
 // consecutive keys per instruction, CP_UNROLL instructions in flight.
-template <int OUT>
-__device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, uint32_t ns) {
+template <int OUT, class Lds>
+__device__ __forceinline__ void expand_segments(const MatchArgs &a, Lds &L, uint32_t ns) {
     const uint32_t lane = lane_id();
     uint32_t nlong = 0;  // wave-uniform; long segment indices are queued in L.seg_scan
     uint32_t nmed = 0;   // TM_QCOPY: medium lists, queued from the front (huge ones from the back)
@@ -481,7 +480,8 @@ __device__ __forceinline__ void expand_segments(const MatchArgs &a, WaveLds &L, 
 
 // MODE_RUNS copy-out: every segment of the wave becomes one host span of its topic (no key is
 // read or written: the consumer reads the ids from the engine's host id arena).
-__device__ __forceinline__ void emit_spans(const MatchArgs &a, const WaveLds &L, const uint4 *seg, uint32_t ns) {
+template <class Lds>
+__device__ __forceinline__ void emit_spans(const MatchArgs &a, const Lds &L, const uint4 *seg, uint32_t ns) {
     uint4 *spans = reinterpret_cast<uint4 *>(a.keys);
     for (uint32_t j = lane_id(); j < ns; j += WAVE) {
         const uint4 g = seg[j];
@@ -497,10 +497,104 @@ __device__ __forceinline__ void emit_spans(const MatchArgs &a, const WaveLds &L,
     }
 }
 
-template <bool STATS, int OUT>
+#if TM_PRELOOK
+// Pre-pass: one wave per 64 consecutive topics stages their bytes in LDS and runs the
+// pre-scan of k_match_fast (TM_PRESCAN_PRELOOK) at this kernel's own occupancy (2 KiB of LDS
+// per wave instead of the walk's 10), writing each topic's word ids and level count for
+// k_match_fast<PRE> (MatchArgs.pre_wid / pre_meta).  The walk then holds neither the topic
+// bytes nor the pre-scan's registers.
+template <bool STATS>
+__global__ __launch_bounds__(WAVE) void k_prescan(MatchArgs a) {
+    __shared__ uint8_t tb[TBCAP];
+    const uint32_t lane = lane_id();
+    const uint32_t t0 = blockIdx.x * WAVE, t = t0 + lane;
+    const bool active = t < a.n;
+    const uint32_t wb0 = a.off[BI(t0, off)], wb1 = a.off[BI(min(t0 + WAVE, a.n), off)];
+    const uint32_t tbase = wb0 & ~15u;
+    const bool staged = ((reinterpret_cast<uintptr_t>(a.bytes) & 15u) == 0) && (wb1 - tbase <= (uint32_t)TBCAP);
+    if (staged) {
+        for (uint32_t j = lane * 16; tbase + j < wb1; j += WAVE * 16) {
+            if (tbase + j + 16 <= wb1) {
+                *reinterpret_cast<uint4 *>(&tb[j]) = *reinterpret_cast<const uint4 *>(a.bytes + BIN(tbase + j, 16, bytes));
+            } else {
+                for (uint32_t k = 0; tbase + j + k < wb1; k++) tb[j + k] = a.bytes[BI(tbase + j + k, bytes)];
+            }
+        }
+        __syncthreads();
+    }
+    auto byte_at = [&](uint32_t i) -> uint8_t { return staged ? tb[i - tbase] : a.bytes[BI(i, bytes)]; };
+    bool badarg = false, dollar = false;
+    uint32_t nl = 0, b = 0, e = 0, pre_b = 0, probes = 0;
+    uint32_t widr[TM_PRELOOK];
+    if (active) {
+        b = a.off[BI(t, off)];
+        e = a.off[BI(t + 1, off)];
+        dollar = (e > b) && byte_at(b) == '$';
+        // TM_PRESCAN_PRELOOK's work, with its collision / long-word path moved out of the
+        // unrolled loop (here the compiler would otherwise keep the per-level arrays in scratch)
+        uint64_t key[TM_PRELOOK];
+        uint32_t tag[TM_PRELOOK], wst[TM_PRELOOK];
+        uint4 x[TM_PRELOOK];
+        uint32_t i = b;
+#pragma unroll
+        for (int l = 0; l < TM_PRELOOK; l++) {
+            widr[l] = NONE;
+            tag[l] = NONE;  // no such level
+            key[l] = 0;
+            wst[l] = 0;
+            if (i <= e) {  // level l exists and starts at byte i
+                wst[l] = i;
+                key[l] = level_key(&i, e, byte_at);
+                const uint32_t len = i - wst[l];
+                if (len == 1 && (key[l] == '+' || key[l] == '#') && !a.topic_words) badarg = true;
+                tag[l] = len > 8 ? (len | W_LONG) : len;
+                x[l] = *reinterpret_cast<const uint4 *>(a.wtab + BI(word_slot_hash(key[l], tag[l]) & a.wmask, wtab));
+                probes++;
+                nl++;
+                i++;
+            }
+        }
+        pre_b = i;
+#pragma unroll
+        for (int l = 0; l < TM_PRELOOK; l++) {
+            if (tag[l] == NONE) continue;
+            const uint32_t len = tag[l] & ~W_LONG;
+            const uint4 y = x[l];
+            if (y.w == NONE) continue;  // not in the dictionary
+            if (len <= 8 && y.z == tag[l] && y.x == (uint32_t)key[l] && y.y == (uint32_t)(key[l] >> 32))
+                widr[l] = y.w;
+            else  // a collision chain or a long word (byte check): the whole lookup again (rare)
+                widr[l] = word_lookup(a, key[l], len, wst[l], byte_at, &probes);
+        }
+        if (pre_b <= e) {  // levels past TM_PRELOOK: count them and check for badarg
+            uint32_t st = pre_b;
+            for (uint32_t i2 = pre_b;; ++i2) {
+                const bool end = i2 == e;
+                const uint8_t c = end ? (uint8_t)'/' : byte_at(i2);
+                if (c == '/') {
+                    if (i2 - st == 1 && (byte_at(st) == '+' || byte_at(st) == '#') && !a.topic_words) badarg = true;
+                    nl++;
+                    st = i2 + 1;
+                    if (end) break;
+                }
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < TM_PRELOOK; l++) a.pre_wid[BI((uint64_t)l * a.pre_stride + t, pre_wid)] = widr[l];
+        a.pre_meta[BI(t, pre_meta)] =
+            make_uint2(min(nl, 0x3FFFFFFFu) | (badarg ? 1u << 30 : 0u) | (dollar ? 1u << 31 : 0u), pre_b);
+    }
+    if constexpr (STATS) {
+        const uint64_t p = wave_sum64(probes);
+        if (lane == 0 && a.stats) atomicAdd(&a.stats[2], (unsigned long long)p);
+    }
+}
+#endif
+
+template <bool STATS, int OUT, bool PRE>
 __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) {
     constexpr bool RUNS = OUT == O_RUNS;
-    __shared__ WaveLds L;
+    __shared__ WaveLdsT<PRE ? 16 : TBCAP> L;
     uint32_t *const wchunks = a.wave_chunks + BIN((uint64_t)blockIdx.x * MAXCHUNK, MAXCHUNK, wave_chunks);  // this wave's flushed chunks
     const uint32_t lane = lane_id();
     const uint32_t t = blockIdx.x * a.tpw + lane;
@@ -516,7 +610,9 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     const uint32_t t0 = blockIdx.x * a.tpw;
     const uint32_t wb0 = a.off[BI(t0, off)], wb1 = a.off[BI(min(t0 + a.tpw, a.n), off)];
     const uint32_t tbase = wb0 & ~15u;
-    const bool staged = ((reinterpret_cast<uintptr_t>(a.bytes) & 15u) == 0) && (wb1 - tbase <= (uint32_t)TBCAP);
+    // (PRE: k_prescan did the pre-scan; only levels past TM_PRELOOK read bytes, from HBM)
+    const bool staged =
+        !PRE && ((reinterpret_cast<uintptr_t>(a.bytes) & 15u) == 0) && (wb1 - tbase <= (uint32_t)TBCAP);
     if (staged) {
         for (uint32_t j = lane * 16; tbase + j < wb1; j += WAVE * 16) {
             if (tbase + j + 16 <= wb1) {
@@ -535,7 +631,19 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
 #if TM_PRELOOK
     uint32_t widr[TM_PRELOOK];  // word ids of the first TM_PRELOOK levels
     uint32_t pre_b = 0;         // byte where level TM_PRELOOK starts
-    if (active) {
+    uint32_t pre_w0 = NONE;     // PRE: level 0's word id, loaded with the topic's meta
+    if constexpr (PRE) {
+        if (active) {
+            b = a.off[BI(t, off)];
+            e = a.off[BI(t + 1, off)];
+            const uint2 m = a.pre_meta[BI(t, pre_meta)];
+            pre_w0 = a.pre_wid[BI(t, pre_wid)];
+            nl = m.x & 0x3FFFFFFFu;
+            badarg = (m.x >> 30) & 1u;
+            dollar = (m.x >> 31) != 0;
+            pre_b = m.y;
+        }
+    } else if (active) {
         b = a.off[BI(t, off)];
         e = a.off[BI(t + 1, off)];
         dollar = (e > b) && byte_at(b) == '$';
@@ -583,7 +691,10 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
     auto level_word = [&](uint32_t slot, uint32_t lv) {
 #if TM_PRELOOK
         if (lv < (uint32_t)TM_PRELOOK) {
-            L.wid[slot][lane] = prelook_word(widr, lv);
+            if constexpr (PRE)
+                L.wid[slot][lane] = lv == 0 ? pre_w0 : a.pre_wid[BI((uint64_t)lv * a.pre_stride + t, pre_wid)];
+            else
+                L.wid[slot][lane] = prelook_word(widr, lv);
             return;
         }
 #endif
@@ -1744,17 +1855,33 @@ hipError_t launch_match(const MatchArgs &a, hipStream_t s) {
         k_first_slow<<<grid < 2048u ? grid : 2048u, WAVE, 0, s>>>(a);
         return hipGetLastError();
     }
-    if (a.ev_fast0 && (e = hipEventRecord(a.ev_fast0, s))) return e;
+    if (a.ev_fast0 && (e = hipEventRecord(a.ev_fast0, s))) return e;  // (the timed span includes k_prescan)
+#if TM_PRELOOK
+    // (not the ids copy-outs: at PRE's 5 waves per SIMD their id arrays went to scratch)
+    if (a.pre_wid && a.mode != MODE_IDS32 && a.mode != MODE_IDS64) {
+        const unsigned pgrid = (unsigned)(((uint64_t)a.n + WAVE - 1) / WAVE);
+        if (a.stats) k_prescan<true><<<pgrid, WAVE, 0, s>>>(a);
+        else k_prescan<false><<<pgrid, WAVE, 0, s>>>(a);
+        if ((e = hipGetLastError())) return e;
+        if (a.mode == MODE_RUNS) {
+            if (a.stats) k_match_fast<true, O_RUNS, true><<<grid, WAVE, 0, s>>>(a);
+            else k_match_fast<false, O_RUNS, true><<<grid, WAVE, 0, s>>>(a);
+        } else {
+            if (a.stats) k_match_fast<true, O_KEYS, true><<<grid, WAVE, 0, s>>>(a);
+            else k_match_fast<false, O_KEYS, true><<<grid, WAVE, 0, s>>>(a);
+        }
+    } else
+#endif
     if (a.mode == MODE_RUNS) {
-        if (a.stats) k_match_fast<true, O_RUNS><<<grid, WAVE, 0, s>>>(a);
-        else k_match_fast<false, O_RUNS><<<grid, WAVE, 0, s>>>(a);
+        if (a.stats) k_match_fast<true, O_RUNS, false><<<grid, WAVE, 0, s>>>(a);
+        else k_match_fast<false, O_RUNS, false><<<grid, WAVE, 0, s>>>(a);
     } else if (a.mode == MODE_IDS32) {
-        k_match_fast<false, O_IDS32><<<grid, WAVE, 0, s>>>(a);
+        k_match_fast<false, O_IDS32, false><<<grid, WAVE, 0, s>>>(a);
     } else if (a.mode == MODE_IDS64) {
-        k_match_fast<false, O_IDS64><<<grid, WAVE, 0, s>>>(a);
+        k_match_fast<false, O_IDS64, false><<<grid, WAVE, 0, s>>>(a);
     } else {
-        if (a.stats) k_match_fast<true, O_KEYS><<<grid, WAVE, 0, s>>>(a);
-        else k_match_fast<false, O_KEYS><<<grid, WAVE, 0, s>>>(a);
+        if (a.stats) k_match_fast<true, O_KEYS, false><<<grid, WAVE, 0, s>>>(a);
+        else k_match_fast<false, O_KEYS, false><<<grid, WAVE, 0, s>>>(a);
     }
     if ((e = hipGetLastError())) return e;
     if (a.ev_fast1 && (e = hipEventRecord(a.ev_fast1, s))) return e;

@@ -56,3 +56,15 @@ def _bounds_guard():
     if r is not None and r[0] > _BOUNDS_SEEN[0]:
         _BOUNDS_SEEN[0] = r[0]
         pytest.fail(f"bounds build: {r[0]} findings: {r[1]}")
+
+
+def pytest_terminal_summary(terminalreporter):
+    """Under EMQX_TM_LIB: which library the run mapped, and (bounds build) its findings."""
+    if not os.environ.get("EMQX_TM_LIB"):
+        return
+    from emqx_amd import _native as N
+    if N._lib is None:
+        return
+    r = N.debug_bounds()
+    terminalreporter.write_line(f"library {N.LIB_PATH}: bounds checks {'active' if r is not None else 'absent'}"
+                                + (f", {r[0]} findings{': ' + r[1] if r[0] else ''}" if r is not None else ""))

@@ -7,6 +7,7 @@ keeps serving and the batch is retried (apps/emqx/src/emqx_router_syncer.erl:269
 Here every call may come from any thread (include/emqx_tm.h "Threading"); each batch sees
 exactly ONE committed epoch (checked bit-exactly against that epoch's oracle); a commit that
 would pass a capacity is refused before anything changes."""
+import os
 import threading
 
 import numpy as np
@@ -484,5 +485,7 @@ def test_host_form_readers_overlap():
                 assert dg[k] == want[k], (form, T, k)
     print(f"runs form: one thread {walls[(0, 1)] * 1e3:.2f} ms, four threads {walls[(0, 4)] * 1e3:.2f} ms; keys form: "
           f"{walls[(1, 1)] * 1e3:.2f} / {walls[(1, 4)] * 1e3:.2f} ms ({reps} calls of {per} topics per thread)")
+    if "bounds" in os.path.basename(os.environ.get("EMQX_TM_LIB", "")):
+        return  # the bounds build synchronises after every launch to scan its canaries: no overlap
     assert walls[(0, 4)] < 2.0 * walls[(0, 1)], walls
     eng.close()

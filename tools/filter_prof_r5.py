@@ -41,7 +41,7 @@ def line(name):
 
 print("# `k_filter_walk` at config C (10.65 M keys), round 5 source — `tools/prof_filter_r5.sh`\n")
 for name, what in (("mixed", "mixed 100 K-query batch (stored / one '+' / prefix + '#')"),
-                   ("plus", "one-'+' queries only (≈ 3 K), split into parts (default 16384:4096)"),
+                   ("plus", "one-'+' queries only (≈ 3 K), split into parts (16384:4096, the round's first default)"),
                    ("plus_nosplit", "one-'+' queries only, unsplit (EMQX_TM_FILTER_SPLIT=0)")):
     ls = trace(name)
     j = line(name)

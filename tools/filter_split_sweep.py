@@ -24,6 +24,8 @@ def main():
     eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
     eng.commit()
     sets = {"plus": bench.filter_queries(w, 9000, kinds=[1]), "mixed": bench.filter_queries(w, 100000)}
+    if os.environ.get("QUERIES"):  # e.g. QUERIES=plus
+        sets = {k: v for k, v in sets.items() if k in os.environ["QUERIES"].split(",")}
     ref = {}
     for name, (qb, qo) in sets.items():
         qo = np.ascontiguousarray(qo, dtype=np.uint32)

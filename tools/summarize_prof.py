@@ -20,7 +20,8 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "k_match_fast<false, 0>"  # STATS off, keys output (the headline step)
+KERNEL = "k_match_fast<false, 0"  # STATS off, keys output (the headline step; <.., PRE> since round 5)
+PRE = "k_prescan<false>"            # round 5: the pre-scan kernel launched ahead of it (if any)
 
 
 def per_kernel(path, kernel=KERNEL):
@@ -43,12 +44,21 @@ def main(src, dst):
     out["kernel_stats"] = [{k: r[k] for k in ("Name", "Calls", "AverageNs", "Percentage", "MinNs", "MaxNs")}
                            for r in rows]
     fast = [r for r in rows if KERNEL in r["Name"]][0]
-    avg_ns = float(fast["AverageNs"])
-    pmc = {}
+    pre = [r for r in rows if PRE in r["Name"]]
+    # the step's kernels: k_prescan (when launched) + k_match_fast, per launch pair
+    avg_ns = float(fast["AverageNs"]) + (float(pre[0]["AverageNs"]) if pre else 0.0)
+    out["kernels"] = [KERNEL] + ([PRE] if pre else [])
+    pmc, pmc_pre = {}, {}
     for name in ("fetch", "write", "tcc", "sq"):
         p = os.path.join(src, name, f"{name}_counter_collection.csv")
         if os.path.exists(p):
             pmc.update(per_kernel(p))
+            if pre:
+                pmc_pre.update(per_kernel(p, PRE))
+    for k in ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum"):
+        if k in pmc and k in pmc_pre:
+            pmc[k] += pmc_pre[k]
+    out["pmc_per_launch_prescan"] = pmc_pre
     out["pmc_per_launch"] = pmc
     bench = json.load(open(os.path.join(src, "trace.bench.json")))
     out["bench_line"] = bench

@@ -73,6 +73,12 @@ VARIANTS = {
     "el2": ([], 2),
     "el4": ([], 4),
     "el8": ([], 8),
+    # round 5: the pre-scan as its own kernel (k_prescan) ahead of k_match_fast<PRE>
+    "pre": (["-DTM_PREPASS=1"], 0),
+    "nopass": (["-DTM_PREPASS=0"], 0),
+    "pre_w20": (["-DTM_PREPASS=1", "-DTM_MIN_WAVES=5"], 0),
+    "pre2": (["-DTM_PREPASS=1"], 0),
+    "nopass2": (["-DTM_PREPASS=0"], 0),
 }
 
 
