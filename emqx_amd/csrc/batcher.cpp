@@ -47,6 +47,7 @@
 
 extern "C" int tmx_engine_device(const tm_engine *eng);  // engine.cpp, library-internal
 extern "C" int tmx_engine_grow_pools(tm_engine *eng, uint32_t set, uint64_t seg_demand, uint64_t fr_demand);
+extern "C" int tmx_engine_reserve_batch(tm_engine *eng, uint32_t set, uint32_t n, uint64_t bytes);
 extern "C" void tmx_engine_pool_caps(const tm_engine *eng, uint32_t set, uint64_t *seg_chunks, uint64_t *fr_chunks);
 extern "C" int tmx_result_ids32_device(tm_engine *eng, uint32_t set, uint32_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
                                        void *stream);
@@ -1267,6 +1268,11 @@ struct tm_batcher {
             // EMQX_TM_STREAMS=1: every window on one stream and one buffer set (A/B runs)
             const char *es = std::getenv("EMQX_TM_STREAMS");
             const uint32_t nstreams = es && std::atoi(es) == 1 ? 1u : 2u;
+            // the engine's buffer sets sized for max_batch windows of up to 128 B per topic
+            // now, not by the first window that outgrows them (later growth stays possible)
+            for (uint32_t st = 0; st < nstreams; st++)
+                if (tmx_engine_reserve_batch(eng, st, cfg.max_batch, (uint64_t)cfg.max_batch * 128) != TM_OK)
+                    return TM_ENOMEM;
             for (uint32_t i = 0; i < NSLOT_MAX; i++) {
                 slot[i].set = nstreams == 2 ? (i & 1u) : 0u;
                 for (hipEvent_t &e : slot[i].cev)

@@ -5384,6 +5384,16 @@ __attribute__((visibility("hidden"))) int tmx_batch_match_runs(tm_engine *eng, u
     *d_ctl_out = eng->bb->p_ctl;
     return TM_OK;
 }
+// library-internal (batcher.cpp): size buffer set `set` for batches of up to n topics and
+// `bytes` topic bytes before the first window, so no window grows them (a growth waits for
+// the whole device: the aggregator's slowest windows, round 5)
+__attribute__((visibility("hidden"))) int tmx_engine_reserve_batch(tm_engine *eng, uint32_t set, uint32_t n,
+                                                                   uint64_t bytes) {
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    eng->bb = eng->batch_set(set);
+    if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
+    return ensure_batch(eng, n, bytes);
+}
 // library-internal (batcher.cpp): tm_reserve_matches for the aggregator's buffer set
 __attribute__((visibility("hidden"))) int tmx_batch_reserve_matches(tm_engine *eng, uint32_t set, uint64_t keys_cap) {
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
