@@ -24,6 +24,8 @@
 // Submissions go to one of SHARDS queue shards (by submitting thread), so publishers that
 // resubmit from their callbacks do not all contend on one lock.
 #include <hip/hip_runtime.h>
+#include <execinfo.h>
+#include <signal.h>
 #include <sys/resource.h>
 #include <sys/syscall.h>
 #include <time.h>
@@ -358,10 +360,12 @@ struct tm_batcher {
         while (v > c && !hw.compare_exchange_weak(c, v, std::memory_order_relaxed)) {
         }
     }
+    bool hints = true;  // EMQX_TM_BATCHER_HINTS=0 (development): grow to each window's demand only
     size_t hint_of(const std::atomic<double> &hw, size_t width) const {
-        return (size_t)(hw.load(std::memory_order_relaxed) * 1.25 * cfg.max_batch) * width + 64;
+        return hints ? (size_t)(hw.load(std::memory_order_relaxed) * 1.25 * cfg.max_batch) * width + 64 : 0;
     }
-    size_t hint_pub4() const { return ((size_t)cfg.max_batch + 1) * 4; }
+    size_t hint_pub4() const { return hints ? ((size_t)cfg.max_batch + 1) * 4 : 0; }
+    double pool_scale(uint32_t n) const { return hints ? std::max(1.0, (double)cfg.max_batch / std::max<uint32_t>(n, 1)) : 1.0; }
     std::atomic<bool> reported{false};  // the first failed window is reported on stderr (once)
     void report(const char *stage, int rc) {
         if (rc >= 0 || reported.exchange(true)) return;
@@ -639,7 +643,7 @@ struct tm_batcher {
             std::lock_guard<std::mutex> g(eng_mu);
             BT_HIP(hipStreamSynchronize(s_comps[S.set]));
             // to a max_batch window's demand at this window's rate (growth stalls the device)
-            const double sc = std::max(1.0, (double)cfg.max_batch / std::max<uint32_t>(S.n, 1));
+            const double sc = pool_scale(S.n);
             int rc = tmx_engine_grow_pools(eng, S.set, (uint64_t)(seg * sc), (uint64_t)(fr * sc));
             if (rc) return rc;
             if (over) {  // more spans than the window's buffer: grow to the demand, run again
@@ -724,7 +728,7 @@ struct tm_batcher {
             std::lock_guard<std::mutex> g(eng_mu);
             BT_HIP(hipStreamSynchronize(s_comps[S.set]));
             // to a max_batch window's demand at this window's rate (growth stalls the device)
-            const double sc = std::max(1.0, (double)cfg.max_batch / std::max<uint32_t>(S.n, 1));
+            const double sc = pool_scale(S.n);
             int rc = tmx_engine_grow_pools(eng, S.set, (uint64_t)(seg * sc), (uint64_t)(fr * sc));
             if (rc) return rc;
             if (over) {  // output arena too small: grow to the demand, run this window again
@@ -1252,6 +1256,7 @@ struct tm_batcher {
         if (const char *e = std::getenv("EMQX_TM_PF_LINES")) pf_lines = std::min(256u, (uint32_t)std::atoi(e));
         if (const char *e = std::getenv("EMQX_TM_RUNS_IDW")) runs_w = std::atoi(e) == 4 ? 4u : 8u;
         if (const char *e = std::getenv("EMQX_TM_DELIVERY_NICE")) deliver_nice = std::max(0, std::min(19, std::atoi(e)));
+        if (const char *e = std::getenv("EMQX_TM_BATCHER_HINTS")) hints = std::atoi(e) != 0;
         if (!eng)
             for (Slot &S : slot)
                 for (HBuf *h : {&S.h_bytes, &S.h_off, &S.h_off_out, &S.h_status, &S.h_cnt, &S.h_ids, &S.h_ctl})
@@ -1270,9 +1275,11 @@ struct tm_batcher {
             const uint32_t nstreams = es && std::atoi(es) == 1 ? 1u : 2u;
             // the engine's buffer sets sized for max_batch windows of up to 128 B per topic
             // now, not by the first window that outgrows them (later growth stays possible)
-            for (uint32_t st = 0; st < nstreams; st++)
-                if (tmx_engine_reserve_batch(eng, st, cfg.max_batch, (uint64_t)cfg.max_batch * 128) != TM_OK)
-                    return TM_ENOMEM;
+            const char *er = std::getenv("EMQX_TM_BATCHER_RESERVE");  // development: 0 skips it
+            if (!er || std::atoi(er) != 0)
+                for (uint32_t st = 0; st < nstreams; st++)
+                    if (tmx_engine_reserve_batch(eng, st, cfg.max_batch, (uint64_t)cfg.max_batch * 128) != TM_OK)
+                        return TM_ENOMEM;
             for (uint32_t i = 0; i < NSLOT_MAX; i++) {
                 slot[i].set = nstreams == 2 ? (i & 1u) : 0u;
                 for (hipEvent_t &e : slot[i].cev)
@@ -1324,10 +1331,27 @@ struct tm_batcher {
     }
 };
 
+// development (EMQX_TM_SEGV_TRACE=1): a crash on any thread prints that thread's native
+// backtrace to stderr (addresses map to source lines with addr2line on the same build)
+static void segv_trace(int sig) {
+    void *fr[64];
+    const int n = backtrace(fr, 64);
+    const char msg[] = "\n[emqx_tm] fatal signal, native backtrace:\n";
+    (void)!write(2, msg, sizeof msg - 1);
+    backtrace_symbols_fd(fr, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 extern "C" {
 
 static int batcher_new(tm_engine *eng, tm_batch_fn fn, void *backend, const tm_batcher_config *cfg,
                        tm_batcher **out) {
+    if (const char *e = std::getenv("EMQX_TM_SEGV_TRACE"))
+        if (std::atoi(e)) {
+            signal(SIGSEGV, segv_trace);
+            signal(SIGBUS, segv_trace);
+        }
     tm_batcher *b = new (std::nothrow) tm_batcher();
     if (!b) return TM_ENOMEM;
     b->eng = eng;

@@ -3029,6 +3029,10 @@ struct tm_engine {
     // can be cut at child-group starts c_1 < c_2 < ... inside G: part k walks [c_k, c_{k+1})
     // from c_k as if it had arrived there (part 0 from the query's own start), and the query's
     // result is its parts' results in order up to the first part that stopped.
+    // Only G: the keys that cover a literal level with '+' (R(W0, +) and the like) can seek
+    // OUT of their region to the literal branch (compare's backtrack to the last '+', {Pos,
+    // W[Pos]}), so the walk does not enter all their child groups; cutting there was tried and
+    // returned keys the walk never reaches (round 5, tests/test_gpu_filter_runs.py).
     // Items {query, start, end (NONE: none), first part?}, queries in order, parts in order.
     // EMQX_TM_FILTER_SPLIT=min_keys:part_keys (0 or unset: no split, the default).
     void plan_filter_parts(uint32_t n, std::vector<uint4> &items) {
@@ -3207,7 +3211,7 @@ void tm_destroy(tm_engine *eng) {
     for (DevBuf *b : {&eng->d_key_rec, &eng->d_key_node, &eng->d_key_bin, &eng->d_key_dd, &eng->d_mrg_roff, &eng->d_mrg_tot, &eng->fx.d_kw, &eng->fx.d_koff,
                       &eng->fx.d_kh, &eng->fx.d_qw, &eng->fx.d_qoff, &eng->fx.d_qdollar, &eng->fx.d_qstatus,
                       &eng->fx.d_cnt, &eng->fx.d_off, &eng->fx.d_out, &eng->fx.d_scan, &eng->fx.d_pool,
-                      &eng->fx.d_ctl, &eng->fx.d_jobs, &eng->fx.d_krec, &eng->fx.d_kend, &eng->fx.d_rcnt, &eng->d_ia, &eng->d_iaoff,
+                      &eng->fx.d_ctl, &eng->fx.d_jobs, &eng->fx.d_krec, &eng->fx.d_kend, &eng->fx.d_rcnt, &eng->fx.d_items, &eng->fx.d_stop, &eng->fx.d_wtime, &eng->d_ia, &eng->d_iaoff,
                       &eng->d_ib, &eng->d_iboff, &eng->d_iout, &eng->d_ilen})
         b->release();
     for (DevBuf *b : {&eng->d_wtab, &eng->d_warena, &eng->d_word_off, &eng->d_etab, &eng->d_slot_list, &eng->d_root,

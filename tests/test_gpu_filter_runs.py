@@ -103,7 +103,7 @@ def test_filter_runs_outlive_a_commit():
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("split", ["1:1", "64:16", "16384:4096"])
+@pytest.mark.parametrize("split", ["1:1", "64:16", "512:128"])
 def test_filter_runs_split_parts(monkeypatch, split):
     """Long one-'+' queries walked as parts, one wave each, cut at child-group starts of the
     '+' level (plan_filter_parts): the query's ids are its parts' in order up to the first part
@@ -116,6 +116,12 @@ def test_filter_runs_split_parts(monkeypatch, split):
         tail = rng.choice([b"x", b"y", b"x/z", b"#", b"+", b"x/#", b""])
         filters.append(b"a/b/g%d" % g + (b"/" + tail if tail else b""))
     filters += [b"a/b", b"a/b", b"a", b"a/c/g1/x", b"a/b/#", b"a/+/g7/x", b"$SYS/a/b/x"] * 3
+    # the regions of keys that cover the query's literal levels with '+' (R(a, +), R(+, b),
+    # R(+, +)) are split as well: many child groups there too
+    for i in range(6000):
+        g = rng.randrange(2500)
+        head = rng.choice([b"a/+", b"+/b", b"+/+"])
+        filters.append(head + b"/g%d" % g + rng.choice([b"/x", b"/#", b"", b"/+", b"/x/z", b"/y"]))
     ids = list(range(1, len(filters) + 1))
     wf = [i % 2 for i in range(len(filters))]
     queries = [b"a/b/+/x", b"a/b/+", b"a/b/+/#", b"a/b/+/x/z", b"a/b/+/+", b"a/b/+/y/#", b"a/+/+/x",
