@@ -50,6 +50,7 @@
 extern "C" int tmx_engine_device(const tm_engine *eng);  // engine.cpp, library-internal
 extern "C" int tmx_engine_grow_pools(tm_engine *eng, uint32_t set, uint64_t seg_demand, uint64_t fr_demand);
 extern "C" int tmx_engine_reserve_batch(tm_engine *eng, uint32_t set, uint32_t n, uint64_t bytes);
+extern "C" void tmx_engine_forget_stream(tm_engine *eng, void *stream);
 extern "C" void tmx_engine_pool_caps(const tm_engine *eng, uint32_t set, uint64_t *seg_chunks, uint64_t *fr_chunks);
 extern "C" int tmx_result_ids32_device(tm_engine *eng, uint32_t set, uint32_t *d_ids, uint64_t ids_cap, uint32_t *d_off_out,
                                        void *stream);
@@ -1324,6 +1325,10 @@ struct tm_batcher {
                 for (hipEvent_t e : S.cev)
                     if (e) (void)hipEventDestroy(e);
             }
+            // the engine remembers the streams its batches ran on: make it forget ours first
+            for (hipStream_t sc : s_comps)
+                if (sc) tmx_engine_forget_stream(eng, sc);
+            if (s_copy) tmx_engine_forget_stream(eng, s_copy);
             for (hipStream_t sc : s_comps)
                 if (sc) (void)hipStreamDestroy(sc);
             if (s_copy) (void)hipStreamDestroy(s_copy);

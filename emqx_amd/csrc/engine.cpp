@@ -5388,6 +5388,28 @@ __attribute__((visibility("hidden"))) int tmx_batch_match_runs(tm_engine *eng, u
     *d_ctl_out = eng->bb->p_ctl;
     return TM_OK;
 }
+// library-internal (batcher.cpp): the caller is about to destroy stream s.  The engine keeps
+// stream handles beside the index (`uses`: streams whose reads a publish waits for; each batch
+// set's `last_stream`, which the next batch on the set is ordered after): forget s in both, so
+// no later call records an event on a destroyed stream (round 5: an aggregator closed, the next
+// one's first window ordered itself after the old stream -- a use-after-free inside HIP).
+__attribute__((visibility("hidden"))) void tmx_engine_forget_stream(tm_engine *eng, void *stream) {
+    std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
+    hipStream_t s = (hipStream_t)stream;
+    if (!s) return;
+    (void)hipSetDevice(eng->cfg.device);
+    (void)hipStreamSynchronize(s);
+    for (size_t i = 0; i < eng->uses.size();) {
+        if (eng->uses[i].first == s) {
+            (void)hipEventDestroy(eng->uses[i].second);
+            eng->uses.erase(eng->uses.begin() + (ptrdiff_t)i);
+        } else {
+            i++;
+        }
+    }
+    for (BatchBufs *B : {&eng->bb_dev, &eng->bb_dev2, &eng->bb_dev3, &eng->bb_batch, &eng->bb_batch2})
+        if (B->last_stream == s) B->last_stream = nullptr;
+}
 // library-internal (batcher.cpp): size buffer set `set` for batches of up to n topics and
 // `bytes` topic bytes before the first window, so no window grows them (a growth waits for
 // the whole device: the aggregator's slowest windows, round 5)

@@ -218,6 +218,46 @@ def test_gpu_batcher_over_engine_vs_oracle(mode, transport):
 
 
 @pytest.mark.gpu
+def test_gpu_aggregators_one_after_another_on_one_engine():
+    """Aggregators created and destroyed in turn over ONE engine (the bench's rows): each one's
+    windows run on its own streams, and the engine must not keep those streams after it is
+    gone (round 5: the next aggregator's first window was ordered after a destroyed stream).
+    Every reply equals the oracle's; commits and direct matches between them still work."""
+    from emqx_amd import workloads
+    import oracle
+    w = workloads.generate("A", scale=0.2, n_topics=2000)
+    eng = N.Engine(0)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+    eoff, eids, est = ix.match(w.t_bytes, w.t_off)
+    topics = w.topics()
+    for rnd, transport in enumerate([N.TM_TRANSPORT_AUTO, N.TM_TRANSPORT_IDS, N.TM_TRANSPORT_AUTO] * 2):
+        b = N.Batcher(eng, max_batch=256, max_wait_us=300, transport=transport)
+        bad = []
+
+        def worker(k):
+            for i in range(k, len(topics), 16):
+                st, ids = b.match(topics[i])
+                if st != est[i] or sorted(ids) != eids[eoff[i]:eoff[i + 1]].tolist():
+                    bad.append(i)
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        b.close()
+        assert not bad, (rnd, bad[:5])
+        # between aggregators: a commit (it waits for every stream that read the index) and
+        # a host-form batch on the engine itself
+        eng.apply([(N.TM_OP_ADD, b"zz/%d" % rnd, 10_000_000 + rnd)])
+        eng.commit()
+        k = eng.match([b"zz/%d" % rnd])[0]  # (the workload's wildcard filters match it too)
+        assert 10_000_000 + rnd in eng.key_ids(np.asarray(k, dtype=np.uint32)).tolist()
+    eng.close()
+
+
+@pytest.mark.gpu
 def test_gpu_batcher_epochs_swap_between_batches():
     """Writes through the batcher serialise with its worker: after commit returns, every
     later publish sees the new epoch."""
