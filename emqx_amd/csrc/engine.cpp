@@ -5418,7 +5418,17 @@ __attribute__((visibility("hidden"))) int tmx_engine_reserve_batch(tm_engine *en
     std::lock_guard<std::recursive_mutex> g(eng->mu_dev);
     eng->bb = eng->batch_set(set);
     if (hipSetDevice(eng->cfg.device) != hipSuccess) return TM_EDEVICE;
-    return ensure_batch(eng, n, bytes);
+    int rc = ensure_batch(eng, n, bytes);
+    if (rc) return rc;
+    // what a window of n topics grows besides (ids transport: per-wave info, scan scratch),
+    // and the chunk pools at 4x / 4x the first batch's default (config C's 12 K-publish windows
+    // asked for ~2x of it): the growth the round-5 window traces showed as 13-20 ms stalls
+    const uint64_t nwaves = match_grid(n, pick_tpw(n, eng->cfg.topics_per_wave));
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_wave_info, nwaves * 16 + 16), TM_ENOMEM, "alloc");
+    TM_TRY_HIP(eng->grow_buf(eng->bb->d_res_scan, scan_scratch_words(n) * 4), TM_ENOMEM, "alloc");
+    eng->bb->seg_demand_last = std::max<uint64_t>(eng->bb->seg_demand_last, ((uint64_t)n + 63) / 64 * 32);
+    eng->bb->fr_demand_last = std::max<uint64_t>(eng->bb->fr_demand_last, ((uint64_t)n + 63) / 64 * 16);
+    return grow_pools(eng);
 }
 // library-internal (batcher.cpp): tm_reserve_matches for the aggregator's buffer set
 __attribute__((visibility("hidden"))) int tmx_batch_reserve_matches(tm_engine *eng, uint32_t set, uint64_t keys_cap) {
