@@ -455,6 +455,26 @@ def cpu_topology():
     return info
 
 
+def cgroup_cpu_stat():
+    """The job's cgroup CPU accounting (cgroup v2 cpu.stat): periods, throttled periods and
+    throttled time.  With a quota (cpu.max), a period whose quota runs out stops every thread
+    of the job until the period ends -- the match path's threads included.  {} when absent."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            kv = dict(line.split() for line in f if line.strip())
+        return {k: int(kv[k]) for k in ("nr_periods", "nr_throttled", "throttled_usec") if k in kv}
+    except (OSError, ValueError):
+        return {}
+
+
+def cgroup_delta(a, b):
+    if not a or not b:
+        return None
+    return {"periods": b.get("nr_periods", 0) - a.get("nr_periods", 0),
+            "throttled_periods": b.get("nr_throttled", 0) - a.get("nr_throttled", 0),
+            "throttled_ms": round((b.get("throttled_usec", 0) - a.get("throttled_usec", 0)) / 1e3, 3)}
+
+
 def host_rss_gib():
     """Peak resident host memory of this rank (the engine's host master copy + workload)."""
     import resource
@@ -1391,17 +1411,20 @@ def rebuild_leg(eng, w, d_bytes, d_off, n, topic_bytes, dev, frac=0.13):
     th.start()
     time.sleep(0.5)
     n_full0 = eng.stats()["n_full_rebuilds"]
+    cg0 = cgroup_cpu_stat()
     t0 = time.perf_counter()
     eng.apply_packed(N.TM_OP_DEL, fb, off, ids)
     eng.apply_packed(N.TM_OP_ADD, fb, off, ids)
     eng.commit()
     t1 = time.perf_counter()
+    cg1 = cgroup_cpu_stat()
     time.sleep(0.3)
     stop.set()
     th.join()
     st = eng.stats()
     before = [d for t, d in lat if t < t0]
     during = [d for t, d in lat if t0 <= t < t1]
+    worst = max(((d, t) for t, d in lat if t0 <= t < t1), default=None)
     return {"ops": 2 * k, "full_rebuild": int(st["n_full_rebuilds"]) > int(n_full0),
             "commit_s": round(t1 - t0, 3),
             "commit_phase_s": {"apply": round(st["commit_apply_us"] / 1e6, 3),
@@ -1415,6 +1438,8 @@ def rebuild_leg(eng, w, d_bytes, d_off, n, topic_bytes, dev, frac=0.13):
             "match_ms_during_commit": {"p50": round(float(np.percentile(during, 50)) * 1e3, 3) if during else None,
                                        "p99": round(float(np.percentile(during, 99)) * 1e3, 3) if during else None,
                                        "max": round(float(np.max(during)) * 1e3, 3) if during else None},
+            "max_at_ms": round((worst[1] - t0) * 1e3, 1) if worst else None,
+            "cgroup_during_commit": cgroup_delta(cg0, cg1),
             "note": "one epoch re-keys a share of the route keys (deleted and re-added: the same key set, all of them "
                     "deltas) so the commit takes the full-rebuild path; the index is uploaded into a standby device "
                     "image while the second thread keeps matching; match latency is wall time per batch incl. "

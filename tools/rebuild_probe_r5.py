@@ -1,0 +1,42 @@
+"""Matches during a forced full rebuild of config C, repeated, with the job's cgroup throttling
+counted over each commit (bench.py's rebuild leg, alone).  One JSON line per rebuild.
+
+    python tools/rebuild_probe_r5.py 3
+
+(profiles/r05_rebuild_probe.jsonl also holds runs with an experimental commit-helper count,
+env_commit_threads 16 vs none = 14; that knob was not kept.)"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from emqx_amd import _native as N  # noqa: E402
+from emqx_amd import workloads  # noqa: E402
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    n = 1_000_000
+    w = workloads.generate("C", n_topics=n)
+    eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
+    eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+    eng.commit()
+    dev = torch.device("cuda", 0)
+    d_bytes = torch.from_numpy(w.t_bytes).to(dev)
+    d_off = torch.from_numpy(w.t_off.view(np.int32)).to(dev)
+    torch.cuda.synchronize()
+    for r in range(reps):
+        out = bench.rebuild_leg(eng, w, d_bytes, d_off, n, int(d_off[n].item()), dev)
+        out.pop("note", None)
+        out["rep"] = r
+        out["env_commit_threads"] = os.environ.get("EMQX_TM_COMMIT_THREADS")
+        print(json.dumps(out), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
