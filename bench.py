@@ -868,15 +868,22 @@ def main():
                      "note": "H2D of the topics + kernels + D2H of every key + host result view; "
                              "bounded by PCIe D2H of the keys"}
         host_runs = host_runs_leg(eng, tb, to32, n, w, reps=max(10, args.steps))
+        # the host-bound legs re-pick their cores first: another job may have moved onto the
+        # ones picked at start-up (threads created from here on inherit the new set)
+        placed_b = placement.pin_to_gpu(local) if placed.get("pinned") and args.batcher_seconds > 0 else None
         batcher = batcher_load(eng, tb, to32, args.batcher_seconds) if args.batcher_seconds > 0 else None
         if batcher is not None:
+            batcher["host_placement"] = placed_b
             batcher["on_replica"] = replica_batcher_leg(eng, tb, to32, args.batcher_seconds)
 
     # ---------------------------------------------------------------- CPU baseline + parity sample
     cpu = None
     parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile and not args.quick:
+        placed_c = placement.pin_to_gpu(local) if placed.get("pinned") else None
         cpu, parity = cpu_baseline(args, w, eng, tb, to, n)
+        if cpu is not None and placed_c is not None:
+            cpu["host_placement"] = placed_c
     # the rest of the index API on the same engine, off the headline metric
     legs = rank == 0 and world == 1 and not args.profile and not args.quick
     filt = filter_leg(args, w, eng, 20000) if legs else None

@@ -110,6 +110,9 @@ def one_per_core(cpus, k):
     return pick_cores(cpus, k)
 
 
+_first_affinity = None
+
+
 def pin_to_gpu(device: int = 0, quota_cut: bool = True) -> dict:
     """Restrict this process (and the threads it creates later) to the GPU-local CPUs that
     it may use.  Returns what was done, for the bench line.
@@ -125,8 +128,11 @@ def pin_to_gpu(device: int = 0, quota_cut: bool = True) -> dict:
     there too; round 5's final check saw a run pinned to the socket's first 16 cores get 3.4
     CPUs of use out of 16, with its aggregator at a fifth of its rate), beginning at a
     per-GPU offset."""
+    global _first_affinity
     local = gpu_local_cpus(device)
-    before = sorted(os.sched_getaffinity(0))
+    if _first_affinity is None:  # a later call picks again from the set the process started with
+        _first_affinity = sorted(os.sched_getaffinity(0))
+    before = _first_affinity
     if not local:
         return {"pinned": False, "reason": "no local_cpulist for the GPU"}
     use = sorted(set(local) & set(before))
