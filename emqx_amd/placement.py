@@ -111,6 +111,7 @@ def one_per_core(cpus, k):
 
 
 _first_affinity = None
+KEEP_BUSY = 0.10  # a re-pick keeps its cores while at most this busy
 
 
 def pin_to_gpu(device: int = 0, quota_cut: bool = True) -> dict:
@@ -143,6 +144,14 @@ def pin_to_gpu(device: int = 0, quota_cut: bool = True) -> dict:
     if quota_cut and quota and quota < len(use):
         busy = cpu_busy(use)
         use_all = use
+        cur = sorted(os.sched_getaffinity(0))
+        if (_first_affinity != cur and len(cur) == quota and set(cur) <= set(use_all)
+                and busy and sum(busy.get(c, 0.0) for c in cur) / len(cur) <= KEEP_BUSY):
+            # a later call keeps the cores picked before while they stay free: the threads
+            # started earlier (the HIP runtime's among them) stay on them
+            return {"pinned": True, "kept": True, "cpus": len(cur), "of": len(before), "quota_cpus": quota,
+                    "gpu_local_cpus": len(local),
+                    "busy_kept": round(sum(busy.get(c, 0.0) for c in cur) / len(cur), 3)}
         use = pick_cores(use_all, quota, busy, start=device * quota)
         if busy:
             info = {"busy_chosen": round(sum(busy.get(c, 0.0) for c in use) / len(use), 3),
