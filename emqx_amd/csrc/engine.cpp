@@ -454,7 +454,21 @@ static unsigned usable_cpus() {
     }();
     return n;
 }
-static unsigned commit_threads() { return std::max(1u, std::min(16u, usable_cpus())); }
+// Helpers of a commit's parallel phases: the usable CPUs less two, at most 16.  The two are left
+// to the threads that keep matching meanwhile: on a process pinned to quota-many CPUs, as many
+// helpers as CPUs leave a matching thread waiting for a time slice (EMQX_TM_COMMIT_THREADS
+// overrides).
+static unsigned commit_threads() {
+    static const unsigned n = [] {
+        if (const char *e = getenv("EMQX_TM_COMMIT_THREADS")) {
+            const int v = atoi(e);
+            if (v > 0) return (unsigned)v;
+        }
+        const unsigned u = usable_cpus();
+        return std::max(1u, std::min(16u, u > 4 ? u - 2 : u));
+    }();
+    return n;
+}
 
 // A few resident threads that split large host copies (staging a pageable batch into pinned
 // memory): thread start-up per copy would cost more than the copy of one sub-batch.

@@ -1,7 +1,7 @@
 """Matches during a forced full rebuild of config C, repeated, with the job's cgroup throttling
 counted over each commit (bench.py's rebuild leg, alone).  One JSON line per rebuild.
 
-    python tools/rebuild_probe_r5.py 3
+    [PIN=1] [EMQX_TM_COMMIT_THREADS=K] python tools/rebuild_probe_r5.py 3
 
 (profiles/r05_rebuild_probe.jsonl also holds runs with an experimental commit-helper count,
 env_commit_threads 16 vs none = 14; that knob was not kept.)"""
@@ -20,6 +20,9 @@ from emqx_amd import workloads  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    if os.environ.get("PIN"):  # as bench.py: the GPU's socket cut to the cgroup quota
+        from emqx_amd import placement
+        print(json.dumps({"placement": placement.pin_to_gpu(0)}), flush=True)
     n = 1_000_000
     w = workloads.generate("C", n_topics=n)
     eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=w.n_keys * 4)
