@@ -543,6 +543,121 @@ def launch_check():
         dist.destroy_process_group()
 
 
+
+LINE_MAX = 12 * 1024  # the driver parses the one printed line; round 5's 32 KB line was not parsed
+
+
+def _pick(d, *keys):
+    return {k: d[k] for k in keys if d and k in d} if d else None
+
+
+def compact_line(out, detail_path):
+    """The ONE printed JSON line: the headline fields, the roofline and CPU baseline, parity,
+    and a one-level summary of every leg.  Everything else (window traces, per-depth walk
+    counters, per-publisher-count aggregator rows, per-epoch churn timings) goes to
+    `detail_path` beside it."""
+    line = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                                "p50_batch_ms", "p99_batch_ms") if k in out}
+    rf = out.get("roofline") or {}
+    line["roofline"] = _pick(rf, "bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms",
+                             "algorithmic_bytes_per_launch", "frac_per_step")
+    if rf.get("traffic_source"):
+        line["roofline"]["traffic_source"] = rf["traffic_source"][:160]
+    cpu = out.get("cpu_baseline")
+    if cpu:
+        line["cpu_baseline"] = _pick(cpu, "value", "unit", "cores", "kind", "value_1_thread")
+        line["cpu_baseline"]["sample"] = cpu.get("sample", "")[:240]
+        if cpu.get("host"):
+            line["cpu_baseline"]["cpu_model"] = cpu["host"].get("model")
+    else:
+        line["cpu_baseline"] = None
+    line["parity"] = out.get("parity")
+    if out.get("replica_parity") is not None:
+        line["replica_parity"] = out["replica_parity"]
+    line["one_batch_in_flight"] = _pick(out.get("one_batch_in_flight"), "publishes_per_s", "ms_per_step", "p99_batch_ms")
+    e2e = out.get("end_to_end")
+    line["end_to_end"] = _pick(e2e, "api", "publishes_per_s", "ms_per_batch", "p99_batch_ms")
+    if e2e and e2e.get("parity"):
+        line["end_to_end"]["parity_mismatches"] = e2e["parity"].get("mismatches")
+    b = out.get("batcher")
+    if b and b.get("runs"):
+        cpu_v = cpu["value"] if cpu else None
+        rows = {}
+        for r in b["runs"]:
+            key = f"{r['publishers']} {r['transport'].split()[0]} {r['callback'].split(' (')[0]}"
+            rows[key] = {"publishes_per_s": r["publishes_per_s"], "lat_p99_ms": r["lat_p99_ms"],
+                         "x_cpu": round(r["publishes_per_s"] / cpu_v, 1) if cpu_v else None}
+        line["batcher"] = {"api": b.get("api"), "rows": rows}
+        head = [r for r in b["runs"] if r["publishers"] == 65536 and r["transport"] == "runs"
+                and r["callback"].startswith("id list")]
+        if head:
+            line["batcher"]["headline_65536_id_list"] = rows[next(k for k in rows if k.startswith("65536 runs id list"))]
+        rep = b.get("on_replica")
+        if rep and rep.get("runs"):
+            line["batcher"]["on_replica"] = {f"{r['publishers']}": r["publishes_per_s"] for r in rep["runs"]}
+    line["other_modes_ms"] = {k: v["ms_per_batch"] for k, v in (out.get("other_modes") or {}).items()}
+    rb = out.get("rebuild_under_load")
+    if rb:
+        line["rebuild_under_load"] = _pick(rb, "ops", "full_rebuild", "commit_s", "commit_phase_s", "max_at_ms")
+        line["rebuild_under_load"]["match_ms_during_commit"] = rb.get("match_ms_during_commit")
+        line["rebuild_under_load"]["match_ms_before"] = rb.get("match_ms_before")
+    ch = out.get("churn_E")
+    if ch:
+        line["churn_E"] = _pick(ch, "epochs", "ops_per_epoch", "route_ops_per_s", "commit_ms_p50", "commit_ms_p99",
+                                "commit_stall_ms_p50", "match_ms_p50", "publishes_per_s_incl_commit", "full_rebuilds")
+        if ch.get("parity"):
+            line["churn_E"]["parity_mismatches"] = ch["parity"].get("mismatches")
+    cb = out.get("config_B")
+    if cb:
+        line["config_B"] = _pick(cb, "publishes_per_s", "ms_per_batch", "p99_batch_ms", "kernel_ms")
+        if cb.get("roofline"):
+            line["config_B"]["roofline_frac"] = cb["roofline"].get("frac")
+    mf = out.get("matches_filter")
+    if mf:
+        line["matches_filter"] = _pick(mf, "queries", "queries_per_s", "ms_per_batch")
+        if mf.get("cpu_baseline"):
+            line["matches_filter"]["cpu_queries_per_s"] = mf["cpu_baseline"].get("value")
+        if mf.get("parity"):
+            line["matches_filter"]["parity_mismatches"] = mf["parity"].get("mismatches")
+    it = out.get("intersection")
+    if it:
+        line["intersection"] = _pick(it, "pairs", "pairs_per_s", "ms_per_batch")
+        if it.get("cpu_baseline"):
+            line["intersection"]["cpu_pairs_per_s"] = it["cpu_baseline"].get("value")
+        if it.get("parity"):
+            line["intersection"]["parity_mismatches"] = it["parity"].get("mismatches")
+    for k in ("spill_topics", "build_s", "batches_in_flight", "host_peak_rss_gib_max_over_ranks"):
+        if k in out:
+            line[k] = out[k]
+    if out.get("library"):
+        line["library"] = _pick(out["library"], "path", "src_sha")
+    if out.get("replication"):
+        line["replication"] = out["replication"]
+    line["detail"] = detail_path
+    s = json.dumps(line)
+    if len(s) > LINE_MAX:  # never print a line the driver cannot take: drop the widest legs first
+        for k in ("batcher", "rebuild_under_load", "churn_E", "matches_filter", "intersection", "config_B"):
+            line.pop(k, None)
+            s = json.dumps(line)
+            if len(s) <= LINE_MAX:
+                break
+    return s
+
+
+def write_detail(out, name="bench_detail.json"):
+    """The full record (every leg, every trace) beside the printed line; returns its path."""
+    d = os.path.join(ROOT, "gpurun_out")
+    try:
+        os.makedirs(d, exist_ok=True)
+        path = os.path.join(d, name)
+        with open(path, "w") as f:
+            json.dump(out, f)
+        return os.path.relpath(path, ROOT)
+    except OSError as e:
+        return f"not written: {e}"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -983,7 +1098,7 @@ def main():
                              "image_bytes": int(eng.image_size()), "image_s": round(image_s, 2)}
                             if world > 1 else None),
         }
-        print(json.dumps(out), flush=True)
+        print(compact_line(out, write_detail(out)), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

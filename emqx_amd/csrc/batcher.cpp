@@ -197,7 +197,13 @@ struct DBuf {
         cap = 0;
         size_t c = std::max<size_t>(std::max<size_t>(bytes + bytes / 4, hint), 4096);
         hipError_t e = hipMalloc(&p, c);
+        if (e != hipSuccess && c > bytes) {  // the hint did not fit: the window's own demand
+            (void)hipGetLastError();
+            c = std::max<size_t>(bytes, 4096);
+            e = hipMalloc(&p, c);
+        }
         if (e == hipSuccess) cap = c;
+        else p = nullptr;
         return e;
     }
     ~DBuf() {
@@ -228,7 +234,13 @@ struct HBuf {
             return hipSuccess;
         }
         hipError_t e = hipHostMalloc(&p, c, hipHostMallocDefault);
+        if (e != hipSuccess && c > bytes) {  // the hint did not fit: the window's own demand
+            (void)hipGetLastError();
+            c = std::max<size_t>(bytes, 4096);
+            e = hipHostMalloc(&p, c, hipHostMallocDefault);
+        }
         if (e == hipSuccess) cap = c;
+        else p = nullptr;
         return e;
     }
     template <class T>
@@ -331,6 +343,7 @@ struct Slot {
     DBuf d_spans, d_soff, d_scnt, d_kcnt, d_st, d_cur;
     HBuf h_spans, h_soff, h_scnt, h_kcnt;
     uint64_t spans_cap = 0;
+    uint64_t spans_need = 0;  // a re-run's span demand (complete_runs), 0 otherwise
     const void *d_ctl = nullptr;
     uint32_t set = 0;  // the engine buffer set and compute stream of this slot (slot index & 1)
 };
@@ -354,19 +367,32 @@ struct tm_batcher {
     // runs transport: spans per publish of recent windows (sizes the next); written by the
     // completion thread, read by the cutter (found by ThreadSanitizer, round 4)
     std::atomic<double> spans_per_pub{4.0};
-    // per-publish high-water marks: buffer sizes for a max_batch window (DBuf/HBuf::ensure)
+    // per-publish high-water marks: buffer sizes for a max_batch window (DBuf/HBuf::ensure).
+    // Only windows of at least max_batch/8 publishes raise them: a lone high-fan-out publish
+    // in a low-load window (one publish, 10 K route ids) would otherwise size every later
+    // window's buffers at 1.25 x max_batch x 10 K ids.  Each hint is capped at HINT_MAX bytes;
+    // past that a buffer grows to a window's own demand (DBuf/HBuf::ensure).
     std::atomic<double> hw_bytes{64.0}, hw_spans{4.0}, hw_ids{16.0};
-    static void raise_hw(std::atomic<double> &hw, double v) {
+    static constexpr size_t HINT_MAX = size_t(256) << 20;
+    void raise_hw(std::atomic<double> &hw, double v, uint32_t n) {
+        if ((uint64_t)n * 8 < cfg.max_batch) return;
         double c = hw.load(std::memory_order_relaxed);
         while (v > c && !hw.compare_exchange_weak(c, v, std::memory_order_relaxed)) {
         }
     }
     bool hints = true;  // EMQX_TM_BATCHER_HINTS=0 (development): grow to each window's demand only
     size_t hint_of(const std::atomic<double> &hw, size_t width) const {
-        return hints ? (size_t)(hw.load(std::memory_order_relaxed) * 1.25 * cfg.max_batch) * width + 64 : 0;
+        if (!hints) return 0;
+        const double b = hw.load(std::memory_order_relaxed) * 1.25 * cfg.max_batch * (double)width + 64;
+        return (size_t)std::min<double>(b, (double)HINT_MAX);
     }
     size_t hint_pub4() const { return hints ? ((size_t)cfg.max_batch + 1) * 4 : 0; }
-    double pool_scale(uint32_t n) const { return hints ? std::max(1.0, (double)cfg.max_batch / std::max<uint32_t>(n, 1)) : 1.0; }
+    // pool growth for a max_batch window at this window's rate, from windows of at least
+    // max_batch/8 publishes only (at most 8x their demand)
+    double pool_scale(uint32_t n) const {
+        if (!hints) return 1.0;
+        return std::min(8.0, std::max(1.0, (double)cfg.max_batch / std::max<uint32_t>(n, 1)));
+    }
     std::atomic<bool> reported{false};  // the first failed window is reported on stderr (once)
     void report(const char *stage, int rc) {
         if (rc >= 0 || reported.exchange(true)) return;
@@ -499,7 +525,7 @@ struct tm_batcher {
         S.t_old = ~0ull;
         for (const Pending &p : S.pubs) S.t_old = std::min(S.t_old, p.t0);
         S.nbytes = at;
-        if (S.n) raise_hw(hw_bytes, (double)at / S.n);
+        if (S.n) raise_hw(hw_bytes, (double)at / S.n, S.n);
         uint32_t *o = S.h_off.as<uint32_t>();
         uint32_t pos = 0;
         for (uint32_t i = 0; i < S.n; i++) {
@@ -540,7 +566,7 @@ struct tm_batcher {
         if (S.mode == TM_MATCH_ALL) {
             // the walk writes the route ids itself (u32 while every id fits), compacted
             // topic-major: no key handles, no separate id pass (tm_match_ids_device)
-            S.ids_cap = std::max<uint64_t>(S.ids_cap, std::max<uint64_t>(hint_of(hw_ids, 1), 1 << 16));
+            S.ids_cap = std::max<uint64_t>(S.ids_cap, std::max<uint64_t>(hint_of(hw_ids, 8) / 8, 1 << 16));
             BT_HIP(S.d_ids.ensure(S.ids_cap * 8 + 8));
             S.narrow = true;
             int rc = tmx_batch_match_ids(eng, S.set, (const uint8_t *)S.d_bytes.p, (const uint32_t *)S.d_off.p, n, S.nbytes, 4,
@@ -598,8 +624,9 @@ struct tm_batcher {
         for (HBuf *h : {&S.h_soff, &S.h_scnt, &S.h_kcnt, &S.h_status}) BT_HIP(h->ensure((size_t)n * 4 + 4, hint_pub4()));
         BT_HIP(S.h_ctl.ensure(64));
         if (!S.ev) BT_HIP(hipEventCreateWithFlags(&S.ev, EV_FLAGS));
-        const uint64_t want =
-            std::max<uint64_t>(4096, (uint64_t)(spans_per_pub.load(std::memory_order_relaxed) * 1.5 * n) + 1024);
+        const uint64_t want = std::max<uint64_t>(
+            std::max<uint64_t>(4096, (uint64_t)(spans_per_pub.load(std::memory_order_relaxed) * 1.5 * n) + 1024),
+            S.spans_need);
         if (S.spans_cap < want) {
             BT_HIP(S.d_spans.ensure(want * 16, hint_of(hw_spans, 16)));
             S.spans_cap = S.d_spans.cap / 16;
@@ -648,22 +675,29 @@ struct tm_batcher {
             int rc = tmx_engine_grow_pools(eng, S.set, (uint64_t)(seg * sc), (uint64_t)(fr * sc));
             if (rc) return rc;
             if (over) {  // more spans than the window's buffer: grow to the demand, run again
-                raise_hw(hw_spans, (double)total / std::max<uint32_t>(S.n, 1));
-                spans_per_pub.store(std::max(spans_per_pub.load(std::memory_order_relaxed),
-                                             (double)total / std::max<uint32_t>(S.n, 1)),
-                                    std::memory_order_relaxed);
+                raise_hw(hw_spans, (double)total / std::max<uint32_t>(S.n, 1), S.n);
+                if ((uint64_t)S.n * 8 >= cfg.max_batch)  // a small window sizes only its own re-run
+                    spans_per_pub.store(std::max(spans_per_pub.load(std::memory_order_relaxed),
+                                                 (double)total / std::max<uint32_t>(S.n, 1)),
+                                        std::memory_order_relaxed);
+                S.spans_need = total + total / 8 + 1024;
                 S.wflags |= TM_WIN_RERUN;
-                if ((rc = enqueue(S))) return rc;
+                rc = enqueue(S);
+                S.spans_need = 0;
+                if (rc) return rc;
                 BT_HIP(hipEventSynchronize(S.ev));
                 S.t_gpu = now_ns();
                 total = S.h_ctl.as<uint64_t>()[0];
                 if (total > S.spans_cap) return TM_EDEVICE;
             }
         }
-        spans_per_pub.store(0.9 * spans_per_pub.load(std::memory_order_relaxed) +
-                                0.1 * ((double)total / std::max<uint32_t>(S.n, 1)),
-                            std::memory_order_relaxed);
-        raise_hw(hw_spans, (double)total / std::max<uint32_t>(S.n, 1));
+        {  // a moving average weighted by the window's size (small windows barely move it)
+            const double a = 0.1 * std::min(1.0, 8.0 * S.n / std::max<uint32_t>(cfg.max_batch, 1));
+            spans_per_pub.store((1 - a) * spans_per_pub.load(std::memory_order_relaxed) +
+                                    a * ((double)total / std::max<uint32_t>(S.n, 1)),
+                                std::memory_order_relaxed);
+        }
+        raise_hw(hw_spans, (double)total / std::max<uint32_t>(S.n, 1), S.n);
         BT_HIP(S.h_spans.ensure(total * 16 + 16, hint_of(hw_spans, 16)));
         S.nchunk = 1;
         S.chunk_lo[0] = 0;
@@ -733,8 +767,8 @@ struct tm_batcher {
             int rc = tmx_engine_grow_pools(eng, S.set, (uint64_t)(seg * sc), (uint64_t)(fr * sc));
             if (rc) return rc;
             if (over) {  // output arena too small: grow to the demand, run this window again
-                raise_hw(hw_ids, (double)total / std::max<uint32_t>(S.n, 1));
-                const uint64_t want = std::max<uint64_t>(total + total / 8 + 1024, hint_of(hw_ids, 1));
+                raise_hw(hw_ids, (double)total / std::max<uint32_t>(S.n, 1), S.n);
+                const uint64_t want = std::max<uint64_t>(total + total / 8 + 1024, hint_of(hw_ids, 8) / 8);
                 // a TM_MATCH_ALL window's walk writes ids: u64 ones take two words of the arena
                 const uint64_t words = S.mode == TM_MATCH_ALL && !S.narrow ? 2 * want : want;
                 if ((rc = tmx_batch_reserve_matches(eng, S.set, words))) return rc;
@@ -766,7 +800,7 @@ struct tm_batcher {
         const uint32_t *oo = S.h_off_out.as<uint32_t>();
         const uint64_t got = oo[S.n];
         const uint64_t w = S.narrow ? 4 : 8;
-        raise_hw(hw_ids, (double)got / std::max<uint32_t>(S.n, 1));
+        raise_hw(hw_ids, (double)got / std::max<uint32_t>(S.n, 1), S.n);
         BT_HIP(S.h_ids.ensure(got * w + 8, hint_of(hw_ids, w)));
         // chunks of >= 2 MiB of ids, at most MAXCH, cut at publish boundaries
         uint32_t nch = (uint32_t)std::min<uint64_t>(Slot::MAXCH, std::max<uint64_t>(1, got * w >> 21));
@@ -1015,8 +1049,10 @@ struct tm_batcher {
     // the last TM_BATCHER_WINDOWS windows' stage stamps (tm_batcher_windows)
     std::unique_ptr<tm_batcher_window[]> wins{new tm_batcher_window[TM_BATCHER_WINDOWS]};
     std::atomic<uint64_t> win_next{0}, win_first{0};  // ring positions; win_first: the reset's
+    std::mutex win_mu;  // a record is written and copied whole (tm_batcher_windows reads no torn entry)
     void trace_window(Slot &S) {
         if (!S.n) return;
+        std::lock_guard<std::mutex> g(win_mu);
         const uint64_t i = win_next.fetch_add(1, std::memory_order_relaxed);
         tm_batcher_window &w = wins[i % TM_BATCHER_WINDOWS];
         w.n = S.n;
@@ -1034,7 +1070,8 @@ struct tm_batcher {
         w.cut_ivcsw = (uint16_t)std::min<uint32_t>(S.cut_ivcsw, 0xFFFF);
         w.wait_ivcsw = (uint16_t)std::min<uint32_t>(S.wait_ivcsw, 0xFFFF);
         w.del_cpu_us = (uint32_t)(S.del_cpu_ns.load(std::memory_order_relaxed) / 1000);
-        w.del_wall_us = (uint32_t)(S.del_wall_ns.load(std::memory_order_relaxed) / 1000);
+        // rounded up: a window delivered in under 1 us still records its (nonzero) wall time
+        w.del_wall_us = (uint32_t)((S.del_wall_ns.load(std::memory_order_relaxed) + 999) / 1000);
         w.del_ivcsw = S.del_ivcsw.load(std::memory_order_relaxed);
         w.reserved = 0;
     }
@@ -1279,8 +1316,13 @@ struct tm_batcher {
             const char *er = std::getenv("EMQX_TM_BATCHER_RESERVE");  // development: 0 skips it
             if (!er || std::atoi(er) != 0)
                 for (uint32_t st = 0; st < nstreams; st++)
-                    if (tmx_engine_reserve_batch(eng, st, cfg.max_batch, (uint64_t)cfg.max_batch * 128) != TM_OK)
-                        return TM_ENOMEM;
+                    if (tmx_engine_reserve_batch(eng, st, cfg.max_batch, (uint64_t)cfg.max_batch * 128) != TM_OK) {
+                        // not fatal: the buffers grow to the windows' demand instead
+                        std::fprintf(stderr, "tm_batcher: reserving buffer set %u failed (%s); growing lazily\n", st,
+                                     tm_last_error(eng));
+                        (void)hipGetLastError();
+                        break;
+                    }
             for (uint32_t i = 0; i < NSLOT_MAX; i++) {
                 slot[i].set = nstreams == 2 ? (i & 1u) : 0u;
                 for (hipEvent_t &e : slot[i].cev)
@@ -1322,16 +1364,24 @@ struct tm_batcher {
             (void)hipSetDevice(device);
             for (Slot &S : slot) {
                 if (S.ev) (void)hipEventDestroy(S.ev);
-                for (hipEvent_t e : S.cev)
-                    if (e) (void)hipEventDestroy(e);
+                S.ev = nullptr;
+                for (hipEvent_t &e : S.cev)
+                    if (e) {
+                        (void)hipEventDestroy(e);
+                        e = nullptr;
+                    }
             }
             // the engine remembers the streams its batches ran on: make it forget ours first
             for (hipStream_t sc : s_comps)
                 if (sc) tmx_engine_forget_stream(eng, sc);
             if (s_copy) tmx_engine_forget_stream(eng, s_copy);
-            for (hipStream_t sc : s_comps)
-                if (sc) (void)hipStreamDestroy(sc);
+            for (hipStream_t &sc : s_comps)
+                if (sc) {
+                    (void)hipStreamDestroy(sc);
+                    sc = nullptr;
+                }
             if (s_copy) (void)hipStreamDestroy(s_copy);
+            s_copy = nullptr;
         }
     }
 };
@@ -1364,6 +1414,7 @@ static int batcher_new(tm_engine *eng, tm_batch_fn fn, void *backend, const tm_b
     b->backend = backend;
     int rc = b->start(cfg);
     if (rc) {
+        b->stop();  // streams and events created before the failure (no thread runs yet)
         delete b;
         return rc;
     }
@@ -1517,6 +1568,7 @@ int tm_batcher_stats_reset(tm_batcher *b) {
 
 int tm_batcher_windows(tm_batcher *b, tm_batcher_window *out, uint32_t cap, uint32_t *n_out) {
     if (!b || !n_out || (cap && !out)) return TM_EINVAL;
+    std::lock_guard<std::mutex> g(b->win_mu);
     const uint64_t hi = b->win_next.load(std::memory_order_acquire);
     uint64_t lo = std::max(b->win_first.load(std::memory_order_relaxed),
                            hi > TM_BATCHER_WINDOWS ? hi - TM_BATCHER_WINDOWS : 0);

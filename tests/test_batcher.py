@@ -554,3 +554,52 @@ def test_gpu_batcher_span_kinds_vs_oracle(wide_ids, idw, monkeypatch):
         else:
             assert st == est[i] or (wide_ids and st == N.TM_ESTATE), i
     eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", [N.TM_TRANSPORT_AUTO, N.TM_TRANSPORT_IDS], ids=["runs", "ids"])
+def test_gpu_lone_high_fanout_publish_does_not_size_later_windows(transport):
+    """with the default max_batch (65,536), one publish matching 16,384
+    filters alone in its window must not set the per-publish sizing marks (they would size the
+    next windows' buffers at 1.25 x 65,536 x 16,384 ids: GBs of HBM and pinned host memory).
+    Device and host memory stay within a bound after it, and later windows stay correct."""
+    import psutil
+    import torch
+    levels = 14
+    topic = "/".join(f"l{k}" for k in range(levels)).encode()
+    filters = ["/".join("+" if (m >> k) & 1 else f"l{k}" for k in range(levels)).encode() for m in range(1 << levels)]
+    eng = N.Engine(0)
+    eng.apply([(N.TM_OP_ADD, f, i) for i, f in enumerate(filters)] + [(N.TM_OP_ADD, b"x/+", 1 << 20)])
+    eng.commit()
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(0)[0]
+    rss0 = psutil.Process().memory_info().rss
+    b = N.Batcher(eng, max_wait_us=200, transport=transport)  # max_batch 0: the default 65,536
+    try:
+        for _ in range(3):  # lone publishes, each its own window
+            st, ids = b.match(topic)
+            assert st >= 0 and sorted(int(i) for i in ids) == list(range(1 << levels))
+        # then a window of ordinary publishes from many threads
+        bad = []
+
+        def worker(k):
+            for j in range(200):
+                st, ids = b.match(b"x/%d" % (k * 1000 + j))
+                if sorted(int(i) for i in ids) != [1 << 20]:
+                    bad.append((k, j))
+
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not bad, bad[:4]
+        st, ids = b.match(topic)
+        assert len(ids) == 1 << levels
+        free1 = torch.cuda.mem_get_info(0)[0]
+        rss1 = psutil.Process().memory_info().rss
+    finally:
+        b.close()
+        eng.close()
+    assert free0 - free1 < (1 << 30), (free0 - free1) / 2**20  # MiB of HBM the aggregator took
+    assert rss1 - rss0 < (1 << 30), (rss1 - rss0) / 2**20

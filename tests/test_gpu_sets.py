@@ -110,6 +110,7 @@ def test_two_direct_sets_on_a_replica():
     # route ids of set 0's batch (result_ids_device reads tm_match_device's set) equal the master's
     ids_t = torch.zeros(int(cnt.sum()) + 1, dtype=torch.int64, device=dev)
     ioff_t = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()  # the zero-fill (torch's stream) lands before the engine's writes (its own stream)
     rep.result_ids_device(ids_t.data_ptr(), ids_t.numel(), ioff_t.data_ptr())
     torch.cuda.synchronize()
     io = ioff_t.cpu().numpy().view(np.uint32)

@@ -175,6 +175,10 @@ def _sets(eng, w, mode=N.TM_MATCH_ALL):
     lo = torch.empty(n + 1, dtype=torch.int32, device=dev)
     ids = torch.zeros(max(total, 1), dtype=torch.int64, device=dev)
     flags = torch.zeros(1, dtype=torch.int32, device=dev)
+    # the fills above ran on torch's stream; the engine writes on its own NON-BLOCKING stream
+    # (stream 0 = the batch's stream, include/emqx_tm.h tm_match_device), which is not ordered
+    # after torch's: the zeros must land before the engine's id writes, not after them
+    torch.cuda.synchronize()
     eng.result_ids_device_ex(ids.data_ptr(), max(total, 1), lo.data_ptr(), flags.data_ptr(), 0)
     torch.cuda.synchronize()
     assert int(flags.item()) == 0
