@@ -602,6 +602,9 @@ def compact_line(out, detail_path):
         line["rebuild_under_load"] = _pick(rb, "ops", "full_rebuild", "commit_s", "commit_phase_s", "max_at_ms")
         line["rebuild_under_load"]["match_ms_during_commit"] = rb.get("match_ms_during_commit")
         line["rebuild_under_load"]["match_ms_before"] = rb.get("match_ms_before")
+        if rb.get("slowest_matches"):
+            line["rebuild_under_load"]["slowest_matches"] = rb["slowest_matches"][:2]
+            line["rebuild_under_load"]["publish_reallocs"] = rb.get("publish_reallocs")
     ch = out.get("churn_E")
     if ch:
         line["churn_E"] = _pick(ch, "epochs", "ops_per_epoch", "route_ops_per_s", "commit_ms_p50", "commit_ms_p99",
@@ -1523,30 +1526,46 @@ def rebuild_leg(eng, w, d_bytes, d_off, n, topic_bytes, dev, frac=0.13):
 
     def matcher():
         while not stop.is_set():
-            t0 = time.perf_counter()
+            t0 = time.monotonic()  # CLOCK_MONOTONIC, as the engine's commit marks
             eng.match_device(d_bytes.data_ptr(), d_off.data_ptr(), m, int(topic_bytes_m), s2.cuda_stream)
             s2.synchronize()
-            lat.append((t0, time.perf_counter() - t0))
+            lat.append((t0, time.monotonic() - t0))
 
+    import gc
+    gc_was = gc.isenabled()
+    gc.disable()  # no collector pauses in the matcher's timings
     topic_bytes_m = int(d_off[m].item())
     th = threading.Thread(target=matcher)
     th.start()
     time.sleep(0.5)
     n_full0 = eng.stats()["n_full_rebuilds"]
     cg0 = cgroup_cpu_stat()
-    t0 = time.perf_counter()
+    t0 = time.monotonic()
     eng.apply_packed(N.TM_OP_DEL, fb, off, ids)
     eng.apply_packed(N.TM_OP_ADD, fb, off, ids)
     eng.commit()
-    t1 = time.perf_counter()
+    t1 = time.monotonic()
     cg1 = cgroup_cpu_stat()
     time.sleep(0.3)
     stop.set()
     th.join()
+    if gc_was:
+        gc.enable()
     st = eng.stats()
+    marks = eng.commit_marks()
+    steps = [(k, v) for k, v in marks.items() if k != "reallocs" and v]
+
+    def phase(t):  # the publish step running at time t (or the host phases before the upload)
+        cur = "apply+lists" if t >= t0 else "before"
+        for k, v in steps:
+            if t >= v:
+                cur = k
+        return cur if t <= t1 else "after"
+
     before = [d for t, d in lat if t < t0]
     during = [d for t, d in lat if t0 <= t < t1]
     worst = max(((d, t) for t, d in lat if t0 <= t < t1), default=None)
+    slow = sorted(((d, t) for t, d in lat if t0 <= t < t1), reverse=True)[:4]
     return {"ops": 2 * k, "full_rebuild": int(st["n_full_rebuilds"]) > int(n_full0),
             "commit_s": round(t1 - t0, 3),
             "commit_phase_s": {"apply": round(st["commit_apply_us"] / 1e6, 3),
@@ -1561,6 +1580,12 @@ def rebuild_leg(eng, w, d_bytes, d_off, n, topic_bytes, dev, frac=0.13):
                                        "p99": round(float(np.percentile(during, 99)) * 1e3, 3) if during else None,
                                        "max": round(float(np.max(during)) * 1e3, 3) if during else None},
             "max_at_ms": round((worst[1] - t0) * 1e3, 1) if worst else None,
+            # the publish's steps (ms from the commit call) and the slowest matches beside them,
+            # each with the step running when it started and when it ended
+            "publish_steps_ms": {k: round((v - t0) * 1e3, 1) for k, v in steps},
+            "publish_reallocs": marks["reallocs"],
+            "slowest_matches": [{"ms": round(d * 1e3, 3), "at_ms": round((t - t0) * 1e3, 1),
+                                 "step_at_start": phase(t), "step_at_end": phase(t + d)} for d, t in slow],
             "cgroup_during_commit": cgroup_delta(cg0, cg1),
             "note": "one epoch re-keys a share of the route keys (deleted and re-added: the same key set, all of them "
                     "deltas) so the commit takes the full-rebuild path; the index is uploaded into a standby device "

@@ -66,7 +66,7 @@ EXPORTS = (
     "tm_discard_staged", "tm_result_release", "tm_match_batch_runs", "tm_runs_release", "tm_build_info",
     "tm_match_ids_device", "tm_merge_shard_ids_device", "tm_debug_depth_stats", "tm_match_device_set",
     "tm_debug_image_check", "tm_match_filter_batch_runs",
-    "tm_device_sync_set", "tm_debug_bounds",
+    "tm_device_sync_set", "tm_debug_bounds", "tm_debug_commit_marks",
 )
 # every symbol include/emqx_tm_batcher.h declares
 BATCHER_EXPORTS = (
@@ -228,6 +228,7 @@ def load() -> C.CDLL:
     lib.tm_debug_depth_stats.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.tm_debug_image_check.argtypes = [C.c_void_p, P(C.c_uint32)]
     lib.tm_debug_bounds.argtypes = [C.c_void_p, P(C.c_uint64), C.c_char_p, C.c_uint32]
+    lib.tm_debug_commit_marks.argtypes = [C.c_void_p, P(C.c_uint64)]
     lib.tm_result_ids_device.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
     lib.tm_result_ids_device_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
     lib.tm_match_ids_device.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
@@ -678,6 +679,17 @@ class Engine:
         """tm_debug_bounds: (hits, first findings) of the bounds-checked debug build over the
         whole process, or None when the loaded library is the product build."""
         return debug_bounds(self)
+
+    COMMIT_MARKS = ("start", "node_image", "edge_table", "staged", "synced", "swap_begin", "swap_end", "standby_kept")
+
+    def commit_marks(self):
+        """tm_debug_commit_marks: the last full publish's step times (time.monotonic() seconds,
+        None for a step that did not run) and the device buffers it (re)allocated."""
+        out = (C.c_uint64 * 9)()
+        self._check(self.lib.tm_debug_commit_marks(self.h, out))
+        marks = {k: (out[i] / 1e6 if out[i] else None) for i, k in enumerate(self.COMMIT_MARKS)}
+        marks["reallocs"] = int(out[8])
+        return marks
 
     def depth_stats(self):
         """Per walk depth (tm_debug_depth_stats): list of dicts {depth, edge_probes, cycles,

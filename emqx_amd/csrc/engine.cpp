@@ -2040,7 +2040,7 @@ struct tm_engine {
         DevBuf nb;
         hipError_t e = nb.ensure(std::max<size_t>(bytes * num / den, 4096));
         if (e) return e;
-        if (bytes && (e = hipMemcpyAsync(nb.p, h.data(), bytes, hipMemcpyHostToDevice, stream))) {
+        if (bytes && (e = upload(nb.p, h.data(), bytes, stream))) {
             nb.release();
             return e;
         }
@@ -2100,18 +2100,74 @@ struct tm_engine {
     // while matches keep running on the current image (mu_dev is not held); then, under
     // mu_dev, the in-flight matches drain and the buffers swap.  At config C that is ~20 GiB
     // uploaded beside the match path; the match path stalls only for the swap.
+    // Full-publish uploads go through this pinned ring, never straight from pageable host
+    // memory: the HIP runtime pins a large pageable source on the fly (a driver mapping of the
+    // host range), and unmapping that range again (the runtime's unpin, or the free of the host
+    // vector at the end of the commit) makes the driver invalidate the process's GPU mappings
+    // beside the matches.  Two chunks, each filled by the commit's helper threads while the
+    // other one's DMA runs.
+    static constexpr size_t UP_CHUNK = size_t(32) << 20;
+    PinBuf up_pin[2];
+    hipEvent_t up_ev[2] = {};
+    uint32_t up_next = 0;
+    hipError_t upload(void *dst, const void *src, size_t bytes, hipStream_t s) {
+        for (size_t at = 0; at < bytes; at += UP_CHUNK) {
+            const size_t n = std::min(UP_CHUNK, bytes - at);
+            const uint32_t k = up_next++ & 1u;
+            hipError_t e;
+            if (!up_ev[k]) {
+                if ((e = hipEventCreateWithFlags(&up_ev[k], hipEventDisableTiming))) return e;
+            } else if ((e = hipEventSynchronize(up_ev[k]))) {  // the chunk's previous DMA is done
+                return e;
+            }
+            if ((e = up_pin[k].ensure(UP_CHUNK))) return e;
+            uint8_t *pin = up_pin[k].as<uint8_t>();
+            const uint8_t *from = static_cast<const uint8_t *>(src) + at;
+            const unsigned nt = n < (size_t(4) << 20) ? 1u : std::min(8u, commit_threads());
+            pool.run(nt, [&](unsigned j) {
+                const size_t a = n * j / nt, b = n * (j + 1) / nt;
+                std::memcpy(pin + a, from + a, b - a);
+            });
+            if ((e = hipMemcpyAsync(static_cast<uint8_t *>(dst) + at, pin, n, hipMemcpyHostToDevice, s))) return e;
+            if ((e = hipEventRecord(up_ev[k], s))) return e;
+        }
+        return hipSuccess;
+    }
+    void upload_release() {
+        for (uint32_t k = 0; k < 2; k++) {
+            if (up_ev[k]) {
+                (void)hipEventSynchronize(up_ev[k]);
+                (void)hipEventDestroy(up_ev[k]);
+                up_ev[k] = nullptr;
+            }
+            up_pin[k].release();
+        }
+    }
+    // Full publish into a STANDBY image: every array is uploaded into fresh buffers on s_build
+    // while matches keep running on the current image (mu_dev is not held); then, under
+    // mu_dev, the in-flight matches drain and the buffers swap.  At config C that is ~20 GiB
+    // uploaded beside the match path; the match path stalls only for the swap.
+    uint32_t pub_reallocs = 0;  // device buffers (re)allocated by the last full publish
     template <class V, class T = typename V::value_type>
-    static hipError_t stage_to(DevBuf &d, const V &h, hipStream_t s, uint64_t *used, size_t num = 3,
-                               size_t den = 2) {
+    hipError_t stage_to(DevBuf &d, const V &h, hipStream_t s, uint64_t *used, size_t num = 3, size_t den = 2) {
         const size_t bytes = h.size() * sizeof(T);
         // a standby buffer that holds the array is reused as it is (no allocation beside the
         // matches); a new one gets headroom for the delta commits that follow
-        hipError_t e = (d.p && bytes <= d.cap) ? hipSuccess : d.ensure(std::max<size_t>(bytes * num / den, 4096));
+        hipError_t e = hipSuccess;
+        if (!(d.p && bytes <= d.cap)) {
+            e = d.ensure(std::max<size_t>(bytes * num / den, 4096));
+            pub_reallocs++;
+        }
         if (e) return e;
-        if (bytes && (e = hipMemcpyAsync(d.p, h.data(), bytes, hipMemcpyHostToDevice, s))) return e;
+        if (bytes && (e = upload(d.p, h.data(), bytes, s))) return e;
         *used = bytes;
         return hipSuccess;
     }
+    // steady-clock microseconds of the last full publish's steps (tm_debug_commit_marks):
+    // start, node image uploaded, edge table built, arrays staged, upload synced, swap begin,
+    // swap end, standby kept
+    uint64_t pub_marks[8] = {};
+    DevBuf d_nim;  // the node image the edge table is built from (kept between full publishes)
     uint64_t last_swap_us = 0;  // mu_dev held by the last full publish's swap (tm_stats)
     // The standby image (round 5).  A full publish used to allocate ~20 GiB of fresh buffers
     // (config C) beside the matches and hipFree the previous image after the swap; both stall
@@ -2140,6 +2196,7 @@ struct tm_engine {
     }
     void standby_release() {
         for (DevBuf &d : standby) d.release();
+        d_nim.release();
     }
     // after a swap: the previous image (sb) becomes the standby, grown to the live image's
     // capacities when the device has room (else dropped: the next full publish allocates)
@@ -2177,6 +2234,9 @@ struct tm_engine {
         patch.reset();
         patch.full = true;  // replicas reload from an image
         DevBuf sb[A_N];
+        for (uint64_t &m : pub_marks) m = 0;
+        pub_marks[0] = now_us();
+        pub_reallocs = 0;
         for (uint32_t a = 0; a < A_N; a++) {  // upload into the standby image's buffers
             std::swap(sb[a].p, standby[a].p);
             std::swap(sb[a].cap, standby[a].cap);
@@ -2200,18 +2260,21 @@ struct tm_engine {
             const EdgeSlot r = edge_rec(v);
             nim[i] = NodeImage{node_slot[v], r.parent, r.word, r.bloom, r.info, node_slist[v]};
         });
-        DevBuf d_nim;
         const uint64_t slots = edge_slots();
+        const size_t nim_bytes = std::max<size_t>(nim.size() * sizeof(NodeImage), 4096);
+        const bool grow_nim = d_nim.cap < nim_bytes, grow_etab = sb[A_ETAB].cap < slots * sizeof(EdgeSlot) || !sb[A_ETAB].p,
+                   grow_sl = sb[A_SLOT_LIST].cap < slots * 4 || !sb[A_SLOT_LIST].p;
+        pub_reallocs += grow_nim + grow_etab + grow_sl;
         if ((e = sb[A_ETAB].ensure(slots * sizeof(EdgeSlot))) || (e = sb[A_SLOT_LIST].ensure(slots * 4)) ||
-            (e = d_nim.ensure(std::max<size_t>(nim.size() * sizeof(NodeImage), 4096))) ||
-            (nim.size() && (e = hipMemcpyAsync(d_nim.p, nim.data(), nim.size() * sizeof(NodeImage), hipMemcpyHostToDevice, s))) ||
-            (e = launch_edge_image(sb[A_ETAB].as<uint4>(), sb[A_SLOT_LIST].as<uint32_t>(), slots, d_nim.as<NodeImage>(), nim.size(), s,
-                                   std::min(sb[A_ETAB].cap / 16, sb[A_SLOT_LIST].cap / 4), bnd_rec())) ||
-            (e = bnd_after(s, "edge image")) || (e = hipStreamSynchronize(s))) {
-            d_nim.release();
+            (e = d_nim.ensure(grow_nim ? nim_bytes + nim_bytes / 4 : nim_bytes)) ||
+            (nim.size() && (e = upload(d_nim.p, nim.data(), nim.size() * sizeof(NodeImage), s))))
             return fail(e);
-        }
-        d_nim.release();
+        pub_marks[1] = now_us();
+        if ((e = launch_edge_image(sb[A_ETAB].as<uint4>(), sb[A_SLOT_LIST].as<uint32_t>(), slots, d_nim.as<NodeImage>(), nim.size(), s,
+                                   std::min(sb[A_ETAB].cap / 16, sb[A_SLOT_LIST].cap / 4), bnd_rec())) ||
+            (e = bnd_after(s, "edge image")) || (e = hipStreamSynchronize(s)))
+            return fail(e);
+        pub_marks[2] = now_us();
         hvec<NodeImage>().swap(nim);
         used[A_ETAB] = slots * sizeof(EdgeSlot);
         used[A_SLOT_LIST] = slots * 4;
@@ -2224,10 +2287,13 @@ struct tm_engine {
             (e = hipMemcpyAsync(sb[A_ROOT].p, &root, sizeof(RootRec), hipMemcpyHostToDevice, s)))
             return fail(e);
         used[A_ROOT] = sizeof(RootRec);
+        pub_marks[3] = now_us();
         if ((e = hipStreamSynchronize(s))) return fail(e);
+        pub_marks[4] = now_us();
         {
             std::lock_guard<std::recursive_mutex> g(mu_dev);
             const uint64_t t0 = now_us();
+            pub_marks[5] = t0;
             if ((e = quiesce())) return fail(e);  // matches in flight finish on the old image
             for (uint32_t a = 0; a < A_N; a++) {
                 DevBuf *d = arr_buf(a);
@@ -2240,9 +2306,11 @@ struct tm_engine {
             arena_dev = arena.size();
             dirty_kid.clear();
             set_view();
-            last_swap_us = now_us() - t0;
+            pub_marks[6] = now_us();
+            last_swap_us = pub_marks[6] - t0;
         }
         standby_keep(sb);  // the previous image (nothing in flight reads it) is the next standby
+        pub_marks[7] = now_us();
         return hipSuccess;
     }
 
@@ -3232,6 +3300,7 @@ void tm_destroy(tm_engine *eng) {
                       &eng->d_arena, &eng->d_scatter_idx, &eng->d_scatter_src, &eng->d_stats, &eng->d_sblob})
         b->release();
     eng->standby_release();
+    eng->upload_release();
     eng->h_cursor.release();
     eng->h_sblob.release();
     if (eng->ev_fast0) (void)hipEventDestroy(eng->ev_fast0);
@@ -4832,6 +4901,14 @@ int tm_debug_timing(tm_engine *eng, int enable, float *ms_out) {
         TM_TRY_HIP(hipEventElapsedTime(ms_out, eng->ev_fast0, eng->ev_fast1), TM_EDEVICE, "elapsed");
     }
     eng->timing_on = enable != 0;
+    return TM_OK;
+}
+
+int tm_debug_commit_marks(const tm_engine *eng, uint64_t *out9) {
+    if (!eng || !out9) return TM_EINVAL;
+    std::lock_guard<std::mutex> g(const_cast<tm_engine *>(eng)->mu_commit);
+    for (int k = 0; k < 8; k++) out9[k] = eng->pub_marks[k];
+    out9[8] = eng->pub_reallocs;
     return TM_OK;
 }
 

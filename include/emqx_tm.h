@@ -482,6 +482,11 @@ int tm_debug_image_check(tm_engine *eng, uint32_t *diff_mask);
  * canary tails plus host copies past a buffer's end; msg (cap bytes) the first findings.  The
  * product build returns TM_ENOTFOUND (it checks nothing). */
 int tm_debug_bounds(tm_engine *eng, uint64_t *hits, char *msg, uint32_t cap);
+/* diagnostics (ABI 10): steady-clock (CLOCK_MONOTONIC) microseconds of the last full publish's
+ * steps, for attributing a match stall to one of them: out9[0..7] = start, node image
+ * uploaded, edge table built, arrays staged, upload synced, swap begin, swap end, standby
+ * kept (0: that step did not run); out9[8] = device buffers the publish (re)allocated. */
+int tm_debug_commit_marks(const tm_engine *eng, uint64_t *out9);
 
 #ifdef __cplusplus
 }
