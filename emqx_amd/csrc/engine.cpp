@@ -259,7 +259,6 @@ struct BatchBufs {
 constexpr uint64_t EDGE_LOAD_INV = 16;
 // Largest edge table: node ids are u32 slot indices and must stay below the sentinels
 // (NONE, W_PLUS, ROOT_ID); 2^31 slots = 32 GiB of HBM.
-constexpr uint64_t MAX_EDGE_SLOTS = 1ull << 31;
 // Word table load <= 1/WORD_LOAD_INV (small: it sizes with the vocabulary, not the nodes).
 constexpr uint64_t WORD_LOAD_INV = 4;
 
@@ -279,7 +278,10 @@ struct PatchRec {
     uint64_t a;      // P_TAIL: first element written; P_WHOLE: capacity (bytes) to allocate
     uint64_t bytes;  // payload bytes following this record (8-byte padded)
 };
-constexpr uint64_t PATCH_MAGIC = 0x3148435441504d54ull, IMAGE_MAGIC = 0x31474d494d545845ull;
+// "TMPATCH2" / "EXTMIMG2": the trailing digit is the layout version (2: LIST_HDR 6, the HDR_DD
+// collapse word of round 5), so a replica of another build refuses the image or patch instead
+// of reading every list header one word off
+constexpr uint64_t PATCH_MAGIC = 0x3248435441504d54ull, IMAGE_MAGIC = 0x32474d494d545845ull;
 constexpr size_t STATS_BYTES = 96 * 8;  // walk counters (device_api.h MatchArgs.stats)
 
 struct PatchHdr {
@@ -1322,7 +1324,7 @@ struct tm_engine {
     // where the device's linear probe for (parent slot, word) ends: the first free slot
     uint64_t edge_place(uint32_t parent_dev, uint32_t word) const {
         uint64_t s = edge_home(parent_dev, word, emask);
-        while (slot_taken(s)) s = (s + 1) & emask;
+        while (slot_taken(s)) s = next_slot(s, emask);
         return s;
     }
     // Re-place every node: slot positions hash the parent's slot, so nodes go in in
@@ -1361,7 +1363,7 @@ struct tm_engine {
         if ((n_edges + 1) * edge_load_inv() > edge_slots()) {
             // a node is its slot index (u32, below the NONE/ROOT_ID sentinels): at the
             // size cap the table fills up to half instead of growing
-            if (edge_slots() < MAX_EDGE_SLOTS) edge_rehash(edge_slots() * 2);
+            if (edge_slots() < MAX_EDGE_SLOTS) edge_rehash(std::min<uint64_t>(edge_slots() * 2, MAX_EDGE_SLOTS));
             else if ((n_edges + 1) * 2 > edge_slots()) {
                 edge_full = true;
                 return ROOT;  // dropped; commit() reports TM_ENOMEM
@@ -2088,6 +2090,7 @@ struct tm_engine {
         std::vector<uint32_t> node, bin;
         std::vector<uint8_t> dd;
     };
+    KeyArrays h_ka;  // kept between full publishes, as h_nim
     void key_arrays(KeyArrays &k) const {
         k.rec.resize(keys.size() * 2);
         k.node.resize(keys.size());
@@ -2168,6 +2171,11 @@ struct tm_engine {
     // swap end, standby kept
     uint64_t pub_marks[8] = {};
     DevBuf d_nim;  // the node image the edge table is built from (kept between full publishes)
+    // The host arrays a full publish fills, kept between publishes (≈ 1.8 GB at config C): a
+    // fresh 1.5 GB node image per rebuild was first-touched by 14 helper threads, and those page
+    // faults held the process's address-space lock against everything else mapping memory
+    // beside them (a 10 ms match in the rebuild probe, profiles/r06_rebuild_probe_rb1.jsonl)
+    hvec<NodeImage> h_nim;
     uint64_t last_swap_us = 0;  // mu_dev held by the last full publish's swap (tm_stats)
     // The standby image (round 5).  A full publish used to allocate ~20 GiB of fresh buffers
     // (config C) beside the matches and hipFree the previous image after the swap; both stall
@@ -2242,7 +2250,7 @@ struct tm_engine {
             std::swap(sb[a].cap, standby[a].cap);
         }
         uint64_t used[A_N] = {};
-        KeyArrays ka;
+        KeyArrays &ka = h_ka;
         key_arrays(ka);
         hipStream_t s = s_build;
         hipError_t e;
@@ -2254,7 +2262,8 @@ struct tm_engine {
         // the edge table and slot lists: reused when the standby holds them (ensure keeps a
         // buffer at least as large)
         // the edge table: built on the device from one record per node
-        hvec<NodeImage> nim(node_parent.size() - 1);
+        hvec<NodeImage> &nim = h_nim;
+        nim.resize(node_parent.size() - 1);
         par_for(nim.size(), [&](size_t i) {
             const uint32_t v = (uint32_t)i + 1;
             const EdgeSlot r = edge_rec(v);
@@ -2275,7 +2284,6 @@ struct tm_engine {
             (e = bnd_after(s, "edge image")) || (e = hipStreamSynchronize(s)))
             return fail(e);
         pub_marks[2] = now_us();
-        hvec<NodeImage>().swap(nim);
         used[A_ETAB] = slots * sizeof(EdgeSlot);
         used[A_SLOT_LIST] = slots * 4;
         if ((e = stage_to(sb[A_WTAB], wtab, s, &used[A_WTAB], 1, 1)) || (e = stage_to(sb[A_WARENA], warena, s, &used[A_WARENA])) ||
@@ -2789,6 +2797,15 @@ struct tm_engine {
         const bool was_full = need_full;
         epoch++;
         hipError_t e = publish(need_full);
+        if (e == hipErrorOutOfMemory && standby_bytes() && !(cfg.flags & TM_CFG_FAIL_FLUSH_ONCE)) {
+            // the standby image (a second copy of the index, unused until the next full
+            // publish) gives its HBM back, and the publish runs once more
+            (void)hipGetLastError();
+            drop_scatters();
+            standby_release();
+            patch.reset();  // the failed attempt's records go; the retry records the epoch again
+            e = publish(need_full);
+        }
         if (e != hipSuccess) {
             // the device still holds the previous epoch, intact (allocations come before any
             // in-place write); the host copy has advanced: the next commit re-uploads it whole
@@ -3226,9 +3243,13 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
         delete eng;
         return TM_EDEVICE;  // kernels are built for gfx950 only
     }
+    // a full publish's standby build runs at the device's lowest stream priority: the matches
+    // beside it (on the engine's and the callers' streams) are dispatched first
+    int prio_least = 0, prio_greatest = 0;
     if (hipSetDevice(eng->cfg.device) != hipSuccess ||
         hipStreamCreateWithFlags(&eng->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&eng->s_build, hipStreamNonBlocking) != hipSuccess) {
+        hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&eng->s_build, hipStreamNonBlocking, prio_least) != hipSuccess) {
         tm_destroy(eng);
         return TM_EDEVICE;
     }

@@ -122,18 +122,26 @@ TM_HD uint64_t word_slot_hash(uint64_t key, uint32_t len) { return mix64(key ^ (
 TM_HD uint64_t edge_hash(uint32_t parent, uint32_t word) {
     return mix64(((uint64_t)parent << 32) | word);
 }
-// Home slot of edge (parent, word), where its linear probe starts.  TM_PLUS_NEAR=1 starts a
-// '+' edge right after its parent's own slot, so the '+' probe that follows the walk's read
-// of that slot usually hits the same L2 line: it cuts the walk's L2 misses by 8 % and its
-// HBM fetch by 11 %, yet a same-process A/B (tools/sweep.py plusnear/plushash, profiles/
-// r04_sweep_plus_aa.jsonl) times it 1 % slower -- the walk waits on round trips, not on
-// misses, and the clustering adds probes.  So every edge starts at its hash.
+// Home slot of edge (parent, word), where its linear probe starts.  The table has emask + 1
+// slots, any count up to MAX_EDGE_SLOTS (not only powers of two): the home slot is the top 32
+// bits of the hash scaled to the slot count (one 32 x 32 -> 64 multiply), and a probe that
+// runs off the end wraps to slot 0 (next_slot).  Round 6: a power-of-two table stopped at
+// 2^31 slots (the next one would reach the NONE / ROOT_ID sentinels), which held config D at
+// load 0.26; it now grows to MAX_EDGE_SLOTS.
+// TM_PLUS_NEAR=1 starts a '+' edge right after its parent's own slot, so the '+' probe that
+// follows the walk's read of that slot usually hits the same L2 line: it cuts the walk's L2
+// misses by 8 % and its HBM fetch by 11 %, yet a same-process A/B (tools/sweep.py plusnear/
+// plushash, profiles/r04_sweep_plus_aa.jsonl) times it 1 % slower -- the walk waits on round
+// trips, not on misses, and the clustering adds probes.  So every edge starts at its hash
+// (DESIGN.md §4).
 #ifndef TM_PLUS_NEAR
 #define TM_PLUS_NEAR 0
 #endif
+constexpr uint64_t MAX_EDGE_SLOTS = 0xF0000000ull;  // below the sentinels; a multiple of 64
+TM_HD uint64_t next_slot(uint64_t s, uint64_t emask) { return s == emask ? 0 : s + 1; }
 TM_HD uint64_t edge_home(uint32_t parent, uint32_t word, uint64_t emask) {
-    return (TM_PLUS_NEAR && word == W_PLUS && parent != ROOT_ID) ? ((uint64_t)parent + 1) & emask
-                                                                 : edge_hash(parent, word) & emask;
+    if (TM_PLUS_NEAR && word == W_PLUS && parent != ROOT_ID) return next_slot(parent, emask);
+    return ((uint64_t)(uint32_t)(edge_hash(parent, word) >> 32) * (uint32_t)(emask + 1)) >> 32;
 }
 
 }  // namespace tmx

@@ -219,7 +219,7 @@ __device__ __forceinline__ bool edge_probe(const MatchArgs &a, uint32_t parent, 
             *r = Rec{(uint32_t)s, x.z, x.w};
             return true;
         }
-        s = (s + 1) & a.emask;
+        s = next_slot(s, a.emask);
     }
 }
 
@@ -856,7 +856,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                                 r1[k] = Rec{(uint32_t)s1[k], x1[k].z, x1[k].w};
                                 f1[k] = true;
                                 p1[k] = false;
-                            } else s1[k] = (s1[k] + 1) & a.emask;
+                            } else s1[k] = next_slot(s1[k], a.emask);
                         }
                         if (p2[k]) {
                             if (x2[k].x == NONE) p2[k] = false;
@@ -864,7 +864,7 @@ __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) 
                                 r2[k] = Rec{(uint32_t)s2[k], x2[k].z, x2[k].w};
                                 f2[k] = true;
                                 p2[k] = false;
-                            } else s2[k] = (s2[k] + 1) & a.emask;
+                            } else s2[k] = next_slot(s2[k], a.emask);
                         }
                     }
                 }
@@ -1633,7 +1633,7 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
                                 r1[k] = Rec{(uint32_t)s1[k], x1[k].z, x1[k].w};
                                 f1[k] = true;
                                 p1[k] = false;
-                            } else s1[k] = (s1[k] + 1) & a.emask;
+                            } else s1[k] = next_slot(s1[k], a.emask);
                         }
                         if (p2[k]) {
                             if (x2[k].x == NONE) p2[k] = false;
@@ -1641,7 +1641,7 @@ __global__ __launch_bounds__(WAVE) void k_match_first_wave(MatchArgs a) {
                                 r2[k] = Rec{(uint32_t)s2[k], x2[k].z, x2[k].w};
                                 f2[k] = true;
                                 p2[k] = false;
-                            } else s2[k] = (s2[k] + 1) & a.emask;
+                            } else s2[k] = next_slot(s2[k], a.emask);
                         }
                     }
                 }

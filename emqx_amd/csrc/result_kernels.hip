@@ -774,24 +774,32 @@ __global__ void k_edge_clear(uint4 *etab, uint32_t *slot_list, uint64_t cap, uin
 
 __global__ void k_edge_place(uint4 *etab, uint32_t *slot_list, const NodeImage *nodes, uint64_t n, uint64_t cap,
                              uint64_t buf_slots, unsigned long long *bnd) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const NodeImage r = nodes[i];
-    // a record past the table the publish sized (cap) would be a host bug: the bounds build
-    // reports it against the table's size, not the buffer's
-    const uint64_t j = BIR(BIR(r.slot, cap, bnd), buf_slots, bnd);
-    etab[j] = make_uint4(r.parent, r.word, r.bloom, r.info);
-    slot_list[j] = r.list;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const NodeImage r = nodes[i];
+        // a record past the table the publish sized (cap) would be a host bug: the bounds build
+        // reports it against the table's size, not the buffer's
+        const uint64_t j = BIR(BIR(r.slot, cap, bnd), buf_slots, bnd);
+        etab[j] = make_uint4(r.parent, r.word, r.bloom, r.info);
+        slot_list[j] = r.list;
+    }
 }
+
+// Both kernels run beside the matches of the image being replaced (a full publish into the
+// standby): at most EDGE_IMAGE_BLOCKS workgroups each (grid-stride), so they hold two of a CU's
+// wave slots instead of all of them; the matches' waves keep the rest (a match of 131,072
+// publishes beside an uncapped build took 1-2.6 ms instead of 0.135).
+constexpr uint64_t EDGE_IMAGE_BLOCKS = 512;
 
 hipError_t launch_edge_image(uint4 *etab, uint32_t *slot_list, uint64_t cap, const NodeImage *nodes, uint64_t n,
                              hipStream_t s, uint64_t buf_slots, unsigned long long *bnd) {
     if (!cap) return hipSuccess;
     const uint64_t want = (cap + 255) / 256;
-    k_edge_clear<<<(unsigned)std::min<uint64_t>(want, 16384), 256, 0, s>>>(etab, slot_list, cap, buf_slots, bnd);
+    k_edge_clear<<<(unsigned)std::min<uint64_t>(want, EDGE_IMAGE_BLOCKS), 256, 0, s>>>(etab, slot_list, cap, buf_slots, bnd);
     hipError_t e = hipGetLastError();
     if (e || !n) return e;
-    k_edge_place<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(etab, slot_list, nodes, n, cap, buf_slots, bnd);
+    k_edge_place<<<(unsigned)std::min<uint64_t>((n + 255) / 256, EDGE_IMAGE_BLOCKS), 256, 0, s>>>(etab, slot_list, nodes, n,
+                                                                                               cap, buf_slots, bnd);
     return hipGetLastError();
 }
 

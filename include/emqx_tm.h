@@ -200,7 +200,8 @@ typedef struct tm_stats_t {
     uint64_t edge_slots;    /* device edge-table capacity (slots)           */
     uint64_t word_slots;    /* device word-table capacity (slots)           */
     uint64_t list_words;    /* u32 words in the terminal-list arena (live+garbage) */
-    uint64_t device_bytes;  /* HBM held by the frozen index                 */
+    uint64_t device_bytes;  /* HBM held by the frozen index (the standby image, standby_bytes,
+                               is not included) */
     uint64_t n_full_rebuilds;
     uint64_t n_delta_commits;
     uint64_t n_slow_topics; /* topics routed to the spill kernel in the last batch */

@@ -21,6 +21,9 @@ for s in $STEPS; do
           || { tail -n 20 gpurun_out/r06_bench_$T.err; exit 4; }
       cp gpurun_out/bench_detail.json gpurun_out/r06_bench_detail_$T.json
       wc -c gpurun_out/r06_bench_$T.json ;;
+    rebuild)
+      PIN=1 timeout -k 10 400 python -u tools/rebuild_probe_r6.py ${REPS:-4} > gpurun_out/r06_rebuild_probe_$T.jsonl \
+          2> gpurun_out/r06_rebuild_probe_$T.err || { tail -n 20 gpurun_out/r06_rebuild_probe_$T.err; exit 6; } ;;
     quick)
       timeout -k 10 300 python -u bench.py --quick --batcher-seconds 0 --steps 40 > gpurun_out/r06_quick_$T.json \
           2> gpurun_out/r06_quick_$T.err || { tail -n 20 gpurun_out/r06_quick_$T.err; exit 5; } ;;
