@@ -52,6 +52,7 @@ TM_CFG_FORCE_SLOW = 1
 TM_CFG_RECORD_PATCH = 2
 TM_CFG_FAIL_HOST_CALLS = 4
 TM_CFG_FAIL_FLUSH_ONCE = 8
+TM_CFG_EDGE_EXACT = 16
 TM_RES_KEYS_OVERFLOW = 1
 TM_RES_IDS_OVERFLOW = 2
 

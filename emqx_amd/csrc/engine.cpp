@@ -3278,7 +3278,11 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
         v->push_back(0);
     }
     eng->emap_rehash(next_pow2(std::max<uint64_t>(rn * 2, 1024)));
-    eng->edge_rehash(std::min<uint64_t>(next_pow2(std::max<uint64_t>(rn * eng->edge_load_inv(), 1024)), MAX_EDGE_SLOTS));
+    {
+        const uint64_t want = std::max<uint64_t>(rn * eng->edge_load_inv(), 1024);
+        eng->edge_rehash(std::min<uint64_t>((eng->cfg.flags & TM_CFG_EDGE_EXACT) ? (want + 63) & ~63ull : next_pow2(want),
+                                            MAX_EDGE_SLOTS));
+    }
     eng->kset_rehash(next_pow2(std::max<uint64_t>(rk * 2, 1024)));
     eng->keys.reserve(rk);
     eng->need_full = true;

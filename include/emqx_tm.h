@@ -133,6 +133,10 @@ extern "C" {
                                      its read lease, to check a failed call leaves no lease held */
 #define TM_CFG_FAIL_FLUSH_ONCE 8u /* test aid (ABI 10): the first delta commit that scatters fails
                                      in its upload, as an out-of-HBM staging buffer would */
+#define TM_CFG_EDGE_EXACT 16u     /* (ABI 10) size the edge table at reserve_nodes x edge_load_inv
+                                     slots rounded up to 64, not to a power of two (the table
+                                     takes any slot count up to 0xF0000000; it still doubles when
+                                     it fills, up to that cap) */
 
 typedef struct tm_engine tm_engine;
 
@@ -150,7 +154,7 @@ typedef struct tm_config {
                                      waits for its longest probe chain, so lower load shortens
                                      the walk at the price of HBM (16 B per slot) */
     uint32_t topics_per_wave;     /* 0 = by batch size (4..64); else 4, 8, 16, 32 or 64 */
-    uint32_t max_nodes;           /* trie-node budget (0 = the edge table's limit, 2^30): a commit
+    uint32_t max_nodes;           /* trie-node budget (0 = the edge table's limit, 0x78000000): a commit
                                      that would pass it fails with TM_ENOMEM, ops kept staged */
     uint32_t max_list_words;      /* terminal-list arena budget in u32 words (0 = 2^32 - 16) */
 } tm_config;

@@ -138,3 +138,76 @@ def test_failed_delta_upload_leaves_no_stale_scatters():
         assert fulls == [True, False]  # the retry re-published whole, then deltas resumed
     finally:
         eng.close()
+
+
+@pytest.mark.timeout(300)
+def test_edge_table_of_any_slot_count():
+    """Round 6: the edge table takes any slot count up to 0xF0000000 (the home slot is the top
+    32 bits of the hash scaled to the count, probes wrap at the end), which lifts config D off
+    the 2^31-slot power-of-two cap.  TM_CFG_EDGE_EXACT sizes a small table at a count that is
+    not a power of two; deltas (in-place slot scatters), a growth past load 1/16 (a doubling
+    to another non-power-of-two count) and a replica built from the image all stay exact."""
+    w = workloads.generate("E", scale=0.05, n_topics=20_000)
+    nodes = w.n_keys * 3 + 1  # 16 x this, rounded up to 64: not a power of two
+    eng = N.Engine(0, reserve_keys=w.n_keys, reserve_nodes=nodes, flags=N.TM_CFG_EDGE_EXACT, record_patch=True)
+    try:
+        slots0 = eng.stats()["edge_slots"]
+        assert slots0 == (nodes * 16 + 63) // 64 * 64 and slots0 & (slots0 - 1), slots0
+        eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+        eng.commit()
+        ix = oracle.OrderedIndex(w.f_bytes, w.f_off, w.f_id)
+        _check_full_batch(eng, w, ix, 4_000, seed=1)
+        assert eng.image_check() == []
+        _churn(eng, w, epochs=2, frac=0.02, seed=3, sample=3_000)
+        # grow the trie past load 1/16: the table doubles (still not a power of two)
+        grow = [(b"g%d/h%d/+/#" % (k % 991, k), 10**9 + k) for k in range(slots0 // 16)]
+        eng.apply([(N.TM_OP_ADD, f, i) for f, i in grow])
+        eng.commit()
+        slots1 = eng.stats()["edge_slots"]
+        k = slots1 // slots0
+        assert k >= 2 and slots1 == slots0 * k and k & (k - 1) == 0 and slots1 & (slots1 - 1), (slots0, slots1)
+        assert eng.image_check() == []
+        # a replica of the grown index answers as the master
+        import torch
+        n = eng.image_size()
+        img = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
+        eng.image_export(img.data_ptr(), n)
+        rep = N.Engine.replica_from_image(0, img.data_ptr(), n)
+        try:
+            assert rep.stats()["edge_slots"] == slots1
+            om, cm, km, sm = eng.match_packed(w.t_bytes, w.t_off)
+            orr, cr, kr, sr = rep.match_packed(w.t_bytes, w.t_off)
+            assert np.array_equal(cm, cr) and np.array_equal(sm, sr)
+            for t in range(0, w.n_topics, 7):  # the same key handles on both
+                assert np.array_equal(np.sort(km[om[t]:om[t] + cm[t]]), np.sort(kr[orr[t]:orr[t] + cr[t]])), t
+        finally:
+            rep.close()
+    finally:
+        eng.close()
+
+
+def test_image_of_another_layout_version_is_refused():
+    """LIST_HDR grew (round 5) without a magic change, so a replica of another build
+    would read every list header one word off.  The image magic carries the layout version now:
+    an image whose magic is the previous version's is refused (TM_EINVAL), not loaded."""
+    import torch
+    w = workloads.generate("A", scale=0.05, n_topics=100)
+    eng = N.Engine(0)
+    try:
+        eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
+        eng.commit()
+        n = eng.image_size()
+        img = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
+        eng.image_export(img.data_ptr(), n)
+        ok = N.Engine.replica_from_image(0, img.data_ptr(), n)
+        ok.close()
+        old = torch.from_numpy(np.array([0x31474d494d545845], dtype=np.uint64).view(np.uint8)).to("cuda:0")
+        img[:8].copy_(old)
+        torch.cuda.synchronize()
+        with pytest.raises(N.TMError) as ei:
+            N.Engine.replica_from_image(0, img.data_ptr(), n)
+        assert ei.value.rc == N.TM_EINVAL
+    finally:
+        eng.close()
