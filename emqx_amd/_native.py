@@ -58,7 +58,7 @@ TM_RES_IDS_OVERFLOW = 2
 
 # every symbol include/emqx_tm.h declares (tests check the .so exports them all)
 EXPORTS = (
-    "tm_abi_version", "tm_create", "tm_destroy", "tm_last_error", "tm_apply", "tm_apply_packed",
+    "tm_abi_version", "tm_create", "tm_destroy", "tm_last_error", "tm_create_last_error", "tm_apply", "tm_apply_packed",
     "tm_commit_epoch", "tm_match_batch", "tm_match_device", "tm_device_sync",
     "tm_reserve_matches", "tm_key_info", "tm_key_ids", "tm_stats", "tm_debug_stats", "tm_debug_timing",
     "tm_result_ids_device", "tm_merge_shards_device", "tm_merge_shards", "tm_match_device_mode",
@@ -197,6 +197,8 @@ def load() -> C.CDLL:
     lib.tm_destroy.restype = None
     lib.tm_last_error.argtypes = [C.c_void_p]
     lib.tm_last_error.restype = C.c_char_p
+    lib.tm_create_last_error.argtypes = []
+    lib.tm_create_last_error.restype = C.c_char_p
     lib.tm_apply.argtypes = [C.c_void_p, P(tm_op), C.c_size_t]
     lib.tm_apply_packed.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_size_t]
@@ -249,7 +251,7 @@ def load() -> C.CDLL:
     lib.tm_merge_shards.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
                                     C.c_void_p, C.c_uint64]
     for name in EXPORTS:
-        if name not in ("tm_destroy", "tm_last_error", "tm_abi_version", "tm_build_info"):
+        if name not in ("tm_destroy", "tm_last_error", "tm_create_last_error", "tm_abi_version", "tm_build_info"):
             getattr(lib, name).restype = C.c_int
     lib.tm_batcher_create.argtypes = [C.c_void_p, P(tm_batcher_config), P(C.c_void_p)]
     lib.tm_batcher_create_fn.argtypes = [tm_batch_fn, C.c_void_p, P(tm_batcher_config), P(C.c_void_p)]
@@ -366,7 +368,8 @@ class Engine:
             rc = self.lib.tm_replica_create(C.byref(cfg), C.c_void_p(_image[0]), _image[1],
                                             C.c_void_p(_image[2]) if _image[2] else None, C.byref(h))
         if rc != TM_OK:
-            raise TMError(rc, "tm_create failed (no gfx950 HIP device visible?)")
+            why = self.lib.tm_create_last_error().decode(errors="replace")
+            raise TMError(rc, f"tm_create failed: {why or 'no gfx950 HIP device visible?'}")
         self.h = h
         self.device = device
         self.replica = _image is not None

@@ -18,6 +18,9 @@
 
 #include <sched.h>
 #include <sys/mman.h>
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -155,6 +158,10 @@ struct DevBuf {
         hipError_t e = hipMalloc(&p, want + BND_CANARY);
         if (e == hipSuccess) {
             cap = want;
+            // EMQX_TM_POISON=1 (test aid): every new device buffer starts as 0xA7 bytes, so a read
+            // of memory nothing wrote shows up as garbage, not as the zeros a fresh page holds
+            static const bool poison = getenv("EMQX_TM_POISON") && atoi(getenv("EMQX_TM_POISON")) != 0;
+            if (poison && (e = hipMemset(p, 0xA7, want)) == hipSuccess) e = hipStreamSynchronize(nullptr);
 #if TM_BOUNDS
             e = hipMemset(static_cast<uint8_t *>(p) + want, BND_FILL, BND_CANARY);
             std::lock_guard<std::mutex> g(bnd_registry().m);
@@ -249,6 +256,13 @@ struct BatchBufs {
                           &d_seg_pool, &d_fr_pool, &d_wave_chunks, &d_ukeys, &d_ucnt, &d_dd_wl, &d_dd_wl_n, &d_kcnt,
                           &d_rcur, &d_ctl, &d_wave_info, &d_pre, &d_res_scan})
             b->release();
+        // the sizes recorded for the released buffers go with them (a later ensure_batch
+        // allocates again instead of trusting a capacity nothing holds)
+        p_ctl = nullptr;
+        ctl_cur = 0;
+        keys_cap = seg_chunks = fr_chunks = ukeys_cap = 0;
+        seg_demand_last = fr_demand_last = 0;
+        last_stream = nullptr;
     }
 };
 
@@ -336,6 +350,11 @@ std::string &tl_err() {
     thread_local std::string s;
     return s;
 }
+// tm_create_last_error(): why the calling thread's last tm_create / tm_replica_create failed
+std::string &tl_create_err() {
+    thread_local std::string s;
+    return s;
+}
 struct ErrSlot {
     ErrSlot &operator=(std::string s) {
         tl_err() = std::move(s);
@@ -361,6 +380,16 @@ struct WorkPool {
     uint64_t gen = 0;
     bool quit = false;
     void loop(unsigned id) {
+        // A commit's helpers run below the threads that keep matching beside the commit: on a
+        // process pinned to as many CPUs as it has threads, a matching thread woken by its GPU
+        // event then preempts a helper at once instead of waiting out a helper's time slice
+        // (10 ms matches during a full rebuild's apply/lists phases, profiles/r06_bench_b.json).
+        // Raising one's own nice value needs no privilege.  EMQX_TM_HELPER_NICE overrides (0: off).
+        static const int nice_v = [] {
+            const char *e = getenv("EMQX_TM_HELPER_NICE");
+            return e ? atoi(e) : 10;
+        }();
+        if (nice_v > 0) (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), nice_v);
         uint64_t seen = 0;
         for (;;) {
             const std::function<void(unsigned)> *j;
@@ -924,6 +953,36 @@ struct tm_engine {
         pool.run(nt, [&](unsigned k) {
             for (size_t i = n * k / nt, e = n * (k + 1) / nt; i < e; i++) f(i);
         });
+    }
+    // The edge image of a full publish (clear every slot, then place every node) in slices of
+    // about 0.1-0.2 ms each, every slice waited for and followed by a pause, so a match running
+    // beside the rebuild shares the memory system with at most one slice.  Launched whole, the
+    // two kernels (3 + 5 ms at config C: 20 GiB of writes, 64 M random record scatters) stretched
+    // a 0.13 ms match to 3-5 ms (profiles/r06_rebuild_probe_nice.jsonl).  EMQX_TM_EDGE_PACE_US:
+    // the pause (default 150; 0 launches each kernel whole, unpaced).
+    hipError_t edge_image_paced(uint4 *etab, uint32_t *sl, uint64_t slots, const NodeImage *nodes, uint64_t n,
+                                hipStream_t s, uint64_t buf_slots) {
+        static const long pace_us = [] {
+            const char *e = getenv("EMQX_TM_EDGE_PACE_US");
+            return e ? atol(e) : 150L;
+        }();
+        constexpr uint64_t CLEAR_SLICE = 32ull << 20, PLACE_SLICE = 2ull << 20;  // slots / records
+        if (pace_us <= 0) return launch_edge_image(etab, sl, slots, nodes, n, s, buf_slots, bnd_rec());
+        hipError_t e = hipSuccess;
+        auto pause = [&]() -> hipError_t {
+            hipError_t r = hipStreamSynchronize(s);
+            if (r == hipSuccess) std::this_thread::sleep_for(std::chrono::microseconds(pace_us));
+            return r;
+        };
+        for (uint64_t lo = 0; lo < slots && !e; lo += CLEAR_SLICE) {
+            e = launch_edge_clear_range(etab, sl, lo, std::min(slots, lo + CLEAR_SLICE), s, buf_slots, bnd_rec());
+            if (!e && (lo + CLEAR_SLICE < slots || n)) e = pause();
+        }
+        for (uint64_t lo = 0; lo < n && !e; lo += PLACE_SLICE) {
+            e = launch_edge_place_range(etab, sl, slots, nodes + lo, std::min(n - lo, PLACE_SLICE), s, buf_slots, bnd_rec());
+            if (!e && lo + PLACE_SLICE < n) e = pause();
+        }
+        return e;
     }
     std::once_flag copier_once;
     hipEvent_t ev_chain = nullptr;  // orders a device match after the previous one's stream
@@ -2279,8 +2338,8 @@ struct tm_engine {
             (nim.size() && (e = upload(d_nim.p, nim.data(), nim.size() * sizeof(NodeImage), s))))
             return fail(e);
         pub_marks[1] = now_us();
-        if ((e = launch_edge_image(sb[A_ETAB].as<uint4>(), sb[A_SLOT_LIST].as<uint32_t>(), slots, d_nim.as<NodeImage>(), nim.size(), s,
-                                   std::min(sb[A_ETAB].cap / 16, sb[A_SLOT_LIST].cap / 4), bnd_rec())) ||
+        if ((e = edge_image_paced(sb[A_ETAB].as<uint4>(), sb[A_SLOT_LIST].as<uint32_t>(), slots, d_nim.as<NodeImage>(),
+                                  nim.size(), s, std::min(sb[A_ETAB].cap / 16, sb[A_SLOT_LIST].cap / 4))) ||
             (e = bnd_after(s, "edge image")) || (e = hipStreamSynchronize(s)))
             return fail(e);
         pub_marks[2] = now_us();
@@ -3233,13 +3292,16 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
     eng->master_nonce = mix64((uint64_t)std::chrono::steady_clock::now().time_since_epoch().count() ^
                               (uint64_t)(uintptr_t)eng) | 1ull;
     int ndev = 0;
+    tl_create_err().clear();
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= eng->cfg.device || eng->cfg.device < 0) {
+        tl_create_err() = "tm_create: no such HIP device";
         delete eng;
         return TM_EDEVICE;
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, eng->cfg.device) != hipSuccess ||
         std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        tl_create_err() = "tm_create: the device is not a gfx950";
         delete eng;
         return TM_EDEVICE;  // kernels are built for gfx950 only
     }
@@ -3250,14 +3312,17 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
         hipStreamCreateWithFlags(&eng->stream, hipStreamNonBlocking) != hipSuccess ||
         hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess ||
         hipStreamCreateWithPriority(&eng->s_build, hipStreamNonBlocking, prio_least) != hipSuccess) {
+        tl_create_err() = std::string("tm_create: stream creation failed: ") + hipGetErrorString(hipGetLastError());
         tm_destroy(eng);
         return TM_EDEVICE;
     }
     if (!eng->reserve_ids()) {
+        tl_create_err() = "tm_create: no address space for the id arena reservation";
         tm_destroy(eng);
         return TM_ENOMEM;
     }
     if (!tm_engine::bnd_init(eng->cfg.device)) {
+        tl_create_err() = "tm_create: bounds-build init failed";
         tm_destroy(eng);
         return TM_EDEVICE;
     }
@@ -3292,6 +3357,7 @@ int tm_create(const tm_config *cfg, tm_engine **out) {
         rc = eng->commit(nullptr);  // empty epoch 1: device tables exist from the start
     }
     if (rc != TM_OK) {
+        tl_create_err() = std::string("tm_create: the first (empty) publish failed: ") + tl_err();
         tm_destroy(eng);
         return rc;
     }
@@ -3325,6 +3391,7 @@ void tm_destroy(tm_engine *eng) {
                       &eng->d_arena, &eng->d_scatter_idx, &eng->d_scatter_src, &eng->d_stats, &eng->d_sblob})
         b->release();
     eng->standby_release();
+    eng->d_nim.release();
     eng->upload_release();
     eng->h_cursor.release();
     eng->h_sblob.release();
@@ -3364,6 +3431,7 @@ __attribute__((visibility("hidden"))) void tmx_engine_lock(tm_engine *eng) { eng
 __attribute__((visibility("hidden"))) void tmx_engine_unlock(tm_engine *eng) { eng->mu_dev.unlock(); }
 
 const char *tm_last_error(const tm_engine *eng) { return eng ? eng->err.c_str() : "null engine"; }
+const char *tm_create_last_error(void) { return tl_create_err().c_str(); }
 
 static int replica_refuses(tm_engine *eng, const char *what) {
     eng->err = std::string(what) + ": a replica is read-only and keeps no host copy of the keys (use the master)";
@@ -3479,7 +3547,10 @@ static int ensure_batch(tm_engine *eng, uint32_t n, uint64_t bytes) {
     TM_TRY_HIP(eng->grow_buf(eng->bb->d_slow_list, (size_t)n * 4 + 4), TM_ENOMEM, "alloc");
     if (!eng->bb->d_ctl.p) {
         TM_TRY_HIP(eng->grow_buf(eng->bb->d_ctl, 2 * CTL_BYTES), TM_ENOMEM, "alloc");
-        TM_TRY_HIP(hipMemset(eng->bb->d_ctl.p, 0, 2 * CTL_BYTES), TM_EDEVICE, "memset");  // both blocks start at 0
+        // both blocks start at 0, and are 0 before any stream's launch reads them (hipMemset runs
+        // on the null stream, which the engine's non-blocking streams do not wait for)
+        TM_TRY_HIP(hipMemset(eng->bb->d_ctl.p, 0, 2 * CTL_BYTES), TM_EDEVICE, "memset");
+        TM_TRY_HIP(hipStreamSynchronize(nullptr), TM_EDEVICE, "memset sync");
     }
     TM_TRY_HIP(eng->grow_buf(eng->d_stats, STATS_BYTES), TM_ENOMEM, "alloc");
     TM_TRY_HIP(eng->grow_buf(eng->bb->d_scr_w, (bytes + 2ull * n + 2) * 4), TM_ENOMEM, "alloc");
@@ -3518,7 +3589,9 @@ static int grow_pools(tm_engine *eng) {
     if (eng->cfg.seg_chunks) return TM_OK;  // fixed by the caller (test aid)
     if (eng->bb->seg_demand_last > eng->bb->seg_chunks) {
         uint64_t want = eng->bb->seg_demand_last + eng->bb->seg_demand_last / 4 + 64;
-        TM_TRY_HIP(eng->grow_buf(eng->bb->d_seg_pool, want * SEG_CHUNK * sizeof(uint4)), TM_ENOMEM, "alloc seg pool");
+        TM_TRY_HIP(eng->grow_buf(eng->bb->d_seg_pool, want * SEG_CHUNK * sizeof(uint4)), TM_ENOMEM,
+                   "alloc seg pool (" + std::to_string(want * SEG_CHUNK * sizeof(uint4)) + " B for a demand of " +
+                       std::to_string(eng->bb->seg_demand_last) + " chunks)");
         eng->bb->seg_chunks = want;
     }
     if (eng->bb->fr_demand_last > eng->bb->fr_chunks) {
@@ -4183,6 +4256,17 @@ int tm_device_sync_set(tm_engine *eng, uint32_t set) {
         eng->n_slow_last = *(uint32_t *)(h + 8);
         eng->bb->seg_demand_last = *(uint64_t *)(h + 16);
         eng->bb->fr_demand_last = *(uint64_t *)(h + 24);
+        if (eng->bb->seg_demand_last >> 31 || eng->bb->fr_demand_last >> 31) {
+            // a counter block no launch could have produced (a wave takes at most SEG_MAXCHUNK
+            // chunks): report it instead of sizing a pool from it
+            char m[256];
+            snprintf(m, sizeof m, "tm_device_sync: impossible counter block (block %u of %p: cursor %llx seg %llx fr %llx)",
+                     eng->bb->ctl_cur, (void *)eng->bb->d_ctl.p, (unsigned long long)*(uint64_t *)h,
+                     (unsigned long long)eng->bb->seg_demand_last, (unsigned long long)eng->bb->fr_demand_last);
+            eng->err = m;
+            eng->bb->seg_demand_last = eng->bb->fr_demand_last = 0;
+            return TM_EDEVICE;
+        }
         return grow_pools(eng);
     }
     return TM_OK;
@@ -5077,6 +5161,7 @@ int tm_replica_create(const tm_config *cfg, const void *d_image, uint64_t bytes,
     hvec<uint32_t>().swap(eng->kset);
     // the host id arena stays: the replica fills it from its device copy (runs form)
     if ((rc = tm_replica_load(eng, d_image, bytes, stream)) != TM_OK) {
+        tl_create_err() = std::string("tm_replica_create: loading the image failed: ") + tl_err();
         tm_destroy(eng);
         return rc;
     }

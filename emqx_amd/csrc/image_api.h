@@ -24,5 +24,10 @@ static_assert(sizeof(NodeImage) == 24, "node image record is 24 B");
 // bnd the bounds record (read by the TM_BOUNDS build only).
 hipError_t launch_edge_image(uint4 *etab, uint32_t *slot_list, uint64_t cap, const NodeImage *nodes, uint64_t n,
                              hipStream_t s, uint64_t buf_slots = ~0ull, unsigned long long *bnd = nullptr);
+// The same in slices: clear slots [lo, hi); place records nodes[0..n) (all below cap).
+hipError_t launch_edge_clear_range(uint4 *etab, uint32_t *slot_list, uint64_t lo, uint64_t hi, hipStream_t s,
+                                   uint64_t buf_slots = ~0ull, unsigned long long *bnd = nullptr);
+hipError_t launch_edge_place_range(uint4 *etab, uint32_t *slot_list, uint64_t cap, const NodeImage *nodes, uint64_t n,
+                                   hipStream_t s, uint64_t buf_slots = ~0ull, unsigned long long *bnd = nullptr);
 
 }  // namespace tmx

@@ -594,7 +594,10 @@ __global__ __launch_bounds__(WAVE) void k_prescan(MatchArgs a) {
 template <bool STATS, int OUT, bool PRE>
 __global__ __launch_bounds__(WAVE, TM_MIN_WAVES) void k_match_fast(MatchArgs a) {
     constexpr bool RUNS = OUT == O_RUNS;
-    __shared__ WaveLdsT<PRE ? 16 : TBCAP> L;
+#ifndef TM_PRE_PAD
+#define TM_PRE_PAD 0  // experiment knob: 1 keeps the PRE walk's LDS at the fused kernel's size (16 waves/CU)
+#endif
+    __shared__ WaveLdsT<(PRE && !TM_PRE_PAD) ? 16 : TBCAP> L;
     uint32_t *const wchunks = a.wave_chunks + BIN((uint64_t)blockIdx.x * MAXCHUNK, MAXCHUNK, wave_chunks);  // this wave's flushed chunks
     const uint32_t lane = lane_id();
     const uint32_t t = blockIdx.x * a.tpw + lane;

@@ -762,10 +762,10 @@ hipError_t launch_scatter8(uint64_t *dst, const uint64_t *idx, const uint64_t *s
 // ---------------------------------------------------------------------------
 // The edge table image of a full publish: every slot empty, then each node's record in its
 // slot.  HBM-bound writes (20 B per slot, then 20 B per node at random slots).
-__global__ void k_edge_clear(uint4 *etab, uint32_t *slot_list, uint64_t cap, uint64_t buf_slots,
+__global__ void k_edge_clear(uint4 *etab, uint32_t *slot_list, uint64_t lo, uint64_t hi, uint64_t buf_slots,
                              unsigned long long *bnd) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cap; i += stride) {
+    for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += stride) {
         const uint64_t j = BIR(i, buf_slots, bnd);
         etab[j] = make_uint4(NONE, 0u, 0u, 0u);
         slot_list[j] = 0u;
@@ -788,19 +788,34 @@ __global__ void k_edge_place(uint4 *etab, uint32_t *slot_list, const NodeImage *
 // Both kernels run beside the matches of the image being replaced (a full publish into the
 // standby): at most EDGE_IMAGE_BLOCKS workgroups each (grid-stride), so they hold two of a CU's
 // wave slots instead of all of them; the matches' waves keep the rest (a match of 131,072
-// publishes beside an uncapped build took 1-2.6 ms instead of 0.135).
+// publishes beside an uncapped build took 1-2.6 ms instead of 0.135).  The
+// engine also launches them in slices (launch_edge_*_range), paced from the host, so a match
+// shares the memory system with at most one slice.
 constexpr uint64_t EDGE_IMAGE_BLOCKS = 512;
+
+hipError_t launch_edge_clear_range(uint4 *etab, uint32_t *slot_list, uint64_t lo, uint64_t hi, hipStream_t s,
+                                   uint64_t buf_slots, unsigned long long *bnd) {
+    if (hi <= lo) return hipSuccess;
+    const uint64_t want = (hi - lo + 255) / 256;
+    k_edge_clear<<<(unsigned)std::min<uint64_t>(want, EDGE_IMAGE_BLOCKS), 256, 0, s>>>(etab, slot_list, lo, hi, buf_slots,
+                                                                                       bnd);
+    return hipGetLastError();
+}
+
+hipError_t launch_edge_place_range(uint4 *etab, uint32_t *slot_list, uint64_t cap, const NodeImage *nodes, uint64_t n,
+                                   hipStream_t s, uint64_t buf_slots, unsigned long long *bnd) {
+    if (!n) return hipSuccess;
+    k_edge_place<<<(unsigned)std::min<uint64_t>((n + 255) / 256, EDGE_IMAGE_BLOCKS), 256, 0, s>>>(etab, slot_list, nodes, n,
+                                                                                               cap, buf_slots, bnd);
+    return hipGetLastError();
+}
 
 hipError_t launch_edge_image(uint4 *etab, uint32_t *slot_list, uint64_t cap, const NodeImage *nodes, uint64_t n,
                              hipStream_t s, uint64_t buf_slots, unsigned long long *bnd) {
     if (!cap) return hipSuccess;
-    const uint64_t want = (cap + 255) / 256;
-    k_edge_clear<<<(unsigned)std::min<uint64_t>(want, EDGE_IMAGE_BLOCKS), 256, 0, s>>>(etab, slot_list, cap, buf_slots, bnd);
-    hipError_t e = hipGetLastError();
-    if (e || !n) return e;
-    k_edge_place<<<(unsigned)std::min<uint64_t>((n + 255) / 256, EDGE_IMAGE_BLOCKS), 256, 0, s>>>(etab, slot_list, nodes, n,
-                                                                                               cap, buf_slots, bnd);
-    return hipGetLastError();
+    hipError_t e = launch_edge_clear_range(etab, slot_list, 0, cap, s, buf_slots, bnd);
+    if (e) return e;
+    return launch_edge_place_range(etab, slot_list, cap, nodes, n, s, buf_slots, bnd);
 }
 
 }  // namespace tmx

@@ -233,6 +233,9 @@ const char *tm_build_info(void);
 int         tm_create(const tm_config *cfg, tm_engine **out);
 void        tm_destroy(tm_engine *eng);
 const char *tm_last_error(const tm_engine *eng);
+/* Why the calling thread's last tm_create / tm_replica_create failed ("" after a success on
+ * that thread, or before any call). */
+const char *tm_create_last_error(void);
 
 /* writes ------------------------------------------------------------------ */
 int tm_apply(tm_engine *eng, const tm_op *ops, size_t n);

@@ -58,6 +58,28 @@ def _bounds_guard():
         pytest.fail(f"bounds build: {r[0]} findings: {r[1]}")
 
 
+_MEM_LOG = os.environ.get("EMQX_TM_TEST_MEMLOG", "")
+
+
+@pytest.fixture(autouse=True)
+def _device_memory_release(request):
+    """After every GPU test: collect the engines a test left unreferenced (their __del__ closes
+    them) and hand torch's cached blocks back, so one test's HBM is free for the next (the
+    full-size config-D tests need tens of GiB).  EMQX_TM_TEST_MEMLOG=<file> records the free HBM
+    after each test, to find a test that keeps device memory."""
+    yield
+    if request.node.get_closest_marker("gpu") is None or not torch.cuda.is_initialized():
+        return
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    if _MEM_LOG:
+        free, total = torch.cuda.mem_get_info(0)
+        with open(_MEM_LOG, "a") as f:
+            f.write(f"{free / 2**30:9.2f} GiB free of {total / 2**30:.1f}  {request.node.nodeid}\n")
+
+
 def pytest_terminal_summary(terminalreporter):
     """Under EMQX_TM_LIB: which library the run mapped, and (bounds build) its findings."""
     if not os.environ.get("EMQX_TM_LIB"):

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 for s in $STEPS; do
   case $s in
     test)
-      timeout -k 10 480 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+      EMQX_TM_TEST_MEMLOG=gpurun_out/r06_memlog_$T.txt timeout -k 10 480 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
           > gpurun_out/r06_pytest_gpu_$T.log 2>&1 || { tail -n 30 gpurun_out/r06_pytest_gpu_$T.log; exit 1; }
       tail -n 2 gpurun_out/r06_pytest_gpu_$T.log ;;
     smoke)

@@ -79,6 +79,8 @@ VARIANTS = {
     "pre_w20": (["-DTM_PREPASS=1", "-DTM_MIN_WAVES=5"], 0),
     "pre2": (["-DTM_PREPASS=1"], 0),
     "nopass2": (["-DTM_PREPASS=0"], 0),
+    # round 6: the PRE walk held at 16 waves/CU (LDS padded), to price the word-table probes
+    "pre16": (["-DTM_PREPASS=1", "-DTM_PRE_PAD=1"], 0),
 }
 
 
