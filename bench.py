@@ -86,7 +86,7 @@ def profiled_traffic(workload_keys, batch, any_config=False):
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if d.get("kernel_src_sha") != sha:
+        if not isinstance(d, dict) or d.get("kernel_src_sha") != sha:
             continue
         cfg = d.get("bench_line", {}).get("config", {})
         if not any_config and (cfg.get("route_keys") != workload_keys

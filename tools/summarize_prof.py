@@ -64,7 +64,11 @@ def main(src, dst):
     out["bench_line"] = bench
     fetch = pmc.get("FETCH_SIZE", 0) * 1024
     write = pmc.get("WRITE_SIZE", 0) * 1024
-    keys = bench["roofline"]["walk"]["keys"]
+    walk = bench["roofline"].get("walk")
+    if walk is None:  # round 6: the compact line keeps the walk counters in its side file
+        det = json.load(open(DETAIL or os.path.join(os.path.dirname(os.path.normpath(src)), "bench_detail.json")))
+        walk = det["roofline"]["walk"]
+    keys = walk["keys"]
     traffic = fetch + write
     out["traffic"] = {
         "fetch_bytes": fetch, "write_bytes": write, "hbm_bytes": traffic,
@@ -95,5 +99,9 @@ def main(src, dst):
     print("\n".join(md))
 
 
+DETAIL = None  # the default bench line's side file (argv[3]): walk counters of a full 1 M batch
+
 if __name__ == "__main__":
+    if len(sys.argv) > 3:
+        DETAIL = sys.argv[3]
     main(sys.argv[1], sys.argv[2])
