@@ -136,7 +136,11 @@ def batcher_load(eng, tb, to32, seconds, plan=None):
     dt = max(2, min(14, cpu_topology()["usable_cpus"] - 2))
     plan = plan or [(4096, N.TM_TRANSPORT_AUTO, 0), (65536, N.TM_TRANSPORT_AUTO, 0), (262144, N.TM_TRANSPORT_AUTO, 0),
             (65536, N.TM_TRANSPORT_AUTO, 1), (65536, N.TM_TRANSPORT_AUTO, 3), (65536, N.TM_TRANSPORT_IDS, 0),
-            (65536, N.TM_TRANSPORT_IDS, 3)]  # a replica's transport (no host id arena), u32 ids read in place
+            (65536, N.TM_TRANSPORT_IDS, 3),  # a replica's transport (no host id arena), u32 ids read in place
+            (65536, N.TM_TRANSPORT_AUTO, 0), (65536, N.TM_TRANSPORT_AUTO, 0)]
+    # the headline row (65,536 publishers, id lists) runs three times, spread over the leg: one
+    # 2 s window of it ranged 42-78 M/s across box runs (round 6), so the row reports the
+    # median of the three runs, with all three rates (`repeats`)
     warm = 0.5
     for pubs, transport, spans in plan:
         b = N.Batcher(eng, max_batch=65536, max_wait_us=200, delivery_threads=dt, transport=transport)
@@ -180,6 +184,19 @@ def batcher_load(eng, tb, to32, seconds, plan=None):
                                     "throttled_ms": round(cg[3] / 1e3, 3)}})
         if not runs[-1]["littles_law"]["ok"]:
             log(f"batcher: latency mean {mean_ms:.3f} ms differs from publishers / rate {little_ms:.3f} ms by > 20%")
+    merged, order = {}, []
+    for r in runs:  # repeated rows: the run with the median rate stands for the row
+        k = (r["publishers"], r["transport"], r["callback"])
+        if k not in merged:
+            order.append(k)
+        merged.setdefault(k, []).append(r)
+    runs = []
+    for k in order:
+        g = sorted(merged[k], key=lambda r: r["publishes_per_s"])
+        r = dict(g[len(g) // 2])
+        if len(g) > 1:
+            r["repeats"] = [x["publishes_per_s"] for x in merged[k]]
+        runs.append(r)
     return {"api": f"tm_batcher_submit (max_batch 65536, max_wait 200 us, {dt} delivery threads)", "runs": runs,
             "note": "closed loop: each publisher resubmits from its result callback, which reads every id once; "
                     "six windows in flight (GPU walk / PCIe / callbacks); runs transport: spans cross PCIe and "
@@ -588,6 +605,9 @@ def compact_line(out, detail_path):
             key = f"{r['publishers']} {r['transport'].split()[0]} {r['callback'].split(' (')[0]}"
             rows[key] = {"publishes_per_s": r["publishes_per_s"], "lat_p99_ms": r["lat_p99_ms"],
                          "x_cpu": round(r["publishes_per_s"] / cpu_v, 1) if cpu_v else None}
+            if r.get("repeats"):
+                rows[key]["repeats"] = r["repeats"]
+                rows[key]["stat"] = f"median of {len(r['repeats'])} runs"
         line["batcher"] = {"api": b.get("api"), "rows": rows}
         head = [r for r in b["runs"] if r["publishers"] == 65536 and r["transport"] == "runs"
                 and r["callback"].startswith("id list")]
