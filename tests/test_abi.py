@@ -51,8 +51,11 @@ def test_create_without_device_fails_loudly():
     h = C.c_void_p()
     rc = N.load().tm_create(C.byref(cfg), C.byref(h))
     assert rc == N.TM_EDEVICE and not h.value
-    with pytest.raises(N.TMError):
+    # the calling thread's reason for the failed create (tm_create_last_error, round 6)
+    assert N.load().tm_create_last_error() == b"tm_create: no such HIP device"
+    with pytest.raises(N.TMError) as e:
         N.Engine(0)
+    assert "no such HIP device" in str(e.value)
 
 
 def test_null_and_bad_args_are_rejected_without_device():
