@@ -4922,6 +4922,7 @@ int tm_debug_stats(tm_engine *eng, int enable, uint64_t *out18) {
         TM_TRY_HIP(hipMemcpy(out18, eng->d_stats.p, 18 * 8, hipMemcpyDeviceToHost), TM_EDEVICE, "D2H");
     }
     TM_TRY_HIP(hipMemset(eng->d_stats.p, 0, STATS_BYTES), TM_EDEVICE, "memset");
+    TM_TRY_HIP(hipStreamSynchronize(nullptr), TM_EDEVICE, "memset sync");  // before any stream's launch counts
     eng->stats_on = enable != 0;
     return TM_OK;
 }
