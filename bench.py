@@ -554,8 +554,8 @@ def launch_check():
     if world > 1:
         dist.all_reduce(t)
     if rank == 0:
-        print(json.dumps({"n_gpus": world, "rank_sum": int(t.item()),
-                          "local_ranks": os.environ.get("LOCAL_WORLD_SIZE")}), flush=True)
+        emit(json.dumps({"n_gpus": world, "rank_sum": int(t.item()),
+                          "local_ranks": os.environ.get("LOCAL_WORLD_SIZE")}))
     if world > 1:
         dist.destroy_process_group()
 
@@ -681,6 +681,25 @@ def write_detail(out, name="bench_detail.json"):
         return f"not written: {e}"
 
 
+_STDOUT = sys.stdout
+
+
+def json_stdout_only():
+    """From here on, stdout carries this process's JSON line and nothing else: whatever else
+    writes to fd 1 (gloo's and RCCL's connection banners, a library's print) goes to stderr,
+    so the driver reads one parseable line per run.  (A process that launches the ranks keeps
+    its stdout: they inherit it.)"""
+    global _STDOUT
+    sys.stdout.flush()
+    _STDOUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    sys.stdout = sys.stderr
+
+
+def emit(s: str):
+    print(s, file=_STDOUT, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -731,6 +750,7 @@ def main():
     kind, _ = world_plan(args.gpus, os.environ)
     if kind == "launch":
         sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    json_stdout_only()
     if args.launch_check:
         return launch_check()
     if args.filter_search:
@@ -1121,7 +1141,7 @@ def main():
                              "image_bytes": int(eng.image_size()), "image_s": round(image_s, 2)}
                             if world > 1 else None),
         }
-        print(compact_line(out, write_detail(out)), flush=True)
+        emit(compact_line(out, write_detail(out)))
     if world > 1:
         dist.destroy_process_group()
 
@@ -1233,7 +1253,7 @@ def run_sharded(args):
     if world > 1:
         dist.all_reduce(rss, op=dist.ReduceOp.MAX)
     if rank == 0:
-        print(json.dumps({
+        emit(json.dumps({
             "metric": f"matched publishes/sec, filters hash-sharded over {nshards} GPU shard(s) (config {args.config})",
             "value": round(n * args.steps / elapsed, 1), "unit": "publishes/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -1250,7 +1270,7 @@ def run_sharded(args):
             "wire_bytes_per_rank": wire, "exchanges": variants, "parity": parity,
             "host_peak_rss_gib_max_over_ranks": round(float(rss.item()), 2),
             "backend": backend if world > 1 else None,
-        }), flush=True)
+        }))
     if world > 1:
         dist.destroy_process_group()
 
@@ -1315,8 +1335,8 @@ def run_churn(args):
     """--churn EPOCHS: the churn leg alone, as its own JSON line."""
     cfg = args.config if args.config != "C" else "E"
     r = churn_leg(cfg, args.scale, args.batch, args.churn, args.warmup)
-    print(json.dumps(dict({"metric": "delta-epoch churn: route ops/s committed + matched publishes/s between epochs"},
-                          **r)), flush=True)
+    emit(json.dumps(dict({"metric": "delta-epoch churn: route ops/s committed + matched publishes/s between epochs"},
+                          **r)))
 
 
 def churn_leg(cfg, scale, batch, epochs, warmup):
@@ -1864,14 +1884,14 @@ def run_filter(args):
     eng.apply_packed(N.TM_OP_ADD, w.f_bytes, w.f_off, w.f_id)
     eng.commit()
     r = filter_leg(args, w, eng, args.filter_search)
-    print(json.dumps({
+    emit(json.dumps({
         "metric": "matches_filter/3 topic-filter queries/s (host API, walk-order exact)",
         "value": r["queries_per_s"], "unit": "queries/s", "n_gpus": 1,
         "config": {"workload": f"{args.config}: {w.n_keys} route keys", "queries": r["queries"],
                    "query_mix": r["query_mix"]},
         "ms_per_batch": r["ms_per_batch"], "keys_returned": r["keys_returned"],
         "index_build_ms": r["index_build_ms"], "cpu_baseline": r["cpu_baseline"], "parity": r["parity"],
-    }), flush=True)
+    }))
 
 
 def cpu_baseline(args, w, eng, tb, to, n):
