@@ -108,7 +108,7 @@ int main(int argc, char **argv) {
         in_tail[v] = (p != 0) && (head[p] || in_tail[p]);
         head[v] = !in_tail[v] && sub[v] == 1;
     }
-    uint64_t visits = 0, tail_visits = 0, heads_reached = 0, deep_visits = 0;
+    uint64_t visits = 0, tail_visits = 0, heads_reached = 0, deep_visits = 0, tail_entries = 0;
     std::vector<uint32_t> fr, nx, wids;
     for (size_t t = 0; t < nt; t++) {
         split(std::string_view((const char *)tb.data() + to[t], to[t + 1] - to[t]), lv);
@@ -124,7 +124,10 @@ int main(int argc, char **argv) {
                     if (c == NONE) continue;
                     visits++;
                     deep_visits += d >= 4;
-                    if (in_tail[c]) tail_visits++;
+                    if (in_tail[c]) {
+                        tail_visits++;
+                        tail_entries += head[T.parent[c]];  // the first tail node below its head
+                    }
                     else if (head[c]) heads_reached++;
                     nx.push_back(c);
                 }
@@ -133,9 +136,11 @@ int main(int argc, char **argv) {
         }
     }
     printf("{\"filters\": %zu, \"topics\": %zu, \"nodes\": %zu, \"tail_heads\": %llu, \"nodes_in_tails\": %llu, "
-           "\"visits\": %llu, \"visits_in_tails\": %llu, \"tail_heads_reached\": %llu, \"visits_depth_ge4\": %llu}\n",
+           "\"visits\": %llu, \"visits_in_tails\": %llu, \"tail_entries\": %llu, \"tail_heads_reached\": %llu, "
+           "\"visits_depth_ge4\": %llu}\n",
            nf, nt, nn, (unsigned long long)std::count(head.begin(), head.end(), 1),
            (unsigned long long)std::count(in_tail.begin(), in_tail.end(), 1), (unsigned long long)visits,
-           (unsigned long long)tail_visits, (unsigned long long)heads_reached, (unsigned long long)deep_visits);
+           (unsigned long long)tail_visits, (unsigned long long)tail_entries, (unsigned long long)heads_reached,
+           (unsigned long long)deep_visits);
     return 0;
 }
