@@ -196,6 +196,11 @@ def batcher_load(eng, tb, to32, seconds, plan=None):
         r = dict(g[len(g) // 2])
         if len(g) > 1:
             r["repeats"] = [x["publishes_per_s"] for x in merged[k]]
+            # what each repeat got from the host (a slow one: fewer CPUs, preempted delivery?)
+            r["repeat_host"] = [{"publishes_per_s": x["publishes_per_s"], "cgroup_cpu": x["cgroup_cpu"],
+                                 "stage_busy": x["stage_busy"],
+                                 "slowest_1pct": (x.get("windows") or {}).get("stage_ms_slowest_1pct")}
+                                for x in merged[k]]
         runs.append(r)
     return {"api": f"tm_batcher_submit (max_batch 65536, max_wait 200 us, {dt} delivery threads)", "runs": runs,
             "note": "closed loop: each publisher resubmits from its result callback, which reads every id once; "
