@@ -406,6 +406,10 @@ struct tm_batcher {
     uint32_t pf_pubs = 6, pf_lines = 0;
     // delivery threads' nice value (EMQX_TM_DELIVERY_NICE; unprivileged processes may raise it)
     int deliver_nice = 0;
+    // publish ranges per delivery thread and chunk (EMQX_TM_RANGES_PER_THREAD): with more, a
+    // delivery thread preempted in mid-range holds back fewer publishes while the others take
+    // the rest of the chunk
+    uint32_t ranges_per_thread = 1;
     // runs windows: spans of the u64 id arena (zero-copy for id-list and u64-span callbacks), or
     // (EMQX_TM_RUNS_IDW=4) of the u32 one while every id fits.  Measured on the box at 65,536
     // closed-loop publishers: u32 windows made the id-list and u64-span callbacks
@@ -1028,7 +1032,8 @@ struct tm_batcher {
             const uint32_t lo = S.chunk_lo[j], hi = S.chunk_lo[j + 1];
             S.chunk_ready[j].store(S.cev_wait ? 0 : 1, std::memory_order_relaxed);
             if (hi <= lo) continue;
-            const uint32_t parts = std::max<uint32_t>(1, std::min<uint32_t>(nthreads, (hi - lo) / MIN_RANGE));
+            const uint32_t parts =
+                std::max<uint32_t>(1, std::min<uint32_t>(nthreads * ranges_per_thread, (hi - lo) / MIN_RANGE));
             for (uint32_t k = 0; k < parts; k++)
                 ws.push_back(Work{si, j, lo + (uint32_t)((uint64_t)(hi - lo) * k / parts),
                                   lo + (uint32_t)((uint64_t)(hi - lo) * (k + 1) / parts)});
@@ -1294,6 +1299,8 @@ struct tm_batcher {
         if (const char *e = std::getenv("EMQX_TM_PF_LINES")) pf_lines = std::min(256u, (uint32_t)std::atoi(e));
         if (const char *e = std::getenv("EMQX_TM_RUNS_IDW")) runs_w = std::atoi(e) == 4 ? 4u : 8u;
         if (const char *e = std::getenv("EMQX_TM_DELIVERY_NICE")) deliver_nice = std::max(0, std::min(19, std::atoi(e)));
+        if (const char *e = std::getenv("EMQX_TM_RANGES_PER_THREAD"))
+            ranges_per_thread = (uint32_t)std::max(1, std::min(16, std::atoi(e)));
         if (const char *e = std::getenv("EMQX_TM_BATCHER_HINTS")) hints = std::atoi(e) != 0;
         if (!eng)
             for (Slot &S : slot)

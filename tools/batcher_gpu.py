@@ -1,7 +1,7 @@
 """Batcher sweep on one GPU (bench tooling): config C engine, closed-loop publishers through
 tm_batcher_submit for each (publishers, delivery threads, max_wait_us[, transport, spans callback,
 slots, max_batch, compute streams]) given, one JSON line each.
-Usage: python tools/batcher_gpu.py P:T:W[:TR:SP:NSLOT:MB:ST:PFP:PFL:IDW:NICE] ...   (TR 0 auto/runs, 1 ids; SP 1 = span
+Usage: python tools/batcher_gpu.py P:T:W[:TR:SP:NSLOT:MB:ST:PFP:PFL:IDW:NICE:RPT] ...   (TR 0 auto/runs, 1 ids; SP 1 = span
 callback, 2 = span callback reading no id, 3 = u32-span callback, 4 = u32-span callback reading no id; ST 1 or 2 compute streams, EMQX_TM_STREAMS; PFP/PFL delivery prefetch:
 publishes ahead / lines per reply, 0 lines = first line of each span; IDW 4 / 8: runs windows read
 the engine's u32 / u64 id arena; NICE: delivery threads' nice value).  PIN=1 pins the process to the GPU's socket first."""
@@ -61,6 +61,8 @@ def main():
         os.environ["EMQX_TM_RUNS_IDW"] = str(idw)
         nice = v[11] if len(v) > 11 else 0
         os.environ["EMQX_TM_DELIVERY_NICE"] = str(nice)
+        rpt = v[12] if len(v) > 12 else 1  # publish ranges per delivery thread and chunk
+        os.environ["EMQX_TM_RANGES_PER_THREAD"] = str(rpt)
         b = N.Batcher(eng, max_batch=mb, max_wait_us=wait, delivery_threads=th, transport=tr)
         got, ids, errs, cs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
         win = N.tm_batcher_stats()
@@ -73,7 +75,7 @@ def main():
         b.close()
         print(json.dumps({"publishers": pubs, "threads": th, "max_wait_us": wait, "transport": tr, "spans": sp,
                           "nslot": nslot, "max_batch": mb, "streams": nst, "rc": rc, "errors": errs.value,
-                          "pf_pubs": pfp, "pf_lines": pfl, "runs_idw": idw, "nice": nice,
+                          "pf_pubs": pfp, "pf_lines": pfl, "runs_idw": idw, "nice": nice, "ranges_per_thread": rpt,
                           "publishes_per_s": round(win.lat_count / win.window_s),
                           "publishes_per_s_whole_run": round(got.value / el.value),
                           "ids_per_publish": round(ids.value / max(got.value, 1), 1),
