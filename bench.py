@@ -117,7 +117,7 @@ def _loadgen():
     return lg
 
 
-def batcher_load(eng, tb, to32, seconds, plan=None):
+def batcher_load(eng, tb, to32, seconds, plan=None, repin=None):
     """End to end through the batching aggregator (include/emqx_tm_batcher.h): P concurrent
     publishers, each with one publish in flight (tools/loadgen.cpp), each publish answered
     with its own route ids on the host, every id read once by the callback (a checksum, as a
@@ -143,6 +143,10 @@ def batcher_load(eng, tb, to32, seconds, plan=None):
     # median of the three runs, with all three rates (`repeats`)
     warm = 0.5
     for pubs, transport, spans in plan:
+        # each row's threads start on cores picked just before it: the rate follows the CPUs the
+        # process gets (round 6: three runs of one row at 14.6 / 11.1 / 9.1 CPUs of use made
+        # 76 / 58 / 46 M/s, 5.2 M/s per CPU each, the slow ones preempted by other jobs)
+        placed_row = repin() if repin else None
         b = N.Batcher(eng, max_batch=65536, max_wait_us=200, delivery_threads=dt, transport=transport)
         got, ids, errs, cs, el = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_double()
         win = N.tm_batcher_stats()
@@ -179,6 +183,7 @@ def batcher_load(eng, tb, to32, seconds, plan=None):
                      "stage_busy": {k: round(st[k + "_us"] * 1e-6 / el.value, 3)
                                     for k in ("cut", "enqueue", "gpu_wait", "copy", "deliver")},
                      "windows": window_stages(wbuf, wn.value),
+                     "host_placement": placed_row,
                      "cgroup_cpu": {"usage_cpus": round(cg[0] * 1e-6 / max(win.window_s, 1e-9), 2),
                                     "periods": int(cg[1]), "throttled_periods": int(cg[2]),
                                     "throttled_ms": round(cg[3] / 1e3, 3)}})
@@ -198,6 +203,7 @@ def batcher_load(eng, tb, to32, seconds, plan=None):
             r["repeats"] = [x["publishes_per_s"] for x in merged[k]]
             # what each repeat got from the host (a slow one: fewer CPUs, preempted delivery?)
             r["repeat_host"] = [{"publishes_per_s": x["publishes_per_s"], "cgroup_cpu": x["cgroup_cpu"],
+                                 "host_placement": x.get("host_placement"),
                                  "stage_busy": x["stage_busy"],
                                  "slowest_1pct": (x.get("windows") or {}).get("stage_ms_slowest_1pct")}
                                 for x in merged[k]]
@@ -1034,7 +1040,8 @@ def main():
         # the host-bound legs re-pick their cores first: another job may have moved onto the
         # ones picked at start-up (threads created from here on inherit the new set)
         placed_b = placement.pin_to_gpu(local) if placed.get("pinned") and args.batcher_seconds > 0 else None
-        batcher = batcher_load(eng, tb, to32, args.batcher_seconds) if args.batcher_seconds > 0 else None
+        repin = (lambda: placement.pin_to_gpu(local)) if placed.get("pinned") else None
+        batcher = batcher_load(eng, tb, to32, args.batcher_seconds, repin=repin) if args.batcher_seconds > 0 else None
         if batcher is not None:
             batcher["host_placement"] = placed_b
             batcher["on_replica"] = replica_batcher_leg(eng, tb, to32, args.batcher_seconds)
