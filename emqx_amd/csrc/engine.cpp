@@ -3164,7 +3164,10 @@ struct tm_engine {
             (e = hipMemcpy(fx.d_krec.p, krec.data(), krec.size() * 4, hipMemcpyHostToDevice)) ||
             (!kw.empty() && (e = hipMemcpy(fx.d_kw.p, kw.data(), kw.size() * 4, hipMemcpyHostToDevice))) ||
             (e = hipMemcpy(fx.d_koff.p, koff.data(), koff.size() * 4, hipMemcpyHostToDevice)) ||
-            (!kh.empty() && (e = hipMemcpy(fx.d_kh.p, kh.data(), kh.size() * 4, hipMemcpyHostToDevice)))) {
+            (!kh.empty() && (e = hipMemcpy(fx.d_kh.p, kh.data(), kh.size() * 4, hipMemcpyHostToDevice))) ||
+            // a copy from pageable memory may return before its DMA lands, and only the null
+            // stream is ordered after it: wait before the walks on the engine's streams read it
+            (e = hipStreamSynchronize(nullptr))) {
             err = std::string("matches_filter index upload: ") + hipGetErrorString(e);
             return TM_EDEVICE;
         }
